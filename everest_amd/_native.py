@@ -1,0 +1,106 @@
+"""ctypes binding of the C-ABI in include/everest_amd.h (libeverest_amd.so, gfx950).
+
+The library is built in-tree (``everest_amd/_lib``) by ``__graft_entry__.build()`` /
+``make -C everest_amd/csrc``.  There is no fallback: if the library is missing every op
+raises ``NativeLibraryError``.  ``torch`` is imported first so that the HIP runtime torch
+ships (SONAME libamdhip64.so.7) is the one the library binds to — one runtime, one set of
+streams per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_longlong, c_void_p
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libeverest_amd.so")
+
+c_double_p = c_void_p  # device / host pointers are passed as integers
+c_int_p = c_void_p
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class EvrQnehviState(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int), ("nb", c_int), ("S", c_int), ("m", c_int),
+        ("c", c_void_p), ("ym", c_void_p), ("ys", c_void_p), ("kxx", c_void_p),
+        ("zq", c_void_p), ("obj_a", c_void_p), ("obj_b", c_void_p),
+        ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p),
+    ]
+
+
+_SIGS = {
+    "evr_version": ([], c_int),
+    "evr_last_error": ([], c_char_p),
+    "evr_device_arch": ([c_int, c_char_p, c_int], c_int),
+    "evr_stream_sync": ([c_void_p], c_int),
+    "evr_kernel_matrix": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 10, c_int),
+    "evr_kernel_cross_grad": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 10, c_int),
+    "evr_kernel_lengthscale_grad": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p], c_int),
+    "evr_gp_mll_terms": ([c_void_p, c_int, c_int] + [c_void_p] * 5, c_int),
+    "evr_gemm_f64": ([c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_void_p, c_int, c_longlong,
+                      c_void_p, c_int, c_longlong, c_double, c_void_p, c_int, c_longlong, c_int], c_int),
+    "evr_cholesky": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong,
+                      c_double, c_int, c_void_p, c_void_p], c_int),
+    "evr_trsm_lower": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_longlong, c_int, c_void_p, c_int,
+                        c_longlong], c_int),
+    "evr_tri_inv_lower": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong],
+                          c_int),
+    "evr_gp_posterior_finalize": ([c_void_p, c_int, c_int, c_int] + [c_void_p] * 8, c_int),
+    "evr_qnehvi_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+                           c_int),
+    "evr_hvi_forward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p], c_int),
+    "evr_mean_over_samples": ([c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
+    "evr_hvi_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_qnehvi_samples_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p], c_int),
+    "evr_pareto_mask": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "evr_objective_affine": ([c_void_p, c_int, c_int, c_int] + [c_void_p] * 5, c_int),
+    "evr_scale_batched": ([c_void_p, c_int, c_longlong, c_void_p, c_void_p], c_int),
+    "evr_add_selection": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_box_decompose": ([c_int, c_int, c_int, c_void_p, c_longlong, c_longlong, c_longlong, c_void_p,
+                           c_void_p, c_int, POINTER(c_void_p)], c_int),
+    "evr_cells_total": ([c_void_p], c_longlong),
+    "evr_cells_copy": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_cells_free": ([c_void_p], None),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise loudly if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"everest_amd native library not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)."
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = load().evr_last_error().decode(errors="replace")
+        raise RuntimeError(f"everest_amd {what} failed (status {status}): {msg}")
+
+
+def call(name: str, *args):
+    lib = load()
+    check(getattr(lib, name)(*args), name)

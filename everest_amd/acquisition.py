@@ -1,0 +1,217 @@
+"""qNEHVI (q = 1) acquisition resident in HBM — construction, forward and analytic backward.
+
+Replaces [upstream] ``qNoisyExpectedHypervolumeImprovement`` as built by
+``QnehviStrategy._get_acqfs`` (bofire/strategies/predictives/qnehvi.py:23-53:
+prune_baseline=True, cache_root=True, alpha=0, eta=1e-3 without output constraints).
+
+Algebraic restructuring (results preserved): the reference forms, per
+candidate, the joint posterior over [X_baseline; x] through a (n_base+1) x n x n GEMM and
+then solves against the cached baseline root.  Because every baseline point is a training
+point (get_acqf_input_tensors, bofire/strategies/predictives/botorch.py:696-724), all of
+that collapses to one per-ask operator per output
+
+    M_j = [ L^-1 ; G_j ; H_j^T ; alpha_j^T ]     (n + n_base + S + 1) x n
+    G_j = s_j^2 L_base^-1 (P - A_b^T L^-1),  A_b = L^-1 K(X_tr, X_base),  H_j = G_j^T Z_base
+
+applied to k(X_tr, x): R = M K_x is a dense MFMA GEMM over the candidate batch, and
+    mu = m + s (c + alpha.k), var = s^2 (1 - |L^-1 k|^2), L21 = G k, L22^2 = var - |L21|^2,
+    y_s = mu + L21.z_base,s + L22 z_q,s      (= sample_cached_cholesky, psd_safe max_tries=6)
+followed by the box-cell HVI scan and the mean over samples.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+from .gp import GPBatch
+
+
+def draw_sobol_normal_samples(d: int, n: int, seed: int, device=None) -> torch.Tensor:
+    """Scrambled Sobol -> inverse normal CDF ([upstream] draw_sobol_normal_samples with
+    NormalQMCEngine(inv_transform=True)).  Input generation only (host, as in BoTorch)."""
+    eng = torch.quasirandom.SobolEngine(dimension=d, scramble=True, seed=int(seed))
+    u = eng.draw(n, dtype=torch.float64)
+    v = 0.5 + (1 - torch.finfo(u.dtype).eps) * (u - 0.5)
+    z = torch.erfinv(2 * v - 1) * math.sqrt(2)
+    return z if device is None else z.to(device)
+
+
+def sobol_base_samples(S: int, n_points: int, m: int, seed: int) -> torch.Tensor:
+    """S x n_points x m (Sobol dim index = point*m + output)."""
+    return draw_sobol_normal_samples(n_points * m, S, seed).view(S, n_points, m)
+
+
+def _host_threads() -> int:
+    v = os.environ.get("EVR_HOST_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    try:
+        return max(1, int(v)) if v else min(16, os.cpu_count() or 1)
+    except ValueError:
+        return 1
+
+
+@dataclass
+class ConstructionStats:
+    n_train: int
+    n_base: int
+    total_cells: int
+    max_cells: int
+    prune_probs: Optional[np.ndarray] = None
+
+
+class QNEHVI:
+    """Device qNEHVI over the GPs of ``gp`` (one output per objective).
+
+    Parameters mirror the reference constructor: ``X_baseline`` raw (transformed) inputs,
+    ``ref_point`` in objective space, affine objective ``g = a*y + b`` per output.  Base
+    samples may be passed explicitly (parity tests) or are drawn from Sobol seeds.
+    """
+
+    def __init__(self, gp: GPBatch, X_train_raw: np.ndarray, X_baseline_raw: np.ndarray, ref_point, obj_a, obj_b,
+                 S: int = 512, sampler_seed: int = 0, prune_baseline: bool = True, prune_seed: int = 0,
+                 prune_samples: int = 2048, max_frac: float = 1.0, z_prune: Optional[torch.Tensor] = None,
+                 z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
+                 num_threads: Optional[int] = None):
+        dev = gp.device
+        self.gp = gp
+        self.dev = dev
+        m = gp.B
+        n = gp.n
+        self.m, self.n, self.S = m, n, int(S)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.ref = torch.as_tensor(np.asarray(ref_point, dtype=np.float64), **f64)
+        self.obj_a = torch.as_tensor(np.asarray(obj_a, dtype=np.float64), **f64)
+        self.obj_b = torch.as_tensor(np.asarray(obj_b, dtype=np.float64), **f64)
+        # baseline rows -> training rows (exact match of the transformed inputs)
+        X_train_raw = np.asarray(X_train_raw, dtype=np.float64)
+        X_baseline_raw = np.asarray(X_baseline_raw, dtype=np.float64)
+        first = {}
+        for i, row in enumerate(map(tuple, X_train_raw)):
+            first.setdefault(row, i)
+        try:
+            base_rows = np.array([first[tuple(r)] for r in X_baseline_raw], dtype=np.int64)
+        except KeyError as e:
+            raise ValueError("qNEHVI: every baseline point must be a training point of the models") from e
+
+        # ---- joint posterior at the training inputs (shared by prune and baseline) --------
+        K = gp.kernel_train(noise=False)                                  # m x n x n
+        mu_t = ops.gemm(K, gp.alpha.unsqueeze(-1))[..., 0]                 # K alpha
+        mu_train = gp.ym[:, None] + gp.ys[:, None] * (gp.const[:, None] + mu_t)
+        A = ops.gemm(gp.Linv, K)                                          # L^-1 K
+        Sig = ops.gemm(A, A, transA=True, alpha=-1.0, beta=1.0, out=K)    # K - A^T A (in place)
+        ops.scale_batched(Sig, (gp.ys ** 2).contiguous())                 # unstandardize
+
+        # ---- prune_inferior_points_multi_objective --------------------------------------
+        probs = None
+        if prune_baseline:
+            cand = torch.as_tensor(base_rows, device=dev)
+            Sig_c = Sig[:, cand][:, :, cand].contiguous()
+            mu_c = mu_train[:, cand].contiguous()
+            nc = cand.shape[0]
+            Lp, _, _ = ops.cholesky(Sig_c, 1e-8, 3)
+            if z_prune is None:
+                z_prune = sobol_base_samples(prune_samples, nc, m, prune_seed)
+            Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()             # m x nc x S'
+            Yp = ops.gemm(Lp, Zp)
+            Op = ops.objective_affine(Yp, mu_c, self.obj_a, self.obj_b)
+            _, counts = ops.pareto_mask(Op, self.ref, dedup=False, want_mask=False, want_counts=True)
+            probs = counts.cpu().numpy().astype(np.float64) / Zp.shape[2]
+            keep = np.nonzero(probs)[0]
+            max_points = math.ceil(max_frac * nc)
+            if keep.shape[0] > max_points:
+                order = np.argsort(-probs, kind="stable")
+                keep = order[:max_points]
+            keep = np.unique(keep)
+            base_rows = base_rows[keep]
+        nb = int(base_rows.shape[0])
+        self.nb = nb
+        self.base_rows = base_rows
+        idx = torch.as_tensor(base_rows, device=dev)
+
+        # ---- baseline posterior root, samples, box decomposition ----------------------
+        if nb > 0:
+            Sig_b = Sig[:, idx][:, :, idx].contiguous()
+            self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
+            mu_b = mu_train[:, idx].contiguous()
+        S_ = self.S
+        if z_base_full is None:
+            z_base_full = sobol_base_samples(S_, nb, m, sampler_seed)          # S x nb x m
+        if z_new_full is None:
+            z_new_full = sobol_base_samples(S_, nb + 1, m, sampler_seed)       # S x (nb+1) x m
+        self.zq = z_new_full[:, nb, :].to(**f64).contiguous()                 # S x m
+        if nb > 0:
+            Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()            # m x nb x S
+            Yb = ops.gemm(self.L_base, Zb)
+            Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
+            mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
+            lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),
+                                            num_threads or _host_threads(), layout="jis")
+        else:  # no baseline: one cell [ref, inf)
+            lo = np.tile(self.ref.cpu().numpy(), (S_, 1))
+            hi = np.full((S_, m), np.inf)
+            off = np.arange(S_ + 1, dtype=np.int32)
+        self.cell_lo = torch.as_tensor(lo, **f64).contiguous()
+        self.cell_hi = torch.as_tensor(hi, **f64).contiguous()
+        self.cell_off = torch.as_tensor(off, dtype=torch.int32, device=dev).contiguous()
+        counts_c = np.diff(off)
+        self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(off[-1]),
+                                       max_cells=int(counts_c.max()) if len(counts_c) else 0, prune_probs=probs)
+
+        # ---- forward operator M = [Linv; G; H^T; alpha^T] ------------------------------
+        Rr = n + nb + S_ + 1
+        self.Rr = Rr
+        M = torch.empty(m, Rr, n, **f64)
+        M[:, :n].copy_(gp.Linv)
+        if nb > 0:
+            A_b = A[:, :, idx].contiguous()                                     # m x n x nb
+            E = ops.gemm(A_b, gp.Linv, transA=True, alpha=-1.0)                 # -A_b^T Linv
+            ops.add_selection(E, idx.to(torch.int32), None)                      # + P
+            ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
+            ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
+            M[:, n:n + nb].copy_(E)
+            ops.gemm_into(M[:, n + nb:n + nb + S_], Zb, E, transA=True)          # H^T = Z^T G
+        else:
+            M[:, n:n + S_].zero_()
+        M[:, Rr - 1].copy_(gp.alpha)
+        self.M = M
+        self.state = ops.make_state(n, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
+                                    self.cell_lo, self.cell_hi, self.cell_off)
+        self._keep = (self.zq, self.cell_lo, self.cell_hi, self.cell_off, self.obj_a, self.obj_b)
+
+    # ------------------------------------------------------------------------------------
+    def _check_flags(self, flags):
+        if bool(flags.any().item()):
+            raise ops.NotPSDError("qNEHVI: new-point block of the cached Cholesky not p.d. after 6 jitter tries")
+
+    def forward(self, X: torch.Tensor, return_cache: bool = False):
+        """X: b x d raw (transformed) candidates on device -> acquisition values (b)."""
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        b = X.shape[0]
+        Kx = self.gp.cross(X)                       # m x n x b
+        R = ops.gemm(self.M, Kx)                    # m x Rr x b
+        G, L22, flags = ops.qnehvi_samples(self.state, R, b)
+        partial = ops.hvi_forward(self.state, G, b)
+        acq = ops.mean_over_samples(partial)
+        if return_cache:
+            return acq, (X, R, G, L22, flags)
+        self._check_flags(flags)
+        return acq
+
+    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
+        acq, (X, R, G, L22, flags) = self.forward(X, return_cache=True)
+        self._check_flags(flags)
+        b = X.shape[0]
+        if gout is None:
+            gout = torch.ones(b, dtype=torch.float64, device=self.dev)
+        dG = ops.hvi_backward(self.state, G, gout, b)
+        gR = ops.qnehvi_samples_backward(self.state, R, L22, dG, b)
+        dKx = ops.gemm(self.M, gR, transA=True)     # m x n x b
+        gp = self.gp
+        dX = ops.kernel_cross_grad(gp.Xn, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+        return acq, dX

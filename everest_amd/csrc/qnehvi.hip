@@ -1,0 +1,392 @@
+// qNEHVI (q = 1) device kernels on gfx950: cached-Cholesky sampling, box-cell hypervolume
+// improvement scan (forward + backward), Pareto / prune masks.
+//
+// Restates [upstream] BoTorch qNoisyExpectedHypervolumeImprovement as BoFire builds it
+// (bofire/strategies/predictives/qnehvi.py:39-52): samples y_s = mu + L21 z_base + L22 z_q
+// (sample_cached_cholesky, psd_safe_cholesky(max_tries=6) on the 1x1 new block), objective
+// g = a*y + b (bofire/utils/torch_tools.py:389-398), HVI_s = sum_cells prod_j
+// clamp_min(min(g_j, u_j) - l_j, 0), acquisition = mean_s HVI_s.
+#include "common.hpp"
+#include "../../include/everest_amd.h"
+
+namespace evr {
+
+// -------------------------------------------------------------------------------------
+// samples: one thread per (candidate c, objective j)
+// -------------------------------------------------------------------------------------
+__global__ void qn_samples_kernel(int n, int nb, int S, int m, int b, const double* __restrict__ R,
+                                  const double* __restrict__ cc, const double* __restrict__ ym,
+                                  const double* __restrict__ ys, const double* __restrict__ kxx,
+                                  const double* __restrict__ zq, const double* __restrict__ oa,
+                                  const double* __restrict__ ob, double* __restrict__ G, double* __restrict__ L22,
+                                  int* __restrict__ flags) {
+  const int j = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  const long long Rr = (long long)n + nb + S + 1;
+  const double* Rj = R + (size_t)j * Rr * b;
+  double ssv = 0.0, ssw = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double v = Rj[(size_t)i * b + c];
+    ssv = fma(v, v, ssv);
+  }
+  for (int i = n; i < n + nb; ++i) {
+    const double v = Rj[(size_t)i * b + c];
+    ssw = fma(v, v, ssw);
+  }
+  const double a = Rj[(size_t)(n + nb + S) * b + c];
+  const double s = ys[j];
+  const double mu = ym[j] + s * (cc[j] + a);
+  const double var = s * s * (kxx[j] - ssv);
+  const double br = var - ssw;
+  // psd_safe_cholesky on the 1x1 block: plain, then total jitter 1e-8*10^(t-1), t=1..6
+  double l22 = nan("");
+  int flag = 1;
+  if (!isnan(br)) {
+    for (int t = 0; t <= 6; ++t) {
+      const double jit = (t == 0) ? 0.0 : 1e-8 * pow(10.0, (double)(t - 1));
+      if (br + jit > 0.0) {
+        l22 = sqrt(br + jit);
+        flag = 0;
+        break;
+      }
+    }
+  }
+  L22[(size_t)j * b + c] = l22;
+  flags[(size_t)j * b + c] = flag;
+  const double A = oa[j], B0 = ob[j];
+  const double* h = Rj + (size_t)(n + nb) * b + c;
+  for (int si = 0; si < S; ++si) {
+    const double y = mu + h[(size_t)si * b] + l22 * zq[(size_t)si * m + j];
+    G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// HVI forward: grid (candidate tiles, S). Cells of sample s are streamed through LDS in
+// chunks; every lane reads the same cell (LDS broadcast) and updates CPT candidates.
+// -------------------------------------------------------------------------------------
+constexpr int HT = 256;   // threads per block
+constexpr int HCH = 128;  // cells per LDS chunk
+
+template <int M, int CPT>
+__global__ __launch_bounds__(HT) void hvi_fwd_kernel(int S, int b, const double* __restrict__ G,
+                                                     const double* __restrict__ lo, const double* __restrict__ hi,
+                                                     const int* __restrict__ off, double* __restrict__ partial) {
+  const int s = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int cbase = blockIdx.x * HT * CPT;
+  __shared__ double Ls[HCH * M];
+  __shared__ double Hs[HCH * M];
+  double y[CPT][M];
+  double acc[CPT];
+#pragma unroll
+  for (int p = 0; p < CPT; ++p) {
+    const int c = cbase + p * HT + tid;
+    acc[p] = 0.0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) y[p][j] = (c < b) ? G[((size_t)s * M + j) * b + c] : -INFINITY;
+  }
+  const int c0 = off[s], c1 = off[s + 1];
+  for (int k0 = c0; k0 < c1; k0 += HCH) {
+    const int nc = min(HCH, c1 - k0);
+    for (int e = tid; e < nc * M; e += HT) {
+      Ls[e] = lo[(size_t)k0 * M + e];
+      Hs[e] = hi[(size_t)k0 * M + e];
+    }
+    __syncthreads();
+    for (int k = 0; k < nc; ++k) {
+      double l[M], h[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        l[j] = Ls[k * M + j];
+        h[j] = Hs[k * M + j];
+      }
+#pragma unroll
+      for (int p = 0; p < CPT; ++p) {
+        double prod = 1.0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) prod *= fmax(fmin(y[p][j], h[j]) - l[j], 0.0);
+        acc[p] += prod;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int p = 0; p < CPT; ++p) {
+    const int c = cbase + p * HT + tid;
+    if (c < b) partial[(size_t)s * b + c] = acc[p];
+  }
+}
+
+// HVI backward: dG[s][j][c] = gs * sum_cells pass_j * prod_{k != j} len_k
+template <int M>
+__global__ __launch_bounds__(HT) void hvi_bwd_kernel(int S, int b, const double* __restrict__ G,
+                                                     const double* __restrict__ lo, const double* __restrict__ hi,
+                                                     const int* __restrict__ off, const double* __restrict__ gout,
+                                                     double* __restrict__ dG) {
+  const int s = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x * HT + tid;
+  __shared__ double Ls[HCH * M];
+  __shared__ double Hs[HCH * M];
+  double y[M], g[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    y[j] = (c < b) ? G[((size_t)s * M + j) * b + c] : -INFINITY;
+    g[j] = 0.0;
+  }
+  const int c0 = off[s], c1 = off[s + 1];
+  for (int k0 = c0; k0 < c1; k0 += HCH) {
+    const int nc = min(HCH, c1 - k0);
+    for (int e = tid; e < nc * M; e += HT) {
+      Ls[e] = lo[(size_t)k0 * M + e];
+      Hs[e] = hi[(size_t)k0 * M + e];
+    }
+    __syncthreads();
+    for (int k = 0; k < nc; ++k) {
+      double len[M], pass[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const double h = Hs[k * M + j];
+        const double raw = fmin(y[j], h) - Ls[k * M + j];
+        len[j] = fmax(raw, 0.0);
+        // d clamp_min/d raw = (raw >= 0); d minimum/d y = 1 (y<h), 1/2 (y==h), 0 (y>h)
+        const double dmin = (y[j] < h) ? 1.0 : ((y[j] == h) ? 0.5 : 0.0);
+        pass[j] = (raw >= 0.0) ? dmin : 0.0;
+      }
+      double pre[M + 1];
+      pre[0] = 1.0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) pre[j + 1] = pre[j] * len[j];
+      double suf = 1.0;
+#pragma unroll
+      for (int j = M - 1; j >= 0; --j) {
+        g[j] = fma(pass[j], pre[j] * suf, g[j]);
+        suf *= len[j];
+      }
+    }
+    __syncthreads();
+  }
+  if (c < b) {
+    const double gs = gout[c] / (double)S;
+#pragma unroll
+    for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = gs * g[j];
+  }
+}
+
+__global__ void mean_over_samples_kernel(int S, int b, const double* __restrict__ partial, double* __restrict__ acq) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  double s = 0.0;
+  for (int i = 0; i < S; ++i) s += partial[(size_t)i * b + c];
+  acq[c] = s / (double)S;
+}
+
+// samples backward: one thread per (c, j); writes gR_j (Rr x b)
+__global__ void qn_samples_bwd_kernel(int n, int nb, int S, int m, int b, const double* __restrict__ R,
+                                      const double* __restrict__ ys, const double* __restrict__ zq,
+                                      const double* __restrict__ oa, const double* __restrict__ L22,
+                                      const double* __restrict__ dG, double* __restrict__ gR) {
+  const int j = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  const long long Rr = (long long)n + nb + S + 1;
+  const double* Rj = R + (size_t)j * Rr * b;
+  double* gj = gR + (size_t)j * Rr * b;
+  const double A = oa[j];
+  double dmu = 0.0, dl = 0.0;
+  for (int si = 0; si < S; ++si) {
+    const double dy = A * dG[((size_t)si * m + j) * b + c];
+    dmu += dy;
+    dl = fma(dy, zq[(size_t)si * m + j], dl);
+    gj[(size_t)(n + nb + si) * b + c] = dy;
+  }
+  const double s = ys[j];
+  gj[(size_t)(n + nb + S) * b + c] = s * dmu;
+  const double l22 = L22[(size_t)j * b + c];
+  const double dbr = dl / (2.0 * l22);
+  const double dssv = -s * s * dbr;  // var = s^2 (kxx - ssv); br = var - ssw
+  const double dssw = -dbr;
+  for (int i = 0; i < n; ++i) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssv;
+  for (int i = n; i < n + nb; ++i) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssw;
+}
+
+// -------------------------------------------------------------------------------------
+// Pareto mask: thread per (sample s [fast], point i); O layout [j][i][s]
+// -------------------------------------------------------------------------------------
+template <int M>
+__global__ void pareto_kernel(int S, int n, const double* __restrict__ O, const double* __restrict__ ref,
+                              int dedup, unsigned char* __restrict__ mask, int* __restrict__ counts) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (s >= S) return;
+  double yi[M];
+  bool better = true;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    yi[j] = O[((size_t)j * n + i) * S + s];
+    better &= yi[j] > ref[j];
+  }
+  bool nd = better;
+  for (int k = 0; k < n && nd; ++k) {
+    if (k == i) continue;
+    bool ge = true, gt = false, eq = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const double v = O[((size_t)j * n + k) * S + s];
+      ge &= v >= yi[j];
+      gt |= v > yi[j];
+      eq &= v == yi[j];
+    }
+    if (ge && gt) nd = false;
+    if (dedup && eq && k < i) nd = false;
+  }
+  if (mask) mask[(size_t)s * n + i] = nd ? 1 : 0;
+  if (counts && nd) atomicAdd(&counts[i], 1);
+}
+
+__global__ void scale_batched_kernel(long long per, const double* __restrict__ alpha, double* __restrict__ X) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= per) return;
+  X[(size_t)blockIdx.y * per + e] *= alpha[blockIdx.y];
+}
+
+// E[b][r][idx[r]] += val[b]  (adds the row-selection matrix P, scaled, to E: nb x n)
+__global__ void add_selection_kernel(int nb, int n, const int* __restrict__ idx, const double* __restrict__ val,
+                                     double* __restrict__ E) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nb) return;
+  const int b = blockIdx.y;
+  E[((size_t)b * nb + r) * n + idx[r]] += val ? val[b] : 1.0;
+}
+
+__global__ void objective_affine_kernel(int m, int n, int S, const double* __restrict__ Y, const double* __restrict__ mu,
+                                        const double* __restrict__ a, const double* __restrict__ bb,
+                                        double* __restrict__ O) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tot = (long long)m * n * S;
+  if (e >= tot) return;
+  const int j = (int)(e / ((long long)n * S));
+  const int i = (int)((e / S) % n);
+  const double mv = mu ? mu[(size_t)j * n + i] : 0.0;
+  O[e] = fma(a[j], Y[e] + mv, bb[j]);
+}
+
+}  // namespace evr
+
+using namespace evr;
+
+#define EVR_DISPATCH_M(m, MACRO)                                                      \
+  switch (m) {                                                                        \
+    case 1: MACRO(1); break;                                                          \
+    case 2: MACRO(2); break;                                                          \
+    case 3: MACRO(3); break;                                                          \
+    case 4: MACRO(4); break;                                                          \
+    case 5: MACRO(5); break;                                                          \
+    case 6: MACRO(6); break;                                                          \
+    case 7: MACRO(7); break;                                                          \
+    case 8: MACRO(8); break;                                                          \
+    default: EVR_CHECK(false, "number of objectives m=%d not supported (1..8)", m);   \
+  }
+
+extern "C" {
+
+int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, double* G, double* L22,
+                       int* flags) {
+  EVR_CHECK(st && st->m >= 1 && st->S >= 1 && st->n >= 1 && st->nb >= 0, "evr_qnehvi_samples: bad state");
+  if (b == 0) return 0;
+  dim3 grid(cdiv(b, 256), st->m);
+  qn_samples_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys,
+                                                           st->kxx, st->zq, st->obj_a, st->obj_b, G, L22, flags);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* partial) {
+  EVR_CHECK(st && st->S >= 1, "evr_hvi_forward: bad state");
+  if (b == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int cpt = (b > HT) ? 2 : 1;
+  dim3 grid(cdiv(b, HT * cpt), st->S);
+#define L(MM)                                                                                                \
+  if (cpt == 2)                                                                                            \
+    hvi_fwd_kernel<MM, 2><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, partial); \
+  else                                                                                                     \
+    hvi_fwd_kernel<MM, 1><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, partial)
+  EVR_DISPATCH_M(st->m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_mean_over_samples(void* stream, int S, int b, const double* partial, double* acq) {
+  if (b == 0) return 0;
+  mean_over_samples_kernel<<<cdiv(b, 256), 256, 0, (hipStream_t)stream>>>(S, b, partial, acq);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
+                     double* dG) {
+  EVR_CHECK(st && st->S >= 1, "evr_hvi_backward: bad state");
+  if (b == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(cdiv(b, HT), st->S);
+#define L(MM) hvi_bwd_kernel<MM><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, gout, dG)
+  EVR_DISPATCH_M(st->m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* L22,
+                                const double* dG, double* gR) {
+  EVR_CHECK(st && st->m >= 1, "evr_qnehvi_samples_backward: bad state");
+  if (b == 0) return 0;
+  dim3 grid(cdiv(b, 256), st->m);
+  qn_samples_bwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq,
+                                                               st->obj_a, L22, dG, gR);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const double* ref, int dedup,
+                    unsigned char* mask, int* counts) {
+  EVR_CHECK(S >= 1 && n >= 0, "evr_pareto_mask: bad sizes");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(cdiv(S, 64), n);
+#define L(MM) pareto_kernel<MM><<<grid, 64, 0, s>>>(S, n, O, ref, dedup, mask, counts)
+  EVR_DISPATCH_M(m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_scale_batched(void* stream, int B, long long per, const double* alpha, double* X) {
+  if (per == 0) return 0;
+  dim3 grid(cdiv(per, 256), B);
+  scale_batched_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(per, alpha, X);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_add_selection(void* stream, int B, int nb, int n, const int* idx, const double* val, double* E) {
+  if (nb == 0) return 0;
+  dim3 grid(cdiv(nb, 256), B);
+  add_selection_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(nb, n, idx, val, E);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_objective_affine(void* stream, int m, int n, int S, const double* Y, const double* mu, const double* a,
+                         const double* b, double* O) {
+  const long long tot = (long long)m * n * S;
+  if (tot == 0) return 0;
+  objective_affine_kernel<<<cdiv(tot, 256), 256, 0, (hipStream_t)stream>>>(m, n, S, Y, mu, a, b, O);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,195 @@
+"""Exact GPs resident in HBM: batched posterior and MLL (value + gradient) on the HIP kernels.
+
+Mirrors BoFire's ``SingleTaskGPSurrogate`` model (bofire/surrogates/single_task_gp.py:39-71)
+on top of [upstream] BoTorch ``SingleTaskGP``: Normalize(bounds) inputs, Standardize outputs,
+ConstantMean, RBF/Matérn ARD kernel (no outputscale by default), Gaussian likelihood with
+noise >= 1e-4 and hyperpriors; fit = scipy L-BFGS-B on the raw parameters
+(``fit_gpytorch_mll``, max_attempts=10), every loss/gradient evaluated on the device.
+
+``GPBatch`` holds B exact GPs that share the same normalized training inputs (the
+ModelListGP of BotorchSurrogates.compatibilize, bofire/surrogates/botorch_surrogates.py:79-128)
+so that posteriors for all outputs are one batched launch.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import ops
+
+MIN_INFERRED_NOISE_LEVEL = 1e-4
+
+
+def softplus_np(x):
+    return np.logaddexp(0.0, x)
+
+
+def sigmoid_np(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def lognormal_logpdf_np(x, loc, scale):
+    lx = np.log(x)
+    return -lx - math.log(scale) - 0.5 * math.log(2 * math.pi) - 0.5 * ((lx - loc) / scale) ** 2
+
+
+def lognormal_dlogpdf_np(x, loc, scale):
+    lx = np.log(x)
+    return (-1.0 - (lx - loc) / scale ** 2) / x
+
+
+def standardize_params(y: np.ndarray) -> Tuple[float, float]:
+    """[upstream] Standardize(m=1): mean, unbiased std, std < 1e-8 -> 1, n == 1 -> 1."""
+    mean = float(np.mean(y))
+    if y.shape[0] == 1:
+        return mean, 1.0
+    std = float(np.std(y, ddof=1))
+    return mean, (std if std >= 1e-8 else 1.0)
+
+
+@dataclass
+class GPHyper:
+    lengthscale: np.ndarray   # d
+    noise: float
+    constant: float
+    y_mean: float
+    y_std: float
+
+
+class GPBatch:
+    """B exact GPs on shared normalized inputs Xn (n x d, device)."""
+
+    def __init__(self, Xn: torch.Tensor, Y: torch.Tensor, hypers: Sequence[GPHyper], kind: int,
+                 lo: torch.Tensor, hi: torch.Tensor):
+        self.Xn = Xn.contiguous()
+        self.kind = int(kind)
+        self.lo = lo
+        self.hi = hi
+        self.inv_range = 1.0 / (hi - lo)
+        self.hypers = list(hypers)
+        dev = Xn.device
+        self.device = dev
+        self.B = len(hypers)
+        self.n, self.d = Xn.shape
+        t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
+        self.ls = t(np.stack([h.lengthscale for h in hypers]))
+        self.noise = t([h.noise for h in hypers])
+        self.const = t([h.constant for h in hypers])
+        self.ym = t([h.y_mean for h in hypers])
+        self.ys = t([h.y_std for h in hypers])
+        self.kxx = torch.ones(self.B, dtype=torch.float64, device=dev)
+        # standardized targets (B x n)
+        Yc = Y.to(device=dev, dtype=torch.float64).reshape(self.n, self.B).T.contiguous()
+        self.y = ((Yc - self.ym[:, None]) / self.ys[:, None]).contiguous()
+        self.refresh()
+
+    # -- caches: L = chol(K + s2 I), Linv, alpha, M = [Linv; alpha^T] ----------------------
+    def refresh(self):
+        Ky = ops.kernel_matrix(self.Xn, self.Xn, self.ls, self.kind, diag_add=self.noise)
+        self.L, _, _ = ops.cholesky(Ky, 1e-8, 3)
+        self.Linv = ops.tri_inv(self.L)
+        r = (self.y - self.const[:, None]).unsqueeze(-1).contiguous()         # B x n x 1
+        v = ops.gemm(self.Linv, r)
+        self.alpha = ops.gemm(self.Linv, v, transA=True)[..., 0].contiguous()  # B x n
+        self.M = torch.cat([self.Linv, self.alpha.unsqueeze(1)], dim=1).contiguous()  # B x (n+1) x n
+
+    def kernel_train(self, noise: bool = False) -> torch.Tensor:
+        return ops.kernel_matrix(self.Xn, self.Xn, self.ls, self.kind, diag_add=self.noise if noise else None)
+
+    def cross(self, Xraw: torch.Tensor) -> torch.Tensor:
+        """K(Xtr, normalize(Xraw)) : B x n x nt."""
+        return ops.kernel_matrix(self.Xn, Xraw, self.ls, self.kind, shift2=self.lo, scale2=self.inv_range)
+
+    def posterior(self, Xraw: torch.Tensor, observation_noise: bool = False):
+        """Mean and variance (B x nt) at raw (transformed, unnormalized) inputs."""
+        Kx = self.cross(Xraw)
+        R = ops.gemm(self.M, Kx)
+        return ops.posterior_finalize(R, self.const, self.ym, self.ys, self.kxx,
+                                      self.noise if observation_noise else None)
+
+
+# ---------------------------------------------------------------------------------------
+# device MLL value + gradient (one output)
+# ---------------------------------------------------------------------------------------
+class MLLEvaluator:
+    """Exact MLL / n with hyperpriors for one GP on device; raw parameter vector
+    x = [noise, constant, raw_lengthscale(d)] (BoTorch bounds: noise >= 1e-4)."""
+
+    def __init__(self, Xn: torch.Tensor, y_std_space: np.ndarray, kind: int,
+                 ls_prior: Optional[Tuple[float, float]], noise_prior: Optional[Tuple[float, float]]):
+        self.Xn = Xn.contiguous()
+        self.n, self.d = Xn.shape
+        self.kind = kind
+        self.y = np.asarray(y_std_space, dtype=np.float64)
+        self.ls_prior = ls_prior
+        self.noise_prior = noise_prior
+        self.dev = Xn.device
+
+    def __call__(self, x: np.ndarray):
+        n, d = self.n, self.d
+        noise, const, raw = float(x[0]), float(x[1]), np.asarray(x[2:], dtype=np.float64)
+        ls = softplus_np(raw)
+        dev = self.dev
+        ls_t = torch.as_tensor(ls[None, :], device=dev)
+        Ky = ops.kernel_matrix(self.Xn, self.Xn, ls_t, self.kind,
+                               diag_add=torch.tensor([noise], dtype=torch.float64, device=dev))
+        L, _, _ = ops.cholesky(Ky, 1e-8, 3)
+        Linv = ops.tri_inv(L)
+        r = torch.as_tensor((self.y - const)[None, :, None], device=dev)
+        v = ops.gemm(Linv, r)
+        alpha = ops.gemm(Linv, v, transA=True)                       # 1 x n x 1
+        W = ops.gemm(alpha, alpha, transB=True)                      # alpha alpha^T
+        ops.gemm(Linv, Linv, transA=True, alpha=-1.0, beta=1.0, out=W)   # - K^-1
+        gls = ops.kernel_lengthscale_grad(self.Xn, ls_t, W, self.kind)  # 1 x d
+        terms = ops.mll_terms(L, Linv, r[..., 0].contiguous(), alpha[..., 0].contiguous())
+        terms = terms.cpu().numpy()[0]
+        gls = gls.cpu().numpy()[0]
+        logdet, quad, trKinv, sum_a, sum_a2 = terms
+        ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * math.log(2 * math.pi)
+        d_noise = 0.5 * (sum_a2 - trKinv)
+        d_const = sum_a
+        d_ls = 0.5 * gls
+        if self.ls_prior is not None:
+            ll += float(np.sum(lognormal_logpdf_np(ls, *self.ls_prior)))
+            d_ls = d_ls + lognormal_dlogpdf_np(ls, *self.ls_prior)
+        if self.noise_prior is not None:
+            ll += float(lognormal_logpdf_np(noise, *self.noise_prior))
+            d_noise += float(lognormal_dlogpdf_np(noise, *self.noise_prior))
+        d_raw = d_ls * sigmoid_np(raw)
+        g = np.concatenate([[d_noise, d_const], d_raw]) / n
+        return ll / n, g
+
+
+def fit_single(Xn: torch.Tensor, y_raw: np.ndarray, kind: int, ls_prior, noise_prior=(-4.0, 1.0),
+               max_attempts: int = 10, seed: int = 0, options: Optional[dict] = None) -> GPHyper:
+    """fit_gpytorch_mll restated on device kernels: minimise -mll with scipy L-BFGS-B over
+    (noise >= 1e-4, constant, raw lengthscale); on NotPSDError resample the hyperparameters
+    from their priors and retry (max_attempts)."""
+    from scipy.optimize import minimize
+
+    y_mean, y_std = standardize_params(y_raw)
+    y = (y_raw - y_mean) / y_std
+    d = Xn.shape[1]
+    ev = MLLEvaluator(Xn, y, kind, ls_prior, noise_prior)
+    noise0 = math.exp(noise_prior[0] - noise_prior[1] ** 2) if noise_prior else 2 * MIN_INFERRED_NOISE_LEVEL
+    x0 = np.concatenate([[noise0, 0.0], np.zeros(d)])
+    bounds = [(MIN_INFERRED_NOISE_LEVEL, None), (None, None)] + [(None, None)] * d
+    rng = np.random.default_rng(seed)
+    last_err = None
+    for attempt in range(max_attempts):
+        try:
+            res = minimize(lambda x: tuple(-v for v in ev(x)), x0, jac=True, method="L-BFGS-B", bounds=bounds,
+                           options=options or {})
+            xv = res.x
+            return GPHyper(lengthscale=softplus_np(xv[2:]), noise=float(xv[0]), constant=float(xv[1]),
+                           y_mean=y_mean, y_std=y_std)
+        except ops.NotPSDError as e:  # resample from priors (sample_all_priors)
+            last_err = e
+            ls = (np.exp(rng.normal(ls_prior[0], ls_prior[1], d)) if ls_prior else np.full(d, math.log(2.0)))
+            nz = max(float(np.exp(rng.normal(*noise_prior))) if noise_prior else 1e-3, MIN_INFERRED_NOISE_LEVEL)
+            x0 = np.concatenate([[nz, 0.0], np.log(np.expm1(ls))])
+    raise RuntimeError(f"GP fit failed after {max_attempts} attempts: {last_err}")

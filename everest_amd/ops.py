@@ -1,0 +1,357 @@
+"""Torch-tensor level wrappers over the C-ABI (include/everest_amd.h).
+
+Every op runs on torch's *current* HIP stream, takes float64 device tensors, allocates
+its outputs with the torch caching allocator and never frees caller memory.  Shape,
+dtype and device errors raise (``ValueError`` / ``RuntimeError``); there is no CPU path.
+The top-level ops are also registered as PyTorch custom ops (``torch.ops.everest_amd.*``).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import EvrQnehviState, call
+
+KERNELS = {"rbf": 0, "matern05": 1, "matern15": 2, "matern25": 3}
+KIND_BY_NU = {0.5: 1, 1.5: 2, 2.5: 3}
+
+
+class NotPSDError(RuntimeError):
+    """Raised when the jitter ladder of psd_safe_cholesky is exhausted ([upstream]
+    linear_operator NotPSDError, caught by fit_gpytorch_mll's retries)."""
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(t: torch.Tensor, name: str, dtype=torch.float64) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: everest_amd ops run on the MI355X only (got device {t.device}); "
+                           "there is no CPU fallback")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# ---------------------------------------------------------------------------------------
+# kernel matrices
+# ---------------------------------------------------------------------------------------
+def kernel_matrix(X1, X2, lengthscales, kind: int = 0, shift1=None, scale1=None, shift2=None, scale2=None,
+                  outputscale=None, diag_add=None) -> torch.Tensor:
+    """K[b] = os_b * k(norm(X1), norm(X2); ls_b) (+ diag_add_b on i==j).  ls: B x d."""
+    X1 = _dev(X1, "X1")
+    X2 = _dev(X2, "X2")
+    ls = _dev(lengthscales, "lengthscales")
+    if ls.dim() == 1:
+        ls = ls.unsqueeze(0)
+    B, d = ls.shape
+    if X1.shape[-1] != d or X2.shape[-1] != d:
+        raise ValueError(f"kernel_matrix: dims mismatch X1 {tuple(X1.shape)} X2 {tuple(X2.shape)} ls {tuple(ls.shape)}")
+    n1, n2 = X1.shape[0], X2.shape[0]
+    K = torch.empty(B, n1, n2, dtype=torch.float64, device=X1.device)
+    opt = [None if t is None else _dev(t, "aux") for t in (shift1, scale1, shift2, scale2, outputscale, diag_add)]
+    call("evr_kernel_matrix", _stream(), int(kind), B, n1, n2, d, X1.data_ptr(), _p(opt[0]), _p(opt[1]),
+         X2.data_ptr(), _p(opt[2]), _p(opt[3]), ls.data_ptr(), _p(opt[4]), _p(opt[5]), K.data_ptr())
+    return K
+
+
+def kernel_cross_grad(X1, X2, lengthscales, G, kind=0, shift1=None, scale1=None, shift2=None, scale2=None,
+                      outputscale=None) -> torch.Tensor:
+    X1, X2, ls, G = _dev(X1, "X1"), _dev(X2, "X2"), _dev(lengthscales, "ls"), _dev(G, "G")
+    B, d = ls.shape
+    n1, n2 = X1.shape[0], X2.shape[0]
+    if tuple(G.shape) != (B, n1, n2):
+        raise ValueError(f"kernel_cross_grad: G shape {tuple(G.shape)} != {(B, n1, n2)}")
+    dX = torch.empty(n2, d, dtype=torch.float64, device=X1.device)
+    opt = [None if t is None else _dev(t, "aux") for t in (shift1, scale1, shift2, scale2, outputscale)]
+    call("evr_kernel_cross_grad", _stream(), int(kind), B, n1, n2, d, X1.data_ptr(), _p(opt[0]), _p(opt[1]),
+         X2.data_ptr(), _p(opt[2]), _p(opt[3]), ls.data_ptr(), _p(opt[4]), G.data_ptr(), dX.data_ptr())
+    return dX
+
+
+def kernel_lengthscale_grad(X, lengthscales, W, kind=0) -> torch.Tensor:
+    X, ls, W = _dev(X, "X"), _dev(lengthscales, "ls"), _dev(W, "W")
+    B, d = ls.shape
+    n = X.shape[0]
+    g = torch.empty(B, d, dtype=torch.float64, device=X.device)
+    work = torch.empty(B, n, d, dtype=torch.float64, device=X.device)
+    call("evr_kernel_lengthscale_grad", _stream(), int(kind), B, n, d, X.data_ptr(), ls.data_ptr(), W.data_ptr(),
+         g.data_ptr(), work.data_ptr())
+    return g
+
+
+def mll_terms(L, Linv, r, alpha) -> torch.Tensor:
+    """B x 5: logdet, quad, tr(K^-1), sum(alpha), sum(alpha^2)."""
+    L, Linv, r, alpha = _dev(L, "L"), _dev(Linv, "Linv"), _dev(r, "r"), _dev(alpha, "alpha")
+    B, n, _ = L.shape
+    out = torch.empty(B, 5, dtype=torch.float64, device=L.device)
+    call("evr_gp_mll_terms", _stream(), B, n, L.data_ptr(), Linv.data_ptr(), r.data_ptr(), alpha.data_ptr(),
+         out.data_ptr())
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# dense linear algebra
+# ---------------------------------------------------------------------------------------
+def gemm(A, B, transA=False, transB=False, alpha=1.0, beta=0.0, out=None) -> torch.Tensor:
+    """Batched C = alpha op(A) op(B) + beta C on the f64 MFMA kernel.  A, B: (batch) x r x c."""
+    A, B = _dev(A, "A"), _dev(B, "B")
+    a3, b3 = A.dim() == 3, B.dim() == 3
+    if A.dim() == 2:
+        A = A.unsqueeze(0)
+    if B.dim() == 2:
+        B = B.unsqueeze(0)
+    batch = max(A.shape[0], B.shape[0])
+    if A.shape[0] not in (1, batch) or B.shape[0] not in (1, batch):
+        raise ValueError("gemm: batch mismatch")
+    M, K = (A.shape[2], A.shape[1]) if transA else (A.shape[1], A.shape[2])
+    K2, N = (B.shape[2], B.shape[1]) if transB else (B.shape[1], B.shape[2])
+    if K != K2:
+        raise ValueError(f"gemm: inner dims {K} != {K2}")
+    if out is None:
+        out = torch.zeros(batch, M, N, dtype=torch.float64, device=A.device)
+        beta = 0.0
+    else:
+        if out.dim() == 2:
+            out = out.unsqueeze(0)
+        if tuple(out.shape) != (batch, M, N) or not out.is_contiguous():
+            raise ValueError("gemm: bad out tensor")
+    sA = 0 if A.shape[0] == 1 else A.shape[1] * A.shape[2]
+    sB = 0 if B.shape[0] == 1 else B.shape[1] * B.shape[2]
+    call("evr_gemm_f64", _stream(), int(transA), int(transB), M, N, K, float(alpha), A.data_ptr(), A.shape[2], sA,
+         B.data_ptr(), B.shape[2], sB, float(beta), out.data_ptr(), N, M * N, batch)
+    return out if (a3 or b3) else out[0]
+
+
+def gemm_into(out_view: torch.Tensor, A, B, transA=False, transB=False, alpha=1.0, beta=0.0, batch_strides=None):
+    """GEMM writing into a strided 2-D/3-D row block (rows contiguous with leading dim ld)."""
+    A, B = _dev(A, "A"), _dev(B, "B")
+    if A.dim() == 2:
+        A = A.unsqueeze(0)
+    if B.dim() == 2:
+        B = B.unsqueeze(0)
+    o = out_view if out_view.dim() == 3 else out_view.unsqueeze(0)
+    batch = o.shape[0]
+    M, K = (A.shape[2], A.shape[1]) if transA else (A.shape[1], A.shape[2])
+    K2, N = (B.shape[2], B.shape[1]) if transB else (B.shape[1], B.shape[2])
+    if K != K2 or o.shape[1] != M or o.shape[2] != N or o.stride(2) != 1:
+        raise ValueError("gemm_into: shape mismatch")
+    sA = 0 if A.shape[0] == 1 else A.stride(0)
+    sB = 0 if B.shape[0] == 1 else B.stride(0)
+    call("evr_gemm_f64", _stream(), int(transA), int(transB), M, N, K, float(alpha), A.data_ptr(), A.stride(1), sA,
+         B.data_ptr(), B.stride(1), sB, float(beta), o.data_ptr(), o.stride(1), o.stride(0), batch)
+
+
+def cholesky(A: torch.Tensor, jitter0: float = 1e-8, max_tries: int = 3, raise_on_fail: bool = True):
+    """psd_safe_cholesky on a batch (B x n x n).  Returns (L, jitter_used[B], info[B])."""
+    A = _dev(A, "A")
+    squeeze = A.dim() == 2
+    if squeeze:
+        A = A.unsqueeze(0)
+    B, n, n2 = A.shape
+    if n != n2:
+        raise ValueError("cholesky: matrix not square")
+    L = torch.empty_like(A)
+    jit = torch.empty(B, dtype=torch.float64, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    call("evr_cholesky", _stream(), B, n, A.data_ptr(), n, n * n, L.data_ptr(), n, n * n, float(jitter0),
+         int(max_tries), jit.data_ptr(), info.data_ptr())
+    if raise_on_fail:
+        bad = info.cpu()
+        if bool(bad.any()):
+            raise NotPSDError(f"Matrix not positive definite after repeatedly adding jitter up to "
+                              f"{jitter0 * 10 ** (max_tries - 1):.1e} (batch members {bad.nonzero().view(-1).tolist()})")
+    if squeeze:
+        return L[0], jit[0], info[0]
+    return L, jit, info
+
+
+def trsm(L: torch.Tensor, B: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """In place: B <- L^-1 B (or L^-T B).  L: (batch) x n x n, B: (batch) x n x nrhs."""
+    L = _dev(L, "L")
+    if not B.is_contiguous() or B.dtype != torch.float64 or B.device.type != "cuda":
+        raise ValueError("trsm: B must be a contiguous float64 device tensor (solved in place)")
+    L3 = L if L.dim() == 3 else L.unsqueeze(0)
+    B3 = B if B.dim() == 3 else B.unsqueeze(0)
+    batch = B3.shape[0]
+    n = L3.shape[1]
+    nrhs = B3.shape[2]
+    sL = 0 if L3.shape[0] == 1 else n * n
+    call("evr_trsm_lower", _stream(), batch, n, nrhs, L3.data_ptr(), n, sL, int(transpose), B3.data_ptr(), nrhs,
+         n * nrhs)
+    return B
+
+
+def tri_inv(L: torch.Tensor) -> torch.Tensor:
+    L = _dev(L, "L")
+    L3 = L if L.dim() == 3 else L.unsqueeze(0)
+    batch, n, _ = L3.shape
+    out = torch.empty_like(L3)
+    call("evr_tri_inv_lower", _stream(), batch, n, L3.data_ptr(), n, n * n, out.data_ptr(), n, n * n)
+    return out if L.dim() == 3 else out[0]
+
+
+def posterior_finalize(R, c, ym, ys, kxx, noise_add=None):
+    R = _dev(R, "R")
+    B, n1, nt = R.shape
+    mean = torch.empty(B, nt, dtype=torch.float64, device=R.device)
+    var = torch.empty_like(mean)
+    args = [_dev(t, "aux") for t in (c, ym, ys, kxx)]
+    na = None if noise_add is None else _dev(noise_add, "noise")
+    call("evr_gp_posterior_finalize", _stream(), B, n1 - 1, nt, R.data_ptr(), *[a.data_ptr() for a in args],
+         _p(na), mean.data_ptr(), var.data_ptr())
+    return mean, var
+
+
+# ---------------------------------------------------------------------------------------
+# qNEHVI pieces
+# ---------------------------------------------------------------------------------------
+def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cell_lo, cell_hi, cell_off) -> EvrQnehviState:
+    st = EvrQnehviState()
+    st.n, st.nb, st.S, st.m = int(n), int(nb), int(S), int(m)
+    st.c, st.ym, st.ys, st.kxx = c.data_ptr(), ym.data_ptr(), ys.data_ptr(), kxx.data_ptr()
+    st.zq, st.obj_a, st.obj_b = zq.data_ptr(), obj_a.data_ptr(), obj_b.data_ptr()
+    st.cell_lo, st.cell_hi, st.cell_off = cell_lo.data_ptr(), cell_hi.data_ptr(), cell_off.data_ptr()
+    return st
+
+
+def qnehvi_samples(st: EvrQnehviState, R: torch.Tensor, b: int):
+    dev = R.device
+    G = torch.empty(st.S, st.m, b, dtype=torch.float64, device=dev)
+    L22 = torch.empty(st.m, b, dtype=torch.float64, device=dev)
+    flags = torch.empty(st.m, b, dtype=torch.int32, device=dev)
+    call("evr_qnehvi_samples", _stream(), ctypes.byref(st), b, R.data_ptr(), G.data_ptr(), L22.data_ptr(),
+         flags.data_ptr())
+    return G, L22, flags
+
+
+def hvi_forward(st: EvrQnehviState, G: torch.Tensor, b: int):
+    partial = torch.empty(st.S, b, dtype=torch.float64, device=G.device)
+    call("evr_hvi_forward", _stream(), ctypes.byref(st), b, G.data_ptr(), partial.data_ptr())
+    return partial
+
+
+def mean_over_samples(partial: torch.Tensor):
+    S, b = partial.shape
+    acq = torch.empty(b, dtype=torch.float64, device=partial.device)
+    call("evr_mean_over_samples", _stream(), S, b, partial.data_ptr(), acq.data_ptr())
+    return acq
+
+
+def hvi_backward(st: EvrQnehviState, G: torch.Tensor, gout: torch.Tensor, b: int):
+    dG = torch.empty_like(G)
+    gout = _dev(gout, "gout")
+    call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), gout.data_ptr(), dG.data_ptr())
+    return dG
+
+
+def qnehvi_samples_backward(st: EvrQnehviState, R, L22, dG, b: int):
+    gR = torch.empty_like(R)
+    call("evr_qnehvi_samples_backward", _stream(), ctypes.byref(st), b, R.data_ptr(), L22.data_ptr(), dG.data_ptr(),
+         gR.data_ptr())
+    return gR
+
+
+def pareto_mask(O: torch.Tensor, ref: torch.Tensor, dedup: bool, want_mask=True, want_counts=False):
+    """O: m x n x S.  Returns (mask S x n uint8 | None, counts n int32 | None)."""
+    O, ref = _dev(O, "O"), _dev(ref, "ref")
+    m, n, S = O.shape
+    mask = torch.empty(S, n, dtype=torch.uint8, device=O.device) if want_mask else None
+    counts = torch.zeros(n, dtype=torch.int32, device=O.device) if want_counts else None
+    call("evr_pareto_mask", _stream(), S, n, m, O.data_ptr(), ref.data_ptr(), int(dedup), _p(mask), _p(counts))
+    return mask, counts
+
+
+def objective_affine(Y: torch.Tensor, mu: Optional[torch.Tensor], a: torch.Tensor, b: torch.Tensor):
+    Y = _dev(Y, "Y")
+    m, n, S = Y.shape
+    O = torch.empty_like(Y)
+    mu = None if mu is None else _dev(mu, "mu")
+    call("evr_objective_affine", _stream(), m, n, S, Y.data_ptr(), _p(mu), _dev(a, "a").data_ptr(),
+         _dev(b, "b").data_ptr(), O.data_ptr())
+    return O
+
+
+def scale_batched(X: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    """In place X[b] *= alpha[b]."""
+    if not X.is_contiguous():
+        raise ValueError("scale_batched: X must be contiguous")
+    B = X.shape[0]
+    call("evr_scale_batched", _stream(), B, X.numel() // B, _dev(alpha, "alpha").data_ptr(), X.data_ptr())
+    return X
+
+
+def add_selection(E: torch.Tensor, idx: torch.Tensor, val: Optional[torch.Tensor]) -> torch.Tensor:
+    """In place E[b][r][idx[r]] += val[b]; E: B x nb x n, idx int32 (nb)."""
+    B, nb, n = E.shape
+    idx = _dev(idx, "idx", torch.int32)
+    call("evr_add_selection", _stream(), B, nb, n, idx.data_ptr(), _p(None if val is None else _dev(val, "val")),
+         E.data_ptr())
+    return E
+
+
+def box_decompose(obj: np.ndarray, ref: np.ndarray, mask: Optional[np.ndarray] = None, num_threads: int = 0,
+                  layout: str = "jis"):
+    """Host box decomposition.  obj: float64 numpy array, layout 'jis' (m x n x S) or 'sij'
+    (S x n x m).  Returns (lo [C x m], hi [C x m], off [S+1]) numpy arrays."""
+    lib = _native.load()
+    obj = np.ascontiguousarray(obj, dtype=np.float64)
+    if layout == "jis":
+        m, n, S = obj.shape
+        ss, si, sj = 1, S, n * S
+    elif layout == "sij":
+        S, n, m = obj.shape
+        ss, si, sj = n * m, m, 1
+    else:
+        raise ValueError(layout)
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    mk = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    handle = ctypes.c_void_p()
+    _native.check(lib.evr_box_decompose(S, n, m, obj.ctypes.data, ss, si, sj,
+                                        None if mk is None else mk.ctypes.data, ref.ctypes.data, int(num_threads),
+                                        ctypes.byref(handle)), "evr_box_decompose")
+    try:
+        total = lib.evr_cells_total(handle)
+        lo = np.empty((total, m), dtype=np.float64)
+        hi = np.empty((total, m), dtype=np.float64)
+        off = np.empty(S + 1, dtype=np.int32)
+        lib.evr_cells_copy(handle, lo.ctypes.data, hi.ctypes.data, off.ctypes.data)
+    finally:
+        lib.evr_cells_free(handle)
+    return lo, hi, off
+
+
+def device_arch(device: int = 0) -> str:
+    buf = ctypes.create_string_buffer(64)
+    call("evr_device_arch", device, buf, 64)
+    return buf.value.decode()
+
+
+# ---------------------------------------------------------------------------------------
+# torch custom-op registrations (torch.ops.everest_amd.*)
+# ---------------------------------------------------------------------------------------
+try:
+    @torch.library.custom_op("everest_amd::kernel_matrix", mutates_args=())
+    def _op_kernel_matrix(X1: torch.Tensor, X2: torch.Tensor, lengthscales: torch.Tensor, kind: int) -> torch.Tensor:
+        return kernel_matrix(X1, X2, lengthscales, kind)
+
+    @torch.library.custom_op("everest_amd::cholesky", mutates_args=())
+    def _op_cholesky(A: torch.Tensor, jitter0: float, max_tries: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        return cholesky(A, jitter0, max_tries, raise_on_fail=False)
+
+    @torch.library.custom_op("everest_amd::tri_inv", mutates_args=())
+    def _op_tri_inv(L: torch.Tensor) -> torch.Tensor:
+        return tri_inv(L)
+except Exception:  # pragma: no cover - older torch without torch.library.custom_op
+    pass

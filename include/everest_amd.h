@@ -1,0 +1,170 @@
+/*
+ * everest_amd — MI355X-native (gfx950) GP-surrogate + qNEHVI hot path of BoFire.
+ *
+ * C-ABI drop-in boundary.  Plain pointers and sizes only; every device pointer is an
+ * HBM allocation owned by the caller (torch tensors in the Python host layer); every
+ * entry point enqueues on the given HIP stream (hipStream_t passed as void*) and returns
+ * 0 on success, non-zero on error with the message in evr_last_error().  Layouts are
+ * row-major float64 unless stated.
+ *
+ * The reference (experimental-design/everest = BoFire) has no FFI: its hot path hands
+ * control to BoTorch/GPyTorch from Python.  Each entry point below names the reference
+ * call site whose [upstream] arithmetic it replaces (paths relative to the reference root).
+ */
+#ifndef EVEREST_AMD_H
+#define EVEREST_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EVR_VERSION 1
+
+/* kernel families: bofire/kernels/mapper.py:31-69 (RBFKernel, MaternKernel nu) */
+#define EVR_KERNEL_RBF 0
+#define EVR_KERNEL_MATERN05 1
+#define EVR_KERNEL_MATERN15 2
+#define EVR_KERNEL_MATERN25 3
+
+int evr_version(void);
+const char* evr_last_error(void);
+int evr_device_arch(int device, char* buf, int buflen);
+int evr_stream_sync(void* stream);
+
+/* ---- kernel-matrix assembly ---------------------------------------------------------
+ * K[b][i][j] = outputscale[b] * k( ||(x1n_i - x2n_j) / ls[b]|| ) (+ diag_add[b] if i==j)
+ * x1n = (X1 - shift1) * scale1, x2n = (X2 - shift2) * scale2 per column (NULL = identity),
+ * X1: n1 x d, X2: n2 x d, ls: B x d, K: B x n1 x n2 (ld n2).
+ * Replaces gpytorch RBFKernel/MaternKernel forward under the Normalize input transform
+ * called from bofire/surrogates/single_task_gp.py:48-66 and every posterior() call
+ * (bofire/strategies/predictives/botorch.py:180; bofire/surrogates/botorch.py:27,33). */
+int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d,
+                      const double* X1, const double* shift1, const double* scale1,
+                      const double* X2, const double* shift2, const double* scale2,
+                      const double* lengthscales, const double* outputscale,
+                      const double* diag_add, double* K);
+
+/* dX2[c][k] = sum_b sum_i G[b][i][c] * dK_b(x1_i, x2_c)/dX2[c][k]  (chain through shift2/scale2)
+ * G: B x n1 x n2.  Backward of the cross-covariance for the acquisition gradient
+ * (autograd inside gen_candidates_scipy, bofire/strategies/predictives/botorch.py:384-405). */
+int evr_kernel_cross_grad(void* stream, int kind, int B, int n1, int n2, int d,
+                          const double* X1, const double* shift1, const double* scale1,
+                          const double* X2, const double* shift2, const double* scale2,
+                          const double* lengthscales, const double* outputscale,
+                          const double* G, double* dX2);
+
+/* MLL gradient pieces for the exact GP fit (fit_gpytorch_mll,
+ * bofire/surrogates/single_task_gp.py:70-71):
+ * gls[b][k] = sum_{i,j} W[b][i][j] * dK_b[i][j]/d ls[b][k]   (W symmetric, X normalized);
+ * work: B*n*d doubles (per-row partials, summed in fixed order -> bitwise reproducible). */
+int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, const double* X,
+                                const double* lengthscales, const double* W, double* gls,
+                                double* work);
+/* out[b][0..4] = {2 sum log L_ii, r.alpha, ||Linv||_F^2 (= tr K^-1), sum alpha, sum alpha^2}
+ * — the scalar terms of the exact MLL and of its noise/constant gradients. */
+int evr_gp_mll_terms(void* stream, int B, int n, const double* L, const double* Linv,
+                     const double* r, const double* alpha, double* out);
+
+/* ---- dense float64 linear algebra --------------------------------------------------- */
+int evr_gemm_f64(void* stream, int transA, int transB, int M, int N, int K, double alpha,
+                 const double* A, int lda, long long strideA, const double* B, int ldb,
+                 long long strideB, double beta, double* C, int ldc, long long strideC, int batch);
+
+/* Batched Cholesky with [upstream] linear_operator psd_safe_cholesky semantics: plain
+ * attempt, then total diagonal jitter jitter0*10^(t-1) for t = 1..max_tries; info[b] = 0
+ * on success, 1 if still not p.d. (NotPSDError).  A and L must not alias.
+ * Replaces the Cholesky behind GPyTorch exact inference (K + sigma^2 I), the qNEHVI
+ * baseline root (bofire/strategies/predictives/qnehvi.py:46, cache_root=True) and the
+ * prune-sampling root (qnehvi.py:44, prune_baseline=True). */
+int evr_cholesky(void* stream, int batch, int n, const double* A, int lda, long long strideA,
+                 double* L, int ldl, long long strideL, double jitter0, int max_tries,
+                 double* jitter_used, int* info);
+
+/* In-place B <- L^-1 B (transpose=0) or L^-T B (transpose=1); L lower, n x n; B n x nrhs. */
+int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, int ldl,
+                   long long strideL, int transpose, double* B, int ldb, long long strideB);
+int evr_tri_inv_lower(void* stream, int batch, int n, const double* L, int ldl, long long strideL,
+                      double* Linv, int ldi, long long strideI);
+
+/* ---- GP posterior --------------------------------------------------------------------
+ * Given R[b] = [Linv_b; alpha_b^T] * K(Xtr, Xtest)  ((n+1) x nt per output, ld nt):
+ * mean[b][t] = ym[b] + ys[b]*(c[b] + R[b][n][t]);
+ * var[b][t]  = ys[b]^2 * (kxx[b] - sum_{i<n} R[b][i][t]^2 + noise_add[b]).
+ * Replaces [upstream] GPyTorch exact prediction (fast_pred_var covar cache) + Standardize
+ * untransform, called at bofire/strategies/predictives/botorch.py:180 and
+ * bofire/surrogates/botorch.py:27-33. */
+int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* R,
+                              const double* c, const double* ym, const double* ys,
+                              const double* kxx, const double* noise_add,
+                              double* mean, double* var);
+
+/* ---- qNEHVI (q = 1) -----------------------------------------------------------------
+ * Replaces [upstream] qNoisyExpectedHypervolumeImprovement.forward/backward as built at
+ * bofire/strategies/predictives/qnehvi.py:39-52 (cached-Cholesky sampling + box-cell HVI).
+ * Per output j the precomputed operator M_j = [Linv; G; H^T; alpha^T] (rows Rr =
+ * n + nb + S + 1) has been applied to k(Xtr, x): R_j = M_j K_x (Rr x b, ld b). */
+typedef struct {
+  int n, nb, S, m;          /* train points, pruned baseline, MC samples, objectives */
+  const double* c;          /* m: constant mean (standardized space) */
+  const double* ym;         /* m: Standardize mean */
+  const double* ys;         /* m: Standardize std */
+  const double* kxx;        /* m: prior variance k(x,x) */
+  const double* zq;         /* S x m: base samples of the new point */
+  const double* obj_a;      /* m: objective g_j = a_j*y_j + b_j */
+  const double* obj_b;      /* m */
+  /* box-decomposition cells (maximisation space), AoS per cell, ragged per sample */
+  const double* cell_lo;    /* total_cells x m */
+  const double* cell_hi;    /* total_cells x m (may be +inf) */
+  const int* cell_off;      /* S + 1 */
+} evr_qnehvi_state;
+
+/* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b
+ * (0 ok, 1 new-block Cholesky failed after 6 jitter tries). */
+int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R,
+                       double* G, double* L22, int* flags);
+/* partial[s][c] = HVI of G[s][:, c] over the cells of sample s */
+int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
+                    double* partial);
+/* acq[c] = mean_s partial[s][c] */
+int evr_mean_over_samples(void* stream, int S, int b, const double* partial, double* acq);
+/* dG[s][j][c] = gout[c]/S * dHVI_s/dg_j (torch min/clamp_min/prod subgradients) */
+int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
+                     const double* gout, double* dG);
+/* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
+int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
+                                const double* L22, const double* dG, double* gR);
+
+/* ---- Pareto / pruning ---------------------------------------------------------------
+ * O: m x n x S (objective samples, layout [j][i][s]).  For every sample s and point i:
+ * nd = not dominated (maximisation) & (O > ref all) [& first of duplicates if dedup].
+ * mask (S x n bytes, may be NULL); counts (n ints, may be NULL) += nd.
+ * Replaces prune_inferior_points_multi_objective (qnehvi.py:44) and the per-sample
+ * Pareto filter of _pad_batch_pareto_frontier. */
+int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const double* ref,
+                    int dedup, unsigned char* mask, int* counts);
+
+/* Elementwise objective on a sample tensor: O[j][i][s] = a_j*(Y[j][i][s] + mu[j][i]) + b_j */
+int evr_objective_affine(void* stream, int m, int n, int S, const double* Y, const double* mu,
+                         const double* a, const double* b, double* O);
+/* X[b][e] *= alpha[b] for e < per (per-output variance scaling s_y^2 of covariances) */
+int evr_scale_batched(void* stream, int B, long long per, const double* alpha, double* X);
+/* E[b][r][idx[r]] += val[b] (adds the baseline row selection P to E, nb x n per output) */
+int evr_add_selection(void* stream, int B, int nb, int n, const int* idx, const double* val, double* E);
+
+/* ---- host box decomposition ----------------------------------------------------------
+ * Exact partition of the non-dominated region above ref into disjoint boxes, per MC sample
+ * (FastNondominatedPartitioning, alpha = 0, qnehvi.py:50; Lacour et al. 2017 local upper
+ * bounds).  Host memory.  obj: element (s, i, j) at obj[s*ss + i*si + j*sj]; mask (S x n,
+ * nullable) selects the candidate points (Pareto filter is re-applied on the host). */
+typedef struct evr_cells evr_cells;
+int evr_box_decompose(int S, int n, int m, const double* obj, long long ss, long long si,
+                      long long sj, const unsigned char* mask, const double* ref, int num_threads,
+                      evr_cells** out);
+long long evr_cells_total(const evr_cells* c);
+int evr_cells_copy(const evr_cells* c, double* lo, double* hi, int* off);
+void evr_cells_free(evr_cells* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EVEREST_AMD_H */

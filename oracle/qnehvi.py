@@ -1,0 +1,150 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Reference-structure restatement (torch-CPU float64, autograd-capable) of
+``qNoisyExpectedHypervolumeImprovement`` as BoFire builds it
+(bofire/strategies/predictives/qnehvi.py:23-53: prune_baseline=True, cache_root=True,
+alpha=0, no output constraints) and of qEI (bofire/strategies/predictives/sobo.py:51-90).
+
+It deliberately keeps BoTorch's computation *shape*  so that it doubles as
+the CPU baseline timed by bench.py: the joint posterior over [X_baseline; X] is formed per
+candidate with the K(X_full, X_train)·L^-T root GEMM, samples come from
+``sample_cached_cholesky`` and the HVI is the per-cell scan of ``_compute_qehvi``.
+
+Semantics restated ([upstream] BoTorch >= 0.13):
+  * base samples: scrambled Sobol -> inverse normal CDF (``draw_sobol_normal_samples``),
+    laid out S x n_points x m (Sobol dim index = point*m + output), baseline rows fixed,
+    new rows from a (n_base+q)*m-dim draw of the same seed (``_update_base_samples``).
+  * prune: P(point is Pareto-optimal and better than ref) > 0 over 2048 samples of the
+    joint posterior at X_baseline (``prune_inferior_points_multi_objective``).
+  * cached-Cholesky sampling with ``psd_safe_cholesky(max_tries=6)`` on the new block.
+  * HVI with inclusion–exclusion over q-subsets, mean over samples.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from .gp import GPState, TK, kernel_matrix, psd_safe_cholesky
+from .multiobjective import is_non_dominated, nondominated_cells, pareto_above_ref
+
+
+def draw_sobol_normal_samples(d: int, n: int, seed: int) -> torch.Tensor:
+    """[upstream] botorch.utils.sampling.draw_sobol_normal_samples (inv_transform=True)."""
+    eng = torch.quasirandom.SobolEngine(dimension=d, scramble=True, seed=seed)
+    u = eng.draw(n, dtype=torch.float64)
+    v = 0.5 + (1 - torch.finfo(u.dtype).eps) * (u - 0.5)
+    return torch.erfinv(2 * v - 1) * math.sqrt(2)
+
+
+def base_samples(S: int, n_points: int, m: int, seed: int) -> torch.Tensor:
+    return draw_sobol_normal_samples(n_points * m, S, seed).view(S, n_points, m)
+
+
+@dataclass
+class Objective:
+    """Affine objective g_j(y) = a_j*y_j + b_j (Maximize/Minimize with bounds,
+    bofire/utils/torch_tools.py:389-398)."""
+    a: torch.Tensor
+    b: torch.Tensor
+
+    def __call__(self, y):
+        return y * self.a + self.b
+
+
+def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
+    """Per-output joint posterior at Xn (... x p x d, normalized).  Returns mean (... x p x m)
+    and cov (... x m x p x p), computed the GPyTorch way: R = K(X, Xtr) L^-T."""
+    means, covs = [], []
+    for st in models:
+        Ks = kernel_matrix(Xn, st.X, st.lengthscale, st.kind)
+        Linv = torch.linalg.solve_triangular(st.L, torch.eye(st.L.shape[0], **TK), upper=False)
+        R = Ks @ Linv.T
+        mean = st.constant + Ks @ st.alpha
+        cov = kernel_matrix(Xn, Xn, st.lengthscale, st.kind) - R @ R.transpose(-1, -2)
+        means.append(mean * st.y_std + st.y_mean)
+        covs.append(cov * st.y_std ** 2)
+    return torch.stack(means, -1), torch.stack(covs, -3)
+
+
+def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0):
+    """prune_inferior_points_multi_objective restated.  z_prune: S' x n x m.  Returns the
+    kept row indices (sorted, unique) into Xn."""
+    mean, cov = joint_posterior(models, Xn)                    # n x m, m x n x n
+    L, _ = psd_safe_cholesky(cov)                              # m x n x n
+    Y = mean.unsqueeze(0) + torch.einsum("jik,skj->sij", L, z_prune)
+    obj = objective(Y)
+    pareto = is_non_dominated(obj, deduplicate=False) & (obj > ref).all(-1)
+    probs = pareto.to(torch.float64).mean(0)
+    idx = probs.nonzero().view(-1)
+    max_points = math.ceil(max_frac * Xn.shape[0])
+    if idx.shape[0] > max_points:
+        _, order = torch.sort(probs, stable=True, descending=True)
+        idx = order[:max_points]
+    return idx.unique(), probs
+
+
+class QNEHVI:
+    """Reference-structure qNEHVI.  models: one GPState per output (shared inputs).
+    Xb_n: baseline (already pruned), normalized.  z_base: S x n_b x m; z_new: S x q x m."""
+
+    def __init__(self, models: List[GPState], Xb_n: torch.Tensor, objective: Objective,
+                 ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor):
+        self.models = models
+        self.Xb = Xb_n
+        self.obj = objective
+        self.ref = ref
+        self.z_base = z_base
+        self.z_new = z_new
+        mean_b, cov_b = joint_posterior(models, Xb_n)          # nb x m, m x nb x nb
+        self.L_base, self.base_jitter = psd_safe_cholesky(cov_b)
+        Yb = mean_b.unsqueeze(0) + torch.einsum("jik,skj->sij", self.L_base, z_base)
+        self.base_obj = objective(Yb)                          # S x nb x m
+        self.cells = [nondominated_cells(pareto_above_ref(self.base_obj[s], ref), ref)
+                      for s in range(z_base.shape[0])]
+
+    def samples(self, Xn: torch.Tensor) -> torch.Tensor:
+        """Xn: b x q x d normalized -> samples S x b x q x m (sample_cached_cholesky)."""
+        b, q, _ = Xn.shape
+        nb = self.Xb.shape[0]
+        Xfull = torch.cat([self.Xb.expand(b, nb, self.Xb.shape[-1]), Xn], dim=-2)
+        mean, cov = joint_posterior(self.models, Xfull)         # b x (nb+q) x m, b x m x P x P
+        bottom = cov[..., -q:, :]
+        bl, br = bottom[..., :nb], bottom[..., nb:]
+        bl_chol = torch.linalg.solve_triangular(self.L_base, bl.transpose(-1, -2), upper=False).transpose(-1, -2)
+        br_to_chol = br - bl_chol @ bl_chol.transpose(-1, -2)
+        br_chol, _ = psd_safe_cholesky(br_to_chol, max_tries=6)
+        newL = torch.cat([bl_chol, br_chol], -1)                 # b x m x q x (nb+q)
+        z = torch.cat([self.z_base, self.z_new], dim=1)          # S x (nb+q) x m
+        s = torch.einsum("bjqk,skj->sbqj", newL, z)
+        return mean[..., -q:, :].unsqueeze(0) + s
+
+    def hvi_per_sample(self, obj: torch.Tensor) -> torch.Tensor:
+        """obj: S x b x q x m -> S x b (inclusion–exclusion over q-subsets)."""
+        import itertools
+        S, b, q, m = obj.shape
+        out = torch.zeros(S, b, **TK)
+        for s in range(S):
+            lo, hi = self.cells[s][0], self.cells[s][1]           # C x m
+            for i in range(1, q + 1):
+                for sub in itertools.combinations(range(q), i):
+                    ov = obj[s][:, list(sub), :].min(dim=-2).values            # b x m
+                    ln = (torch.minimum(ov.unsqueeze(-2), hi) - lo).clamp_min(0.0)
+                    out[s] = out[s] + ((-1) ** (i + 1)) * ln.prod(-1).sum(-1)
+        return out
+
+    def forward(self, Xn: torch.Tensor) -> torch.Tensor:
+        return self.hvi_per_sample(self.obj(self.samples(Xn))).mean(0)
+
+
+def qei(models, Xn: torch.Tensor, best_f: float, z: torch.Tensor, a: float = 1.0, bconst: float = 0.0):
+    """qEI restated (plain MC sampling): mean_S max_q (g(f_s) - best_f)_+.  Xn: b x q x d,
+    z: S x q (base samples for the single output)."""
+    st = models[0]
+    mean, cov = joint_posterior([st], Xn)                          # b x q x 1, b x 1 x q x q
+    L, _ = psd_safe_cholesky(cov[..., 0, :, :])
+    f = mean[..., 0].unsqueeze(0) + torch.einsum("bqk,sk->sbq", L, z)
+    g = a * f + bconst
+    return (g - best_f).clamp_min(0.0).max(-1).values.mean(0)

@@ -1,0 +1,112 @@
+"""GPU parity of the dense float64 primitives (C-ABI through everest_amd.ops) against the
+torch-CPU float64 oracle.  Tolerances: 1e-12 relative-to-scale for exact-arithmetic
+restatements (GEMM, kernel assembly), 1e-10 for factorizations/solves."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp as ogp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.as_tensor(a, dtype=torch.float64, device=DEV)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (17, 33, 5), (64, 64, 64), (130, 70, 257), (513, 300, 129)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_f64_mfma(shape, ta, tb):
+    from everest_amd import ops
+
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(3, K, M, generator=g, dtype=torch.float64) if ta else torch.randn(3, M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(3, N, K, generator=g, dtype=torch.float64) if tb else torch.randn(3, K, N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(3, M, N, generator=g, dtype=torch.float64)
+    ref = 1.5 * ((A.transpose(1, 2) if ta else A) @ (B.transpose(1, 2) if tb else B)) - 0.5 * C0
+    C = _t(C0).contiguous()
+    ops.gemm(_t(A), _t(B), ta, tb, alpha=1.5, beta=-0.5, out=C)
+    err = (C.cpu() - ref).abs().max().item()
+    assert err <= 1e-12 * max(1.0, ref.abs().max().item()) * max(1, K) ** 0.5
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches row/col swaps in the MFMA C/D map."""
+    from everest_amd import ops
+
+    B = torch.arange(64 * 48, dtype=torch.float64).reshape(64, 48)
+    C = ops.gemm(_t(torch.eye(64)), _t(B))
+    assert torch.equal(C.cpu(), B)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("n1,n2,d", [(1, 1, 1), (37, 91, 6), (256, 256, 6), (130, 65, 32)])
+def test_kernel_matrix(kind, n1, n2, d):
+    from everest_amd import ops
+
+    rng = np.random.default_rng(n1 + n2 + d + kind)
+    X1 = rng.uniform(-1, 2, (n1, d))
+    X2 = rng.uniform(-1, 2, (n2, d))
+    ls = rng.uniform(0.2, 2.0, (3, d))
+    lo, hi = -1.0 * np.ones(d), 2.0 * np.ones(d)
+    os_ = np.array([1.0, 2.0, 0.5])
+    K = ops.kernel_matrix(_t(X1), _t(X2), _t(ls), kind, shift1=_t(lo), scale1=_t(1 / (hi - lo)), shift2=_t(lo),
+                          scale2=_t(1 / (hi - lo)), outputscale=_t(os_)).cpu()
+    for b in range(3):
+        ref = ogp.kernel_matrix(torch.tensor((X1 - lo) / (hi - lo)), torch.tensor((X2 - lo) / (hi - lo)),
+                                torch.tensor(ls[b]), kind, os_[b])
+        assert torch.allclose(K[b], ref, rtol=1e-12, atol=1e-13)
+
+
+@pytest.mark.parametrize("n", [1, 7, 32, 33, 100, 256, 513])
+def test_cholesky_plain(n):
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(n)
+    A = torch.randn(4, n, n + 3, generator=g, dtype=torch.float64)
+    A = A @ A.transpose(1, 2) + 1e-3 * torch.eye(n, dtype=torch.float64)
+    L, jit, info = ops.cholesky(_t(A))
+    ref = torch.linalg.cholesky(A)
+    assert info.cpu().eq(0).all() and jit.cpu().eq(0).all()
+    assert torch.allclose(L.cpu(), ref, rtol=1e-10, atol=1e-10 * ref.abs().max().item())
+
+
+def test_cholesky_jitter_ladder():
+    """Rank-deficient PSD matrices need jitter; singular-negative ones fail -> NotPSDError."""
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    V = torch.randn(3, 40, 10, generator=g, dtype=torch.float64)
+    A = V @ V.transpose(1, 2)                       # rank 10 < 40
+    A[1] = A[1] + torch.eye(40, dtype=torch.float64)  # p.d.: no jitter
+    L, jit, info = ops.cholesky(_t(A), 1e-8, 3, raise_on_fail=False)
+    Lr, jr = ogp.psd_safe_cholesky(A)
+    assert info.cpu().tolist() == [0, 0, 0]
+    assert jit.cpu()[1].item() == 0.0
+    assert torch.allclose(jit.cpu(), jr)
+    assert torch.allclose(L.cpu(), Lr, atol=1e-8)
+    neg = -torch.eye(5, dtype=torch.float64).unsqueeze(0)
+    with pytest.raises(ops.NotPSDError):
+        ops.cholesky(_t(neg))
+    nan = torch.full((1, 4, 4), float("nan"), dtype=torch.float64)
+    _, _, info = ops.cholesky(_t(nan), raise_on_fail=False)
+    assert info.cpu().item() == 1
+
+
+@pytest.mark.parametrize("n,nrhs", [(1, 1), (50, 3), (64, 64), (200, 130), (513, 70)])
+@pytest.mark.parametrize("trans", [False, True])
+def test_trsm_and_inverse(n, nrhs, trans):
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(n + nrhs)
+    A = torch.randn(2, n, n, generator=g, dtype=torch.float64)
+    L = torch.linalg.cholesky(A @ A.transpose(1, 2) + n * torch.eye(n, dtype=torch.float64))
+    B = torch.randn(2, n, nrhs, generator=g, dtype=torch.float64)
+    X = _t(B).contiguous()
+    ops.trsm(_t(L), X, transpose=trans)
+    ref = torch.linalg.solve_triangular(L.transpose(1, 2) if trans else L, B, upper=trans)
+    assert torch.allclose(X.cpu(), ref, rtol=1e-10, atol=1e-11)
+    Li = ops.tri_inv(_t(L)).cpu()
+    assert torch.allclose(Li, torch.linalg.inv(L), rtol=1e-9, atol=1e-11)
