@@ -1,0 +1,303 @@
+#!/usr/bin/env python
+"""Benchmark of the qNEHVI hot path on MI355X (BASELINE.json metric: QnehviStrategy.ask()
+candidates/sec + GP posterior ms, n=512 d=6 m=5).
+
+Workload (BASELINE.json configs[2]): DTLZ2(dim=6, m=5), X_train ~
+U[0,1]^6 (n=512, seed 0), noise-free Y, reference point 1.1 -> -1.1 in objective space
+(MinimizeObjective), 5 exact RBF GPs fitted once on the device and frozen, qNEHVI built as
+BoFire builds it (prune_baseline with 2048 samples, cached root, S=256 Sobol-normal base
+samples), q=1.  A *step* = one acquisition evaluation pass (forward + analytic backward,
+the unit raw screening and the L-BFGS restarts of ask() are made of) over one batch of
+b=512 Sobol candidates already resident in HBM.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): every rank evaluates its own 512-candidate
+shard (weak scaling); each step ends with the RCCL all-gather of the per-shard acquisition
+values that the Boltzmann initial-condition selection needs.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_TFLOPS = 78.6     # MI355X FP64 vector & matrix (AMD spec; = 1/2 the FP32 vector peak 157.3 TF)
+PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def dtlz2(X: np.ndarray, m: int) -> np.ndarray:
+    k = X.shape[1] - m + 1
+    g = ((X[..., -k:] - 0.5) ** 2).sum(-1)
+    fs = []
+    for i in range(m):
+        idx = m - 1 - i
+        f = (1 + g) * np.cos(X[..., :idx] * math.pi / 2).prod(-1)
+        if i > 0:
+            f = f * np.sin(X[..., idx] * math.pi / 2)
+        fs.append(f)
+    return np.stack(fs, -1)
+
+
+def build_state(n: int, d: int, m: int, S: int, device, prune_samples: int = 2048):
+    from everest_amd.acquisition import QNEHVI
+    from everest_amd.gp import GPBatch, fit_single
+
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(n, d))
+    Y = dtlz2(X, m)
+    lo, hi = np.zeros(d), np.ones(d)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)  # noqa: E731
+    Xn = t(X)
+    ls_prior = (math.sqrt(2) + 0.5 * math.log(d), math.sqrt(3))  # bofire/priors/mapper.py:43-50
+    t0 = time.perf_counter()
+    hypers = [fit_single(Xn, Y[:, j], 0, ls_prior, (-4.0, 1.0)) for j in range(m)]
+    torch.cuda.synchronize()
+    t_fit = time.perf_counter() - t0
+    gp = GPBatch(Xn, t(Y), hypers, 0, t(lo), t(hi))
+    t0 = time.perf_counter()
+    acqf = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=1234,
+                  prune_baseline=True, prune_seed=4321, prune_samples=prune_samples)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    return X, Y, gp, hypers, acqf, t_fit, t_build
+
+
+def candidates(b: int, d: int, seed: int, device):
+    eng = torch.quasirandom.SobolEngine(d, scramble=True, seed=seed)
+    return eng.draw(b, dtype=torch.float64).to(device)
+
+
+class KernelTimer:
+    """HIP events on torch's current stream (the stream every everest_amd op launches on)."""
+
+    def __init__(self):
+        self.ev = {}
+
+    def start(self, name):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return (name, e0)
+
+    def stop(self, tok):
+        name, e0 = tok
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.ev.setdefault(name, []).append((e0, e1))
+
+    def summary(self):
+        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in self.ev.items()}
+
+
+def step(acqf, Xc, timer=None):
+    """One evaluation pass: forward + backward over the candidate batch (instrumented)."""
+    from everest_amd import ops
+
+    st = acqf.state
+    b = Xc.shape[0]
+    gp = acqf.gp
+    T = timer
+    tk = T.start("kernel_matrix") if T else None
+    Kx = gp.cross(Xc)
+    if T: T.stop(tk); tk = T.start("gemm_fwd")
+    R = ops.gemm(acqf.M, Kx)
+    if T: T.stop(tk); tk = T.start("samples")
+    G, L22, flags = ops.qnehvi_samples(st, R, b)
+    if T: T.stop(tk); tk = T.start("hvi_fwd")
+    partial = ops.hvi_forward(st, G, b)
+    if T: T.stop(tk); tk = T.start("mean")
+    acq = ops.mean_over_samples(partial)
+    if T: T.stop(tk); tk = T.start("hvi_bwd")
+    gout = torch.ones(b, dtype=torch.float64, device=Xc.device)
+    dG = ops.hvi_backward(st, G, gout, b)
+    if T: T.stop(tk); tk = T.start("samples_bwd")
+    gR = ops.qnehvi_samples_backward(st, R, L22, dG, b)
+    if T: T.stop(tk); tk = T.start("gemm_bwd")
+    dKx = ops.gemm(acqf.M, gR, transA=True)
+    if T: T.stop(tk); tk = T.start("kernel_grad")
+    dX = ops.kernel_cross_grad(gp.Xn, Xc, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+    if T: T.stop(tk)
+    return acq, dX
+
+
+def gp_posterior_ms(device, reps=20):
+    """Config 2: SingleTaskGP RBF posterior (mean+var), n_train=256, d=6, 1024 test points."""
+    from everest_amd.gp import GPBatch, GPHyper
+
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(256, 6))
+    y = dtlz2(X, 5)[:, :1]
+    h = GPHyper(lengthscale=np.full(6, 0.8), noise=1e-3, constant=0.0, y_mean=float(y.mean()),
+                y_std=float(y.std(ddof=1)))
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)  # noqa: E731
+    gp = GPBatch(t(X), t(y), [h], 0, t(np.zeros(6)), t(np.ones(6)))
+    Xs = torch.quasirandom.SobolEngine(6, scramble=True, seed=1).draw(1024, dtype=torch.float64).to(device)
+    for _ in range(3):
+        gp.posterior(Xs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gp.posterior(Xs)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, n_cand=8, reps=3):
+    """Reference-structure CPU restatement (oracle/, torch-CPU fp64, BoTorch computation
+    shape) timed on the host cores: forward+backward over n_cand candidates at the same
+    state (cells injected from the device build so only the evaluation is timed)."""
+    from oracle import gp as ogp
+    from oracle import qnehvi as oq
+
+    d = X.shape[1]
+    Xn = torch.tensor(X)
+    states = []
+    for j, h in enumerate(hypers):
+        y = torch.tensor(Y[:, j])
+        states.append(ogp.GPState(X=Xn, y=(y - h.y_mean) / h.y_std, lengthscale=torch.tensor(h.lengthscale),
+                                  noise=h.noise, constant=h.constant, y_mean=h.y_mean, y_std=h.y_std))
+    nb = acqf.nb
+    off = acqf.cell_off.cpu().numpy()
+    lo, hi = acqf.cell_lo.cpu(), acqf.cell_hi.cpu()
+    cells = [torch.stack([lo[off[s]:off[s + 1]], hi[off[s]:off[s + 1]]]) for s in range(acqf.S)]
+    zq = acqf.zq.cpu().unsqueeze(1)
+    zb = torch.zeros(acqf.S, nb, acqf.m, dtype=torch.float64)
+    orc = oq.QNEHVI(states, Xn[torch.as_tensor(acqf.base_rows)], oq.Objective(-torch.ones(acqf.m),
+                    torch.zeros(acqf.m, dtype=torch.float64)), torch.full((acqf.m,), -1.1, dtype=torch.float64),
+                    zb, zq, cells=cells)
+    x = Xc_cpu[:n_cand].clone().requires_grad_(True)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        v = orc.forward(x.unsqueeze(1))
+        v.sum().backward()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), n_cand
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--d", type=int, default=6)
+    ap.add_argument("--m", type=int, default=5)
+    ap.add_argument("--S", type=int, default=256)
+    ap.add_argument("--b", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=device)
+
+    X, Y, gp, hypers, acqf, t_fit, t_build = build_state(args.n, args.d, args.m, args.S, device)
+    Xc = candidates(args.b, args.d, seed=2 + rank, device=device)
+    gathered = [torch.empty(args.b, dtype=torch.float64, device=device) for _ in range(world)]
+
+    def one_step(timer=None):
+        acq, dX = step(acqf, Xc, timer)
+        if dist is not None:
+            dist.all_gather(gathered, acq)
+        return acq
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    ms = dt / args.steps * 1e3
+    value = world * args.b * args.steps / dt
+
+    # per-kernel device time (separate instrumented pass, events on the launch stream)
+    timer = KernelTimer()
+    for _ in range(max(5, args.steps // 2)):
+        one_step(timer)
+    torch.cuda.synchronize()
+    ktimes = timer.summary()
+
+    if rank == 0:
+        st = acqf.stats
+        sum_cells = st.total_cells
+        m = args.m
+        b = args.b
+        # dominant kernel and its algorithmic work per launch
+        dom = max(ktimes, key=ktimes.get)
+        work = {
+            "hvi_fwd": ("valu", b * sum_cells * 4 * m, "flop"),
+            "hvi_bwd": ("valu", b * sum_cells * (6 * m + 2), "flop"),
+            "gemm_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, "flop"),
+            "gemm_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, "flop"),
+        }
+        roof = None
+        if dom in work:
+            bound, w, _ = work[dom]
+            ach = w / (ktimes[dom] * 1e-3) / 1e12
+            roof = {"bound": bound, "kernel": dom, "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                    "algorithmic_work_per_launch": w}
+        cpu = None
+        if not args.no_cpu_baseline:
+            torch.set_num_threads(min(16, os.cpu_count() or 1))
+            t_cpu, nc = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
+            cpu = {"value": round(nc / t_cpu, 3), "unit": "candidates/s", "cores": torch.get_num_threads(),
+                   "kind": "port", "sample": f"oracle reference-structure forward+backward over {nc} candidates "
+                   f"(same state, n={args.n}, n_base={acqf.nb}, S={args.S}), median of 3"}
+        out = {
+            "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
+            "value": round(value, 2),
+            "unit": "candidates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (DTLZ2 d=6 m=5 train set, Sobol candidates; GPs fitted on device)",
+            "config": {"workload": "qNEHVI fwd+bwd eval pass, DTLZ2(d=6,m=5) n_train=512 S=256 b=512 q=1",
+                       "n_train": args.n, "d": args.d, "m": m, "mc_samples": args.S, "candidates_per_gpu": b,
+                       "n_base": acqf.nb, "cells_total": sum_cells, "cells_max": st.max_cells,
+                       "parallelism": f"candidate-shard x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "gp_posterior_ms": round(gp_posterior_ms(device), 4),
+            "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},
+            "setup_s": {"gp_fit": round(t_fit, 3), "qnehvi_build": round(t_build, 3)},
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

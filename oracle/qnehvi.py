@@ -91,7 +91,9 @@ class QNEHVI:
     Xb_n: baseline (already pruned), normalized.  z_base: S x n_b x m; z_new: S x q x m."""
 
     def __init__(self, models: List[GPState], Xb_n: torch.Tensor, objective: Objective,
-                 ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor):
+                 ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor, cells=None):
+        """``cells`` (list of 2 x C x m per sample) may be injected to time the forward
+        pass alone (bench.py cpu_baseline); parity tests always build their own."""
         self.models = models
         self.Xb = Xb_n
         self.obj = objective
@@ -102,8 +104,11 @@ class QNEHVI:
         self.L_base, self.base_jitter = psd_safe_cholesky(cov_b)
         Yb = mean_b.unsqueeze(0) + torch.einsum("jik,skj->sij", self.L_base, z_base)
         self.base_obj = objective(Yb)                          # S x nb x m
-        self.cells = [nondominated_cells(pareto_above_ref(self.base_obj[s], ref), ref)
-                      for s in range(z_base.shape[0])]
+        if cells is not None:
+            self.cells = cells
+        else:
+            self.cells = [nondominated_cells(pareto_above_ref(self.base_obj[s], ref), ref)
+                          for s in range(z_base.shape[0])]
 
     def samples(self, Xn: torch.Tensor) -> torch.Tensor:
         """Xn: b x q x d normalized -> samples S x b x q x m (sample_cached_cholesky)."""
