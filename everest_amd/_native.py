@@ -62,7 +62,9 @@ _SIGS = {
                                      c_void_p], c_int),
     "evr_pareto_mask": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "evr_objective_affine": ([c_void_p, c_int, c_int, c_int] + [c_void_p] * 5, c_int),
-    "evr_scale_batched": ([c_void_p, c_int, c_longlong, c_void_p, c_void_p], c_int),
+    "evr_qei": ([c_void_p, c_int, c_int, c_int, c_void_p, c_double, c_double, c_double, c_double, c_void_p,
+                 c_double, c_double, c_double, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_scale_batched":([c_void_p, c_int, c_longlong, c_void_p, c_void_p], c_int),
     "evr_add_selection": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_box_decompose": ([c_int, c_int, c_int, c_void_p, c_longlong, c_longlong, c_longlong, c_void_p,
                            c_void_p, c_int, POINTER(c_void_p)], c_int),

@@ -204,6 +204,7 @@ class QNEHVI:
 
     def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
         """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         acq, (X, R, G, L22, flags) = self.forward(X, return_cache=True)
         self._check_flags(flags)
         b = X.shape[0]
@@ -214,4 +215,47 @@ class QNEHVI:
         dKx = ops.gemm(self.M, gR, transA=True)     # m x n x b
         gp = self.gp
         dX = ops.kernel_cross_grad(gp.Xn, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+        return acq, dX
+
+
+class QEI:
+    """Device qEI (q = 1, one output) — [upstream] qExpectedImprovement as built by
+    ``get_acquisition_function("qEI", ...)`` from SoboStrategy._get_acqfs
+    (bofire/strategies/predictives/sobo.py:51-90): best_f = max over X_train of g(posterior
+    mean), plain MC sampling with S Sobol-normal base samples."""
+
+    def __init__(self, gp: GPBatch, X_train_raw: np.ndarray, obj_a: float, obj_b: float, S: int = 512,
+                 seed: int = 0, z: Optional[torch.Tensor] = None):
+        if gp.B != 1:
+            raise ValueError("QEI takes a single-output model")
+        self.gp = gp
+        self.dev = gp.device
+        self.a, self.b = float(obj_a), float(obj_b)
+        Xt = torch.as_tensor(np.asarray(X_train_raw, dtype=np.float64), device=self.dev)
+        mean, _ = gp.posterior(Xt)
+        self.best_f = float((self.a * mean[0] + self.b).max().item())
+        if z is None:
+            z = draw_sobol_normal_samples(1, S, seed)
+        self.z = z.reshape(-1).to(device=self.dev, dtype=torch.float64).contiguous()
+        h = gp.hypers[0]
+        self._scal = (h.constant, h.y_mean, h.y_std, 1.0)
+
+    def _run(self, X, with_grad):
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        R = ops.gemm(self.gp.M, self.gp.cross(X))[0]          # (n+1) x b
+        acq, gR, flags = ops.qei(R, *self._scal, self.z, self.a, self.b, self.best_f, with_grad)
+        if bool(flags.any().item()):
+            raise ops.NotPSDError("qEI: posterior variance not p.d. after 3 jitter tries")
+        return X, acq, gR
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        return self._run(X, False)[1]
+
+    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        X, acq, gR = self._run(X, True)
+        if gout is not None:
+            gR = gR * gout.unsqueeze(0)
+        gp = self.gp
+        dK = ops.gemm(gp.M, gR.unsqueeze(0), transA=True)      # 1 x n x b
+        dX = ops.kernel_cross_grad(gp.Xn, X, gp.ls, dK, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
         return acq, dX

@@ -246,6 +246,57 @@ __global__ void pareto_kernel(int S, int n, const double* __restrict__ O, const 
   if (counts && nd) atomicAdd(&counts[i], 1);
 }
 
+// -------------------------------------------------------------------------------------
+// qEI (q = 1, one output): plain MC sampling f_s = mu + sigma z_s with psd_safe_cholesky
+// (3 jitter tries) on the 1x1 posterior covariance; acq = mean_s (a f_s + b - best_f)_+.
+// R = [Linv; alpha^T] K_x ((n+1) x b).  Also writes gR = d acq / d R for the backward.
+// [upstream] qExpectedImprovement as built at bofire/strategies/predictives/sobo.py:51-90.
+// -------------------------------------------------------------------------------------
+__global__ void qei_kernel(int n, int b, int S, const double* __restrict__ R, double cc, double ym, double ys,
+                           double kxx, const double* __restrict__ z, double oa, double ob, double best_f,
+                           double* __restrict__ acq, double* __restrict__ gR, int* __restrict__ flags) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  double ss = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double v = R[(size_t)i * b + c];
+    ss = fma(v, v, ss);
+  }
+  const double mu = ym + ys * (cc + R[(size_t)n * b + c]);
+  const double var = ys * ys * (kxx - ss);
+  double sd = nan("");
+  int flag = 1;
+  if (!isnan(var)) {
+    for (int t = 0; t <= 3; ++t) {
+      const double jit = (t == 0) ? 0.0 : 1e-8 * pow(10.0, (double)(t - 1));
+      if (var + jit > 0.0) {
+        sd = sqrt(var + jit);
+        flag = 0;
+        break;
+      }
+    }
+  }
+  double tot = 0.0, dmu = 0.0, dsd = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double imp = oa * (mu + sd * z[s]) + ob - best_f;
+    if (imp > 0.0) {
+      tot += imp;
+      dmu += oa;
+      dsd += oa * z[s];
+    }
+  }
+  acq[c] = tot / S;
+  flags[c] = flag;
+  if (gR) {
+    dmu /= S;
+    dsd /= S;
+    const double dvar = dsd / (2.0 * sd);
+    const double dss = -ys * ys * dvar;
+    for (int i = 0; i < n; ++i) gR[(size_t)i * b + c] = 2.0 * R[(size_t)i * b + c] * dss;
+    gR[(size_t)n * b + c] = ys * dmu;
+  }
+}
+
 __global__ void scale_batched_kernel(long long per, const double* __restrict__ alpha, double* __restrict__ X) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= per) return;
@@ -360,6 +411,16 @@ int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const do
 #define L(MM) pareto_kernel<MM><<<grid, 64, 0, s>>>(S, n, O, ref, dedup, mask, counts)
   EVR_DISPATCH_M(m, L);
 #undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_qei(void* stream, int n, int b, int S, const double* R, double c, double ym, double ys, double kxx,
+            const double* z, double obj_a, double obj_b, double best_f, double* acq, double* gR, int* flags) {
+  EVR_CHECK(n >= 1 && S >= 1, "evr_qei: bad sizes");
+  if (b == 0) return 0;
+  qei_kernel<<<cdiv(b, 256), 256, 0, (hipStream_t)stream>>>(n, b, S, R, c, ym, ys, kxx, z, obj_a, obj_b, best_f,
+                                                            acq, gR, flags);
   EVR_LAUNCH_CHECK();
   return 0;
 }

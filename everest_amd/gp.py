@@ -32,14 +32,50 @@ def sigmoid_np(x):
     return 1.0 / (1.0 + np.exp(-x))
 
 
-def lognormal_logpdf_np(x, loc, scale):
-    lx = np.log(x)
-    return -lx - math.log(scale) - 0.5 * math.log(2 * math.pi) - 0.5 * ((lx - loc) / scale) ** 2
+def _prior(p):
+    """Normalise a prior spec: None, (loc, scale) [LogNormal] or (family, p1, p2)."""
+    if p is None:
+        return None
+    if len(p) == 2:
+        return ("lognormal", float(p[0]), float(p[1]))
+    return (p[0], float(p[1]), float(p[2]))
 
 
-def lognormal_dlogpdf_np(x, loc, scale):
-    lx = np.log(x)
-    return (-1.0 - (lx - loc) / scale ** 2) / x
+def prior_logpdf_np(p, x):
+    """gpytorch LogNormalPrior / GammaPrior / NormalPrior log densities (elementwise)."""
+    fam, a, b = p
+    x = np.asarray(x, dtype=np.float64)
+    if fam == "lognormal":
+        lx = np.log(x)
+        return -lx - math.log(b) - 0.5 * math.log(2 * math.pi) - 0.5 * ((lx - a) / b) ** 2
+    if fam == "gamma":
+        return a * math.log(b) - math.lgamma(a) + (a - 1) * np.log(x) - b * x
+    if fam == "normal":
+        return -0.5 * math.log(2 * math.pi * b * b) - 0.5 * ((x - a) / b) ** 2
+    raise ValueError(fam)
+
+
+def prior_dlogpdf_np(p, x):
+    fam, a, b = p
+    x = np.asarray(x, dtype=np.float64)
+    if fam == "lognormal":
+        return (-1.0 - (np.log(x) - a) / b ** 2) / x
+    if fam == "gamma":
+        return (a - 1) / x - b
+    if fam == "normal":
+        return -(x - a) / (b * b)
+    raise ValueError(fam)
+
+
+def prior_sample_np(p, rng, size):
+    fam, a, b = p
+    if fam == "lognormal":
+        return np.exp(rng.normal(a, b, size))
+    if fam == "gamma":
+        return rng.gamma(a, 1.0 / b, size)
+    if fam == "normal":
+        return np.abs(rng.normal(a, b, size))
+    raise ValueError(fam)
 
 
 def standardize_params(y: np.ndarray) -> Tuple[float, float]:
@@ -125,8 +161,8 @@ class MLLEvaluator:
         self.n, self.d = Xn.shape
         self.kind = kind
         self.y = np.asarray(y_std_space, dtype=np.float64)
-        self.ls_prior = ls_prior
-        self.noise_prior = noise_prior
+        self.ls_prior = _prior(ls_prior)
+        self.noise_prior = _prior(noise_prior)
         self.dev = Xn.device
 
     def __call__(self, x: np.ndarray):
@@ -154,28 +190,41 @@ class MLLEvaluator:
         d_const = sum_a
         d_ls = 0.5 * gls
         if self.ls_prior is not None:
-            ll += float(np.sum(lognormal_logpdf_np(ls, *self.ls_prior)))
-            d_ls = d_ls + lognormal_dlogpdf_np(ls, *self.ls_prior)
+            ll += float(np.sum(prior_logpdf_np(self.ls_prior, ls)))
+            d_ls = d_ls + prior_dlogpdf_np(self.ls_prior, ls)
         if self.noise_prior is not None:
-            ll += float(lognormal_logpdf_np(noise, *self.noise_prior))
-            d_noise += float(lognormal_dlogpdf_np(noise, *self.noise_prior))
+            ll += float(prior_logpdf_np(self.noise_prior, noise))
+            d_noise += float(prior_dlogpdf_np(self.noise_prior, noise))
         d_raw = d_ls * sigmoid_np(raw)
         g = np.concatenate([[d_noise, d_const], d_raw]) / n
         return ll / n, g
 
 
 def fit_single(Xn: torch.Tensor, y_raw: np.ndarray, kind: int, ls_prior, noise_prior=(-4.0, 1.0),
-               max_attempts: int = 10, seed: int = 0, options: Optional[dict] = None) -> GPHyper:
+               max_attempts: int = 10, seed: int = 0, options: Optional[dict] = None,
+               standardize: bool = True) -> GPHyper:
     """fit_gpytorch_mll restated on device kernels: minimise -mll with scipy L-BFGS-B over
-    (noise >= 1e-4, constant, raw lengthscale); on NotPSDError resample the hyperparameters
-    from their priors and retry (max_attempts)."""
+    (noise >= 1e-4, constant, raw lengthscale) starting from noise = prior mode (LogNormal
+    noise prior: exp(loc - scale^2)), constant 0, lengthscale softplus(0) = ln 2; on
+    NotPSDError resample the hyperparameters from their priors and retry (max_attempts=10,
+    bofire/surrogates/single_task_gp.py:71)."""
     from scipy.optimize import minimize
 
-    y_mean, y_std = standardize_params(y_raw)
+    if standardize:
+        y_mean, y_std = standardize_params(y_raw)
+    else:
+        y_mean, y_std = 0.0, 1.0
     y = (y_raw - y_mean) / y_std
     d = Xn.shape[1]
-    ev = MLLEvaluator(Xn, y, kind, ls_prior, noise_prior)
-    noise0 = math.exp(noise_prior[0] - noise_prior[1] ** 2) if noise_prior else 2 * MIN_INFERRED_NOISE_LEVEL
+    lsp, nzp = _prior(ls_prior), _prior(noise_prior)
+    ev = MLLEvaluator(Xn, y, kind, lsp, nzp)
+    if nzp is not None and nzp[0] == "lognormal":
+        noise0 = math.exp(nzp[1] - nzp[2] ** 2)
+    elif nzp is not None and nzp[0] == "gamma" and nzp[1] > 1:
+        noise0 = (nzp[1] - 1) / nzp[2]
+    else:
+        noise0 = 2 * MIN_INFERRED_NOISE_LEVEL
+    noise0 = max(noise0, MIN_INFERRED_NOISE_LEVEL)
     x0 = np.concatenate([[noise0, 0.0], np.zeros(d)])
     bounds = [(MIN_INFERRED_NOISE_LEVEL, None), (None, None)] + [(None, None)] * d
     rng = np.random.default_rng(seed)
@@ -187,9 +236,9 @@ def fit_single(Xn: torch.Tensor, y_raw: np.ndarray, kind: int, ls_prior, noise_p
             xv = res.x
             return GPHyper(lengthscale=softplus_np(xv[2:]), noise=float(xv[0]), constant=float(xv[1]),
                            y_mean=y_mean, y_std=y_std)
-        except ops.NotPSDError as e:  # resample from priors (sample_all_priors)
+        except ops.NotPSDError as e:  # sample_all_priors, then retry
             last_err = e
-            ls = (np.exp(rng.normal(ls_prior[0], ls_prior[1], d)) if ls_prior else np.full(d, math.log(2.0)))
-            nz = max(float(np.exp(rng.normal(*noise_prior))) if noise_prior else 1e-3, MIN_INFERRED_NOISE_LEVEL)
+            ls = prior_sample_np(lsp, rng, d) if lsp else np.full(d, math.log(2.0))
+            nz = max(float(prior_sample_np(nzp, rng, 1)[0]) if nzp else 1e-3, MIN_INFERRED_NOISE_LEVEL)
             x0 = np.concatenate([[nz, 0.0], np.log(np.expm1(ls))])
     raise RuntimeError(f"GP fit failed after {max_attempts} attempts: {last_err}")

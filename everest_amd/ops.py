@@ -283,6 +283,18 @@ def objective_affine(Y: torch.Tensor, mu: Optional[torch.Tensor], a: torch.Tenso
     return O
 
 
+def qei(R: torch.Tensor, c: float, ym: float, ys: float, kxx: float, z: torch.Tensor, a: float, b: float,
+        best_f: float, with_grad: bool):
+    R, z = _dev(R, "R"), _dev(z, "z")
+    n1, nb = R.shape
+    acq = torch.empty(nb, dtype=torch.float64, device=R.device)
+    gR = torch.empty_like(R) if with_grad else None
+    flags = torch.empty(nb, dtype=torch.int32, device=R.device)
+    call("evr_qei", _stream(), n1 - 1, nb, z.numel(), R.data_ptr(), float(c), float(ym), float(ys), float(kxx),
+         z.data_ptr(), float(a), float(b), float(best_f), acq.data_ptr(), _p(gR), flags.data_ptr())
+    return acq, gR, flags
+
+
 def scale_batched(X: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
     """In place X[b] *= alpha[b]."""
     if not X.is_contiguous():

@@ -1,0 +1,276 @@
+"""Acquisition optimisation driving the device acquisition functions — restates the
+[upstream] BoTorch ``optimize_acqf`` path that BoFire calls at
+bofire/strategies/predictives/botorch.py:384-405 (q=1, return_best_only=True):
+
+1. raw samples: scrambled Sobol in the bounds, or hit-and-run on the polytope when linear
+   constraints are present (``sample_q_batches_from_polytope``: burn-in 10^4, thinning 32);
+2. the whole raw batch is evaluated in ONE device launch sequence (the reference walks it
+   in chunks of ``batch_limit``);
+3. ``initialize_q_batch_nonneg`` (eta=1, alpha=1e-4) picks ``num_restarts`` starts;
+4. ``gen_candidates_scipy``: per chunk of ``batch_limit`` restarts, scipy L-BFGS-B (box) or
+   SLSQP (linear constraints) minimises -sum_r acq(x_r) with the analytic device gradient;
+5. candidates clamped to the bounds, re-evaluated, best restart returned.
+
+With ``dist`` (torch.distributed, one process per GPU) the raw batch is sharded over the
+ranks and the per-shard acquisition values are all-gathered (RCCL over xGMI) so that every
+rank runs the identical Boltzmann selection; restart chunks are then distributed
+round-robin and the per-chunk best (value, x) pairs all-gathered.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from scipy.optimize import minimize
+
+LinearConstraint = Tuple[np.ndarray, np.ndarray, float]   # (indices, coefficients, rhs): sum c*x[idx] >= rhs
+
+
+@dataclass
+class OptimizeStats:
+    raw_evals: int = 0
+    opt_evals: int = 0
+    opt_iters: int = 0
+    t_raw: float = 0.0
+    t_opt: float = 0.0
+    chunks: List[dict] = field(default_factory=list)
+
+    @property
+    def candidates_evaluated(self) -> int:
+        return self.raw_evals + self.opt_evals
+
+
+def draw_sobol_samples(bounds: np.ndarray, n: int, seed: int) -> np.ndarray:
+    """[upstream] botorch.utils.sampling.draw_sobol_samples (q=1)."""
+    lo, hi = bounds
+    eng = torch.quasirandom.SobolEngine(len(lo), scramble=True, seed=int(seed))
+    u = eng.draw(n, dtype=torch.float64).numpy()
+    return lo + (hi - lo) * u
+
+
+def _as_Ab(d: int, bounds: np.ndarray, ineq: Sequence[LinearConstraint]):
+    """Polytope A x <= b from bounds and BoTorch-form inequality constraints."""
+    rows, rhs = [], []
+    for j in range(d):
+        e = np.zeros(d)
+        e[j] = 1.0
+        rows.append(e.copy()); rhs.append(bounds[1][j])
+        rows.append(-e); rhs.append(-bounds[0][j])
+    for idx, coef, r in ineq:
+        a = np.zeros(d)
+        a[np.asarray(idx, dtype=int)] = -np.asarray(coef, dtype=np.float64)   # sum c x >= r  ->  -c x <= -r
+        rows.append(a); rhs.append(-r)
+    return np.asarray(rows), np.asarray(rhs)
+
+
+def hit_and_run(bounds: np.ndarray, ineq: Sequence[LinearConstraint], eq: Sequence[LinearConstraint], n: int,
+                seed: int, n_burnin: int = 10000, n_thinning: int = 32) -> np.ndarray:
+    """Hit-and-run sampler on {bounds, linear (in)equalities} ([upstream]
+    HitAndRunPolytopeSampler as used by sample_q_batches_from_polytope)."""
+    from scipy.optimize import linprog
+
+    d = bounds.shape[1]
+    A, b = _as_Ab(d, bounds, ineq)
+    # equality constraints: sample in the null space around a feasible point
+    if eq:
+        C = np.zeros((len(eq), d))
+        ce = np.zeros(len(eq))
+        for k, (idx, coef, r) in enumerate(eq):
+            C[k, np.asarray(idx, dtype=int)] = np.asarray(coef, dtype=np.float64)
+            ce[k] = r
+    else:
+        C, ce = np.zeros((0, d)), np.zeros(0)
+    # interior point: maximise the common slack t s.t. A x + t <= b
+    res = linprog(np.r_[np.zeros(d), -1.0], A_ub=np.c_[A, np.ones(len(b))], b_ub=b,
+                  A_eq=np.c_[C, np.zeros(len(ce))] if len(ce) else None, b_eq=ce if len(ce) else None,
+                  bounds=[(None, None)] * d + [(0, 1)], method="highs")
+    if not res.success or res.x[-1] <= 0:
+        raise ValueError("linear constraints define an empty polytope")
+    x = res.x[:d]
+    if len(ce):
+        _, s, Vt = np.linalg.svd(C)
+        rank = int((s > 1e-12).sum())
+        N = Vt[rank:].T
+    else:
+        N = np.eye(d)
+    rng = np.random.default_rng(seed)
+    out = np.empty((n, d))
+    total = n_burnin + n * n_thinning
+    k = 0
+    for it in range(total):
+        r = N @ rng.standard_normal(N.shape[1])
+        r /= np.linalg.norm(r)
+        Ar = A @ r
+        slack = b - A @ x
+        with np.errstate(divide="ignore"):
+            t = slack / Ar
+        tmax = np.min(t[Ar > 1e-14]) if np.any(Ar > 1e-14) else 0.0
+        tmin = np.max(t[Ar < -1e-14]) if np.any(Ar < -1e-14) else 0.0
+        x = x + rng.uniform(tmin, tmax) * r
+        if it >= n_burnin and (it - n_burnin) % n_thinning == n_thinning - 1:
+            out[k] = x
+            k += 1
+    return out
+
+
+def initialize_q_batch_nonneg(X: np.ndarray, acq: np.ndarray, n: int, gen: torch.Generator, eta: float = 1.0,
+                              alpha: float = 1e-4) -> Tuple[np.ndarray, np.ndarray]:
+    """[upstream] botorch.optim.initializers.initialize_q_batch_nonneg (Boltzmann sampling
+    of starting points proportional to exp(eta * acq / max))."""
+    ns = X.shape[0]
+    if n > ns:
+        raise RuntimeError(f"n ({n}) cannot exceed the number of raw samples ({ns})")
+    if n == ns:
+        return X, acq
+    acq_t = torch.as_tensor(acq)
+    max_val, max_idx = torch.max(acq_t, dim=0)
+    if max_val <= 0:
+        warnings.warn("All acquisition values for raw sampled points are nonpositive, so initial conditions are "
+                      "being selected randomly.")
+        idx = torch.randperm(ns, generator=gen)[:n].numpy()
+        return X[idx], acq[idx]
+    pos = acq_t > 0
+    num_pos = int(pos.sum())
+    if num_pos < n:
+        rem = (~pos).nonzero().view(-1)
+        ri = torch.randperm(rem.shape[0], generator=gen)
+        pos[rem[ri[: n - num_pos]]] = True
+        idx = pos.nonzero().view(-1).numpy()
+        return X[idx], acq[idx]
+    alpha_pos = acq_t >= alpha * max_val
+    while alpha_pos.sum() < n:
+        alpha = 0.1 * alpha
+        alpha_pos = acq_t >= alpha * max_val
+    cand = torch.arange(ns)[alpha_pos]
+    w = torch.exp(eta * (acq_t[alpha_pos] / max_val - 1))
+    idx = cand[torch.multinomial(w, n, generator=gen)]
+    if max_idx not in idx:
+        idx[-1] = max_idx
+    idx = idx.numpy()
+    return X[idx], acq[idx]
+
+
+def _scipy_constraints(ineq, eq, nb: int, d: int):
+    cons = []
+    for kind, group in (("ineq", ineq), ("eq", eq)):
+        for idx, coef, rhs in group:
+            idx = np.asarray(idx, dtype=int)
+            coef = np.asarray(coef, dtype=np.float64)
+            for r in range(nb):
+                cols = r * d + idx
+                jac = np.zeros(nb * d)
+                jac[cols] = coef
+                cons.append({"type": kind, "fun": (lambda x, c=cols, k=coef, v=rhs: float(x[c] @ k - v)),
+                             "jac": (lambda x, j=jac: j)})
+    return cons
+
+
+def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int, options: dict,
+                  gen: torch.Generator, inequality_constraints: Sequence[LinearConstraint] = (),
+                  equality_constraints: Sequence[LinearConstraint] = (), dist=None,
+                  stats: Optional[OptimizeStats] = None):
+    """Returns (best x (d,), best value, stats).  ``acqf`` exposes forward(X) and
+    forward_backward(X) on device tensors of raw (transformed) inputs."""
+    import time
+
+    stats = stats or OptimizeStats()
+    bounds = np.asarray(bounds, dtype=np.float64)
+    d = bounds.shape[1]
+    dev = acqf.dev
+    batch_limit = int(options.get("batch_limit") or num_restarts)
+    maxiter = int(options.get("maxiter", 2000))
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
+
+    # 1. raw samples (seeded from the strategy's torch generator -> identical on every rank)
+    seed = int(torch.randint(10_000_000, (1,), generator=gen).item())
+    t0 = time.perf_counter()
+    if inequality_constraints or equality_constraints:
+        X_raw = hit_and_run(bounds, inequality_constraints, equality_constraints, raw_samples, seed)
+    else:
+        X_raw = draw_sobol_samples(bounds, raw_samples, seed)
+    # 2. evaluate (sharded over ranks, all-gather of the per-shard values)
+    Xr = torch.as_tensor(X_raw, dtype=torch.float64, device=dev)
+    if world > 1:
+        per = math.ceil(raw_samples / world)
+        lo_i, hi_i = rank * per, min(raw_samples, (rank + 1) * per)
+        part = torch.zeros(per, dtype=torch.float64, device=dev)
+        if hi_i > lo_i:
+            part[: hi_i - lo_i] = acqf.forward(Xr[lo_i:hi_i])
+        bufs = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(bufs, part)
+        Y_raw = torch.cat(bufs)[:raw_samples]
+    else:
+        Y_raw = acqf.forward(Xr)
+    Y_raw = Y_raw.cpu().numpy()
+    stats.raw_evals += raw_samples
+    stats.t_raw += time.perf_counter() - t0
+
+    # 3. Boltzmann initial conditions
+    X0, _ = initialize_q_batch_nonneg(X_raw, Y_raw, num_restarts, gen)
+
+    # 4. restarts, chunks of batch_limit, scipy on host with device value+gradient
+    t0 = time.perf_counter()
+    lb = np.tile(bounds[0], batch_limit)
+    ub = np.tile(bounds[1], batch_limit)
+    results = []
+    chunks = [(s, min(num_restarts, s + batch_limit)) for s in range(0, num_restarts, batch_limit)]
+
+    def evaluate(X: np.ndarray, with_grad: bool):
+        """Sharded over ranks: each rank runs its slice of the restarts on its GPU, then the
+        (value[, grad]) slices are all-gathered so that every rank holds identical bytes and
+        the replicated host optimiser takes identical steps."""
+        nb = X.shape[0]
+        if world == 1:
+            Xt = torch.as_tensor(X, dtype=torch.float64, device=dev)
+            if with_grad:
+                a, g = acqf.forward_backward(Xt)
+                return a.cpu().numpy(), g.cpu().numpy()
+            return acqf.forward(Xt).cpu().numpy(), None
+        per = math.ceil(nb / world)
+        i0, i1 = min(nb, rank * per), min(nb, (rank + 1) * per)
+        loc = torch.zeros(per, 1 + d, dtype=torch.float64, device=dev)
+        if i1 > i0:
+            Xt = torch.as_tensor(X[i0:i1], dtype=torch.float64, device=dev)
+            if with_grad:
+                a, g = acqf.forward_backward(Xt)
+                loc[: i1 - i0, 0] = a
+                loc[: i1 - i0, 1:] = g
+            else:
+                loc[: i1 - i0, 0] = acqf.forward(Xt)
+        bufs = [torch.empty_like(loc) for _ in range(world)]
+        dist.all_gather(bufs, loc)
+        full = torch.cat(bufs)[:nb].cpu().numpy()
+        return full[:, 0], (full[:, 1:] if with_grad else None)
+
+    for s0, s1 in chunks:
+        nb = s1 - s0
+        x0 = X0[s0:s1].reshape(-1)
+        counter = {"n": 0}
+
+        def f(x):
+            a, g = evaluate(x.reshape(nb, d), True)
+            counter["n"] += 1
+            return -float(a.sum()), -g.reshape(-1)
+
+        bnds = list(zip(np.tile(bounds[0], nb), np.tile(bounds[1], nb)))
+        cons = _scipy_constraints(inequality_constraints, equality_constraints, nb, d)
+        method = "SLSQP" if cons else "L-BFGS-B"
+        res = minimize(f, x0, jac=True, method=method, bounds=bnds, constraints=cons or (),
+                       options={"maxiter": maxiter})
+        Xc = np.clip(res.x.reshape(nb, d), bounds[0], bounds[1])
+        vals, _ = evaluate(Xc, False)
+        stats.opt_evals += counter["n"] * nb + nb
+        stats.opt_iters += int(getattr(res, "nit", 0))
+        stats.chunks.append({"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
+                             "status": int(res.status)})
+        results.append((vals, Xc))
+    vals = np.concatenate([r[0] for r in results])
+    Xs = np.concatenate([r[1] for r in results])
+    k = int(np.argmax(vals))
+    stats.t_opt += time.perf_counter() - t0
+    return Xs[k], float(vals[k]), stats

@@ -1,0 +1,436 @@
+"""Functional strategies with BoFire's API — ``map(data_model)`` returns an object with
+``tell / ask / predict / calc_acquisition`` (bofire/strategies/{strategy,random}.py,
+bofire/strategies/predictives/{predictive,botorch,qehvi,qnehvi,sobo}.py).
+
+The dense work (GP fit and posterior, qNEHVI / qEI construction and evaluation) runs on the
+MI355X through ``everest_amd.gp`` / ``everest_amd.acquisition``; the orchestration (pandas,
+scipy optimiser, box decomposition threads) runs on the host as in the reference.
+Multi-GPU: pass ``dist=torch.distributed`` (one process per GPU, RCCL) to shard the
+acquisition evaluations of ``ask()`` (everest_amd/optim.py).
+"""
+from __future__ import annotations
+
+import warnings
+from typing import List, Optional, Tuple
+
+import numpy as np
+import pandas as pd
+import torch
+
+from . import data_models as dm
+from .acquisition import QNEHVI, QEI
+from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
+from .optim import OptimizeStats, hit_and_run, optimize_acqf
+from .surrogates import BotorchSurrogates, device
+
+
+# ---------------------------------------------------------------------------------------
+# helpers restated from bofire/utils
+# ---------------------------------------------------------------------------------------
+def get_column_names(outputs) -> Tuple[List[str], List[str]]:
+    """bofire/utils/naming_conventions.py:9-33 (continuous outputs)."""
+    keys = outputs.get_keys(dm.ContinuousOutput)
+    return [f"{k}_pred" for k in keys], [f"{k}_sd" for k in keys]
+
+
+def get_ref_point_mask(domain, output_feature_keys=None) -> np.ndarray:
+    """bofire/utils/multiobjective.py:18-55."""
+    if output_feature_keys is None:
+        output_feature_keys = domain.outputs.get_keys_by_objective(
+            [MaximizeObjective, MinimizeObjective, CloseToTargetObjective])
+    if len(output_feature_keys) < 2:
+        raise ValueError("At least two output features have to be provided.")
+    mask = []
+    for key in output_feature_keys:
+        obj = domain.outputs.get_by_key(key).objective
+        if isinstance(obj, MaximizeObjective):
+            mask.append(1.0)
+        elif isinstance(obj, (MinimizeObjective, CloseToTargetObjective)):
+            mask.append(-1.0)
+        else:
+            raise ValueError("Only `MaximizeObjective` and `MinimizeObjective` supported")
+    return np.array(mask)
+
+
+def multiobjective_values(outputs, Y: np.ndarray) -> np.ndarray:
+    """get_multiobjective_objective (bofire/utils/torch_tools.py:699-727) on a numpy array of
+    the objective outputs (columns in get_keys_by_objective order)."""
+    cols = []
+    feats = outputs.get_by_objective([MaximizeObjective, MinimizeObjective, CloseToTargetObjective]).features
+    for j, f in enumerate(feats):
+        cols.append(np.asarray(f.objective(Y[:, j]), dtype=np.float64))
+    return np.stack(cols, axis=-1)
+
+
+def infer_ref_point(domain, experiments: pd.DataFrame, return_masked: bool = False) -> dict:
+    """bofire/utils/multiobjective.py:133-159."""
+    keys = domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective, CloseToTargetObjective])
+    df = domain.outputs.preprocess_experiments_all_valid_outputs(experiments, output_feature_keys=keys)
+    ref = multiobjective_values(domain.outputs, df[keys].values).min(axis=0)
+    mask = get_ref_point_mask(domain)
+    if return_masked is False:
+        ref = ref / mask
+    return {k: ref[i] for i, k in enumerate(keys)}
+
+
+def get_linear_constraints(domain, constraint_type, unit_scaled: bool = False):
+    """bofire/utils/torch_tools.py:45-102: BoTorch form (indices, coefficients, rhs) meaning
+    sum coefficients * x[indices] >= rhs."""
+    out = []
+    keys = domain.inputs.get_keys(dm.domain.Input)
+    for c in domain.constraints.get(constraint_type).constraints:
+        idx, coef, rhs = [], [], 0.0
+        for i, fk in enumerate(c.features):
+            feat = domain.inputs.get_by_key(fk)
+            if feat.is_fixed():
+                rhs -= feat.fixed_value()[0] * c.coefficients[i]
+            else:
+                idx.append(keys.index(fk))
+                coef.append(c.coefficients[i])
+        out.append((np.asarray(idx), -np.asarray(coef, dtype=np.float64), -(rhs + c.rhs)))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# strategy base classes
+# ---------------------------------------------------------------------------------------
+class Strategy:
+    """bofire/strategies/strategy.py:14-280."""
+
+    def __init__(self, data_model):
+        self.domain = data_model.domain
+        self.seed = data_model.seed or int(np.random.default_rng().integers(1000))
+        self.rng = np.random.default_rng(self.seed)
+        self._experiments: Optional[pd.DataFrame] = None
+        self._candidates: Optional[pd.DataFrame] = None
+
+    @classmethod
+    def from_spec(cls, data_model):
+        return cls(data_model=data_model)
+
+    def _get_seed(self) -> int:
+        return int(self.rng.integers(1, 100000))
+
+    @property
+    def experiments(self) -> Optional[pd.DataFrame]:
+        return self._experiments
+
+    @property
+    def candidates(self) -> Optional[pd.DataFrame]:
+        return self._candidates
+
+    def tell(self, experiments: pd.DataFrame, replace: bool = False) -> None:
+        if len(experiments) == 0:
+            return
+        if replace:
+            self.set_experiments(experiments)
+        else:
+            self.add_experiments(experiments)
+        self._tell()
+
+    def _tell(self) -> None:
+        pass
+
+    def ask(self, candidate_count: Optional[int] = None, add_pending: bool = False,
+            raise_validation_error: bool = True) -> pd.DataFrame:
+        if candidate_count is not None and candidate_count < 1:
+            raise ValueError(f"Candidate_count has to be at least 1 but got {candidate_count}.")
+        if not self.has_sufficient_experiments():
+            raise ValueError("Not enough experiments available to execute the strategy.")
+        candidates = self._ask(candidate_count=candidate_count)
+        self.domain.validate_candidates(candidates=candidates, only_inputs=True,
+                                        raise_validation_error=raise_validation_error)
+        if candidate_count is not None and len(candidates) != candidate_count:
+            warnings.warn(f"Expected {candidate_count} candidates, got {len(candidates)}", UserWarning)
+        if add_pending:
+            self.add_candidates(candidates)
+        return candidates
+
+    def has_sufficient_experiments(self) -> bool:
+        raise NotImplementedError
+
+    def _ask(self, candidate_count=None) -> pd.DataFrame:
+        raise NotImplementedError
+
+    def set_candidates(self, candidates: pd.DataFrame):
+        c = self.domain.inputs.validate_experiments(candidates[self.domain.inputs.get_keys()].copy())
+        self._candidates = c[self.domain.inputs.get_keys()]
+
+    def add_candidates(self, candidates: pd.DataFrame):
+        c = self.domain.inputs.validate_experiments(candidates[self.domain.inputs.get_keys()].copy())
+        c = c[self.domain.inputs.get_keys()]
+        self._candidates = c if self._candidates is None else pd.concat((self._candidates, c), ignore_index=True)
+
+    def reset_candidates(self):
+        self._candidates = None
+
+    @property
+    def num_candidates(self) -> int:
+        return 0 if self._candidates is None else len(self._candidates)
+
+    def set_experiments(self, experiments: pd.DataFrame):
+        self._experiments = self.domain.validate_experiments(experiments)
+
+    def add_experiments(self, experiments: pd.DataFrame):
+        e = self.domain.validate_experiments(experiments)
+        self._experiments = e if self._experiments is None else pd.concat((self._experiments, e), ignore_index=True)
+
+    @property
+    def num_experiments(self) -> int:
+        return 0 if self._experiments is None else len(self._experiments)
+
+
+class RandomStrategy(Strategy):
+    """Uniform sampling in the bounds; polytope (hit-and-run) sampling with linear
+    constraints (bofire/strategies/random.py:70-140)."""
+
+    def has_sufficient_experiments(self) -> bool:
+        return True
+
+    def _ask(self, candidate_count: Optional[int] = None) -> pd.DataFrame:
+        n = candidate_count or 1
+        inputs = self.domain.inputs
+        cont = inputs.get(dm.ContinuousInput)
+        lin = self.domain.constraints.get([dm.LinearInequalityConstraint, dm.LinearEqualityConstraint])
+        if len(lin) == 0:
+            return inputs.sample(n, seed=self._get_seed())
+        keys = cont.get_keys()
+        lo = np.array([f.lower_bound for f in cont.features])
+        hi = np.array([f.upper_bound for f in cont.features])
+        ineq = get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
+        eq = get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
+        X = hit_and_run(np.stack([lo, hi]), ineq, eq, n, seed=self._get_seed(), n_burnin=1000, n_thinning=32)
+        df = pd.DataFrame(X, columns=keys)
+        others = inputs.get(excludes=dm.ContinuousInput)
+        if len(others):
+            df = pd.concat([df, others.sample(n, seed=self._get_seed())], axis=1)
+        return df[inputs.get_keys()]
+
+
+class PredictiveStrategy(Strategy):
+    """bofire/strategies/predictives/predictive.py:20-216."""
+
+    def __init__(self, data_model):
+        super().__init__(data_model)
+        self.is_fitted = False
+
+    def ask(self, candidate_count: Optional[int] = None, add_pending: bool = False,
+            raise_validation_error: bool = True) -> pd.DataFrame:
+        candidates = super().ask(candidate_count=candidate_count, add_pending=add_pending,
+                                 raise_validation_error=raise_validation_error)
+        self.domain.validate_candidates(candidates=candidates, raise_validation_error=raise_validation_error)
+        return candidates
+
+    def tell(self, experiments: pd.DataFrame, replace: bool = False, retrain: bool = True):
+        if len(experiments) == 0:
+            return
+        if replace:
+            self.set_experiments(experiments)
+        else:
+            self.add_experiments(experiments)
+        if retrain and self.has_sufficient_experiments():
+            self.fit()
+            self._tell()
+
+    def predict(self, experiments: pd.DataFrame) -> pd.DataFrame:
+        if self.is_fitted is not True:
+            raise ValueError("Model not yet fitted.")
+        preds, stds = self._predict(experiments)
+        pred_cols, sd_cols = get_column_names(self.domain.outputs)
+        predictions = pd.DataFrame(data=np.hstack((preds, stds)), columns=pred_cols + sd_cols)
+        objectives = self.domain.outputs(predictions, experiments_adapt=self.experiments, predictions=True)
+        predictions = pd.concat((predictions, objectives), axis=1)
+        predictions.index = experiments.index
+        return predictions
+
+    def fit(self):
+        assert self.experiments is not None and len(self.experiments) > 0, "No fitting data available"
+        self.domain.validate_experiments(self.experiments, strict=True)
+        self._fit(self.experiments)
+        self.is_fitted = True
+
+
+class BotorchStrategy(PredictiveStrategy):
+    """bofire/strategies/predictives/botorch.py:58-750 (continuous search spaces)."""
+
+    def __init__(self, data_model, dist=None):
+        super().__init__(data_model)
+        self.num_restarts = data_model.num_restarts
+        self.num_raw_samples = data_model.num_raw_samples
+        self.maxiter = data_model.maxiter
+        self.batch_limit = data_model.batch_limit
+        self.surrogate_specs = data_model.surrogate_specs
+        self.surrogates: Optional[BotorchSurrogates] = None
+        self.model = None
+        self.dist = dist
+        # torch.manual_seed(self.seed) in the reference (botorch.py:86); a private generator here
+        self.gen = torch.Generator().manual_seed(int(self.seed))
+        self.last_ask_stats: Optional[OptimizeStats] = None
+
+    @property
+    def input_preprocessing_specs(self):
+        return {k: (v.value if hasattr(v, "value") else v)
+                for k, v in self.surrogate_specs.input_preprocessing_specs.items()}
+
+    def _get_optimizer_options(self) -> dict:
+        return {"batch_limit": self.batch_limit, "maxiter": self.maxiter}
+
+    def _fit(self, experiments: pd.DataFrame):
+        self.surrogates = BotorchSurrogates(self.surrogate_specs)
+        self.surrogates.fit(experiments)
+        self.model = self.surrogates.compatibilize(self.domain.inputs, self.domain.outputs)
+
+    def _transform(self, df: pd.DataFrame) -> np.ndarray:
+        return self.domain.inputs.transform(df[self.domain.inputs.get_keys()],
+                                            self.input_preprocessing_specs).values.astype(np.float64)
+
+    def _predict(self, experiments: pd.DataFrame):
+        X = torch.as_tensor(self._transform(experiments), dtype=torch.float64, device=self.model.device)
+        mean, var = self.model.posterior(X, observation_noise=True)
+        return mean.T.cpu().numpy(), np.sqrt(var.T.cpu().numpy())
+
+    def has_sufficient_experiments(self) -> bool:
+        if self.experiments is None:
+            return False
+        return len(self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)) > 1
+
+    def get_acqf_input_tensors(self):
+        """bofire/strategies/predictives/botorch.py:696-724."""
+        ex = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        clean = ex.drop_duplicates(subset=self.domain.inputs.get_keys(), keep="first")
+        X_train = self._transform(clean)
+        X_pending = self._transform(self.candidates) if self.candidates is not None else None
+        return X_train, X_pending
+
+    def calc_acquisition(self, candidates: pd.DataFrame, combined: bool = False) -> np.ndarray:
+        acqf = self._get_acqfs(1)[0]
+        if combined:
+            raise NotImplementedError("combined (q>1) acquisition values are out of scope (q = 1 kernels)")
+        X = torch.as_tensor(self._transform(candidates), dtype=torch.float64, device=self.model.device)
+        return acqf.forward(X).cpu().numpy()
+
+    def _bounds(self) -> np.ndarray:
+        lo, hi = self.domain.inputs.get_bounds(specs=self.input_preprocessing_specs)
+        return np.array([lo, hi], dtype=np.float64)
+
+    def _ask(self, candidate_count: Optional[int] = None) -> pd.DataFrame:
+        if candidate_count is None:
+            candidate_count = 1
+        assert candidate_count > 0, "candidate_count has to be larger than zero."
+        if self.experiments is None:
+            raise ValueError("No experiments have been provided yet.")
+        if candidate_count != 1:
+            raise NotImplementedError("q > 1 joint candidate batches are not implemented in the MI355X build "
+                                      "(the device kernels evaluate q = 1)")
+        acqf = self._get_acqfs(candidate_count)[0]
+        ineq = get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
+        eq = get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
+        x, val, stats = optimize_acqf(acqf, self._bounds(), self.num_restarts, self.num_raw_samples,
+                                      self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist)
+        stats.best_value = val
+        self.last_ask_stats = stats
+        return self._postprocess_candidates(x[None, :])
+
+    def _postprocess_candidates(self, X: np.ndarray) -> pd.DataFrame:
+        f2i, f2n = self.domain.inputs._transform_info(self.input_preprocessing_specs)
+        cols = [n for k in self.domain.inputs.get_keys() for n in f2n[k]]
+        df = pd.DataFrame(X, columns=cols)
+        df = self.domain.inputs.inverse_transform(df, self.input_preprocessing_specs)
+        preds = self.predict(df)
+        return pd.concat((df, preds), axis=1)
+
+    def _get_acqfs(self, n):
+        raise NotImplementedError
+
+
+class QnehviStrategy(BotorchStrategy):
+    """bofire/strategies/predictives/qehvi.py + qnehvi.py."""
+
+    def __init__(self, data_model, dist=None, **kwargs):
+        super().__init__(data_model, dist=dist)
+        self.num_sobol_samples = data_model.num_sobol_samples
+        self.ref_point = data_model.ref_point
+        self.ref_point_mask = get_ref_point_mask(self.domain)
+        self.alpha = data_model.alpha
+        self.last_acqf: Optional[QNEHVI] = None
+
+    def get_adjusted_refpoint(self) -> List[float]:
+        """bofire/strategies/predictives/qehvi.py:87-110."""
+        assert self.experiments is not None, "No experiments available."
+        if self.ref_point is None:
+            df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+            ref_point = infer_ref_point(self.domain, experiments=df, return_masked=False)
+        else:
+            ref_point = self.ref_point
+        keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
+                                                          CloseToTargetObjective])
+        return (self.ref_point_mask * np.array([ref_point[k] for k in keys])).tolist()
+
+    def _objective_affine(self):
+        keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
+                                                          CloseToTargetObjective])
+        if keys != self.model.output_keys:
+            raise NotImplementedError("every output must carry a Maximize/Minimize objective in this build")
+        a, b = [], []
+        for k in keys:
+            obj = self.domain.outputs.get_by_key(k).objective
+            if not isinstance(obj, (MaximizeObjective, MinimizeObjective)):
+                raise NotImplementedError(f"objective {type(obj).__name__} has no device kernel (affine only)")
+            aa, bb = obj.affine()
+            a.append(aa)
+            b.append(bb)
+        return np.array(a), np.array(b)
+
+    def _get_acqfs(self, n) -> List[QNEHVI]:
+        """bofire/strategies/predictives/qnehvi.py:23-53."""
+        assert self.experiments is not None, "No experiments available."
+        X_train, X_pending = self.get_acqf_input_tensors()
+        if X_pending is not None:
+            raise NotImplementedError("pending candidates (X_pending) are not yet supported on the device path")
+        if self.alpha != 0.0:
+            raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
+        a, b = self._objective_affine()
+        ref = self.get_adjusted_refpoint()
+        # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed
+        prune_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
+        sampler_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
+        acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=self.num_sobol_samples,
+                      sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed)
+        self.last_acqf = acqf
+        return [acqf]
+
+
+class SoboStrategy(BotorchStrategy):
+    """bofire/strategies/predictives/sobo.py:40-120 — qEI on the device."""
+
+    def __init__(self, data_model, dist=None, **kwargs):
+        super().__init__(data_model, dist=dist)
+        self.acquisition_function = data_model.acquisition_function
+
+    def _get_acqfs(self, n):
+        if not isinstance(self.acquisition_function, dm.qEI):
+            raise NotImplementedError(f"{type(self.acquisition_function).__name__} is out of scope; use qEI()")
+        target = self.domain.outputs.get_by_objective([MaximizeObjective, MinimizeObjective]).features[0]
+        if self.model.output_keys.index(target.key) != 0 or len(self.model.output_keys) != 1:
+            raise NotImplementedError("single-output SOBO only")
+        a, b = target.objective.affine()
+        X_train, X_pending = self.get_acqf_input_tensors()
+        if X_pending is not None:
+            raise NotImplementedError("pending candidates are not yet supported on the device path")
+        seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
+        return [QEI(self.model, X_train, a, b, S=512, seed=seed)]
+
+
+STRATEGY_MAP = {
+    dm.QnehviStrategy: QnehviStrategy,
+    dm.SoboStrategy: SoboStrategy,
+    dm.RandomStrategy: RandomStrategy,
+}
+
+
+def map(data_model, **kwargs):
+    """bofire/strategies/mapper.py:7-14."""
+    cls = STRATEGY_MAP.get(type(data_model))
+    if cls is None:
+        raise NotImplementedError(f"{type(data_model).__name__} is out of scope for the MI355X build")
+    return cls(data_model, **kwargs) if cls is not RandomStrategy else cls(data_model)

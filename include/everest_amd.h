@@ -134,6 +134,15 @@ int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const doub
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);
 
+/* ---- qEI (q = 1, single output) -----------------------------------------------------
+ * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+
+ * with sd from psd_safe_cholesky (3 tries) of the posterior variance; gR (nullable) =
+ * d acq / d R for the analytic backward; flags[c] = 1 if the jitter ladder failed.
+ * Replaces [upstream] qExpectedImprovement (bofire/strategies/predictives/sobo.py:51-90). */
+int evr_qei(void* stream, int n, int b, int S, const double* R, double c, double ym, double ys,
+            double kxx, const double* z, double obj_a, double obj_b, double best_f, double* acq,
+            double* gR, int* flags);
+
 /* ---- Pareto / pruning ---------------------------------------------------------------
  * O: m x n x S (objective samples, layout [j][i][s]).  For every sample s and point i:
  * nd = not dominated (maximisation) & (O > ref all) [& first of duplicates if dedup].

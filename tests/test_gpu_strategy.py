@@ -1,0 +1,133 @@
+"""End-to-end BoFire-API tests on the MI355X: tell -> fit on device -> ask -> candidates,
+mirroring tests/bofire/strategies/test_qehvi.py:133-193 and test_ask.py:85-147 of the
+reference (types, shapes, ref point, constraint satisfaction), plus oracle parity of the
+fitted posterior and of the device GP fit."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import everest_amd.data_models as dm
+from everest_amd import strategies
+from everest_amd.benchmarks import DTLZ2, Detergent
+from oracle import gp as ogp
+
+pytestmark = pytest.mark.gpu
+
+
+def _dtlz2_experiments(n=10, dim=6, m=2, seed=0):
+    bench = DTLZ2(dim=dim, num_objectives=m)
+    rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=seed))
+    X = rnd.ask(n)
+    return bench, bench.f(X, return_complete=True)
+
+
+@pytest.mark.parametrize("use_ref_point", [True, False])
+def test_qnehvi_tell_ask_dtlz2(use_ref_point):
+    bench, exps = _dtlz2_experiments()
+    data_model = dm.QnehviStrategy(domain=bench.domain, ref_point=bench.ref_point if use_ref_point else None,
+                                   seed=42, num_sobol_samples=128, num_raw_samples=256, num_restarts=4)
+    s = strategies.map(data_model)
+    s.tell(exps)
+    assert s.is_fitted
+    ref = s.get_adjusted_refpoint()
+    if use_ref_point:
+        assert np.allclose(ref, [-1.1, -1.1])
+    cand = s.ask(1)
+    assert len(cand) == 1
+    for k in bench.domain.inputs.get_keys():
+        assert 0.0 <= cand[k].iloc[0] <= 1.0
+    for k in bench.domain.outputs.get_keys():
+        for suf in ("_pred", "_sd", "_des"):
+            assert f"{k}{suf}" in cand.columns
+    vals = s.calc_acquisition(pd.concat([cand[bench.domain.inputs.get_keys()], exps.iloc[:3]], ignore_index=True))
+    assert vals.shape == (4,) and (vals >= 0).all()
+    st = s.last_ask_stats
+    assert st.raw_evals == 256 and st.opt_evals > 0
+
+
+def test_predict_matches_oracle_posterior():
+    bench, exps = _dtlz2_experiments(n=30, m=3, seed=3)
+    s = strategies.map(dm.QnehviStrategy(domain=bench.domain, seed=1))
+    s.tell(exps)
+    Xq = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=5)).ask(50)
+    pred = s.predict(Xq)
+    for sur in s.surrogates.surrogates:
+        st = sur.state
+        key = sur.output_key
+        o = ogp.GPState(X=torch.tensor((st["X"] - st["lo"]) / (st["hi"] - st["lo"])),
+                        y=torch.tensor((st["y"] - st["y_mean"]) / st["y_std"]),
+                        lengthscale=torch.tensor(st["lengthscale"]), noise=st["noise"], constant=st["constant"],
+                        y_mean=st["y_mean"], y_std=st["y_std"])
+        Xn = torch.tensor((Xq[bench.domain.inputs.get_keys()].values - st["lo"]) / (st["hi"] - st["lo"]))
+        m, v = ogp.posterior(o, Xn, observation_noise=True)
+        assert np.allclose(pred[f"{key}_pred"].values, m.numpy(), rtol=1e-9, atol=1e-9)
+        assert np.allclose(pred[f"{key}_sd"].values, np.sqrt(v.numpy()), rtol=1e-7, atol=1e-9)
+        assert np.allclose(pred[f"{key}_des"].values, -pred[f"{key}_pred"].values)
+
+
+def test_device_fit_matches_oracle_fit():
+    """fit_gpytorch_mll restated: device L-BFGS-B vs oracle L-BFGS-B (torch autograd) reach the
+    same optimum (same start, same bounds; trajectories may differ by rounding)."""
+    from everest_amd.gp import MLLEvaluator, fit_single
+
+    bench, exps = _dtlz2_experiments(n=40, dim=4, m=2, seed=7)
+    X = exps[bench.domain.inputs.get_keys()].values
+    y = exps["f_0"].values
+    prior = ogp.dim_scaled_lognormal(4)
+    h = fit_single(torch.tensor(X, device="cuda"), y, 0, prior, (-4.0, 1.0))
+    st, res = ogp.fit_gp(torch.tensor(X), torch.tensor(y), ogp.RBF, prior, (-4.0, 1.0))
+    yy = (y - y.mean()) / y.std(ddof=1)
+    ev = MLLEvaluator(torch.tensor(X, device="cuda"), yy, 0, prior, (-4.0, 1.0))
+    x_dev = np.r_[h.noise, h.constant, np.log(np.expm1(h.lengthscale))]
+    x_orc = np.r_[st.noise, st.constant, np.log(np.expm1(st.lengthscale.numpy()))]
+    v_dev, _ = ev(x_dev)
+    v_orc, _ = ev(x_orc)
+    assert abs(v_dev - v_orc) <= 1e-6 * max(1.0, abs(v_orc))
+    assert np.allclose(h.lengthscale, st.lengthscale.numpy(), rtol=2e-2)
+
+
+def test_detergent_readme_loop():
+    """README.md:82-104 loop (config 1): 2 initial random points + 4 ask/tell rounds with the
+    two linear inequality constraints (SLSQP restarts on hit-and-run raw samples)."""
+    bench = Detergent()
+    rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=0))
+    exps = bench.f(rnd.ask(2), return_complete=True)
+    s = strategies.map(dm.QnehviStrategy(domain=bench.domain, seed=7, num_sobol_samples=64,
+                                         num_raw_samples=128, num_restarts=4))
+    s.tell(exps)
+    for _ in range(4):
+        c = s.ask(candidate_count=1)
+        assert bench.domain.constraints.is_fulfilled(c, tol=1e-5).all()
+        y = bench.f(c[bench.domain.inputs.get_keys()], return_complete=True)
+        s.tell(y)
+    assert s.num_experiments == 6
+
+
+def test_sobo_qei_matern_parity():
+    from everest_amd.acquisition import QEI
+    from oracle import qnehvi as oq
+
+    bench, exps = _dtlz2_experiments(n=25, dim=4, m=2, seed=11)
+    dom = dm.Domain(inputs=bench.domain.inputs,
+                    outputs=dm.Outputs(features=[dm.ContinuousOutput(key="f_0",
+                                                                      objective=dm.MinimizeObjective(w=1.0))]))
+    spec = dm.SingleTaskGPSurrogate(inputs=dom.inputs, outputs=dom.outputs, kernel=dm.MaternKernel(nu=2.5))
+    s = strategies.map(dm.SoboStrategy(domain=dom, acquisition_function=dm.qEI(), seed=3,
+                                       surrogate_specs=dm.BotorchSurrogates(surrogates=[spec]),
+                                       num_raw_samples=64, num_restarts=2))
+    s.tell(exps[dom.inputs.get_keys() + ["f_0", "valid_f_0"]])
+    cand = s.ask(1)
+    assert len(cand) == 1
+    acqf = s._get_acqfs(1)[0]
+    st = s.surrogates.surrogates[0].state
+    o = ogp.GPState(X=torch.tensor(st["X"]), y=torch.tensor((st["y"] - st["y_mean"]) / st["y_std"]),
+                    lengthscale=torch.tensor(st["lengthscale"]), noise=st["noise"], constant=st["constant"],
+                    y_mean=st["y_mean"], y_std=st["y_std"], kind=ogp.MATERN25)
+    Xc = np.random.default_rng(0).uniform(size=(20, 4))
+    x = torch.tensor(Xc, requires_grad=True)
+    ref = oq.qei([o], x.unsqueeze(1), acqf.best_f, acqf.z.cpu().unsqueeze(-1), a=-1.0, bconst=0.0)
+    ref.sum().backward()
+    acq, dX = acqf.forward_backward(torch.tensor(Xc, device="cuda"))
+    assert torch.allclose(acq.cpu(), ref.detach(), rtol=1e-7, atol=1e-10)
+    assert torch.allclose(dX.cpu(), x.grad, rtol=1e-6, atol=1e-9)
