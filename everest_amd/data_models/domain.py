@@ -216,10 +216,15 @@ class CategoricalInput(Input):
                          data=np.random.default_rng(seed=seed).choice(self.get_allowed_categories(), n))
 
     def get_bounds(self, transform_type=None, values=None, reference_value=None):
-        if transform_type != "ONE_HOT":
+        """bofire/data_models/features/categorical.py:312-345 (ONE_HOT): optimisation bounds
+        close forbidden categories; with data (model fitting) every column is [0, 1]."""
+        if getattr(transform_type, "value", transform_type) != "ONE_HOT":
             raise ValueError(f"categorical `{self.key}` needs a ONE_HOT transform in this build")
         lower = [0.0] * len(self.categories)
-        upper = [1.0 if a else 0.0 for a in self.allowed]
+        if values is None:
+            upper = [1.0 if a else 0.0 for a in self.allowed]
+        else:
+            upper = [1.0] * len(self.categories)
         return lower, upper
 
     def validate_candidental(self, values: pd.Series) -> pd.Series:

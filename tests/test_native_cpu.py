@@ -1,0 +1,78 @@
+"""CPU: the C-ABI library loads, exports every symbol include/everest_amd.h declares, its
+host-side box decomposition matches the oracle, errors surface as messages, and the device
+ops refuse CPU tensors (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "everest_amd.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|long long|void|const char\*)\s+(evr_\w+)\s*\(", hdr, re.M)))
+
+
+def test_library_exports_header_symbols():
+    from everest_amd import _native
+
+    lib = _native.load()
+    syms = _declared_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) <= set(_native.EXPORTED_SYMBOLS) | {"evr_cells_free"}
+    assert lib.evr_version() == 1
+
+
+def test_error_path_message():
+    from everest_amd import _native
+
+    lib = _native.load()
+    out = ctypes.c_void_p()
+    st = lib.evr_box_decompose(0, 1, 1, None, 0, 0, 0, None, None, 1, ctypes.byref(out))
+    assert st != 0 and b"bad arguments" in lib.evr_last_error()
+
+
+@pytest.mark.parametrize("m,n,S", [(2, 15, 4), (3, 25, 6), (5, 30, 3)])
+def test_host_box_decomposition_matches_oracle(m, n, S):
+    from everest_amd import ops
+    from oracle.multiobjective import hvi_from_cells, nondominated_cells, pareto_above_ref
+
+    rng = np.random.default_rng(m * 100 + n)
+    obj = -rng.uniform(size=(S, n, m))
+    obj[:, 3] = obj[:, 2]                      # exact duplicates are deduplicated
+    ref = -1.1 * np.ones(m)
+    lo, hi, off = ops.box_decompose(obj, ref, None, 3, layout="sij")
+    for s in range(S):
+        c = nondominated_cells(pareto_above_ref(torch.tensor(obj[s]), torch.tensor(ref)), torch.tensor(ref))
+        assert off[s + 1] - off[s] == c.shape[1]
+        y = torch.tensor(-rng.uniform(size=(40, m)) * 0.95)
+        mine = torch.stack([torch.tensor(lo[off[s]:off[s + 1]]), torch.tensor(hi[off[s]:off[s + 1]])])
+        assert torch.allclose(hvi_from_cells(y, c), hvi_from_cells(y, mine), atol=1e-14, rtol=0)
+    # layout 'jis' gives identical cells
+    lo2, hi2, off2 = ops.box_decompose(np.ascontiguousarray(obj.transpose(2, 1, 0)), ref, None, 2, layout="jis")
+    assert np.array_equal(off, off2) and np.array_equal(lo, lo2) and np.array_equal(hi, hi2)
+
+
+def test_box_decomposition_empty_front_single_cell():
+    from everest_amd import ops
+
+    obj = -2.0 * np.ones((2, 3, 3))            # every point worse than the reference
+    lo, hi, off = ops.box_decompose(obj, -1.1 * np.ones(3), None, 1, layout="sij")
+    assert list(off) == [0, 1, 2]
+    assert np.allclose(lo, -1.1) and np.isinf(hi).all()
+
+
+def test_device_ops_refuse_cpu_tensors():
+    from everest_amd import ops
+
+    X = torch.zeros(4, 2, dtype=torch.float64)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.kernel_matrix(X, X, torch.ones(1, 2, dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.cholesky(torch.eye(3, dtype=torch.float64))

@@ -1,0 +1,109 @@
+"""CPU: pin the oracle before trusting it — cross-checks against independent mathematics
+(SURVEY.md §7 step 1): exact hypervolume, scipy Cholesky posterior, finite differences,
+torch autograd, and the psd_safe_cholesky ladder."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp as ogp
+from oracle import multiobjective as omo
+from oracle import qnehvi as oq
+from tests.helpers import make_problem, oracle_states
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_box_cells_match_exact_hypervolume(seed):
+    rng = np.random.default_rng(seed)
+    m = int(rng.integers(2, 6))
+    n = int(rng.integers(0, 9))
+    Y = torch.tensor(rng.uniform(0, 1, (n, m)))
+    ref = torch.tensor(rng.uniform(-0.2, 0.3, m))
+    P = omo.pareto_above_ref(Y, ref) if n else torch.zeros(0, m, dtype=torch.float64)
+    cells = omo.nondominated_cells(P, ref)
+    for _ in range(6):
+        y = rng.uniform(-0.1, 1.2, m)
+        h_cells = omo.hvi_from_cells(torch.tensor(y), cells).item()
+        Pn = P.numpy()
+        h_ie = omo.hv_inclusion_exclusion(np.vstack([Pn, y[None]]), ref.numpy()) - (
+            omo.hv_inclusion_exclusion(Pn, ref.numpy()) if len(Pn) else 0.0)
+        h_sl = omo.hv_slicing(np.vstack([Pn, y[None]]), ref.numpy()) - omo.hv_slicing(Pn, ref.numpy())
+        assert abs(h_cells - h_ie) < 1e-12 and abs(h_cells - h_sl) < 1e-12
+
+
+def test_is_non_dominated_dedup():
+    Y = torch.tensor([[1.0, 2.0], [1.0, 2.0], [0.5, 3.0], [0.4, 1.0]], dtype=torch.float64)
+    assert omo.is_non_dominated(Y).tolist() == [True, False, True, False]
+    assert omo.is_non_dominated(Y, deduplicate=False).tolist() == [True, True, True, False]
+
+
+def test_posterior_vs_scipy_and_mll_grad_fd():
+    X, Y, lo, hi, hyp = make_problem(n=30, d=3, m=1, seed=2)
+    st = oracle_states(X, Y, lo, hi, hyp)[0]
+    Xs = torch.rand(20, 3, dtype=torch.float64)
+    m1, v1 = ogp.posterior(st, Xs, observation_noise=True)
+    m2, v2 = ogp.posterior_scipy(st, Xs, observation_noise=True)
+    assert np.allclose(m1.numpy(), m2, rtol=1e-10) and np.allclose(v1.numpy(), v2, rtol=1e-8)
+    prior = ogp.dim_scaled_lognormal(3)
+    x0 = torch.tensor([2e-3, 0.1, -0.2, 0.3, 0.0], requires_grad=True)
+    v = ogp.mll_value(st.X, st.y, x0[2:], x0[0], x0[1], ogp.RBF, prior)
+    v.backward()
+    for k in range(5):
+        e = torch.zeros(5, dtype=torch.float64)
+        e[k] = 1e-6
+        fp = ogp.mll_value(st.X, st.y, (x0 + e)[2:], (x0 + e)[0], (x0 + e)[1], ogp.RBF, prior).item()
+        fm = ogp.mll_value(st.X, st.y, (x0 - e)[2:], (x0 - e)[0], (x0 - e)[1], ogp.RBF, prior).item()
+        assert abs((fp - fm) / 2e-6 - x0.grad[k].item()) < 1e-5 * max(1.0, abs(x0.grad[k].item()))
+
+
+def test_psd_safe_cholesky_ladder():
+    V = torch.randn(20, 4, dtype=torch.float64, generator=torch.Generator().manual_seed(0))
+    A = V @ V.T                                            # rank 4
+    L, jit = ogp.psd_safe_cholesky(A)
+    assert jit.item() in (1e-8, 1e-7, 1e-6)
+    with pytest.raises(ogp.NotPSDError):
+        ogp.psd_safe_cholesky(-torch.eye(3, dtype=torch.float64))
+
+
+def test_sobol_normal_samples_pinned():
+    """The Sobol-normal base samples that both sides consume (torch SobolEngine, scrambled)."""
+    z = oq.draw_sobol_normal_samples(6, 4, seed=123)
+    z2 = oq.draw_sobol_normal_samples(6, 4, seed=123)
+    assert torch.equal(z, z2) and z.shape == (4, 6)
+    assert abs(z.mean().item()) < 1.5
+    from everest_amd.acquisition import draw_sobol_normal_samples as prod_draw
+    assert torch.equal(prod_draw(6, 4, 123), z)
+
+
+def test_qnehvi_oracle_hvi_equals_hv_difference():
+    """qNEHVI for one sample equals HV(P_s U {y_s}) - HV(P_s) computed by slicing."""
+    X, Y, lo, hi, hyp = make_problem(n=12, d=3, m=3, seed=4)
+    st = oracle_states(X, Y, lo, hi, hyp)
+    obj = oq.Objective(-torch.ones(3, dtype=torch.float64), torch.zeros(3, dtype=torch.float64))
+    ref = torch.full((3,), -1.1, dtype=torch.float64)
+    Xn = torch.tensor((X - lo) / (hi - lo))
+    zb = oq.base_samples(4, 12, 3, 1)
+    zn = oq.base_samples(4, 13, 3, 1)
+    q = oq.QNEHVI(st, Xn, obj, ref, zb, zn[:, 12:13, :])
+    xc = torch.rand(3, 1, 3, dtype=torch.float64)
+    g = q.obj(q.samples(xc))
+    per = q.hvi_per_sample(g)
+    for s in range(4):
+        P = omo.pareto_above_ref(q.base_obj[s], ref).numpy()
+        for c in range(3):
+            y = g[s, c, 0].numpy()
+            ex = omo.hv_slicing(np.vstack([P, y[None]]), ref.numpy()) - omo.hv_slicing(P, ref.numpy())
+            assert abs(per[s, c].item() - ex) < 1e-12
+
+
+def test_prune_keeps_only_possible_pareto_points():
+    X, Y, lo, hi, hyp = make_problem(n=30, d=3, m=2, seed=5)
+    st = oracle_states(X, Y, lo, hi, hyp)
+    obj = oq.Objective(-torch.ones(2, dtype=torch.float64), torch.zeros(2, dtype=torch.float64))
+    idx, probs = oq.prune_baseline(st, torch.tensor((X - lo) / (hi - lo)), obj,
+                                   torch.full((2,), -1.1, dtype=torch.float64), oq.base_samples(256, 30, 2, 3))
+    assert set(idx.tolist()) == set(np.nonzero(probs.numpy())[0].tolist())
+    assert 0 < len(idx) < 30
