@@ -113,9 +113,7 @@ def step(acqf, Xc, timer=None):
     if T: T.stop(tk); tk = T.start("samples")
     G, L22, flags = ops.qnehvi_samples(st, R, b)
     if T: T.stop(tk); tk = T.start("hvi_fwd")
-    partial = ops.hvi_forward(st, G, b)
-    if T: T.stop(tk); tk = T.start("mean")
-    acq = ops.mean_over_samples(partial)
+    acq = ops.hvi_forward(st, G, b)
     if T: T.stop(tk); tk = T.start("hvi_bwd")
     gout = torch.ones(b, dtype=torch.float64, device=Xc.device)
     dG = ops.hvi_backward(st, G, gout, b)

@@ -30,7 +30,7 @@ class EvrQnehviState(ctypes.Structure):
         ("n", c_int), ("nb", c_int), ("S", c_int), ("m", c_int),
         ("c", c_void_p), ("ym", c_void_p), ("ys", c_void_p), ("kxx", c_void_p),
         ("zq", c_void_p), ("obj_a", c_void_p), ("obj_b", c_void_p),
-        ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p),
+        ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p), ("max_cells", c_int),
     ]
 
 
@@ -48,16 +48,20 @@ _SIGS = {
                       c_void_p, c_int, c_longlong, c_double, c_void_p, c_int, c_longlong, c_int], c_int),
     "evr_cholesky": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong,
                       c_double, c_int, c_void_p, c_void_p], c_int),
-    "evr_trsm_lower": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_longlong, c_int, c_void_p, c_int,
+    "evr_cholesky_inverse": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong,
+                              c_void_p, c_int, c_longlong, c_double, c_int, c_void_p, c_void_p], c_int),
+    "evr_trsm_lower":([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_longlong, c_int, c_void_p, c_int,
                         c_longlong], c_int),
     "evr_tri_inv_lower": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong],
                           c_int),
     "evr_gp_posterior_finalize": ([c_void_p, c_int, c_int, c_int] + [c_void_p] * 8, c_int),
     "evr_qnehvi_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
                            c_int),
-    "evr_hvi_forward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p], c_int),
+    "evr_hvi_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int], c_longlong),
+    "evr_hvi_forward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_mean_over_samples": ([c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
-    "evr_hvi_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_hvi_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+                         c_int),
     "evr_qnehvi_samples_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p], c_int),
     "evr_pareto_mask": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),

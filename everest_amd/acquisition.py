@@ -98,6 +98,9 @@ class QNEHVI:
         except KeyError as e:
             raise ValueError("qNEHVI: every baseline point must be a training point of the models") from e
 
+        import time as _time
+        tm = {}
+        t0 = _time.perf_counter()
         # ---- joint posterior at the training inputs (shared by prune and baseline) --------
         K = gp.kernel_train(noise=False)                                  # m x n x n
         mu_t = ops.gemm(K, gp.alpha.unsqueeze(-1))[..., 0]                 # K alpha
@@ -121,6 +124,7 @@ class QNEHVI:
             Op = ops.objective_affine(Yp, mu_c, self.obj_a, self.obj_b)
             _, counts = ops.pareto_mask(Op, self.ref, dedup=False, want_mask=False, want_counts=True)
             probs = counts.cpu().numpy().astype(np.float64) / Zp.shape[2]
+            tm["prune"] = _time.perf_counter() - t0
             keep = np.nonzero(probs)[0]
             max_points = math.ceil(max_frac * nc)
             if keep.shape[0] > max_points:
@@ -149,8 +153,12 @@ class QNEHVI:
             Yb = ops.gemm(self.L_base, Zb)
             Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
             mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
-            lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),
+            Ob_h, mask_h = Ob.cpu().numpy(), mask.cpu().numpy()
+            tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
+            t1 = _time.perf_counter()
+            lo, hi, off = ops.box_decompose(Ob_h, self.ref.cpu().numpy(), mask_h,
                                             num_threads or _host_threads(), layout="jis")
+            tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
             lo = np.tile(self.ref.cpu().numpy(), (S_, 1))
             hi = np.full((S_, m), np.inf)
@@ -180,8 +188,11 @@ class QNEHVI:
         M[:, Rr - 1].copy_(gp.alpha)
         self.M = M
         self.state = ops.make_state(n, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
-                                    self.cell_lo, self.cell_hi, self.cell_off)
+                                    self.cell_lo, self.cell_hi, self.cell_off, self.stats.max_cells)
         self._keep = (self.zq, self.cell_lo, self.cell_hi, self.cell_off, self.obj_a, self.obj_b)
+        torch.cuda.synchronize(dev)
+        tm["total"] = _time.perf_counter() - t0
+        self.timings = tm
 
     # ------------------------------------------------------------------------------------
     def _check_flags(self, flags):
@@ -195,8 +206,7 @@ class QNEHVI:
         Kx = self.gp.cross(X)                       # m x n x b
         R = ops.gemm(self.M, Kx)                    # m x Rr x b
         G, L22, flags = ops.qnehvi_samples(self.state, R, b)
-        partial = ops.hvi_forward(self.state, G, b)
-        acq = ops.mean_over_samples(partial)
+        acq = ops.hvi_forward(self.state, G, b)
         if return_cache:
             return acq, (X, R, G, L22, flags)
         self._check_flags(flags)

@@ -137,10 +137,9 @@ void decompose_one(int n, int m, const double* obj, long long si, long long sj, 
     update_lub(L, z.data(), A, nU, nZ);
   }
   const size_t K = L.K();
-  lo_out.clear();
-  hi_out.clear();
-  lo_out.reserve(K * m);
-  hi_out.reserve(K * m);
+  std::vector<double> lo_tmp, hi_tmp;
+  lo_tmp.reserve(K * m);
+  hi_tmp.reserve(K * m);
   std::vector<double> lw(m), up(m);
   for (size_t u = 0; u < K; ++u) {
     const double* uu = &L.U[u * m];
@@ -154,8 +153,26 @@ void decompose_one(int n, int m, const double* obj, long long si, long long sj, 
       ok &= up[j] > lw[j];
     }
     if (!ok) continue;
-    lo_out.insert(lo_out.end(), lw.begin(), lw.end());
-    hi_out.insert(hi_out.end(), up.begin(), up.end());
+    lo_tmp.insert(lo_tmp.end(), lw.begin(), lw.end());
+    hi_tmp.insert(hi_tmp.end(), up.begin(), up.end());
+  }
+  // Cells sorted by their first lower bound (ties: remaining coordinates) so that a device
+  // thread's neighbouring cells share a tight lower envelope (tile skip test in hvi.hip).
+  const size_t C = lo_tmp.size() / m;
+  std::vector<size_t> order(C);
+  for (size_t i = 0; i < C; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    for (int j = 0; j < m; ++j) {
+      const double x = lo_tmp[a * m + j], y = lo_tmp[b * m + j];
+      if (x != y) return x < y;
+    }
+    return a < b;
+  });
+  lo_out.resize(C * m);
+  hi_out.resize(C * m);
+  for (size_t i = 0; i < C; ++i) {
+    std::copy(&lo_tmp[order[i] * m], &lo_tmp[order[i] * m] + m, &lo_out[i * m]);
+    std::copy(&hi_tmp[order[i] * m], &hi_tmp[order[i] * m] + m, &hi_out[i * m]);
   }
 }
 

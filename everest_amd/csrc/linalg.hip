@@ -1,10 +1,14 @@
 // Dense float64 linear algebra for the GP hot path on gfx950:
 //   * batched GEMM on the f64 matrix cores (v_mfma_f64_16x16x4_f64),
-//   * batched Cholesky with the psd_safe_cholesky jitter ladder (one workgroup per
-//     matrix, right-looking, NB=32 LDS diagonal block),
+//   * batched blocked Cholesky (NB = 64, right-looking: LDS diagonal-block kernel + MFMA
+//     panel and lower-triangular trailing-update GEMMs) with the psd_safe_cholesky jitter
+//     ladder, optionally fused with the blocked triangular inverse L^-1,
 //   * batched triangular solve (L^-1 B / L^-T B) blocked by 64 rows through LDS.
 // Replaces the [upstream] torch/LAPACK calls behind GPyTorch's Cholesky / solves
 // (Appendix A.4).
+#include <cmath>
+#include <vector>
+
 #include "common.hpp"
 #include "../../include/everest_amd.h"
 
@@ -25,11 +29,14 @@ template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, double alpha,
                                                        const double* __restrict__ A, int lda, long long sA,
                                                        const double* __restrict__ B, int ldb, long long sB,
-                                                       double beta, double* __restrict__ C, int ldc, long long sC) {
+                                                       double beta, double* __restrict__ C, int ldc, long long sC,
+                                                       int lower_only, const int* __restrict__ skip) {
+  if (skip && skip[blockIdx.z]) return;  // batch member already failed (Cholesky ladder)
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  if (lower_only && n0 > m0 + GT - 1) return;  // tile strictly above the diagonal
   A += blockIdx.z * sA;
   B += blockIdx.z * sB;
   C += blockIdx.z * sC;
-  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
   __shared__ double As[GK][GT + GPAD];
   __shared__ double Bs[GK][GT + GPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, doub
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm + mi * 16 + rq + 4 * r;
       const int cc = n0 + wn + ni * 16 + col;
-      if (row < M && cc < N) {
+      if (row < M && cc < N && (!lower_only || cc <= row)) {
         double* p = C + (size_t)row * ldc + cc;
         *p = alpha * acc[r] + (beta == 0.0 ? 0.0 : beta * (*p));
       }
@@ -81,141 +88,6 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, doub
   store(acc01, 0, 1);
   store(acc10, 1, 0);
   store(acc11, 1, 1);
-}
-
-// ---------------------------------------------------------------------------------------
-// Cholesky with psd_safe_cholesky semantics: try plain; on a non-positive (or NaN) pivot
-// restart from A with total diagonal jitter jitter0 * 10^(t-1), t = 1..max_tries.
-// ---------------------------------------------------------------------------------------
-constexpr int CNB = 32;
-constexpr int CT = 64;  // trailing-update tile
-
-__global__ __launch_bounds__(1024) void chol_kernel(int n, const double* __restrict__ A, long long sA, int lda,
-                                                    double* __restrict__ Lout, long long sL, int ldl, double jitter0,
-                                                    int max_tries, double* __restrict__ jitter_used,
-                                                    int* __restrict__ info) {
-  const int b = blockIdx.x;
-  A += b * sA;
-  double* L = Lout + b * sL;
-  __shared__ double D[CNB][CNB + 1];
-  __shared__ double Pi[CT][CNB + 1];
-  __shared__ double Pj[CT][CNB + 1];
-  __shared__ int fail;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  double jit = 0.0;
-  for (int t = 0; t <= max_tries; ++t) {
-    jit = (t == 0) ? 0.0 : jitter0 * pow(10.0, (double)(t - 1));
-    for (long long e = tid; e < (long long)n * n; e += nt) {
-      const int i = (int)(e / n), j = (int)(e % n);
-      double v = (j <= i) ? A[(size_t)i * lda + j] : 0.0;
-      if (i == j) v += jit;
-      L[(size_t)i * ldl + j] = v;
-    }
-    if (tid == 0) fail = 0;
-    __syncthreads();
-    for (int k0 = 0; k0 < n; k0 += CNB) {
-      const int nb = min(CNB, n - k0);
-      // (1) diagonal block: unnormalised right-looking elimination, one barrier per column
-      for (int e = tid; e < nb * nb; e += nt) {
-        const int i = e / nb, j = e % nb;
-        D[i][j] = (j <= i) ? L[(size_t)(k0 + i) * ldl + k0 + j] : 0.0;
-      }
-      __syncthreads();
-      for (int j = 0; j < nb; ++j) {
-        const double p = D[j][j];
-        if (!(p > 0.0)) break;  // uniform across the workgroup
-        const double ip = 1.0 / p;
-        const int rem = nb - j - 1;
-        for (int e = tid; e < rem * rem; e += nt) {
-          const int i = j + 1 + e / rem, c = j + 1 + e % rem;
-          if (c <= i) D[i][c] -= D[i][j] * D[c][j] * ip;
-        }
-        __syncthreads();
-      }
-      // pivots of the eliminated block are its diagonal; check them all
-      bool bad = false;
-      for (int j = 0; j < nb; ++j) bad |= !(D[j][j] > 0.0);
-      if (bad) {
-        if (tid == 0) fail = 1;
-        __syncthreads();
-        break;
-      }
-      // scale: L_ij = D_ij / sqrt(D_jj)
-      double vals[2];
-      int idx[2];
-      int cnt = 0;
-      for (int e = tid; e < nb * nb && cnt < 2; e += nt, ++cnt) {
-        const int i = e / nb, j = e % nb;
-        idx[cnt] = e;
-        vals[cnt] = (j <= i) ? D[i][j] / sqrt(D[j][j]) : 0.0;
-      }
-      __syncthreads();
-      for (int c = 0; c < cnt; ++c) {
-        const int i = idx[c] / nb, j = idx[c] % nb;
-        D[i][j] = vals[c];
-        L[(size_t)(k0 + i) * ldl + k0 + j] = vals[c];
-      }
-      __syncthreads();
-      // (2) panel: rows r >= k0+nb solve x D^T = a
-      const int r0 = k0 + nb;
-      for (int r = r0 + tid; r < n; r += nt) {
-        double* row = L + (size_t)r * ldl + k0;
-        double x[CNB];
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) {
-          if (c < nb) {
-            double s = row[c];
-#pragma unroll
-            for (int q = 0; q < c; ++q) s -= x[q] * D[c][q];
-            x[c] = s / D[c][c];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < CNB; ++c)
-          if (c < nb) row[c] = x[c];
-      }
-      __syncthreads();
-      // (3) trailing update of the lower triangle: C -= P P^T
-      const int tr = n - r0;
-      if (tr > 0) {
-        const int T = (tr + CT - 1) / CT;
-        for (int ti = 0; ti < T; ++ti) {
-          for (int tj = 0; tj <= ti; ++tj) {
-            for (int e = tid; e < CT * CNB; e += nt) {
-              const int rr = e / CNB, cc = e % CNB;
-              const int gi = r0 + ti * CT + rr, gj = r0 + tj * CT + rr;
-              Pi[rr][cc] = (gi < n && cc < nb) ? L[(size_t)gi * ldl + k0 + cc] : 0.0;
-              Pj[rr][cc] = (gj < n && cc < nb) ? L[(size_t)gj * ldl + k0 + cc] : 0.0;
-            }
-            __syncthreads();
-            // 1024 threads x 4 outputs = 64x64 tile
-            const int tx = tid & 31, ty = tid >> 5;  // cols tx, tx+32 ; rows ty, ty+32
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-#pragma unroll
-              for (int c2 = 0; c2 < 2; ++c2) {
-                const int rr = ty + 32 * a, cc = tx + 32 * c2;
-                const int gi = r0 + ti * CT + rr, gj = r0 + tj * CT + cc;
-                if (gi < n && gj <= gi) {
-                  double s = 0.0;
-#pragma unroll 8
-                  for (int q = 0; q < CNB; ++q) s += Pi[rr][q] * Pj[cc][q];
-                  L[(size_t)gi * ldl + gj] -= s;
-                }
-              }
-            }
-            __syncthreads();
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (!fail) break;
-  }
-  if (tid == 0) {
-    if (jitter_used) jitter_used[b] = jit;
-    if (info) info[b] = fail ? 1 : 0;
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -326,7 +198,249 @@ __global__ void set_identity_kernel(int n, double* M, long long sM, int ldm) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Blocked right-looking Cholesky (NB = 64) with the diagonal-block inverses:
+//   diag:   one workgroup factors L_kk and forms inv(L_kk) by elimination on [A_kk | I]
+//           (64 barrier steps), flags a non-positive pivot in info[b];
+//   panel:  L[k+nb:, k] <- L[k+nb:, k] inv(L_kk)^T       (MFMA GEMM, in place)
+//   update: L[k+nb:, k+nb:] -= P P^T, lower triangle only  (MFMA GEMM)
+// ---------------------------------------------------------------------------------------
+constexpr int BNB = 64;
+
+__global__ void chol_init_kernel(int n, const double* __restrict__ A, long long sA, int lda, double* __restrict__ L,
+                                 long long sL, int ldl, const double* __restrict__ jit) {
+  const int b = blockIdx.y;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)n * n) return;
+  const int i = (int)(e / n), j = (int)(e % n);
+  double v = (j <= i) ? A[b * sA + (size_t)i * lda + j] : 0.0;
+  if (i == j) v += jit[b];
+  L[b * sL + (size_t)i * ldl + j] = v;
+}
+
+// Factor the diagonal block at k0 (already updated), write L_kk into L and inv(L_kk) to
+// Dinv (ld BNB).  Elimination keeps the unnormalised pivots d_j: L = L_unit d^1/2 and
+// inv(L) = d^-1/2 inv(L_unit), with inv(L_unit) accumulated in E.
+__global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* __restrict__ Lm, long long sL, int ldl,
+                                                        double* __restrict__ Dinv, long long sD,
+                                                        int* __restrict__ info) {
+  const int b = blockIdx.x;
+  if (info[b]) return;
+  double* L = Lm + b * sL;
+  double* Di = Dinv + b * sD;
+  const int nb = min(BNB, n - k0);
+  __shared__ double D[BNB][BNB + 1];
+  __shared__ double E[BNB][BNB + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < BNB * BNB; e += 256) {
+    const int i = e / BNB, c = e % BNB;
+    D[i][c] = (i < nb && c <= i) ? L[(size_t)(k0 + i) * ldl + k0 + c] : 0.0;
+    E[i][c] = (i == c) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    const double p = D[j][j];
+    if (!(p > 0.0)) break;  // uniform
+    const double ip = 1.0 / p;
+    const int rem = nb - j - 1;
+    const int t1 = rem * rem, t2 = rem * (j + 1);
+    for (int e = tid; e < t1 + t2; e += 256) {
+      if (e < t1) {
+        const int i = j + 1 + e / rem, c = j + 1 + e % rem;
+        if (c <= i) D[i][c] -= D[i][j] * D[c][j] * ip;
+      } else {
+        const int f = e - t1;
+        const int i = j + 1 + f / (j + 1), c = f % (j + 1);
+        E[i][c] -= D[i][j] * ip * E[j][c];
+      }
+    }
+    __syncthreads();
+  }
+  int bad = -1;
+  for (int j = nb - 1; j >= 0; --j)
+    if (!(D[j][j] > 0.0)) bad = j;
+  if (bad >= 0) {
+    if (tid == 0) info[b] = k0 + bad + 1;
+    return;
+  }
+  for (int e = tid; e < BNB * BNB; e += 256) {
+    const int i = e / BNB, c = e % BNB;
+    if (i < nb && c < nb) {
+      const double lv = (c <= i) ? D[i][c] / sqrt(D[c][c]) : 0.0;
+      L[(size_t)(k0 + i) * ldl + k0 + c] = lv;
+      Di[(size_t)i * BNB + c] = (c <= i) ? E[i][c] / sqrt(D[i][i]) : 0.0;
+    } else {
+      Di[(size_t)i * BNB + c] = (i == c) ? 1.0 : 0.0;
+    }
+  }
+}
+
+// Inverse of every 64x64 diagonal block of a given lower-triangular L (grid (blocks, batch)):
+// column-parallel forward substitution, row steps separated by barriers.
+__global__ __launch_bounds__(256) void diag_block_inverse_kernel(int n, const double* __restrict__ Lm, long long sL,
+                                                                 int ldl, double* __restrict__ Dinv, long long sD) {
+  const int blk = blockIdx.x, b = blockIdx.y;
+  const double* L = Lm + b * sL;
+  double* Di = Dinv + b * sD + (size_t)blk * BNB * BNB;
+  const int r0 = blk * BNB, nb = min(BNB, n - r0);
+  __shared__ double T[BNB][BNB + 1];
+  __shared__ double X[BNB][BNB + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < BNB * BNB; e += 256) {
+    const int i = e / BNB, c = e % BNB;
+    T[i][c] = (i < nb && c <= i) ? L[(size_t)(r0 + i) * ldl + r0 + c] : (i == c ? 1.0 : 0.0);
+    X[i][c] = 0.0;
+  }
+  __syncthreads();
+  // row r: X[r][c] = (delta_rc - sum_{c<=t<r} T[r][t] X[t][c]) / T[r][r], c <= r; 4 threads/column
+  const int c = tid & 63, part = tid >> 6;
+  for (int r = 0; r < BNB; ++r) {
+    double s = 0.0;
+    if (c <= r)
+      for (int t = c + part; t < r; t += 4) s = fma(T[r][t], X[t][c], s);
+    __shared__ double red[4][BNB];
+    red[part][c] = s;
+    __syncthreads();
+    if (part == 0 && c <= r) {
+      const double tot = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      X[r][c] = ((r == c ? 1.0 : 0.0) - tot) / T[r][r];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < BNB * BNB; e += 256) {
+    const int i = e / BNB, cc = e % BNB;
+    Di[(size_t)i * BNB + cc] = (i < nb && cc < nb) ? X[i][cc] : (i == cc ? 1.0 : 0.0);
+  }
+}
+
+// X = 0 except the diagonal blocks, which receive Dinv (batch x nblk x 64 x 64)
+__global__ void place_diag_blocks_kernel(int n, const double* __restrict__ Dinv, long long sD, double* __restrict__ X,
+                                         long long sX, int ldx) {
+  const int b = blockIdx.y;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)n * n) return;
+  const int i = (int)(e / n), j = (int)(e % n);
+  const int bi = i / BNB, bj = j / BNB;
+  double v = 0.0;
+  if (bi == bj) v = Dinv[b * sD + ((size_t)bi * BNB + (i - bi * BNB)) * BNB + (j - bj * BNB)];
+  X[b * sX + (size_t)i * ldx + j] = v;
+}
+
 }  // namespace evr
+
+namespace {
+using namespace evr;
+
+int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alpha, const double* A, int lda,
+                long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
+                int batch, int lower_only = 0, const int* skip = nullptr) {
+  if (M == 0 || N == 0) return 0;
+  dim3 grid(cdiv(N, GT), cdiv(M, GT), batch);
+#define G_(TA_, TB_)                                                                                       \
+  gemm_f64_kernel<TA_, TB_><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
+                                                 lower_only, skip)
+  if (!tA && !tB) G_(false, false);
+  else if (!tA && tB) G_(false, true);
+  else if (tA && !tB) G_(true, false);
+  else G_(true, true);
+#undef G_
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+// One blocked factorisation attempt of every batch member (jitter already in L's diagonal).
+int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long sL, double* Dinv, int* info) {
+  const int nblk = (n + BNB - 1) / BNB;
+  const long long sD = (long long)nblk * BNB * BNB;
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int k0 = kb * BNB, nb = std::min(BNB, n - k0), r0 = k0 + nb, t = n - r0;
+    double* Dk = Dinv + (size_t)kb * BNB * BNB;
+    chol_diag_kernel<<<batch, 256, 0, s>>>(n, k0, L, sL, ldl, Dk, sD, info);
+    EVR_LAUNCH_CHECK();
+    if (t <= 0) break;
+    double* P = L + (size_t)r0 * ldl + k0;
+    // panel: P <- P Dk^T (in place; one 64-column tile, K loop completes before the store)
+    if (launch_gemm(s, false, true, t, nb, nb, 1.0, P, ldl, sL, Dk, BNB, sD, 0.0, P, ldl, sL, batch, 0, info))
+      return 1;
+    // trailing update, lower triangle
+    double* C = L + (size_t)r0 * ldl + r0;
+    if (launch_gemm(s, false, true, t, t, nb, -1.0, P, ldl, sL, P, ldl, sL, 1.0, C, ldl, sL, batch, 1, info))
+      return 1;
+  }
+  return 0;
+}
+
+// X = L^-1 from L and the diagonal-block inverses (block forward substitution with GEMMs).
+int tri_inv_blocked(hipStream_t s, int batch, int n, const double* L, int ldl, long long sL, const double* Dinv,
+                    double* X, int ldx, long long sX, double* T, const int* skip) {
+  const int nblk = (n + BNB - 1) / BNB;
+  const long long sD = (long long)nblk * BNB * BNB;
+  dim3 g1(cdiv((long long)n * n, 256), batch);
+  place_diag_blocks_kernel<<<g1, 256, 0, s>>>(n, Dinv, sD, X, sX, ldx);
+  EVR_LAUNCH_CHECK();
+  const long long sT = (long long)BNB * n;
+  for (int i = 1; i < nblk; ++i) {
+    const int r0 = i * BNB, rb = std::min(BNB, n - r0);
+    // T = L[r0:r0+rb, 0:r0] X[0:r0, 0:r0]
+    if (launch_gemm(s, false, false, rb, r0, r0, 1.0, L + (size_t)r0 * ldl, ldl, sL, X, ldx, sX, 0.0, T, n, sT,
+                    batch, 0, skip))
+      return 1;
+    // X[r0:r0+rb, 0:r0] = -inv(L_ii) T
+    if (launch_gemm(s, false, false, rb, r0, rb, -1.0, Dinv + (size_t)i * BNB * BNB, BNB, sD, T, n, sT, 0.0,
+                    X + (size_t)r0 * ldx, ldx, sX, batch, 0, skip))
+      return 1;
+  }
+  return 0;
+}
+
+// Jitter ladder around chol_blocked: members that fail get jitter0*10^(t-1) added to A's
+// diagonal and the batch is refactored (members that already succeeded recompute
+// identically), as psd_safe_cholesky does per failing batch member.
+int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long long sA, double* L, int ldl,
+                long long sL, double jitter0, int max_tries, double* jitter_used, int* info_out, double* Linv,
+                int ldi, long long sI) {
+  const int nblk = (n + BNB - 1) / BNB;
+  const size_t dbytes = sizeof(double) * (size_t)batch * nblk * BNB * BNB;
+  const size_t tbytes = Linv ? sizeof(double) * (size_t)batch * BNB * n : 0;
+  double *Dinv = nullptr, *T = nullptr, *jit_d = nullptr;
+  int* info_d = nullptr;
+  EVR_HIP(hipMallocAsync((void**)&Dinv, dbytes, s));
+  if (tbytes) EVR_HIP(hipMallocAsync((void**)&T, tbytes, s));
+  EVR_HIP(hipMallocAsync((void**)&jit_d, sizeof(double) * batch, s));
+  EVR_HIP(hipMallocAsync((void**)&info_d, sizeof(int) * batch, s));
+  std::vector<double> jit(batch, 0.0);
+  std::vector<int> info(batch, 0);
+  int rc = 0;
+  for (int t = 0; t <= max_tries; ++t) {
+    EVR_HIP(hipMemcpyAsync(jit_d, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
+    EVR_HIP(hipMemsetAsync(info_d, 0, sizeof(int) * batch, s));
+    dim3 g1(cdiv((long long)n * n, 256), batch);
+    chol_init_kernel<<<g1, 256, 0, s>>>(n, A, sA, lda, L, sL, ldl, jit_d);
+    EVR_LAUNCH_CHECK();
+    if ((rc = chol_blocked(s, batch, n, L, ldl, sL, Dinv, info_d))) break;
+    EVR_HIP(hipMemcpyAsync(info.data(), info_d, sizeof(int) * batch, hipMemcpyDeviceToHost, s));
+    EVR_HIP(hipStreamSynchronize(s));
+    bool anyfail = false;
+    for (int b = 0; b < batch; ++b)
+      if (info[b]) {
+        anyfail = true;
+        if (t < max_tries) jit[b] = jitter0 * std::pow(10.0, (double)t);
+      }
+    if (!anyfail || t == max_tries) break;
+  }
+  if (!rc && Linv) rc = tri_inv_blocked(s, batch, n, L, ldl, sL, Dinv, Linv, ldi, sI, T, info_d);
+  if (!rc) {
+    if (jitter_used) EVR_HIP(hipMemcpyAsync(jitter_used, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
+    if (info_out) EVR_HIP(hipMemcpyAsync(info_out, info_d, sizeof(int) * batch, hipMemcpyDeviceToDevice, s));
+  }
+  EVR_HIP(hipStreamSynchronize(s));  // host vectors above must outlive the async copies
+  hipFreeAsync(Dinv, s);
+  if (T) hipFreeAsync(T, s);
+  hipFreeAsync(jit_d, s);
+  hipFreeAsync(info_d, s);
+  return rc;
+}
+}  // namespace
 
 using namespace evr;
 
@@ -337,33 +451,25 @@ int evr_gemm_f64(void* stream, int transA, int transB, int M, int N, int K, doub
                  int ldc, long long strideC, int batch) {
   EVR_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "evr_gemm_f64: bad sizes M=%d N=%d K=%d batch=%d", M, N,
             K, batch);
-  if (M == 0 || N == 0) return 0;
-  dim3 grid(cdiv(N, GT), cdiv(M, GT), batch);
-  hipStream_t s = (hipStream_t)stream;
-  if (!transA && !transB)
-    gemm_f64_kernel<false, false><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
-                                                        ldc, strideC);
-  else if (!transA && transB)
-    gemm_f64_kernel<false, true><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
-                                                       ldc, strideC);
-  else if (transA && !transB)
-    gemm_f64_kernel<true, false><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
-                                                       ldc, strideC);
-  else
-    gemm_f64_kernel<true, true><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
-                                                      ldc, strideC);
-  EVR_LAUNCH_CHECK();
-  return 0;
+  return launch_gemm((hipStream_t)stream, transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
+                     ldc, strideC, batch);
 }
 
 int evr_cholesky(void* stream, int batch, int n, const double* A, int lda, long long strideA, double* L, int ldl,
                  long long strideL, double jitter0, int max_tries, double* jitter_used, int* info) {
   EVR_CHECK(n >= 1 && batch >= 1 && max_tries >= 0, "evr_cholesky: bad sizes n=%d batch=%d", n, batch);
   EVR_CHECK(A != L, "evr_cholesky: A and L must not alias (the jitter ladder restarts from A)");
-  chol_kernel<<<batch, 1024, 0, (hipStream_t)stream>>>(n, A, strideA, lda, L, strideL, ldl, jitter0, max_tries,
-                                                       jitter_used, info);
-  EVR_LAUNCH_CHECK();
-  return 0;
+  return chol_ladder((hipStream_t)stream, batch, n, A, lda, strideA, L, ldl, strideL, jitter0, max_tries,
+                     jitter_used, info, nullptr, 0, 0);
+}
+
+int evr_cholesky_inverse(void* stream, int batch, int n, const double* A, int lda, long long strideA, double* L,
+                         int ldl, long long strideL, double* Linv, int ldi, long long strideI, double jitter0,
+                         int max_tries, double* jitter_used, int* info) {
+  EVR_CHECK(n >= 1 && batch >= 1 && max_tries >= 0, "evr_cholesky_inverse: bad sizes n=%d batch=%d", n, batch);
+  EVR_CHECK(A != L && Linv != L && Linv != A, "evr_cholesky_inverse: A, L and Linv must not alias");
+  return chol_ladder((hipStream_t)stream, batch, n, A, lda, strideA, L, ldl, strideL, jitter0, max_tries,
+                     jitter_used, info, Linv, ldi, strideI);
 }
 
 int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, int ldl, long long strideL,
@@ -382,10 +488,23 @@ int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, in
 int evr_tri_inv_lower(void* stream, int batch, int n, const double* L, int ldl, long long strideL, double* Linv,
                       int ldi, long long strideI) {
   EVR_CHECK(n >= 1 && batch >= 1, "evr_tri_inv_lower: bad sizes");
-  dim3 g1(cdiv((long long)n * n, 256), batch);
-  set_identity_kernel<<<g1, 256, 0, (hipStream_t)stream>>>(n, Linv, strideI, ldi);
-  EVR_LAUNCH_CHECK();
-  return evr_trsm_lower(stream, batch, n, n, L, ldl, strideL, 0, Linv, ldi, strideI);
+  EVR_CHECK(L != Linv, "evr_tri_inv_lower: L and Linv must not alias");
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = (n + BNB - 1) / BNB;
+  double *Dinv = nullptr, *T = nullptr;
+  EVR_HIP(hipMallocAsync((void**)&Dinv, sizeof(double) * (size_t)batch * nblk * BNB * BNB, s));
+  EVR_HIP(hipMallocAsync((void**)&T, sizeof(double) * (size_t)batch * BNB * n, s));
+  dim3 g(nblk, batch);
+  diag_block_inverse_kernel<<<g, 256, 0, s>>>(n, L, strideL, ldl, Dinv, (long long)nblk * BNB * BNB);
+  int rc = 0;
+  if (hipGetLastError() != hipSuccess) {
+    set_error("evr_tri_inv_lower: launch failed");
+    rc = 1;
+  }
+  if (!rc) rc = tri_inv_blocked(s, batch, n, L, ldl, strideL, Dinv, Linv, ldi, strideI, T, nullptr);
+  hipFreeAsync(Dinv, s);
+  hipFreeAsync(T, s);
+  return rc;
 }
 
 }  // extern "C"

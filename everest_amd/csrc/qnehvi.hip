@@ -12,28 +12,51 @@
 namespace evr {
 
 // -------------------------------------------------------------------------------------
-// samples: one thread per (candidate c, objective j)
+// samples: block = BX candidates x RY row groups (256 threads); the row sums of squares
+// are split over the RY groups and reduced through LDS in a fixed order, then every
+// group writes its share of the S samples.  Grid (candidate tiles, m).
 // -------------------------------------------------------------------------------------
-__global__ void qn_samples_kernel(int n, int nb, int S, int m, int b, const double* __restrict__ R,
-                                  const double* __restrict__ cc, const double* __restrict__ ym,
-                                  const double* __restrict__ ys, const double* __restrict__ kxx,
-                                  const double* __restrict__ zq, const double* __restrict__ oa,
-                                  const double* __restrict__ ob, double* __restrict__ G, double* __restrict__ L22,
-                                  int* __restrict__ flags) {
+template <int BX>
+__global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, int m, int b,
+                                                         const double* __restrict__ R,
+                                                         const double* __restrict__ cc,
+                                                         const double* __restrict__ ym,
+                                                         const double* __restrict__ ys,
+                                                         const double* __restrict__ kxx,
+                                                         const double* __restrict__ zq,
+                                                         const double* __restrict__ oa,
+                                                         const double* __restrict__ ob, double* __restrict__ G,
+                                                         double* __restrict__ L22, int* __restrict__ flags) {
+  constexpr int RY = 256 / BX;
+  __shared__ double red[2][RY][BX];
   const int j = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= b) return;
+  const int cx = threadIdx.x % BX, ry = threadIdx.x / BX;
+  const int c = blockIdx.x * BX + cx;
+  const bool live = c < b;
   const long long Rr = (long long)n + nb + S + 1;
   const double* Rj = R + (size_t)j * Rr * b;
   double ssv = 0.0, ssw = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double v = Rj[(size_t)i * b + c];
-    ssv = fma(v, v, ssv);
+  if (live) {
+    for (int i = ry; i < n; i += RY) {
+      const double v = Rj[(size_t)i * b + c];
+      ssv = fma(v, v, ssv);
+    }
+    for (int i = n + ry; i < n + nb; i += RY) {
+      const double v = Rj[(size_t)i * b + c];
+      ssw = fma(v, v, ssw);
+    }
   }
-  for (int i = n; i < n + nb; ++i) {
-    const double v = Rj[(size_t)i * b + c];
-    ssw = fma(v, v, ssw);
+  red[0][ry][cx] = ssv;
+  red[1][ry][cx] = ssw;
+  __syncthreads();
+  ssv = 0.0;
+  ssw = 0.0;
+#pragma unroll
+  for (int g = 0; g < RY; ++g) {
+    ssv += red[0][g][cx];
+    ssw += red[1][g][cx];
   }
+  if (!live) return;
   const double a = Rj[(size_t)(n + nb + S) * b + c];
   const double s = ys[j];
   const double mu = ym[j] + s * (cc[j] + a);
@@ -52,126 +75,15 @@ __global__ void qn_samples_kernel(int n, int nb, int S, int m, int b, const doub
       }
     }
   }
-  L22[(size_t)j * b + c] = l22;
-  flags[(size_t)j * b + c] = flag;
+  if (ry == 0) {
+    L22[(size_t)j * b + c] = l22;
+    flags[(size_t)j * b + c] = flag;
+  }
   const double A = oa[j], B0 = ob[j];
   const double* h = Rj + (size_t)(n + nb) * b + c;
-  for (int si = 0; si < S; ++si) {
+  for (int si = ry; si < S; si += RY) {
     const double y = mu + h[(size_t)si * b] + l22 * zq[(size_t)si * m + j];
     G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
-  }
-}
-
-// -------------------------------------------------------------------------------------
-// HVI forward: grid (candidate tiles, S). Cells of sample s are streamed through LDS in
-// chunks; every lane reads the same cell (LDS broadcast) and updates CPT candidates.
-// -------------------------------------------------------------------------------------
-constexpr int HT = 256;   // threads per block
-constexpr int HCH = 128;  // cells per LDS chunk
-
-template <int M, int CPT>
-__global__ __launch_bounds__(HT) void hvi_fwd_kernel(int S, int b, const double* __restrict__ G,
-                                                     const double* __restrict__ lo, const double* __restrict__ hi,
-                                                     const int* __restrict__ off, double* __restrict__ partial) {
-  const int s = blockIdx.y;
-  const int tid = threadIdx.x;
-  const int cbase = blockIdx.x * HT * CPT;
-  __shared__ double Ls[HCH * M];
-  __shared__ double Hs[HCH * M];
-  double y[CPT][M];
-  double acc[CPT];
-#pragma unroll
-  for (int p = 0; p < CPT; ++p) {
-    const int c = cbase + p * HT + tid;
-    acc[p] = 0.0;
-#pragma unroll
-    for (int j = 0; j < M; ++j) y[p][j] = (c < b) ? G[((size_t)s * M + j) * b + c] : -INFINITY;
-  }
-  const int c0 = off[s], c1 = off[s + 1];
-  for (int k0 = c0; k0 < c1; k0 += HCH) {
-    const int nc = min(HCH, c1 - k0);
-    for (int e = tid; e < nc * M; e += HT) {
-      Ls[e] = lo[(size_t)k0 * M + e];
-      Hs[e] = hi[(size_t)k0 * M + e];
-    }
-    __syncthreads();
-    for (int k = 0; k < nc; ++k) {
-      double l[M], h[M];
-#pragma unroll
-      for (int j = 0; j < M; ++j) {
-        l[j] = Ls[k * M + j];
-        h[j] = Hs[k * M + j];
-      }
-#pragma unroll
-      for (int p = 0; p < CPT; ++p) {
-        double prod = 1.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) prod *= fmax(fmin(y[p][j], h[j]) - l[j], 0.0);
-        acc[p] += prod;
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int p = 0; p < CPT; ++p) {
-    const int c = cbase + p * HT + tid;
-    if (c < b) partial[(size_t)s * b + c] = acc[p];
-  }
-}
-
-// HVI backward: dG[s][j][c] = gs * sum_cells pass_j * prod_{k != j} len_k
-template <int M>
-__global__ __launch_bounds__(HT) void hvi_bwd_kernel(int S, int b, const double* __restrict__ G,
-                                                     const double* __restrict__ lo, const double* __restrict__ hi,
-                                                     const int* __restrict__ off, const double* __restrict__ gout,
-                                                     double* __restrict__ dG) {
-  const int s = blockIdx.y;
-  const int tid = threadIdx.x;
-  const int c = blockIdx.x * HT + tid;
-  __shared__ double Ls[HCH * M];
-  __shared__ double Hs[HCH * M];
-  double y[M], g[M];
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    y[j] = (c < b) ? G[((size_t)s * M + j) * b + c] : -INFINITY;
-    g[j] = 0.0;
-  }
-  const int c0 = off[s], c1 = off[s + 1];
-  for (int k0 = c0; k0 < c1; k0 += HCH) {
-    const int nc = min(HCH, c1 - k0);
-    for (int e = tid; e < nc * M; e += HT) {
-      Ls[e] = lo[(size_t)k0 * M + e];
-      Hs[e] = hi[(size_t)k0 * M + e];
-    }
-    __syncthreads();
-    for (int k = 0; k < nc; ++k) {
-      double len[M], pass[M];
-#pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const double h = Hs[k * M + j];
-        const double raw = fmin(y[j], h) - Ls[k * M + j];
-        len[j] = fmax(raw, 0.0);
-        // d clamp_min/d raw = (raw >= 0); d minimum/d y = 1 (y<h), 1/2 (y==h), 0 (y>h)
-        const double dmin = (y[j] < h) ? 1.0 : ((y[j] == h) ? 0.5 : 0.0);
-        pass[j] = (raw >= 0.0) ? dmin : 0.0;
-      }
-      double pre[M + 1];
-      pre[0] = 1.0;
-#pragma unroll
-      for (int j = 0; j < M; ++j) pre[j + 1] = pre[j] * len[j];
-      double suf = 1.0;
-#pragma unroll
-      for (int j = M - 1; j >= 0; --j) {
-        g[j] = fma(pass[j], pre[j] * suf, g[j]);
-        suf *= len[j];
-      }
-    }
-    __syncthreads();
-  }
-  if (c < b) {
-    const double gs = gout[c] / (double)S;
-#pragma unroll
-    for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = gs * g[j];
   }
 }
 
@@ -183,33 +95,53 @@ __global__ void mean_over_samples_kernel(int S, int b, const double* __restrict_
   acq[c] = s / (double)S;
 }
 
-// samples backward: one thread per (c, j); writes gR_j (Rr x b)
-__global__ void qn_samples_bwd_kernel(int n, int nb, int S, int m, int b, const double* __restrict__ R,
-                                      const double* __restrict__ ys, const double* __restrict__ zq,
-                                      const double* __restrict__ oa, const double* __restrict__ L22,
-                                      const double* __restrict__ dG, double* __restrict__ gR) {
+// samples backward: same (BX x RY) blocking; writes gR_j (Rr x b)
+template <int BX>
+__global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int S, int m, int b,
+                                                             const double* __restrict__ R,
+                                                             const double* __restrict__ ys,
+                                                             const double* __restrict__ zq,
+                                                             const double* __restrict__ oa,
+                                                             const double* __restrict__ L22,
+                                                             const double* __restrict__ dG, double* __restrict__ gR) {
+  constexpr int RY = 256 / BX;
+  __shared__ double red[2][RY][BX];
   const int j = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= b) return;
+  const int cx = threadIdx.x % BX, ry = threadIdx.x / BX;
+  const int c = blockIdx.x * BX + cx;
+  const bool live = c < b;
   const long long Rr = (long long)n + nb + S + 1;
   const double* Rj = R + (size_t)j * Rr * b;
   double* gj = gR + (size_t)j * Rr * b;
   const double A = oa[j];
   double dmu = 0.0, dl = 0.0;
-  for (int si = 0; si < S; ++si) {
-    const double dy = A * dG[((size_t)si * m + j) * b + c];
-    dmu += dy;
-    dl = fma(dy, zq[(size_t)si * m + j], dl);
-    gj[(size_t)(n + nb + si) * b + c] = dy;
+  if (live) {
+    for (int si = ry; si < S; si += RY) {
+      const double dy = A * dG[((size_t)si * m + j) * b + c];
+      dmu += dy;
+      dl = fma(dy, zq[(size_t)si * m + j], dl);
+      gj[(size_t)(n + nb + si) * b + c] = dy;
+    }
   }
+  red[0][ry][cx] = dmu;
+  red[1][ry][cx] = dl;
+  __syncthreads();
+  dmu = 0.0;
+  dl = 0.0;
+#pragma unroll
+  for (int g = 0; g < RY; ++g) {
+    dmu += red[0][g][cx];
+    dl += red[1][g][cx];
+  }
+  if (!live) return;
   const double s = ys[j];
-  gj[(size_t)(n + nb + S) * b + c] = s * dmu;
+  if (ry == 0) gj[(size_t)(n + nb + S) * b + c] = s * dmu;
   const double l22 = L22[(size_t)j * b + c];
   const double dbr = dl / (2.0 * l22);
   const double dssv = -s * s * dbr;  // var = s^2 (kxx - ssv); br = var - ssw
   const double dssw = -dbr;
-  for (int i = 0; i < n; ++i) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssv;
-  for (int i = n; i < n + nb; ++i) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssw;
+  for (int i = ry; i < n; i += RY) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssv;
+  for (int i = n + ry; i < n + nb; i += RY) gj[(size_t)i * b + c] = 2.0 * Rj[(size_t)i * b + c] * dssw;
 }
 
 // -------------------------------------------------------------------------------------
@@ -347,26 +279,16 @@ int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const do
                        int* flags) {
   EVR_CHECK(st && st->m >= 1 && st->S >= 1 && st->n >= 1 && st->nb >= 0, "evr_qnehvi_samples: bad state");
   if (b == 0) return 0;
-  dim3 grid(cdiv(b, 256), st->m);
-  qn_samples_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys,
-                                                           st->kxx, st->zq, st->obj_a, st->obj_b, G, L22, flags);
-  EVR_LAUNCH_CHECK();
-  return 0;
-}
-
-int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* partial) {
-  EVR_CHECK(st && st->S >= 1, "evr_hvi_forward: bad state");
-  if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int cpt = (b > HT) ? 2 : 1;
-  dim3 grid(cdiv(b, HT * cpt), st->S);
-#define L(MM)                                                                                                \
-  if (cpt == 2)                                                                                            \
-    hvi_fwd_kernel<MM, 2><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, partial); \
-  else                                                                                                     \
-    hvi_fwd_kernel<MM, 1><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, partial)
-  EVR_DISPATCH_M(st->m, L);
-#undef L
+  if (b <= 256) {  // small batches: 16 candidates x 16 row groups per block
+    dim3 grid(cdiv(b, 16), st->m);
+    qn_samples_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys, st->kxx,
+                                               st->zq, st->obj_a, st->obj_b, G, L22, flags);
+  } else {
+    dim3 grid(cdiv(b, 64), st->m);
+    qn_samples_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys, st->kxx,
+                                               st->zq, st->obj_a, st->obj_b, G, L22, flags);
+  }
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -378,26 +300,20 @@ int evr_mean_over_samples(void* stream, int S, int b, const double* partial, dou
   return 0;
 }
 
-int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
-                     double* dG) {
-  EVR_CHECK(st && st->S >= 1, "evr_hvi_backward: bad state");
-  if (b == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  dim3 grid(cdiv(b, HT), st->S);
-#define L(MM) hvi_bwd_kernel<MM><<<grid, HT, 0, s>>>(st->S, b, G, st->cell_lo, st->cell_hi, st->cell_off, gout, dG)
-  EVR_DISPATCH_M(st->m, L);
-#undef L
-  EVR_LAUNCH_CHECK();
-  return 0;
-}
-
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* L22,
                                 const double* dG, double* gR) {
   EVR_CHECK(st && st->m >= 1, "evr_qnehvi_samples_backward: bad state");
   if (b == 0) return 0;
-  dim3 grid(cdiv(b, 256), st->m);
-  qn_samples_bwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq,
-                                                               st->obj_a, L22, dG, gR);
+  hipStream_t s = (hipStream_t)stream;
+  if (b <= 256) {
+    dim3 grid(cdiv(b, 16), st->m);
+    qn_samples_bwd_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq, st->obj_a,
+                                                   L22, dG, gR);
+  } else {
+    dim3 grid(cdiv(b, 64), st->m);
+    qn_samples_bwd_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq, st->obj_a,
+                                                   L22, dG, gR);
+  }
   EVR_LAUNCH_CHECK();
   return 0;
 }

@@ -126,8 +126,7 @@ class GPBatch:
     # -- caches: L = chol(K + s2 I), Linv, alpha, M = [Linv; alpha^T] ----------------------
     def refresh(self):
         Ky = ops.kernel_matrix(self.Xn, self.Xn, self.ls, self.kind, diag_add=self.noise)
-        self.L, _, _ = ops.cholesky(Ky, 1e-8, 3)
-        self.Linv = ops.tri_inv(self.L)
+        self.L, self.Linv, _, _ = ops.cholesky_inverse(Ky, 1e-8, 3)
         r = (self.y - self.const[:, None]).unsqueeze(-1).contiguous()         # B x n x 1
         v = ops.gemm(self.Linv, r)
         self.alpha = ops.gemm(self.Linv, v, transA=True)[..., 0].contiguous()  # B x n
@@ -173,8 +172,7 @@ class MLLEvaluator:
         ls_t = torch.as_tensor(ls[None, :], device=dev)
         Ky = ops.kernel_matrix(self.Xn, self.Xn, ls_t, self.kind,
                                diag_add=torch.tensor([noise], dtype=torch.float64, device=dev))
-        L, _, _ = ops.cholesky(Ky, 1e-8, 3)
-        Linv = ops.tri_inv(L)
+        L, Linv, _, _ = ops.cholesky_inverse(Ky, 1e-8, 3)
         r = torch.as_tensor((self.y - const)[None, :, None], device=dev)
         v = ops.gemm(Linv, r)
         alpha = ops.gemm(Linv, v, transA=True)                       # 1 x n x 1

@@ -177,6 +177,31 @@ def cholesky(A: torch.Tensor, jitter0: float = 1e-8, max_tries: int = 3, raise_o
     return L, jit, info
 
 
+def cholesky_inverse(A: torch.Tensor, jitter0: float = 1e-8, max_tries: int = 3, raise_on_fail: bool = True):
+    """(L, L^-1, jitter_used, info) from one blocked pass (psd_safe_cholesky semantics)."""
+    A = _dev(A, "A")
+    squeeze = A.dim() == 2
+    if squeeze:
+        A = A.unsqueeze(0)
+    B, n, n2 = A.shape
+    if n != n2:
+        raise ValueError("cholesky_inverse: matrix not square")
+    L = torch.empty_like(A)
+    Li = torch.empty_like(A)
+    jit = torch.empty(B, dtype=torch.float64, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    call("evr_cholesky_inverse", _stream(), B, n, A.data_ptr(), n, n * n, L.data_ptr(), n, n * n, Li.data_ptr(), n,
+         n * n, float(jitter0), int(max_tries), jit.data_ptr(), info.data_ptr())
+    if raise_on_fail:
+        bad = info.cpu()
+        if bool(bad.any()):
+            raise NotPSDError(f"Matrix not positive definite after repeatedly adding jitter up to "
+                              f"{jitter0 * 10 ** (max_tries - 1):.1e} (batch members {bad.nonzero().view(-1).tolist()})")
+    if squeeze:
+        return L[0], Li[0], jit[0], info[0]
+    return L, Li, jit, info
+
+
 def trsm(L: torch.Tensor, B: torch.Tensor, transpose: bool = False) -> torch.Tensor:
     """In place: B <- L^-1 B (or L^-T B).  L: (batch) x n x n, B: (batch) x n x nrhs."""
     L = _dev(L, "L")
@@ -217,12 +242,14 @@ def posterior_finalize(R, c, ym, ys, kxx, noise_add=None):
 # ---------------------------------------------------------------------------------------
 # qNEHVI pieces
 # ---------------------------------------------------------------------------------------
-def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cell_lo, cell_hi, cell_off) -> EvrQnehviState:
+def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cell_lo, cell_hi, cell_off,
+               max_cells: int) -> EvrQnehviState:
     st = EvrQnehviState()
     st.n, st.nb, st.S, st.m = int(n), int(nb), int(S), int(m)
     st.c, st.ym, st.ys, st.kxx = c.data_ptr(), ym.data_ptr(), ys.data_ptr(), kxx.data_ptr()
     st.zq, st.obj_a, st.obj_b = zq.data_ptr(), obj_a.data_ptr(), obj_b.data_ptr()
     st.cell_lo, st.cell_hi, st.cell_off = cell_lo.data_ptr(), cell_hi.data_ptr(), cell_off.data_ptr()
+    st.max_cells = int(max_cells)
     return st
 
 
@@ -236,10 +263,17 @@ def qnehvi_samples(st: EvrQnehviState, R: torch.Tensor, b: int):
     return G, L22, flags
 
 
-def hvi_forward(st: EvrQnehviState, G: torch.Tensor, b: int):
-    partial = torch.empty(st.S, b, dtype=torch.float64, device=G.device)
-    call("evr_hvi_forward", _stream(), ctypes.byref(st), b, G.data_ptr(), partial.data_ptr())
-    return partial
+def _hvi_work(st: EvrQnehviState, b: int, backward: bool, device) -> torch.Tensor:
+    n = _native.load().evr_hvi_workspace_doubles(ctypes.byref(st), b, int(backward))
+    return torch.empty(max(1, n), dtype=torch.float64, device=device)
+
+
+def hvi_forward(st: EvrQnehviState, G: torch.Tensor, b: int) -> torch.Tensor:
+    """acq[c] = mean_s HVI_s (register-tiled scan + deterministic reduction)."""
+    acq = torch.empty(b, dtype=torch.float64, device=G.device)
+    work = _hvi_work(st, b, False, G.device)
+    call("evr_hvi_forward", _stream(), ctypes.byref(st), b, G.data_ptr(), work.data_ptr(), acq.data_ptr())
+    return acq
 
 
 def mean_over_samples(partial: torch.Tensor):
@@ -252,7 +286,9 @@ def mean_over_samples(partial: torch.Tensor):
 def hvi_backward(st: EvrQnehviState, G: torch.Tensor, gout: torch.Tensor, b: int):
     dG = torch.empty_like(G)
     gout = _dev(gout, "gout")
-    call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), gout.data_ptr(), dG.data_ptr())
+    work = _hvi_work(st, b, True, G.device)
+    call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), gout.data_ptr(), work.data_ptr(),
+         dG.data_ptr())
     return dG
 
 

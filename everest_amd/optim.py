@@ -247,13 +247,25 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         full = torch.cat(bufs)[:nb].cpu().numpy()
         return full[:, 0], (full[:, 1:] if with_grad else None)
 
-    for s0, s1 in chunks:
+    # Independent chunks (batch_limit < num_restarts) are separate scipy problems in the
+    # reference: with at least as many chunks as ranks each rank owns whole chunks and runs
+    # them with no per-iteration collective; a single joint chunk is evaluated sharded.
+    own_chunks = world > 1 and len(chunks) >= world
+    local_world = 1 if own_chunks else world
+    for ci, (s0, s1) in enumerate(chunks):
+        if own_chunks and ci % world != rank:
+            continue
         nb = s1 - s0
         x0 = X0[s0:s1].reshape(-1)
         counter = {"n": 0}
 
         def f(x):
-            a, g = evaluate(x.reshape(nb, d), True)
+            if local_world == 1:
+                Xt = torch.as_tensor(x.reshape(nb, d), dtype=torch.float64, device=dev)
+                a, g = acqf.forward_backward(Xt)
+                a, g = a.cpu().numpy(), g.cpu().numpy()
+            else:
+                a, g = evaluate(x.reshape(nb, d), True)
             counter["n"] += 1
             return -float(a.sum()), -g.reshape(-1)
 
@@ -263,14 +275,33 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         res = minimize(f, x0, jac=True, method=method, bounds=bnds, constraints=cons or (),
                        options={"maxiter": maxiter})
         Xc = np.clip(res.x.reshape(nb, d), bounds[0], bounds[1])
-        vals, _ = evaluate(Xc, False)
+        if local_world == 1:
+            vals = acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)).cpu().numpy()
+        else:
+            vals, _ = evaluate(Xc, False)
         stats.opt_evals += counter["n"] * nb + nb
         stats.opt_iters += int(getattr(res, "nit", 0))
         stats.chunks.append({"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
                              "status": int(res.status)})
         results.append((vals, Xc))
-    vals = np.concatenate([r[0] for r in results])
-    Xs = np.concatenate([r[1] for r in results])
-    k = int(np.argmax(vals))
+    if results:
+        vals = np.concatenate([r[0] for r in results])
+        Xs = np.concatenate([r[1] for r in results])
+        k = int(np.argmax(vals))
+        best_v, best_x = float(vals[k]), Xs[k]
+    else:
+        best_v, best_x = -np.inf, np.zeros(d)
+    if own_chunks:   # all-gather every rank's best (value, x) over RCCL; argmax (ties -> lowest rank)
+        loc = torch.tensor(np.r_[best_v, best_x], dtype=torch.float64, device=dev)
+        bufs = [torch.empty_like(loc) for _ in range(world)]
+        dist.all_gather(bufs, loc)
+        allv = torch.stack(bufs).cpu().numpy()
+        k = int(np.argmax(allv[:, 0]))
+        best_v, best_x = float(allv[k, 0]), allv[k, 1:]
+        cnt = torch.tensor([stats.opt_evals], dtype=torch.float64, device=dev)
+        dist.all_reduce(cnt)
+        stats.opt_evals_global = int(cnt.item())
+    else:
+        stats.opt_evals_global = stats.opt_evals
     stats.t_opt += time.perf_counter() - t0
-    return Xs[k], float(vals[k]), stats
+    return best_x, best_v, stats

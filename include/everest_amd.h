@@ -80,6 +80,13 @@ int evr_cholesky(void* stream, int batch, int n, const double* A, int lda, long 
                  double* L, int ldl, long long strideL, double jitter0, int max_tries,
                  double* jitter_used, int* info);
 
+/* evr_cholesky plus L^-1 (Linv) from the same blocked pass (diagonal-block inverses are
+ * by-products of the factorisation).  A, L and Linv must not alias. */
+int evr_cholesky_inverse(void* stream, int batch, int n, const double* A, int lda, long long strideA,
+                         double* L, int ldl, long long strideL, double* Linv, int ldi,
+                         long long strideI, double jitter0, int max_tries, double* jitter_used,
+                         int* info);
+
 /* In-place B <- L^-1 B (transpose=0) or L^-T B (transpose=1); L lower, n x n; B n x nrhs. */
 int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, int ldl,
                    long long strideL, int transpose, double* B, int ldb, long long strideB);
@@ -116,20 +123,24 @@ typedef struct {
   const double* cell_lo;    /* total_cells x m */
   const double* cell_hi;    /* total_cells x m (may be +inf) */
   const int* cell_off;      /* S + 1 */
+  int max_cells;            /* max_s (cell_off[s+1] - cell_off[s]) — host-known, sizes the launch */
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b
  * (0 ok, 1 new-block Cholesky failed after 6 jitter tries). */
 int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                        double* G, double* L22, int* flags);
-/* partial[s][c] = HVI of G[s][:, c] over the cells of sample s */
+/* Workspace (doubles) the HVI scan needs for b candidates (per-(sample, cell-chunk) partials). */
+long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backward);
+/* acq[c] = mean_s HVI_s(G[s][:, c]) over the cells of sample s (register-tiled cell x
+ * candidate scan, deterministic two-stage reduction). */
 int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
-                    double* partial);
+                    double* work, double* acq);
 /* acq[c] = mean_s partial[s][c] */
 int evr_mean_over_samples(void* stream, int S, int b, const double* partial, double* acq);
 /* dG[s][j][c] = gout[c]/S * dHVI_s/dg_j (torch min/clamp_min/prod subgradients) */
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
-                     const double* gout, double* dG);
+                     const double* gout, double* work, double* dG);
 /* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);

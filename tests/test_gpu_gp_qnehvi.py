@@ -105,5 +105,8 @@ def test_qnehvi_large_batch_consistency():
     Xc = torch.tensor(lo + (hi - lo) * rng.uniform(size=(1024, 6)), device="cuda")
     full = dq.forward(Xc)
     part = torch.cat([dq.forward(Xc[i:i + 1]) for i in range(0, 1024, 97)])
-    assert torch.allclose(full[::97], part, rtol=0, atol=0)
+    # the tiling plan (and so the summation order) depends on b: equal up to rounding
+    assert torch.allclose(full[::97], part, rtol=1e-12, atol=1e-15)
     assert (full >= 0).all()
+    again = dq.forward(Xc)
+    assert torch.equal(full, again)              # bitwise reproducible for a fixed batch
