@@ -113,10 +113,9 @@ def step(acqf, Xc, timer=None):
     if T: T.stop(tk); tk = T.start("samples")
     G, L22, flags = ops.qnehvi_samples(st, R, b)
     if T: T.stop(tk); tk = T.start("hvi_fwd")
-    acq = ops.hvi_forward(st, G, b)
+    acq = ops.hvi_forward(st, G, b, flags)
     if T: T.stop(tk); tk = T.start("hvi_bwd")
-    gout = torch.ones(b, dtype=torch.float64, device=Xc.device)
-    dG = ops.hvi_backward(st, G, gout, b)
+    dG = ops.hvi_backward(st, G, None, b)
     if T: T.stop(tk); tk = T.start("samples_bwd")
     gR = ops.qnehvi_samples_backward(st, R, L22, dG, b)
     if T: T.stop(tk); tk = T.start("gemm_bwd")

@@ -58,7 +58,8 @@ _SIGS = {
     "evr_qnehvi_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
                            c_int),
     "evr_hvi_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int], c_longlong),
-    "evr_hvi_forward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_hvi_forward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_int),
     "evr_mean_over_samples": ([c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
     "evr_hvi_backward": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
                          c_int),

@@ -195,31 +195,27 @@ class QNEHVI:
         self.timings = tm
 
     # ------------------------------------------------------------------------------------
-    def _check_flags(self, flags):
-        if bool(flags.any().item()):
-            raise ops.NotPSDError("qNEHVI: new-point block of the cached Cholesky not p.d. after 6 jitter tries")
-
     def forward(self, X: torch.Tensor, return_cache: bool = False):
-        """X: b x d raw (transformed) candidates on device -> acquisition values (b)."""
+        """X: b x d raw (transformed) candidates on device -> acquisition values (b).
+
+        A candidate whose new-point Cholesky block stays not p.d. after the 6-rung jitter
+        ladder gets NaN (no device->host sync here); ``optim.host_values`` turns a NaN into
+        the NotPSDError BoTorch raises from sample_cached_cholesky."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
         Kx = self.gp.cross(X)                       # m x n x b
         R = ops.gemm(self.M, Kx)                    # m x Rr x b
         G, L22, flags = ops.qnehvi_samples(self.state, R, b)
-        acq = ops.hvi_forward(self.state, G, b)
+        acq = ops.hvi_forward(self.state, G, b, flags)
         if return_cache:
             return acq, (X, R, G, L22, flags)
-        self._check_flags(flags)
         return acq
 
     def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
         """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         acq, (X, R, G, L22, flags) = self.forward(X, return_cache=True)
-        self._check_flags(flags)
         b = X.shape[0]
-        if gout is None:
-            gout = torch.ones(b, dtype=torch.float64, device=self.dev)
         dG = ops.hvi_backward(self.state, G, gout, b)
         gR = ops.qnehvi_samples_backward(self.state, R, L22, dG, b)
         dKx = ops.gemm(self.M, gR, transA=True)     # m x n x b

@@ -220,17 +220,30 @@ __global__ __launch_bounds__(HV_THREADS) void hvi_bwd_tiled(int b, int nchunk, i
   }
 }
 
-// acq[c] = (1/S) sum_s sum_chunk work[s][chunk][c]   (fixed order)
-__global__ void hvi_reduce_fwd(int S, int nchunk, int b, const double* __restrict__ work, double* __restrict__ acq) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= b) return;
-  double tot = 0.0;
-  for (int s = 0; s < S; ++s) {
-    double ps = 0.0;
-    for (int k = 0; k < nchunk; ++k) ps += work[((size_t)s * nchunk + k) * b + c];
-    tot += ps;
+// acq[c] = (1/S) sum_{s, chunk} work[s][chunk][c] — block of 16 candidates x 16 partial
+// groups, fixed-order tree over the groups (bitwise reproducible).  A candidate whose
+// new-point Cholesky block failed (flags[j][c] != 0 for some j) gets NaN.
+__global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, int m, const double* __restrict__ work,
+                                                      const int* __restrict__ flags, double* __restrict__ acq) {
+  __shared__ double red[16][17];
+  const int cx = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
+  const int tot = S * nchunk;
+  double sum = 0.0;
+  if (c < b)
+    for (int k = g; k < tot; k += 16) sum += work[(size_t)k * b + c];
+  red[g][cx] = sum;
+  __syncthreads();
+  for (int o = 8; o > 0; o >>= 1) {
+    if (g < o) red[g][cx] += red[g + o][cx];
+    __syncthreads();
   }
-  acq[c] = tot / (double)S;
+  if (g == 0 && c < b) {
+    bool bad = false;
+    if (flags)
+      for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + c] != 0;
+    acq[c] = bad ? nan("") : red[0][cx] / (double)S;
+  }
 }
 
 // dG[s][j][c] = gout[c]/S * sum_chunk work[s][chunk][j][c]
@@ -243,7 +256,7 @@ __global__ void hvi_reduce_bwd(int S, int nchunk, int M, int b, const double* __
   const int s = (int)(e / ((long long)b * M));
   double sum = 0.0;
   for (int k = 0; k < nchunk; ++k) sum += work[(((size_t)s * nchunk + k) * M + j) * b + c];
-  dG[e] = gout[c] / (double)S * sum;
+  dG[e] = (gout ? gout[c] : 1.0) / (double)S * sum;
 }
 
 struct HviPlan {
@@ -294,7 +307,8 @@ long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backw
   return (long long)st->S * p.nchunk * b * (backward ? st->m : 1);
 }
 
-int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* work, double* acq) {
+int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const int* flags,
+                    double* work, double* acq) {
   EVR_CHECK(st && st->S >= 1 && work && acq, "evr_hvi_forward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -310,14 +324,14 @@ int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const doubl
   EVR_M_SWITCH(st->m, L);
 #undef L
   EVR_LAUNCH_CHECK();
-  hvi_reduce_fwd<<<cdiv(b, 256), 256, 0, s>>>(st->S, p.nchunk, b, work, acq);
+  hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, p.nchunk, b, st->m, work, flags, acq);
   EVR_LAUNCH_CHECK();
   return 0;
 }
 
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
                      double* work, double* dG) {
-  EVR_CHECK(st && st->S >= 1 && work && dG && gout, "evr_hvi_backward: bad arguments");
+  EVR_CHECK(st && st->S >= 1 && work && dG, "evr_hvi_backward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   HviPlan p = hvi_plan(st, b);

@@ -25,41 +25,57 @@ namespace evr {
 // ---------------------------------------------------------------------------------------
 constexpr int GT = 64, GK = 16, GPAD = 16;
 
+// Split-K: blockIdx.z = batch member * ksplit + k-slice.  With ksplit > 1 the raw partial
+// products go to W[(slice * batch + member) * M * N] and gemm_splitk_reduce applies
+// alpha / beta in a fixed slice order (deterministic).  Global loads of k-step t+1 are
+// issued into registers before the MFMAs of step t (latency hiding for the narrow-N,
+// long-K shapes of the posterior / qNEHVI operator products).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, double alpha,
                                                        const double* __restrict__ A, int lda, long long sA,
                                                        const double* __restrict__ B, int ldb, long long sB,
                                                        double beta, double* __restrict__ C, int ldc, long long sC,
-                                                       int lower_only, const int* __restrict__ skip) {
-  if (skip && skip[blockIdx.z]) return;  // batch member already failed (Cholesky ladder)
+                                                       int lower_only, const int* __restrict__ skip, int ksplit,
+                                                       int kchunk, double* __restrict__ W) {
+  const int bz = blockIdx.z / ksplit, kz = blockIdx.z - bz * ksplit;
+  if (skip && skip[bz]) return;  // batch member already failed (Cholesky ladder)
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
   if (lower_only && n0 > m0 + GT - 1) return;  // tile strictly above the diagonal
-  A += blockIdx.z * sA;
-  B += blockIdx.z * sB;
-  C += blockIdx.z * sC;
+  A += bz * sA;
+  B += bz * sB;
+  const int kbeg = kz * kchunk, kend = min(K, kbeg + kchunk);
   __shared__ double As[GK][GT + GPAD];
   __shared__ double Bs[GK][GT + GPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   double4_t acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-  for (int k0 = 0; k0 < K; k0 += GK) {
+  // per-thread staging coordinates (4 elements of A and of B per k-step)
+  int am[4], ak[4], bn[4], bk[4];
 #pragma unroll
-    for (int e0 = 0; e0 < GT * GK; e0 += 256) {
-      const int e = e0 + tid;
-      int mm, kk;
-      if (!TA) { kk = e & 15; mm = e >> 4; } else { mm = e & 63; kk = e >> 6; }
-      const int gm = m0 + mm, gk = k0 + kk;
-      double v = 0.0;
-      if (gm < M && gk < K) v = TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
-      As[kk][mm] = v;
-      int nn;
-      if (!TB) { nn = e & 63; kk = e >> 6; } else { kk = e & 15; nn = e >> 4; }
-      const int gn = n0 + nn, gk2 = k0 + kk;
-      double w = 0.0;
-      if (gn < N && gk2 < K) w = TB ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn];
-      Bs[kk][nn] = w;
+  for (int u = 0; u < 4; ++u) {
+    const int e = u * 256 + tid;
+    if (!TA) { ak[u] = e & 15; am[u] = e >> 4; } else { am[u] = e & 63; ak[u] = e >> 6; }
+    if (!TB) { bn[u] = e & 63; bk[u] = e >> 6; } else { bk[u] = e & 15; bn[u] = e >> 4; }
+  }
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gm = m0 + am[u], gk = k0 + ak[u];
+      ra[u] = (gm < M && gk < kend) ? (TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.0;
+      const int gn = n0 + bn[u], gk2 = k0 + bk[u];
+      rb[u] = (gn < N && gk2 < kend) ? (TB ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn]) : 0.0;
+    }
+  };
+  if (kbeg < kend) fetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += GK) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      As[ak[u]][am[u]] = ra[u];
+      Bs[bk[u]][bn[u]] = rb[u];
     }
     __syncthreads();
+    if (k0 + GK < kend) fetch(k0 + GK);
     const int i = lane & 15, kq = lane >> 4;
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
@@ -73,14 +89,20 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, doub
     __syncthreads();
   }
   const int col = lane & 15, rq = lane >> 4;
+  double* Cb = C + bz * sC;
+  double* Wb = W ? W + ((size_t)kz * (gridDim.z / ksplit) + bz) * (size_t)M * N : nullptr;
   auto store = [&](const double4_t& acc, int mi, int ni) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm + mi * 16 + rq + 4 * r;
       const int cc = n0 + wn + ni * 16 + col;
       if (row < M && cc < N && (!lower_only || cc <= row)) {
-        double* p = C + (size_t)row * ldc + cc;
-        *p = alpha * acc[r] + (beta == 0.0 ? 0.0 : beta * (*p));
+        if (Wb) {
+          Wb[(size_t)row * N + cc] = acc[r];
+        } else {
+          double* p = Cb + (size_t)row * ldc + cc;
+          *p = alpha * acc[r] + (beta == 0.0 ? 0.0 : beta * (*p));
+        }
       }
     }
   };
@@ -88,6 +110,20 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(int M, int N, int K, doub
   store(acc01, 0, 1);
   store(acc10, 1, 0);
   store(acc11, 1, 1);
+}
+
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(int M, int N, int batch, int ksplit, double alpha,
+                                                          const double* __restrict__ W, double beta,
+                                                          double* __restrict__ C, int ldc, long long sC) {
+  const long long mn = (long long)M * N;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= mn) return;
+  const int bz = blockIdx.y;
+  double acc = 0.0;
+  for (int kz = 0; kz < ksplit; ++kz) acc += W[((size_t)kz * batch + bz) * mn + e];
+  const int row = (int)(e / N), cc = (int)(e - (long long)row * N);
+  double* p = C + bz * sC + (size_t)row * ldc + cc;
+  *p = alpha * acc + (beta == 0.0 ? 0.0 : beta * (*p));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -333,18 +369,36 @@ using namespace evr;
 
 int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alpha, const double* A, int lda,
                 long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
-                int batch, int lower_only = 0, const int* skip = nullptr) {
+                int batch, int lower_only = 0, const int* skip = nullptr, bool allow_split = false) {
   if (M == 0 || N == 0) return 0;
-  dim3 grid(cdiv(N, GT), cdiv(M, GT), batch);
+  const int tiles = cdiv(N, GT) * cdiv(M, GT) * batch;
+  // Split K when the tile grid cannot fill the 256 CUs and each slice keeps >= 8 k-steps
+  // (only for non-aliased outputs: the Cholesky panel update runs in place).
+  int ksplit = 1;
+  if (allow_split && !lower_only && !skip && tiles < 512) {
+    ksplit = std::min(cdiv(1024, tiles), K / (8 * GK));
+    ksplit = std::max(1, std::min(ksplit, 32));
+  }
+  const int kchunk = ksplit > 1 ? cdiv(cdiv(K, ksplit), GK) * GK : std::max(K, 1);
+  if (ksplit > 1) ksplit = cdiv(K, kchunk);
+  double* W = nullptr;
+  if (ksplit > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ksplit * batch * M * N, s));
+  dim3 grid(cdiv(N, GT), cdiv(M, GT), batch * ksplit);
 #define G_(TA_, TB_)                                                                                       \
   gemm_f64_kernel<TA_, TB_><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
-                                                 lower_only, skip)
+                                                 lower_only, skip, ksplit, kchunk, W)
   if (!tA && !tB) G_(false, false);
   else if (!tA && tB) G_(false, true);
   else if (tA && !tB) G_(true, false);
   else G_(true, true);
 #undef G_
   EVR_LAUNCH_CHECK();
+  if (ksplit > 1) {
+    dim3 g2(cdiv((long long)M * N, 256), batch);
+    gemm_splitk_reduce<<<g2, 256, 0, s>>>(M, N, batch, ksplit, alpha, W, beta, C, ldc, sC);
+    EVR_LAUNCH_CHECK();
+    EVR_HIP(hipFreeAsync(W, s));
+  }
   return 0;
 }
 
@@ -434,10 +488,10 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
     if (info_out) EVR_HIP(hipMemcpyAsync(info_out, info_d, sizeof(int) * batch, hipMemcpyDeviceToDevice, s));
   }
   EVR_HIP(hipStreamSynchronize(s));  // host vectors above must outlive the async copies
-  hipFreeAsync(Dinv, s);
-  if (T) hipFreeAsync(T, s);
-  hipFreeAsync(jit_d, s);
-  hipFreeAsync(info_d, s);
+  (void)hipFreeAsync(Dinv, s);
+  if (T) (void)hipFreeAsync(T, s);
+  (void)hipFreeAsync(jit_d, s);
+  (void)hipFreeAsync(info_d, s);
   return rc;
 }
 }  // namespace
@@ -451,8 +505,9 @@ int evr_gemm_f64(void* stream, int transA, int transB, int M, int N, int K, doub
                  int ldc, long long strideC, int batch) {
   EVR_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "evr_gemm_f64: bad sizes M=%d N=%d K=%d batch=%d", M, N,
             K, batch);
+  const bool alias = C == A || C == B;
   return launch_gemm((hipStream_t)stream, transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb, strideB, beta, C,
-                     ldc, strideC, batch);
+                     ldc, strideC, batch, 0, nullptr, !alias);
 }
 
 int evr_cholesky(void* stream, int batch, int n, const double* A, int lda, long long strideA, double* L, int ldl,
@@ -502,8 +557,8 @@ int evr_tri_inv_lower(void* stream, int batch, int n, const double* L, int ldl, 
     rc = 1;
   }
   if (!rc) rc = tri_inv_blocked(s, batch, n, L, ldl, strideL, Dinv, Linv, ldi, strideI, T, nullptr);
-  hipFreeAsync(Dinv, s);
-  hipFreeAsync(T, s);
+  (void)hipFreeAsync(Dinv, s);
+  (void)hipFreeAsync(T, s);
   return rc;
 }
 

@@ -268,11 +268,13 @@ def _hvi_work(st: EvrQnehviState, b: int, backward: bool, device) -> torch.Tenso
     return torch.empty(max(1, n), dtype=torch.float64, device=device)
 
 
-def hvi_forward(st: EvrQnehviState, G: torch.Tensor, b: int) -> torch.Tensor:
-    """acq[c] = mean_s HVI_s (register-tiled scan + deterministic reduction)."""
+def hvi_forward(st: EvrQnehviState, G: torch.Tensor, b: int, flags: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """acq[c] = mean_s HVI_s (register-tiled scan + deterministic reduction); NaN where
+    ``flags`` (m x b int32 from qnehvi_samples) marks a failed new-point Cholesky."""
     acq = torch.empty(b, dtype=torch.float64, device=G.device)
     work = _hvi_work(st, b, False, G.device)
-    call("evr_hvi_forward", _stream(), ctypes.byref(st), b, G.data_ptr(), work.data_ptr(), acq.data_ptr())
+    call("evr_hvi_forward", _stream(), ctypes.byref(st), b, G.data_ptr(), _p(flags), work.data_ptr(),
+         acq.data_ptr())
     return acq
 
 
@@ -283,11 +285,13 @@ def mean_over_samples(partial: torch.Tensor):
     return acq
 
 
-def hvi_backward(st: EvrQnehviState, G: torch.Tensor, gout: torch.Tensor, b: int):
+def hvi_backward(st: EvrQnehviState, G: torch.Tensor, gout: Optional[torch.Tensor], b: int):
+    """dG = gout/S * dHVI/dG (gout None = ones)."""
     dG = torch.empty_like(G)
-    gout = _dev(gout, "gout")
+    if gout is not None:
+        gout = _dev(gout, "gout")
     work = _hvi_work(st, b, True, G.device)
-    call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), gout.data_ptr(), work.data_ptr(),
+    call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), _p(gout), work.data_ptr(),
          dG.data_ptr())
     return dG
 

@@ -169,6 +169,17 @@ def _scipy_constraints(ineq, eq, nb: int, d: int):
     return cons
 
 
+def host_values(t: torch.Tensor) -> np.ndarray:
+    """Device acquisition values -> host; NaN marks a candidate whose posterior block was
+    not p.d. after the jitter ladder (QNEHVI.forward) and raises NotPSDError like the
+    reference.  Every rank sees the same gathered NaN, so all ranks raise together."""
+    v = t.cpu().numpy()
+    if np.isnan(v).any():
+        from .ops import NotPSDError
+        raise NotPSDError("acquisition: posterior covariance block not p.d. after the jitter ladder")
+    return v
+
+
 def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int, options: dict,
                   gen: torch.Generator, inequality_constraints: Sequence[LinearConstraint] = (),
                   equality_constraints: Sequence[LinearConstraint] = (), dist=None,
@@ -206,7 +217,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         Y_raw = torch.cat(bufs)[:raw_samples]
     else:
         Y_raw = acqf.forward(Xr)
-    Y_raw = Y_raw.cpu().numpy()
+    Y_raw = host_values(Y_raw)
     stats.raw_evals += raw_samples
     stats.t_raw += time.perf_counter() - t0
 
@@ -229,8 +240,8 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             Xt = torch.as_tensor(X, dtype=torch.float64, device=dev)
             if with_grad:
                 a, g = acqf.forward_backward(Xt)
-                return a.cpu().numpy(), g.cpu().numpy()
-            return acqf.forward(Xt).cpu().numpy(), None
+                return host_values(a), g.cpu().numpy()
+            return host_values(acqf.forward(Xt)), None
         per = math.ceil(nb / world)
         i0, i1 = min(nb, rank * per), min(nb, (rank + 1) * per)
         loc = torch.zeros(per, 1 + d, dtype=torch.float64, device=dev)
@@ -245,6 +256,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         bufs = [torch.empty_like(loc) for _ in range(world)]
         dist.all_gather(bufs, loc)
         full = torch.cat(bufs)[:nb].cpu().numpy()
+        host_values(torch.from_numpy(full[:, 0]))
         return full[:, 0], (full[:, 1:] if with_grad else None)
 
     # Independent chunks (batch_limit < num_restarts) are separate scipy problems in the
@@ -263,7 +275,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             if local_world == 1:
                 Xt = torch.as_tensor(x.reshape(nb, d), dtype=torch.float64, device=dev)
                 a, g = acqf.forward_backward(Xt)
-                a, g = a.cpu().numpy(), g.cpu().numpy()
+                a, g = host_values(a), g.cpu().numpy()
             else:
                 a, g = evaluate(x.reshape(nb, d), True)
             counter["n"] += 1
@@ -276,7 +288,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
                        options={"maxiter": maxiter})
         Xc = np.clip(res.x.reshape(nb, d), bounds[0], bounds[1])
         if local_world == 1:
-            vals = acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)).cpu().numpy()
+            vals = host_values(acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)))
         else:
             vals, _ = evaluate(Xc, False)
         stats.opt_evals += counter["n"] * nb + nb

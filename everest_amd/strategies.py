@@ -20,7 +20,7 @@ import torch
 from . import data_models as dm
 from .acquisition import QNEHVI, QEI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
-from .optim import OptimizeStats, hit_and_run, optimize_acqf
+from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf
 from .surrogates import BotorchSurrogates, device
 
 
@@ -307,7 +307,7 @@ class BotorchStrategy(PredictiveStrategy):
         if combined:
             raise NotImplementedError("combined (q>1) acquisition values are out of scope (q = 1 kernels)")
         X = torch.as_tensor(self._transform(candidates), dtype=torch.float64, device=self.model.device)
-        return acqf.forward(X).cpu().numpy()
+        return host_values(acqf.forward(X))
 
     def _bounds(self) -> np.ndarray:
         lo, hi = self.domain.inputs.get_bounds(specs=self.input_preprocessing_specs)

@@ -133,12 +133,13 @@ int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const do
 /* Workspace (doubles) the HVI scan needs for b candidates (per-(sample, cell-chunk) partials). */
 long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backward);
 /* acq[c] = mean_s HVI_s(G[s][:, c]) over the cells of sample s (register-tiled cell x
- * candidate scan, deterministic two-stage reduction). */
+ * candidate scan, deterministic two-stage reduction); acq[c] = NaN where flags (m x b,
+ * from evr_qnehvi_samples, nullable) report a failed new-point Cholesky block. */
 int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
-                    double* work, double* acq);
+                    const int* flags, double* work, double* acq);
 /* acq[c] = mean_s partial[s][c] */
 int evr_mean_over_samples(void* stream, int S, int b, const double* partial, double* acq);
-/* dG[s][j][c] = gout[c]/S * dHVI_s/dg_j (torch min/clamp_min/prod subgradients) */
+/* dG[s][j][c] = gout[c]/S * dHVI_s/dg_j (torch min/clamp_min/prod subgradients; gout NULL = 1) */
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
                      const double* gout, double* work, double* dG);
 /* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
