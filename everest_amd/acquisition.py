@@ -32,19 +32,10 @@ from . import ops
 from .gp import GPBatch
 
 
-def draw_sobol_normal_samples(d: int, n: int, seed: int, device=None) -> torch.Tensor:
-    """Scrambled Sobol -> inverse normal CDF ([upstream] draw_sobol_normal_samples with
-    NormalQMCEngine(inv_transform=True)).  Input generation only (host, as in BoTorch)."""
-    eng = torch.quasirandom.SobolEngine(dimension=d, scramble=True, seed=int(seed))
-    u = eng.draw(n, dtype=torch.float64)
-    v = 0.5 + (1 - torch.finfo(u.dtype).eps) * (u - 0.5)
-    z = torch.erfinv(2 * v - 1) * math.sqrt(2)
-    return z if device is None else z.to(device)
-
-
-def sobol_base_samples(S: int, n_points: int, m: int, seed: int) -> torch.Tensor:
-    """S x n_points x m (Sobol dim index = point*m + output)."""
-    return draw_sobol_normal_samples(n_points * m, S, seed).view(S, n_points, m)
+def sobol_base_samples(S: int, n_points: int, m: int, seed: int, device) -> torch.Tensor:
+    """Device Sobol-normal base samples in the GEMM-ready layout m x n_points x S
+    ([upstream] draw_sobol_normal_samples(n_points*m, S, seed), Sobol dim = point*m + output)."""
+    return ops.sobol_normal(S, n_points * m, seed, device, layout=1, m=m)
 
 
 def _host_threads() -> int:
@@ -118,8 +109,9 @@ class QNEHVI:
             nc = cand.shape[0]
             Lp, _, _ = ops.cholesky(Sig_c, 1e-8, 3)
             if z_prune is None:
-                z_prune = sobol_base_samples(prune_samples, nc, m, prune_seed)
-            Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()             # m x nc x S'
+                Zp = sobol_base_samples(prune_samples, nc, m, prune_seed, dev)   # m x nc x S'
+            else:
+                Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()
             Yp = ops.gemm(Lp, Zp)
             Op = ops.objective_affine(Yp, mu_c, self.obj_a, self.obj_b)
             _, counts = ops.pareto_mask(Op, self.ref, dedup=False, want_mask=False, want_counts=True)
@@ -143,13 +135,16 @@ class QNEHVI:
             self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
         S_ = self.S
-        if z_base_full is None:
-            z_base_full = sobol_base_samples(S_, nb, m, sampler_seed)          # S x nb x m
+        # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed
         if z_new_full is None:
-            z_new_full = sobol_base_samples(S_, nb + 1, m, sampler_seed)       # S x (nb+1) x m
-        self.zq = z_new_full[:, nb, :].to(**f64).contiguous()                 # S x m
+            self.zq = ops.sobol_normal(S_, (nb + 1) * m, sampler_seed, dev, d0=nb * m, nd=m)   # S x m
+        else:
+            self.zq = z_new_full[:, nb, :].to(**f64).contiguous()
         if nb > 0:
-            Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()            # m x nb x S
+            if z_base_full is None:
+                Zb = sobol_base_samples(S_, nb, m, sampler_seed, dev)                # m x nb x S
+            else:
+                Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
             Yb = ops.gemm(self.L_base, Zb)
             Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
             mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
@@ -241,7 +236,7 @@ class QEI:
         mean, _ = gp.posterior(Xt)
         self.best_f = float((self.a * mean[0] + self.b).max().item())
         if z is None:
-            z = draw_sobol_normal_samples(1, S, seed)
+            z = ops.sobol_normal(S, 1, seed, self.dev)
         self.z = z.reshape(-1).to(device=self.dev, dtype=torch.float64).contiguous()
         h = gp.hypers[0]
         self._scal = (h.constant, h.y_mean, h.y_std, 1.0)

@@ -353,6 +353,44 @@ def add_selection(E: torch.Tensor, idx: torch.Tensor, val: Optional[torch.Tensor
     return E
 
 
+_SOBOL_DIRECTIONS = {}
+
+
+def _sobol_directions(dim: int) -> torch.Tensor:
+    """Unscrambled 30-bit direction numbers of torch's SobolEngine (Joe-Kuo D(6) table as
+    torch ships it), cached per dimension; scrambled per seed by evr_sobol_scramble."""
+    V = _SOBOL_DIRECTIONS.get(dim)
+    if V is None:
+        V = torch.zeros(dim, 30, dtype=torch.long)
+        torch._sobol_engine_initialize_state_(V, dim)
+        if len(_SOBOL_DIRECTIONS) > 16:
+            _SOBOL_DIRECTIONS.clear()
+        _SOBOL_DIRECTIONS[dim] = V
+    return V
+
+
+def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[int] = None,
+                 layout: int = 0, m: int = 1) -> torch.Tensor:
+    """Device draw_sobol_normal_samples(dim, n, seed) restricted to dims [d0, d0+nd).
+
+    layout 0 -> n x nd; layout 1 -> m x (nd/m) x n (sample index fastest, the GEMM-ready
+    layout of the baseline / prune samples: dim t = point*m + output)."""
+    nd = dim - d0 if nd is None else nd
+    if not (0 <= d0 and d0 + nd <= dim):
+        raise ValueError("sobol_normal: dims out of range")
+    V = _sobol_directions(dim).clone()
+    shift = torch.empty(dim, dtype=torch.long)
+    call("evr_sobol_scramble", dim, int(seed), V.data_ptr(), shift.data_ptr())
+    Vd = V.to(device, non_blocking=False)
+    sd = shift.to(device)
+    if layout == 0:
+        out = torch.empty(n, nd, dtype=torch.float64, device=device)
+    else:
+        out = torch.empty(m, nd // m, n, dtype=torch.float64, device=device)
+    call("evr_sobol_normal", _stream(), n, nd, d0, Vd.data_ptr(), sd.data_ptr(), layout, m, out.data_ptr())
+    return out
+
+
 def box_decompose(obj: np.ndarray, ref: np.ndarray, mask: Optional[np.ndarray] = None, num_threads: int = 0,
                   layout: str = "jis"):
     """Host box decomposition.  obj: float64 numpy array, layout 'jis' (m x n x S) or 'sij'

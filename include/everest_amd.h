@@ -185,6 +185,18 @@ long long evr_cells_total(const evr_cells* c);
 int evr_cells_copy(const evr_cells* c, double* lo, double* hi, int* off);
 void evr_cells_free(evr_cells* c);
 
+/* ---- quasi-MC base samples -------------------------------------------------------------
+ * Replaces [upstream] draw_sobol_normal_samples / torch.quasirandom.SobolEngine(scramble=True)
+ * as called by the qNEHVI samplers (bofire/strategies/predictives/qnehvi.py:39-52, seed from
+ * the strategy RNG bofire/strategies/predictives/botorch.py:86).
+ * evr_sobol_scramble (host): V (dim x 30 int64, in/out) holds the unscrambled direction
+ * numbers and receives SobolEngine(dim, scramble=True, seed).sobolstate; shift (dim) receives
+ * .shift.  evr_sobol_normal (device): normal samples of points 0..n-1, dims [d0, d0+nd):
+ * layout 0 -> out[k*nd + t]; layout 1 -> out[(o*np + p)*n + k] with t = p*m + o, np = nd/m. */
+int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long* shift);
+int evr_sobol_normal(void* stream, int n, int nd, int d0, const long long* V, const long long* shift,
+                     int layout, int m, double* out);
+
 #ifdef __cplusplus
 }
 #endif

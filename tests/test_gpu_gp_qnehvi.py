@@ -110,3 +110,45 @@ def test_qnehvi_large_batch_consistency():
     assert (full >= 0).all()
     again = dq.forward(Xc)
     assert torch.equal(full, again)              # bitwise reproducible for a fixed batch
+
+
+@pytest.mark.parametrize("dim,n,seed", [(1, 512, 3), (15, 257, 42), (2560, 2048, 987)])
+def test_device_sobol_normal_matches_engine(dim, n, seed):
+    """Device Sobol-normal samples vs torch SobolEngine + erfinv on the host (the oracle's
+    draw): same scrambled points, erfinv agreeing to a few ulp (glibc vs device erf/exp)."""
+    from everest_amd import ops
+
+    ref = oq.draw_sobol_normal_samples(dim, n, seed)                    # n x dim
+    z = ops.sobol_normal(n, dim, seed, "cuda").cpu()
+    assert z.shape == ref.shape
+    # erfinv's condition number grows like exp(z^2/2) in the tails: an ulp of erf() in the
+    # Newton steps moves z by ~1e-16 * exp(z^2/2); scale the tolerance accordingly.
+    err = (z - ref).abs() / (1.0 + torch.exp(ref * ref / 2))
+    assert err.max() < 1e-13, (err.max().item(), (z - ref).abs().max().item())
+    assert (z == ref).double().mean() > 0.5, (z == ref).double().mean().item()
+    if dim % 5 == 0:                                                      # m x points x n layout
+        m = 5
+        z1 = ops.sobol_normal(n, dim, seed, "cuda", layout=1, m=m).cpu()
+        assert torch.equal(z1, z.view(n, dim // m, m).permute(2, 1, 0))
+    zt = ops.sobol_normal(n, dim, seed, "cuda", d0=dim - 1, nd=1).cpu()   # tail dims only
+    assert torch.equal(zt[:, 0], z[:, -1])
+
+
+def test_qnehvi_device_samples_match_host_samples():
+    """QNEHVI drawing its own (device) base samples equals the build fed the oracle's host
+    draws: same pruned baseline, acquisition values to 1e-10."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 60, 6, 5, 32
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=8)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(m), np.zeros(m), -1.1 * np.ones(m)
+    auto = QNEHVI(gp, X, X, ref, a, b, S=S, sampler_seed=7, prune_baseline=True, prune_seed=11, prune_samples=256)
+    nc = n
+    zp = oq.base_samples(256, nc, m, 11)
+    nb = auto.nb
+    host = QNEHVI(gp, X, X, ref, a, b, S=S, prune_baseline=True, prune_samples=256, z_prune=zp,
+                  z_base_full=oq.base_samples(S, nb, m, 7), z_new_full=oq.base_samples(S, nb + 1, m, 7))
+    assert np.array_equal(auto.base_rows, host.base_rows)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(64, d)), device="cuda")
+    assert torch.allclose(auto.forward(Xc), host.forward(Xc), rtol=1e-10, atol=1e-13)

@@ -76,3 +76,41 @@ def test_device_ops_refuse_cpu_tensors():
         ops.kernel_matrix(X, X, torch.ones(1, 2, dtype=torch.float64))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.cholesky(torch.eye(3, dtype=torch.float64))
+
+
+@pytest.mark.parametrize("dim,seed", [(1, 0), (5, 17), (64, 123456), (2561, 987654)])
+def test_sobol_scramble_matches_torch_engine(dim, seed):
+    """evr_sobol_scramble reproduces SobolEngine(dim, scramble=True, seed) state bit for bit
+    (mt19937 stream of torch.Generator.manual_seed, LMS matrices, random shift)."""
+    from everest_amd import _native
+
+    V = torch.zeros(dim, 30, dtype=torch.long)
+    torch._sobol_engine_initialize_state_(V, dim)
+    shift = torch.empty(dim, dtype=torch.long)
+    assert _native.load().evr_sobol_scramble(dim, seed, V.data_ptr(), shift.data_ptr()) == 0
+    eng = torch.quasirandom.SobolEngine(dim, scramble=True, seed=seed)
+    assert torch.equal(V, eng.sobolstate)
+    assert torch.equal(shift, eng.shift)
+
+
+def test_sobol_gray_code_closed_form_matches_engine():
+    """Point k = shift ^ XOR_{bits of gray(k)} V (the device kernel's indexing) equals the
+    engine's sequential draw; point 0 goes through float32 like SobolEngine._first_point."""
+    dim, n = 7, 300
+    eng = torch.quasirandom.SobolEngine(dim, scramble=True, seed=31)
+    u = eng.draw(n, dtype=torch.float64)
+    V, sh = eng.sobolstate, eng.shift
+    for k in (0, 1, 2, 3, 5, 127, 128, 255, 299):
+        x = sh.clone()
+        if k == 0:
+            ref = sh.to(torch.float32).to(torch.float64) / 2 ** 30
+        else:
+            g = k ^ (k >> 1)
+            b = 0
+            while g:
+                if g & 1:
+                    x ^= V[:, b]
+                g >>= 1
+                b += 1
+            ref = x.to(torch.float64) / 2 ** 30
+        assert torch.equal(u[k], ref), k

@@ -74,8 +74,6 @@ def test_sobol_normal_samples_pinned():
     z2 = oq.draw_sobol_normal_samples(6, 4, seed=123)
     assert torch.equal(z, z2) and z.shape == (4, 6)
     assert abs(z.mean().item()) < 1.5
-    from everest_amd.acquisition import draw_sobol_normal_samples as prod_draw
-    assert torch.equal(prod_draw(6, 4, 123), z)
 
 
 def test_qnehvi_oracle_hvi_equals_hv_difference():
