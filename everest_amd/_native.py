@@ -76,6 +76,12 @@ _SIGS = {
     "evr_cells_total": ([c_void_p], c_longlong),
     "evr_cells_copy": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "evr_cells_free": ([c_void_p], None),
+    "evr_box_device_limits": ([c_int, c_int, c_void_p, c_void_p], c_int),
+    "evr_box_device_workspace_bytes": ([c_int, c_int, c_int, c_int], c_longlong),
+    "evr_box_decompose_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                  c_void_p], c_int),
+    "evr_box_pack_device": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+                            c_int),
     "evr_sobol_scramble": ([c_int, ctypes.c_ulonglong, c_void_p, c_void_p], c_int),
     "evr_sobol_normal": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
 }

@@ -67,7 +67,7 @@ class QNEHVI:
                  S: int = 512, sampler_seed: int = 0, prune_baseline: bool = True, prune_seed: int = 0,
                  prune_samples: int = 2048, max_frac: float = 1.0, z_prune: Optional[torch.Tensor] = None,
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
-                 num_threads: Optional[int] = None):
+                 num_threads: Optional[int] = None, box_device: Optional[bool] = None):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -147,22 +147,30 @@ class QNEHVI:
                 Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
             Yb = ops.gemm(self.L_base, Zb)
             Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
-            mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
-            Ob_h, mask_h = Ob.cpu().numpy(), mask.cpu().numpy()
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
             t1 = _time.perf_counter()
-            lo, hi, off = ops.box_decompose(Ob_h, self.ref.cpu().numpy(), mask_h,
-                                            num_threads or _host_threads(), layout="jis")
+            if box_device if box_device is not None else ops.box_device_supported(nb, m):
+                lo, hi, off_d, counts_c = ops.box_decompose_device(Ob, self.ref)
+                self.box_path = "device"
+            else:  # beyond the device kernel's LDS / key-width limits: native host partition
+                mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
+                lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),
+                                                num_threads or _host_threads(), layout="jis")
+                lo, hi = torch.as_tensor(lo, **f64), torch.as_tensor(hi, **f64)
+                off_d = torch.as_tensor(off, dtype=torch.int32, device=dev)
+                counts_c = np.diff(off)
+                self.box_path = "host"
             tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
-            lo = np.tile(self.ref.cpu().numpy(), (S_, 1))
-            hi = np.full((S_, m), np.inf)
-            off = np.arange(S_ + 1, dtype=np.int32)
-        self.cell_lo = torch.as_tensor(lo, **f64).contiguous()
-        self.cell_hi = torch.as_tensor(hi, **f64).contiguous()
-        self.cell_off = torch.as_tensor(off, dtype=torch.int32, device=dev).contiguous()
-        counts_c = np.diff(off)
-        self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(off[-1]),
+            lo = self.ref.unsqueeze(0).repeat(S_, 1)
+            hi = torch.full((S_, m), math.inf, **f64)
+            off_d = torch.arange(S_ + 1, dtype=torch.int32, device=dev)
+            counts_c = np.ones(S_, dtype=np.int64)
+            self.box_path = "none"
+        self.cell_lo = lo.contiguous()
+        self.cell_hi = hi.contiguous()
+        self.cell_off = off_d.contiguous()
+        self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(np.sum(counts_c)),
                                        max_cells=int(counts_c.max()) if len(counts_c) else 0, prune_probs=probs)
 
         # ---- forward operator M = [Linv; G; H^T; alpha^T] ------------------------------

@@ -1,0 +1,418 @@
+// Exact box decomposition of the non-dominated region on the device, one workgroup per
+// Monte-Carlo sample (S = 256..512 samples fill the 256 CUs).
+//
+// Same mathematics as box_decomposition.cpp (the host restatement of [upstream] BoTorch
+// FastNondominatedPartitioning, alpha = 0, used by BoFire's qNEHVI at
+// bofire/strategies/predictives/qnehvi.py:50): local upper bounds (LUBs) of the
+// minimisation problem on z = -g, incremental update of Lacour, Klamroth & Fonseca (2017)
+// over the sample's Pareto points in index order, one disjoint box per LUB.
+//
+// MI355X-first representation.  A LUB u is fully determined by its defining points
+// Z^k(u), k = 0..m-1 (u_k = Z^k_k(u)), so the whole LUB is ONE 64-bit key of m point
+// indices (12 bits each for m <= 5).  The sample's points live in LDS; the LUB keys in
+// HBM (per-sample slab).  Field 0 holds the rank of Z^0 in descending z_0 order instead of
+// the index, so sorting the keys sorts the cells by their first lower bound — the order
+// the HVI tile-skip test wants — and, keys being unique, the final cell order is
+// deterministic even though the LUB slab is updated with LDS atomics.
+//
+// Per Pareto point z:  (a) scan the slab, collect A = {u : u > z strictly};  (b) for every
+// (u in A, j) test z_j >= max_{k != j} Z^k_j(u) and emit u^j = (z_j, u_-j) with Z^j = z;
+// (c) new keys overwrite A's slots, the rest append (holes are tombstoned and compacted
+// when they pile up).  Then every live LUB's box is tested non-empty and its key emitted;
+// keys are bitonic-sorted (LDS when they fit, else in the HBM slab).  A pack kernel writes
+// [lo, hi] in the HVI kernels' layout from the sorted keys.
+#include <algorithm>
+#include <cmath>
+
+#include "common.hpp"
+#include "../../include/everest_amd.h"
+
+namespace evr {
+
+constexpr int BD_THREADS = 1024;
+constexpr unsigned long long BD_DEAD = ~0ull;
+constexpr int BD_LDS_BYTES = 160 * 1024 - 2048;  // dynamic LDS budget (static counters aside)
+
+__host__ __device__ constexpr int bd_field_bits(int m) { return m <= 4 ? 16 : (m == 5 ? 12 : 64 / m); }
+
+struct BdLayout {
+  // per-sample slabs (elements): lub, buf: cap u64; aidx: cap int; pts: (n+m)*m double; inv0: n+m int
+  long long cap;
+  int n, m;
+  size_t off_lub, off_buf, off_aidx, off_pts, off_inv0, off_nf, bytes;
+};
+
+static BdLayout bd_layout(int S, int n, int m, int cap) {
+  BdLayout L;
+  L.cap = cap;
+  L.n = n;
+  L.m = m;
+  size_t o = 0;
+  auto take = [&](size_t b) {
+    size_t r = o;
+    o += (b + 255) & ~(size_t)255;
+    return r;
+  };
+  L.off_lub = take(sizeof(unsigned long long) * (size_t)S * cap);
+  L.off_buf = take(sizeof(unsigned long long) * (size_t)S * cap);
+  L.off_aidx = take(sizeof(int) * (size_t)S * cap);
+  L.off_pts = take(sizeof(double) * (size_t)S * (n + m) * m);
+  L.off_inv0 = take(sizeof(int) * (size_t)S * (n + m));
+  L.off_nf = take(sizeof(int) * (size_t)S);
+  L.bytes = o;
+  return L;
+}
+
+// LDS bytes for the points (raw + filtered), flags, inverse rank table.
+static size_t bd_lds_fixed(int n, int m) {
+  return sizeof(double) * ((size_t)n * m + (size_t)(n + m) * m) + sizeof(int) * (size_t)(4 * n + 2 * m + 8);
+}
+
+template <int M>
+struct Key {
+  static constexpr int FB = bd_field_bits(M);
+  static constexpr unsigned long long FMASK = (1ull << FB) - 1;
+  __device__ static int field(unsigned long long k, int j) { return (int)((k >> (FB * (M - 1 - j))) & FMASK); }
+  __device__ static unsigned long long set(unsigned long long k, int j, int v) {
+    const int sh = FB * (M - 1 - j);
+    return (k & ~(FMASK << sh)) | ((unsigned long long)v << sh);
+  }
+};
+
+// Bitonic sort (ascending) of P2 keys in `a` (LDS or global), all threads of the block.
+template <typename Ptr>
+__device__ void bd_bitonic(Ptr a, int P2) {
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P2; i += BD_THREADS) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long x = a[i], y = a[l];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int M>
+__global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, const double* __restrict__ obj,
+                                                              const double* __restrict__ ref, int cap, int sortcap,
+                                                              unsigned char* __restrict__ ws, BdLayout Lo,
+                                                              int* __restrict__ counts, int* __restrict__ status) {
+  using K = Key<M>;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  double* raw = (double*)smem;                  // n x M   (min-space, all points)
+  double* pt = raw + (size_t)n * M;             // (n+M) x M filtered points then dummies
+  int* flag = (int*)(pt + (size_t)(n + M) * M); // n
+  int* pos = flag + n;                          // n
+  int* inv0 = pos + n;                          // n + M: point index of rank r
+  int* rank = inv0 + n + M;                     // n + M: rank of point index i
+  unsigned long long* sbuf = (unsigned long long*)(((uintptr_t)(rank + n + M) + 15) & ~(uintptr_t)15);
+  __shared__ int sh_nf, sh_nA, sh_nNew, sh_cnt, sh_err;
+
+  unsigned long long* lub = (unsigned long long*)(ws + Lo.off_lub) + (size_t)s * cap;
+  unsigned long long* buf = (unsigned long long*)(ws + Lo.off_buf) + (size_t)s * cap;
+  int* aidx = (int*)(ws + Lo.off_aidx) + (size_t)s * cap;
+  double* gpts = (double*)(ws + Lo.off_pts) + (size_t)s * (n + M) * M;
+  int* ginv0 = (int*)(ws + Lo.off_inv0) + (size_t)s * (n + M);
+
+  // ---- 1. load, better-than-ref + Pareto filter with dedup (first occurrence kept) --------
+  for (int e = tid; e < n * M; e += BD_THREADS) {
+    const int i = e / M, j = e - i * M;
+    raw[e] = -obj[((size_t)j * n + i) * S + s];
+  }
+  if (tid == 0) sh_err = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += BD_THREADS) {
+    bool keep = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) keep &= raw[i * M + j] < -ref[j];  // g > ref  <=>  z < -ref
+    for (int k = 0; k < n && keep; ++k) {
+      if (k == i) continue;
+      bool cand = true, le = true, lt = false, eq = true;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const double v = raw[k * M + j], w = raw[i * M + j];
+        cand &= v < -ref[j];
+        le &= v <= w;
+        lt |= v < w;
+        eq &= v == w;
+      }
+      if (cand && ((le && lt) || (eq && k < i))) keep = false;
+    }
+    flag[i] = keep ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid == 0) {  // ordered compaction (n is small; one thread keeps index order)
+    int c = 0;
+    for (int i = 0; i < n; ++i) {
+      pos[i] = c;
+      c += flag[i];
+    }
+    sh_nf = c;
+  }
+  __syncthreads();
+  const int nf = sh_nf;
+  for (int e = tid; e < n * M; e += BD_THREADS) {
+    const int i = e / M;
+    if (flag[i]) pt[pos[i] * M + (e - i * M)] = raw[e];
+  }
+  for (int e = tid; e < M * M; e += BD_THREADS) {  // dummies D_k: R_k at k, -inf elsewhere
+    const int k = e / M, j = e - k * M;
+    pt[(nf + k) * M + j] = (j == k) ? -ref[k] : -INFINITY;
+  }
+  __syncthreads();
+  // rank of every point (and D_0) in descending z_0 (ties: index order); inv0[rank] = index
+  for (int i = tid; i <= nf; i += BD_THREADS) {
+    const double v = pt[i * M];
+    int r = 0;
+    for (int k = 0; k <= nf; ++k) {
+      const double w = pt[k * M];
+      r += (w > v) || (w == v && k < i);
+    }
+    inv0[r] = i;
+    rank[i] = r;
+  }
+  __syncthreads();
+
+  // ---- 2. incremental LUB update ------------------------------------------------------
+  int Kend = 1, holes = 0;
+  if (tid == 0) {
+    unsigned long long k0 = 0;
+    k0 = K::set(k0, 0, rank[nf]);  // rank of D_0
+    for (int j = 1; j < M; ++j) k0 = K::set(k0, j, nf + j);
+    lub[0] = k0;
+  }
+  __syncthreads();
+  for (int p = 0; p < nf; ++p) {
+    double z[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) z[j] = pt[p * M + j];
+    if (tid == 0) {
+      sh_nA = 0;
+      sh_nNew = 0;
+    }
+    __syncthreads();
+    // (a) LUBs strictly above z
+    for (int u = tid; u < Kend; u += BD_THREADS) {
+      const unsigned long long key = lub[u];
+      if (key == BD_DEAD) continue;
+      bool dom = pt[inv0[K::field(key, 0)] * M] > z[0];
+#pragma unroll
+      for (int j = 1; j < M; ++j) dom &= pt[K::field(key, j) * M + j] > z[j];
+      if (dom) aidx[atomicAdd(&sh_nA, 1)] = u;
+    }
+    __syncthreads();
+    const int nA = sh_nA;
+    // (b) admissible projections u^j
+    for (int t = tid; t < nA * M; t += BD_THREADS) {
+      const int a = t / M, j = t - a * M;
+      const unsigned long long key = lub[aidx[a]];
+      double zmax = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        if (k == j) continue;
+        const int pk = (k == 0) ? inv0[K::field(key, 0)] : K::field(key, k);
+        zmax = fmax(zmax, pt[pk * M + j]);
+      }
+      if (z[j] >= zmax) {
+        const int slot = atomicAdd(&sh_nNew, 1);
+        if (slot < cap) buf[slot] = K::set(key, j, j == 0 ? rank[p] : p);
+      }
+    }
+    __syncthreads();
+    const int nNew = sh_nNew;
+    if (Kend + (nNew > nA ? nNew - nA : 0) > cap || nNew > cap) {
+      if (tid == 0) sh_err = 1;
+      break;
+    }
+    // (c) overwrite A's slots, append the rest, tombstone the leftovers
+    const int top = nNew > nA ? nNew : nA;
+    for (int i = tid; i < top; i += BD_THREADS) {
+      if (i < nNew) {
+        const int dst = (i < nA) ? aidx[i] : Kend + (i - nA);
+        lub[dst] = buf[i];
+      } else {
+        lub[aidx[i]] = BD_DEAD;
+      }
+    }
+    if (nNew > nA) Kend += nNew - nA;
+    else holes += nA - nNew;
+    __syncthreads();
+    if (holes > 256 && holes * 4 > Kend) {  // compact (order is irrelevant: keys are sorted at the end)
+      if (tid == 0) sh_cnt = 0;
+      __syncthreads();
+      for (int u = tid; u < Kend; u += BD_THREADS) {
+        const unsigned long long key = lub[u];
+        if (key != BD_DEAD) buf[atomicAdd(&sh_cnt, 1)] = key;
+      }
+      __syncthreads();
+      const int cnt = sh_cnt;
+      for (int u = tid; u < cnt; u += BD_THREADS) lub[u] = buf[u];
+      Kend = cnt;
+      holes = 0;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (sh_err) {
+    if (tid == 0) {
+      status[s] = 1;
+      counts[s] = 0;
+    }
+    return;
+  }
+
+  // ---- 3. non-empty boxes -> keys, sorted ---------------------------------------------
+  if (tid == 0) sh_cnt = 0;
+  __syncthreads();
+  for (int u = tid; u < Kend; u += BD_THREADS) {
+    const unsigned long long key = lub[u];
+    if (key == BD_DEAD) continue;
+    int P[M];
+    P[0] = inv0[K::field(key, 0)];
+#pragma unroll
+    for (int j = 1; j < M; ++j) P[j] = K::field(key, j);
+    bool ok = true;
+#pragma unroll
+    for (int j = 1; j < M; ++j) {  // box in min-space: [max_{k<j} Z^k_j, u_j); dim 0 unbounded below
+      double lo = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < j; ++k) lo = fmax(lo, pt[P[k] * M + j]);
+      ok &= pt[P[j] * M + j] > lo;
+    }
+    if (ok) buf[atomicAdd(&sh_cnt, 1)] = key;
+  }
+  __syncthreads();
+  const int C = sh_cnt;
+  int P2 = 1;
+  while (P2 < C) P2 <<= 1;
+  if (P2 <= sortcap) {
+    for (int i = tid; i < P2; i += BD_THREADS) sbuf[i] = (i < C) ? buf[i] : BD_DEAD;
+    __syncthreads();
+    bd_bitonic(sbuf, P2);
+    for (int i = tid; i < C; i += BD_THREADS) buf[i] = sbuf[i];
+  } else {
+    for (int i = C + tid; i < P2; i += BD_THREADS) buf[i] = BD_DEAD;  // P2 <= cap (cap is a power of 2)
+    __syncthreads();
+    bd_bitonic(buf, P2);
+  }
+  // points + decode table for the pack kernel
+  for (int e = tid; e < (nf + M) * M; e += BD_THREADS) gpts[e] = pt[e];
+  for (int r = tid; r <= nf; r += BD_THREADS) ginv0[r] = inv0[r];
+  if (tid == 0) {
+    counts[s] = C;
+    status[s] = 0;
+    ((int*)(ws + Lo.off_nf))[s] = nf;
+  }
+}
+
+// cell c of sample s (off[s] + i): lo_j = -u_j, hi_0 = +inf, hi_j = -max_{k<j} Z^k_j
+template <int M>
+__global__ __launch_bounds__(256) void bd_pack_kernel(int S, int n, int cap, const unsigned char* __restrict__ ws,
+                                                      BdLayout Lo, const int* __restrict__ off,
+                                                      double* __restrict__ lo, double* __restrict__ hi) {
+  using K = Key<M>;
+  const int s = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int c0 = off[s], C = off[s + 1] - c0;
+  if (i >= C) return;
+  const unsigned long long key = ((const unsigned long long*)(ws + Lo.off_buf))[(size_t)s * cap + i];
+  const double* pt = (const double*)(ws + Lo.off_pts) + (size_t)s * (n + M) * M;
+  const int* inv0 = (const int*)(ws + Lo.off_inv0) + (size_t)s * (n + M);
+  int P[M];
+  P[0] = inv0[K::field(key, 0)];
+#pragma unroll
+  for (int j = 1; j < M; ++j) P[j] = K::field(key, j);
+  const size_t o = (size_t)(c0 + i) * M;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    double bl = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < j; ++k) bl = fmax(bl, pt[P[k] * M + j]);
+    lo[o + j] = -pt[P[j] * M + j];
+    hi[o + j] = -bl;
+  }
+}
+
+}  // namespace evr
+
+using namespace evr;
+
+#define EVR_BD_SWITCH(m, MACRO)                                                       \
+  switch (m) {                                                                        \
+    case 1: MACRO(1); break;                                                          \
+    case 2: MACRO(2); break;                                                          \
+    case 3: MACRO(3); break;                                                          \
+    case 4: MACRO(4); break;                                                          \
+    case 5: MACRO(5); break;                                                          \
+    case 6: MACRO(6); break;                                                          \
+    case 7: MACRO(7); break;                                                          \
+    case 8: MACRO(8); break;                                                          \
+    default: EVR_CHECK(false, "box decomposition: m=%d not supported (1..8)", m);     \
+  }
+
+extern "C" {
+
+int evr_box_device_limits(int n, int m, int* max_points_out, long long* lds_bytes_out) {
+  EVR_CHECK(m >= 1 && m <= 8 && n >= 0, "evr_box_device_limits: bad arguments");
+  const long long idx_limit = (1ll << bd_field_bits(m)) - 2 - m;   // field values < 2^FB - 1
+  const size_t fixed = bd_lds_fixed(n, m);
+  if (max_points_out) *max_points_out = (int)std::min<long long>(idx_limit, 1 << 20);
+  if (lds_bytes_out) *lds_bytes_out = (long long)fixed;
+  return (n <= idx_limit && fixed + 16 + 8 * 64 <= (size_t)BD_LDS_BYTES) ? 0 : 3;
+}
+
+long long evr_box_device_workspace_bytes(int S, int n, int m, int cap) {
+  if (S < 1 || n < 0 || m < 1 || cap < 1) return 0;
+  return (long long)bd_layout(S, n, m, cap).bytes;
+}
+
+int evr_box_decompose_device(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
+                             void* work, int* counts, int* status) {
+  EVR_CHECK(S >= 1 && n >= 1 && m >= 1 && m <= 8 && obj && ref && work && counts && status,
+            "evr_box_decompose_device: bad arguments");
+  EVR_CHECK(cap >= 2 && (cap & (cap - 1)) == 0, "evr_box_decompose_device: cap must be a power of two");
+  EVR_CHECK(evr_box_device_limits(n, m, nullptr, nullptr) == 0,
+            "evr_box_decompose_device: n=%d points x m=%d exceed the device limits", n, m);
+  const BdLayout Lo = bd_layout(S, n, m, cap);
+  const size_t fixed = bd_lds_fixed(n, m) + 16;
+  int sortcap = 1;
+  while ((size_t)(sortcap * 2) * 8 + fixed <= (size_t)BD_LDS_BYTES && sortcap * 2 <= cap) sortcap *= 2;
+  const size_t lds = fixed + (size_t)sortcap * 8;
+  hipStream_t s = (hipStream_t)stream;
+#define L(MM)                                                                                           \
+  do {                                                                                                  \
+    EVR_HIP(hipFuncSetAttribute((const void*)bd_build_kernel<MM>,                                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                 \
+    bd_build_kernel<MM><<<S, BD_THREADS, lds, s>>>(S, n, obj, ref, cap, sortcap, (unsigned char*)work, \
+                                                   Lo, counts, status);                                 \
+  } while (0)
+  EVR_BD_SWITCH(m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_box_pack_device(void* stream, int S, int n, int m, int cap, const void* work, const int* off, int max_cells,
+                        double* lo, double* hi) {
+  EVR_CHECK(S >= 1 && n >= 1 && m >= 1 && m <= 8 && work && off && lo && hi, "evr_box_pack_device: bad arguments");
+  if (max_cells <= 0) return 0;
+  const BdLayout Lo = bd_layout(S, n, m, cap);
+  dim3 grid(cdiv(max_cells, 256), S);
+  hipStream_t s = (hipStream_t)stream;
+#define L(MM) bd_pack_kernel<MM><<<grid, 256, 0, s>>>(S, n, cap, (const unsigned char*)work, Lo, off, lo, hi)
+  EVR_BD_SWITCH(m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

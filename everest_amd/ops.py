@@ -353,6 +353,43 @@ def add_selection(E: torch.Tensor, idx: torch.Tensor, val: Optional[torch.Tensor
     return E
 
 
+def box_device_supported(n: int, m: int) -> bool:
+    return _native.load().evr_box_device_limits(int(n), int(m), None, None) == 0
+
+
+def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20):
+    """Device box decomposition of every sample of O (m x n x S objective values) above ref.
+
+    Returns (lo [C x m], hi [C x m], off [S+1] int32 on the device, counts [S] host numpy).
+    One host sync (the per-sample cell counts size the packed arrays and the HVI plan); a
+    sample overflowing ``cap`` LUB slots reruns the batch with 4x the capacity."""
+    O, ref = _dev(O, "O"), _dev(ref, "ref")
+    m, n, S = O.shape
+    dev = O.device
+    while True:
+        nbytes = _native.load().evr_box_device_workspace_bytes(S, n, m, cap)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        cs = torch.empty(2, S, dtype=torch.int32, device=dev)
+        call("evr_box_decompose_device", _stream(), S, n, m, O.data_ptr(), ref.data_ptr(), cap, ws.data_ptr(),
+             cs[0].data_ptr(), cs[1].data_ptr())
+        h = cs.cpu().numpy()
+        if not h[1].any():
+            break
+        if cap >= max_cap:
+            raise RuntimeError(f"box decomposition: more than {max_cap} local upper bounds in one sample")
+        cap *= 4
+    counts = h[0].astype(np.int64)
+    off_h = np.zeros(S + 1, dtype=np.int64)
+    np.cumsum(counts, out=off_h[1:])
+    total = int(off_h[-1])
+    off = torch.as_tensor(off_h.astype(np.int32)).to(dev)
+    lo = torch.empty(total, m, dtype=torch.float64, device=dev)
+    hi = torch.empty(total, m, dtype=torch.float64, device=dev)
+    call("evr_box_pack_device", _stream(), S, n, m, cap, ws.data_ptr(), off.data_ptr(),
+         int(counts.max()) if S else 0, lo.data_ptr(), hi.data_ptr())
+    return lo, hi, off, counts
+
+
 _SOBOL_DIRECTIONS = {}
 
 

@@ -185,6 +185,20 @@ long long evr_cells_total(const evr_cells* c);
 int evr_cells_copy(const evr_cells* c, double* lo, double* hi, int* off);
 void evr_cells_free(evr_cells* c);
 
+/* ---- device box decomposition (same partition as evr_box_decompose) --------------------
+ * One workgroup per sample; obj is m x n x S on the device (objective values, maximisation),
+ * ref (m) on the device.  Every LUB is a 64-bit key of defining-point indices, cap keys per
+ * sample (power of two).  status[s] = 1 if sample s overflowed cap (retry with a larger
+ * cap).  counts[s] = number of non-empty cells.  evr_box_pack_device then writes the cells
+ * (sorted by first lower bound) at rows off[s] .. off[s+1]-1 of lo / hi (C x m).
+ * evr_box_device_limits returns 0 if (n, m) fits the kernel (LDS, key width), else 3. */
+int evr_box_device_limits(int n, int m, int* max_points, long long* lds_bytes);
+long long evr_box_device_workspace_bytes(int S, int n, int m, int cap);
+int evr_box_decompose_device(void* stream, int S, int n, int m, const double* obj, const double* ref,
+                             int cap, void* work, int* counts, int* status);
+int evr_box_pack_device(void* stream, int S, int n, int m, int cap, const void* work, const int* off,
+                        int max_cells, double* lo, double* hi);
+
 /* ---- quasi-MC base samples -------------------------------------------------------------
  * Replaces [upstream] draw_sobol_normal_samples / torch.quasirandom.SobolEngine(scramble=True)
  * as called by the qNEHVI samplers (bofire/strategies/predictives/qnehvi.py:39-52, seed from

@@ -35,7 +35,7 @@ def main(n=512, S=256, raw=1024, restarts=20, asks=3):
         st = s.last_ask_stats
         rows.append(dict(ask_s=round(dt, 4), construction=s.last_acqf.timings, raw_s=round(st.t_raw, 4),
                          opt_s=round(st.t_opt, 4), raw_evals=st.raw_evals, opt_evals=st.opt_evals,
-                         opt_iters=st.opt_iters, chunks=st.chunks, n_base=s.last_acqf.nb,
+                         opt_iters=st.opt_iters, chunks=st.chunks, n_base=s.last_acqf.nb, box_path=s.last_acqf.box_path,
                          cells=s.last_acqf.stats.total_cells, best=float(st.best_value)))
     print(json.dumps(dict(tell_s=round(t_tell, 3), asks=rows), default=float))
 
