@@ -112,10 +112,8 @@ def step(acqf, Xc, timer=None):
     R = ops.gemm(acqf.M, Kx)
     if T: T.stop(tk); tk = T.start("samples")
     G, L22, flags = ops.qnehvi_samples(st, R, b)
-    if T: T.stop(tk); tk = T.start("hvi_fwd")
-    acq = ops.hvi_forward(st, G, b, flags)
-    if T: T.stop(tk); tk = T.start("hvi_bwd")
-    dG = ops.hvi_backward(st, G, None, b)
+    if T: T.stop(tk); tk = T.start("hvi_fwd_bwd")
+    acq, dG = ops.hvi_forward_backward(st, G, b, flags)
     if T: T.stop(tk); tk = T.start("samples_bwd")
     gR = ops.qnehvi_samples_backward(st, R, L22, dG, b)
     if T: T.stop(tk); tk = T.start("gemm_bwd")
@@ -163,8 +161,8 @@ def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, n_cand=8, reps=3):
         states.append(ogp.GPState(X=Xn, y=(y - h.y_mean) / h.y_std, lengthscale=torch.tensor(h.lengthscale),
                                   noise=h.noise, constant=h.constant, y_mean=h.y_mean, y_std=h.y_std))
     nb = acqf.nb
-    off = acqf.cell_off.cpu().numpy()
-    lo, hi = acqf.cell_lo.cpu(), acqf.cell_hi.cpu()
+    off = acqf.cells.off.cpu().numpy()
+    lo, hi = (t.cpu() for t in acqf.cells.explicit())
     cells = [torch.stack([lo[off[s]:off[s + 1]], hi[off[s]:off[s + 1]]]) for s in range(acqf.S)]
     zq = acqf.zq.cpu().unsqueeze(1)
     zb = torch.zeros(acqf.S, nb, acqf.m, dtype=torch.float64)

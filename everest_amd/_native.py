@@ -31,6 +31,7 @@ class EvrQnehviState(ctypes.Structure):
         ("c", c_void_p), ("ym", c_void_p), ("ys", c_void_p), ("kxx", c_void_p),
         ("zq", c_void_p), ("obj_a", c_void_p), ("obj_b", c_void_p),
         ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p), ("max_cells", c_int),
+        ("cell_keys", c_void_p), ("cell_pts", c_void_p), ("cell_rank0", c_void_p), ("pts_stride", c_int),
     ]
 
 
@@ -80,8 +81,10 @@ _SIGS = {
     "evr_box_device_workspace_bytes": ([c_int, c_int, c_int, c_int], c_longlong),
     "evr_box_decompose_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p], c_int),
-    "evr_box_pack_device": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
-                            c_int),
+    "evr_box_pack_keys_device": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                  c_void_p, c_void_p], c_int),
+    "evr_cells_from_keys": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int] + [c_void_p] * 5, c_int),
+    "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
     "evr_sobol_scramble": ([c_int, ctypes.c_ulonglong, c_void_p, c_void_p], c_int),
     "evr_sobol_normal": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
 }

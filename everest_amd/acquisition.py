@@ -150,26 +150,23 @@ class QNEHVI:
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
             t1 = _time.perf_counter()
             if box_device if box_device is not None else ops.box_device_supported(nb, m):
-                lo, hi, off_d, counts_c = ops.box_decompose_device(Ob, self.ref)
+                cells = ops.box_decompose_device(Ob, self.ref)
                 self.box_path = "device"
             else:  # beyond the device kernel's LDS / key-width limits: native host partition
                 mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
                 lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),
                                                 num_threads or _host_threads(), layout="jis")
-                lo, hi = torch.as_tensor(lo, **f64), torch.as_tensor(hi, **f64)
-                off_d = torch.as_tensor(off, dtype=torch.int32, device=dev)
-                counts_c = np.diff(off)
+                cells = ops.Cells(torch.as_tensor(off, dtype=torch.int32, device=dev), np.diff(off), m,
+                                  lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64))
                 self.box_path = "host"
             tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
-            lo = self.ref.unsqueeze(0).repeat(S_, 1)
-            hi = torch.full((S_, m), math.inf, **f64)
-            off_d = torch.arange(S_ + 1, dtype=torch.int32, device=dev)
-            counts_c = np.ones(S_, dtype=np.int64)
+            cells = ops.Cells(torch.arange(S_ + 1, dtype=torch.int32, device=dev), np.ones(S_, dtype=np.int64), m,
+                              lo=self.ref.unsqueeze(0).repeat(S_, 1).contiguous(),
+                              hi=torch.full((S_, m), math.inf, **f64))
             self.box_path = "none"
-        self.cell_lo = lo.contiguous()
-        self.cell_hi = hi.contiguous()
-        self.cell_off = off_d.contiguous()
+        self.cells = cells
+        counts_c = cells.counts
         self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(np.sum(counts_c)),
                                        max_cells=int(counts_c.max()) if len(counts_c) else 0, prune_probs=probs)
 
@@ -191,8 +188,8 @@ class QNEHVI:
         M[:, Rr - 1].copy_(gp.alpha)
         self.M = M
         self.state = ops.make_state(n, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
-                                    self.cell_lo, self.cell_hi, self.cell_off, self.stats.max_cells)
-        self._keep = (self.zq, self.cell_lo, self.cell_hi, self.cell_off, self.obj_a, self.obj_b)
+                                    cells)
+        self._keep = (self.zq, self.obj_a, self.obj_b)
         torch.cuda.synchronize(dev)
         tm["total"] = _time.perf_counter() - t0
         self.timings = tm
@@ -217,9 +214,11 @@ class QNEHVI:
     def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
         """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        acq, (X, R, G, L22, flags) = self.forward(X, return_cache=True)
         b = X.shape[0]
-        dG = ops.hvi_backward(self.state, G, gout, b)
+        Kx = self.gp.cross(X)
+        R = ops.gemm(self.M, Kx)
+        G, L22, flags = ops.qnehvi_samples(self.state, R, b)
+        acq, dG = ops.hvi_forward_backward(self.state, G, b, flags, gout)
         gR = ops.qnehvi_samples_backward(self.state, R, L22, dG, b)
         dKx = ops.gemm(self.M, gR, transA=True)     # m x n x b
         gp = self.gp

@@ -19,8 +19,8 @@
 // (u in A, j) test z_j >= max_{k != j} Z^k_j(u) and emit u^j = (z_j, u_-j) with Z^j = z;
 // (c) new keys overwrite A's slots, the rest append (holes are tombstoned and compacted
 // when they pile up).  Then every live LUB's box is tested non-empty and its key emitted;
-// keys are bitonic-sorted (LDS when they fit, else in the HBM slab).  A pack kernel writes
-// [lo, hi] in the HVI kernels' layout from the sorted keys.
+// keys are bitonic-sorted (LDS when they fit, else in the HBM slab) and packed per sample;
+// the HVI scan decodes them against the sample's point table (hvi.hip).
 #include <algorithm>
 #include <cmath>
 
@@ -32,8 +32,6 @@ namespace evr {
 constexpr int BD_THREADS = 1024;
 constexpr unsigned long long BD_DEAD = ~0ull;
 constexpr int BD_LDS_BYTES = 160 * 1024 - 2048;  // dynamic LDS budget (static counters aside)
-
-__host__ __device__ constexpr int bd_field_bits(int m) { return m <= 4 ? 16 : (m == 5 ? 12 : 64 / m); }
 
 struct BdLayout {
   // per-sample slabs (elements): lub, buf: cap u64; aidx: cap int; pts: (n+m)*m double; inv0: n+m int
@@ -68,17 +66,6 @@ static size_t bd_lds_fixed(int n, int m) {
   return sizeof(double) * ((size_t)n * m + (size_t)(n + m) * m) + sizeof(int) * (size_t)(4 * n + 2 * m + 8);
 }
 
-template <int M>
-struct Key {
-  static constexpr int FB = bd_field_bits(M);
-  static constexpr unsigned long long FMASK = (1ull << FB) - 1;
-  __device__ static int field(unsigned long long k, int j) { return (int)((k >> (FB * (M - 1 - j))) & FMASK); }
-  __device__ static unsigned long long set(unsigned long long k, int j, int v) {
-    const int sh = FB * (M - 1 - j);
-    return (k & ~(FMASK << sh)) | ((unsigned long long)v << sh);
-  }
-};
-
 // Bitonic sort (ascending) of P2 keys in `a` (LDS or global), all threads of the block.
 template <typename Ptr>
 __device__ void bd_bitonic(Ptr a, int P2) {
@@ -105,7 +92,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
                                                               const double* __restrict__ ref, int cap, int sortcap,
                                                               unsigned char* __restrict__ ws, BdLayout Lo,
                                                               int* __restrict__ counts, int* __restrict__ status) {
-  using K = Key<M>;
+  using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
   double* raw = (double*)smem;                  // n x M   (min-space, all points)
@@ -314,31 +301,44 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
   }
 }
 
-// cell c of sample s (off[s] + i): lo_j = -u_j, hi_0 = +inf, hi_j = -max_{k<j} Z^k_j
+// explicit cells from compressed ones: cell off[s] + i of sample s -> lo / hi rows
 template <int M>
-__global__ __launch_bounds__(256) void bd_pack_kernel(int S, int n, int cap, const unsigned char* __restrict__ ws,
-                                                      BdLayout Lo, const int* __restrict__ off,
-                                                      double* __restrict__ lo, double* __restrict__ hi) {
-  using K = Key<M>;
+__global__ __launch_bounds__(256) void cells_from_keys_kernel(int stride, const int* __restrict__ off,
+                                                              const unsigned long long* __restrict__ keys,
+                                                              const double* __restrict__ pts,
+                                                              const int* __restrict__ rank0, double* __restrict__ lo,
+                                                              double* __restrict__ hi) {
+  using K = CellKey<M>;
   const int s = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int c0 = off[s], C = off[s + 1] - c0;
   if (i >= C) return;
-  const unsigned long long key = ((const unsigned long long*)(ws + Lo.off_buf))[(size_t)s * cap + i];
-  const double* pt = (const double*)(ws + Lo.off_pts) + (size_t)s * (n + M) * M;
-  const int* inv0 = (const int*)(ws + Lo.off_inv0) + (size_t)s * (n + M);
-  int P[M];
-  P[0] = inv0[K::field(key, 0)];
-#pragma unroll
-  for (int j = 1; j < M; ++j) P[j] = K::field(key, j);
+  double l[M], h[M];
+  K::decode(keys[c0 + i], pts + (size_t)s * stride * M, rank0 + (size_t)s * stride, l, h);
   const size_t o = (size_t)(c0 + i) * M;
 #pragma unroll
   for (int j = 0; j < M; ++j) {
-    double bl = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < j; ++k) bl = fmax(bl, pt[P[k] * M + j]);
-    lo[o + j] = -pt[P[j] * M + j];
-    hi[o + j] = -bl;
+    lo[o + j] = l[j];
+    hi[o + j] = h[j];
+  }
+}
+
+// compressed cells for the HVI scan: sorted keys packed at off[s], plus the point tables
+template <int M>
+__global__ __launch_bounds__(256) void bd_pack_keys_kernel(int S, int n, int cap, const unsigned char* __restrict__ ws,
+                                                           BdLayout Lo, const int* __restrict__ off,
+                                                           unsigned long long* __restrict__ keys,
+                                                           double* __restrict__ pts, int* __restrict__ rank0) {
+  const int s = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int c0 = off[s], C = off[s + 1] - c0;
+  if (i < C) keys[c0 + i] = ((const unsigned long long*)(ws + Lo.off_buf))[(size_t)s * cap + i];
+  if (blockIdx.x == 0) {
+    const size_t np = (size_t)(n + M);
+    const double* gp = (const double*)(ws + Lo.off_pts) + s * np * M;
+    const int* gi = (const int*)(ws + Lo.off_inv0) + s * np;
+    for (size_t e = threadIdx.x; e < np * M; e += 256) pts[s * np * M + e] = gp[e];
+    for (size_t e = threadIdx.x; e < np; e += 256) rank0[s * np + e] = gi[e];
   }
 }
 
@@ -401,14 +401,30 @@ int evr_box_decompose_device(void* stream, int S, int n, int m, const double* ob
   return 0;
 }
 
-int evr_box_pack_device(void* stream, int S, int n, int m, int cap, const void* work, const int* off, int max_cells,
-                        double* lo, double* hi) {
-  EVR_CHECK(S >= 1 && n >= 1 && m >= 1 && m <= 8 && work && off && lo && hi, "evr_box_pack_device: bad arguments");
+int evr_cells_from_keys(void* stream, int S, int m, int stride, const int* off, int max_cells,
+                        const unsigned long long* keys, const double* pts, const int* rank0, double* lo,
+                        double* hi) {
+  EVR_CHECK(S >= 1 && m >= 1 && m <= 8 && stride > m && off && keys && pts && rank0 && lo && hi,
+            "evr_cells_from_keys: bad arguments");
   if (max_cells <= 0) return 0;
-  const BdLayout Lo = bd_layout(S, n, m, cap);
   dim3 grid(cdiv(max_cells, 256), S);
   hipStream_t s = (hipStream_t)stream;
-#define L(MM) bd_pack_kernel<MM><<<grid, 256, 0, s>>>(S, n, cap, (const unsigned char*)work, Lo, off, lo, hi)
+#define L(MM) cells_from_keys_kernel<MM><<<grid, 256, 0, s>>>(stride, off, keys, pts, rank0, lo, hi)
+  EVR_BD_SWITCH(m, L);
+#undef L
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_box_pack_keys_device(void* stream, int S, int n, int m, int cap, const void* work, const int* off,
+                             int max_cells, unsigned long long* keys, double* pts, int* rank0) {
+  EVR_CHECK(S >= 1 && n >= 1 && m >= 1 && m <= 8 && work && off && keys && pts && rank0,
+            "evr_box_pack_keys_device: bad arguments");
+  const BdLayout Lo = bd_layout(S, n, m, cap);
+  dim3 grid(std::max(1, cdiv(max_cells, 256)), S);
+  hipStream_t s = (hipStream_t)stream;
+#define L(MM) \
+  bd_pack_keys_kernel<MM><<<grid, 256, 0, s>>>(S, n, cap, (const unsigned char*)work, Lo, off, keys, pts, rank0)
   EVR_BD_SWITCH(m, L);
 #undef L
   EVR_LAUNCH_CHECK();

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -71,5 +72,38 @@ __device__ __forceinline__ double kernel_dscale(int kind, double d2) {
   const double s = 2.23606797749979 * d;
   return -(5.0 / 3.0) * (1.0 + s) * exp(-s);
 }
+
+// Compressed box cell (box_device.hip -> hvi.hip): one 64-bit key of the m defining-point
+// indices of a local upper bound, field 0 (most significant) holding the rank of Z^0 in
+// descending first coordinate.  bd_field_bits(m) bits per field.
+__host__ __device__ constexpr int bd_field_bits(int m) { return m <= 4 ? 16 : (m == 5 ? 12 : 64 / m); }
+
+template <int M>
+struct CellKey {
+  static constexpr int FB = bd_field_bits(M);
+  static constexpr unsigned long long FMASK = (1ull << FB) - 1;
+  __device__ static int field(unsigned long long k, int j) { return (int)((k >> (FB * (M - 1 - j))) & FMASK); }
+  __device__ static unsigned long long set(unsigned long long k, int j, int v) {
+    const int sh = FB * (M - 1 - j);
+    return (k & ~(FMASK << sh)) | ((unsigned long long)v << sh);
+  }
+  // maximisation-space cell of the key: lo_j = -u_j, hi_j = -max_{k<j} Z^k_j (hi_0 = +inf).
+  // pt: the sample's (points + dummies) x M table (minimisation space), rank0: rank -> index.
+  __device__ static void decode(unsigned long long key, const double* pt, const int* rank0, double* lo,
+                                double* hi) {
+    int P[M];
+    P[0] = rank0[field(key, 0)];
+#pragma unroll
+    for (int j = 1; j < M; ++j) P[j] = field(key, j);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double bl = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < j; ++k) bl = fmax(bl, pt[P[k] * M + j]);
+      lo[j] = -pt[P[j] * M + j];
+      hi[j] = -bl;
+    }
+  }
+};
 
 }  // namespace evr

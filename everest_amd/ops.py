@@ -119,8 +119,8 @@ def gemm(A, B, transA=False, transB=False, alpha=1.0, beta=0.0, out=None) -> tor
     K2, N = (B.shape[2], B.shape[1]) if transB else (B.shape[1], B.shape[2])
     if K != K2:
         raise ValueError(f"gemm: inner dims {K} != {K2}")
-    if out is None:
-        out = torch.zeros(batch, M, N, dtype=torch.float64, device=A.device)
+    if out is None:  # beta = 0: the kernel never reads C
+        out = torch.empty(batch, M, N, dtype=torch.float64, device=A.device)
         beta = 0.0
     else:
         if out.dim() == 2:
@@ -242,14 +242,16 @@ def posterior_finalize(R, c, ym, ys, kxx, noise_add=None):
 # ---------------------------------------------------------------------------------------
 # qNEHVI pieces
 # ---------------------------------------------------------------------------------------
-def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cell_lo, cell_hi, cell_off,
-               max_cells: int) -> EvrQnehviState:
+def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cells: "Cells") -> EvrQnehviState:
     st = EvrQnehviState()
     st.n, st.nb, st.S, st.m = int(n), int(nb), int(S), int(m)
     st.c, st.ym, st.ys, st.kxx = c.data_ptr(), ym.data_ptr(), ys.data_ptr(), kxx.data_ptr()
     st.zq, st.obj_a, st.obj_b = zq.data_ptr(), obj_a.data_ptr(), obj_b.data_ptr()
-    st.cell_lo, st.cell_hi, st.cell_off = cell_lo.data_ptr(), cell_hi.data_ptr(), cell_off.data_ptr()
-    st.max_cells = int(max_cells)
+    st.cell_lo, st.cell_hi = _p(cells.lo), _p(cells.hi)
+    st.cell_off = cells.off.data_ptr()
+    st.max_cells = int(cells.max_cells)
+    st.cell_keys, st.cell_pts, st.cell_rank0 = _p(cells.keys), _p(cells.pts), _p(cells.rank0)
+    st.pts_stride = int(cells.stride)
     return st
 
 
@@ -294,6 +296,19 @@ def hvi_backward(st: EvrQnehviState, G: torch.Tensor, gout: Optional[torch.Tenso
     call("evr_hvi_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), _p(gout), work.data_ptr(),
          dG.data_ptr())
     return dG
+
+
+def hvi_forward_backward(st: EvrQnehviState, G: torch.Tensor, b: int, flags: Optional[torch.Tensor] = None,
+                         gout: Optional[torch.Tensor] = None):
+    """One fused scan: (acq (b), dG = gout/S * dHVI/dG)."""
+    acq = torch.empty(b, dtype=torch.float64, device=G.device)
+    dG = torch.empty_like(G)
+    if gout is not None:
+        gout = _dev(gout, "gout")
+    work = _hvi_work(st, b, True, G.device)
+    call("evr_hvi_forward_backward", _stream(), ctypes.byref(st), b, G.data_ptr(), _p(flags), _p(gout),
+         work.data_ptr(), acq.data_ptr(), dG.data_ptr())
+    return acq, dG
 
 
 def qnehvi_samples_backward(st: EvrQnehviState, R, L22, dG, b: int):
@@ -357,10 +372,42 @@ def box_device_supported(n: int, m: int) -> bool:
     return _native.load().evr_box_device_limits(int(n), int(m), None, None) == 0
 
 
-def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20):
-    """Device box decomposition of every sample of O (m x n x S objective values) above ref.
+class Cells:
+    """Box cells of S samples on the device, ragged by ``off`` (S+1 int32): either explicit
+    (``lo``/``hi``, C x m) or compressed (``keys`` C uint64 + per-sample point tables ``pts``
+    S x stride x m and ``rank0`` S x stride, the device box decomposition's output)."""
 
-    Returns (lo [C x m], hi [C x m], off [S+1] int32 on the device, counts [S] host numpy).
+    def __init__(self, off, counts, m, lo=None, hi=None, keys=None, pts=None, rank0=None, stride=0):
+        self.off, self.counts, self.m = off, np.asarray(counts, dtype=np.int64), int(m)
+        self.lo, self.hi, self.keys, self.pts, self.rank0, self.stride = lo, hi, keys, pts, rank0, int(stride)
+
+    @property
+    def S(self) -> int:
+        return int(self.counts.shape[0])
+
+    @property
+    def total(self) -> int:
+        return int(self.counts.sum())
+
+    @property
+    def max_cells(self) -> int:
+        return int(self.counts.max()) if self.S else 0
+
+    def explicit(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(lo, hi) rows (C x m, maximisation space); expands compressed cells on the device."""
+        if self.keys is None:
+            return self.lo, self.hi
+        lo = torch.empty(self.total, self.m, dtype=torch.float64, device=self.off.device)
+        hi = torch.empty_like(lo)
+        call("evr_cells_from_keys", _stream(), self.S, self.m, self.stride, self.off.data_ptr(), self.max_cells,
+             self.keys.data_ptr(), self.pts.data_ptr(), self.rank0.data_ptr(), lo.data_ptr(), hi.data_ptr())
+        return lo, hi
+
+
+def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20) -> Cells:
+    """Device box decomposition of every sample of O (m x n x S objective values) above ref,
+    returned compressed (64-bit keys + point tables, see Cells).
+
     One host sync (the per-sample cell counts size the packed arrays and the HVI plan); a
     sample overflowing ``cap`` LUB slots reruns the batch with 4x the capacity."""
     O, ref = _dev(O, "O"), _dev(ref, "ref")
@@ -383,11 +430,13 @@ def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, m
     np.cumsum(counts, out=off_h[1:])
     total = int(off_h[-1])
     off = torch.as_tensor(off_h.astype(np.int32)).to(dev)
-    lo = torch.empty(total, m, dtype=torch.float64, device=dev)
-    hi = torch.empty(total, m, dtype=torch.float64, device=dev)
-    call("evr_box_pack_device", _stream(), S, n, m, cap, ws.data_ptr(), off.data_ptr(),
-         int(counts.max()) if S else 0, lo.data_ptr(), hi.data_ptr())
-    return lo, hi, off, counts
+    stride = n + m
+    keys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)      # uint64 bit patterns
+    pts = torch.empty(S, stride, m, dtype=torch.float64, device=dev)
+    rank0 = torch.empty(S, stride, dtype=torch.int32, device=dev)
+    call("evr_box_pack_keys_device", _stream(), S, n, m, cap, ws.data_ptr(), off.data_ptr(),
+         int(counts.max()) if S else 0, keys.data_ptr(), pts.data_ptr(), rank0.data_ptr())
+    return Cells(off, counts, m, keys=keys, pts=pts, rank0=rank0, stride=stride)
 
 
 _SOBOL_DIRECTIONS = {}

@@ -124,13 +124,21 @@ typedef struct {
   const double* cell_hi;    /* total_cells x m (may be +inf) */
   const int* cell_off;      /* S + 1 */
   int max_cells;            /* max_s (cell_off[s+1] - cell_off[s]) — host-known, sizes the launch */
+  /* compressed cells (device box decomposition, evr_box_pack_keys_device): when cell_keys is
+   * not NULL the scan rebuilds every cell from its 64-bit key of defining-point indices and
+   * the sample's point table, and cell_lo / cell_hi are not read. */
+  const unsigned long long* cell_keys; /* total_cells */
+  const double* cell_pts;   /* S x pts_stride x m: minimisation-space points, then m dummies */
+  const int* cell_rank0;    /* S x pts_stride: point index of rank r (key field 0) */
+  int pts_stride;           /* rows per sample of cell_pts / cell_rank0 */
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b
  * (0 ok, 1 new-block Cholesky failed after 6 jitter tries). */
 int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                        double* G, double* L22, int* flags);
-/* Workspace (doubles) the HVI scan needs for b candidates (per-(sample, cell-chunk) partials). */
+/* Workspace (doubles) the HVI scan needs for b candidates (per-(sample, cell-chunk)
+ * partials); backward != 0 sizes it for evr_hvi_backward / evr_hvi_forward_backward. */
 long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backward);
 /* acq[c] = mean_s HVI_s(G[s][:, c]) over the cells of sample s (register-tiled cell x
  * candidate scan, deterministic two-stage reduction); acq[c] = NaN where flags (m x b,
@@ -142,6 +150,10 @@ int evr_mean_over_samples(void* stream, int S, int b, const double* partial, dou
 /* dG[s][j][c] = gout[c]/S * dHVI_s/dg_j (torch min/clamp_min/prod subgradients; gout NULL = 1) */
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
                      const double* gout, double* work, double* dG);
+/* One fused scan: acq (as evr_hvi_forward, NaN on flags) and dG (as evr_hvi_backward). */
+int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
+                             const int* flags, const double* gout, double* work, double* acq,
+                             double* dG);
 /* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);
@@ -189,15 +201,21 @@ void evr_cells_free(evr_cells* c);
  * One workgroup per sample; obj is m x n x S on the device (objective values, maximisation),
  * ref (m) on the device.  Every LUB is a 64-bit key of defining-point indices, cap keys per
  * sample (power of two).  status[s] = 1 if sample s overflowed cap (retry with a larger
- * cap).  counts[s] = number of non-empty cells.  evr_box_pack_device then writes the cells
- * (sorted by first lower bound) at rows off[s] .. off[s+1]-1 of lo / hi (C x m).
+ * cap).  counts[s] = number of non-empty cells.  evr_box_pack_keys_device then packs the
+ * sorted keys at off[s] (cells ordered by first lower bound) with the per-sample point tables
+ * pts (S x (n+m) x m) and rank0 (S x (n+m)) -> evr_qnehvi_state.cell_keys / cell_pts /
+ * cell_rank0, pts_stride n+m.  evr_cells_from_keys expands them into explicit lo / hi rows.
  * evr_box_device_limits returns 0 if (n, m) fits the kernel (LDS, key width), else 3. */
 int evr_box_device_limits(int n, int m, int* max_points, long long* lds_bytes);
 long long evr_box_device_workspace_bytes(int S, int n, int m, int cap);
 int evr_box_decompose_device(void* stream, int S, int n, int m, const double* obj, const double* ref,
                              int cap, void* work, int* counts, int* status);
-int evr_box_pack_device(void* stream, int S, int n, int m, int cap, const void* work, const int* off,
-                        int max_cells, double* lo, double* hi);
+int evr_box_pack_keys_device(void* stream, int S, int n, int m, int cap, const void* work,
+                             const int* off, int max_cells, unsigned long long* keys, double* pts,
+                             int* rank0);
+int evr_cells_from_keys(void* stream, int S, int m, int stride, const int* off, int max_cells,
+                        const unsigned long long* keys, const double* pts, const int* rank0,
+                        double* lo, double* hi);
 
 /* ---- quasi-MC base samples -------------------------------------------------------------
  * Replaces [upstream] draw_sobol_normal_samples / torch.quasirandom.SobolEngine(scramble=True)

@@ -36,8 +36,9 @@ def test_device_box_decomposition_matches_host(m, n, S, variant):
     O[:, 2] = O[:, 3] - 0.05
     lo_h, hi_h, off_h = ops.box_decompose(O, ref, None, 4, layout="sij")
     Od = torch.tensor(np.ascontiguousarray(O.transpose(2, 1, 0)), device="cuda")   # m x n x S
-    lo_d, hi_d, off_d, counts = ops.box_decompose_device(Od, torch.tensor(ref, device="cuda"))
-    off_d = off_d.cpu().numpy()
+    cells = ops.box_decompose_device(Od, torch.tensor(ref, device="cuda"))
+    lo_d, hi_d = cells.explicit()
+    off_d = cells.off.cpu().numpy()
     assert np.array_equal(off_d, off_h)
     lo_d, hi_d = lo_d.cpu().numpy(), hi_d.cpu().numpy()
     for s in range(S):
@@ -51,9 +52,11 @@ def test_device_box_decomposition_capacity_retry_and_determinism():
     O = _front(8, 80, 5, seed=3)
     Od = torch.tensor(np.ascontiguousarray(O.transpose(2, 1, 0)), device="cuda")
     ref = torch.full((5,), -1.1, dtype=torch.float64, device="cuda")
-    lo1, hi1, off1, _ = ops.box_decompose_device(Od, ref, cap=4)         # overflows, reruns x4 ...
-    lo2, hi2, off2, _ = ops.box_decompose_device(Od, ref)
-    assert torch.equal(off1, off2) and torch.equal(lo1, lo2) and torch.equal(hi1, hi2)
+    c1 = ops.box_decompose_device(Od, ref, cap=4)         # overflows, reruns x4 ...
+    c2 = ops.box_decompose_device(Od, ref)
+    assert torch.equal(c1.off, c2.off) and torch.equal(c1.keys, c2.keys)
+    (lo1, hi1), (lo2, hi2) = c1.explicit(), c2.explicit()
+    assert torch.equal(lo1, lo2) and torch.equal(hi1, hi2)
 
 
 def test_device_box_volume_equals_exact_hypervolume():
@@ -64,7 +67,7 @@ def test_device_box_volume_equals_exact_hypervolume():
     O = _front(1, n, m, seed=11)[0]
     ref = -1.1 * np.ones(m)
     Od = torch.tensor(np.ascontiguousarray(O.T[:, :, None]), device="cuda")
-    lo, hi, off, _ = ops.box_decompose_device(Od, torch.tensor(ref, device="cuda"))
+    lo, hi = ops.box_decompose_device(Od, torch.tensor(ref, device="cuda")).explicit()
     lo, hi = lo.cpu().numpy(), hi.cpu().numpy()
     # cells partition the NON-dominated region above ref; HV = box(ref, cap) - non-dominated part
     cap = np.zeros(m)

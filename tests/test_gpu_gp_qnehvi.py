@@ -152,3 +152,25 @@ def test_qnehvi_device_samples_match_host_samples():
     assert np.array_equal(auto.base_rows, host.base_rows)
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(64, d)), device="cuda")
     assert torch.allclose(auto.forward(Xc), host.forward(Xc), rtol=1e-10, atol=1e-13)
+
+
+def test_qnehvi_compressed_cells_match_explicit_cells():
+    """Device box decomposition (64-bit cell keys decoded in the scan) vs the host partition
+    (explicit [lo, hi] rows): same cell count, same acquisition values and gradients."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 80, 6, 4, 32
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=21)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(m), np.zeros(m), -1.1 * np.ones(m)
+    kw = dict(S=S, sampler_seed=3, prune_baseline=True, prune_seed=5, prune_samples=256)
+    dev_q = QNEHVI(gp, X, X, ref, a, b, box_device=True, **kw)
+    host_q = QNEHVI(gp, X, X, ref, a, b, box_device=False, **kw)
+    assert dev_q.box_path == "device" and host_q.box_path == "host"
+    assert dev_q.stats.total_cells == host_q.stats.total_cells
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(4).uniform(size=(40, d)), device="cuda")
+    a1, g1 = dev_q.forward_backward(Xc)
+    a2, g2 = host_q.forward_backward(Xc)
+    assert torch.allclose(a1, a2, rtol=1e-12, atol=1e-15)
+    assert torch.allclose(g1, g2, rtol=1e-10, atol=1e-13)
+    assert torch.allclose(dev_q.forward(Xc), a1, rtol=1e-12, atol=1e-15)
