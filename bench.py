@@ -146,14 +146,17 @@ def gp_posterior_ms(device, reps=20):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, n_cand=8, reps=3):
+def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, chunk=8, budget_s=15.0):
     """Reference-structure CPU restatement (oracle/, torch-CPU fp64, BoTorch computation
-    shape) timed on the host cores: forward+backward over n_cand candidates at the same
-    state (cells injected from the device build so only the evaluation is timed)."""
+    shape: joint posterior over [X_base; x] per forward, per-sample cell scan, autograd
+    backward) timed on the host cores over a BOUNDED sample of the same workload: chunks of
+    ``chunk`` candidates (BoFire's default batch_limit = 8,
+    bofire/data_models/strategies/predictives/botorch.py:101-108) from the same candidate
+    batch, forward+backward each, until ``budget_s`` of CPU wall time is spent.  The cells
+    are injected from the device build so only the evaluation is timed."""
     from oracle import gp as ogp
     from oracle import qnehvi as oq
 
-    d = X.shape[1]
     Xn = torch.tensor(X)
     states = []
     for j, h in enumerate(hypers):
@@ -169,14 +172,60 @@ def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, n_cand=8, reps=3):
     orc = oq.QNEHVI(states, Xn[torch.as_tensor(acqf.base_rows)], oq.Objective(-torch.ones(acqf.m),
                     torch.zeros(acqf.m, dtype=torch.float64)), torch.full((acqf.m,), -1.1, dtype=torch.float64),
                     zb, zq, cells=cells)
-    x = Xc_cpu[:n_cand].clone().requires_grad_(True)
-    ts = []
-    for _ in range(reps):
+    done, spent, i = 0, 0.0, 0
+    while spent < budget_s and (i + 1) * chunk <= Xc_cpu.shape[0]:
+        x = Xc_cpu[i * chunk:(i + 1) * chunk].clone().requires_grad_(True)
         t0 = time.perf_counter()
         v = orc.forward(x.unsqueeze(1))
         v.sum().backward()
+        spent += time.perf_counter() - t0
+        done += chunk
+        i += 1
+    return spent, done
+
+
+def _traffic(path, kernel):
+    """Per-launch HBM bytes of ``kernel`` from the committed PMC summary (FETCH_SIZE doubled
+    per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE), or None."""
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = tab.get(kernel)
+    return ent if ent and "bytes_per_launch" in ent else None
+
+
+def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: int = 2):
+    """Full QnehviStrategy.ask() (config 4 shape on one GPU: 1024 raw Sobol candidates +
+    20 L-BFGS-B restarts, q=1) through the BoFire-compatible strategy API; returns the
+    median ask() wall time and acquisition evaluations / s (raw + optimizer evaluations)."""
+    import pandas as pd
+
+    import everest_amd.data_models as dm
+    from everest_amd import strategies
+    from everest_amd.benchmarks import DTLZ2
+
+    bm = DTLZ2(dim=6, num_objectives=5)
+    Xd = pd.DataFrame(np.random.default_rng(0).uniform(size=(n, 6)), columns=bm.domain.inputs.get_keys())
+    s = strategies.map(dm.QnehviStrategy(domain=bm.domain, ref_point=bm.ref_point, seed=1, num_sobol_samples=S,
+                                         num_raw_samples=raw, num_restarts=restarts))
+    t0 = time.perf_counter()
+    s.tell(bm.f(Xd, return_complete=True))
+    torch.cuda.synchronize()
+    t_tell = time.perf_counter() - t0
+    s.ask(1)  # warm-up (first construction pays one-time allocations)
+    ts, evals = [], []
+    for _ in range(asks):
+        t0 = time.perf_counter()
+        s.ask(1)
+        torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    return float(np.median(ts)), n_cand
+        st = s.last_ask_stats
+        evals.append(st.raw_evals + st.opt_evals)
+    i = int(np.argsort(ts)[len(ts) // 2])
+    return {"ask_s": round(ts[i], 4), "evals": int(evals[i]), "evals_per_s": round(evals[i] / ts[i], 1),
+            "tell_s": round(t_tell, 3), "raw_samples": raw, "restarts": restarts, "mc_samples": S}
 
 
 def main():
@@ -190,6 +239,9 @@ def main():
     ap.add_argument("--S", type=int, default=256)
     ap.add_argument("--b", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ask", action="store_true", help="skip the full QnehviStrategy.ask() timing")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"),
+                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,28 +296,38 @@ def main():
         sum_cells = st.total_cells
         m = args.m
         b = args.b
-        # dominant kernel and its algorithmic work per launch
+        # dominant kernel and its algorithmic work per launch: the dense
+        # reference scan touches every (candidate, cell) pair — min, sub, max, mul per
+        # objective forward; the fused backward adds the prefix/suffix products and the
+        # subgradient FMA (6m + 2 flop per pair in total).
         dom = max(ktimes, key=ktimes.get)
         work = {
-            "hvi_fwd": ("valu", b * sum_cells * 4 * m, "flop"),
-            "hvi_bwd": ("valu", b * sum_cells * (6 * m + 2), "flop"),
-            "gemm_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, "flop"),
-            "gemm_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, "flop"),
+            "hvi_fwd_bwd": ("valu", b * sum_cells * (6 * m + 2), PEAK_FP64_TFLOPS),
+            "gemm_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
+            "gemm_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
         }
         roof = None
         if dom in work:
-            bound, w, _ = work[dom]
+            bound, w, peak = work[dom]
             ach = w / (ktimes[dom] * 1e-3) / 1e12
-            roof = {"bound": bound, "kernel": dom, "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": None,
-                    "algorithmic_work_per_launch": w}
+            roof = {"bound": bound, "kernel": dom, "achieved": round(ach, 3), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                    "algorithmic_work_per_launch": w, "launch_ms": round(ktimes[dom], 4)}
+            tr = _traffic(args.traffic_json, dom)
+            if tr is not None:
+                roof["traffic"] = tr["bytes_per_launch"]
+                roof["traffic_source"] = tr["source"]
         cpu = None
         if not args.no_cpu_baseline:
             torch.set_num_threads(min(16, os.cpu_count() or 1))
             t_cpu, nc = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
             cpu = {"value": round(nc / t_cpu, 3), "unit": "candidates/s", "cores": torch.get_num_threads(),
-                   "kind": "port", "sample": f"oracle reference-structure forward+backward over {nc} candidates "
-                   f"(same state, n={args.n}, n_base={acqf.nb}, S={args.S}), median of 3"}
+                   "kind": "port", "sample": f"oracle reference-structure forward+backward over the first {nc} "
+                   f"of the same {b} candidates in chunks of 8 (batch_limit), same state (n={args.n}, "
+                   f"n_base={acqf.nb}, S={args.S}), {t_cpu:.1f} s of CPU wall time"}
+        ask = None
+        if world == 1 and not args.no_ask:
+            ask = ask_throughput(args.n, args.S)
         out = {
             "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
             "value": round(value, 2),
@@ -288,6 +350,7 @@ def main():
             "gp_posterior_ms": round(gp_posterior_ms(device), 4),
             "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},
             "setup_s": {"gp_fit": round(t_fit, 3), "qnehvi_build": round(t_build, 3)},
+            "ask": ask,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, bench line, rocprofv3 kernel stats of the same bench
+# command, and two PMC passes (FETCH_SIZE / WRITE_SIZE) for the HBM-traffic figure.
+# usage: bash tools/gpu_round.sh <tag>     (outputs under gpurun_out/<tag>/)
+set -o pipefail
+TAG=${1:-run}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # step <name> <timeout_s> cmd...
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%H:%M:%S)] $name"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%H:%M:%S)] $name rc=$rc"
+  return $rc
+}
+step pytest 600 python -m pytest tests -m gpu -x -q &&
+step bench 600 python bench.py &&
+step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+     python bench.py --no-cpu-baseline --no-ask &&
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
+     --kernel-include-regex "hvi_|kmat_kernel|qn_samples" -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ask &&
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
+     --kernel-include-regex "hvi_|kmat_kernel|qn_samples" -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ask &&
+python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json"
+echo "done rc=$?"
