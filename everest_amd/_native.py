@@ -32,6 +32,8 @@ class EvrQnehviState(ctypes.Structure):
         ("zq", c_void_p), ("obj_a", c_void_p), ("obj_b", c_void_p),
         ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p), ("max_cells", c_int),
         ("cell_keys", c_void_p), ("cell_pts", c_void_p), ("cell_rank0", c_void_p), ("pts_stride", c_int),
+        ("grp_off", c_void_p), ("grp_keys", c_void_p), ("grp_rank", c_void_p), ("grp_box", c_void_p),
+        ("sorted_lo", c_void_p), ("max_groups", c_int),
     ]
 
 
@@ -85,6 +87,9 @@ _SIGS = {
                                   c_void_p, c_void_p], c_int),
     "evr_cells_from_keys": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int] + [c_void_p] * 5, c_int),
     "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
+    "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
+    "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
+                                  c_int),
     "evr_sobol_scramble": ([c_int, ctypes.c_ulonglong, c_void_p, c_void_p], c_int),
     "evr_sobol_normal": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
 }

@@ -67,7 +67,8 @@ class QNEHVI:
                  S: int = 512, sampler_seed: int = 0, prune_baseline: bool = True, prune_seed: int = 0,
                  prune_samples: int = 2048, max_frac: float = 1.0, z_prune: Optional[torch.Tensor] = None,
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
-                 num_threads: Optional[int] = None, box_device: Optional[bool] = None):
+                 num_threads: Optional[int] = None, box_device: Optional[bool] = None,
+                 kd_scan: Optional[bool] = None):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -152,6 +153,9 @@ class QNEHVI:
             if box_device if box_device is not None else ops.box_device_supported(nb, m):
                 cells = ops.box_decompose_device(Ob, self.ref)
                 self.box_path = "device"
+                if kd_scan if kd_scan is not None else ops.kd_supported(cells):
+                    ops.cells_kd_order(cells)
+                    self.box_path = "device+kd"
             else:  # beyond the device kernel's LDS / key-width limits: native host partition
                 mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
                 lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),

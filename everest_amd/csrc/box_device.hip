@@ -337,8 +337,11 @@ __global__ __launch_bounds__(256) void bd_pack_keys_kernel(int S, int n, int cap
     const size_t np = (size_t)(n + M);
     const double* gp = (const double*)(ws + Lo.off_pts) + s * np * M;
     const int* gi = (const int*)(ws + Lo.off_inv0) + s * np;
-    for (size_t e = threadIdx.x; e < np * M; e += 256) pts[s * np * M + e] = gp[e];
-    for (size_t e = threadIdx.x; e < np; e += 256) rank0[s * np + e] = gi[e];
+    // rows past the nf Pareto points + M dummies are unused: +inf (never a lower bound, and a
+    // well-defined rank for the kd ordering of cells_kd.hip)
+    const size_t nv = (size_t)((const int*)(ws + Lo.off_nf))[s] + M;
+    for (size_t e = threadIdx.x; e < np * M; e += 256) pts[s * np * M + e] = e < nv * M ? gp[e] : INFINITY;
+    for (size_t e = threadIdx.x; e < np; e += 256) rank0[s * np + e] = e + M <= nv ? gi[e] : 0;  // ranks 0..nf
   }
 }
 

@@ -252,6 +252,10 @@ def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cells: "Cells") ->
     st.max_cells = int(cells.max_cells)
     st.cell_keys, st.cell_pts, st.cell_rank0 = _p(cells.keys), _p(cells.pts), _p(cells.rank0)
     st.pts_stride = int(cells.stride)
+    kd = cells.kd
+    if kd is not None:
+        st.grp_off, st.grp_keys, st.grp_rank = kd.goff.data_ptr(), kd.keys.data_ptr(), kd.rank.data_ptr()
+        st.grp_box, st.sorted_lo, st.max_groups = kd.box.data_ptr(), kd.sorted_lo.data_ptr(), int(kd.max_groups)
     return st
 
 
@@ -380,6 +384,7 @@ class Cells:
     def __init__(self, off, counts, m, lo=None, hi=None, keys=None, pts=None, rank0=None, stride=0):
         self.off, self.counts, self.m = off, np.asarray(counts, dtype=np.int64), int(m)
         self.lo, self.hi, self.keys, self.pts, self.rank0, self.stride = lo, hi, keys, pts, rank0, int(stride)
+        self.kd: Optional[KdGroups] = None
 
     @property
     def S(self) -> int:
@@ -402,6 +407,43 @@ class Cells:
         call("evr_cells_from_keys", _stream(), self.S, self.m, self.stride, self.off.data_ptr(), self.max_cells,
              self.keys.data_ptr(), self.pts.data_ptr(), self.rank0.data_ptr(), lo.data_ptr(), hi.data_ptr())
         return lo, hi
+
+
+class KdGroups:
+    """kd-ordered groups of 16 compressed cells (cells_kd.hip) for the sparse HVI scan."""
+
+    def __init__(self, goff, keys, rank, box, sorted_lo, max_groups):
+        self.goff, self.keys, self.rank, self.box = goff, keys, rank, box
+        self.sorted_lo, self.max_groups = sorted_lo, int(max_groups)
+
+
+def kd_supported(cells: Cells) -> bool:
+    if cells.keys is None or cells.S == 0:
+        return False
+    return _native.load().evr_cells_kd_limits(cells.stride, cells.m, cells.max_cells, None) == 0
+
+
+def cells_kd_order(cells: Cells) -> KdGroups:
+    """kd order + rank index of compressed cells (one workgroup per sample); attaches and
+    returns the KdGroups (the HVI scan then runs the sparse three-level filter)."""
+    if cells.keys is None:
+        raise ValueError("cells_kd_order needs compressed cells (device box decomposition)")
+    S, m, stride = cells.S, cells.m, cells.stride
+    dev = cells.off.device
+    ng = (cells.counts + 15) // 16
+    goff_h = np.zeros(S + 1, dtype=np.int64)
+    np.cumsum(ng, out=goff_h[1:])
+    G = int(goff_h[-1])
+    goff = torch.as_tensor(goff_h.astype(np.int32)).to(dev)
+    keys = torch.empty(max(G, 1) * 16, dtype=torch.int64, device=dev)
+    rank = torch.empty(max(G, 1) * m * 16, dtype=torch.int16, device=dev)       # uint16 bit patterns
+    box = torch.empty(max(G, 1) * 8, dtype=torch.int16, device=dev)
+    sorted_lo = torch.empty(S, m, stride, dtype=torch.float64, device=dev)
+    call("evr_cells_kd_order_device", _stream(), S, m, stride, cells.off.data_ptr(), goff.data_ptr(),
+         cells.max_cells, cells.keys.data_ptr(), cells.pts.data_ptr(), cells.rank0.data_ptr(), keys.data_ptr(),
+         rank.data_ptr(), box.data_ptr(), sorted_lo.data_ptr())
+    cells.kd = KdGroups(goff, keys, rank, box, sorted_lo, int(ng.max()) if S else 0)
+    return cells.kd
 
 
 def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20) -> Cells:

@@ -131,6 +131,14 @@ typedef struct {
   const double* cell_pts;   /* S x pts_stride x m: minimisation-space points, then m dummies */
   const int* cell_rank0;    /* S x pts_stride: point index of rank r (key field 0) */
   int pts_stride;           /* rows per sample of cell_pts / cell_rank0 */
+  /* kd-ordered cell groups (evr_cells_kd_order_device, needs the compressed cells above):
+   * when grp_off is not NULL the scan runs the sparse group -> cell -> term filter */
+  const int* grp_off;                  /* S + 1: group offsets, 16 cells per group */
+  const unsigned long long* grp_keys;  /* grp_off[S]*16 cell keys in kd order */
+  const unsigned short* grp_rank;      /* grp_off[S] x m x 16 per-cell lower-bound ranks (0xFFFF pad) */
+  const unsigned short* grp_box;       /* grp_off[S] x 8: per-group minimum rank per objective */
+  const double* sorted_lo;             /* S x m x pts_stride ascending lower-bound values */
+  int max_groups;                      /* max_s (grp_off[s+1] - grp_off[s]) */
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b
@@ -216,6 +224,22 @@ int evr_box_pack_keys_device(void* stream, int S, int n, int m, int cap, const v
 int evr_cells_from_keys(void* stream, int S, int m, int stride, const int* off, int max_cells,
                         const unsigned long long* keys, const double* pts, const int* rank0,
                         double* lo, double* hi);
+
+/* ---- kd ordering of compressed cells for the sparse HVI scan -------------------------
+ * Per sample (one workgroup each): rank tables of the point rows per objective, a kd split
+ * order of the cells (median split on the objective of largest rank spread, leaves of 16),
+ * then per group of 16 cells: the keys (okeys, goff[S]*16), the cells' lower-bound ranks
+ * (ork, goff[S] x m x 16 u16, 0xFFFF padding), the group's minimum rank per objective (ogb,
+ * goff[S] x 8 u16) and per sample the ascending lower-bound values (osv, S x m x stride).
+ * goff[s] = sum_{s'<s} ceil(counts[s'] / 16).  evr_cells_kd_limits returns 0 if max_cells /
+ * stride fit the kernel (LDS sort buffer), else 3 (the tiled scan is used then).
+ * Replaces nothing in the reference: an MI355X-side index over the [upstream]
+ * FastNondominatedPartitioning cells (bofire/strategies/predictives/qnehvi.py:50). */
+int evr_cells_kd_limits(int stride, int m, int max_cells, long long* lds_bytes);
+int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int* off, const int* goff,
+                              int max_cells, const unsigned long long* keys, const double* pts,
+                              const int* rank0, unsigned long long* okeys, unsigned short* ork,
+                              unsigned short* ogb, double* osv);
 
 /* ---- quasi-MC base samples -------------------------------------------------------------
  * Replaces [upstream] draw_sobol_normal_samples / torch.quasirandom.SobolEngine(scramble=True)

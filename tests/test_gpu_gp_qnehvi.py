@@ -166,7 +166,7 @@ def test_qnehvi_compressed_cells_match_explicit_cells():
     kw = dict(S=S, sampler_seed=3, prune_baseline=True, prune_seed=5, prune_samples=256)
     dev_q = QNEHVI(gp, X, X, ref, a, b, box_device=True, **kw)
     host_q = QNEHVI(gp, X, X, ref, a, b, box_device=False, **kw)
-    assert dev_q.box_path == "device" and host_q.box_path == "host"
+    assert dev_q.box_path.startswith("device") and host_q.box_path == "host"
     assert dev_q.stats.total_cells == host_q.stats.total_cells
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(4).uniform(size=(40, d)), device="cuda")
     a1, g1 = dev_q.forward_backward(Xc)
