@@ -15,7 +15,7 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_longlong, c_void_p
 import torch  # noqa: F401  (must precede loading the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libeverest_amd.so")
+LIB_PATH = os.environ.get("EVR_LIB_PATH") or os.path.join(_HERE, "_lib", "libeverest_amd.so")
 
 c_double_p = c_void_p  # device / host pointers are passed as integers
 c_int_p = c_void_p

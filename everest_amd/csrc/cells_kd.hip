@@ -21,7 +21,7 @@
 //      every segment by its objective; segments split at 16*ceil(len/32) so every group of
 //      16 lies in one leaf;
 //   3. outputs per group of 16: keys in kd order, per-cell rank coordinates ([j][16] u16,
-//      0xFFFF padding) and the group's minimum rank per objective.
+//      0x7FFF padding) and the group's minimum rank per objective.
 // Deterministic: keys are unique (cell index in the low bits), so the order never depends
 // on thread timing.
 #include "common.hpp"
@@ -32,7 +32,7 @@ namespace evr {
 constexpr int KD_THREADS = 1024;
 constexpr int KD_MAX_CELLS = 8192;          // LDS sort buffer (64 KB)
 constexpr int KD_MAX_GROUPS = KD_MAX_CELLS / 16;
-constexpr unsigned short KD_PAD = 0xFFFF;
+constexpr unsigned short KD_PAD = 0x7FFF;   // > every threshold (ranks < 2^15: packed signed compares)
 
 __device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
   for (int k = 2; k <= P2; k <<= 1) {
@@ -217,7 +217,7 @@ int evr_cells_kd_limits(int stride, int m, int max_cells, long long* lds_bytes) 
   while (P2 < max_cells) P2 <<= 1;
   const long long lds = (long long)P2 * 8 + (long long)stride * m * 10 + 16;
   if (lds_bytes) *lds_bytes = lds;
-  return (max_cells <= KD_MAX_CELLS && stride < 0xFFFF && lds <= 96 * 1024) ? 0 : 3;
+  return (max_cells <= KD_MAX_CELLS && stride < 0x7FFF && lds <= 96 * 1024) ? 0 : 3;
 }
 
 int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int* off, const int* goff,

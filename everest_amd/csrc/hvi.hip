@@ -276,7 +276,7 @@ struct HviKd {
 };
 
 struct KdLds {
-  size_t pt, sv, r0, gb, mA, pA, bytes;
+  size_t pt, r0, gb, mA, pA, bytes;
 };
 
 __host__ __device__ inline KdLds kd_lds(int stride, int M, int max_groups) {
@@ -284,8 +284,6 @@ __host__ __device__ inline KdLds kd_lds(int stride, int M, int max_groups) {
   const size_t nq = (size_t)(max_groups + 15) / 16;
   size_t o = 0;
   L.pt = o;
-  o += (size_t)stride * M * 8;
-  L.sv = o;
   o += (size_t)stride * M * 8;
   L.r0 = o;
   o += (size_t)stride * 4;
@@ -339,71 +337,162 @@ __device__ __forceinline__ int block_scan256(int v, int* wsum, int* total) {
   return off + incl - v;
 }
 
+// DPP cross-lane moves (gfx9 encodings): row_shr:n = 0x110 + n, row_bcast:15 = 0x142,
+// row_bcast:31 = 0x143.  Lanes without a valid source keep `old`.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i32(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = dpp_i32<CTRL, ROWMASK>(0, (int)x);
+  const int hi = dpp_i32<CTRL, ROWMASK>(0, (int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// one Hillis-Steele step of the segmented scan: add the source lane's partial if it lies in
+// the same segment (segments are contiguous runs of equal key)
+template <int CTRL, int ROWMASK, int NV>
+__device__ __forceinline__ void seg_step(int key, double (&val)[NV]) {
+  const int k2 = dpp_i32<CTRL, ROWMASK>(-2, key);
+  double x[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x[v] = dpp_f64<CTRL, ROWMASK>(val[v]);
+  if (k2 == key) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) val[v] += x[v];
+  }
+}
+// wave-wide segmented inclusive scan (fixed tree: deterministic)
+template <int NV>
+__device__ __forceinline__ void seg_scan_wave(int key, double (&val)[NV]) {
+  seg_step<0x111, 0xF>(key, val);
+  seg_step<0x112, 0xF>(key, val);
+  seg_step<0x114, 0xF>(key, val);
+  seg_step<0x118, 0xF>(key, val);
+  seg_step<0x142, 0xA>(key, val);
+  seg_step<0x143, 0xC>(key, val);
+}
+
+// packed 16-bit "rank < threshold" test: for every u16 half of w, bit 15 of the half is set
+// iff rank < t (ranks and thresholds < 2^15, so the signed 16-bit difference is negative)
+typedef short kd_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned int kd_lt16(unsigned int w, unsigned int t) {
+  const kd_s16x2 a = __builtin_bit_cast(kd_s16x2, w), b = __builtin_bit_cast(kd_s16x2, t);
+  return __builtin_bit_cast(unsigned int, (kd_s16x2)(a - b));
+}
+
+// t[s][j][c] = #{point rows p of sample s : lower-bound value_j(p) <= G[s][j][c]} (binary
+// search in the sample's ascending values, staged in LDS); one workgroup per (j, s).
+__global__ __launch_bounds__(256) void hvi_thresholds(int b, int M, int stride, const double* __restrict__ G,
+                                                      const double* __restrict__ sorted_lo, int* __restrict__ th) {
+  extern __shared__ double thv[];
+  const int j = blockIdx.x, s = blockIdx.y;
+  const double* src = sorted_lo + ((size_t)s * M + j) * stride;
+  for (int e = threadIdx.x; e < stride; e += 256) thv[e] = src[e];
+  __syncthreads();
+  const size_t row = ((size_t)s * M + j) * b;
+  for (int c = threadIdx.x; c < b; c += 256) {
+    const double y = G[row + c];
+    int lo = 0, hi = stride;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (thv[mid] <= y) lo = mid + 1;
+      else hi = mid;
+    }
+    th[row + c] = lo;
+  }
+}
+
+// LDS staging with the loads of 4 elements issued before their stores
+template <typename T>
+__device__ __forceinline__ void kd_stage(T* __restrict__ dst, const T* __restrict__ src, int n) {
+  int e = threadIdx.x;
+  for (; e + 3 * 256 < n; e += 4 * 256) {
+    const T a = src[e], b = src[e + 256], c = src[e + 512], d = src[e + 768];
+    dst[e] = a;
+    dst[e + 256] = b;
+    dst[e + 512] = c;
+    dst[e + 768] = d;
+  }
+  for (; e < n; e += 256) dst[e] = src[e];
+}
+
 template <int M, bool BWD>
-__global__ __launch_bounds__(256) void hvi_kd(int b, int S, const double* __restrict__ G, HviKd kd,
+__global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const double* __restrict__ G,
+                                              const int* __restrict__ thg, HviKd kd,
                                               const double* __restrict__ gout, double* __restrict__ part,
                                               double* __restrict__ dG) {
   constexpr int NV = BWD ? M + 1 : 1;
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kd_dyn[];
   __shared__ double yv[KD_CT][M];
-  __shared__ int th[KD_CT][M];
+  __shared__ uint4 thp[KD_CT];             // packed 16-bit thresholds (objectives >= M: 1)
   __shared__ double acc[4][KD_CT][NV];     // per-wave accumulators (no inter-wave races)
   __shared__ int wmask[256], wcg[256], scanbuf[256], wsum[4];
-  const int s = blockIdx.y, c0 = blockIdx.x * KD_CT, tid = threadIdx.x;
+  // XCD-aware placement: consecutive workgroups go round-robin over the 8 XCDs, so the
+  // candidate tiles of one sample are remapped onto one XCD (its L2 holds the sample's
+  // keys, ranks and point table once instead of eight times).
+  int s, tile;
+  {
+    const int L = blockIdx.x + ntiles * blockIdx.y;
+    if ((S & 7) == 0) {
+      const int xcd = L & 7, k = L >> 3;
+      s = xcd + 8 * (k / ntiles);
+      tile = k % ntiles;
+    } else {
+      s = blockIdx.y;
+      tile = blockIdx.x;
+    }
+  }
+  const int c0 = tile * KD_CT, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int stride = kd.stride;
   const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
   const int NQ = (Gs + 15) >> 4;
   const KdLds Lo = kd_lds(stride, M, kd.max_groups);
   double* pt = (double*)(kd_dyn + Lo.pt);
-  double* sv = (double*)(kd_dyn + Lo.sv);
   int* r0 = (int*)(kd_dyn + Lo.r0);
   uint4* gb = (uint4*)(kd_dyn + Lo.gb);
   unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
   int* pA = (int*)(kd_dyn + Lo.pA);
 
-  for (int e = tid; e < stride * M; e += 256) {
-    pt[e] = kd.pts[(size_t)s * stride * M + e];
-    sv[e] = kd.sv[(size_t)s * stride * M + e];
-  }
-  for (int e = tid; e < stride; e += 256) r0[e] = kd.rank0[(size_t)s * stride + e];
-  for (int e = tid; e < Gs; e += 256) gb[e] = ((const uint4*)kd.gbox)[gbase + e];
+  kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
+  kd_stage(r0, kd.rank0 + (size_t)s * stride, stride);
+  kd_stage(gb, (const uint4*)kd.gbox + gbase, Gs);
   for (int e = tid; e < KD_CT * M; e += 256) {
-    const int c = e / M, j = e - c * M;
+    const int j = e / KD_CT, c = e - j * KD_CT;
     yv[c][j] = (c0 + c < b) ? G[((size_t)s * M + j) * b + c0 + c] : -INFINITY;
+  }
+  if (tid < KD_CT) {
+    const bool in = c0 + tid < b;
+    unsigned int w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      unsigned int v = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * q + h;
+        const unsigned int t = (j < M) ? (in ? (unsigned int)thg[((size_t)s * M + j) * b + c0 + tid] : 0u) : 1u;
+        v |= t << (16 * h);
+      }
+      w[q] = v;
+    }
+    thp[tid] = make_uint4(w[0], w[1], w[2], w[3]);
   }
   for (int e = tid; e < 4 * KD_CT * NV; e += 256) (&acc[0][0][0])[e] = 0.0;
   __syncthreads();
-  for (int e = tid; e < KD_CT * M; e += 256) {
-    const int c = e / M, j = e - c * M;
-    const double y = yv[c][j];
-    const double* v = sv + (size_t)j * stride;
-    int lo = 0, hi = stride;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (v[mid] <= y) lo = mid + 1;
-      else hi = mid;
-    }
-    th[c][j] = lo;
-  }
-  __syncthreads();
 
-  // ---- A: group filter (lane = candidate) ----
+  // ---- A: group filter (lane = candidate): 4 packed subtractions per group ----
   {
-    int t[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) t[j] = th[lane][j];
+    const uint4 t = thp[lane];
     for (int q = wave; q < NQ; q += 4) {
       unsigned int mask = 0;
       const int gend = min(16, Gs - q * 16);
       for (int k = 0; k < gend; ++k) {
         const uint4 v = gb[q * 16 + k];
-        const unsigned int w[4] = {v.x, v.y, v.z, v.w};
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < M; ++j) ok &= (int)((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) < t[j];
-        mask |= (unsigned int)ok << k;
+        const unsigned int x = kd_lt16(v.x, t.x) & kd_lt16(v.y, t.y) & kd_lt16(v.z, t.z) & kd_lt16(v.w, t.w);
+        mask |= (unsigned int)((x & 0x80008000u) == 0x80008000u) << k;
       }
       mA[q * KD_CT + lane] = (unsigned short)mask;
     }
@@ -426,8 +515,11 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, const double* __rest
   }
   __syncthreads();
 
-  for (int wb = 0; wb < PA; wb += 256) {
-    // ---- B: cell filter (thread = passing (candidate, group) pair) ----
+#ifndef EVR_KD_DBG
+#define EVR_KD_DBG 0
+#endif
+  for (int wb = 0; wb < (EVR_KD_DBG == 1 ? 0 : PA); wb += 256) {
+    // ---- B: cell filter (thread = passing (candidate, group) pair), packed compares ----
     const int p = wb + tid;
     unsigned int mB = 0;
     int cg = 0;
@@ -441,20 +533,27 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, const double* __rest
       const int c = lo / NQ, q = lo - c * NQ;
       const int g = q * 16 + kth_bit16(mA[q * KD_CT + c], p - pA[lo]);
       const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
-      mB = 0xFFFFu;
+      const uint4 tq = thp[c];
+      const unsigned int tw[4] = {tq.x, tq.y, tq.z, tq.w};
+      unsigned int a[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = 0xFFFFFFFFu;
 #pragma unroll
       for (int j = 0; j < M; ++j) {
-        const int tj = th[c][j];
-        const uint4 a = rp[2 * j], bq = rp[2 * j + 1];
-        const unsigned int w[8] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w};
-        unsigned int pass = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          pass |= (unsigned int)((int)(w[i] & 0xFFFFu) < tj) << (2 * i);
-          pass |= (unsigned int)((int)(w[i] >> 16) < tj) << (2 * i + 1);
-        }
-        mB &= pass;
+        const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        const unsigned int tt = th16 | (th16 << 16);
+        const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+        a[0] &= kd_lt16(r1.x, tt);
+        a[1] &= kd_lt16(r1.y, tt);
+        a[2] &= kd_lt16(r1.z, tt);
+        a[3] &= kd_lt16(r1.w, tt);
+        a[4] &= kd_lt16(r2.x, tt);
+        a[5] &= kd_lt16(r2.y, tt);
+        a[6] &= kd_lt16(r2.z, tt);
+        a[7] &= kd_lt16(r2.w, tt);
       }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mB |= (((a[i] >> 15) & 1u) | ((a[i] >> 30) & 2u)) << (2 * i);
       cg = (c << 16) | g;
     }
     wmask[tid] = (int)mB;
@@ -463,7 +562,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, const double* __rest
     scanbuf[tid] = block_scan256(__popc(mB), wsum, &EW);   // exclusive prefixes
     __syncthreads();
     // ---- C: evaluation (thread = exact (cell, candidate) pair) ----
-    for (int cb = 0; cb < EW; cb += 256) {
+    for (int cb = 0; cb < (EVR_KD_DBG == 2 ? 0 : EW); cb += 256) {
       const int q = cb + tid;
       int rcv = -1;
       double val[NV];
@@ -511,18 +610,13 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, const double* __rest
         }
         rcv = c;
       }
-      // wave-level segmented inclusive scan (pairs of a candidate are contiguous; fixed
-      // shuffle tree -> deterministic), segment ends add into this wave's accumulators
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int rup = __shfl_up(rcv, o, 64);
-        const bool same = (lane >= o) && (rup == rcv);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          const double x = __shfl_up(val[v], o, 64);
-          if (same) val[v] += x;
-        }
-      }
+#if EVR_KD_DBG == 3
+      if (rcv >= 0) for (int v = 0; v < NV; ++v) acc[wave][rcv][v] += val[v];
+      continue;
+#endif
+      // wave-level segmented inclusive scan (pairs of a candidate are contiguous) on DPP
+      // moves; segment ends add into this wave's accumulators
+      seg_scan_wave<NV>(rcv, val);
       const int rnext = __shfl_down(rcv, 1, 64);
       if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
 #pragma unroll
@@ -591,15 +685,29 @@ static HviKd hvi_kd_of(const evr_qnehvi_state* st) {
                st->pts_stride, st->max_groups};
 }
 
+// workspace (doubles): S x b partials | S x M x b int thresholds
+static long long hvi_kd_workspace(const evr_qnehvi_state* st, int b) {
+  return (long long)st->S * b + ((long long)st->S * st->m * b + 1) / 2;
+}
+
 template <int M, bool BWD>
 static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
-                         double* part, double* dG) {
+                         double* part, double* dG, const int* flags, double* acq) {
   const KdLds Lo = kd_lds(st->pts_stride, M, st->max_groups);
+  const int ntiles = cdiv(b, KD_CT);
+  int* th = (int*)(part + (size_t)st->S * b);   // workspace tail: S x M x b thresholds
+  hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(b, M, st->pts_stride, G,
+                                                                                     st->sorted_lo, th);
+  EVR_LAUNCH_CHECK();
   EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)Lo.bytes));
-  dim3 grid(cdiv(b, KD_CT), st->S);
-  hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, G, hvi_kd_of(st), gout, part, dG);
+  dim3 grid(ntiles, st->S);
+  hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, G, th, hvi_kd_of(st), gout, part, dG);
   EVR_LAUNCH_CHECK();
+  if (acq) {
+    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, 1, b, M, part, flags, acq);
+    EVR_LAUNCH_CHECK();
+  }
   return 0;
 }
 
@@ -662,7 +770,7 @@ extern "C" {
 
 long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backward) {
   if (!st || b <= 0) return 0;
-  if (st->grp_off) return (long long)st->S * b;
+  if (st->grp_off) return hvi_kd_workspace(st, b);
   HviPlan p = hvi_plan(st, b);
   return (long long)st->S * p.nchunk * b * (backward ? st->m + 1 : 1);
 }
@@ -675,13 +783,10 @@ int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const doubl
   hipStream_t s = (hipStream_t)stream;
   int rc = 0;
   if (st->grp_off) {
-#define L(MM) rc = hvi_kd_launch<MM, false>(s, st, b, G, nullptr, work, nullptr)
+#define L(MM) rc = hvi_kd_launch<MM, false>(s, st, b, G, nullptr, work, nullptr, flags, acq)
     EVR_M_SWITCH(st->m, L);
 #undef L
-    if (rc) return rc;
-    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, 1, b, st->m, work, flags, acq);
-    EVR_LAUNCH_CHECK();
-    return 0;
+    return rc;
   }
   HviPlan p = hvi_plan(st, b);
 #define L(MM) rc = hvi_launch<MM, false>(s, st, b, p, G, work, nullptr)
@@ -701,15 +806,10 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
   hipStream_t s = (hipStream_t)stream;
   if (st->grp_off) {
     int rc = 0;
-#define L(MM) rc = hvi_kd_launch<MM, true>(s, st, b, G, gout, work, dG)
+#define L(MM) rc = hvi_kd_launch<MM, true>(s, st, b, G, gout, work, dG, flags, acq)
     EVR_M_SWITCH(st->m, L);
 #undef L
-    if (rc) return rc;
-    if (acq) {
-      hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, 1, b, st->m, work, flags, acq);
-      EVR_LAUNCH_CHECK();
-    }
-    return 0;
+    return rc;
   }
   HviPlan p = hvi_plan(st, b);
   double* wf = work;

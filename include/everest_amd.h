@@ -135,7 +135,7 @@ typedef struct {
    * when grp_off is not NULL the scan runs the sparse group -> cell -> term filter */
   const int* grp_off;                  /* S + 1: group offsets, 16 cells per group */
   const unsigned long long* grp_keys;  /* grp_off[S]*16 cell keys in kd order */
-  const unsigned short* grp_rank;      /* grp_off[S] x m x 16 per-cell lower-bound ranks (0xFFFF pad) */
+  const unsigned short* grp_rank;      /* grp_off[S] x m x 16 per-cell lower-bound ranks (0x7FFF pad) */
   const unsigned short* grp_box;       /* grp_off[S] x 8: per-group minimum rank per objective */
   const double* sorted_lo;             /* S x m x pts_stride ascending lower-bound values */
   int max_groups;                      /* max_s (grp_off[s+1] - grp_off[s]) */
@@ -229,7 +229,7 @@ int evr_cells_from_keys(void* stream, int S, int m, int stride, const int* off, 
  * Per sample (one workgroup each): rank tables of the point rows per objective, a kd split
  * order of the cells (median split on the objective of largest rank spread, leaves of 16),
  * then per group of 16 cells: the keys (okeys, goff[S]*16), the cells' lower-bound ranks
- * (ork, goff[S] x m x 16 u16, 0xFFFF padding), the group's minimum rank per objective (ogb,
+ * (ork, goff[S] x m x 16 u16, 0x7FFF padding), the group's minimum rank per objective (ogb,
  * goff[S] x 8 u16) and per sample the ascending lower-bound values (osv, S x m x stride).
  * goff[s] = sum_{s'<s} ceil(counts[s'] / 16).  evr_cells_kd_limits returns 0 if max_cells /
  * stride fit the kernel (LDS sort buffer), else 3 (the tiled scan is used then).
