@@ -108,16 +108,14 @@ def step(acqf, Xc, timer=None):
     T = timer
     tk = T.start("kernel_matrix") if T else None
     Kx = gp.cross(Xc)
-    if T: T.stop(tk); tk = T.start("gemm_fwd")
-    R = ops.gemm(acqf.M, Kx)
+    if T: T.stop(tk); tk = T.start("proj_fwd")
+    R, P = ops.qnehvi_project(st, acqf.M, Kx, b)
     if T: T.stop(tk); tk = T.start("samples")
-    G, L22, flags = ops.qnehvi_samples(st, R, b)
+    G, L22, flags = ops.qnehvi_samples_norms(st, R, P, b)
     if T: T.stop(tk); tk = T.start("hvi_fwd_bwd")
     acq, dG = ops.hvi_forward_backward(st, G, b, flags)
-    if T: T.stop(tk); tk = T.start("samples_bwd")
-    gR = ops.qnehvi_samples_backward(st, R, L22, dG, b)
-    if T: T.stop(tk); tk = T.start("gemm_bwd")
-    dKx = ops.gemm(acqf.M, gR, transA=True)
+    if T: T.stop(tk); tk = T.start("proj_bwd")
+    dKx = ops.qnehvi_project_backward(st, acqf.M, R, L22, dG, b)
     if T: T.stop(tk); tk = T.start("kernel_grad")
     dX = ops.kernel_cross_grad(gp.Xn, Xc, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
     if T: T.stop(tk)
@@ -303,8 +301,8 @@ def main():
         dom = max(ktimes, key=ktimes.get)
         work = {
             "hvi_fwd_bwd": ("valu", b * sum_cells * (6 * m + 2), PEAK_FP64_TFLOPS),
-            "gemm_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
-            "gemm_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
+            "proj_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
+            "proj_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
         }
         roof = None
         if dom in work:

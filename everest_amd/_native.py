@@ -87,6 +87,10 @@ _SIGS = {
                                   c_void_p, c_void_p], c_int),
     "evr_cells_from_keys": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int] + [c_void_p] * 5, c_int),
     "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
+    "evr_qnehvi_norms_rows": ([POINTER(EvrQnehviState)], c_int),
+    "evr_qnehvi_project": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 4, c_int),
+    "evr_qnehvi_samples_norms": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
+    "evr_qnehvi_project_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),

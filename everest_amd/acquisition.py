@@ -208,8 +208,8 @@ class QNEHVI:
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
         Kx = self.gp.cross(X)                       # m x n x b
-        R = ops.gemm(self.M, Kx)                    # m x Rr x b
-        G, L22, flags = ops.qnehvi_samples(self.state, R, b)
+        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)    # m x Rr x b + partial norms
+        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
         acq = ops.hvi_forward(self.state, G, b, flags)
         if return_cache:
             return acq, (X, R, G, L22, flags)
@@ -220,11 +220,10 @@ class QNEHVI:
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
         Kx = self.gp.cross(X)
-        R = ops.gemm(self.M, Kx)
-        G, L22, flags = ops.qnehvi_samples(self.state, R, b)
+        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)
+        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
         acq, dG = ops.hvi_forward_backward(self.state, G, b, flags, gout)
-        gR = ops.qnehvi_samples_backward(self.state, R, L22, dG, b)
-        dKx = ops.gemm(self.M, gR, transA=True)     # m x n x b
+        dKx = ops.qnehvi_project_backward(self.state, self.M, R, L22, dG, b)    # m x n x b
         gp = self.gp
         dX = ops.kernel_cross_grad(gp.Xn, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
         return acq, dX

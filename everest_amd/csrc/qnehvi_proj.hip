@@ -1,0 +1,414 @@
+// qNEHVI projection GEMMs with fused prologue / epilogue (gfx950 f64 MFMA).
+//
+// Forward:  R_j = M_j K_x  (M_j = [L^-1; G; H^T; alpha^T], Rr x n; K_x: n x b), as in
+// acquisition.py.  The epilogue also emits, per 64-row tile and candidate, the partial sums
+// of squares of the L^-1 k rows (rows < n) and of the L21 rows (n <= row < n + nb), so the
+// sampling step reads (rows-tiles x 2) partials and the S + 1 sample / mean rows instead of
+// the whole 21 MB R (the old samples kernel re-read all of R with 40 workgroups).
+//
+// Backward: dK_x,j = M_j^T gR_j with gR_j never materialised.  gR_j is, per candidate c,
+//   rows < n:            2 R[i][c] dssv(c)      (var = s^2 (kxx - |L^-1 k|^2))
+//   n <= rows < n + nb:  2 R[i][c] dssw(c)      (L22^2 = var - |L21|^2)
+//   sample rows s:       a_j dG[s][j][c]
+//   mean row:            s_j dmu(c),  dmu = sum_s a_j dG, dl = sum_s a_j dG zq[s][j],
+//                        dbr = dl / (2 L22), dssv = -s^2 dbr, dssw = -dbr.
+// A small kernel reduces dmu, dl over the samples into per-candidate coefficients; the GEMM
+// fetch then generates gR from R, dG and those coefficients — one pass over R and dG, no
+// 21 MB gR write + re-read (the unfused qn_samples_bwd_kernel + gemm^T).  Both GEMMs split K
+// (fixed-order reduction) when their tile grid cannot fill the 256 CUs (small candidate
+// batches: the L-BFGS restarts).
+//
+// Tile: 64 x 64 outputs per 256-thread workgroup, 4 waves x (2 x 2) v_mfma_f64_16x16x4f64,
+// K step 16 staged through LDS, global loads of step t+1 issued before the MFMAs of step t.
+#include <algorithm>
+
+#include "common.hpp"
+#include "../../include/everest_amd.h"
+
+using double4_t = __attribute__((ext_vector_type(4))) double;
+
+namespace evr {
+
+constexpr int PT = 64, PK = 16, PPAD = 16;
+
+// 64 x 64 f64 MFMA tile over k in [kbeg, kend): fa(row, k) / fb(k, col) fetch one element
+// (tile-local row / col); the fetch of step t+1 is issued before the MFMAs of step t.
+// TA: A element (row, k) is contiguous along row (coalesce the A fetch along rows).
+template <bool TA, class FA, class FB>
+__device__ __forceinline__ void proj_tile(int kbeg, int kend, FA fa, FB fb, double4_t (&acc)[4]) {
+  __shared__ double As[PK][PT + PPAD];
+  __shared__ double Bs[PK][PT + PPAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  int am[4], ak[4], bn[4], bk[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = u * 256 + tid;
+    if (TA) { am[u] = e & 63; ak[u] = e >> 6; } else { ak[u] = e & 15; am[u] = e >> 4; }
+    bn[u] = e & 63;
+    bk[u] = e >> 6;
+  }
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + ak[u], kb = k0 + bk[u];
+      ra[u] = (k < kend) ? fa(am[u], k) : 0.0;
+      rb[u] = (kb < kend) ? fb(kb, bn[u]) : 0.0;
+    }
+  };
+  if (kbeg < kend) fetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += PK) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      As[ak[u]][am[u]] = ra[u];
+      Bs[bk[u]][bn[u]] = rb[u];
+    }
+    __syncthreads();
+    if (k0 + PK < kend) fetch(k0 + PK);
+    const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < PK; kk += 4) {
+      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
+      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+}
+
+// visit the tile's outputs: f(local_row, local_col, value) — D map of v_mfma_f64_16x16x4:
+// register r of lane l holds D[(l >> 4) + 4 r][l & 15]
+template <class F>
+__device__ __forceinline__ void proj_for_each(const double4_t (&acc)[4], F f) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int col = lane & 15, rq = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f(wm + (q >> 1) * 16 + rq + 4 * r, wn + (q & 1) * 16 + col, acc[q][r]);
+}
+
+// partial sums of squares of a 64 x 64 tile of R, by row class (cls 0: rows < n, 1: rows in
+// [n, n + nb)), reduced over the tile's rows in a fixed order -> P[j][rt][cls][c]
+__device__ __forceinline__ void proj_norms(const double (&sq)[2][2], int n0, int b, double* __restrict__ Pout) {
+  __shared__ double red[4][32][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, rq = lane >> 4;
+  double v4[2][2];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int cls = 0; cls < 2; ++cls) {
+      double v = sq[ni][cls];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      v4[ni][cls] = v;
+    }
+  if (rq == 0) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      red[wave][ni * 16 + col][0] = v4[ni][0];
+      red[wave][ni * 16 + col][1] = v4[ni][1];
+    }
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int cls = tid >> 6, t = tid & 63;
+    const int h = t >> 5, cw = t & 31;   // waves h (rows 0-31) and h + 2 (rows 32-63) share columns
+    const double v = red[h][cw][cls] + red[h + 2][cw][cls];
+    if (n0 + t < b) Pout[(size_t)cls * b + n0 + t] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// forward: R_j = M_j K_x,j (+ partial norms), optional split-K into W
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qn_proj_fwd(int n, int nb, int Rr, int b, int m, const double* __restrict__ Mm,
+                                                   const double* __restrict__ Kx, double* __restrict__ R,
+                                                   double* __restrict__ P, int nrt, int ksplit, int kchunk,
+                                                   double* __restrict__ W) {
+  const int j = blockIdx.z / ksplit, kz = blockIdx.z - j * ksplit;
+  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
+  const double* A = Mm + (size_t)j * Rr * n;
+  const double* B = Kx + (size_t)j * n * b;
+  double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  const int kbeg = kz * kchunk, kend = min(n, kbeg + kchunk);
+  proj_tile<false>(
+      kbeg, kend, [&](int r, int k) { return (m0 + r < Rr) ? A[(size_t)(m0 + r) * n + k] : 0.0; },
+      [&](int k, int c) { return (n0 + c < b) ? B[(size_t)k * b + n0 + c] : 0.0; }, acc);
+  if (ksplit > 1) {
+    double* Wz = W + ((size_t)kz * m + j) * Rr * b;
+    proj_for_each(acc, [&](int r, int c, double v) {
+      if (m0 + r < Rr && n0 + c < b) Wz[(size_t)(m0 + r) * b + n0 + c] = v;
+    });
+    return;
+  }
+  double* Rj = R + (size_t)j * Rr * b;
+  double sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  proj_for_each(acc, [&](int r, int c, double v) {
+    const int row = m0 + r;
+    if (row < Rr && n0 + c < b) Rj[(size_t)row * b + n0 + c] = v;
+    const int ni = (c & 31) >> 4;
+    if (row < n) sq[ni][0] += v * v;
+    else if (row < n + nb) sq[ni][1] += v * v;
+  });
+  proj_norms(sq, n0, b, P + ((size_t)j * nrt + blockIdx.y) * 2 * b);
+}
+
+// split-K reduction of the forward: R = sum_kz W[kz] (fixed order) + the partial norms
+__global__ __launch_bounds__(256) void qn_proj_fwd_reduce(int n, int nb, int Rr, int b, int m, int ksplit,
+                                                          const double* __restrict__ W, double* __restrict__ R,
+                                                          double* __restrict__ P, int nrt) {
+  const int j = blockIdx.z;
+  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // reuse the MFMA D layout so proj_norms' reduction order applies unchanged
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int col = lane & 15, rq = lane >> 4;
+  double sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  double* Rj = R + (size_t)j * Rr * b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm + (q >> 1) * 16 + rq + 4 * r, c = n0 + wn + (q & 1) * 16 + col;
+      double v = 0.0;
+      if (row < Rr && c < b) {
+        for (int kz = 0; kz < ksplit; ++kz) v += W[(((size_t)kz * m + j) * Rr + row) * b + c];
+        Rj[(size_t)row * b + c] = v;
+      }
+      if (row < n) sq[q & 1][0] += v * v;
+      else if (row < n + nb) sq[q & 1][1] += v * v;
+    }
+  proj_norms(sq, n0, b, P + ((size_t)j * nrt + blockIdx.y) * 2 * b);
+}
+
+// ---------------------------------------------------------------------------------------
+// samples from the partial norms: thread per (candidate, output, chunk of SCH samples)
+// ---------------------------------------------------------------------------------------
+constexpr int SCH = 16;
+
+__global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int m, int b, int nrt_used, int nrt,
+                                                       const double* __restrict__ P, const double* __restrict__ R,
+                                                       const double* __restrict__ cc, const double* __restrict__ ym,
+                                                       const double* __restrict__ ys, const double* __restrict__ kxx,
+                                                       const double* __restrict__ zq, const double* __restrict__ oa,
+                                                       const double* __restrict__ ob, double* __restrict__ G,
+                                                       double* __restrict__ L22, int* __restrict__ flags) {
+  const int c = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y, chunk = blockIdx.z;
+  if (c >= b) return;
+  const long long Rr = (long long)n + nb + S + 1;
+  const double* Pj = P + (size_t)j * nrt * 2 * b;
+  double ssv = 0.0, ssw = 0.0;
+  for (int rt = 0; rt < nrt_used; ++rt) {
+    ssv += Pj[((size_t)rt * 2 + 0) * b + c];
+    ssw += Pj[((size_t)rt * 2 + 1) * b + c];
+  }
+  const double* Rj = R + (size_t)j * Rr * b;
+  const double a = Rj[(size_t)(Rr - 1) * b + c];
+  const double s = ys[j];
+  const double mu = ym[j] + s * (cc[j] + a);
+  const double var = s * s * (kxx[j] - ssv);
+  const double br = var - ssw;
+  // psd_safe_cholesky on the 1x1 block: plain, then total jitter 1e-8*10^(t-1), t=1..6
+  double l22 = nan("");
+  int flag = 1;
+  if (!isnan(br)) {
+    for (int t = 0; t <= 6; ++t) {
+      const double jit = (t == 0) ? 0.0 : 1e-8 * pow(10.0, (double)(t - 1));
+      if (br + jit > 0.0) {
+        l22 = sqrt(br + jit);
+        flag = 0;
+        break;
+      }
+    }
+  }
+  if (chunk == 0) {
+    L22[(size_t)j * b + c] = l22;
+    flags[(size_t)j * b + c] = flag;
+  }
+  const double A = oa[j], B0 = ob[j];
+  const double* h = Rj + (size_t)(n + nb) * b + c;
+  const int s1 = min(S, (chunk + 1) * SCH);
+  for (int si = chunk * SCH; si < s1; ++si) {
+    const double y = mu + h[(size_t)si * b] + l22 * zq[(size_t)si * m + j];
+    G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backward coefficients of gR per (output, candidate): coef[j][0..2][c] =
+// (2 dssv, 2 dssw, s dmu); 64 candidates x 16 sample groups per block, fixed-order sum
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void qn_bwd_coef(int S, int m, int b, const double* __restrict__ dG,
+                                                    const double* __restrict__ L22, const double* __restrict__ ys,
+                                                    const double* __restrict__ zq, const double* __restrict__ oa,
+                                                    double* __restrict__ coef) {
+  __shared__ double red[16][64][2];
+  const int j = blockIdx.y, cx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const double aj = oa[j];
+  double dmu = 0.0, dl = 0.0;
+  if (c < b) {
+    for (int s = g; s < S; s += 16) {
+      const double dy = aj * dG[((size_t)s * m + j) * b + c];
+      dmu += dy;
+      dl = fma(dy, zq[(size_t)s * m + j], dl);
+    }
+  }
+  red[g][cx][0] = dmu;
+  red[g][cx][1] = dl;
+  __syncthreads();
+  if (g == 0 && c < b) {
+    dmu = 0.0;
+    dl = 0.0;
+    for (int q = 0; q < 16; ++q) {
+      dmu += red[q][cx][0];
+      dl += red[q][cx][1];
+    }
+    const double sj = ys[j];
+    const double dbr = dl / (2.0 * L22[(size_t)j * b + c]);
+    coef[((size_t)j * 3 + 0) * b + c] = -2.0 * sj * sj * dbr;
+    coef[((size_t)j * 3 + 1) * b + c] = -2.0 * dbr;
+    coef[((size_t)j * 3 + 2) * b + c] = sj * dmu;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backward: dKx_j = M_j^T gR_j with gR generated in the fetch, optional split-K into W
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int m, int b,
+                                                   const double* __restrict__ Mm, const double* __restrict__ R,
+                                                   const double* __restrict__ dG, const double* __restrict__ oa,
+                                                   const double* __restrict__ coef, double* __restrict__ dK,
+                                                   int ksplit, int kchunk, double* __restrict__ W) {
+  const int j = blockIdx.z / ksplit, kz = blockIdx.z - j * ksplit;
+  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
+  const int Rr = n + nb + S + 1;
+  const double* A = Mm + (size_t)j * Rr * n;   // A(row, k) = M_j[k][row]
+  const double* Rj = R + (size_t)j * Rr * b;
+  const double* cj = coef + (size_t)j * 3 * b;
+  const double aj = oa[j];
+  __shared__ double cf[3][PT];
+  if (threadIdx.x < 3 * PT) {
+    const int q = threadIdx.x / PT, c = threadIdx.x - q * PT;
+    cf[q][c] = (n0 + c < b) ? cj[(size_t)q * b + n0 + c] : 0.0;
+  }
+  __syncthreads();
+  double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  const int kbeg = kz * kchunk, kend = min(Rr, kbeg + kchunk);
+  proj_tile<true>(
+      kbeg, kend, [&](int r, int k) { return (m0 + r < n) ? A[(size_t)k * n + m0 + r] : 0.0; },
+      [&](int k, int c) {
+        if (n0 + c >= b) return 0.0;
+        if (k < n) return Rj[(size_t)k * b + n0 + c] * cf[0][c];
+        if (k < n + nb) return Rj[(size_t)k * b + n0 + c] * cf[1][c];
+        if (k < n + nb + S) return aj * dG[((size_t)(k - n - nb) * m + j) * b + n0 + c];
+        return cf[2][c];
+      },
+      acc);
+  double* out = (ksplit > 1) ? W + ((size_t)kz * m + j) * n * b : dK + (size_t)j * n * b;
+  proj_for_each(acc, [&](int r, int c, double v) {
+    if (m0 + r < n && n0 + c < b) out[(size_t)(m0 + r) * b + n0 + c] = v;
+  });
+}
+
+__global__ __launch_bounds__(256) void qn_splitk_sum(long long per, int ksplit, const double* __restrict__ W,
+                                                     double* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= per) return;
+  double v = 0.0;
+  for (int kz = 0; kz < ksplit; ++kz) v += W[(size_t)kz * per + e];
+  out[e] = v;
+}
+
+// split K when the tile grid cannot fill the chip; each slice keeps >= 8 k-steps
+static int proj_ksplit(int tiles, int K, int* kchunk) {
+  int ks = 1;
+  if (tiles < 512) ks = std::max(1, std::min(std::min(cdiv(1024, tiles), K / (8 * PK)), 32));
+  *kchunk = ks > 1 ? cdiv(cdiv(K, ks), PK) * PK : std::max(K, 1);
+  return ks > 1 ? cdiv(K, *kchunk) : 1;
+}
+
+}  // namespace evr
+
+using namespace evr;
+
+extern "C" {
+
+int evr_qnehvi_norms_rows(const evr_qnehvi_state* st) {
+  if (!st) return 0;
+  return cdiv((long long)st->n + st->nb + st->S + 1, PT);
+}
+
+int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const double* Mm, const double* Kx,
+                       double* R, double* norms) {
+  EVR_CHECK(st && Mm && Kx && R && norms && b >= 0, "evr_qnehvi_project: bad arguments");
+  if (b == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int Rr = st->n + st->nb + st->S + 1;
+  const int nrt = cdiv(Rr, PT);
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * nrt * st->m, st->n, &kchunk);
+  double* W = nullptr;
+  if (ks > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ks * st->m * Rr * b, s));
+  dim3 grid(cdiv(b, PT), nrt, st->m * ks);
+  qn_proj_fwd<<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
+  EVR_LAUNCH_CHECK();
+  if (ks > 1) {
+    qn_proj_fwd_reduce<<<dim3(cdiv(b, PT), nrt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, ks, W, R, norms,
+                                                                       nrt);
+    EVR_LAUNCH_CHECK();
+    EVR_HIP(hipFreeAsync(W, s));
+  }
+  return 0;
+}
+
+int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* norms,
+                             double* G, double* L22, int* flags) {
+  EVR_CHECK(st && R && norms && G && L22 && flags && b >= 0, "evr_qnehvi_samples_norms: bad arguments");
+  if (b == 0) return 0;
+  const int Rr = st->n + st->nb + st->S + 1;
+  const int nrt = cdiv(Rr, PT);
+  const int nrt_used = cdiv(st->n + st->nb, PT);
+  dim3 grid(cdiv(b, 64), st->m, cdiv(st->S, SCH));
+  qn_samples_norms<<<grid, 64, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, nrt_used, nrt, norms, R,
+                                                          st->c, st->ym, st->ys, st->kxx, st->zq, st->obj_a,
+                                                          st->obj_b, G, L22, flags);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
+                                const double* L22, const double* dG, double* dKx) {
+  EVR_CHECK(st && Mm && R && L22 && dG && dKx && b >= 0, "evr_qnehvi_project_backward: bad arguments");
+  if (b == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int Rr = st->n + st->nb + st->S + 1;
+  double* coef = nullptr;
+  EVR_HIP(hipMallocAsync((void**)&coef, sizeof(double) * (size_t)st->m * 3 * b, s));
+  qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
+  EVR_LAUNCH_CHECK();
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
+  double* W = nullptr;
+  if (ks > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ks * st->m * st->n * b, s));
+  dim3 grid(cdiv(b, PT), cdiv(st->n, PT), st->m * ks);
+  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
+  EVR_LAUNCH_CHECK();
+  if (ks > 1) {
+    const long long per = (long long)st->m * st->n * b;
+    qn_splitk_sum<<<cdiv(per, 256), 256, 0, s>>>(per, ks, W, dKx);
+    EVR_LAUNCH_CHECK();
+    EVR_HIP(hipFreeAsync(W, s));
+  }
+  EVR_HIP(hipFreeAsync(coef, s));
+  return 0;
+}
+
+}  // extern "C"

@@ -269,6 +269,37 @@ def qnehvi_samples(st: EvrQnehviState, R: torch.Tensor, b: int):
     return G, L22, flags
 
 
+def qnehvi_project(st: EvrQnehviState, M: torch.Tensor, Kx: torch.Tensor, b: int):
+    """R = M Kx (m x Rr x b) and the partial norms the sampling step needs (one fused GEMM)."""
+    dev = Kx.device
+    Rr = st.n + st.nb + st.S + 1
+    R = torch.empty(st.m, Rr, b, dtype=torch.float64, device=dev)
+    nrt = _native.load().evr_qnehvi_norms_rows(ctypes.byref(st))
+    P = torch.empty(st.m, nrt, 2, b, dtype=torch.float64, device=dev)
+    call("evr_qnehvi_project", _stream(), ctypes.byref(st), b, _dev(M, "M").data_ptr(), _dev(Kx, "Kx").data_ptr(),
+         R.data_ptr(), P.data_ptr())
+    return R, P
+
+
+def qnehvi_samples_norms(st: EvrQnehviState, R: torch.Tensor, P: torch.Tensor, b: int):
+    dev = R.device
+    G = torch.empty(st.S, st.m, b, dtype=torch.float64, device=dev)
+    L22 = torch.empty(st.m, b, dtype=torch.float64, device=dev)
+    flags = torch.empty(st.m, b, dtype=torch.int32, device=dev)
+    call("evr_qnehvi_samples_norms", _stream(), ctypes.byref(st), b, R.data_ptr(), P.data_ptr(), G.data_ptr(),
+         L22.data_ptr(), flags.data_ptr())
+    return G, L22, flags
+
+
+def qnehvi_project_backward(st: EvrQnehviState, M: torch.Tensor, R: torch.Tensor, L22: torch.Tensor,
+                            dG: torch.Tensor, b: int) -> torch.Tensor:
+    """dKx = M^T gR (m x n x b) with gR generated inside the GEMM."""
+    dK = torch.empty(st.m, st.n, b, dtype=torch.float64, device=R.device)
+    call("evr_qnehvi_project_backward", _stream(), ctypes.byref(st), b, M.data_ptr(), R.data_ptr(), L22.data_ptr(),
+         dG.data_ptr(), dK.data_ptr())
+    return dK
+
+
 def _hvi_work(st: EvrQnehviState, b: int, backward: bool, device) -> torch.Tensor:
     n = _native.load().evr_hvi_workspace_doubles(ctypes.byref(st), b, int(backward))
     return torch.empty(max(1, n), dtype=torch.float64, device=device)

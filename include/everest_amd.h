@@ -166,6 +166,22 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);
 
+/* Fused projection path (qnehvi_proj.hip), replacing gemm + evr_qnehvi_samples +
+ * evr_qnehvi_samples_backward + gemm^T:
+ * evr_qnehvi_project: R_j = M_j Kx_j (M: m x Rr x n, Kx: m x n x b, R: m x Rr x b) and the
+ *   per-64-row-tile partial sums of squares norms (m x evr_qnehvi_norms_rows(st) x 2 x b).
+ * evr_qnehvi_samples_norms: G, L22, flags as evr_qnehvi_samples, from R's sample / mean rows
+ *   and the partial norms.
+ * evr_qnehvi_project_backward: dKx_j = M_j^T gR_j (n x b per output) with gR generated in
+ *   the K loop from R, L22 and dG (never written to memory). */
+int evr_qnehvi_norms_rows(const evr_qnehvi_state* st);
+int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const double* M, const double* Kx,
+                       double* R, double* norms);
+int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R,
+                             const double* norms, double* G, double* L22, int* flags);
+int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* M,
+                                const double* R, const double* L22, const double* dG, double* dKx);
+
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+
  * with sd from psd_safe_cholesky (3 tries) of the posterior variance; gR (nullable) =

@@ -1,0 +1,38 @@
+"""GPU: fused qNEHVI projection path (qnehvi_proj.hip) vs the unfused kernels on the same
+state: R = M Kx, partial-norm sampling vs evr_qnehvi_samples, and the backward GEMM with
+generated gR vs evr_qnehvi_samples_backward + M^T gR."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import device_gp, make_problem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,d,m,S,b", [(120, 6, 5, 64, 200), (70, 4, 3, 40, 33), (40, 3, 2, 17, 1)])
+def test_fused_projection_matches_unfused(n, d, m, S, b):
+    from everest_amd import ops
+    from everest_amd.acquisition import QNEHVI
+
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=n + b)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=3, prune_baseline=True,
+               prune_seed=4, prune_samples=256)
+    st = q.state
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b).uniform(size=(b, d)), device="cuda")
+    Kx = gp.cross(Xc)
+    R0 = ops.gemm(q.M, Kx)
+    G0, L0, f0 = ops.qnehvi_samples(st, R0, b)
+    R1, P = ops.qnehvi_project(st, q.M, Kx, b)
+    G1, L1, f1 = ops.qnehvi_samples_norms(st, R1, P, b)
+    assert torch.allclose(R1, R0, rtol=1e-13, atol=1e-14)
+    assert torch.equal(f0, f1)
+    assert torch.allclose(L1, L0, rtol=1e-9, atol=1e-12)
+    assert torch.allclose(G1, G0, rtol=1e-10, atol=1e-12)
+    dG = torch.randn(G0.shape, dtype=torch.float64, device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+    gR = ops.qnehvi_samples_backward(st, R0, L0, dG, b)
+    dK0 = ops.gemm(q.M, gR, transA=True)
+    dK1 = ops.qnehvi_project_backward(st, q.M, R1, L1, dG, b)
+    scale = dK0.abs().max()
+    assert torch.allclose(dK1, dK0, rtol=1e-8, atol=1e-11 * scale)
