@@ -122,6 +122,27 @@ def step(acqf, Xc, timer=None):
     return acq, dX
 
 
+def scan_counts(acqf, Xc):
+    """Exact work of the sparse HVI scan at this batch (device counters of hvi_kd): passing
+    (candidate, group) pairs, evaluated (cell, candidate) terms, (candidate, group) tests."""
+    from everest_amd import ops
+
+    st = acqf.state
+    if not st.grp_off:
+        return {"group_pairs": 0, "terms": 0, "group_tests": 0}
+    b = Xc.shape[0]
+    ctr = torch.zeros(4, dtype=torch.int64, device=Xc.device)
+    R, P = ops.qnehvi_project(st, acqf.M, acqf.gp.cross(Xc), b)
+    G, L22, flags = ops.qnehvi_samples_norms(st, R, P, b)
+    st.scan_counters = ctr.data_ptr()
+    try:
+        ops.hvi_forward_backward(st, G, b, flags)
+        c = ctr.cpu().numpy()
+    finally:
+        st.scan_counters = None
+    return {"group_pairs": int(c[0]), "terms": int(c[1]), "group_tests": int(c[2])}
+
+
 def gp_posterior_ms(device, reps=20):
     """Config 2: SingleTaskGP RBF posterior (mean+var), n_train=256, d=6, 1024 test points."""
     from everest_amd.gp import GPBatch, GPHyper
@@ -294,27 +315,47 @@ def main():
         sum_cells = st.total_cells
         m = args.m
         b = args.b
-        # dominant kernel and its algorithmic work per launch: the dense
-        # reference scan touches every (candidate, cell) pair — min, sub, max, mul per
-        # objective forward; the fused backward adds the prefix/suffix products and the
-        # subgradient FMA (6m + 2 flop per pair in total).
-        dom = max(ktimes, key=ktimes.get)
-        work = {
-            "hvi_fwd_bwd": ("valu", b * sum_cells * (6 * m + 2), PEAK_FP64_TFLOPS),
-            "proj_fwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
-            "proj_bwd": ("mfma", 2.0 * m * acqf.Rr * args.n * b, PEAK_FP64_TFLOPS),
+        # per-kernel rooflines (SURVEY.md §8(d) work per unit x units per launch / launch time)
+        Rr, n, d = acqf.Rr, args.n, args.d
+        nrt = math.ceil(Rr / 64)
+        counts = scan_counts(acqf, Xc)
+        hvi_useful = counts["terms"] * (6 * m + 2)
+        table = {
+            # (bound, work, unit): bytes for HBM-bound kernels, flops otherwise
+            "kernel_matrix": ("hbm", 8.0 * (m * n * b + n * d + b * d + m * d), "B"),
+            "proj_fwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
+            "samples": ("hbm", 8.0 * m * b * (args.S + 1 + 2 * nrt) + 8.0 * args.S * m * b, "B"),
+            "hvi_fwd_bwd": ("valu", float(hvi_useful), "flop"),
+            "proj_bwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
+            "kernel_grad": ("hbm", 8.0 * (m * n * b + n * d + b * d), "B"),
         }
+        kernels = {}
+        for k, (bound, w, unit) in table.items():
+            if k not in ktimes:
+                continue
+            t = ktimes[k] * 1e-3
+            if unit == "B":
+                ach, peak, u = w / t / 1e9, PEAK_HBM_GBS, "GB/s"
+            else:
+                ach, peak, u = w / t / 1e12, PEAK_FP64_TFLOPS, "TFLOP/s"
+            kernels[k] = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": u,
+                          "frac": round(ach / peak, 4), "work_per_launch": w, "launch_ms": round(ktimes[k], 4)}
+        dom = max(ktimes, key=ktimes.get)
         roof = None
-        if dom in work:
-            bound, w, peak = work[dom]
-            ach = w / (ktimes[dom] * 1e-3) / 1e12
-            roof = {"bound": bound, "kernel": dom, "achieved": round(ach, 3), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-                    "algorithmic_work_per_launch": w, "launch_ms": round(ktimes[dom], 4)}
+        if dom in kernels:
+            r = kernels[dom]
+            roof = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"],
+                    "unit": r["unit"], "frac": r["frac"], "traffic": None,
+                    "algorithmic_work_per_launch": r["work_per_launch"], "launch_ms": r["launch_ms"]}
             tr = _traffic(args.traffic_json, dom)
             if tr is not None:
                 roof["traffic"] = tr["bytes_per_launch"]
                 roof["traffic_source"] = tr["source"]
+        if "hvi_fwd_bwd" in kernels:
+            kernels["hvi_fwd_bwd"]["scan"] = {
+                "dense_pairs": b * sum_cells, "group_tests": counts["group_tests"], "group_pairs": counts["group_pairs"],
+                "terms": counts["terms"],
+                "dense_equivalent_TFLOPs": round(b * sum_cells * (6 * m + 2) / (ktimes["hvi_fwd_bwd"] * 1e-3) / 1e12, 2)}
         cpu = None
         if not args.no_cpu_baseline:
             torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -344,6 +385,7 @@ def main():
                        "n_base": acqf.nb, "cells_total": sum_cells, "cells_max": st.max_cells,
                        "parallelism": f"candidate-shard x{world}"},
             "roofline": roof,
+            "kernels": kernels,
             "cpu_baseline": cpu,
             "gp_posterior_ms": round(gp_posterior_ms(device), 4),
             "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},

@@ -33,7 +33,14 @@ class EvrQnehviState(ctypes.Structure):
         ("cell_lo", c_void_p), ("cell_hi", c_void_p), ("cell_off", c_void_p), ("max_cells", c_int),
         ("cell_keys", c_void_p), ("cell_pts", c_void_p), ("cell_rank0", c_void_p), ("pts_stride", c_int),
         ("grp_off", c_void_p), ("grp_keys", c_void_p), ("grp_rank", c_void_p), ("grp_box", c_void_p),
-        ("sorted_lo", c_void_p), ("max_groups", c_int),
+        ("sorted_lo", c_void_p), ("max_groups", c_int), ("scan_counters", c_void_p),
+    ]
+
+
+class EvrQnehviModel(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int), ("d", c_int), ("kind", c_int),
+        ("Xn", c_void_p), ("lengthscales", c_void_p), ("shift", c_void_p), ("scale", c_void_p), ("M", c_void_p),
     ]
 
 
@@ -91,6 +98,12 @@ _SIGS = {
     "evr_qnehvi_project": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 4, c_int),
     "evr_qnehvi_samples_norms": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
     "evr_qnehvi_project_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
+    "evr_qnehvi_plan_workspace_bytes": ([POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_int],
+                                        c_longlong),
+    "evr_qnehvi_plan_create": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_int, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_int, POINTER(c_void_p)], c_int),
+    "evr_qnehvi_plan_run": ([c_void_p, c_void_p], c_int),
+    "evr_qnehvi_plan_destroy": ([c_void_p], None),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),

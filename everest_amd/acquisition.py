@@ -28,7 +28,7 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-from . import ops
+from . import _native, ops
 from .gp import GPBatch
 
 
@@ -194,12 +194,59 @@ class QNEHVI:
         self.state = ops.make_state(n, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
                                     cells)
         self._keep = (self.zq, self.obj_a, self.obj_b)
+        self._lo_c = gp.lo.to(torch.float64).contiguous()
+        self._scale_c = gp.inv_range.to(torch.float64).contiguous()
+        self.model = _native.EvrQnehviModel(n=n, d=gp.d, kind=gp.kind, Xn=gp.Xn.data_ptr(), lengthscales=gp.ls.data_ptr(),
+                                            shift=self._lo_c.data_ptr(), scale=self._scale_c.data_ptr(),
+                                            M=self.M.data_ptr())
+        self._plans = {}
         torch.cuda.synchronize(dev)
         tm["total"] = _time.perf_counter() - t0
         self.timings = tm
 
     # ------------------------------------------------------------------------------------
+    def plan(self, b: int, backward: bool) -> ops.QnehviPlan:
+        """Native evaluation plan for batch size b (cached; hipGraph unless EVR_GRAPH=0)."""
+        key = (int(b), bool(backward))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) >= 8:
+                self._plans.pop(next(iter(self._plans)))
+            p = ops.QnehviPlan(self.state, self.model, int(b), bool(backward), self.dev,
+                               graph=os.environ.get("EVR_GRAPH", "1") != "0")
+            self._plans[key] = p
+        return p
+
     def forward(self, X: torch.Tensor, return_cache: bool = False):
+        """X: b x d raw (transformed) candidates on device -> acquisition values (b), through
+        the native plan (one C-ABI call); see forward_ops for the op-by-op chain."""
+        if return_cache:
+            return self.forward_ops(X, return_cache=True)
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        p = self.plan(X.shape[0], False)
+        p.X.copy_(X)
+        p.run()
+        return p.acq.clone()
+
+    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d)) through the native plan."""
+        if gout is not None:
+            return self.forward_backward_ops(X, gout)
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        p = self.plan(X.shape[0], True)
+        p.X.copy_(X)
+        p.run()
+        return p.acq.clone(), p.dX.clone()
+
+    def eval_host(self, x: np.ndarray, backward: bool):
+        """Host round trip for the scipy optimiser: x (b x d numpy) -> (acq, dX or None)
+        numpy, one pinned H2D copy, one plan launch, one D2H copy."""
+        b = x.shape[0]
+        out = self.plan(b, backward).run_host(x)
+        acq = out[:b].copy()
+        return acq, (out[b:].reshape(b, -1).copy() if backward else None)
+
+    def forward_ops(self, X: torch.Tensor, return_cache: bool = False):
         """X: b x d raw (transformed) candidates on device -> acquisition values (b).
 
         A candidate whose new-point Cholesky block stays not p.d. after the 6-rung jitter
@@ -215,8 +262,8 @@ class QNEHVI:
             return acq, (X, R, G, L22, flags)
         return acq
 
-    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
-        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
+    def forward_backward_ops(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        """Op-by-op chain: returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
         Kx = self.gp.cross(X)

@@ -273,6 +273,7 @@ struct HviKd {
   const int* rank0;
   int stride;
   int max_groups;
+  unsigned long long* counters;
 };
 
 struct KdLds {
@@ -511,7 +512,13 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
       pA[e] = run;
       run += __popc(mA[(e % NQ) * KD_CT + e / NQ]);
     }
-    if (tid == 0) pA[NE] = PA;
+    if (tid == 0) {
+      pA[NE] = PA;
+      if (kd.counters) {
+        atomicAdd(kd.counters + 0, (unsigned long long)PA);
+        atomicAdd(kd.counters + 2, (unsigned long long)min(b - c0, KD_CT) * Gs);
+      }
+    }
   }
   __syncthreads();
 
@@ -560,6 +567,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
     wcg[tid] = cg;
     int EW;
     scanbuf[tid] = block_scan256(__popc(mB), wsum, &EW);   // exclusive prefixes
+    if (kd.counters && tid == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
     __syncthreads();
     // ---- C: evaluation (thread = exact (cell, candidate) pair) ----
     for (int cb = 0; cb < (EVR_KD_DBG == 2 ? 0 : EW); cb += 256) {
@@ -682,7 +690,7 @@ static HviPlan hvi_plan(const evr_qnehvi_state* st, int b) {
 
 static HviKd hvi_kd_of(const evr_qnehvi_state* st) {
   return HviKd{st->grp_off, st->grp_keys, st->grp_rank, st->grp_box, st->sorted_lo, st->cell_pts, st->cell_rank0,
-               st->pts_stride, st->max_groups};
+               st->pts_stride, st->max_groups, st->scan_counters};
 }
 
 // workspace (doubles): S x b partials | S x M x b int thresholds

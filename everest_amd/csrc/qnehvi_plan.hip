@@ -1,0 +1,183 @@
+// Native evaluation plan of the qNEHVI acquisition (q = 1): one C-ABI call runs the whole
+// device chain of QNEHVI.forward / forward_backward (everest_amd/acquisition.py),
+//   K_x = k(X_train, normalize(X))            kernel_matrix.hip
+//   R, norms = M K_x                          qnehvi_proj.hip (fused epilogue)
+//   G, L22, flags                             qnehvi_proj.hip (samples from the norms)
+//   acq (, dG)                                hvi.hip (sparse kd scan or tiled scan)
+//   dK_x = M^T gR (generated)                 qnehvi_proj.hip
+//   dX = sum_j dK_x,j . dk/dx                 kernel_matrix.hip
+// with every intermediate carved from one caller-owned workspace, optionally captured once
+// into a hipGraph and replayed — the L-BFGS restarts of ask() (b = 20) issue one graph
+// launch per iteration instead of a dozen kernel launches through the Python binding.
+// The plan copies the state / model structs; the device buffers they point to, the
+// workspace and the X / output buffers must outlive it (the Python QNEHVI object owns them).
+#include <cstring>
+#include <new>
+
+#include "common.hpp"
+#include "../../include/everest_amd.h"
+
+namespace evr {
+size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b);
+int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* Kx, double* R,
+                 double* norms, double* W);
+size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b);
+int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
+                  const double* L22, const double* dG, double* dKx, double* ws);
+int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
+                  double* L22, int* flags);
+
+struct PlanLayout {
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, bytes;
+};
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, int backward) {
+  PlanLayout L{};
+  const size_t m = st->m, n = st->n, Rr = (size_t)st->n + st->nb + st->S + 1;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t r = o;
+    o += al256(bytes);
+    return r;
+  };
+  L.Kx = take(8 * m * n * b);
+  L.R = take(8 * m * Rr * b);
+  L.P = take(8 * m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b);
+  L.Wf = take(8 * proj_forward_ws_doubles(st, b));
+  L.G = take(8 * (size_t)st->S * m * b);
+  L.L22 = take(8 * m * b);
+  L.flags = take(4 * m * b);
+  L.hvi = take(8 * (size_t)evr_hvi_workspace_doubles(st, b, backward));
+  if (backward) {
+    L.dG = take(8 * (size_t)st->S * m * b);
+    L.bws = take(8 * proj_backward_ws_doubles(st, b));
+    L.dKx = take(8 * m * n * b);
+  }
+  L.bytes = o;
+  (void)md;
+  return L;
+}
+
+}  // namespace evr
+
+using namespace evr;
+
+struct evr_qnehvi_plan {
+  evr_qnehvi_state st;
+  evr_qnehvi_model md;
+  int b, backward;
+  const double* X;
+  unsigned char* work;
+  double* acq;
+  double* dX;
+  PlanLayout L;
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+};
+
+static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
+  const evr_qnehvi_state* st = &p->st;
+  const evr_qnehvi_model* md = &p->md;
+  const int b = p->b, m = st->m, n = st->n, d = md->d;
+  unsigned char* w = p->work;
+  double* Kx = (double*)(w + p->L.Kx);
+  double* R = (double*)(w + p->L.R);
+  double* P = (double*)(w + p->L.P);
+  double* G = (double*)(w + p->L.G);
+  double* L22 = (double*)(w + p->L.L22);
+  int* flags = (int*)(w + p->L.flags);
+  double* hw = (double*)(w + p->L.hvi);
+  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+                                 md->lengthscales, nullptr, nullptr, Kx))
+    return rc;
+  if (int rc = proj_forward(s, st, b, md->M, Kx, R, P, p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr))
+    return rc;
+  if (int rc = samples_norms(s, st, b, R, P, G, L22, flags)) return rc;
+  if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
+  double* dG = (double*)(w + p->L.dG);
+  double* dKx = (double*)(w + p->L.dKx);
+  if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
+  if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;
+  return evr_kernel_cross_grad(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+                               md->lengthscales, nullptr, dKx, p->dX);
+}
+
+extern "C" {
+
+long long evr_qnehvi_plan_workspace_bytes(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                                          int backward) {
+  if (!st || !md || b <= 0) return 0;
+  return (long long)plan_layout(st, md, b, backward).bytes;
+}
+
+int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                           int backward, const double* X, void* work, double* acq, double* dX, int use_graph,
+                           evr_qnehvi_plan** out) {
+  EVR_CHECK(st && md && out && X && work && acq && b >= 1 && (!backward || dX) && md->M && md->Xn &&
+                md->lengthscales && md->n == st->n && md->d >= 1 && md->kind >= 0 && md->kind <= 3,
+            "evr_qnehvi_plan_create: bad arguments");
+  evr_qnehvi_plan* p = new (std::nothrow) evr_qnehvi_plan();
+  EVR_CHECK(p, "evr_qnehvi_plan_create: out of host memory");
+  p->st = *st;
+  p->md = *md;
+  p->b = b;
+  p->backward = backward ? 1 : 0;
+  p->X = X;
+  p->work = (unsigned char*)work;
+  p->acq = acq;
+  p->dX = dX;
+  p->L = plan_layout(st, md, b, p->backward);
+  p->graph = nullptr;
+  p->exec = nullptr;
+  if (use_graph) {
+    hipStream_t s = (hipStream_t)stream;
+    // capture on a private stream so the caller's stream (torch's) never enters capture mode
+    hipStream_t cs = nullptr;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
+      delete p;
+      EVR_CHECK(false, "evr_qnehvi_plan_create: hipStreamCreate failed");
+    }
+    int rc = 0;
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = 1;
+    if (!rc) rc = plan_chain(cs, p);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(cs, &g);
+    if (!rc && e == hipSuccess && g) {
+      if (hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0) == hipSuccess) p->graph = g;
+      else rc = 1;
+    } else {
+      rc = rc ? rc : 1;
+    }
+    (void)hipStreamDestroy(cs);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      delete p;
+      const std::string why = last_error();
+      EVR_CHECK(false, "evr_qnehvi_plan_create: graph capture failed (%s)", why.c_str());
+    }
+    (void)s;
+  }
+  *out = p;
+  return 0;
+}
+
+int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
+  EVR_CHECK(p, "evr_qnehvi_plan_run: null plan");
+  hipStream_t s = (hipStream_t)stream;
+  if (p->exec) {
+    EVR_HIP(hipGraphLaunch(p->exec, s));
+    return 0;
+  }
+  return plan_chain(s, p);
+}
+
+void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
+  if (!p) return;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  delete p;
+}
+
+}  // extern "C"

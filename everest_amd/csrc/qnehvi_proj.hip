@@ -335,6 +335,74 @@ static int proj_ksplit(int tiles, int K, int* kchunk) {
   return ks > 1 ? cdiv(K, *kchunk) : 1;
 }
 
+// ---- internal launchers (workspace supplied by the caller; qnehvi_plan.hip) ----------
+size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b) {
+  const int Rr = st->n + st->nb + st->S + 1;
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(Rr, PT) * st->m, st->n, &kchunk);
+  return ks > 1 ? (size_t)ks * st->m * Rr * b : 0;
+}
+
+int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* Kx, double* R,
+                 double* norms, double* W) {
+  if (b == 0) return 0;
+  const int Rr = st->n + st->nb + st->S + 1;
+  const int nrt = cdiv(Rr, PT);
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * nrt * st->m, st->n, &kchunk);
+  EVR_CHECK(ks == 1 || W, "proj_forward: split-K workspace missing");
+  dim3 grid(cdiv(b, PT), nrt, st->m * ks);
+  qn_proj_fwd<<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
+  EVR_LAUNCH_CHECK();
+  if (ks > 1) {
+    qn_proj_fwd_reduce<<<dim3(cdiv(b, PT), nrt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, ks, W, R, norms,
+                                                                       nrt);
+    EVR_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b) {
+  const int Rr = st->n + st->nb + st->S + 1;
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
+  return (size_t)st->m * 3 * b + (ks > 1 ? (size_t)ks * st->m * st->n * b : 0);
+}
+
+int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
+                  const double* L22, const double* dG, double* dKx, double* ws) {
+  if (b == 0) return 0;
+  const int Rr = st->n + st->nb + st->S + 1;
+  double* coef = ws;
+  qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
+  EVR_LAUNCH_CHECK();
+  int kchunk = 0;
+  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
+  double* W = ws + (size_t)st->m * 3 * b;
+  dim3 grid(cdiv(b, PT), cdiv(st->n, PT), st->m * ks);
+  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
+  EVR_LAUNCH_CHECK();
+  if (ks > 1) {
+    const long long per = (long long)st->m * st->n * b;
+    qn_splitk_sum<<<cdiv(per, 256), 256, 0, s>>>(per, ks, W, dKx);
+    EVR_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
+                  double* L22, int* flags) {
+  if (b == 0) return 0;
+  const int Rr = st->n + st->nb + st->S + 1;
+  const int nrt = cdiv(Rr, PT);
+  const int nrt_used = cdiv(st->n + st->nb, PT);
+  dim3 grid(cdiv(b, 64), st->m, cdiv(st->S, SCH));
+  qn_samples_norms<<<grid, 64, 0, s>>>(st->n, st->nb, st->S, st->m, b, nrt_used, nrt, norms, R, st->c, st->ym, st->ys,
+                                        st->kxx, st->zq, st->obj_a, st->obj_b, G, L22, flags);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace evr
 
 using namespace evr;
@@ -351,37 +419,18 @@ int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const do
   EVR_CHECK(st && Mm && Kx && R && norms && b >= 0, "evr_qnehvi_project: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int Rr = st->n + st->nb + st->S + 1;
-  const int nrt = cdiv(Rr, PT);
-  int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * nrt * st->m, st->n, &kchunk);
+  const size_t wn = proj_forward_ws_doubles(st, b);
   double* W = nullptr;
-  if (ks > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ks * st->m * Rr * b, s));
-  dim3 grid(cdiv(b, PT), nrt, st->m * ks);
-  qn_proj_fwd<<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
-  EVR_LAUNCH_CHECK();
-  if (ks > 1) {
-    qn_proj_fwd_reduce<<<dim3(cdiv(b, PT), nrt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, ks, W, R, norms,
-                                                                       nrt);
-    EVR_LAUNCH_CHECK();
-    EVR_HIP(hipFreeAsync(W, s));
-  }
-  return 0;
+  if (wn) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * wn, s));
+  const int rc = proj_forward(s, st, b, Mm, Kx, R, norms, W);
+  if (W) EVR_HIP(hipFreeAsync(W, s));
+  return rc;
 }
 
 int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* norms,
                              double* G, double* L22, int* flags) {
   EVR_CHECK(st && R && norms && G && L22 && flags && b >= 0, "evr_qnehvi_samples_norms: bad arguments");
-  if (b == 0) return 0;
-  const int Rr = st->n + st->nb + st->S + 1;
-  const int nrt = cdiv(Rr, PT);
-  const int nrt_used = cdiv(st->n + st->nb, PT);
-  dim3 grid(cdiv(b, 64), st->m, cdiv(st->S, SCH));
-  qn_samples_norms<<<grid, 64, 0, (hipStream_t)stream>>>(st->n, st->nb, st->S, st->m, b, nrt_used, nrt, norms, R,
-                                                          st->c, st->ym, st->ys, st->kxx, st->zq, st->obj_a,
-                                                          st->obj_b, G, L22, flags);
-  EVR_LAUNCH_CHECK();
-  return 0;
+  return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags);
 }
 
 int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
@@ -389,26 +438,11 @@ int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b,
   EVR_CHECK(st && Mm && R && L22 && dG && dKx && b >= 0, "evr_qnehvi_project_backward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int Rr = st->n + st->nb + st->S + 1;
-  double* coef = nullptr;
-  EVR_HIP(hipMallocAsync((void**)&coef, sizeof(double) * (size_t)st->m * 3 * b, s));
-  qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
-  EVR_LAUNCH_CHECK();
-  int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
-  double* W = nullptr;
-  if (ks > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ks * st->m * st->n * b, s));
-  dim3 grid(cdiv(b, PT), cdiv(st->n, PT), st->m * ks);
-  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
-  EVR_LAUNCH_CHECK();
-  if (ks > 1) {
-    const long long per = (long long)st->m * st->n * b;
-    qn_splitk_sum<<<cdiv(per, 256), 256, 0, s>>>(per, ks, W, dKx);
-    EVR_LAUNCH_CHECK();
-    EVR_HIP(hipFreeAsync(W, s));
-  }
-  EVR_HIP(hipFreeAsync(coef, s));
-  return 0;
+  double* ws = nullptr;
+  EVR_HIP(hipMallocAsync((void**)&ws, sizeof(double) * proj_backward_ws_doubles(st, b), s));
+  const int rc = proj_backward(s, st, b, Mm, R, L22, dG, dKx, ws);
+  EVR_HIP(hipFreeAsync(ws, s));
+  return rc;
 }
 
 }  // extern "C"

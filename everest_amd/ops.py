@@ -300,6 +300,50 @@ def qnehvi_project_backward(st: EvrQnehviState, M: torch.Tensor, R: torch.Tensor
     return dK
 
 
+class QnehviPlan:
+    """Native evaluation plan of the whole qNEHVI chain for a fixed batch size b
+    (qnehvi_plan.hip): persistent device buffers X (b x d), out = [acq (b) | dX (b x d)] and
+    the workspace; run() is one C-ABI call (one hipGraph launch when ``graph``)."""
+
+    def __init__(self, st: EvrQnehviState, model: "_native.EvrQnehviModel", b: int, backward: bool, device,
+                 graph: bool = True):
+        lib = _native.load()
+        d = int(model.d)
+        self.b, self.d, self.backward = int(b), d, bool(backward)
+        self.X = torch.zeros(b, d, dtype=torch.float64, device=device)
+        self.out = torch.empty(b * (1 + d), dtype=torch.float64, device=device)
+        nbytes = lib.evr_qnehvi_plan_workspace_bytes(ctypes.byref(st), ctypes.byref(model), b, int(backward))
+        self.work = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        self.acq = self.out[:b]
+        self.dX = self.out[b:].view(b, d)
+        self.host = torch.empty(b * (1 + d), dtype=torch.float64, pin_memory=True)
+        self.xhost = torch.empty(b, d, dtype=torch.float64, pin_memory=True)
+        h = ctypes.c_void_p()
+        call("evr_qnehvi_plan_create", _stream(), ctypes.byref(st), ctypes.byref(model), b, int(backward),
+             self.X.data_ptr(), self.work.data_ptr(), self.acq.data_ptr(),
+             self.dX.data_ptr() if backward else None, int(graph), ctypes.byref(h))
+        self._h = h
+        self._lib = lib
+
+    def run(self):
+        call("evr_qnehvi_plan_run", _stream(), self._h)
+
+    def run_host(self, x: np.ndarray) -> np.ndarray:
+        """x (b x d numpy) -> host copy of [acq | dX] (one H2D, one graph launch, one D2H)."""
+        self.xhost.numpy()[...] = x
+        self.X.copy_(self.xhost, non_blocking=True)
+        self.run()
+        self.host.copy_(self.out, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return self.host.numpy()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.evr_qnehvi_plan_destroy(h)
+            self._h = None
+
+
 def _hvi_work(st: EvrQnehviState, b: int, backward: bool, device) -> torch.Tensor:
     n = _native.load().evr_hvi_workspace_doubles(ctypes.byref(st), b, int(backward))
     return torch.empty(max(1, n), dtype=torch.float64, device=device)

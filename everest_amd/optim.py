@@ -272,7 +272,10 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         counter = {"n": 0}
 
         def f(x):
-            if local_world == 1:
+            if local_world == 1 and hasattr(acqf, "eval_host"):
+                a, g = acqf.eval_host(x.reshape(nb, d), True)
+                a = host_values(torch.from_numpy(a))
+            elif local_world == 1:
                 Xt = torch.as_tensor(x.reshape(nb, d), dtype=torch.float64, device=dev)
                 a, g = acqf.forward_backward(Xt)
                 a, g = host_values(a), g.cpu().numpy()

@@ -139,6 +139,9 @@ typedef struct {
   const unsigned short* grp_box;       /* grp_off[S] x 8: per-group minimum rank per objective */
   const double* sorted_lo;             /* S x m x pts_stride ascending lower-bound values */
   int max_groups;                      /* max_s (grp_off[s+1] - grp_off[s]) */
+  /* optional scan statistics (nullable, device): [0] += passing (candidate, group) pairs,
+   * [1] += exact (cell, candidate) terms evaluated, [2] += (candidate, group) tests */
+  unsigned long long* scan_counters;
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b
@@ -181,6 +184,31 @@ int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, co
                              const double* norms, double* G, double* L22, int* flags);
 int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* M,
                                 const double* R, const double* L22, const double* dG, double* dKx);
+
+/* Native evaluation plan of the whole qNEHVI chain (qnehvi_plan.hip): K_x, fused projection,
+ * samples, HVI scan (+ backward: projection^T with generated gR, cross-covariance gradient)
+ * in one call, every intermediate carved from `work`, optionally captured into a hipGraph
+ * (use_graph) and replayed by evr_qnehvi_plan_run.  X: b x d raw (transformed) candidates;
+ * acq: b; dX: b x d (backward).  The plan copies *st / *md; the buffers they and X / work /
+ * acq / dX point to must outlive the plan.
+ * Replaces one [upstream] qNoisyExpectedHypervolumeImprovement forward (+ autograd backward)
+ * call of gen_candidates_scipy (bofire/strategies/predictives/botorch.py:384-405). */
+typedef struct {
+  int n, d, kind;              /* training points, input dims, EVR_KERNEL_* */
+  const double* Xn;            /* n x d normalized training inputs */
+  const double* lengthscales;  /* m x d */
+  const double* shift;         /* d: Normalize lower bounds (candidates arrive raw) */
+  const double* scale;         /* d: 1 / (upper - lower) */
+  const double* M;             /* m x (n + nb + S + 1) x n forward operator [Linv; G; H^T; alpha^T] */
+} evr_qnehvi_model;
+typedef struct evr_qnehvi_plan evr_qnehvi_plan;
+long long evr_qnehvi_plan_workspace_bytes(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                                          int backward);
+int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                           int backward, const double* X, void* work, double* acq, double* dX, int use_graph,
+                           evr_qnehvi_plan** out);
+int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* plan);
+void evr_qnehvi_plan_destroy(evr_qnehvi_plan* plan);
 
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+

@@ -36,3 +36,26 @@ def test_fused_projection_matches_unfused(n, d, m, S, b):
     dK1 = ops.qnehvi_project_backward(st, q.M, R1, L1, dG, b)
     scale = dK0.abs().max()
     assert torch.allclose(dK1, dK0, rtol=1e-8, atol=1e-11 * scale)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_native_plan_matches_op_chain(graph, monkeypatch):
+    """evr_qnehvi_plan (one C-ABI call, hipGraph replay) == the op-by-op chain, bitwise (same
+    kernels, same order, deterministic reductions); repeated runs reuse the captured graph."""
+    from everest_amd.acquisition import QNEHVI
+
+    monkeypatch.setenv("EVR_GRAPH", "1" if graph else "0")
+    n, d, m, S = 90, 5, 4, 48
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=33)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=5, prune_baseline=True,
+               prune_seed=6, prune_samples=256)
+    rng = np.random.default_rng(0)
+    for b in (20, 20, 130, 1):
+        Xc = torch.tensor(lo + (hi - lo) * rng.uniform(size=(b, d)), device="cuda")
+        a0, g0 = q.forward_backward_ops(Xc)
+        a1, g1 = q.forward_backward(Xc)
+        assert torch.equal(a0, a1) and torch.equal(g0, g1)
+        assert torch.equal(q.forward(Xc), q.forward_ops(Xc))
+        ah, gh = q.eval_host(Xc.cpu().numpy(), True)
+        assert np.array_equal(ah, a0.cpu().numpy()) and np.array_equal(gh, g0.cpu().numpy())

@@ -18,21 +18,26 @@ import sys
 from collections import defaultdict
 
 OPS = {
-    "hvi_fwd_bwd": [r"hvi_tiled<\d+, \d+, true, true>", r"hvi_reduce_fwd", r"hvi_reduce_bwd"],
     "kernel_matrix": [r"kmat_kernel"],
-    "samples": [r"qn_samples_kernel"],
-    "samples_bwd": [r"qn_samples_bwd_kernel"],
+    "proj_fwd": [r"qn_proj_fwd\(", r"qn_proj_fwd_reduce"],
+    "samples": [r"qn_samples_norms"],
+    "hvi_fwd_bwd": [r"hvi_thresholds", r"hvi_kd<", r"hvi_tiled<\d+, \d+, (true|false), true>", r"hvi_reduce_fwd",
+                    r"hvi_reduce_bwd"],
+    "proj_bwd": [r"qn_bwd_coef", r"qn_proj_bwd", r"qn_splitk_sum"],
+    "kernel_grad": [r"kcross_grad_kernel"],
 }
+LAST = int(os.environ.get("PMC_LAST", "10"))   # tools/loop_step.py: the last N dispatches are the steps
 
 
 def per_kernel(d, counter):
     vals = defaultdict(list)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if row.get("Counter_Name") != counter:
-                    continue
-                vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+            rows = [r for r in csv.DictReader(f) if r.get("Counter_Name") == counter]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        for row in rows:
+            vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    vals = {k: v[-LAST:] for k, v in vals.items()}
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
 
