@@ -8,7 +8,9 @@ U[0,1]^6 (n=512, seed 0), noise-free Y, reference point 1.1 -> -1.1 in objective
 BoFire builds it (prune_baseline with 2048 samples, cached root, S=256 Sobol-normal base
 samples), q=1.  A *step* = one acquisition evaluation pass (forward + analytic backward,
 the unit raw screening and the L-BFGS restarts of ask() are made of) over one batch of
-b=512 Sobol candidates already resident in HBM.
+b=512 Sobol candidates already resident in HBM, run through the native evaluation plan
+(everest_amd/csrc/qnehvi_plan.hip — the path ask() uses); the per-kernel breakdown comes
+from a separate instrumented pass over the same kernels launched one by one.
 
 Multi-GPU (torchrun, one process per GPU, RCCL): every rank evaluates its own 512-candidate
 shard (weak scaling); each step ends with the RCCL all-gather of the per-shard acquisition
@@ -278,8 +280,17 @@ def main():
     Xc = candidates(args.b, args.d, seed=2 + rank, device=device)
     gathered = [torch.empty(args.b, dtype=torch.float64, device=device) for _ in range(world)]
 
+    # production path: the native evaluation plan (whole chain in one C-ABI call / hipGraph),
+    # candidates already resident in its HBM input buffer
+    plan = acqf.plan(args.b, True)
+    plan.X.copy_(Xc)
+
     def one_step(timer=None):
-        acq, dX = step(acqf, Xc, timer)
+        if timer is None:
+            plan.run()
+            acq = plan.acq
+        else:                       # instrumented op-by-op chain (same kernels) for the breakdown
+            acq, _ = step(acqf, Xc, timer)
         if dist is not None:
             dist.all_gather(gathered, acq)
         return acq

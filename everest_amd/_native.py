@@ -50,7 +50,8 @@ _SIGS = {
     "evr_device_arch": ([c_int, c_char_p, c_int], c_int),
     "evr_stream_sync": ([c_void_p], c_int),
     "evr_kernel_matrix": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 10, c_int),
-    "evr_kernel_cross_grad": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 10, c_int),
+    "evr_kernel_cross_grad": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 11, c_int),
+    "evr_kernel_cross_grad_workspace_doubles": ([c_int, c_int, c_int], c_longlong),
     "evr_kernel_lengthscale_grad": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p], c_int),
     "evr_gp_mll_terms": ([c_void_p, c_int, c_int] + [c_void_p] * 5, c_int),
@@ -95,9 +96,11 @@ _SIGS = {
     "evr_cells_from_keys": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int] + [c_void_p] * 5, c_int),
     "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
     "evr_qnehvi_norms_rows": ([POINTER(EvrQnehviState)], c_int),
-    "evr_qnehvi_project": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 4, c_int),
+    "evr_qnehvi_project": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
+    "evr_qnehvi_project_workspace_doubles": ([POINTER(EvrQnehviState), c_int], c_longlong),
     "evr_qnehvi_samples_norms": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
-    "evr_qnehvi_project_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
+    "evr_qnehvi_project_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
+    "evr_qnehvi_project_backward_workspace_doubles": ([POINTER(EvrQnehviState), c_int], c_longlong),
     "evr_qnehvi_plan_workspace_bytes": ([POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_int],
                                         c_longlong),
     "evr_qnehvi_plan_create": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_int, c_void_p,

@@ -44,6 +44,14 @@ const char* last_error();
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// XCD-aware workgroup order (bijective for any nwg): consecutive blocks are dealt
+// round-robin over the 8 XCDs, so give every XCD a contiguous chunk of the tile grid
+// (neighbouring tiles share operand panels -> L2 hits).  Returns the tile index.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // Kernel families (same numbering as include/everest_amd.h EVR_KERNEL_*).
 enum KernelKind { RBF = 0, MATERN05 = 1, MATERN15 = 2, MATERN25 = 3 };
 

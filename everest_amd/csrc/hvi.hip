@@ -215,8 +215,10 @@ __global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, 
   const int c = blockIdx.x * 16 + cx;
   const int tot = S * nchunk;
   double sum = 0.0;
-  if (c < b)
+  if (c < b) {
+#pragma unroll 8
     for (int k = g; k < tot; k += 16) sum += work[(size_t)k * b + c];
+  }
   red[g][cx] = sum;
   __syncthreads();
   for (int o = 8; o > 0; o >>= 1) {

@@ -6,6 +6,8 @@
 // (rows ty+16a, cols tx+16c) so that each store instruction writes 16 consecutive
 // doubles of a row.  Distances are formed from explicit differences (no x^2+x'^2-2xx'
 // cancellation).  HBM-bound for small d: 8 bytes written per entry.
+#include <algorithm>
+
 #include "common.hpp"
 #include "../../include/everest_amd.h"
 
@@ -85,9 +87,13 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
   }
 }
 
-// dX2[c][k] = sum_b sum_i G[b][i][c] * dk_b(x1_i, x2_c)/dx2_ck ; one workgroup per c.
+// dX2[c][k] = sum_b sum_i G[b][i][c] * dk_b(x1_i, x2_c)/dx2_ck.
+// Block = 64 candidates (lanes; G rows read coalesced, candidates fastest) x 4 row groups
+// (waves; all lanes of a wave share the training row -> broadcast loads); the rows are
+// split over gridDim.y blocks, the per-split partials part[split][c][k] summed in a fixed
+// order by kcross_grad_reduce (bitwise reproducible).
 template <int MAXD>
-__global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d,
+__global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d, int rows_per,
                                                           const double* __restrict__ X1,
                                                           const double* __restrict__ sh1,
                                                           const double* __restrict__ sc1,
@@ -96,65 +102,107 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
                                                           const double* __restrict__ sc2,
                                                           const double* __restrict__ ls,
                                                           const double* __restrict__ os,
-                                                          const double* __restrict__ G, double* __restrict__ dX2) {
-  const int c = blockIdx.x;
-  const int tid = threadIdx.x;
-  __shared__ double red[256];
+                                                          const double* __restrict__ G, double* __restrict__ part) {
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const int split = blockIdx.y;
+  const int i0 = split * rows_per, i1 = min(n1, i0 + rows_per);
+  __shared__ double red[4][64][MAXD];
   double x2[MAXD];
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) {
-    if (k < d) {
-      double w = X2[(size_t)c * d + k];
+    double w = 0.0;
+    if (k < d && c < n2) {
+      w = X2[(size_t)c * d + k];
       if (sh2) w -= sh2[k];
       if (sc2) w *= sc2[k];
-      x2[k] = w;
     }
+    x2[k] = w;
   }
   double acc[MAXD];
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) acc[k] = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const double* lsb = ls + (size_t)b * d;
-    const double scale = os ? os[b] : 1.0;
-    const double* Gb = G + (size_t)b * n1 * n2;
-    for (int i = tid; i < n1; i += 256) {
-      const double g = Gb[(size_t)i * n2 + c];
-      if (g == 0.0) continue;
-      double diff[MAXD];
-      double d2 = 0.0;
+  if (c < n2) {
+    for (int b = 0; b < B; ++b) {
+      const double* lsb = ls + (size_t)b * d;
+      const double scale = os ? os[b] : 1.0;
+      const double* Gb = G + (size_t)b * n1 * n2;
+      double il[MAXD];
 #pragma unroll
-      for (int k = 0; k < MAXD; ++k) {
-        if (k < d) {
-          double v = X1[(size_t)i * d + k];
-          if (sh1) v -= sh1[k];
-          if (sc1) v *= sc1[k];
-          const double il = 1.0 / lsb[k];
-          const double df = (x2[k] - v) * il;
-          diff[k] = df * il;  // (x2 - x1)/ls^2
-          d2 = fma(df, df, d2);
+      for (int k = 0; k < MAXD; ++k) il[k] = (k < d) ? 1.0 / lsb[k] : 0.0;
+      for (int i = i0 + ry; i < i1; i += 4) {
+        const double g = Gb[(size_t)i * n2 + c];
+        double diff[MAXD];
+        double d2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) {
+          if (k < d) {
+            double v = X1[(size_t)i * d + k];
+            if (sh1) v -= sh1[k];
+            if (sc1) v *= sc1[k];
+            const double df = (x2[k] - v) * il[k];
+            diff[k] = df * il[k];  // (x2 - x1)/ls^2
+            d2 = fma(df, df, d2);
+          }
         }
+        const double sgl = g * scale * kernel_dscale(kind, d2);
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k)
+          if (k < d) acc[k] = fma(sgl, diff[k], acc[k]);
       }
-      const double s = g * scale * kernel_dscale(kind, d2);
-#pragma unroll
-      for (int k = 0; k < MAXD; ++k)
-        if (k < d) acc[k] = fma(s, diff[k], acc[k]);
     }
   }
-  // block reduction per dim
-  for (int k = 0; k < d; ++k) {
-    double v = 0.0;
 #pragma unroll
-    for (int kk = 0; kk < MAXD; ++kk)
-      if (kk == k) v = acc[kk];
-    red[tid] = v;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
+  for (int k = 0; k < MAXD; ++k) red[ry][cx][k] = acc[k];
+  __syncthreads();
+  if (ry == 0 && c < n2) {
+    for (int k = 0; k < d; ++k) {
+      const double v = ((red[0][cx][k] + red[1][cx][k]) + red[2][cx][k]) + red[3][cx][k];
+      part[((size_t)split * n2 + c) * d + k] = v;
     }
-    if (tid == 0) dX2[(size_t)c * d + k] = red[0] * (sc2 ? sc2[k] : 1.0);
-    __syncthreads();
   }
+}
+
+__global__ void kcross_grad_reduce(int nsplit, int n2, int d, const double* __restrict__ part,
+                                   const double* __restrict__ sc2, double* __restrict__ dX2) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)n2 * d) return;
+  const int k = (int)(e % d);
+  double v = 0.0;
+#pragma unroll 8
+  for (int sp = 0; sp < nsplit; ++sp) v += part[(size_t)sp * n2 * d + e];   // loads issued ahead
+  dX2[e] = v * (sc2 ? sc2[k] : 1.0);
+}
+
+// row split of kcross_grad: fill >= 512 blocks, >= 16 rows per block
+static int kcross_nsplit(int n1, int n2) {
+  const int ct = cdiv(n2, 64);
+  int ns = cdiv(512, ct);
+  ns = std::max(1, std::min(ns, cdiv(n1, 16)));
+  return ns;
+}
+
+size_t kcross_grad_ws_doubles(int n1, int n2, int d) { return (size_t)kcross_nsplit(n1, n2) * n2 * d; }
+
+int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
+                       const double* scale1, const double* X2, const double* shift2, const double* scale2,
+                       const double* lengthscales, const double* outputscale, const double* G, double* dX2,
+                       double* work) {
+  const int ns = kcross_nsplit(n1, n2);
+  const int rows_per = cdiv(n1, ns);
+  dim3 grid(cdiv(n2, 64), ns);
+#define LAUNCH(MD)                                                                                         \
+  kcross_grad_kernel<MD><<<grid, 256, 0, s>>>(kind, B, n1, n2, d, rows_per, X1, shift1, scale1, X2, shift2, \
+                                              scale2, lengthscales, outputscale, G, work)
+  if (d <= 8) LAUNCH(8);
+  else if (d <= 16) LAUNCH(16);
+  else if (d <= 32) LAUNCH(32);
+  else LAUNCH(64);
+#undef LAUNCH
+  EVR_LAUNCH_CHECK();
+  kcross_grad_reduce<<<cdiv((long long)n2 * d, 256), 256, 0, s>>>(ns, n2, d, work, scale2, dX2);
+  EVR_LAUNCH_CHECK();
+  return 0;
 }
 
 // part[b][i][k] = sum_j W[b][i][j] * dK_b[i][j]/dls_k, dK/dls_k = -dscale * diff_k^2 / ls_k^3
@@ -304,20 +352,20 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
 int evr_kernel_cross_grad(void* stream, int kind, int B, int n1, int n2, int d, const double* X1,
                           const double* shift1, const double* scale1, const double* X2, const double* shift2,
                           const double* scale2, const double* lengthscales, const double* outputscale,
-                          const double* G, double* dX2) {
+                          const double* G, double* dX2, double* work) {
   EVR_CHECK(kind >= 0 && kind <= 3 && B >= 1 && d >= 1 && d <= KMAXD, "evr_kernel_cross_grad: bad args");
   if (n2 == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-#define LAUNCH(MD)                                                                                       \
-  kcross_grad_kernel<MD><<<n2, 256, 0, s>>>(kind, B, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                            lengthscales, outputscale, G, dX2)
-  if (d <= 8) LAUNCH(8);
-  else if (d <= 16) LAUNCH(16);
-  else if (d <= 32) LAUNCH(32);
-  else LAUNCH(64);
-#undef LAUNCH
-  EVR_LAUNCH_CHECK();
-  return 0;
+  const bool own = work == nullptr;
+  if (own) EVR_HIP(hipMallocAsync((void**)&work, sizeof(double) * kcross_grad_ws_doubles(n1, n2, d), s));
+  const int rc = kcross_grad_launch(s, kind, B, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, lengthscales,
+                                    outputscale, G, dX2, work);
+  if (own) EVR_HIP(hipFreeAsync(work, s));
+  return rc;
+}
+
+long long evr_kernel_cross_grad_workspace_doubles(int n1, int n2, int d) {
+  return (n1 > 0 && n2 > 0 && d > 0) ? (long long)kcross_grad_ws_doubles(n1, n2, d) : 0;
 }
 
 int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, const double* X,

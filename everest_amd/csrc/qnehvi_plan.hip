@@ -26,9 +26,14 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
                   const double* L22, const double* dG, double* dKx, double* ws);
 int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
                   double* L22, int* flags);
+size_t kcross_grad_ws_doubles(int n1, int n2, int d);
+int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
+                       const double* scale1, const double* X2, const double* shift2, const double* scale2,
+                       const double* lengthscales, const double* outputscale, const double* G, double* dX2,
+                       double* work);
 
 struct PlanLayout {
-  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, bytes;
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, bytes;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -54,9 +59,9 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     L.dG = take(8 * (size_t)st->S * m * b);
     L.bws = take(8 * proj_backward_ws_doubles(st, b));
     L.dKx = take(8 * m * n * b);
+    L.kg = take(8 * kcross_grad_ws_doubles(st->n, b, md->d));
   }
   L.bytes = o;
-  (void)md;
   return L;
 }
 
@@ -100,8 +105,8 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   double* dKx = (double*)(w + p->L.dKx);
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;
-  return evr_kernel_cross_grad(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
-                               md->lengthscales, nullptr, dKx, p->dX);
+  return kcross_grad_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+                            md->lengthscales, nullptr, dKx, p->dX, (double*)(w + p->L.kg));
 }
 
 extern "C" {

@@ -132,8 +132,11 @@ __global__ __launch_bounds__(256) void qn_proj_fwd(int n, int nb, int Rr, int b,
                                                    const double* __restrict__ Kx, double* __restrict__ R,
                                                    double* __restrict__ P, int nrt, int ksplit, int kchunk,
                                                    double* __restrict__ W) {
-  const int j = blockIdx.z / ksplit, kz = blockIdx.z - j * ksplit;
-  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int bx = t % gx, by = (t / gx) % gy, bz = t / (gx * gy);
+  const int j = bz / ksplit, kz = bz - j * ksplit;
+  const int m0 = by * PT, n0 = bx * PT;
   const double* A = Mm + (size_t)j * Rr * n;
   const double* B = Kx + (size_t)j * n * b;
   double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(256) void qn_proj_fwd(int n, int nb, int Rr, int b,
     if (row < n) sq[ni][0] += v * v;
     else if (row < n + nb) sq[ni][1] += v * v;
   });
-  proj_norms(sq, n0, b, P + ((size_t)j * nrt + blockIdx.y) * 2 * b);
+  proj_norms(sq, n0, b, P + ((size_t)j * nrt + by) * 2 * b);
 }
 
 // split-K reduction of the forward: R = sum_kz W[kz] (fixed order) + the partial norms
@@ -179,6 +182,7 @@ __global__ __launch_bounds__(256) void qn_proj_fwd_reduce(int n, int nb, int Rr,
       const int row = m0 + wm + (q >> 1) * 16 + rq + 4 * r, c = n0 + wn + (q & 1) * 16 + col;
       double v = 0.0;
       if (row < Rr && c < b) {
+#pragma unroll 4
         for (int kz = 0; kz < ksplit; ++kz) v += W[(((size_t)kz * m + j) * Rr + row) * b + c];
         Rj[(size_t)row * b + c] = v;
       }
@@ -255,6 +259,7 @@ __global__ __launch_bounds__(1024) void qn_bwd_coef(int S, int m, int b, const d
   const double aj = oa[j];
   double dmu = 0.0, dl = 0.0;
   if (c < b) {
+#pragma unroll 4
     for (int s = g; s < S; s += 16) {
       const double dy = aj * dG[((size_t)s * m + j) * b + c];
       dmu += dy;
@@ -287,8 +292,11 @@ __global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int m, 
                                                    const double* __restrict__ dG, const double* __restrict__ oa,
                                                    const double* __restrict__ coef, double* __restrict__ dK,
                                                    int ksplit, int kchunk, double* __restrict__ W) {
-  const int j = blockIdx.z / ksplit, kz = blockIdx.z - j * ksplit;
-  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int bx = t % gx, by = (t / gx) % gy, bz = t / (gx * gy);
+  const int j = bz / ksplit, kz = bz - j * ksplit;
+  const int m0 = by * PT, n0 = bx * PT;
   const int Rr = n + nb + S + 1;
   const double* A = Mm + (size_t)j * Rr * n;   // A(row, k) = M_j[k][row]
   const double* Rj = R + (size_t)j * Rr * b;
@@ -323,14 +331,16 @@ __global__ __launch_bounds__(256) void qn_splitk_sum(long long per, int ksplit, 
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= per) return;
   double v = 0.0;
+#pragma unroll 4
   for (int kz = 0; kz < ksplit; ++kz) v += W[(size_t)kz * per + e];
   out[e] = v;
 }
 
-// split K when the tile grid cannot fill the chip; each slice keeps >= 8 k-steps
+// split K when the tile grid cannot fill the chip (aim at >= 512 workgroups, i.e. two per
+// CU); each slice keeps >= 8 k-steps.  More slices than that only add partial-sum traffic.
 static int proj_ksplit(int tiles, int K, int* kchunk) {
   int ks = 1;
-  if (tiles < 512) ks = std::max(1, std::min(std::min(cdiv(1024, tiles), K / (8 * PK)), 32));
+  if (tiles < 512) ks = std::max(1, std::min(std::min(cdiv(512, tiles), K / (8 * PK)), 32));
   *kchunk = ks > 1 ? cdiv(cdiv(K, ks), PK) * PK : std::max(K, 1);
   return ks > 1 ? cdiv(K, *kchunk) : 1;
 }
@@ -414,16 +424,20 @@ int evr_qnehvi_norms_rows(const evr_qnehvi_state* st) {
   return cdiv((long long)st->n + st->nb + st->S + 1, PT);
 }
 
+long long evr_qnehvi_project_workspace_doubles(const evr_qnehvi_state* st, int b) {
+  return (st && b > 0) ? (long long)proj_forward_ws_doubles(st, b) : 0;
+}
+
 int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const double* Mm, const double* Kx,
-                       double* R, double* norms) {
+                       double* R, double* norms, double* work) {
   EVR_CHECK(st && Mm && Kx && R && norms && b >= 0, "evr_qnehvi_project: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t wn = proj_forward_ws_doubles(st, b);
-  double* W = nullptr;
-  if (wn) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * wn, s));
-  const int rc = proj_forward(s, st, b, Mm, Kx, R, norms, W);
-  if (W) EVR_HIP(hipFreeAsync(W, s));
+  const bool own = wn && !work;
+  if (own) EVR_HIP(hipMallocAsync((void**)&work, sizeof(double) * wn, s));
+  const int rc = proj_forward(s, st, b, Mm, Kx, R, norms, work);
+  if (own) EVR_HIP(hipFreeAsync(work, s));
   return rc;
 }
 
@@ -433,15 +447,19 @@ int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, co
   return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags);
 }
 
+long long evr_qnehvi_project_backward_workspace_doubles(const evr_qnehvi_state* st, int b) {
+  return (st && b > 0) ? (long long)proj_backward_ws_doubles(st, b) : 0;
+}
+
 int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
-                                const double* L22, const double* dG, double* dKx) {
+                                const double* L22, const double* dG, double* dKx, double* work) {
   EVR_CHECK(st && Mm && R && L22 && dG && dKx && b >= 0, "evr_qnehvi_project_backward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  double* ws = nullptr;
-  EVR_HIP(hipMallocAsync((void**)&ws, sizeof(double) * proj_backward_ws_doubles(st, b), s));
-  const int rc = proj_backward(s, st, b, Mm, R, L22, dG, dKx, ws);
-  EVR_HIP(hipFreeAsync(ws, s));
+  const bool own = !work;
+  if (own) EVR_HIP(hipMallocAsync((void**)&work, sizeof(double) * proj_backward_ws_doubles(st, b), s));
+  const int rc = proj_backward(s, st, b, Mm, R, L22, dG, dKx, work);
+  if (own) EVR_HIP(hipFreeAsync(work, s));
   return rc;
 }
 

@@ -66,6 +66,11 @@ def kernel_matrix(X1, X2, lengthscales, kind: int = 0, shift1=None, scale1=None,
     return K
 
 
+def _workspace(ndoubles: int, device) -> torch.Tensor:
+    """Scratch for a native op (torch caching allocator; no device-side malloc)."""
+    return torch.empty(max(int(ndoubles), 1), dtype=torch.float64, device=device)
+
+
 def kernel_cross_grad(X1, X2, lengthscales, G, kind=0, shift1=None, scale1=None, shift2=None, scale2=None,
                       outputscale=None) -> torch.Tensor:
     X1, X2, ls, G = _dev(X1, "X1"), _dev(X2, "X2"), _dev(lengthscales, "ls"), _dev(G, "G")
@@ -75,8 +80,10 @@ def kernel_cross_grad(X1, X2, lengthscales, G, kind=0, shift1=None, scale1=None,
         raise ValueError(f"kernel_cross_grad: G shape {tuple(G.shape)} != {(B, n1, n2)}")
     dX = torch.empty(n2, d, dtype=torch.float64, device=X1.device)
     opt = [None if t is None else _dev(t, "aux") for t in (shift1, scale1, shift2, scale2, outputscale)]
+    work = _workspace(_native.load().evr_kernel_cross_grad_workspace_doubles(n1, n2, d), X1.device)
     call("evr_kernel_cross_grad", _stream(), int(kind), B, n1, n2, d, X1.data_ptr(), _p(opt[0]), _p(opt[1]),
-         X2.data_ptr(), _p(opt[2]), _p(opt[3]), ls.data_ptr(), _p(opt[4]), G.data_ptr(), dX.data_ptr())
+         X2.data_ptr(), _p(opt[2]), _p(opt[3]), ls.data_ptr(), _p(opt[4]), G.data_ptr(), dX.data_ptr(),
+         work.data_ptr())
     return dX
 
 
@@ -276,8 +283,9 @@ def qnehvi_project(st: EvrQnehviState, M: torch.Tensor, Kx: torch.Tensor, b: int
     R = torch.empty(st.m, Rr, b, dtype=torch.float64, device=dev)
     nrt = _native.load().evr_qnehvi_norms_rows(ctypes.byref(st))
     P = torch.empty(st.m, nrt, 2, b, dtype=torch.float64, device=dev)
+    work = _workspace(_native.load().evr_qnehvi_project_workspace_doubles(ctypes.byref(st), b), dev)
     call("evr_qnehvi_project", _stream(), ctypes.byref(st), b, _dev(M, "M").data_ptr(), _dev(Kx, "Kx").data_ptr(),
-         R.data_ptr(), P.data_ptr())
+         R.data_ptr(), P.data_ptr(), work.data_ptr())
     return R, P
 
 
@@ -295,8 +303,9 @@ def qnehvi_project_backward(st: EvrQnehviState, M: torch.Tensor, R: torch.Tensor
                             dG: torch.Tensor, b: int) -> torch.Tensor:
     """dKx = M^T gR (m x n x b) with gR generated inside the GEMM."""
     dK = torch.empty(st.m, st.n, b, dtype=torch.float64, device=R.device)
+    work = _workspace(_native.load().evr_qnehvi_project_backward_workspace_doubles(ctypes.byref(st), b), R.device)
     call("evr_qnehvi_project_backward", _stream(), ctypes.byref(st), b, M.data_ptr(), R.data_ptr(), L22.data_ptr(),
-         dG.data_ptr(), dK.data_ptr())
+         dG.data_ptr(), dK.data_ptr(), work.data_ptr())
     return dK
 
 

@@ -51,7 +51,9 @@ int evr_kernel_cross_grad(void* stream, int kind, int B, int n1, int n2, int d,
                           const double* X1, const double* shift1, const double* scale1,
                           const double* X2, const double* shift2, const double* scale2,
                           const double* lengthscales, const double* outputscale,
-                          const double* G, double* dX2);
+                          const double* G, double* dX2, double* work);
+/* doubles of `work` evr_kernel_cross_grad needs (row-split partials); work NULL = allocate */
+long long evr_kernel_cross_grad_workspace_doubles(int n1, int n2, int d);
 
 /* MLL gradient pieces for the exact GP fit (fit_gpytorch_mll,
  * bofire/surrogates/single_task_gp.py:70-71):
@@ -176,14 +178,18 @@ int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b,
  * evr_qnehvi_samples_norms: G, L22, flags as evr_qnehvi_samples, from R's sample / mean rows
  *   and the partial norms.
  * evr_qnehvi_project_backward: dKx_j = M_j^T gR_j (n x b per output) with gR generated in
- *   the K loop from R, L22 and dG (never written to memory). */
+ *   the K loop from R, L22 and dG (never written to memory).
+ * `work` (split-K partials, gR coefficients): the *_workspace_doubles size, NULL = allocate. */
 int evr_qnehvi_norms_rows(const evr_qnehvi_state* st);
 int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const double* M, const double* Kx,
-                       double* R, double* norms);
+                       double* R, double* norms, double* work);
+long long evr_qnehvi_project_workspace_doubles(const evr_qnehvi_state* st, int b);
 int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                              const double* norms, double* G, double* L22, int* flags);
 int evr_qnehvi_project_backward(void* stream, const evr_qnehvi_state* st, int b, const double* M,
-                                const double* R, const double* L22, const double* dG, double* dKx);
+                                const double* R, const double* L22, const double* dG, double* dKx,
+                                double* work);
+long long evr_qnehvi_project_backward_workspace_doubles(const evr_qnehvi_state* st, int b);
 
 /* Native evaluation plan of the whole qNEHVI chain (qnehvi_plan.hip): K_x, fused projection,
  * samples, HVI scan (+ backward: projection^T with generated gR, cross-covariance gradient)
