@@ -27,6 +27,7 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
                   double* L22, int* flags);
 size_t kcross_grad_ws_doubles(int n1, int n2, int d);
+int gemm_backend_init();
 int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                        const double* scale1, const double* X2, const double* shift2, const double* scale2,
                        const double* lengthscales, const double* outputscale, const double* G, double* dX2,
@@ -136,6 +137,10 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->L = plan_layout(st, md, b, p->backward);
   p->graph = nullptr;
   p->exec = nullptr;
+  if (int rc = gemm_backend_init()) {
+    delete p;
+    return rc;
+  }
   if (use_graph) {
     hipStream_t s = (hipStream_t)stream;
     // capture on a private stream so the caller's stream (torch's) never enters capture mode

@@ -21,15 +21,22 @@
 // Tile: 64 x 64 outputs per 256-thread workgroup, 4 waves x (2 x 2) v_mfma_f64_16x16x4f64,
 // K step 16 staged through LDS, global loads of step t+1 issued before the MFMAs of step t.
 #include <algorithm>
+#include <cstdlib>
+
+#include <rocblas/rocblas.h>
 
 #include "common.hpp"
 #include "../../include/everest_amd.h"
 
 using double4_t = __attribute__((ext_vector_type(4))) double;
 
+#ifndef EVR_PK
+#define EVR_PK 16
+#endif
 namespace evr {
 
-constexpr int PT = 64, PK = 16, PPAD = 16;
+constexpr int PT = 64, PK = EVR_PK, PPAD = 16;
+constexpr int PU = PT * PK / 256;   // staged elements of A and of B per thread and k-step
 
 // 64 x 64 f64 MFMA tile over k in [kbeg, kend): fa(row, k) / fb(k, col) fetch one element
 // (tile-local row / col); the fetch of step t+1 is issued before the MFMAs of step t.
@@ -40,18 +47,18 @@ __device__ __forceinline__ void proj_tile(int kbeg, int kend, FA fa, FB fb, doub
   __shared__ double Bs[PK][PT + PPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  int am[4], ak[4], bn[4], bk[4];
+  int am[PU], ak[PU], bn[PU], bk[PU];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < PU; ++u) {
     const int e = u * 256 + tid;
-    if (TA) { am[u] = e & 63; ak[u] = e >> 6; } else { ak[u] = e & 15; am[u] = e >> 4; }
-    bn[u] = e & 63;
-    bk[u] = e >> 6;
+    if (TA) { am[u] = e % PT; ak[u] = e / PT; } else { ak[u] = e % PK; am[u] = e / PK; }
+    bn[u] = e % PT;
+    bk[u] = e / PT;
   }
-  double ra[4], rb[4];
+  double ra[PU], rb[PU];
   auto fetch = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PU; ++u) {
       const int k = k0 + ak[u], kb = k0 + bk[u];
       ra[u] = (k < kend) ? fa(am[u], k) : 0.0;
       rb[u] = (kb < kend) ? fb(kb, bn[u]) : 0.0;
@@ -60,7 +67,7 @@ __device__ __forceinline__ void proj_tile(int kbeg, int kend, FA fa, FB fb, doub
   if (kbeg < kend) fetch(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += PK) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PU; ++u) {
       As[ak[u]][am[u]] = ra[u];
       Bs[bk[u]][bn[u]] = rb[u];
     }
@@ -345,9 +352,98 @@ static int proj_ksplit(int tiles, int K, int* kchunk) {
   return ks > 1 ? cdiv(K, *kchunk) : 1;
 }
 
+// ---------------------------------------------------------------------------------------
+// Library-GEMM variant (rocBLAS dgemm for the plain contractions, hand-written fused
+// epilogue / prologue kernels around them).  rocBLAS' f64 MFMA kernels reach ~48 TF/s at
+// this shape vs ~26 TF/s for the 64x64 tile above; EVR_GEMM=mfma selects the fully fused
+// kernels instead.
+// ---------------------------------------------------------------------------------------
+// partial norms of R rows [0, n + nb) per 64-row tile: block = 64 candidates x 4 row groups
+__global__ __launch_bounds__(256) void qn_norms_rows(int n, int nb, int Rr, int b, int nrt,
+                                                     const double* __restrict__ R, double* __restrict__ P) {
+  const int j = blockIdx.z, rt = blockIdx.y;
+  const int cx = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  __shared__ double red[4][64][2];
+  double s0 = 0.0, s1 = 0.0;
+  if (c < b) {
+    const double* Rj = R + (size_t)j * Rr * b;
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+      const int row = rt * 64 + rg * 16 + r;
+      if (row < n + nb) {
+        const double v = Rj[(size_t)row * b + c];
+        if (row < n) s0 = fma(v, v, s0);
+        else s1 = fma(v, v, s1);
+      }
+    }
+  }
+  red[rg][cx][0] = s0;
+  red[rg][cx][1] = s1;
+  __syncthreads();
+  if (rg < 2 && c < b) {
+    const double v = ((red[0][cx][rg] + red[1][cx][rg]) + red[2][cx][rg]) + red[3][cx][rg];
+    P[(((size_t)j * nrt + rt) * 2 + rg) * b + c] = v;
+  }
+}
+
+// gR_j (Rr x b) from R, dG and the per-candidate coefficients (see the header)
+__global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int S, int m, int b, const double* __restrict__ R,
+                                                 const double* __restrict__ dG, const double* __restrict__ oa,
+                                                 const double* __restrict__ coef, double* __restrict__ gR) {
+  const int Rr = n + nb + S + 1;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)m * Rr * b) return;
+  const int c = (int)(e % b);
+  const long long rj = e / b;
+  const int row = (int)(rj % Rr), j = (int)(rj / Rr);
+  const double* cj = coef + (size_t)j * 3 * b;
+  double v;
+  if (row < n) v = R[e] * cj[c];
+  else if (row < n + nb) v = R[e] * cj[(size_t)b + c];
+  else if (row < n + nb + S) v = oa[j] * dG[((size_t)(row - n - nb) * m + j) * b + c];
+  else v = cj[(size_t)2 * b + c];
+  gR[e] = v;
+}
+
+static bool use_rocblas() {
+  static const bool v = [] {
+    const char* e = std::getenv("EVR_GEMM");
+    return !(e && std::string(e) == "mfma");
+  }();
+  return v;
+}
+
+static rocblas_handle rb_handle() {
+  thread_local rocblas_handle h = nullptr;
+  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
+  return h;
+}
+
+// row-major C = op(A) op(B) batched (alpha 1, beta 0) through rocBLAS' column-major dgemm
+static int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA,
+                   const double* B, int ldb, long long sB, double* C, int ldc, long long sC, int batch) {
+  rocblas_handle h = rb_handle();
+  EVR_CHECK(h, "rocBLAS handle creation failed");
+  EVR_CHECK(rocblas_set_stream(h, s) == rocblas_status_success, "rocblas_set_stream failed");
+  const double one = 1.0, zero = 0.0;
+  const rocblas_status st = rocblas_dgemm_strided_batched(h, rocblas_operation_none,
+                                                           tA ? rocblas_operation_transpose : rocblas_operation_none,
+                                                           N, M, K, &one, B, ldb, sB, A, lda, sA, &zero, C, ldc, sC,
+                                                           batch);
+  EVR_CHECK(st == rocblas_status_success, "rocblas_dgemm_strided_batched failed (%d)", (int)st);
+  return 0;
+}
+
+int gemm_backend_init() {
+  if (use_rocblas()) EVR_CHECK(rb_handle(), "rocBLAS handle creation failed");
+  return 0;
+}
+
 // ---- internal launchers (workspace supplied by the caller; qnehvi_plan.hip) ----------
 size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b) {
   const int Rr = st->n + st->nb + st->S + 1;
+  if (use_rocblas()) return 0;
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(Rr, PT) * st->m, st->n, &kchunk);
   return ks > 1 ? (size_t)ks * st->m * Rr * b : 0;
@@ -358,6 +454,15 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
   if (b == 0) return 0;
   const int Rr = st->n + st->nb + st->S + 1;
   const int nrt = cdiv(Rr, PT);
+  if (use_rocblas()) {
+    if (int rc = rb_gemm(s, false, Rr, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R, b,
+                         (long long)Rr * b, st->m))
+      return rc;
+    qn_norms_rows<<<dim3(cdiv(b, 64), cdiv(st->n + st->nb, 64), st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, nrt, R,
+                                                                                     norms);
+    EVR_LAUNCH_CHECK();
+    return 0;
+  }
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * nrt * st->m, st->n, &kchunk);
   EVR_CHECK(ks == 1 || W, "proj_forward: split-K workspace missing");
@@ -372,8 +477,13 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
   return 0;
 }
 
+// backward: the generated-gR MFMA kernel wins at small candidate batches (the L-BFGS
+// restarts), gR materialisation + rocBLAS from b = 64 on (measured on MI355X)
+static bool bwd_rocblas(int b) { return use_rocblas() && b >= 64; }
+
 size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b) {
   const int Rr = st->n + st->nb + st->S + 1;
+  if (bwd_rocblas(b)) return (size_t)st->m * 3 * b + (size_t)st->m * Rr * b;   // coefficients + gR
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
   return (size_t)st->m * 3 * b + (ks > 1 ? (size_t)ks * st->m * st->n * b : 0);
@@ -386,6 +496,14 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
   double* coef = ws;
   qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
   EVR_LAUNCH_CHECK();
+  if (bwd_rocblas(b)) {
+    double* gR = ws + (size_t)st->m * 3 * b;
+    const long long tot = (long long)st->m * Rr * b;
+    qn_gen_gr<<<cdiv(tot, 256), 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, dG, st->obj_a, coef, gR);
+    EVR_LAUNCH_CHECK();
+    return rb_gemm(s, true, st->n, b, Rr, Mm, st->n, (long long)Rr * st->n, gR, b, (long long)Rr * b, dKx, b,
+                   (long long)st->n * b, st->m);
+  }
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
   double* W = ws + (size_t)st->m * 3 * b;

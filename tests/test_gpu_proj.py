@@ -26,7 +26,7 @@ def test_fused_projection_matches_unfused(n, d, m, S, b):
     G0, L0, f0 = ops.qnehvi_samples(st, R0, b)
     R1, P = ops.qnehvi_project(st, q.M, Kx, b)
     G1, L1, f1 = ops.qnehvi_samples_norms(st, R1, P, b)
-    assert torch.allclose(R1, R0, rtol=1e-13, atol=1e-14)
+    assert torch.allclose(R1, R0, rtol=1e-12, atol=1e-13 * R0.abs().max().item())   # GEMM backends round differently
     assert torch.equal(f0, f1)
     assert torch.allclose(L1, L0, rtol=1e-9, atol=1e-12)
     assert torch.allclose(G1, G0, rtol=1e-10, atol=1e-12)
