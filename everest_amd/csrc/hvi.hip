@@ -297,7 +297,7 @@ __host__ __device__ inline KdLds kd_lds(int stride, int M, int max_groups) {
   o += nq * KD_CT * 2;
   o = (o + 15) & ~(size_t)15;
   L.pA = o;
-  o += (KD_CT * nq + 1) * 4;
+  o += (KD_CT * nq + 4) * 4;   // 4 waves x (16 candidates x nq + 1)
   L.bytes = o;
   return L;
 }
@@ -421,21 +421,48 @@ __device__ __forceinline__ void kd_stage(T* __restrict__ dst, const T* __restric
   for (; e < n; e += 256) dst[e] = src[e];
 }
 
+// LDS-coherent wave-level sync: this wave's LDS writes are visible to its other lanes
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// wave-wide exclusive scan of ints on DPP moves; *total = sum over the wave
+__device__ __forceinline__ int wave_scan_excl(int v, int* total) {
+  int x = v;
+  x += dpp_i32<0x111, 0xF>(0, x);
+  x += dpp_i32<0x112, 0xF>(0, x);
+  x += dpp_i32<0x114, 0xF>(0, x);
+  x += dpp_i32<0x118, 0xF>(0, x);
+  x += dpp_i32<0x142, 0xA>(0, x);
+  x += dpp_i32<0x143, 0xC>(0, x);
+  *total = __builtin_amdgcn_readlane(x, 63);
+  return x - v;
+}
+
+// Wave-independent sparse scan: the workgroup (sample s, tile of 64 candidates) stages the
+// sample's point table, group minima, candidate values and thresholds once; after that
+// barrier each wave owns 16 candidates and runs the group filter, the cell filter windows,
+// the term evaluation and the accumulation alone (wave-level DPP scans, no workgroup
+// barriers) — candidates are wave-exclusive, so the accumulators need no inter-wave order.
 template <int M, bool BWD>
-__global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const double* __restrict__ G,
+__global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                               const int* __restrict__ thg, HviKd kd,
                                               const double* __restrict__ gout, double* __restrict__ part,
                                               double* __restrict__ dG) {
+  // nsplit > 1 (small candidate batches): the sample's 16-group chunks are split over
+  // gridDim.z workgroups; part / dG then receive raw per-split partials
+  // [s][split][c] / [s][split][j][c] for hvi_reduce_fwd / hvi_reduce_bwd (fixed order).
   constexpr int NV = BWD ? M + 1 : 1;
+  constexpr int CW = KD_CT / 4;            // candidates per wave
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kd_dyn[];
   __shared__ double yv[KD_CT][M];
   __shared__ uint4 thp[KD_CT];             // packed 16-bit thresholds (objectives >= M: 1)
-  __shared__ double acc[4][KD_CT][NV];     // per-wave accumulators (no inter-wave races)
-  __shared__ int wmask[256], wcg[256], scanbuf[256], wsum[4];
-  // XCD-aware placement: consecutive workgroups go round-robin over the 8 XCDs, so the
-  // candidate tiles of one sample are remapped onto one XCD (its L2 holds the sample's
-  // keys, ranks and point table once instead of eight times).
+  __shared__ double acc[KD_CT][NV];
+  __shared__ int wmask[4][64], wcg[4][64], wpre[4][64];
+  // XCD-aware placement: the candidate tiles of one sample share one XCD's L2
   int s, tile;
   {
     const int L = blockIdx.x + ntiles * blockIdx.y;
@@ -451,18 +478,23 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
   const int c0 = tile * KD_CT, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int stride = kd.stride;
-  const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
-  const int NQ = (Gs + 15) >> 4;
+  const int split = blockIdx.z;
+  const int NQall = (kd.goff[s + 1] - kd.goff[s] + 15) >> 4;
+  const int qper = (NQall + nsplit - 1) / nsplit;
+  const int q0 = min(NQall, split * qper);
+  const int NQ = min(NQall, q0 + qper) - q0;                 // this workgroup's 16-group chunks
+  const int gbase = kd.goff[s] + 16 * q0;
+  const int Gs = min(kd.goff[s + 1] - gbase, 16 * NQ);
   const KdLds Lo = kd_lds(stride, M, kd.max_groups);
   double* pt = (double*)(kd_dyn + Lo.pt);
   int* r0 = (int*)(kd_dyn + Lo.r0);
   uint4* gb = (uint4*)(kd_dyn + Lo.gb);
   unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
-  int* pA = (int*)(kd_dyn + Lo.pA);
+  int* pA = (int*)(kd_dyn + Lo.pA) + wave * (CW * NQ + 1);   // this wave's prefix array
 
   kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
   kd_stage(r0, kd.rank0 + (size_t)s * stride, stride);
-  kd_stage(gb, (const uint4*)kd.gbox + gbase, Gs);
+  if (Gs > 0) kd_stage(gb, (const uint4*)kd.gbox + gbase, Gs);
   for (int e = tid; e < KD_CT * M; e += 256) {
     const int j = e / KD_CT, c = e - j * KD_CT;
     yv[c][j] = (c0 + c < b) ? G[((size_t)s * M + j) * b + c0 + c] : -INFINITY;
@@ -483,13 +515,16 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
     }
     thp[tid] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  for (int e = tid; e < 4 * KD_CT * NV; e += 256) (&acc[0][0][0])[e] = 0.0;
+  for (int e = tid; e < KD_CT * NV; e += 256) (&acc[0][0])[e] = 0.0;
   __syncthreads();
+  const int cbase = wave * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
+  if (c0 + cbase >= b) return;
 
-  // ---- A: group filter (lane = candidate): 4 packed subtractions per group ----
+  // ---- A: group filter; lane = (candidate, quarter of the 16-group chunks) ----
   {
-    const uint4 t = thp[lane];
-    for (int q = wave; q < NQ; q += 4) {
+    const int cl = lane & (CW - 1), qq = lane >> 4;
+    const uint4 t = thp[cbase + cl];
+    for (int q = qq; q < NQ; q += 4) {
       unsigned int mask = 0;
       const int gend = min(16, Gs - q * 16);
       for (int k = 0; k < gend; ++k) {
@@ -497,39 +532,39 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
         const unsigned int x = kd_lt16(v.x, t.x) & kd_lt16(v.y, t.y) & kd_lt16(v.z, t.z) & kd_lt16(v.w, t.w);
         mask |= (unsigned int)((x & 0x80008000u) == 0x80008000u) << k;
       }
-      mA[q * KD_CT + lane] = (unsigned short)mask;
+      mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
     }
   }
-  __syncthreads();
-  // candidate-major prefix over entries e = c * NQ + q
-  const int NE = KD_CT * NQ;
+  wave_sync();
+  // candidate-major prefix over this wave's entries e = cl * NQ + q
+  const int NE = CW * NQ;
   int PA;
   {
-    const int per = (NE + 255) / 256;
-    const int e0 = min(NE, tid * per), e1 = min(NE, e0 + per);
+    const int per = (NE + 63) / 64;
+    const int e0 = min(NE, lane * per), e1 = min(NE, e0 + per);
     int loc = 0;
-    for (int e = e0; e < e1; ++e) loc += __popc(mA[(e % NQ) * KD_CT + e / NQ]);
-    int run = block_scan256(loc, wsum, &PA);
+    for (int e = e0; e < e1; ++e) loc += __popc(mA[(e % NQ) * KD_CT + cbase + e / NQ]);
+    int run = wave_scan_excl(loc, &PA);
     for (int e = e0; e < e1; ++e) {
       pA[e] = run;
-      run += __popc(mA[(e % NQ) * KD_CT + e / NQ]);
+      run += __popc(mA[(e % NQ) * KD_CT + cbase + e / NQ]);
     }
-    if (tid == 0) {
+    if (lane == 0) {
       pA[NE] = PA;
       if (kd.counters) {
         atomicAdd(kd.counters + 0, (unsigned long long)PA);
-        atomicAdd(kd.counters + 2, (unsigned long long)min(b - c0, KD_CT) * Gs);
+        atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - c0 - cbase, CW)) * Gs);
       }
     }
   }
-  __syncthreads();
+  wave_sync();
 
-#ifndef EVR_KD_DBG
-#define EVR_KD_DBG 0
-#endif
-  for (int wb = 0; wb < (EVR_KD_DBG == 1 ? 0 : PA); wb += 256) {
-    // ---- B: cell filter (thread = passing (candidate, group) pair), packed compares ----
-    const int p = wb + tid;
+  int* wm = wmask[wave];
+  int* wc = wcg[wave];
+  int* wp = wpre[wave];
+  for (int wb = 0; wb < PA; wb += 64) {
+    // ---- B: cell filter (lane = passing (candidate, group) pair), packed compares ----
+    const int p = wb + lane;
     unsigned int mB = 0;
     int cg = 0;
     if (p < PA) {
@@ -539,7 +574,8 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
         if (pA[mid] <= p) lo = mid;
         else hi = mid - 1;
       }
-      const int c = lo / NQ, q = lo - c * NQ;
+      const int cl = lo / NQ, q = lo - cl * NQ;
+      const int c = cbase + cl;
       const int g = q * 16 + kth_bit16(mA[q * KD_CT + c], p - pA[lo]);
       const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
       const uint4 tq = thp[c];
@@ -565,28 +601,29 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
       for (int i = 0; i < 8; ++i) mB |= (((a[i] >> 15) & 1u) | ((a[i] >> 30) & 2u)) << (2 * i);
       cg = (c << 16) | g;
     }
-    wmask[tid] = (int)mB;
-    wcg[tid] = cg;
     int EW;
-    scanbuf[tid] = block_scan256(__popc(mB), wsum, &EW);   // exclusive prefixes
-    if (kd.counters && tid == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
-    __syncthreads();
-    // ---- C: evaluation (thread = exact (cell, candidate) pair) ----
-    for (int cb = 0; cb < (EVR_KD_DBG == 2 ? 0 : EW); cb += 256) {
-      const int q = cb + tid;
+    const int pre = wave_scan_excl(__popc(mB), &EW);
+    wm[lane] = (int)mB;
+    wc[lane] = cg;
+    wp[lane] = pre;
+    if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
+    wave_sync();
+    // ---- C: evaluation (lane = exact (cell, candidate) term) ----
+    for (int cb = 0; cb < EW; cb += 64) {
+      const int q = cb + lane;
       int rcv = -1;
       double val[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) val[v] = 0.0;
       if (q < EW) {
-        int lo = 0, hi = 255;
+        int lo = 0, hi = 63;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
-          if (scanbuf[mid] <= q) lo = mid;
+          if (wp[mid] <= q) lo = mid;
           else hi = mid - 1;
         }
-        const int c = wcg[lo] >> 16, g = wcg[lo] & 0xFFFF;
-        const int bit = kth_bit16((unsigned int)wmask[lo], q - scanbuf[lo]);
+        const int c = wc[lo] >> 16, g = wc[lo] & 0xFFFF;
+        const int bit = kth_bit16((unsigned int)wm[lo], q - wp[lo]);
         double l[M], u[M];
         K::decode(kd.gkeys[(size_t)(gbase + g) * 16 + bit], pt, r0, l, u);
         double y[M];
@@ -620,30 +657,28 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, const do
         }
         rcv = c;
       }
-#if EVR_KD_DBG == 3
-      if (rcv >= 0) for (int v = 0; v < NV; ++v) acc[wave][rcv][v] += val[v];
-      continue;
-#endif
-      // wave-level segmented inclusive scan (pairs of a candidate are contiguous) on DPP
-      // moves; segment ends add into this wave's accumulators
+      // segmented scan over the round (terms of a candidate are contiguous); segment ends
+      // add into the candidate's accumulator (owned by this wave)
       seg_scan_wave<NV>(rcv, val);
       const int rnext = __shfl_down(rcv, 1, 64);
       if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) acc[wave][rcv][v] += val[v];
+        for (int v = 0; v < NV; ++v) acc[rcv][v] += val[v];
       }
     }
-    __syncthreads();  // wmask / wcg / scanbuf are rewritten by the next window
+    wave_sync();   // wm / wc / wp are rewritten by the next window
   }
-  __syncthreads();
-  auto total = [&](int c, int v) { return ((acc[0][c][v] + acc[1][c][v]) + acc[2][c][v]) + acc[3][c][v]; };
-  for (int e = tid; e < KD_CT; e += 256)
-    if (c0 + e < b) part[(size_t)s * b + c0 + e] = total(e, 0);
+  wave_sync();
+  // outputs of this wave's candidates
+  const size_t ss = (size_t)s * nsplit + split;
+  if (lane < CW && c0 + cbase + lane < b) part[ss * b + c0 + cbase + lane] = acc[cbase + lane][0];
   if (BWD) {
-    for (int e = tid; e < KD_CT * M; e += 256) {
-      const int j = e / KD_CT, c = e - j * KD_CT;
-      if (c0 + c < b)
-        dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * total(c, NV > 1 ? 1 + j : 0);
+    for (int e = lane; e < CW * M; e += 64) {
+      const int j = e / CW, cl = e - j * CW, c = cbase + cl;
+      if (c0 + c >= b) continue;
+      const double v = acc[c][NV > 1 ? 1 + j : 0];
+      if (nsplit == 1) dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * v;
+      else dG[(ss * M + j) * b + c0 + c] = v;
     }
   }
 }
@@ -695,9 +730,18 @@ static HviKd hvi_kd_of(const evr_qnehvi_state* st) {
                st->pts_stride, st->max_groups, st->scan_counters};
 }
 
-// workspace (doubles): S x b partials | S x M x b int thresholds
+// group-range splits per sample: fill ~1024 workgroups at small candidate batches
+static int hvi_kd_nsplit(const evr_qnehvi_state* st, int b) {
+  const int tiles = cdiv(b, KD_CT) * st->S;
+  const int nq = (st->max_groups + 15) / 16;
+  return std::max(1, std::min(std::min(cdiv(1024, tiles), 8), std::max(nq, 1)));
+}
+
+// workspace (doubles): S x ns x b partials | S x M x b int thresholds | (ns > 1) S x ns x M x b dG partials
 static long long hvi_kd_workspace(const evr_qnehvi_state* st, int b) {
-  return (long long)st->S * b + ((long long)st->S * st->m * b + 1) / 2;
+  const long long ns = hvi_kd_nsplit(st, b);
+  return (long long)st->S * ns * b + ((long long)st->S * st->m * b + 1) / 2 +
+         (ns > 1 ? (long long)st->S * ns * st->m * b : 0);
 }
 
 template <int M, bool BWD>
@@ -705,17 +749,25 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
                          double* part, double* dG, const int* flags, double* acq) {
   const KdLds Lo = kd_lds(st->pts_stride, M, st->max_groups);
   const int ntiles = cdiv(b, KD_CT);
-  int* th = (int*)(part + (size_t)st->S * b);   // workspace tail: S x M x b thresholds
+  const int ns = hvi_kd_nsplit(st, b);
+  int* th = (int*)(part + (size_t)st->S * ns * b);   // workspace: thresholds, then dG partials
+  double* dgp = (double*)(th + (((size_t)st->S * M * b + 1) & ~(size_t)1));
   hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(b, M, st->pts_stride, G,
                                                                                      st->sorted_lo, th);
   EVR_LAUNCH_CHECK();
   EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)Lo.bytes));
-  dim3 grid(ntiles, st->S);
-  hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, G, th, hvi_kd_of(st), gout, part, dG);
+  dim3 grid(ntiles, st->S, ns);
+  hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
+                                               ns > 1 ? dgp : dG);
   EVR_LAUNCH_CHECK();
   if (acq) {
-    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, 1, b, M, part, flags, acq);
+    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, ns, b, M, part, flags, acq);
+    EVR_LAUNCH_CHECK();
+  }
+  if (BWD && ns > 1) {
+    const long long tot = (long long)st->S * M * b;
+    hvi_reduce_bwd<<<cdiv(tot, 256), 256, 0, s>>>(st->S, ns, M, b, dgp, gout, dG);
     EVR_LAUNCH_CHECK();
   }
   return 0;
