@@ -260,37 +260,50 @@ __global__ __launch_bounds__(256) void kls_grad_kernel(int kind, int n, int d, c
   }
 }
 
-__global__ void colsum_kernel(int B, int n, int d, const double* __restrict__ part, double* __restrict__ out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B * d) return;
-  const int b = e / d, k = e % d;
+// out[b][k] = sum_i part[b][i][k]: one block per (b, k), strided partials + fixed LDS tree
+__global__ __launch_bounds__(256) void colsum_kernel(int B, int n, int d, const double* __restrict__ part,
+                                                     double* __restrict__ out) {
+  const int b = blockIdx.x / d, k = blockIdx.x % d;
+  __shared__ double red[256];
   double s = 0.0;
-  for (int i = 0; i < n; ++i) s += part[((size_t)b * n + i) * d + k];
-  out[e] = s;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[((size_t)b * n + i) * d + k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[(size_t)b * d + k] = red[0];
 }
 
-// Scalars of the exact MLL per output b (one block each):
+// Scalars of the exact MLL per output b:
 // out[b] = {logdet = 2 sum log L_ii, quad = r.alpha, trKinv = ||Linv||_F^2, sum alpha, sum alpha^2}
+// Pass 1: grid (B, MT_CHUNKS): rows i = chunk, chunk + MT_CHUNKS, ... of Linv read coalesced
+// (threads over columns); per-chunk partials.  Pass 2 sums the chunks in a fixed order.
+constexpr int MT_CHUNKS = 32;
+
 __global__ __launch_bounds__(256) void mll_terms_kernel(int n, const double* __restrict__ L,
                                                         const double* __restrict__ Linv,
                                                         const double* __restrict__ r,
                                                         const double* __restrict__ alpha,
-                                                        double* __restrict__ out) {
-  const int b = blockIdx.x;
+                                                        double* __restrict__ part) {
+  const int b = blockIdx.x, ch = blockIdx.y;
   const int tid = threadIdx.x;
   const double* Lb = L + (size_t)b * n * n;
   const double* Ib = Linv + (size_t)b * n * n;
   const double* rb = r + (size_t)b * n;
   const double* ab = alpha + (size_t)b * n;
   double t[5] = {0, 0, 0, 0, 0};
-  for (int i = tid; i < n; i += 256) {
-    t[0] += log(Lb[(size_t)i * n + i]);
-    t[1] = fma(rb[i], ab[i], t[1]);
-    t[3] += ab[i];
-    t[4] = fma(ab[i], ab[i], t[4]);
-    for (int j = 0; j <= i; ++j) {
+  for (int i = ch; i < n; i += MT_CHUNKS) {
+    for (int j = tid; j <= i; j += 256) {
       const double v = Ib[(size_t)i * n + j];
       t[2] = fma(v, v, t[2]);
+    }
+    if (tid == 0) {
+      t[0] += log(Lb[(size_t)i * n + i]);
+      t[1] = fma(rb[i], ab[i], t[1]);
+      t[3] += ab[i];
+      t[4] = fma(ab[i], ab[i], t[4]);
     }
   }
   __shared__ double red[256];
@@ -301,9 +314,19 @@ __global__ __launch_bounds__(256) void mll_terms_kernel(int n, const double* __r
       if (tid < o) red[tid] += red[tid + o];
       __syncthreads();
     }
-    if (tid == 0) out[b * 5 + q] = (q == 0) ? 2.0 * red[0] : red[0];
+    if (tid == 0) part[((size_t)b * MT_CHUNKS + ch) * 5 + q] = red[0];
     __syncthreads();
   }
+}
+
+__global__ void mll_terms_finalize(int B, const double* __restrict__ part, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * 5) return;
+  const int b = e / 5, q = e % 5;
+  double s = 0.0;
+#pragma unroll 8
+  for (int ch = 0; ch < MT_CHUNKS; ++ch) s += part[((size_t)b * MT_CHUNKS + ch) * 5 + q];
+  out[e] = (q == 0) ? 2.0 * s : s;
 }
 
 __global__ void posterior_finalize_kernel(int B, int n, int nt, const double* __restrict__ R,
@@ -381,7 +404,7 @@ int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, con
   else LAUNCH(64);
 #undef LAUNCH
   EVR_LAUNCH_CHECK();
-  colsum_kernel<<<cdiv(B * d, 64), 64, 0, s>>>(B, n, d, work, gls);
+  colsum_kernel<<<B * d, 256, 0, s>>>(B, n, d, work, gls);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -389,8 +412,14 @@ int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, con
 int evr_gp_mll_terms(void* stream, int B, int n, const double* L, const double* Linv, const double* r,
                      const double* alpha, double* out) {
   EVR_CHECK(B >= 1 && n >= 1, "evr_gp_mll_terms: bad sizes");
-  mll_terms_kernel<<<B, 256, 0, (hipStream_t)stream>>>(n, L, Linv, r, alpha, out);
+  hipStream_t s = (hipStream_t)stream;
+  double* part = nullptr;
+  EVR_HIP(hipMallocAsync((void**)&part, sizeof(double) * (size_t)B * MT_CHUNKS * 5, s));
+  mll_terms_kernel<<<dim3(B, MT_CHUNKS), 256, 0, s>>>(n, L, Linv, r, alpha, part);
   EVR_LAUNCH_CHECK();
+  mll_terms_finalize<<<cdiv(B * 5, 64), 64, 0, s>>>(B, part, out);
+  EVR_LAUNCH_CHECK();
+  EVR_HIP(hipFreeAsync(part, s));
   return 0;
 }
 

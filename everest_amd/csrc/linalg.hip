@@ -274,21 +274,16 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
     E[i][c] = (i == c) ? 1.0 : 0.0;
   }
   __syncthreads();
+  // 16 x 16 thread grid over (row i, column c): no integer division in the step loop
+  const int tx = tid & 15, ty = tid >> 4;
   for (int j = 0; j < nb; ++j) {
     const double p = D[j][j];
     if (!(p > 0.0)) break;  // uniform
     const double ip = 1.0 / p;
-    const int rem = nb - j - 1;
-    const int t1 = rem * rem, t2 = rem * (j + 1);
-    for (int e = tid; e < t1 + t2; e += 256) {
-      if (e < t1) {
-        const int i = j + 1 + e / rem, c = j + 1 + e % rem;
-        if (c <= i) D[i][c] -= D[i][j] * D[c][j] * ip;
-      } else {
-        const int f = e - t1;
-        const int i = j + 1 + f / (j + 1), c = f % (j + 1);
-        E[i][c] -= D[i][j] * ip * E[j][c];
-      }
+    for (int i = j + 1 + ty; i < nb; i += 16) {
+      const double dij = D[i][j] * ip;
+      for (int c = j + 1 + tx; c <= i; c += 16) D[i][c] -= dij * D[c][j];
+      for (int c = tx; c <= j; c += 16) E[i][c] -= dij * E[j][c];
     }
     __syncthreads();
   }
