@@ -186,8 +186,30 @@ class BotorchSurrogates:
         self.surrogates = [SingleTaskGPSurrogate(s) for s in data_model.surrogates]
 
     def fit(self, experiments: pd.DataFrame):
-        for s in self.surrogates:
-            s.fit(experiments)
+        """Fits the per-output GPs (independent problems, as in the reference's sequential
+        loop) concurrently: one host thread and one HIP stream per output, so the small,
+        latency-bound MLL kernels of the outputs overlap on the device.  Every fit is
+        deterministic on its own stream, so the hyperparameters do not depend on the overlap.
+        EVR_FIT_THREADS=1 restores the sequential loop."""
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+
+        workers = int(os.environ.get("EVR_FIT_THREADS", "0") or 0) or len(self.surrogates)
+        if workers <= 1 or len(self.surrogates) <= 1 or not torch.cuda.is_available():
+            for s in self.surrogates:
+                s.fit(experiments)
+            return
+        dev = device()
+
+        def run(s):
+            stream = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(stream):
+                s.fit(experiments)
+            stream.synchronize()
+
+        with ThreadPoolExecutor(max_workers=min(workers, len(self.surrogates))) as ex:
+            for f in [ex.submit(run, s) for s in self.surrogates]:
+                f.result()
 
     def compatibilize(self, inputs, outputs) -> GPBatch:
         """One batched device model over the outputs in domain order (ModelListGP analogue).
