@@ -20,8 +20,8 @@ step bench 600 python bench.py &&
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
      python bench.py --no-cpu-baseline --no-ask &&
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
-     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad" -- python tools/loop_step.py 10 &&
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 &&
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
-     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad" -- python tools/loop_step.py 10 &&
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 &&
 python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json"
 echo "done rc=$?"
