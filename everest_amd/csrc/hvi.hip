@@ -26,6 +26,10 @@
 #include <cstdlib>
 
 #include "common.hpp"
+
+#ifndef EVR_KD_EXP
+#define EVR_KD_EXP 0   // experiment switches of the instrumented builds (0 = production)
+#endif
 #include "../../include/everest_amd.h"
 
 namespace evr {
@@ -446,6 +450,22 @@ __device__ __forceinline__ int wave_scan_excl(int v, int* total) {
 // barrier each wave owns 16 candidates and runs the group filter, the cell filter windows,
 // the term evaluation and the accumulation alone (wave-level DPP scans, no workgroup
 // barriers) — candidates are wave-exclusive, so the accumulators need no inter-wave order.
+#ifndef EVR_KD_PROF
+#define EVR_KD_PROF 0
+#endif
+// phase timers of the instrumented build (EVR_KD_PROF=1): per-wave clock deltas summed into
+// counters[4 + phase] (0 stage, 1 group filter + prefix, 2 cell filter, 3 term evaluation,
+// 4 segmented scan + accumulate)
+#define KD_T0() long long kd_t = EVR_KD_PROF ? clock64() : 0
+#define KD_T(ph)                                                                      \
+  do {                                                                                \
+    if (EVR_KD_PROF && kd.counters) {                                                 \
+      const long long kd_n = clock64();                                               \
+      if ((threadIdx.x & 63) == 0) atomicAdd(kd.counters + 4 + (ph), (unsigned long long)(kd_n - kd_t)); \
+      kd_t = kd_n;                                                                    \
+    }                                                                                 \
+  } while (0)
+
 template <int M, bool BWD>
 __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                               const int* __restrict__ thg, HviKd kd,
@@ -478,6 +498,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
   const int c0 = tile * KD_CT, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int stride = kd.stride;
+  KD_T0();
   const int split = blockIdx.z;
   const int NQall = (kd.goff[s + 1] - kd.goff[s] + 15) >> 4;
   const int qper = (NQall + nsplit - 1) / nsplit;
@@ -517,6 +538,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
   }
   for (int e = tid; e < KD_CT * NV; e += 256) (&acc[0][0])[e] = 0.0;
   __syncthreads();
+  KD_T(0);
   const int cbase = wave * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
   if (c0 + cbase >= b) return;
 
@@ -558,6 +580,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
     }
   }
   wave_sync();
+  KD_T(1);
 
   int* wm = wmask[wave];
   int* wc = wcg[wave];
@@ -603,29 +626,52 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
     }
     int EW;
     const int pre = wave_scan_excl(__popc(mB), &EW);
+    KD_T(2);
     wm[lane] = (int)mB;
     wc[lane] = cg;
     wp[lane] = pre;
     if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
     wave_sync();
     // ---- C: evaluation (lane = exact (cell, candidate) term) ----
+    // software-pipelined: the next round's term is located and its key load issued before
+    // the current round is decoded and evaluated (hides the L2 latency of the key fetch)
+    auto locate = [&](int q, int& c, unsigned long long& key) {
+      int lo = 0, hi = 63;
+      if (EVR_KD_EXP == 2) lo = hi = q & 63;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (wp[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      c = wc[lo] >> 16;
+      const int g = wc[lo] & 0xFFFF;
+      const int bit = kth_bit16((unsigned int)wm[lo], q - wp[lo]);
+      key = kd.gkeys[(size_t)(gbase + g) * 16 + bit];
+    };
+    int cnext = -1;
+    unsigned long long knext = 0;
+    if (lane < EW) locate(lane, cnext, knext);
     for (int cb = 0; cb < EW; cb += 64) {
       const int q = cb + lane;
+      const int c = cnext;
+      const unsigned long long key = knext;
+      cnext = -1;
+      if (cb + 64 + lane < EW) locate(cb + 64 + lane, cnext, knext);
       int rcv = -1;
       double val[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) val[v] = 0.0;
       if (q < EW) {
-        int lo = 0, hi = 63;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (wp[mid] <= q) lo = mid;
-          else hi = mid - 1;
-        }
-        const int c = wc[lo] >> 16, g = wc[lo] & 0xFFFF;
-        const int bit = kth_bit16((unsigned int)wm[lo], q - wp[lo]);
         double l[M], u[M];
-        K::decode(kd.gkeys[(size_t)(gbase + g) * 16 + bit], pt, r0, l, u);
+        if (EVR_KD_EXP == 1) {
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            l[j] = -1.0 + 1e-3 * (double)((key >> (8 * j)) & 0xFF);
+            u[j] = l[j] + 0.5;
+          }
+        } else {
+          K::decode(key, pt, r0, l, u);
+        }
         double y[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) y[j] = yv[c][j];
@@ -657,6 +703,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
         }
         rcv = c;
       }
+      KD_T(3);
       // segmented scan over the round (terms of a candidate are contiguous); segment ends
       // add into the candidate's accumulator (owned by this wave)
       seg_scan_wave<NV>(rcv, val);
@@ -665,6 +712,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[rcv][v] += val[v];
       }
+      KD_T(4);
     }
     wave_sync();   // wm / wc / wp are rewritten by the next window
   }

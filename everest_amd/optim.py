@@ -180,12 +180,78 @@ def host_values(t: torch.Tensor) -> np.ndarray:
     return v
 
 
+def _reduce_constraints(cons: Sequence[LinearConstraint], fixed: dict, free: List[int]) -> List[LinearConstraint]:
+    """Constraints over the free dims only: fixed terms move to the right-hand side
+    ([upstream] botorch _generate_unfixed_lin_constraints)."""
+    pos = {j: k for k, j in enumerate(free)}
+    out = []
+    for idx, coef, rhs in cons:
+        idx = np.asarray(idx, dtype=int)
+        coef = np.asarray(coef, dtype=np.float64)
+        keep = np.array([i in pos for i in idx], dtype=bool)
+        r = float(rhs) - float(sum(c * fixed[int(i)] for i, c in zip(idx[~keep], coef[~keep])))
+        if keep.any():
+            out.append((np.array([pos[int(i)] for i in idx[keep]]), coef[keep], r))
+    return out
+
+
+class _FixedFeatures:
+    """Acquisition over the free dims with the fixed ones inserted ([upstream]
+    FixedFeatureAcquisitionFunction as used by optimize_acqf(fixed_features=...))."""
+
+    def __init__(self, acqf, d: int, fixed: dict):
+        self.acqf, self.d, self.dev = acqf, d, acqf.dev
+        self.fixed_idx = np.array(sorted(fixed), dtype=int)
+        self.fixed_val = np.array([fixed[j] for j in sorted(fixed)], dtype=np.float64)
+        self.free = [j for j in range(d) if j not in fixed]
+
+    def full_np(self, x: np.ndarray) -> np.ndarray:
+        X = np.empty((x.shape[0], self.d))
+        X[:, self.free] = x
+        X[:, self.fixed_idx] = self.fixed_val
+        return X
+
+    def _full_t(self, X: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(X.shape[0], self.d, dtype=torch.float64, device=self.dev)
+        out[:, self.free] = X.to(device=self.dev, dtype=torch.float64)
+        out[:, torch.as_tensor(self.fixed_idx, device=self.dev)] = torch.as_tensor(self.fixed_val, device=self.dev)
+        return out
+
+    def forward(self, X):
+        return self.acqf.forward(self._full_t(X))
+
+    def forward_backward(self, X):
+        a, g = self.acqf.forward_backward(self._full_t(X))
+        return a, g[:, self.free]
+
+    def eval_host(self, x: np.ndarray, backward: bool):
+        if hasattr(self.acqf, "eval_host"):
+            a, g = self.acqf.eval_host(self.full_np(x), backward)
+            return a, (g[:, self.free] if backward else None)
+        Xt = torch.as_tensor(self.full_np(x), dtype=torch.float64, device=self.dev)
+        if backward:
+            a, g = self.acqf.forward_backward(Xt)
+            return a.cpu().numpy(), g[:, self.free].cpu().numpy()
+        return self.acqf.forward(Xt).cpu().numpy(), None
+
+
 def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int, options: dict,
                   gen: torch.Generator, inequality_constraints: Sequence[LinearConstraint] = (),
                   equality_constraints: Sequence[LinearConstraint] = (), dist=None,
-                  stats: Optional[OptimizeStats] = None):
+                  stats: Optional[OptimizeStats] = None, fixed_features: Optional[dict] = None):
     """Returns (best x (d,), best value, stats).  ``acqf`` exposes forward(X) and
-    forward_backward(X) on device tensors of raw (transformed) inputs."""
+    forward_backward(X) on device tensors of raw (transformed) inputs.  ``fixed_features``
+    {column: value} are held fixed: raw samples get them set, the restarts optimise the free
+    columns only ([upstream] optimize_acqf(fixed_features=...))."""
+    if fixed_features:
+        bounds = np.asarray(bounds, dtype=np.float64)
+        d_full = bounds.shape[1]
+        fx = {int(k): float(v) for k, v in fixed_features.items()}
+        wrap = _FixedFeatures(acqf, d_full, fx)
+        x, v, st = optimize_acqf(wrap, bounds[:, wrap.free], num_restarts, raw_samples, options, gen,
+                                 _reduce_constraints(inequality_constraints, fx, wrap.free),
+                                 _reduce_constraints(equality_constraints, fx, wrap.free), dist=dist, stats=stats)
+        return wrap.full_np(x[None, :])[0], v, st
     import time
 
     stats = stats or OptimizeStats()
@@ -320,3 +386,20 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         stats.opt_evals_global = stats.opt_evals
     stats.t_opt += time.perf_counter() - t0
     return best_x, best_v, stats
+
+
+def optimize_acqf_mixed(acqf, bounds: np.ndarray, fixed_features_list: Sequence[dict], num_restarts: int,
+                        raw_samples: int, options: dict, gen: torch.Generator,
+                        inequality_constraints: Sequence[LinearConstraint] = (),
+                        equality_constraints: Sequence[LinearConstraint] = (), dist=None):
+    """[upstream] botorch.optim.optimize_acqf_mixed (q = 1), as BoFire calls it for the
+    EXHAUSTIVE categorical method (bofire/strategies/predictives/botorch.py:358-378): one
+    optimize_acqf per fixed-feature combination, best acquisition value wins (first on ties)."""
+    stats = OptimizeStats()
+    best = (None, -np.inf)
+    for ff in fixed_features_list:
+        x, v, stats = optimize_acqf(acqf, bounds, num_restarts, raw_samples, options, gen, inequality_constraints,
+                                    equality_constraints, dist=dist, stats=stats, fixed_features=ff)
+        if best[0] is None or v > best[1]:
+            best = (x, v)
+    return best[0], best[1], stats

@@ -20,7 +20,7 @@ import torch
 from . import data_models as dm
 from .acquisition import QNEHVI, QEI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
-from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf
+from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
 from .surrogates import BotorchSurrogates, device
 
 
@@ -260,6 +260,7 @@ class BotorchStrategy(PredictiveStrategy):
         self.maxiter = data_model.maxiter
         self.batch_limit = data_model.batch_limit
         self.surrogate_specs = data_model.surrogate_specs
+        self.categorical_method = getattr(data_model.categorical_method, "value", data_model.categorical_method)
         self.surrogates: Optional[BotorchSurrogates] = None
         self.model = None
         self.dist = dist
@@ -325,11 +326,62 @@ class BotorchStrategy(PredictiveStrategy):
         acqf = self._get_acqfs(candidate_count)[0]
         ineq = get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
         eq = get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
-        x, val, stats = optimize_acqf(acqf, self._bounds(), self.num_restarts, self.num_raw_samples,
-                                      self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist)
+        combos = self.get_categorical_combinations()
+        if len(combos) > 1:     # EXHAUSTIVE categorical method: optimize_acqf_mixed
+            x, val, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts, self.num_raw_samples,
+                                                self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist)
+        else:
+            x, val, stats = optimize_acqf(acqf, self._bounds(), self.num_restarts, self.num_raw_samples,
+                                          self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
+                                          fixed_features=combos[0] or None)
         stats.best_value = val
         self.last_ask_stats = stats
         return self._postprocess_candidates(x[None, :])
+
+    def get_fixed_features(self) -> dict:
+        """bofire/strategies/predictives/botorch.py:530-595 (continuous / one-hot part):
+        fixed inputs, and with the FREE categorical method the forbidden one-hot columns."""
+        f2i, _ = self.domain.inputs._transform_info(self.input_preprocessing_specs)
+        fixed = {}
+        for feat in self.domain.inputs.get().features:
+            fv = feat.fixed_value() if hasattr(feat, "fixed_value") else None
+            if fv is not None:
+                if isinstance(feat, dm.CategoricalInput):
+                    enc = feat.to_onehot_encoding(pd.Series([fv[0]])).values[0]
+                    for j, idx in enumerate(f2i[feat.key]):
+                        fixed[idx] = float(enc[j])
+                else:
+                    fixed[f2i[feat.key][0]] = float(fv[0])
+        if self.categorical_method == "FREE":
+            for feat in self.domain.inputs.get([dm.CategoricalInput]).features:
+                if self.input_preprocessing_specs.get(feat.key) == "ONE_HOT" and not feat.is_fixed():
+                    for cat in feat.get_forbidden_categories():
+                        j = feat.categories.index(cat)
+                        fixed[f2i[feat.key][j]] = 0.0
+        return fixed
+
+    def get_categorical_combinations(self) -> list:
+        """bofire/strategies/predictives/botorch.py:597-672 (ONE_HOT categoricals): with the
+        EXHAUSTIVE categorical method every combination of allowed categories (itertools
+        product in input order) becomes one fixed-feature dict on top of the fixed basis."""
+        import itertools
+
+        basis = self.get_fixed_features()
+        if self.categorical_method == "FREE":
+            return [basis]
+        feats = [f for f in self.domain.inputs.get([dm.CategoricalInput]).features if not f.is_fixed()]
+        if not feats:
+            return [basis]
+        f2i, _ = self.domain.inputs._transform_info(self.input_preprocessing_specs)
+        out = []
+        for combo in itertools.product(*[[(f, c) for c in f.get_allowed_categories()] for f in feats]):
+            ff = dict(basis)
+            for f, c in combo:
+                enc = f.to_onehot_encoding(pd.Series([c])).values[0]
+                for j, idx in enumerate(f2i[f.key]):
+                    ff[idx] = float(enc[j])
+            out.append(ff)
+        return out
 
     def _postprocess_candidates(self, X: np.ndarray) -> pd.DataFrame:
         f2i, f2n = self.domain.inputs._transform_info(self.input_preprocessing_specs)
