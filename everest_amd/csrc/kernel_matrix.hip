@@ -87,6 +87,102 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
   }
 }
 
+// Kernel-matrix assembly on the matrix cores for wide inputs (d >= 16): the 64x64 tile of
+// dot products u1_i . u2_j (u = normalised x / ls) runs on v_mfma_f64_16x16x4f64 over the
+// d axis, the epilogue forms d2 = |u1|^2 + |u2|^2 - 2 u1.u2 (clamped at 0; exactly 0 where a
+// diagonal entry pairs bitwise-identical points, as GPyTorch's sq_dist does for x1_eq_x2),
+// applies the kernel, outputscale and diagonal add, and streams the tile out: the f64 VALU
+// distance loop of kmat_kernel (2 flop per coordinate per entry) was the bound at d = 32.
+using kd4_t = __attribute__((ext_vector_type(4))) double;
+
+template <int DP>
+__global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
+                                                        const double* __restrict__ X1, const double* __restrict__ sh1,
+                                                        const double* __restrict__ sc1, const double* __restrict__ X2,
+                                                        const double* __restrict__ sh2, const double* __restrict__ sc2,
+                                                        const double* __restrict__ ls, const double* __restrict__ os,
+                                                        const double* __restrict__ dg, double* __restrict__ K) {
+  __shared__ double As[DP][KT + 2];
+  __shared__ double Bs[DP][KT + 2];
+  __shared__ double na[KT], nb2[KT];
+  __shared__ int eqr[KT];   // diagonal tiles: row r of both operands bitwise identical
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int bx = t % gx, by = (t / gx) % gy, b = t / (gx * gy);
+  const int i0 = by * KT, j0 = bx * KT;
+  const double* lsb = ls + (size_t)b * d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < KT * DP; e += 256) {
+    const int r = e / DP, k = e - r * DP;
+    double v = 0.0, w = 0.0;
+    if (k < d) {
+      const double il = 1.0 / lsb[k];
+      if (i0 + r < n1) {
+        v = X1[(size_t)(i0 + r) * d + k];
+        if (sh1) v -= sh1[k];
+        if (sc1) v *= sc1[k];
+        v *= il;
+      }
+      if (j0 + r < n2) {
+        w = X2[(size_t)(j0 + r) * d + k];
+        if (sh2) w -= sh2[k];
+        if (sc2) w *= sc2[k];
+        w *= il;
+      }
+    }
+    As[k][r] = v;
+    Bs[k][r] = w;
+  }
+  __syncthreads();
+  if (tid < 2 * KT) {
+    const int r = tid & (KT - 1);
+    double sq = 0.0;
+    if (tid < KT) {
+      int eq = 1;
+      for (int k = 0; k < DP; ++k) {
+        sq = fma(As[k][r], As[k][r], sq);
+        eq &= As[k][r] == Bs[k][r];
+      }
+      na[r] = sq;
+      eqr[r] = eq;
+    } else {
+      for (int k = 0; k < DP; ++k) sq = fma(Bs[k][r], Bs[k][r], sq);
+      nb2[r] = sq;
+    }
+  }
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int i = lane & 15, kq = lane >> 4;
+  kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int kk = 0; kk < DP; kk += 4) {
+    const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
+    const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+  }
+  __syncthreads();   // na / nb2
+  const double scale = os ? os[b] : 1.0;
+  const double dadd = dg ? dg[b] : 0.0;
+  double* Kb = K + (size_t)b * n1 * n2;
+  const int col = lane & 15, rq = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+      const int gi = i0 + li, gj = j0 + lj;
+      if (gi < n1 && gj < n2) {
+        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+        if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
+        double v = scale * kernel_value(kind, d2);
+        if (gi == gj) v += dadd;
+        Kb[(size_t)gi * n2 + gj] = v;
+      }
+    }
+}
+
 // dX2[c][k] = sum_b sum_i G[b][i][c] * dk_b(x1_i, x2_c)/dx2_ck.
 // Block = 64 candidates (lanes; G rows read coalesced, candidates fastest) x 4 row groups
 // (waves; all lanes of a wave share the training row -> broadcast loads); the rows are
@@ -365,6 +461,19 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
             B, n1, n2, d);
   if (n1 == 0 || n2 == 0) return 0;
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
+  if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
+    hipStream_t s = (hipStream_t)stream;
+#define KM(DP_)                                                                                                 \
+  kmat_mfma_kernel<DP_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2,     \
+                                             lengthscales, outputscale, diag_add, K)
+    if (d <= 16) KM(16);
+    else if (d <= 32) KM(32);
+    else if (d <= 48) KM(48);
+    else KM(64);
+#undef KM
+    EVR_LAUNCH_CHECK();
+    return 0;
+  }
   const size_t lds = (size_t)2 * KT * (d + 1) * sizeof(double);
   kmat_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2,
                                                        lengthscales, outputscale, diag_add, K);

@@ -57,7 +57,8 @@ def test_kernel_matrix(kind, n1, n2, d):
     for b in range(3):
         ref = ogp.kernel_matrix(torch.tensor((X1 - lo) / (hi - lo)), torch.tensor((X2 - lo) / (hi - lo)),
                                 torch.tensor(ls[b]), kind, os_[b])
-        assert torch.allclose(K[b], ref, rtol=1e-12, atol=1e-13)
+        tol = 1e-13 if d < 16 else 1e-11     # d >= 16: matrix-core distance expansion (GPyTorch's sq_dist)
+        assert torch.allclose(K[b], ref, rtol=1e-12, atol=tol)
 
 
 @pytest.mark.parametrize("n", [1, 7, 32, 33, 100, 256, 513])
@@ -110,3 +111,43 @@ def test_trsm_and_inverse(n, nrhs, trans):
     assert torch.allclose(X.cpu(), ref, rtol=1e-10, atol=1e-11)
     Li = ops.tri_inv(_t(L)).cpu()
     assert torch.allclose(Li, torch.linalg.inv(L), rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("d,kind", [(16, 0), (32, 3), (40, 1), (64, 2)])
+def test_kernel_matrix_wide_mfma(d, kind):
+    """d >= 16 runs the matrix-core distance expansion: symmetric (diagonal exactly k(0) +
+    noise) and cross calls vs explicit differences in float64."""
+    from everest_amd import ops
+
+    rng = np.random.default_rng(d)
+    n1, n2, B = 300, 130, 2
+    lo, hi = np.zeros(d), np.full(d, 2.0)
+    X1 = rng.uniform(0, 2, size=(n1, d))
+    X2 = rng.uniform(0, 2, size=(n2, d))
+    ls = rng.uniform(0.5, 2.0, size=(B, d))
+    noise = np.array([1e-3, 2e-2])
+    t = lambda a: torch.tensor(a, dtype=torch.float64, device="cuda")  # noqa: E731
+
+    def ref(A, Bm, b):
+        U = torch.tensor((A - lo) / (hi - lo) / ls[b]); V = torch.tensor((Bm - lo) / (hi - lo) / ls[b])
+        d2 = ((U[:, None, :] - V[None, :, :]) ** 2).sum(-1)
+        r = torch.sqrt(torch.clamp(d2, min=1e-30))
+        if kind == 0:
+            return torch.exp(-0.5 * d2)
+        if kind == 1:
+            return torch.exp(-r)
+        if kind == 2:
+            return (1 + 3 ** 0.5 * r) * torch.exp(-(3 ** 0.5) * r)
+        return (1 + 5 ** 0.5 * r + 5.0 / 3.0 * d2) * torch.exp(-(5 ** 0.5) * r)
+
+    inv = t(1.0 / (hi - lo))
+    Ks = ops.kernel_matrix(t(X1), t(X1), t(ls), kind, shift1=t(lo), scale1=inv, shift2=t(lo), scale2=inv,
+                           diag_add=t(noise)).cpu()
+    Kc = ops.kernel_matrix(t(X1), t(X2), t(ls), kind, shift1=t(lo), scale1=inv, shift2=t(lo), scale2=inv).cpu()
+    for b in range(B):
+        Rs = ref(X1, X1, b) + noise[b] * torch.eye(n1, dtype=torch.float64)
+        assert torch.allclose(Ks[b], Rs, rtol=1e-10, atol=1e-11)
+        # zero distance on the diagonal: k(0) (kind 1 takes sqrt(1e-30) like GPyTorch) + noise to ~1 ulp;
+        # a rounded expansion would leave d2 ~ 1e-15, i.e. r ~ 3e-8 there
+        assert torch.allclose(torch.diagonal(Ks[b]), torch.diagonal(Rs), rtol=0, atol=2.0 ** -49)
+        assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
