@@ -68,7 +68,7 @@ class QNEHVI:
                  prune_samples: int = 2048, max_frac: float = 1.0, z_prune: Optional[torch.Tensor] = None,
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
                  num_threads: Optional[int] = None, box_device: Optional[bool] = None,
-                 kd_scan: Optional[bool] = None):
+                 kd_scan: Optional[bool] = None, X_pending_raw: Optional[np.ndarray] = None):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -90,14 +90,29 @@ class QNEHVI:
         except KeyError as e:
             raise ValueError("qNEHVI: every baseline point must be a training point of the models") from e
 
+        # pending points ([upstream] set_X_pending with cache_pending=True, max_iep=0) join
+        # the baseline after pruning: the kernel-vector row set grows to X_k = [X_train;
+        # X_pending] (n_k = n + n_p rows), L^-1 / alpha are zero-padded over the pending
+        # columns, and every formula below runs unchanged over n_k.
+        npend = 0 if X_pending_raw is None else int(np.asarray(X_pending_raw).shape[0])
+        self.n_pending = npend
+        if npend > 0:
+            Xp = torch.as_tensor(np.asarray(X_pending_raw, dtype=np.float64).reshape(npend, gp.d), **f64)
+            self.Xk = torch.cat([gp.Xn, (Xp - gp.lo) * gp.inv_range], 0).contiguous()
+        else:
+            self.Xk = gp.Xn
+        nk = n + npend
+        self.nk = nk
+
         import time as _time
         tm = {}
         t0 = _time.perf_counter()
-        # ---- joint posterior at the training inputs (shared by prune and baseline) --------
-        K = gp.kernel_train(noise=False)                                  # m x n x n
-        mu_t = ops.gemm(K, gp.alpha.unsqueeze(-1))[..., 0]                 # K alpha
+        # ---- joint posterior at the training (+ pending) inputs, shared by prune and baseline
+        K = ops.kernel_matrix(self.Xk, self.Xk, gp.ls, gp.kind) if npend else gp.kernel_train(noise=False)
+        Kt = K[:, :, :n].contiguous() if npend else K                      # m x nk x n
+        mu_t = ops.gemm(Kt, gp.alpha.unsqueeze(-1))[..., 0]                # K alpha
         mu_train = gp.ym[:, None] + gp.ys[:, None] * (gp.const[:, None] + mu_t)
-        A = ops.gemm(gp.Linv, K)                                          # L^-1 K
+        A = ops.gemm(gp.Linv, K[:, :n].contiguous() if npend else K)      # L^-1 K  (m x n x nk)
         Sig = ops.gemm(A, A, transA=True, alpha=-1.0, beta=1.0, out=K)    # K - A^T A (in place)
         ops.scale_batched(Sig, (gp.ys ** 2).contiguous())                 # unstandardize
 
@@ -125,6 +140,9 @@ class QNEHVI:
                 keep = order[:max_points]
             keep = np.unique(keep)
             base_rows = base_rows[keep]
+        nb_t = int(base_rows.shape[0])                 # pruned training baseline
+        if npend:
+            base_rows = np.concatenate([base_rows, n + np.arange(npend, dtype=np.int64)])
         nb = int(base_rows.shape[0])
         self.nb = nb
         self.base_rows = base_rows
@@ -136,14 +154,19 @@ class QNEHVI:
             self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
         S_ = self.S
-        # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed
+        # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed;
+        # pending rows from the (nb_t+n_p)*m-dimensional draw ([upstream] _update_base_samples
+        # keeps the earlier rows of the base sampler, the same seed draws the new ones)
         if z_new_full is None:
             self.zq = ops.sobol_normal(S_, (nb + 1) * m, sampler_seed, dev, d0=nb * m, nd=m)   # S x m
         else:
             self.zq = z_new_full[:, nb, :].to(**f64).contiguous()
         if nb > 0:
             if z_base_full is None:
-                Zb = sobol_base_samples(S_, nb, m, sampler_seed, dev)                # m x nb x S
+                Zb = sobol_base_samples(S_, nb_t, m, sampler_seed, dev)              # m x nb x S
+                if npend:
+                    Zp_ = ops.sobol_normal(S_, nb * m, sampler_seed, dev, d0=nb_t * m, nd=npend * m, layout=1, m=m)
+                    Zb = torch.cat([Zb, Zp_], 1).contiguous()
             else:
                 Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
             Yb = ops.gemm(self.L_base, Zb)
@@ -174,29 +197,31 @@ class QNEHVI:
         self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(np.sum(counts_c)),
                                        max_cells=int(counts_c.max()) if len(counts_c) else 0, prune_probs=probs)
 
-        # ---- forward operator M = [Linv; G; H^T; alpha^T] ------------------------------
-        Rr = n + nb + S_ + 1
+        # ---- forward operator M = [Linv; G; H^T; alpha^T] over the nk kernel rows --------
+        Rr = nk + nb + S_ + 1
         self.Rr = Rr
-        M = torch.empty(m, Rr, n, **f64)
-        M[:, :n].copy_(gp.Linv)
+        M = torch.zeros(m, Rr, nk, **f64) if npend else torch.empty(m, Rr, n, **f64)
+        M[:, :n, :n].copy_(gp.Linv)
         if nb > 0:
             A_b = A[:, :, idx].contiguous()                                     # m x n x nb
             E = ops.gemm(A_b, gp.Linv, transA=True, alpha=-1.0)                 # -A_b^T Linv
+            if npend:
+                E = torch.cat([E, torch.zeros(m, nb, npend, **f64)], 2).contiguous()
             ops.add_selection(E, idx.to(torch.int32), None)                      # + P
             ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
             ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
-            M[:, n:n + nb].copy_(E)
-            ops.gemm_into(M[:, n + nb:n + nb + S_], Zb, E, transA=True)          # H^T = Z^T G
+            M[:, nk:nk + nb].copy_(E)
+            ops.gemm_into(M[:, nk + nb:nk + nb + S_], Zb, E, transA=True)        # H^T = Z^T G
         else:
-            M[:, n:n + S_].zero_()
-        M[:, Rr - 1].copy_(gp.alpha)
+            M[:, nk:nk + S_].zero_()
+        M[:, Rr - 1, :n].copy_(gp.alpha)
         self.M = M
-        self.state = ops.make_state(n, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
+        self.state = ops.make_state(nk, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
                                     cells)
         self._keep = (self.zq, self.obj_a, self.obj_b)
         self._lo_c = gp.lo.to(torch.float64).contiguous()
         self._scale_c = gp.inv_range.to(torch.float64).contiguous()
-        self.model = _native.EvrQnehviModel(n=n, d=gp.d, kind=gp.kind, Xn=gp.Xn.data_ptr(), lengthscales=gp.ls.data_ptr(),
+        self.model = _native.EvrQnehviModel(n=nk, d=gp.d, kind=gp.kind, Xn=self.Xk.data_ptr(), lengthscales=gp.ls.data_ptr(),
                                             shift=self._lo_c.data_ptr(), scale=self._scale_c.data_ptr(),
                                             M=self.M.data_ptr())
         self._plans = {}
@@ -246,6 +271,11 @@ class QNEHVI:
         acq = out[:b].copy()
         return acq, (out[b:].reshape(b, -1).copy() if backward else None)
 
+    def _cross(self, X: torch.Tensor) -> torch.Tensor:
+        """K(X_k, normalize(X)) : m x nk x b over the training (+ pending) rows."""
+        gp = self.gp
+        return ops.kernel_matrix(self.Xk, X, gp.ls, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+
     def forward_ops(self, X: torch.Tensor, return_cache: bool = False):
         """X: b x d raw (transformed) candidates on device -> acquisition values (b).
 
@@ -254,7 +284,7 @@ class QNEHVI:
         the NotPSDError BoTorch raises from sample_cached_cholesky."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
-        Kx = self.gp.cross(X)                       # m x n x b
+        Kx = self._cross(X)                         # m x nk x b
         R, P = ops.qnehvi_project(self.state, self.M, Kx, b)    # m x Rr x b + partial norms
         G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
         acq = ops.hvi_forward(self.state, G, b, flags)
@@ -266,13 +296,13 @@ class QNEHVI:
         """Op-by-op chain: returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         b = X.shape[0]
-        Kx = self.gp.cross(X)
+        Kx = self._cross(X)
         R, P = ops.qnehvi_project(self.state, self.M, Kx, b)
         G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
         acq, dG = ops.hvi_forward_backward(self.state, G, b, flags, gout)
-        dKx = ops.qnehvi_project_backward(self.state, self.M, R, L22, dG, b)    # m x n x b
+        dKx = ops.qnehvi_project_backward(self.state, self.M, R, L22, dG, b)    # m x nk x b
         gp = self.gp
-        dX = ops.kernel_cross_grad(gp.Xn, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+        dX = ops.kernel_cross_grad(self.Xk, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
         return acq, dX
 
 

@@ -437,8 +437,6 @@ class QnehviStrategy(BotorchStrategy):
         """bofire/strategies/predictives/qnehvi.py:23-53."""
         assert self.experiments is not None, "No experiments available."
         X_train, X_pending = self.get_acqf_input_tensors()
-        if X_pending is not None:
-            raise NotImplementedError("pending candidates (X_pending) are not yet supported on the device path")
         if self.alpha != 0.0:
             raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
         a, b = self._objective_affine()
@@ -447,7 +445,7 @@ class QnehviStrategy(BotorchStrategy):
         prune_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
         sampler_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=self.num_sobol_samples,
-                      sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed)
+                      sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending)
         self.last_acqf = acqf
         return [acqf]
 

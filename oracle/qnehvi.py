@@ -43,6 +43,19 @@ def base_samples(S: int, n_points: int, m: int, seed: int) -> torch.Tensor:
     return draw_sobol_normal_samples(n_points * m, S, seed).view(S, n_points, m)
 
 
+def base_samples_pending(S: int, nb: int, npend: int, q: int, m: int, seed: int):
+    """Base samples once ``npend`` pending points join a baseline of ``nb`` pruned points
+    ([upstream] ``set_X_pending`` with cache_pending=True, max_iep=0: the points are appended
+    to X_baseline and the base sampler is extended by ``_update_base_samples``, which keeps
+    the existing rows and takes the new rows from a draw of the enlarged dimension with the
+    same seed).  Returns (z_base S x (nb+npend) x m, z_new S x q x m)."""
+    zb = base_samples(S, nb, m, seed)
+    if npend:
+        zb = torch.cat([zb, base_samples(S, nb + npend, m, seed)[:, nb:]], 1)
+    zn = base_samples(S, nb + npend + q, m, seed)[:, nb + npend:]
+    return zb, zn
+
+
 @dataclass
 class Objective:
     """Affine objective g_j(y) = a_j*y_j + b_j (Maximize/Minimize with bounds,

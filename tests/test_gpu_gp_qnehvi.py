@@ -174,3 +174,64 @@ def test_qnehvi_compressed_cells_match_explicit_cells():
     assert torch.allclose(a1, a2, rtol=1e-12, atol=1e-15)
     assert torch.allclose(g1, g2, rtol=1e-10, atol=1e-13)
     assert torch.allclose(dev_q.forward(Xc), a1, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("npend,prune", [(1, True), (4, True), (3, False)])
+def test_qnehvi_pending_parity(npend, prune):
+    """X_pending joins the pruned baseline (cache_pending, max_iep = 0): device values and
+    gradients vs the oracle over the enlarged baseline with the extended base samples."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 40, 4, 3, 32
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=n + npend)
+    ost = oracle_states(X, Y, lo, hi, hyp)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(m), np.zeros(m), -1.1 * np.ones(m)
+    objective = oq.Objective(torch.tensor(a), torch.tensor(b))
+    rng = np.random.default_rng(npend)
+    Xp = lo + (hi - lo) * rng.uniform(size=(npend, d))
+    Xn = torch.tensor((X - lo) / (hi - lo))
+    zp = oq.base_samples(64, n, m, 11)
+    idx = torch.arange(n)
+    if prune:
+        idx, _ = oq.prune_baseline(ost, Xn, objective, torch.tensor(ref), zp)
+    nb = idx.shape[0]
+    zb, zn = oq.base_samples_pending(S, nb, npend, 1, m, 7)
+    Xb = torch.cat([Xn[idx], torch.tensor((Xp - lo) / (hi - lo))], 0)
+    orc = oq.QNEHVI(ost, Xb, objective, torch.tensor(ref), zb, zn)
+    zfull = torch.cat([zb, zn], 1)
+    dq = QNEHVI(gp, X, X, ref, a, b, S=S, prune_baseline=prune, z_prune=zp, z_base_full=zb, z_new_full=zfull,
+                prune_samples=64, X_pending_raw=Xp)
+    assert dq.nb == nb + npend and dq.n_pending == npend
+    assert dq.stats.total_cells == sum(c.shape[1] for c in orc.cells)
+    Xc = lo + (hi - lo) * np.random.default_rng(5).uniform(size=(29, d))
+    acq, dX = dq.forward_backward(torch.tensor(Xc, device="cuda"))
+    xt = torch.tensor(Xc, requires_grad=True)
+    r = orc.forward(((xt - torch.tensor(lo)) / torch.tensor(hi - lo)).unsqueeze(1))
+    r.sum().backward()
+    assert torch.allclose(acq.cpu(), r.detach(), rtol=1e-6, atol=1e-9)
+    assert torch.allclose(dX.cpu(), xt.grad, rtol=1e-5, atol=1e-7)
+    # the op-by-op chain agrees with the native plan
+    assert torch.allclose(dq.forward_ops(torch.tensor(Xc, device="cuda")), acq, rtol=1e-12, atol=1e-15)
+
+
+def test_qnehvi_pending_device_samples_match_host_samples():
+    """Pending rows of the device-drawn base samples come from the (nb+np)*m-dim Sobol draw,
+    the new point's from the (nb+np+1)*m-dim one: equal to the oracle's host draws."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S, npend = 50, 5, 4, 32, 2
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=12)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(m), np.zeros(m), -1.1 * np.ones(m)
+    Xp = lo + (hi - lo) * np.random.default_rng(2).uniform(size=(npend, d))
+    auto = QNEHVI(gp, X, X, ref, a, b, S=S, sampler_seed=7, prune_baseline=True, prune_seed=11, prune_samples=128,
+                  X_pending_raw=Xp)
+    nb = auto.nb - npend
+    zb, zn = oq.base_samples_pending(S, nb, npend, 1, m, 7)
+    host = QNEHVI(gp, X, X, ref, a, b, S=S, prune_baseline=True, prune_samples=128,
+                  z_prune=oq.base_samples(128, n, m, 11), z_base_full=zb, z_new_full=torch.cat([zb, zn], 1),
+                  X_pending_raw=Xp)
+    assert np.array_equal(auto.base_rows, host.base_rows)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(64, d)), device="cuda")
+    assert torch.allclose(auto.forward(Xc), host.forward(Xc), rtol=1e-10, atol=1e-13)

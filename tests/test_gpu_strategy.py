@@ -46,6 +46,27 @@ def test_qnehvi_tell_ask_dtlz2(use_ref_point):
     assert st.raw_evals == 256 and st.opt_evals > 0
 
 
+def test_qnehvi_ask_add_pending():
+    """ask(add_pending=True) stores the candidate; the next ask() folds it into the baseline
+    (X_pending, bofire/strategies/predictives/qnehvi.py:47), which removes its improvement."""
+    bench, exps = _dtlz2_experiments(n=12, seed=3)
+    s = strategies.map(dm.QnehviStrategy(domain=bench.domain, ref_point=bench.ref_point, seed=7,
+                                         num_sobol_samples=128, num_raw_samples=256, num_restarts=4))
+    s.tell(exps)
+    c1 = s.ask(1, add_pending=True)
+    assert s.candidates is not None and len(s.candidates) == 1
+    keys = bench.domain.inputs.get_keys()
+    before = s.last_acqf
+    v_before = float(before.forward(torch.tensor(s._transform(c1), device=before.dev))[0])
+    c2 = s.ask(1, add_pending=True)
+    acqf = s.last_acqf
+    assert acqf.n_pending == 1 and acqf.nb == len(acqf.base_rows) and acqf.base_rows[-1] == acqf.n
+    v_after = float(acqf.forward(torch.tensor(s._transform(c1), device=acqf.dev))[0])
+    assert v_before > 0 and v_after < 0.1 * v_before
+    assert not np.allclose(c1[keys].values, c2[keys].values)
+    assert len(s.candidates) == 2
+
+
 def test_predict_matches_oracle_posterior():
     bench, exps = _dtlz2_experiments(n=30, m=3, seed=3)
     s = strategies.map(dm.QnehviStrategy(domain=bench.domain, seed=1))
