@@ -255,8 +255,98 @@ __global__ void chol_init_kernel(int n, const double* __restrict__ A, long long 
 }
 
 // Factor the diagonal block at k0 (already updated), write L_kk into L and inv(L_kk) to
-// Dinv (ld BNB).  Elimination keeps the unnormalised pivots d_j: L = L_unit d^1/2 and
-// inv(L) = d^-1/2 inv(L_unit), with inv(L_unit) accumulated in E.
+// Dinv (ld BNB).  Blocked inside the 64x64 block with 16-wide panels:
+//   (1) wave 0 factors the 16x16 diagonal sub-block in registers (lane = row x column
+//       quad; the pivot column / inverse row are exchanged through LDS with wave-level
+//       ordering only) keeping unnormalised pivots d_j: L = L_unit d^1/2 and
+//       inv(L) = d^-1/2 inv(L_unit), inv(L_unit) accumulated alongside;
+//   (2) all waves: panel L21 = A21 L11^-T;   (3) trailing A22 -= L21 L21^T;
+// then inv(L_kk) is assembled from the four diagonal inverses by block forward
+// substitution (X_ij = -X_ii sum_k L_ik X_kj, by distance i - j).  12 workgroup barriers
+// and 64 wave-synchronous pivot steps instead of 64 workgroup-wide steps.
+constexpr int CP = 16;   // panel width
+#ifdef EVR_CHOL_PROF
+__device__ unsigned long long chol_prof[16];
+#define CHOL_T(k) if (threadIdx.x == 0) chol_prof[k] += __builtin_readcyclecounter();
+#define CHOL_T0(k) if (threadIdx.x == 0) chol_prof[k] -= __builtin_readcyclecounter();
+#else
+#define CHOL_T(k)
+#define CHOL_T0(k)
+#endif
+
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
+// Returns the first failing local pivot index or -1 (uniform over the wave).
+__device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
+                                              double* erow, double* piv) {
+  const int lane = threadIdx.x & 63, r = lane >> 2, q = lane & 3;
+  double a[4], e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = q + 4 * k;
+    a[k] = (c <= r) ? A[c0 + r][c0 + c] : 0.0;
+    e[k] = (c == r) ? 1.0 : 0.0;
+  }
+  int bad = -1;
+#pragma unroll
+  for (int j = 0; j < CP; ++j) {
+    if (q == (j & 3)) colj[r] = a[j >> 2];            // pivot column (unnormalised)
+    if (r == j) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) erow[q + 4 * k] = e[k];   // inverse row j (final)
+    }
+    lds_wave_sync();
+    const double p = colj[j];
+    if (!(p > 0.0)) {
+      bad = j;
+      break;
+    }
+    if (lane == 0) piv[j] = p;
+    double ip = __builtin_amdgcn_rcp(p);            // + 2 Newton steps (pivots are normal, > 0)
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    const double m = colj[r] * ip;
+    const bool below = r > j;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = q + 4 * k;
+      const double dn = fma(-m, colj[c], a[k]);
+      const double en = fma(-m, erow[c], e[k]);
+      a[k] = (below && c > j && c <= r) ? dn : a[k];
+      e[k] = (below && c <= j) ? en : e[k];
+    }
+    __builtin_amdgcn_wave_barrier();   // one wave: LDS ops complete in order; keep the compiler's order
+  }
+  if (bad >= 0) return bad;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = q + 4 * k;
+    A[c0 + r][c0 + c] = (c <= r) ? a[k] / sqrt(piv[c]) : 0.0;
+    X[c0 + r][c0 + c] = (c <= r) ? e[k] / sqrt(piv[r]) : 0.0;
+  }
+  return -1;
+}
+
+// acc += P Q over one 16x16x16 block product on the f64 matrix cores (fragment maps as in
+// gemm_f64_kernel); P = M1[pr.., pc..] (or its transpose), Q = M2[qr.., qc..] (or transpose).
+template <bool PT, bool QT>
+__device__ __forceinline__ double4_t mm16(const double (*M1)[BNB + 1], int pr, int pc, const double (*M2)[BNB + 1],
+                                          int qr, int qc, double4_t acc) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < CP; kk += 4) {
+    const double a = PT ? M1[pr + kk + kq][pc + i] : M1[pr + i][pc + kk + kq];
+    const double b = QT ? M2[qr + i][qc + kk + kq] : M2[qr + kk + kq][qc + i];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* __restrict__ Lm, long long sL, int ldl,
                                                         double* __restrict__ Dinv, long long sD,
                                                         int* __restrict__ info) {
@@ -265,41 +355,95 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
   double* L = Lm + b * sL;
   double* Di = Dinv + b * sD;
   const int nb = min(BNB, n - k0);
-  __shared__ double D[BNB][BNB + 1];
-  __shared__ double E[BNB][BNB + 1];
-  const int tid = threadIdx.x;
+  __shared__ double A[BNB][BNB + 1];
+  __shared__ double X[BNB][BNB + 1];
+  __shared__ double colj[CP], erow[CP], piv[CP];
+  __shared__ int fail;
+  const int tid = threadIdx.x, wave = tid >> 6;
   for (int e = tid; e < BNB * BNB; e += 256) {
-    const int i = e / BNB, c = e % BNB;
-    D[i][c] = (i < nb && c <= i) ? L[(size_t)(k0 + i) * ldl + k0 + c] : 0.0;
-    E[i][c] = (i == c) ? 1.0 : 0.0;
+    const int i = e >> 6, c = e & 63;
+    // padding rows / columns beyond nb factor as the identity
+    A[i][c] = (i < nb && c <= i) ? L[(size_t)(k0 + i) * ldl + k0 + c] : (i == c ? 1.0 : 0.0);
+    X[i][c] = 0.0;
   }
+  if (tid == 0) fail = -1;
   __syncthreads();
-  // 16 x 16 thread grid over (row i, column c): no integer division in the step loop
-  const int tx = tid & 15, ty = tid >> 4;
-  for (int j = 0; j < nb; ++j) {
-    const double p = D[j][j];
-    if (!(p > 0.0)) break;  // uniform
-    const double ip = 1.0 / p;
-    for (int i = j + 1 + ty; i < nb; i += 16) {
-      const double dij = D[i][j] * ip;
-      for (int c = j + 1 + tx; c <= i; c += 16) D[i][c] -= dij * D[c][j];
-      for (int c = tx; c <= j; c += 16) E[i][c] -= dij * E[j][c];
+  CHOL_T0(0)
+  for (int p = 0; p < BNB / CP; ++p) {
+    const int c0 = p * CP;
+    CHOL_T0(1)
+    if (wave == 0) {
+      const int bad = panel_factor16(A, X, c0, colj, erow, piv);
+      if (bad >= 0 && (tid & 63) == 0) fail = c0 + bad;
+    }
+    __syncthreads();
+    CHOL_T(1)
+    if (fail >= 0) break;
+    const int r0 = c0 + CP, R = BNB - r0;
+    if (R == 0) break;
+    CHOL_T0(2)
+    // (2) panel L21 = A21 X11^T (X11 = inv(L11), lower): wave w < R/16 owns row tile w
+    const int lane = tid & 63, fc = lane & 15, fr = lane >> 4;
+    double4_t acc = {0, 0, 0, 0};
+    if (wave < R / CP) acc = mm16<false, true>(A, r0 + CP * wave, c0, X, c0, c0, acc);
+    __syncthreads();
+    if (wave < R / CP)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) A[r0 + CP * wave + fr + 4 * q][c0 + fc] = acc[q];
+    __syncthreads();
+    CHOL_T(2)
+    CHOL_T0(3)
+    // (3) trailing update of the lower tile triangle: A_ij -= L21_i L21_j^T
+    {
+      const int nt = R / CP;
+      for (int tt = wave; tt < nt * (nt + 1) / 2; tt += 4) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
+        const int tj = tt - ti * (ti + 1) / 2;
+        double4_t u = {0, 0, 0, 0};
+        u = mm16<false, true>(A, r0 + CP * ti, c0, A, r0 + CP * tj, c0, u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = fr + 4 * q;
+          if (ti != tj || fc <= rr) A[r0 + CP * ti + rr][r0 + CP * tj + fc] -= u[q];
+        }
+      }
+    }
+    __syncthreads();
+    CHOL_T(3)
+  }
+  CHOL_T(0)
+  CHOL_T0(4)
+  if (fail >= 0) {
+    if (fail < nb && tid == 0) info[b] = k0 + fail + 1;
+    if (fail < nb) return;
+  }
+  // inv(L) off-diagonal blocks by distance dd = i - j: wave pr owns the pair (pr + dd, pr);
+  // T = sum_k L_ik X_kj stays in the accumulator, which is already the B fragment of X_ii T
+  for (int dd = 1; dd < BNB / CP; ++dd) {
+    const int np = BNB / CP - dd;
+    if (wave < np) {
+      const int i = wave + dd, j = wave;
+      const int lane = tid & 63, fc = lane & 15, fr = lane >> 4;
+      double4_t tacc = {0, 0, 0, 0};
+      for (int k = j; k < i; ++k) tacc = mm16<false, false>(A, CP * i, CP * k, X, CP * k, CP * j, tacc);
+      double4_t y = {0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double a = X[CP * i + fc][CP * i + 4 * q + fr];
+        y = __builtin_amdgcn_mfma_f64_16x16x4f64(a, tacc[q], y, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) X[CP * i + fr + 4 * q][CP * j + fc] = -y[q];
     }
     __syncthreads();
   }
-  int bad = -1;
-  for (int j = nb - 1; j >= 0; --j)
-    if (!(D[j][j] > 0.0)) bad = j;
-  if (bad >= 0) {
-    if (tid == 0) info[b] = k0 + bad + 1;
-    return;
-  }
+  CHOL_T(4)
   for (int e = tid; e < BNB * BNB; e += 256) {
-    const int i = e / BNB, c = e % BNB;
+    const int i = e >> 6, c = e & 63;
     if (i < nb && c < nb) {
-      const double lv = (c <= i) ? D[i][c] / sqrt(D[c][c]) : 0.0;
-      L[(size_t)(k0 + i) * ldl + k0 + c] = lv;
-      Di[(size_t)i * BNB + c] = (c <= i) ? E[i][c] / sqrt(D[i][i]) : 0.0;
+      L[(size_t)(k0 + i) * ldl + k0 + c] = (c <= i) ? A[i][c] : 0.0;
+      Di[(size_t)i * BNB + c] = (c <= i) ? X[i][c] : 0.0;
     } else {
       Di[(size_t)i * BNB + c] = (i == c) ? 1.0 : 0.0;
     }
