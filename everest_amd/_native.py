@@ -66,6 +66,8 @@ _SIGS = {
     "evr_tri_inv_lower": ([c_void_p, c_int, c_int, c_void_p, c_int, c_longlong, c_void_p, c_int, c_longlong],
                           c_int),
     "evr_gp_posterior_finalize": ([c_void_p, c_int, c_int, c_int] + [c_void_p] * 8, c_int),
+    "evr_gp_posterior_workspace_doubles": ([c_int, c_int, c_int], c_longlong),
+    "evr_gp_posterior": ([c_void_p, c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 14, c_int),
     "evr_qnehvi_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p],
                            c_int),
     "evr_hvi_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int], c_longlong),

@@ -425,27 +425,55 @@ __global__ void mll_terms_finalize(int B, const double* __restrict__ part, doubl
   out[e] = (q == 0) ? 2.0 * s : s;
 }
 
-__global__ void posterior_finalize_kernel(int B, int n, int nt, const double* __restrict__ R,
-                                          const double* __restrict__ cc, const double* __restrict__ ym,
-                                          const double* __restrict__ ys, const double* __restrict__ kxx,
-                                          const double* __restrict__ noise, double* __restrict__ mean,
-                                          double* __restrict__ var) {
+// Column reduction of R = [Linv; alpha^T] K_x: block = 64 test points (lanes, coalesced
+// rows) x 16 row groups (waves of 64 threads... 1024 threads); every thread sums its rows
+// with 4 independent accumulators, the 16 group partials are combined in a fixed order.
+__global__ __launch_bounds__(1024) void posterior_finalize_kernel(int B, int n, int nt, const double* __restrict__ R,
+                                                                  const double* __restrict__ cc,
+                                                                  const double* __restrict__ ym,
+                                                                  const double* __restrict__ ys,
+                                                                  const double* __restrict__ kxx,
+                                                                  const double* __restrict__ noise,
+                                                                  double* __restrict__ mean, double* __restrict__ var) {
   const int b = blockIdx.y;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
+  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int t = blockIdx.x * 64 + tx;
+  __shared__ double part[16][64];
   const double* Rb = R + (size_t)b * (n + 1) * nt;
-  double ss = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double v = Rb[(size_t)i * nt + t];
-    ss = fma(v, v, ss);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (t < nt) {
+    int i = g;
+    for (; i + 48 < n; i += 64) {
+      const double v0 = Rb[(size_t)i * nt + t], v1 = Rb[(size_t)(i + 16) * nt + t];
+      const double v2 = Rb[(size_t)(i + 32) * nt + t], v3 = Rb[(size_t)(i + 48) * nt + t];
+      s0 = fma(v0, v0, s0);
+      s1 = fma(v1, v1, s1);
+      s2 = fma(v2, v2, s2);
+      s3 = fma(v3, v3, s3);
+    }
+    for (; i < n; i += 16) {
+      const double v = Rb[(size_t)i * nt + t];
+      s0 = fma(v, v, s0);
+    }
   }
-  const double a = Rb[(size_t)n * nt + t];
-  const double s = ys[b];
-  mean[(size_t)b * nt + t] = ym[b] + s * (cc[b] + a);
-  double v = kxx[b] - ss;
-  if (noise) v += noise[b];
-  var[(size_t)b * nt + t] = s * s * v;
+  part[g][tx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && t < nt) {
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ss += part[k][tx];
+    const double a = Rb[(size_t)n * nt + t];
+    const double s = ys[b];
+    mean[(size_t)b * nt + t] = ym[b] + s * (cc[b] + a);
+    double v = kxx[b] - ss;
+    if (noise) v += noise[b];
+    var[(size_t)b * nt + t] = s * s * v;
+  }
 }
+
+int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA, const double* B,
+            int ldb, long long sB, double* C, int ldc, long long sC, int batch);
+int gemm_backend_init();
 
 }  // namespace evr
 
@@ -537,11 +565,34 @@ int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* 
                               double* mean, double* var) {
   EVR_CHECK(B >= 1 && n >= 1 && nt >= 0, "evr_gp_posterior_finalize: bad sizes");
   if (nt == 0) return 0;
-  dim3 grid(cdiv(nt, 256), B);
-  posterior_finalize_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(B, n, nt, R, c, ym, ys, kxx, noise_add, mean,
-                                                                   var);
+  dim3 grid(cdiv(nt, 64), B);
+  posterior_finalize_kernel<<<grid, 1024, 0, (hipStream_t)stream>>>(B, n, nt, R, c, ym, ys, kxx, noise_add, mean,
+                                                                    var);
   EVR_LAUNCH_CHECK();
   return 0;
+}
+
+long long evr_gp_posterior_workspace_doubles(int B, int n, int nt) {
+  return (B > 0 && n > 0 && nt > 0) ? (long long)B * nt * (2LL * n + 1) : 0;
+}
+
+int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const double* Xn, const double* X,
+                     const double* shift, const double* scale, const double* lengthscales, const double* M,
+                     const double* c, const double* ym, const double* ys, const double* kxx,
+                     const double* noise_add, double* mean, double* var, double* work) {
+  EVR_CHECK(B >= 1 && n >= 1 && nt >= 0 && d >= 1 && Xn && M && work, "evr_gp_posterior: bad arguments");
+  if (nt == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  double* Kx = work;                                   // B x n x nt
+  double* R = work + (size_t)B * n * nt;               // B x (n+1) x nt
+  if (int rc = evr_kernel_matrix(stream, kind, B, n, nt, d, Xn, nullptr, nullptr, X, shift, scale, lengthscales,
+                                 nullptr, nullptr, Kx))
+    return rc;
+  if (int rc = gemm_backend_init()) return rc;
+  if (int rc = rb_gemm(s, false, n + 1, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
+                       (long long)(n + 1) * nt, B))
+    return rc;
+  return evr_gp_posterior_finalize(stream, B, n, nt, R, c, ym, ys, kxx, noise_add, mean, var);
 }
 
 }  // extern "C"

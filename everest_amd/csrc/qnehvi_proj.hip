@@ -421,7 +421,7 @@ static rocblas_handle rb_handle() {
 }
 
 // row-major C = op(A) op(B) batched (alpha 1, beta 0) through rocBLAS' column-major dgemm
-static int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA,
+int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA,
                    const double* B, int ldb, long long sB, double* C, int ldc, long long sC, int batch) {
   rocblas_handle h = rb_handle();
   EVR_CHECK(h, "rocBLAS handle creation failed");

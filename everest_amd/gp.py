@@ -141,10 +141,9 @@ class GPBatch:
 
     def posterior(self, Xraw: torch.Tensor, observation_noise: bool = False):
         """Mean and variance (B x nt) at raw (transformed, unnormalized) inputs."""
-        Kx = self.cross(Xraw)
-        R = ops.gemm(self.M, Kx)
-        return ops.posterior_finalize(R, self.const, self.ym, self.ys, self.kxx,
-                                      self.noise if observation_noise else None)
+        Xraw = Xraw.to(device=self.device, dtype=torch.float64).contiguous()
+        return ops.gp_posterior(self.Xn, Xraw, self.lo, self.inv_range, self.ls, self.M, self.kind, self.const,
+                                self.ym, self.ys, self.kxx, self.noise if observation_noise else None)
 
 
 # ---------------------------------------------------------------------------------------

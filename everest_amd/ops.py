@@ -246,6 +246,24 @@ def posterior_finalize(R, c, ym, ys, kxx, noise_add=None):
     return mean, var
 
 
+def gp_posterior(Xn, X, shift, scale, lengthscales, M, kind, c, ym, ys, kxx, noise_add=None):
+    """Mean and variance (B x nt) in one native call: kernel_matrix -> R = M K_x -> finalize."""
+    Xn, X, M = _dev(Xn, "Xn"), _dev(X, "X"), _dev(M, "M")
+    B, n1, n = M.shape
+    nt, d = X.shape
+    if n1 != n + 1 or Xn.shape != (n, d):
+        raise ValueError("gp_posterior: shape mismatch")
+    mean = torch.empty(B, nt, dtype=torch.float64, device=X.device)
+    var = torch.empty_like(mean)
+    work = _workspace(_native.load().evr_gp_posterior_workspace_doubles(B, n, nt), X.device)
+    aux = [_dev(t, "aux") for t in (shift, scale, lengthscales, c, ym, ys, kxx)]
+    na = None if noise_add is None else _dev(noise_add, "noise")
+    call("evr_gp_posterior", _stream(), B, n, nt, d, int(kind), Xn.data_ptr(), X.data_ptr(), aux[0].data_ptr(),
+         aux[1].data_ptr(), aux[2].data_ptr(), M.data_ptr(), aux[3].data_ptr(), aux[4].data_ptr(), aux[5].data_ptr(),
+         aux[6].data_ptr(), _p(na), mean.data_ptr(), var.data_ptr(), work.data_ptr())
+    return mean, var
+
+
 # ---------------------------------------------------------------------------------------
 # qNEHVI pieces
 # ---------------------------------------------------------------------------------------

@@ -107,6 +107,15 @@ int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* 
                               const double* kxx, const double* noise_add,
                               double* mean, double* var);
 
+/* Whole posterior in one call: K_x = k(Xn, normalize(X)) (kernel_matrix), R = M K_x
+ * (M = [Linv; alpha^T], B x (n+1) x n), then the finalize above.  work: B*nt*(2n+1)
+ * doubles (evr_gp_posterior_workspace_doubles). */
+long long evr_gp_posterior_workspace_doubles(int B, int n, int nt);
+int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const double* Xn, const double* X,
+                     const double* shift, const double* scale, const double* lengthscales, const double* M,
+                     const double* c, const double* ym, const double* ys, const double* kxx,
+                     const double* noise_add, double* mean, double* var, double* work);
+
 /* ---- qNEHVI (q = 1) -----------------------------------------------------------------
  * Replaces [upstream] qNoisyExpectedHypervolumeImprovement.forward/backward as built at
  * bofire/strategies/predictives/qnehvi.py:39-52 (cached-Cholesky sampling + box-cell HVI).
