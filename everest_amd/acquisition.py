@@ -68,7 +68,8 @@ class QNEHVI:
                  prune_samples: int = 2048, max_frac: float = 1.0, z_prune: Optional[torch.Tensor] = None,
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
                  num_threads: Optional[int] = None, box_device: Optional[bool] = None,
-                 kd_scan: Optional[bool] = None, X_pending_raw: Optional[np.ndarray] = None):
+                 kd_scan: Optional[bool] = None, X_pending_raw: Optional[np.ndarray] = None,
+                 root: Optional[str] = None):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -197,8 +198,22 @@ class QNEHVI:
         self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(np.sum(counts_c)),
                                        max_cells=int(counts_c.max()) if len(counts_c) else 0, prune_probs=probs)
 
-        # ---- forward operator M = [Linv; G; H^T; alpha^T] over the nk kernel rows --------
-        Rr = nk + nb + S_ + 1
+        # ---- forward operator over the nk kernel rows -------------------------------------
+        # "split" (the literal restatement): M = [Linv; G; H^T; alpha^T], L22^2 =
+        #   s^2 (kxx - |Linv k|^2) - |G k|^2.
+        # "fused" (default): the two quadratic forms share one root C with
+        #   C^T C = Linv^T Linv + G^T G / s^2,  C = Lv^T Lp^-1,  Lv = chol(D0 + V^T V),
+        #   V = (G / s) Lp,  Lp = diag(L, I_pending),  D0 = diag(1_n, 0_pending)
+        # (I + V^T V >= I is well conditioned; no Gram matrix of Linv is ever formed), so
+        # M = [C; H^T; alpha^T] has nk + S + 1 rows instead of nk + nb + S + 1 and the
+        # samples / backward kernels see a baseline-free layout (state nb = 0).
+        root = root or os.environ.get("EVR_ROOT", "fused")
+        if root not in ("fused", "split"):
+            raise ValueError(f"root must be 'fused' or 'split', got {root!r}")
+        fused = root == "fused" and nb > 0
+        self.root = "fused" if fused else "split"
+        nb_rows = 0 if fused else nb
+        Rr = nk + nb_rows + S_ + 1
         self.Rr = Rr
         M = torch.zeros(m, Rr, nk, **f64) if npend else torch.empty(m, Rr, n, **f64)
         M[:, :n, :n].copy_(gp.Linv)
@@ -210,14 +225,29 @@ class QNEHVI:
             ops.add_selection(E, idx.to(torch.int32), None)                      # + P
             ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
             ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
-            M[:, nk:nk + nb].copy_(E)
-            ops.gemm_into(M[:, nk + nb:nk + nb + S_], Zb, E, transA=True)        # H^T = Z^T G
+            ops.gemm_into(M[:, nk + nb_rows:nk + nb_rows + S_], Zb, E, transA=True)   # H^T = Z^T G
+            if fused:
+                Lp = torch.zeros(m, nk, nk, **f64)
+                Lp[:, :n, :n].copy_(gp.L)
+                Lpi = torch.zeros(m, nk, nk, **f64)
+                Lpi[:, :n, :n].copy_(gp.Linv)
+                if npend:
+                    Lp[:, n:, n:].copy_(torch.eye(npend, **f64))
+                    Lpi[:, n:, n:].copy_(torch.eye(npend, **f64))
+                ops.scale_batched(E, (1.0 / gp.ys).contiguous())                 # G / s
+                V = ops.gemm(E, Lp)                                              # nb x nk
+                Iv = ops.gemm(V, V, transA=True)                                 # V^T V
+                Iv.diagonal(dim1=-2, dim2=-1)[:, :n] += 1.0                      # + D0
+                Lv, _, _ = ops.cholesky(Iv, 1e-8, 3)
+                ops.gemm_into(M[:, :nk], Lv, Lpi, transA=True)                   # C = Lv^T Lp^-1
+            else:
+                M[:, nk:nk + nb].copy_(E)
         else:
             M[:, nk:nk + S_].zero_()
         M[:, Rr - 1, :n].copy_(gp.alpha)
         self.M = M
-        self.state = ops.make_state(nk, nb, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
-                                    cells)
+        self.state = ops.make_state(nk, nb_rows, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a,
+                                    self.obj_b, cells)
         self._keep = (self.zq, self.obj_a, self.obj_b)
         self._lo_c = gp.lo.to(torch.float64).contiguous()
         self._scale_c = gp.inv_range.to(torch.float64).contiguous()

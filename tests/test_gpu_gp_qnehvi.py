@@ -235,3 +235,25 @@ def test_qnehvi_pending_device_samples_match_host_samples():
     assert np.array_equal(auto.base_rows, host.base_rows)
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(64, d)), device="cuda")
     assert torch.allclose(auto.forward(Xc), host.forward(Xc), rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.parametrize("npend", [0, 2])
+def test_qnehvi_fused_root_matches_split_root(npend):
+    """The fused quadratic-form root C (C^T C = Linv^T Linv + G^T G / s^2) reproduces the
+    literal [Linv; G] operator: values and gradients agree to rounding."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 80, 5, 4, 64
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=21)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(m), np.zeros(m), -1.1 * np.ones(m)
+    Xp = lo + (hi - lo) * np.random.default_rng(4).uniform(size=(npend, d)) if npend else None
+    kw = dict(S=S, sampler_seed=3, prune_baseline=True, prune_seed=5, prune_samples=256, X_pending_raw=Xp)
+    fused = QNEHVI(gp, X, X, ref, a, b, root="fused", **kw)
+    split = QNEHVI(gp, X, X, ref, a, b, root="split", **kw)
+    assert fused.root == "fused" and split.root == "split" and fused.Rr == split.Rr - split.nb
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(6).uniform(size=(200, d)), device="cuda")
+    af, gf = fused.forward_backward(Xc)
+    as_, gs = split.forward_backward(Xc)
+    assert torch.allclose(af, as_, rtol=1e-9, atol=1e-12)
+    assert torch.allclose(gf, gs, rtol=1e-7, atol=1e-10)
