@@ -16,6 +16,7 @@ namespace evr {
 constexpr int KT = 64;
 constexpr int KMAXD = 64;
 
+template <int RA, int KIND>
 __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int d, const double* __restrict__ X1,
                                                    const double* __restrict__ sh1, const double* __restrict__ sc1,
                                                    const double* __restrict__ X2, const double* __restrict__ sh2,
@@ -24,44 +25,61 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
                                                    double* __restrict__ K) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.z;
-  const int i0 = blockIdx.y * KT, j0 = blockIdx.x * KT;
+  const int i0 = blockIdx.y * (16 * RA), j0 = blockIdx.x * KT;
   const int ld = d + 1;
   double* A = smem;            // KT x ld
-  double* Bt = smem + KT * ld;  // KT x ld
+  double* Bt = smem + 16 * RA * ld;  // KT x ld
   const double* lsb = ls + (size_t)b * d;
   const int tid = threadIdx.x;
-  for (int e = tid; e < KT * d; e += 256) {
-    const int r = e / d, k = e % d;
-    const double il = 1.0 / lsb[k];
-    double v = 0.0, w = 0.0;
-    if (i0 + r < n1) {
-      v = X1[(size_t)(i0 + r) * d + k];
-      if (sh1) v -= sh1[k];
-      if (sc1) v *= sc1[k];
+  // d < 16: at most 4 staging elements per thread; all loads issued before the first wait
+  double xv[4], xw[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int e = tid + 256 * t;
+    const int r = e / d;
+    xv[t] = 0.0;
+    xw[t] = 0.0;
+    if (e < KT * d) {
+      if (r < 16 * RA && i0 + r < n1) xv[t] = X1[(size_t)(i0 + r) * d + (e - r * d)];
+      if (j0 + r < n2) xw[t] = X2[(size_t)(j0 + r) * d + (e - r * d)];
     }
-    if (j0 + r < n2) {
-      w = X2[(size_t)(j0 + r) * d + k];
-      if (sh2) w -= sh2[k];
-      if (sc2) w *= sc2[k];
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int e = tid + 256 * t;
+    if (e < KT * d) {
+      const int r = e / d, k = e - r * d;
+      const double il = 1.0 / lsb[k];
+      double v = 0.0, w = 0.0;
+      if (r < 16 * RA && i0 + r < n1) {
+        v = xv[t];
+        if (sh1) v -= sh1[k];
+        if (sc1) v *= sc1[k];
+      }
+      if (j0 + r < n2) {
+        w = xw[t];
+        if (sh2) w -= sh2[k];
+        if (sc2) w *= sc2[k];
+      }
+      if (r < 16 * RA) A[r * ld + k] = v * il;
+      Bt[r * ld + k] = w * il;
     }
-    A[r * ld + k] = v * il;
-    Bt[r * ld + k] = w * il;
   }
   __syncthreads();
   const int tx = tid & 15, ty = tid >> 4;
-  double acc[4][4];
+  double acc[RA][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < RA; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = 0.0;
   for (int k = 0; k < d; ++k) {
-    double av[4], bv[4];
+    double av[RA], bv[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) av[a] = A[(ty + 16 * a) * ld + k];
+    for (int a = 0; a < RA; ++a) av[a] = A[(ty + 16 * a) * ld + k];
 #pragma unroll
     for (int c = 0; c < 4; ++c) bv[c] = Bt[(tx + 16 * c) * ld + k];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < RA; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const double df = av[a] - bv[c];
@@ -72,14 +90,14 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n1 * n2;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < RA; ++a) {
     const int i = i0 + ty + 16 * a;
     if (i >= n1) continue;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int j = j0 + tx + 16 * c;
       if (j < n2) {
-        double v = scale * kernel_value(kind, acc[a][c]);
+        double v = scale * kernel_value(KIND, acc[a][c]);
         if (i == j) v += dadd;
         Kb[(size_t)i * n2 + j] = v;
       }
@@ -95,7 +113,7 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
 // distance loop of kmat_kernel (2 flop per coordinate per entry) was the bound at d = 32.
 using kd4_t = __attribute__((ext_vector_type(4))) double;
 
-template <int DP>
+template <int DP, int KIND>
 __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
                                                         const double* __restrict__ X1, const double* __restrict__ sh1,
                                                         const double* __restrict__ sc1, const double* __restrict__ X2,
@@ -112,26 +130,45 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const int i0 = by * KT, j0 = bx * KT;
   const double* lsb = ls + (size_t)b * d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < KT * DP; e += 256) {
+  // staging: every load of the tile is issued before the first wait (NE independent
+  // loads per operand per thread), then the normalised values go to LDS
+  constexpr int NE = (KT * DP + 255) / 256;
+  double v[NE], w[NE];
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {
+    const int e = tid + 256 * t;
     const int r = e / DP, k = e - r * DP;
-    double v = 0.0, w = 0.0;
-    if (k < d) {
-      const double il = 1.0 / lsb[k];
-      if (i0 + r < n1) {
-        v = X1[(size_t)(i0 + r) * d + k];
-        if (sh1) v -= sh1[k];
-        if (sc1) v *= sc1[k];
-        v *= il;
-      }
-      if (j0 + r < n2) {
-        w = X2[(size_t)(j0 + r) * d + k];
-        if (sh2) w -= sh2[k];
-        if (sc2) w *= sc2[k];
-        w *= il;
-      }
+    v[t] = 0.0;
+    w[t] = 0.0;
+    if (e < KT * DP && k < d) {
+      if (i0 + r < n1) v[t] = X1[(size_t)(i0 + r) * d + k];
+      if (j0 + r < n2) w[t] = X2[(size_t)(j0 + r) * d + k];
     }
-    As[k][r] = v;
-    Bs[k][r] = w;
+  }
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {
+    const int e = tid + 256 * t;
+    const int r = e / DP, k = e - r * DP;
+    if (e < KT * DP) {
+      double a = 0.0, c = 0.0;
+      if (k < d) {
+        const double il = 1.0 / lsb[k];
+        if (i0 + r < n1) {
+          a = v[t];
+          if (sh1) a -= sh1[k];
+          if (sc1) a *= sc1[k];
+          a *= il;
+        }
+        if (j0 + r < n2) {
+          c = w[t];
+          if (sh2) c -= sh2[k];
+          if (sc2) c *= sc2[k];
+          c *= il;
+        }
+      }
+      As[k][r] = a;
+      Bs[k][r] = c;
+    }
   }
   __syncthreads();
   if (tid < 2 * KT) {
@@ -176,7 +213,7 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
       if (gi < n1 && gj < n2) {
         double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
         if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
-        double v = scale * kernel_value(kind, d2);
+        double v = scale * kernel_value(KIND, d2);
         if (gi == gj) v += dadd;
         Kb[(size_t)gi * n2 + gj] = v;
       }
@@ -491,20 +528,43 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
-#define KM(DP_)                                                                                                 \
-  kmat_mfma_kernel<DP_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2,     \
-                                             lengthscales, outputscale, diag_add, K)
-    if (d <= 16) KM(16);
-    else if (d <= 32) KM(32);
-    else if (d <= 48) KM(48);
-    else KM(64);
+#define KMK(DP_, K_)                                                                                        \
+  kmat_mfma_kernel<DP_, K_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                 lengthscales, outputscale, diag_add, K)
+#define KM(DP_)                         \
+  if (kind == RBF) KMK(DP_, RBF);           \
+  else if (kind == MATERN05) KMK(DP_, MATERN05); \
+  else if (kind == MATERN15) KMK(DP_, MATERN15); \
+  else KMK(DP_, MATERN25)
+    if (d <= 16) { KM(16); }
+    else if (d <= 32) { KM(32); }
+    else if (d <= 48) { KM(48); }
+    else { KM(64); }
+#undef KMK
 #undef KM
     EVR_LAUNCH_CHECK();
     return 0;
   }
-  const size_t lds = (size_t)2 * KT * (d + 1) * sizeof(double);
-  kmat_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2,
-                                                       lengthscales, outputscale, diag_add, K);
+  static const int ra = [] {
+    const char* e = getenv("EVR_KMAT_RA");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
+  const size_t lds = (size_t)(KT + 16 * ra) * (d + 1) * sizeof(double);
+  dim3 g(cdiv(n2, KT), cdiv(n1, 16 * ra), B);
+#define KTK(RA_, K_)                                                                              \
+  kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
+                                                             scale2, lengthscales, outputscale, diag_add, K)
+#define KT_(RA_)                         \
+  if (kind == RBF) KTK(RA_, RBF);           \
+  else if (kind == MATERN05) KTK(RA_, MATERN05); \
+  else if (kind == MATERN15) KTK(RA_, MATERN15); \
+  else KTK(RA_, MATERN25)
+  if (ra == 1) { KT_(1); }
+  else if (ra == 2) { KT_(2); }
+  else { KT_(4); }
+#undef KTK
+#undef KT_
   EVR_LAUNCH_CHECK();
   return 0;
 }
