@@ -46,6 +46,35 @@ def _host_threads() -> int:
         return 1
 
 
+def _single_cell(ref: torch.Tensor, S: int, m: int) -> ops.Cells:
+    """Empty Pareto set: one cell [ref, +inf) per sample (the whole region above ref)."""
+    dev = ref.device
+    return ops.Cells(torch.arange(S + 1, dtype=torch.int32, device=dev), np.ones(S, dtype=np.int64), m,
+                     lo=ref.unsqueeze(0).repeat(S, 1).contiguous(),
+                     hi=torch.full((S, m), math.inf, dtype=torch.float64, device=dev))
+
+
+def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None, num_threads=None):
+    """Exact non-dominated box decomposition above ref of every sample of O (m x P x S):
+    device kernel + kd ordering, or the native host partition beyond the device limits.
+    Returns (cells, path)."""
+    m, P, _ = O.shape
+    dev = O.device
+    if box_device if box_device is not None else ops.box_device_supported(P, m):
+        cells = ops.box_decompose_device(O, ref)
+        path = "device"
+        if kd_scan if kd_scan is not None else ops.kd_supported(cells):
+            ops.cells_kd_order(cells)
+            path = "device+kd"
+        return cells, path
+    mask, _ = ops.pareto_mask(O, ref, dedup=True)
+    lo, hi, off = ops.box_decompose(O.cpu().numpy(), ref.cpu().numpy(), mask.cpu().numpy(),
+                                    num_threads or _host_threads(), layout="jis")
+    f64 = dict(dtype=torch.float64, device=dev)
+    return ops.Cells(torch.as_tensor(off, dtype=torch.int32, device=dev), np.diff(off), m,
+                     lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64)), "host"
+
+
 @dataclass
 class ConstructionStats:
     n_train: int
@@ -55,7 +84,88 @@ class ConstructionStats:
     prune_probs: Optional[np.ndarray] = None
 
 
-class QNEHVI:
+class _BoxHviAcqf:
+    """Evaluation side shared by qNEHVI and qEHVI: the per-ask operator ``M`` applied to the
+    cross-covariance, the sampling step, the box-cell HVI scan and their analytic backward
+    (subclasses set gp, dev, Xk, M, state, model and _plans)."""
+
+    def plan(self, b: int, backward: bool) -> ops.QnehviPlan:
+        """Native evaluation plan for batch size b (cached; hipGraph unless EVR_GRAPH=0)."""
+        key = (int(b), bool(backward))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) >= 8:
+                self._plans.pop(next(iter(self._plans)))
+            p = ops.QnehviPlan(self.state, self.model, int(b), bool(backward), self.dev,
+                               graph=os.environ.get("EVR_GRAPH", "1") != "0")
+            self._plans[key] = p
+        return p
+
+    def forward(self, X: torch.Tensor, return_cache: bool = False):
+        """X: b x d raw (transformed) candidates on device -> acquisition values (b), through
+        the native plan (one C-ABI call); see forward_ops for the op-by-op chain."""
+        if return_cache:
+            return self.forward_ops(X, return_cache=True)
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        p = self.plan(X.shape[0], False)
+        p.X.copy_(X)
+        p.run()
+        return p.acq.clone()
+
+    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d)) through the native plan."""
+        if gout is not None:
+            return self.forward_backward_ops(X, gout)
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        p = self.plan(X.shape[0], True)
+        p.X.copy_(X)
+        p.run()
+        return p.acq.clone(), p.dX.clone()
+
+    def eval_host(self, x: np.ndarray, backward: bool):
+        """Host round trip for the scipy optimiser: x (b x d numpy) -> (acq, dX or None)
+        numpy, one pinned H2D copy, one plan launch, one D2H copy."""
+        b = x.shape[0]
+        out = self.plan(b, backward).run_host(x)
+        acq = out[:b].copy()
+        return acq, (out[b:].reshape(b, -1).copy() if backward else None)
+
+    def _cross(self, X: torch.Tensor) -> torch.Tensor:
+        """K(X_k, normalize(X)) : m x nk x b over the training (+ pending) rows."""
+        gp = self.gp
+        return ops.kernel_matrix(self.Xk, X, gp.ls, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+
+    def forward_ops(self, X: torch.Tensor, return_cache: bool = False):
+        """X: b x d raw (transformed) candidates on device -> acquisition values (b).
+
+        A candidate whose new-point Cholesky block stays not p.d. after the 6-rung jitter
+        ladder gets NaN (no device->host sync here); ``optim.host_values`` turns a NaN into
+        the NotPSDError BoTorch raises from sample_cached_cholesky."""
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        b = X.shape[0]
+        Kx = self._cross(X)                         # m x nk x b
+        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)    # m x Rr x b + partial norms
+        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
+        acq = ops.hvi_forward(self.state, G, b, flags)
+        if return_cache:
+            return acq, (X, R, G, L22, flags)
+        return acq
+
+    def forward_backward_ops(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
+        """Op-by-op chain: returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
+        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
+        b = X.shape[0]
+        Kx = self._cross(X)
+        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)
+        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
+        acq, dG = ops.hvi_forward_backward(self.state, G, b, flags, gout)
+        dKx = ops.qnehvi_project_backward(self.state, self.M, R, L22, dG, b)    # m x nk x b
+        gp = self.gp
+        dX = ops.kernel_cross_grad(self.Xk, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
+        return acq, dX
+
+
+class QNEHVI(_BoxHviAcqf):
     """Device qNEHVI over the GPs of ``gp`` (one output per objective).
 
     Parameters mirror the reference constructor: ``X_baseline`` raw (transformed) inputs,
@@ -174,24 +284,10 @@ class QNEHVI:
             Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
             t1 = _time.perf_counter()
-            if box_device if box_device is not None else ops.box_device_supported(nb, m):
-                cells = ops.box_decompose_device(Ob, self.ref)
-                self.box_path = "device"
-                if kd_scan if kd_scan is not None else ops.kd_supported(cells):
-                    ops.cells_kd_order(cells)
-                    self.box_path = "device+kd"
-            else:  # beyond the device kernel's LDS / key-width limits: native host partition
-                mask, _ = ops.pareto_mask(Ob, self.ref, dedup=True)
-                lo, hi, off = ops.box_decompose(Ob.cpu().numpy(), self.ref.cpu().numpy(), mask.cpu().numpy(),
-                                                num_threads or _host_threads(), layout="jis")
-                cells = ops.Cells(torch.as_tensor(off, dtype=torch.int32, device=dev), np.diff(off), m,
-                                  lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64))
-                self.box_path = "host"
+            cells, self.box_path = _decompose(Ob, self.ref, box_device, kd_scan, num_threads)
             tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
-            cells = ops.Cells(torch.arange(S_ + 1, dtype=torch.int32, device=dev), np.ones(S_, dtype=np.int64), m,
-                              lo=self.ref.unsqueeze(0).repeat(S_, 1).contiguous(),
-                              hi=torch.full((S_, m), math.inf, **f64))
+            cells = _single_cell(self.ref, S_, m)
             self.box_path = "none"
         self.cells = cells
         counts_c = cells.counts
@@ -259,81 +355,65 @@ class QNEHVI:
         tm["total"] = _time.perf_counter() - t0
         self.timings = tm
 
-    # ------------------------------------------------------------------------------------
-    def plan(self, b: int, backward: bool) -> ops.QnehviPlan:
-        """Native evaluation plan for batch size b (cached; hipGraph unless EVR_GRAPH=0)."""
-        key = (int(b), bool(backward))
-        p = self._plans.get(key)
-        if p is None:
-            if len(self._plans) >= 8:
-                self._plans.pop(next(iter(self._plans)))
-            p = ops.QnehviPlan(self.state, self.model, int(b), bool(backward), self.dev,
-                               graph=os.environ.get("EVR_GRAPH", "1") != "0")
-            self._plans[key] = p
-        return p
 
-    def forward(self, X: torch.Tensor, return_cache: bool = False):
-        """X: b x d raw (transformed) candidates on device -> acquisition values (b), through
-        the native plan (one C-ABI call); see forward_ops for the op-by-op chain."""
-        if return_cache:
-            return self.forward_ops(X, return_cache=True)
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        p = self.plan(X.shape[0], False)
-        p.X.copy_(X)
-        p.run()
-        return p.acq.clone()
 
-    def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
-        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d)) through the native plan."""
-        if gout is not None:
-            return self.forward_backward_ops(X, gout)
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        p = self.plan(X.shape[0], True)
-        p.X.copy_(X)
-        p.run()
-        return p.acq.clone(), p.dX.clone()
+class QEHVI(_BoxHviAcqf):
+    """Device qEHVI (q = 1) — [upstream] ``qExpectedHypervolumeImprovement`` as built by
+    ``QehviStrategy._get_acqfs`` (bofire/strategies/predictives/qehvi.py:37-79:
+    NondominatedPartitioning of the observed objectives better than the reference point)
+    and by ``get_acquisition_function("qEHVI")`` from ``MoboStrategy._get_acqfs``
+    (bofire/strategies/predictives/mobo.py:44-90: FastNondominatedPartitioning of the
+    objective-transformed observations).  Both partitions are exact (alpha = 0), so the
+    cells cover the same region and the HVI values agree.
 
-    def eval_host(self, x: np.ndarray, backward: bool):
-        """Host round trip for the scipy optimiser: x (b x d numpy) -> (acq, dX or None)
-        numpy, one pinned H2D copy, one plan launch, one D2H copy."""
-        b = x.shape[0]
-        out = self.plan(b, backward).run_host(x)
-        acq = out[:b].copy()
-        return acq, (out[b:].reshape(b, -1).copy() if backward else None)
+    Unlike qNEHVI the cells are fixed (one partition of ``Y_part`` shared by all samples) and
+    the samples are independent per output: y_s = mu(x) + sqrt(var(x)) z_s, z_s the s-th
+    row of an m-dimensional Sobol-normal draw (the 1x1 posterior root with the same
+    jitter ladder).  The device layout is the qNEHVI one with nb = 0 and no H^T rows
+    (M = [L^-1; alpha^T], state.no_h = 1): one (n + 1)-row projection GEMM, the same
+    sampling, sparse-scan and backward kernels."""
 
-    def _cross(self, X: torch.Tensor) -> torch.Tensor:
-        """K(X_k, normalize(X)) : m x nk x b over the training (+ pending) rows."""
-        gp = self.gp
-        return ops.kernel_matrix(self.Xk, X, gp.ls, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
-
-    def forward_ops(self, X: torch.Tensor, return_cache: bool = False):
-        """X: b x d raw (transformed) candidates on device -> acquisition values (b).
-
-        A candidate whose new-point Cholesky block stays not p.d. after the 6-rung jitter
-        ladder gets NaN (no device->host sync here); ``optim.host_values`` turns a NaN into
-        the NotPSDError BoTorch raises from sample_cached_cholesky."""
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        b = X.shape[0]
-        Kx = self._cross(X)                         # m x nk x b
-        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)    # m x Rr x b + partial norms
-        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
-        acq = ops.hvi_forward(self.state, G, b, flags)
-        if return_cache:
-            return acq, (X, R, G, L22, flags)
-        return acq
-
-    def forward_backward_ops(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
-        """Op-by-op chain: returns (acq (b), d sum_c gout_c acq_c / dX (b x d))."""
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        b = X.shape[0]
-        Kx = self._cross(X)
-        R, P = ops.qnehvi_project(self.state, self.M, Kx, b)
-        G, L22, flags = ops.qnehvi_samples_norms(self.state, R, P, b)
-        acq, dG = ops.hvi_forward_backward(self.state, G, b, flags, gout)
-        dKx = ops.qnehvi_project_backward(self.state, self.M, R, L22, dG, b)    # m x nk x b
-        gp = self.gp
-        dX = ops.kernel_cross_grad(self.Xk, X, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
-        return acq, dX
+    def __init__(self, gp: GPBatch, Y_part: np.ndarray, ref_point, obj_a, obj_b, S: int = 512,
+                 sampler_seed: int = 0, z: Optional[torch.Tensor] = None, box_device: Optional[bool] = None,
+                 kd_scan: Optional[bool] = None, num_threads: Optional[int] = None):
+        dev = gp.device
+        self.gp, self.dev = gp, dev
+        m, n = gp.B, gp.n
+        self.m, self.n, self.S, self.nb, self.nk = m, n, int(S), 0, n
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.ref = torch.as_tensor(np.asarray(ref_point, dtype=np.float64), **f64)
+        self.obj_a = torch.as_tensor(np.asarray(obj_a, dtype=np.float64), **f64)
+        self.obj_b = torch.as_tensor(np.asarray(obj_b, dtype=np.float64), **f64)
+        Y_part = np.asarray(Y_part, dtype=np.float64).reshape(-1, m)
+        self.Xk = gp.Xn
+        S_ = self.S
+        if Y_part.shape[0] > 0:
+            O = torch.as_tensor(np.ascontiguousarray(Y_part.T), **f64)[:, :, None].expand(m, Y_part.shape[0], S_)
+            cells, self.box_path = _decompose(O.contiguous(), self.ref, box_device, kd_scan, num_threads)
+        else:
+            cells, self.box_path = _single_cell(self.ref, S_, m), "none"
+        self.cells = cells
+        cnt = cells.counts
+        self.stats = ConstructionStats(n_train=n, n_base=0, total_cells=int(np.sum(cnt)),
+                                       max_cells=int(cnt.max()) if len(cnt) else 0)
+        if z is None:
+            self.zq = ops.sobol_normal(S_, m, sampler_seed, dev)                  # S x m
+        else:
+            self.zq = z.reshape(S_, m).to(**f64).contiguous()
+        self.Rr = n + 1
+        M = torch.empty(m, n + 1, n, **f64)
+        M[:, :n].copy_(gp.Linv)
+        M[:, n].copy_(gp.alpha)
+        self.M = M
+        self.state = ops.make_state(n, 0, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a, self.obj_b,
+                                    cells, no_h=True)
+        self._lo_c = gp.lo.to(torch.float64).contiguous()
+        self._scale_c = gp.inv_range.to(torch.float64).contiguous()
+        self.model = _native.EvrQnehviModel(n=n, d=gp.d, kind=gp.kind, Xn=self.Xk.data_ptr(),
+                                            lengthscales=gp.ls.data_ptr(), shift=self._lo_c.data_ptr(),
+                                            scale=self._scale_c.data_ptr(), M=self.M.data_ptr())
+        self._plans = {}
+        torch.cuda.synchronize(dev)
 
 
 class QEI:

@@ -93,6 +93,12 @@ __device__ __forceinline__ double exp_k(double x) {
   return __builtin_ldexp(fma(t, p, t), k >> 6);
 }
 
+// qNEHVI operator layout: H^T rows in M (S, or 0 for qEHVI) and total rows Rr.
+template <class State>
+inline int qn_nh(const State* st) { return st->no_h ? 0 : st->S; }
+template <class State>
+inline int qn_rows(const State* st) { return st->n + st->nb + qn_nh(st) + 1; }
+
 // Kernel families (same numbering as include/everest_amd.h EVR_KERNEL_*).
 enum KernelKind { RBF = 0, MATERN05 = 1, MATERN15 = 2, MATERN25 = 3 };
 

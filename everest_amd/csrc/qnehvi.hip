@@ -17,7 +17,7 @@ namespace evr {
 // group writes its share of the S samples.  Grid (candidate tiles, m).
 // -------------------------------------------------------------------------------------
 template <int BX>
-__global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, int m, int b,
+__global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, int nh, int m, int b,
                                                          const double* __restrict__ R,
                                                          const double* __restrict__ cc,
                                                          const double* __restrict__ ym,
@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, i
   const int cx = threadIdx.x % BX, ry = threadIdx.x / BX;
   const int c = blockIdx.x * BX + cx;
   const bool live = c < b;
-  const long long Rr = (long long)n + nb + S + 1;
+  const long long Rr = (long long)n + nb + nh + 1;
   const double* Rj = R + (size_t)j * Rr * b;
   double ssv = 0.0, ssw = 0.0;
   if (live) {
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, i
     ssw += red[1][g][cx];
   }
   if (!live) return;
-  const double a = Rj[(size_t)(n + nb + S) * b + c];
+  const double a = Rj[(size_t)(n + nb + nh) * b + c];
   const double s = ys[j];
   const double mu = ym[j] + s * (cc[j] + a);
   const double var = s * s * (kxx[j] - ssv);
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void qn_samples_kernel(int n, int nb, int S, i
   const double A = oa[j], B0 = ob[j];
   const double* h = Rj + (size_t)(n + nb) * b + c;
   for (int si = ry; si < S; si += RY) {
-    const double y = mu + h[(size_t)si * b] + l22 * zq[(size_t)si * m + j];
+    const double y = (nh ? mu + h[(size_t)si * b] : mu) + l22 * zq[(size_t)si * m + j];
     G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
   }
 }
@@ -97,7 +97,7 @@ __global__ void mean_over_samples_kernel(int S, int b, const double* __restrict_
 
 // samples backward: same (BX x RY) blocking; writes gR_j (Rr x b)
 template <int BX>
-__global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int S, int m, int b,
+__global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int S, int nh, int m, int b,
                                                              const double* __restrict__ R,
                                                              const double* __restrict__ ys,
                                                              const double* __restrict__ zq,
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int 
   const int cx = threadIdx.x % BX, ry = threadIdx.x / BX;
   const int c = blockIdx.x * BX + cx;
   const bool live = c < b;
-  const long long Rr = (long long)n + nb + S + 1;
+  const long long Rr = (long long)n + nb + nh + 1;
   const double* Rj = R + (size_t)j * Rr * b;
   double* gj = gR + (size_t)j * Rr * b;
   const double A = oa[j];
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int 
       const double dy = A * dG[((size_t)si * m + j) * b + c];
       dmu += dy;
       dl = fma(dy, zq[(size_t)si * m + j], dl);
-      gj[(size_t)(n + nb + si) * b + c] = dy;
+      if (nh) gj[(size_t)(n + nb + si) * b + c] = dy;
     }
   }
   red[0][ry][cx] = dmu;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void qn_samples_bwd_kernel(int n, int nb, int 
   }
   if (!live) return;
   const double s = ys[j];
-  if (ry == 0) gj[(size_t)(n + nb + S) * b + c] = s * dmu;
+  if (ry == 0) gj[(size_t)(n + nb + nh) * b + c] = s * dmu;
   const double l22 = L22[(size_t)j * b + c];
   const double dbr = dl / (2.0 * l22);
   const double dssv = -s * s * dbr;  // var = s^2 (kxx - ssv); br = var - ssw
@@ -282,11 +282,11 @@ int evr_qnehvi_samples(void* stream, const evr_qnehvi_state* st, int b, const do
   hipStream_t s = (hipStream_t)stream;
   if (b <= 256) {  // small batches: 16 candidates x 16 row groups per block
     dim3 grid(cdiv(b, 16), st->m);
-    qn_samples_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys, st->kxx,
+    qn_samples_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, R, st->c, st->ym, st->ys, st->kxx,
                                                st->zq, st->obj_a, st->obj_b, G, L22, flags);
   } else {
     dim3 grid(cdiv(b, 64), st->m);
-    qn_samples_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->c, st->ym, st->ys, st->kxx,
+    qn_samples_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, R, st->c, st->ym, st->ys, st->kxx,
                                                st->zq, st->obj_a, st->obj_b, G, L22, flags);
   }
   EVR_LAUNCH_CHECK();
@@ -307,11 +307,11 @@ int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b,
   hipStream_t s = (hipStream_t)stream;
   if (b <= 256) {
     dim3 grid(cdiv(b, 16), st->m);
-    qn_samples_bwd_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq, st->obj_a,
+    qn_samples_bwd_kernel<16><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, R, st->ys, st->zq, st->obj_a,
                                                    L22, dG, gR);
   } else {
     dim3 grid(cdiv(b, 64), st->m);
-    qn_samples_bwd_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, st->ys, st->zq, st->obj_a,
+    qn_samples_bwd_kernel<64><<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, R, st->ys, st->zq, st->obj_a,
                                                    L22, dG, gR);
   }
   EVR_LAUNCH_CHECK();

@@ -41,7 +41,7 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, int backward) {
   PlanLayout L{};
-  const size_t m = st->m, n = st->n, Rr = (size_t)st->n + st->nb + st->S + 1;
+  const size_t m = st->m, n = st->n, Rr = (size_t)qn_rows(st);
   size_t o = 0;
   auto take = [&](size_t bytes) {
     const size_t r = o;

@@ -204,7 +204,8 @@ __global__ __launch_bounds__(256) void qn_proj_fwd_reduce(int n, int nb, int Rr,
 // ---------------------------------------------------------------------------------------
 constexpr int SCH = 16;
 
-__global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int m, int b, int nrt_used, int nrt,
+__global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int nh, int m, int b, int nrt_used,
+                                                       int nrt,
                                                        const double* __restrict__ P, const double* __restrict__ R,
                                                        const double* __restrict__ cc, const double* __restrict__ ym,
                                                        const double* __restrict__ ys, const double* __restrict__ kxx,
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
                                                        double* __restrict__ L22, int* __restrict__ flags) {
   const int c = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y, chunk = blockIdx.z;
   if (c >= b) return;
-  const long long Rr = (long long)n + nb + S + 1;
+  const long long Rr = (long long)n + nb + nh + 1;
   const double* Pj = P + (size_t)j * nrt * 2 * b;
   double ssv = 0.0, ssw = 0.0;
   for (int rt = 0; rt < nrt_used; ++rt) {
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
   const double* h = Rj + (size_t)(n + nb) * b + c;
   const int s1 = min(S, (chunk + 1) * SCH);
   for (int si = chunk * SCH; si < s1; ++si) {
-    const double y = mu + h[(size_t)si * b] + l22 * zq[(size_t)si * m + j];
+    const double y = (nh ? mu + h[(size_t)si * b] : mu) + l22 * zq[(size_t)si * m + j];
     G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
   }
 }
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(1024) void qn_bwd_coef(int S, int m, int b, const d
 // ---------------------------------------------------------------------------------------
 // backward: dKx_j = M_j^T gR_j with gR generated in the fetch, optional split-K into W
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int m, int b,
+__global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int nh, int m, int b,
                                                    const double* __restrict__ Mm, const double* __restrict__ R,
                                                    const double* __restrict__ dG, const double* __restrict__ oa,
                                                    const double* __restrict__ coef, double* __restrict__ dK,
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int m, 
   const int bx = t % gx, by = (t / gx) % gy, bz = t / (gx * gy);
   const int j = bz / ksplit, kz = bz - j * ksplit;
   const int m0 = by * PT, n0 = bx * PT;
-  const int Rr = n + nb + S + 1;
+  const int Rr = n + nb + nh + 1;
   const double* A = Mm + (size_t)j * Rr * n;   // A(row, k) = M_j[k][row]
   const double* Rj = R + (size_t)j * Rr * b;
   const double* cj = coef + (size_t)j * 3 * b;
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int m, 
         if (n0 + c >= b) return 0.0;
         if (k < n) return Rj[(size_t)k * b + n0 + c] * cf[0][c];
         if (k < n + nb) return Rj[(size_t)k * b + n0 + c] * cf[1][c];
-        if (k < n + nb + S) return aj * dG[((size_t)(k - n - nb) * m + j) * b + n0 + c];
+        if (k < n + nb + nh) return aj * dG[((size_t)(k - n - nb) * m + j) * b + n0 + c];
         return cf[2][c];
       },
       acc);
@@ -388,10 +389,10 @@ __global__ __launch_bounds__(256) void qn_norms_rows(int n, int nb, int Rr, int 
 }
 
 // gR_j (Rr x b) from R, dG and the per-candidate coefficients (see the header)
-__global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int S, int m, int b, const double* __restrict__ R,
+__global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int nh, int m, int b, const double* __restrict__ R,
                                                  const double* __restrict__ dG, const double* __restrict__ oa,
                                                  const double* __restrict__ coef, double* __restrict__ gR) {
-  const int Rr = n + nb + S + 1;
+  const int Rr = n + nb + nh + 1;
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= (long long)m * Rr * b) return;
   const int c = (int)(e % b);
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int S, int m, in
   double v;
   if (row < n) v = R[e] * cj[c];
   else if (row < n + nb) v = R[e] * cj[(size_t)b + c];
-  else if (row < n + nb + S) v = oa[j] * dG[((size_t)(row - n - nb) * m + j) * b + c];
+  else if (row < n + nb + nh) v = oa[j] * dG[((size_t)(row - n - nb) * m + j) * b + c];
   else v = cj[(size_t)2 * b + c];
   gR[e] = v;
 }
@@ -442,7 +443,7 @@ int gemm_backend_init() {
 
 // ---- internal launchers (workspace supplied by the caller; qnehvi_plan.hip) ----------
 size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b) {
-  const int Rr = st->n + st->nb + st->S + 1;
+  const int Rr = qn_rows(st);
   if (use_rocblas()) return 0;
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(Rr, PT) * st->m, st->n, &kchunk);
@@ -452,7 +453,7 @@ size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b) {
 int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* Kx, double* R,
                  double* norms, double* W) {
   if (b == 0) return 0;
-  const int Rr = st->n + st->nb + st->S + 1;
+  const int Rr = qn_rows(st);
   const int nrt = cdiv(Rr, PT);
   if (use_rocblas()) {
     if (int rc = rb_gemm(s, false, Rr, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R, b,
@@ -482,7 +483,7 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
 static bool bwd_rocblas(int b) { return use_rocblas() && b >= 64; }
 
 size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b) {
-  const int Rr = st->n + st->nb + st->S + 1;
+  const int Rr = qn_rows(st);
   if (bwd_rocblas(b)) return (size_t)st->m * 3 * b + (size_t)st->m * Rr * b;   // coefficients + gR
   int kchunk = 0;
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
@@ -492,14 +493,14 @@ size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b) {
 int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
                   const double* L22, const double* dG, double* dKx, double* ws) {
   if (b == 0) return 0;
-  const int Rr = st->n + st->nb + st->S + 1;
+  const int Rr = qn_rows(st);
   double* coef = ws;
   qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
   EVR_LAUNCH_CHECK();
   if (bwd_rocblas(b)) {
     double* gR = ws + (size_t)st->m * 3 * b;
     const long long tot = (long long)st->m * Rr * b;
-    qn_gen_gr<<<cdiv(tot, 256), 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, R, dG, st->obj_a, coef, gR);
+    qn_gen_gr<<<cdiv(tot, 256), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, R, dG, st->obj_a, coef, gR);
     EVR_LAUNCH_CHECK();
     return rb_gemm(s, true, st->n, b, Rr, Mm, st->n, (long long)Rr * st->n, gR, b, (long long)Rr * b, dKx, b,
                    (long long)st->n * b, st->m);
@@ -508,7 +509,7 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
   const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
   double* W = ws + (size_t)st->m * 3 * b;
   dim3 grid(cdiv(b, PT), cdiv(st->n, PT), st->m * ks);
-  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
+  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
   EVR_LAUNCH_CHECK();
   if (ks > 1) {
     const long long per = (long long)st->m * st->n * b;
@@ -521,11 +522,11 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
                   double* L22, int* flags) {
   if (b == 0) return 0;
-  const int Rr = st->n + st->nb + st->S + 1;
+  const int Rr = qn_rows(st);
   const int nrt = cdiv(Rr, PT);
   const int nrt_used = cdiv(st->n + st->nb, PT);
   dim3 grid(cdiv(b, 64), st->m, cdiv(st->S, SCH));
-  qn_samples_norms<<<grid, 64, 0, s>>>(st->n, st->nb, st->S, st->m, b, nrt_used, nrt, norms, R, st->c, st->ym, st->ys,
+  qn_samples_norms<<<grid, 64, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, nrt_used, nrt, norms, R, st->c, st->ym, st->ys,
                                         st->kxx, st->zq, st->obj_a, st->obj_b, G, L22, flags);
   EVR_LAUNCH_CHECK();
   return 0;
@@ -539,7 +540,7 @@ extern "C" {
 
 int evr_qnehvi_norms_rows(const evr_qnehvi_state* st) {
   if (!st) return 0;
-  return cdiv((long long)st->n + st->nb + st->S + 1, PT);
+  return cdiv((long long)qn_rows(st), PT);
 }
 
 long long evr_qnehvi_project_workspace_doubles(const evr_qnehvi_state* st, int b) {

@@ -4,4 +4,5 @@ from .domain import (BaseModel, CategoricalInput, CloseToTargetObjective, Constr
 from .models import (BotorchSurrogates, CategoricalEncodingEnum, CategoricalMethodEnum,
                      DimensionalityScaledLogNormalPrior, GammaPrior, LogNormalPrior, MaternKernel, NormalPrior,
                      QehviStrategy, QnehviStrategy, RandomStrategy, RBFKernel, ScalerEnum, SingleTaskGPSurrogate,
-                     SoboStrategy, qEI, qLogEI, qLogNEI, qNEI)
+                     SoboStrategy, MoboStrategy, qEHVI, qEI, qLogEHVI, qLogEI, qLogNEHVI, qLogNEI, qNEHVI,
+                     qNEI)

@@ -178,24 +178,65 @@ class BotorchSurrogates(BaseModel):
 # ---------------------------------------------------------------------------------------
 # acquisition functions (bofire/data_models/acquisition_functions/acquisition_function.py)
 # ---------------------------------------------------------------------------------------
-class qEI(BaseModel):
+class _AcqfMC(BaseModel):
+    """n_mc_samples must be a power of two (bofire IntPowerOfTwo)."""
+
+    @field_validator("n_mc_samples", check_fields=False)
+    @classmethod
+    def _p2mc(cls, v):
+        return _is_power_of_two(v)
+
+
+class qEI(_AcqfMC):
     type: Literal["qEI"] = "qEI"
+    n_mc_samples: int = 512
 
 
-class qLogEI(BaseModel):
+class qLogEI(_AcqfMC):
     type: Literal["qLogEI"] = "qLogEI"
+    n_mc_samples: int = 512
 
 
-class qNEI(BaseModel):
+class qNEI(_AcqfMC):
     type: Literal["qNEI"] = "qNEI"
     prune_baseline: bool = True
+    n_mc_samples: int = 512
 
 
-class qLogNEI(BaseModel):
+class qLogNEI(_AcqfMC):
     type: Literal["qLogNEI"] = "qLogNEI"
     prune_baseline: bool = True
+    n_mc_samples: int = 512
 
 
+class qEHVI(_AcqfMC):
+    type: Literal["qEHVI"] = "qEHVI"
+    alpha: Annotated[float, Field(ge=0)] = 0.0
+    n_mc_samples: int = 512
+
+
+class qLogEHVI(_AcqfMC):
+    type: Literal["qLogEHVI"] = "qLogEHVI"
+    alpha: Annotated[float, Field(ge=0)] = 0.0
+    n_mc_samples: int = 512
+
+
+class qNEHVI(_AcqfMC):
+    type: Literal["qNEHVI"] = "qNEHVI"
+    alpha: Annotated[float, Field(ge=0)] = 0.0
+    prune_baseline: bool = True
+    n_mc_samples: int = 512
+
+
+class qLogNEHVI(_AcqfMC):
+    type: Literal["qLogNEHVI"] = "qLogNEHVI"
+    alpha: Annotated[float, Field(ge=0)] = 0.0
+    prune_baseline: bool = True
+    n_mc_samples: int = 512
+
+
+AnyMultiObjectiveAcquisitionFunction = Annotated[Union[qEHVI, qLogEHVI, qNEHVI, qLogNEHVI],
+                                                 Field(discriminator="type")]
 AnySingleObjectiveAcquisitionFunction = Annotated[Union[qEI, qLogEI, qNEI, qLogNEI], Field(discriminator="type")]
 
 
@@ -298,9 +339,27 @@ class QnehviStrategy(QehviStrategy):
     alpha: Annotated[float, Field(ge=0, le=0.5)] = 0.0
 
 
+class MoboStrategy(MultiobjectiveStrategy):
+    """bofire/data_models/strategies/predictives/mobo.py:24-80."""
+    type: Literal["MoboStrategy"] = "MoboStrategy"
+    ref_point: Optional[Dict[str, float]] = None
+    acquisition_function: AnyMultiObjectiveAcquisitionFunction = Field(default_factory=qLogNEHVI)
+
+    @model_validator(mode="after")
+    def _ref(self):
+        if self.ref_point is None:
+            return self
+        keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
+                                                          CloseToTargetObjective])
+        if sorted(keys) != sorted(self.ref_point.keys()):
+            raise ValueError(f"Provided refpoint do not match the domain, expected keys: {keys}")
+        return self
+
+
 class SoboStrategy(BotorchStrategy):
     type: Literal["SoboStrategy"] = "SoboStrategy"
     acquisition_function: AnySingleObjectiveAcquisitionFunction = Field(default_factory=qLogNEI)
 
 
-AnyStrategy = Annotated[Union[QnehviStrategy, SoboStrategy, RandomStrategy], Field(discriminator="type")]
+AnyStrategy = Annotated[Union[QnehviStrategy, QehviStrategy, MoboStrategy, SoboStrategy, RandomStrategy],
+                       Field(discriminator="type")]

@@ -267,9 +267,11 @@ def gp_posterior(Xn, X, shift, scale, lengthscales, M, kind, c, ym, ys, kxx, noi
 # ---------------------------------------------------------------------------------------
 # qNEHVI pieces
 # ---------------------------------------------------------------------------------------
-def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cells: "Cells") -> EvrQnehviState:
+def make_state(n, nb, S, m, c, ym, ys, kxx, zq, obj_a, obj_b, cells: "Cells", no_h: bool = False) -> EvrQnehviState:
+    """no_h: the operator M carries no H^T rows (qEHVI: samples mu + L22 z, nb = 0)."""
     st = EvrQnehviState()
     st.n, st.nb, st.S, st.m = int(n), int(nb), int(S), int(m)
+    st.no_h = int(bool(no_h))
     st.c, st.ym, st.ys, st.kxx = c.data_ptr(), ym.data_ptr(), ys.data_ptr(), kxx.data_ptr()
     st.zq, st.obj_a, st.obj_b = zq.data_ptr(), obj_a.data_ptr(), obj_b.data_ptr()
     st.cell_lo, st.cell_hi = _p(cells.lo), _p(cells.hi)
@@ -297,7 +299,7 @@ def qnehvi_samples(st: EvrQnehviState, R: torch.Tensor, b: int):
 def qnehvi_project(st: EvrQnehviState, M: torch.Tensor, Kx: torch.Tensor, b: int):
     """R = M Kx (m x Rr x b) and the partial norms the sampling step needs (one fused GEMM)."""
     dev = Kx.device
-    Rr = st.n + st.nb + st.S + 1
+    Rr = st.n + st.nb + (0 if st.no_h else st.S) + 1
     R = torch.empty(st.m, Rr, b, dtype=torch.float64, device=dev)
     nrt = _native.load().evr_qnehvi_norms_rows(ctypes.byref(st))
     P = torch.empty(st.m, nrt, 2, b, dtype=torch.float64, device=dev)

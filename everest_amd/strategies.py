@@ -18,7 +18,7 @@ import pandas as pd
 import torch
 
 from . import data_models as dm
-from .acquisition import QNEHVI, QEI
+from .acquisition import QEHVI, QNEHVI, QEI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
 from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
 from .surrogates import BotorchSurrogates, device
@@ -395,19 +395,11 @@ class BotorchStrategy(PredictiveStrategy):
         raise NotImplementedError
 
 
-class QnehviStrategy(BotorchStrategy):
-    """bofire/strategies/predictives/qehvi.py + qnehvi.py."""
-
-    def __init__(self, data_model, dist=None, **kwargs):
-        super().__init__(data_model, dist=dist)
-        self.num_sobol_samples = data_model.num_sobol_samples
-        self.ref_point = data_model.ref_point
-        self.ref_point_mask = get_ref_point_mask(self.domain)
-        self.alpha = data_model.alpha
-        self.last_acqf: Optional[QNEHVI] = None
+class _MultiobjectiveMixin:
+    """Reference point and objective handling shared by the hypervolume strategies
+    (bofire/strategies/predictives/qehvi.py:87-110, mobo.py:92-115)."""
 
     def get_adjusted_refpoint(self) -> List[float]:
-        """bofire/strategies/predictives/qehvi.py:87-110."""
         assert self.experiments is not None, "No experiments available."
         if self.ref_point is None:
             df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
@@ -419,6 +411,8 @@ class QnehviStrategy(BotorchStrategy):
         return (self.ref_point_mask * np.array([ref_point[k] for k in keys])).tolist()
 
     def _objective_affine(self):
+        """g_j = a_j y_j + b_j per output (bofire/utils/torch_tools.py:384-402); the device
+        kernels take affine objectives (Maximize / Minimize with bounds)."""
         keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
                                                           CloseToTargetObjective])
         if keys != self.model.output_keys:
@@ -433,6 +427,50 @@ class QnehviStrategy(BotorchStrategy):
             b.append(bb)
         return np.array(a), np.array(b)
 
+    def _observed_outputs(self) -> np.ndarray:
+        """Valid observations of the objective outputs (n x m, model output order)."""
+        df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        return df[self.model.output_keys].values.astype(np.float64)
+
+    def _draw_seed(self) -> int:
+        return int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
+
+
+class QehviStrategy(_MultiobjectiveMixin, BotorchStrategy):
+    """bofire/strategies/predictives/qehvi.py:24-85 — qEHVI on the device."""
+
+    def __init__(self, data_model, dist=None, **kwargs):
+        super().__init__(data_model, dist=dist)
+        self.num_sobol_samples = data_model.num_sobol_samples
+        self.ref_point = data_model.ref_point
+        self.ref_point_mask = get_ref_point_mask(self.domain)
+        self.last_acqf = None
+
+    def _get_acqfs(self, n) -> List[QEHVI]:
+        """bofire/strategies/predictives/qehvi.py:37-79: the partition is built from the
+        masked observations better than the reference point (not objective-transformed)."""
+        assert self.experiments is not None, "No experiments available."
+        _, X_pending = self.get_acqf_input_tensors()
+        if X_pending is not None:
+            raise NotImplementedError("qEHVI with pending candidates needs q > 1 inclusion-exclusion "
+                                      "(out of scope: the device kernels evaluate q = 1)")
+        a, b = self._objective_affine()
+        train_obj = self._observed_outputs() * self.ref_point_mask
+        ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
+        better = (train_obj > ref).all(axis=-1)
+        acqf = QEHVI(self.model, train_obj[better], ref, a, b, S=self.num_sobol_samples,
+                     sampler_seed=self._draw_seed())
+        self.last_acqf = acqf
+        return [acqf]
+
+
+class QnehviStrategy(QehviStrategy):
+    """bofire/strategies/predictives/qnehvi.py:16-53."""
+
+    def __init__(self, data_model, dist=None, **kwargs):
+        super().__init__(data_model, dist=dist)
+        self.alpha = data_model.alpha
+
     def _get_acqfs(self, n) -> List[QNEHVI]:
         """bofire/strategies/predictives/qnehvi.py:23-53."""
         assert self.experiments is not None, "No experiments available."
@@ -442,10 +480,51 @@ class QnehviStrategy(BotorchStrategy):
         a, b = self._objective_affine()
         ref = self.get_adjusted_refpoint()
         # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed
-        prune_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
-        sampler_seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
+        prune_seed = self._draw_seed()
+        sampler_seed = self._draw_seed()
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=self.num_sobol_samples,
                       sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending)
+        self.last_acqf = acqf
+        return [acqf]
+
+
+class MoboStrategy(_MultiobjectiveMixin, BotorchStrategy):
+    """bofire/strategies/predictives/mobo.py:28-115: the acquisition function comes from the
+    data model ([upstream] botorch.acquisition.factory.get_acquisition_function) — qEHVI
+    over the FastNondominatedPartitioning of the objective-transformed observations, or
+    qNEHVI with the data model's prune_baseline; mc_samples = n_mc_samples."""
+
+    def __init__(self, data_model, dist=None, **kwargs):
+        super().__init__(data_model, dist=dist)
+        self.ref_point = data_model.ref_point
+        self.ref_point_mask = get_ref_point_mask(self.domain)
+        self.acquisition_function = data_model.acquisition_function
+        self.last_acqf = None
+
+    def _get_acqfs(self, n):
+        assert self.is_fitted is True, "Model not trained."
+        assert self.experiments is not None, "No experiments available."
+        af = self.acquisition_function
+        if getattr(af, "alpha", 0.0) != 0.0:
+            raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
+        X_train, X_pending = self.get_acqf_input_tensors()
+        a, b = self._objective_affine()
+        ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
+        S = int(af.n_mc_samples)
+        if isinstance(af, dm.qEHVI):
+            if X_pending is not None:
+                raise NotImplementedError("qEHVI with pending candidates needs q > 1 inclusion-exclusion "
+                                          "(out of scope: the device kernels evaluate q = 1)")
+            Y = self._observed_outputs()
+            acqf = QEHVI(self.model, Y * a + b, ref, a, b, S=S, sampler_seed=self._draw_seed())
+        elif isinstance(af, dm.qNEHVI):
+            prune_seed = self._draw_seed() if af.prune_baseline else 0
+            sampler_seed = self._draw_seed()
+            acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=S, sampler_seed=sampler_seed,
+                          prune_baseline=af.prune_baseline, prune_seed=prune_seed, X_pending_raw=X_pending)
+        else:
+            raise NotImplementedError(f"{type(af).__name__} has no device kernel in this build "
+                                      "(qEHVI and qNEHVI do)")
         self.last_acqf = acqf
         return [acqf]
 
@@ -468,11 +547,13 @@ class SoboStrategy(BotorchStrategy):
         if X_pending is not None:
             raise NotImplementedError("pending candidates are not yet supported on the device path")
         seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
-        return [QEI(self.model, X_train, a, b, S=512, seed=seed)]
+        return [QEI(self.model, X_train, a, b, S=int(self.acquisition_function.n_mc_samples), seed=seed)]
 
 
 STRATEGY_MAP = {
     dm.QnehviStrategy: QnehviStrategy,
+    dm.QehviStrategy: QehviStrategy,
+    dm.MoboStrategy: MoboStrategy,
     dm.SoboStrategy: SoboStrategy,
     dm.RandomStrategy: RandomStrategy,
 }

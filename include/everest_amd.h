@@ -120,7 +120,8 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
  * Replaces [upstream] qNoisyExpectedHypervolumeImprovement.forward/backward as built at
  * bofire/strategies/predictives/qnehvi.py:39-52 (cached-Cholesky sampling + box-cell HVI).
  * Per output j the precomputed operator M_j = [Linv; G; H^T; alpha^T] (rows Rr =
- * n + nb + S + 1) has been applied to k(Xtr, x): R_j = M_j K_x (Rr x b, ld b). */
+ * n + nb + S + 1; n + nb + 1 with no_h) has been applied to k(Xtr, x): R_j = M_j K_x
+ * (Rr x b, ld b). */
 typedef struct {
   int n, nb, S, m;          /* train points, pruned baseline, MC samples, objectives */
   const double* c;          /* m: constant mean (standardized space) */
@@ -153,6 +154,10 @@ typedef struct {
   /* optional scan statistics (nullable, device): [0] += passing (candidate, group) pairs,
    * [1] += exact (cell, candidate) terms evaluated, [2] += (candidate, group) tests */
   unsigned long long* scan_counters;
+  /* 0: M = [Linv; G; H^T; alpha^T] (qNEHVI).  1: M carries no H^T rows (Rr = n + nb + 1) and
+   * the samples have no baseline term, y_s = mu + L22 zq_s — qEHVI, where the cells come
+   * from the observed Pareto front instead of per-sample baseline draws (nb = 0). */
+  int no_h;
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b

@@ -3,7 +3,8 @@
 Reference-structure restatement (torch-CPU float64, autograd-capable) of
 ``qNoisyExpectedHypervolumeImprovement`` as BoFire builds it
 (bofire/strategies/predictives/qnehvi.py:23-53: prune_baseline=True, cache_root=True,
-alpha=0, no output constraints) and of qEI (bofire/strategies/predictives/sobo.py:51-90).
+alpha=0, no output constraints), of qEHVI (QehviStrategy / MoboStrategy) and of qEI
+(bofire/strategies/predictives/sobo.py:51-90).
 
 It deliberately keeps BoTorch's computation *shape*  so that it doubles as
 the CPU baseline timed by bench.py: the joint posterior over [X_baseline; X] is formed per
@@ -155,6 +156,39 @@ class QNEHVI:
 
     def forward(self, Xn: torch.Tensor) -> torch.Tensor:
         return self.hvi_per_sample(self.obj(self.samples(Xn))).mean(0)
+
+
+class QEHVI:
+    """Reference-structure qEHVI ([upstream] qExpectedHypervolumeImprovement) as built by
+    QehviStrategy._get_acqfs (bofire/strategies/predictives/qehvi.py:37-79) and by
+    get_acquisition_function("qEHVI") in MoboStrategy._get_acqfs
+    (bofire/strategies/predictives/mobo.py:44-90): one exact partition of the non-dominated
+    region of ``Y_part`` above ``ref`` shared by all samples, samples of the independent
+    per-output posterior at the candidates only (no baseline), HVI by inclusion–exclusion
+    over q-subsets, mean over samples.  z: S x q x m (Sobol dim = point*m + output)."""
+
+    def __init__(self, models: List[GPState], Y_part: torch.Tensor, objective: Objective, ref: torch.Tensor,
+                 z: torch.Tensor):
+        self.models, self.obj, self.ref, self.z = models, objective, ref, z
+        self.cell = nondominated_cells(pareto_above_ref(Y_part, ref), ref)
+
+    def samples(self, Xn: torch.Tensor) -> torch.Tensor:
+        mean, cov = joint_posterior(self.models, Xn)               # b x q x m, b x m x q x q
+        L, _ = psd_safe_cholesky(cov, max_tries=6)
+        return mean.unsqueeze(0) + torch.einsum("bjqk,skj->sbqj", L, self.z)
+
+    def forward(self, Xn: torch.Tensor) -> torch.Tensor:
+        import itertools
+        obj = self.obj(self.samples(Xn))                           # S x b x q x m
+        S, b, q, m = obj.shape
+        lo, hi = self.cell[0], self.cell[1]
+        out = torch.zeros(S, b, **TK)
+        for i in range(1, q + 1):
+            for sub in itertools.combinations(range(q), i):
+                ov = obj[:, :, list(sub), :].min(dim=-2).values                   # S x b x m
+                ln = (torch.minimum(ov.unsqueeze(-2), hi) - lo).clamp_min(0.0)    # S x b x C x m
+                out = out + ((-1) ** (i + 1)) * ln.prod(-1).sum(-1)
+        return out.mean(0)
 
 
 def qei(models, Xn: torch.Tensor, best_f: float, z: torch.Tensor, a: float = 1.0, bconst: float = 0.0):

@@ -76,6 +76,21 @@ p = DimensionalityScaledLogNormalPrior()
 out["dim_scaled_prior"] = {"loc": p.loc, "loc_scaling": p.loc_scaling, "scale": p.scale,
                            "scale_scaling": p.scale_scaling}
 
+# hypervolume strategies and acquisition-function data models
+# (data_models/strategies/predictives/{qehvi,mobo}.py, data_models/acquisition_functions/acquisition_function.py)
+from bofire.data_models.acquisition_functions.api import qEHVI, qEI, qLogEHVI, qLogNEHVI, qNEHVI
+from bofire.data_models.strategies.predictives.mobo import MoboStrategy
+from bofire.data_models.strategies.predictives.qehvi import QehviStrategy
+
+out["acqf_dumps"] = {c.__name__: json.loads(c().model_dump_json()) for c in (qEHVI, qLogEHVI, qNEHVI, qLogNEHVI, qEI)}
+mo = MoboStrategy(domain=det.domain)
+out["mobo_defaults"] = {"acquisition_function": json.loads(mo.acquisition_function.model_dump_json()),
+                        "ref_point": mo.ref_point, "num_restarts": mo.num_restarts,
+                        "num_raw_samples": mo.num_raw_samples, "batch_limit": mo.batch_limit}
+qe = QehviStrategy(domain=det.domain)
+out["qehvi_defaults"] = {"num_sobol_samples": qe.num_sobol_samples, "ref_point": qe.ref_point,
+                         "type": qe.type}
+
 with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_datamodels.json"), "w") as f:
     json.dump(out, f, indent=1)
 print("wrote reference_datamodels.json")

@@ -105,3 +105,33 @@ def test_prune_keeps_only_possible_pareto_points():
                                    torch.full((2,), -1.1, dtype=torch.float64), oq.base_samples(256, 30, 2, 3))
     assert set(idx.tolist()) == set(np.nonzero(probs.numpy())[0].tolist())
     assert 0 < len(idx) < 30
+
+
+def test_qehvi_oracle_equals_exact_hv_difference():
+    """qEHVI restatement: per-sample HVI over the fixed partition equals
+    HV(P u {y_s}) - HV(P) computed by inclusion-exclusion (independent math)."""
+    import numpy as np
+    from oracle import qnehvi as oq
+    from oracle.multiobjective import hv_inclusion_exclusion, pareto_above_ref
+    from tests.helpers import make_problem, oracle_states
+
+    X, Y, lo, hi, hyp = make_problem(n=20, d=3, m=3, seed=2)
+    ost = oracle_states(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(3), np.zeros(3), -1.1 * np.ones(3)
+    obj = oq.Objective(torch.tensor(a), torch.tensor(b))
+    Yp = torch.tensor(Y * a + b)
+    acq = oq.QEHVI(ost, Yp, obj, torch.tensor(ref), oq.base_samples(8, 1, 3, 5))
+    Xc = torch.tensor(np.random.default_rng(0).uniform(size=(4, 1, 3)))
+    v = acq.forward(Xc).numpy()
+    smp = obj(acq.samples(Xc)).numpy()
+    P = pareto_above_ref(Yp, torch.tensor(ref)).numpy()
+    hv0 = hv_inclusion_exclusion(P, ref)
+    ind = np.zeros(4)
+    for s in range(8):
+        for c in range(4):
+            y = smp[s, c, 0]
+            if (y > ref).all():
+                P2 = pareto_above_ref(torch.tensor(np.vstack([P, y])), torch.tensor(ref)).numpy()
+                ind[c] += hv_inclusion_exclusion(P2, ref) - hv0
+    assert np.allclose(v, ind / 8, rtol=1e-9, atol=1e-12)   # HV differences cancel O(1) volumes
+    assert (v > 0).any()
