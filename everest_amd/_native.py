@@ -34,6 +34,7 @@ class EvrQnehviState(ctypes.Structure):
         ("cell_keys", c_void_p), ("cell_pts", c_void_p), ("cell_rank0", c_void_p), ("pts_stride", c_int),
         ("grp_off", c_void_p), ("grp_keys", c_void_p), ("grp_rank", c_void_p), ("grp_box", c_void_p),
         ("sorted_lo", c_void_p), ("max_groups", c_int), ("scan_counters", c_void_p), ("no_h", c_int),
+        ("log_hvi", c_int), ("tau_relu", c_double), ("tau_max", c_double),
     ]
 
 

@@ -89,6 +89,24 @@ class _BoxHviAcqf:
     cross-covariance, the sampling step, the box-cell HVI scan and their analytic backward
     (subclasses set gp, dev, Xk, M, state, model and _plans)."""
 
+    def _use_log_scan(self, tau_relu: float, tau_max: float):
+        """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
+        dense kernel of hvi_log.hip over the explicit cell bounds (compressed cells are
+        expanded once, on the device)."""
+        if not (tau_relu > 0 and tau_max > 0):
+            raise ValueError("tau_relu and tau_max must be positive")
+        lo, hi = self.cells.explicit()
+        st = _native.EvrQnehviState.from_buffer_copy(self.state)
+        st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
+        st.cell_keys = st.cell_pts = st.cell_rank0 = None
+        st.grp_off = st.grp_keys = st.grp_rank = st.grp_box = st.sorted_lo = None
+        st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
+        self._log_cells = (lo, hi)
+        self.state = st
+        self.tau_relu, self.tau_max = float(tau_relu), float(tau_max)
+        self.log_acqf = True      # may be negative: optimize_acqf uses initialize_q_batch
+        self._plans = {}
+
     def plan(self, b: int, backward: bool) -> ops.QnehviPlan:
         """Native evaluation plan for batch size b (cached; hipGraph unless EVR_GRAPH=0)."""
         key = (int(b), bool(backward))
@@ -414,6 +432,33 @@ class QEHVI(_BoxHviAcqf):
                                             scale=self._scale_c.data_ptr(), M=self.M.data_ptr())
         self._plans = {}
         torch.cuda.synchronize(dev)
+
+
+TAU_RELU = 1e-6     # [upstream] botorch.acquisition.logei.TAU_RELU
+TAU_MAX_MO = 1e-3   # [upstream] qLogExpectedHypervolumeImprovement default tau_max
+
+
+class QLogNEHVI(QNEHVI):
+    """Device qLogNEHVI (q = 1, fat = True) — [upstream] qLogNoisyExpectedHypervolumeImprovement,
+    MoboStrategy's default acquisition (bofire/data_models/strategies/predictives/mobo.py:27-29,
+    built at bofire/strategies/predictives/mobo.py:68-90).  Same construction, operator and
+    samples as QNEHVI; the scan is the dense log-space one (hvi_log.hip):
+    acq = logmeanexp_s logsumexp_cells sum_j fatmin(log fatplus(y_j - l_j; tau_relu),
+    log(min(u_j, 1e10) - l_j); tau_max)."""
+
+    def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
+        super().__init__(*args, **kw)
+        self._use_log_scan(tau_relu, tau_max)
+
+
+class QLogEHVI(QEHVI):
+    """Device qLogEHVI (q = 1, fat = True) — [upstream] qLogExpectedHypervolumeImprovement as
+    built by get_acquisition_function("qLogEHVI") in MoboStrategy: the qEHVI partition and
+    samples with the log-space scan."""
+
+    def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
+        super().__init__(*args, **kw)
+        self._use_log_scan(tau_relu, tau_max)
 
 
 class QEI:

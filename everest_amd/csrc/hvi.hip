@@ -846,8 +846,13 @@ static int hvi_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const Hv
   return 0;
 }
 
+long long hvi_log_workspace(const evr_qnehvi_state* st, int b, int backward);
+int hvi_log_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, const int* flags,
+                   const double* gout, double* work, double* acq, double* dG, bool backward);
+
 static int hvi_check_state(const evr_qnehvi_state* st) {
   EVR_CHECK(st && st->S >= 1 && st->m >= 1 && st->cell_off, "hvi: bad state");
+  if (st->log_hvi) return 0;   // hvi_log_launch checks its own inputs
   EVR_CHECK(st->cell_keys ? (st->cell_pts && st->cell_rank0 && st->pts_stride > 0) : (st->cell_lo && st->cell_hi),
             "hvi: state has neither explicit nor compressed cells");
   EVR_CHECK(!st->cell_keys || (size_t)st->pts_stride * (st->m * 8 + 4) <= 64 * 1024,
@@ -880,6 +885,7 @@ extern "C" {
 
 long long evr_hvi_workspace_doubles(const evr_qnehvi_state* st, int b, int backward) {
   if (!st || b <= 0) return 0;
+  if (st->log_hvi) return hvi_log_workspace(st, b, backward);
   if (st->grp_off) return hvi_kd_workspace(st, b);
   HviPlan p = hvi_plan(st, b);
   return (long long)st->S * p.nchunk * b * (backward ? st->m + 1 : 1);
@@ -891,6 +897,7 @@ int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const doubl
   EVR_CHECK(work && acq && G, "evr_hvi_forward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (st->log_hvi) return hvi_log_launch(s, st, b, G, flags, nullptr, work, acq, nullptr, false);
   int rc = 0;
   if (st->grp_off) {
 #define L(MM) rc = hvi_kd_launch<MM, false>(s, st, b, G, nullptr, work, nullptr, flags, acq)
@@ -914,6 +921,7 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
   EVR_CHECK(work && dG && G, "evr_hvi_forward_backward: bad arguments");
   if (b == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (st->log_hvi) return hvi_log_launch(s, st, b, G, flags, gout, work, acq, dG, true);
   if (st->grp_off) {
     int rc = 0;
 #define L(MM) rc = hvi_kd_launch<MM, true>(s, st, b, G, gout, work, dG, flags, acq)

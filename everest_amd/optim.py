@@ -117,6 +117,36 @@ def hit_and_run(bounds: np.ndarray, ineq: Sequence[LinearConstraint], eq: Sequen
     return out
 
 
+def initialize_q_batch(X: np.ndarray, acq: np.ndarray, n: int, gen: torch.Generator,
+                       eta: float = 1.0) -> Tuple[np.ndarray, np.ndarray]:
+    """[upstream] botorch.optim.initializers.initialize_q_batch — Boltzmann sampling with
+    weights exp(eta * z-score of acq), for acquisition functions that can be negative (the
+    log-space ones); the raw maximiser is always kept."""
+    ns = X.shape[0]
+    if n > ns:
+        raise RuntimeError(f"n ({n}) cannot exceed the number of raw samples ({ns})")
+    if n == ns:
+        return X, acq
+    acq_t = torch.as_tensor(acq)
+    Ystd = acq_t.std(dim=0)
+    if not bool(torch.isfinite(Ystd)) or float(Ystd) == 0.0:
+        warnings.warn("All acquisition values for raw samples points are the same for at least one batch. "
+                      "Choosing initial conditions at random.")
+        idx = torch.randperm(ns, generator=gen)[:n].numpy()
+        return X[idx], acq[idx]
+    max_val, max_idx = torch.max(acq_t, dim=0)
+    etaZ = eta * (acq_t - acq_t.mean(dim=0)) / Ystd
+    weights = torch.exp(etaZ)
+    while torch.isinf(weights).any():
+        etaZ = etaZ * 0.5
+        weights = torch.exp(etaZ)
+    idx = torch.multinomial(weights, n, generator=gen)
+    if int(max_idx) not in idx.tolist():
+        idx[-1] = max_idx
+    idx = idx.numpy()
+    return X[idx], acq[idx]
+
+
 def initialize_q_batch_nonneg(X: np.ndarray, acq: np.ndarray, n: int, gen: torch.Generator, eta: float = 1.0,
                               alpha: float = 1e-4) -> Tuple[np.ndarray, np.ndarray]:
     """[upstream] botorch.optim.initializers.initialize_q_batch_nonneg (Boltzmann sampling
@@ -201,6 +231,7 @@ class _FixedFeatures:
 
     def __init__(self, acqf, d: int, fixed: dict):
         self.acqf, self.d, self.dev = acqf, d, acqf.dev
+        self.log_acqf = getattr(acqf, "log_acqf", False)
         self.fixed_idx = np.array(sorted(fixed), dtype=int)
         self.fixed_val = np.array([fixed[j] for j in sorted(fixed)], dtype=np.float64)
         self.free = [j for j in range(d) if j not in fixed]
@@ -288,7 +319,8 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     stats.t_raw += time.perf_counter() - t0
 
     # 3. Boltzmann initial conditions
-    X0, _ = initialize_q_batch_nonneg(X_raw, Y_raw, num_restarts, gen)
+    init = initialize_q_batch if getattr(acqf, "log_acqf", False) else initialize_q_batch_nonneg
+    X0, _ = init(X_raw, Y_raw, num_restarts, gen)
 
     # 4. restarts, chunks of batch_limit, scipy on host with device value+gradient
     t0 = time.perf_counter()

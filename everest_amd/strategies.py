@@ -18,7 +18,7 @@ import pandas as pd
 import torch
 
 from . import data_models as dm
-from .acquisition import QEHVI, QNEHVI, QEI
+from .acquisition import QEHVI, QEI, QLogEHVI, QLogNEHVI, QNEHVI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
 from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
 from .surrogates import BotorchSurrogates, device
@@ -490,9 +490,10 @@ class QnehviStrategy(QehviStrategy):
 
 class MoboStrategy(_MultiobjectiveMixin, BotorchStrategy):
     """bofire/strategies/predictives/mobo.py:28-115: the acquisition function comes from the
-    data model ([upstream] botorch.acquisition.factory.get_acquisition_function) — qEHVI
+    data model ([upstream] botorch.acquisition.factory.get_acquisition_function) — q(Log)EHVI
     over the FastNondominatedPartitioning of the objective-transformed observations, or
-    qNEHVI with the data model's prune_baseline; mc_samples = n_mc_samples."""
+    q(Log)NEHVI with the data model's prune_baseline (qLogNEHVI is the default);
+    mc_samples = n_mc_samples."""
 
     def __init__(self, data_model, dist=None, **kwargs):
         super().__init__(data_model, dist=dist)
@@ -511,20 +512,21 @@ class MoboStrategy(_MultiobjectiveMixin, BotorchStrategy):
         a, b = self._objective_affine()
         ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
         S = int(af.n_mc_samples)
-        if isinstance(af, dm.qEHVI):
+        if isinstance(af, (dm.qEHVI, dm.qLogEHVI)):
             if X_pending is not None:
-                raise NotImplementedError("qEHVI with pending candidates needs q > 1 inclusion-exclusion "
-                                          "(out of scope: the device kernels evaluate q = 1)")
+                raise NotImplementedError(f"{type(af).__name__} with pending candidates needs q > 1 "
+                                          "inclusion-exclusion (out of scope: the device kernels evaluate q = 1)")
             Y = self._observed_outputs()
-            acqf = QEHVI(self.model, Y * a + b, ref, a, b, S=S, sampler_seed=self._draw_seed())
-        elif isinstance(af, dm.qNEHVI):
+            cls = QEHVI if isinstance(af, dm.qEHVI) else QLogEHVI
+            acqf = cls(self.model, Y * a + b, ref, a, b, S=S, sampler_seed=self._draw_seed())
+        elif isinstance(af, (dm.qNEHVI, dm.qLogNEHVI)):
             prune_seed = self._draw_seed() if af.prune_baseline else 0
             sampler_seed = self._draw_seed()
-            acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=S, sampler_seed=sampler_seed,
-                          prune_baseline=af.prune_baseline, prune_seed=prune_seed, X_pending_raw=X_pending)
+            cls = QNEHVI if isinstance(af, dm.qNEHVI) else QLogNEHVI
+            acqf = cls(self.model, self.model.X_raw, X_train, ref, a, b, S=S, sampler_seed=sampler_seed,
+                       prune_baseline=af.prune_baseline, prune_seed=prune_seed, X_pending_raw=X_pending)
         else:
-            raise NotImplementedError(f"{type(af).__name__} has no device kernel in this build "
-                                      "(qEHVI and qNEHVI do)")
+            raise NotImplementedError(f"{type(af).__name__} has no device kernel in this build")
         self.last_acqf = acqf
         return [acqf]
 

@@ -158,6 +158,11 @@ typedef struct {
    * the samples have no baseline term, y_s = mu + L22 zq_s — qEHVI, where the cells come
    * from the observed Pareto front instead of per-sample baseline draws (nb = 0). */
   int no_h;
+  /* 1: log-space scan (qLogNEHVI / qLogEHVI, fat = True): acq = logmeanexp_s logsumexp_cells
+   * sum_j fatmin(log fatplus(y_j - l_j; tau_relu), log(min(u_j, 1e10) - l_j); tau_max), dense
+   * over every cell; needs the explicit cells cell_lo / cell_hi (keys and kd groups unused). */
+  int log_hvi;
+  double tau_relu, tau_max;
 } evr_qnehvi_state;
 
 /* samples: G[s][j][c] = g_j(mu_j + h_js + L22_j zq[s][j]); aux L22: m x b; flags: m x b

@@ -191,6 +191,88 @@ class QEHVI:
         return out.mean(0)
 
 
+# ---------------------------------------------------------------------------------------
+# log-space variants (MoboStrategy's default qLogNEHVI, and qLogEHVI)
+# [upstream] botorch.acquisition.multi_objective.logei._compute_log_qehvi with fat=True and
+# botorch.utils.safe_math (fatplus, fatmax/_pareto, logmeanexp), restated: BoTorch is not
+# available offline, so these constants and forms are parity-unpinned against it.
+# ---------------------------------------------------------------------------------------
+TAU_RELU = 1e-6      # botorch.acquisition.logei.TAU_RELU
+TAU_MAX_MO = 1e-3    # qLogEHVI / qLogNEHVI default tau_max
+FAT_ALPHA = 2.0      # safe_math ALPHA (power decay of the fat max)
+UPPER_CLAMP = 1e10   # cell upper bounds clamp_max (float64)
+
+
+def fatplus(x: torch.Tensor, tau: float) -> torch.Tensor:
+    """tau * (softplus(x/tau) + 0.1 * cauchy(x/tau)), cauchy(x) = 1 / (1 + x^2)."""
+    xt = x / tau
+    return tau * (torch.nn.functional.softplus(xt) + 0.1 / (1 + xt.square()))
+
+
+def _pareto(x: torch.Tensor, alpha: float = FAT_ALPHA) -> torch.Tensor:
+    a = alpha / 2
+    b1 = 2 * a
+    b0 = a * b1
+    return b0 / (b0 + b1 * x + x.square()).pow(a)
+
+
+def fatmax(x: torch.Tensor, dim: int, tau: float, alpha: float = FAT_ALPHA) -> torch.Tensor:
+    """Fat-tailed smooth max with the +inf handling of safe_math._inf_max_helper."""
+    M = x.amax(dim=dim, keepdim=True)
+    is_inf_max = torch.isinf(M) & (M > 0)
+    y_inf = x.masked_fill(~is_inf_max, 0.0)
+    M_no_inf = M.masked_fill(is_inf_max, 0.0)
+    y_no_inf = x.masked_fill(is_inf_max, 0.0) - M_no_inf
+    fm = M_no_inf + tau * _pareto(-y_no_inf / tau, alpha).sum(dim=dim, keepdim=True).log()
+    return torch.where(is_inf_max, y_inf.sum(dim=dim, keepdim=True), fm).squeeze(dim)
+
+
+def fatmin(x: torch.Tensor, dim: int, tau: float) -> torch.Tensor:
+    return -fatmax(-x, dim=dim, tau=tau)
+
+
+def log_hvi_cells(obj: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, tau_relu: float, tau_max: float):
+    """obj: b x m (one sample, q = 1), cells lo/hi: C x m -> logsumexp over the cells of
+    sum_j fatmin(log fatplus(y_j - l_j), log(min(u_j, 1e10) - l_j)) (b)."""
+    log_imp = fatplus(obj.unsqueeze(-2) - lo, tau_relu).log()                 # b x C x m
+    log_len = (hi.clamp_max(UPPER_CLAMP) - lo).log().expand_as(log_imp)       # b x C x m
+    lm = fatmin(torch.stack([log_imp, log_len], -1), dim=-1, tau=tau_max)
+    return torch.logsumexp(lm.sum(-1), dim=-1)
+
+
+def logmeanexp(x: torch.Tensor, dim: int) -> torch.Tensor:
+    return torch.logsumexp(x, dim=dim) - math.log(x.shape[dim])
+
+
+class QLogNEHVI(QNEHVI):
+    """qLogNEHVI (q = 1): the qNEHVI samples and per-sample cells, log-space fat-smoothed HVI,
+    logmeanexp over the samples."""
+
+    def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
+        super().__init__(*args, **kw)
+        self.tau_relu, self.tau_max = tau_relu, tau_max
+
+    def forward(self, Xn: torch.Tensor) -> torch.Tensor:
+        obj = self.obj(self.samples(Xn))                                     # S x b x 1 x m
+        lse = torch.stack([log_hvi_cells(obj[s, :, 0], self.cells[s][0], self.cells[s][1], self.tau_relu,
+                                         self.tau_max) for s in range(obj.shape[0])])
+        return logmeanexp(lse, 0)
+
+
+class QLogEHVI(QEHVI):
+    """qLogEHVI (q = 1): the qEHVI samples and fixed partition, log-space fat-smoothed HVI."""
+
+    def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
+        super().__init__(*args, **kw)
+        self.tau_relu, self.tau_max = tau_relu, tau_max
+
+    def forward(self, Xn: torch.Tensor) -> torch.Tensor:
+        obj = self.obj(self.samples(Xn))[:, :, 0]                            # S x b x m
+        lse = torch.stack([log_hvi_cells(obj[s], self.cell[0], self.cell[1], self.tau_relu, self.tau_max)
+                           for s in range(obj.shape[0])])
+        return logmeanexp(lse, 0)
+
+
 def qei(models, Xn: torch.Tensor, best_f: float, z: torch.Tensor, a: float = 1.0, bconst: float = 0.0):
     """qEI restated (plain MC sampling): mean_S max_q (g(f_s) - best_f)_+.  Xn: b x q x d,
     z: S x q (base samples for the single output)."""

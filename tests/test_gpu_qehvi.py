@@ -120,13 +120,3 @@ def test_mobo_strategy_tell_ask(acqf):
     _check_candidate(bench, cand)
     assert s.last_acqf.S == 64
     assert s.last_ask_stats.raw_evals == 256
-
-
-def test_mobo_default_acqf_is_not_silently_replaced():
-    """The reference default (qLogNEHVI) has no device kernel in this build: ask() must say so
-    instead of falling back to another acquisition function."""
-    bench, exps = _dtlz2_experiments(seed=2)
-    s = strategies.map(dm.MoboStrategy(domain=bench.domain, ref_point=bench.ref_point, seed=5))
-    s.tell(exps)
-    with pytest.raises(NotImplementedError):
-        s.ask(1)

@@ -135,3 +135,33 @@ def test_qehvi_oracle_equals_exact_hv_difference():
                 ind[c] += hv_inclusion_exclusion(P2, ref) - hv0
     assert np.allclose(v, ind / 8, rtol=1e-9, atol=1e-12)   # HV differences cancel O(1) volumes
     assert (v > 0).any()
+
+
+def test_log_hvi_oracle_tends_to_log_qnehvi():
+    """The fat-smoothed log HVI restatement (qLogNEHVI / qLogEHVI) equals log(qNEHVI) /
+    log(qEHVI) as tau_relu, tau_max -> 0, and stays within 1e-5 at the defaults here."""
+    import numpy as np
+    from oracle import qnehvi as oq
+    from tests.helpers import make_problem, oracle_states
+
+    X, Y, lo, hi, hyp = make_problem(n=20, d=3, m=3, seed=2)
+    ost = oracle_states(X, Y, lo, hi, hyp)
+    a, b, ref = -np.ones(3), np.zeros(3), -1.1 * np.ones(3)
+    obj = oq.Objective(torch.tensor(a), torch.tensor(b))
+    Xn = torch.tensor((X - lo) / (hi - lo))
+    zb, zn = oq.base_samples(16, 20, 3, 7), oq.base_samples(16, 21, 3, 7)[:, 20:21]
+    Xc = torch.tensor(np.random.default_rng(0).uniform(size=(6, 1, 3)))
+    v = oq.QNEHVI(ost, Xn, obj, torch.tensor(ref), zb, zn).forward(Xc)
+    tiny = oq.QLogNEHVI(ost, Xn, obj, torch.tensor(ref), zb, zn, tau_relu=1e-12, tau_max=1e-12).forward(Xc)
+    dflt = oq.QLogNEHVI(ost, Xn, obj, torch.tensor(ref), zb, zn).forward(Xc)
+    assert torch.allclose(tiny, v.log(), rtol=1e-10, atol=1e-10)
+    assert torch.allclose(dflt, v.log(), rtol=1e-5, atol=1e-5)
+    z = oq.base_samples(16, 1, 3, 5)
+    e = oq.QEHVI(ost, torch.tensor(Y * a + b), obj, torch.tensor(ref), z).forward(Xc)
+    le = oq.QLogEHVI(ost, torch.tensor(Y * a + b), obj, torch.tensor(ref), z, tau_relu=1e-12,
+                     tau_max=1e-12).forward(Xc)
+    assert torch.allclose(le, e.log(), rtol=1e-10, atol=1e-10)
+    # fat tails: a candidate with zero HVI in every sample still gets a finite value
+    far = torch.full((1, 1, 3), 1.0)
+    lv = oq.QLogNEHVI(ost, Xn, obj, torch.tensor(ref), zb, zn).forward(far)
+    assert torch.isfinite(lv).all()

@@ -20,12 +20,14 @@ def main():
                                                                    keys=acqf.cells.keys, pts=acqf.cells.pts,
                                                                    rank0=acqf.cells.rank0, stride=acqf.cells.stride))
     out = {"box_path": acqf.box_path}
-    for b in (20, 64, 128, 512, 1024):
+    sizes = [int(v) for v in os.environ.get("HVI_SIZES", "20,64,128,512,1024").split(",")]
+    variants = (("kd", acqf.state),) if os.environ.get("HVI_ONLY_KD") else (("kd", acqf.state), ("tiled", dense_state))
+    for b in sizes:
         Xc = bench.candidates(b, 6, seed=2, device=dev)
         R = ops.gemm(acqf.M, gp.cross(Xc))
         G, L22, flags = ops.qnehvi_samples(acqf.state, R, b)
         row = {}
-        for name, st in (("kd", acqf.state), ("tiled", dense_state)):
+        for name, st in variants:
             for _ in range(3):
                 ops.hvi_forward_backward(st, G, b, flags)
             torch.cuda.synchronize()
@@ -38,8 +40,10 @@ def main():
             torch.cuda.synchronize()
             row[name + "_ms"] = round(e0.elapsed_time(e1) / reps, 4)
             row[name + "_acq"] = a
-        row["max_rel_diff"] = float(((row["kd_acq"] - row["tiled_acq"]).abs() / row["tiled_acq"].abs().clamp_min(1e-12)).max())
-        del row["kd_acq"], row["tiled_acq"]
+        if "tiled_acq" in row:
+            row["max_rel_diff"] = float(((row["kd_acq"] - row["tiled_acq"]).abs() / row["tiled_acq"].abs().clamp_min(1e-12)).max())
+            del row["tiled_acq"]
+        row["acq_sum"] = float(row.pop("kd_acq").sum())
         out[f"b{b}"] = row
     print(json.dumps(out))
 
