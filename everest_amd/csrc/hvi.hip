@@ -731,6 +731,344 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// hvi_kd2 — the same sparse scan as hvi_kd (same groups, cells and terms, same pair and term
+// order, same segmented sums: bitwise identical results) with a shorter instruction stream:
+//   * chunk pre-filter: the minimum corner of every 16-group chunk (formed while staging)
+//     rejects a (candidate, chunk) entry with one packed test; the surviving entries are
+//     compacted by ballot and their 16 group tests run lane-dense, instead of every lane
+//     walking the 16 groups of every chunk;
+//   * owner lookups by marks: the pair -> entry map of the cell filter and the term -> pair
+//     map of the evaluation are built by writing each source's first slot into a 64-entry
+//     LDS row and taking a DPP max-scan (one LDS round trip + 6 DPP steps) instead of a
+//     binary search of 6-9 dependent LDS reads per lane; the owner's fields then come over
+//     ds_bpermute from its registers.
+// ---------------------------------------------------------------------------------------
+constexpr int KD_MAX_NQ = 32;   // 16-group chunks per sample (cells_kd keeps <= 512 groups)
+
+__device__ __forceinline__ unsigned int pk_min_u16(unsigned int a, unsigned int b) {
+  return min(a & 0xFFFFu, b & 0xFFFFu) | (min(a >> 16, b >> 16) << 16);
+}
+
+// group / chunk test: every objective's minimum rank below the candidate's threshold
+__device__ __forceinline__ bool kd_pass4(const uint4 v, const uint4 t) {
+  const unsigned int x = kd_lt16(v.x, t.x) & kd_lt16(v.y, t.y) & kd_lt16(v.z, t.z) & kd_lt16(v.w, t.w);
+  return (x & 0x80008000u) == 0x80008000u;
+}
+
+// wave-wide inclusive max-scan on DPP moves (lanes without a source see -1)
+__device__ __forceinline__ int wave_max_incl(int x) {
+  x = max(x, dpp_i32<0x111, 0xF>(-1, x));
+  x = max(x, dpp_i32<0x112, 0xF>(-1, x));
+  x = max(x, dpp_i32<0x114, 0xF>(-1, x));
+  x = max(x, dpp_i32<0x118, 0xF>(-1, x));
+  x = max(x, dpp_i32<0x142, 0xA>(-1, x));
+  x = max(x, dpp_i32<0x143, 0xC>(-1, x));
+  return x;
+}
+
+template <int M, bool BWD>
+__global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
+                                               const int* __restrict__ thg, HviKd kd,
+                                               const double* __restrict__ gout, double* __restrict__ part,
+                                               double* __restrict__ dG) {
+  constexpr int NV = BWD ? M + 1 : 1;
+  constexpr int CW = KD_CT / 4;            // candidates per wave
+  using K = CellKey<M>;
+  extern __shared__ __align__(16) unsigned char kd_dyn[];
+  __shared__ double yv[KD_CT][M];
+  __shared__ uint4 thp[KD_CT];             // packed 16-bit thresholds (objectives >= M: 1)
+  __shared__ double acc[KD_CT][NV];
+  __shared__ uint4 cmin[KD_MAX_NQ];        // chunk minimum corners
+  __shared__ int mkB[4][64], mkC[4][64];   // per-wave owner marks (cell filter / evaluation)
+  int s, tile;
+  {
+    const int L = blockIdx.x + ntiles * blockIdx.y;
+    if ((S & 7) == 0) {
+      const int xcd = L & 7, k = L >> 3;
+      s = xcd + 8 * (k / ntiles);
+      tile = k % ntiles;
+    } else {
+      s = blockIdx.y;
+      tile = blockIdx.x;
+    }
+  }
+  const int c0 = tile * KD_CT, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int stride = kd.stride;
+  KD_T0();
+  const int split = blockIdx.z;
+  const int NQall = (kd.goff[s + 1] - kd.goff[s] + 15) >> 4;
+  const int qper = (NQall + nsplit - 1) / nsplit;
+  const int q0 = min(NQall, split * qper);
+  const int NQ = min(NQall, q0 + qper) - q0;                 // this workgroup's 16-group chunks
+  const int gbase = kd.goff[s] + 16 * q0;
+  const int Gs = min(kd.goff[s + 1] - gbase, 16 * NQ);
+  const KdLds Lo = kd_lds(stride, M, kd.max_groups);
+  double* pt = (double*)(kd_dyn + Lo.pt);
+  int* r0 = (int*)(kd_dyn + Lo.r0);
+  uint4* gb = (uint4*)(kd_dyn + Lo.gb);
+  unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
+  int* pA = (int*)(kd_dyn + Lo.pA) + wave * (CW * NQ + 1);   // this wave's prefix array
+
+  kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
+  kd_stage(r0, kd.rank0 + (size_t)s * stride, stride);
+  if (Gs > 0) kd_stage(gb, (const uint4*)kd.gbox + gbase, Gs);
+  for (int q = tid; q < NQ; q += 256) {    // chunk minima from the same (L2-resident) bytes
+    const uint4* src = (const uint4*)kd.gbox + gbase + 16 * q;
+    const int gend = min(16, Gs - 16 * q);
+    uint4 mn = src[0];
+    for (int k = 1; k < gend; ++k) {
+      const uint4 v = src[k];
+      mn.x = pk_min_u16(mn.x, v.x);
+      mn.y = pk_min_u16(mn.y, v.y);
+      mn.z = pk_min_u16(mn.z, v.z);
+      mn.w = pk_min_u16(mn.w, v.w);
+    }
+    cmin[q] = mn;
+  }
+  for (int e = tid; e < KD_CT * M; e += 256) {
+    const int j = e / KD_CT, c = e - j * KD_CT;
+    yv[c][j] = (c0 + c < b) ? G[((size_t)s * M + j) * b + c0 + c] : -INFINITY;
+  }
+  if (tid < KD_CT) {
+    const bool in = c0 + tid < b;
+    unsigned int w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      unsigned int v = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * q + h;
+        const unsigned int t = (j < M) ? (in ? (unsigned int)thg[((size_t)s * M + j) * b + c0 + tid] : 0u) : 1u;
+        v |= t << (16 * h);
+      }
+      w[q] = v;
+    }
+    thp[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (int e = tid; e < KD_CT * NV; e += 256) (&acc[0][0])[e] = 0.0;
+  __syncthreads();
+  KD_T(0);
+  const int cbase = wave * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
+  if (c0 + cbase >= b) return;
+  const int NE = CW * NQ;
+
+  // ---- A: chunk pre-filter (lane = (chunk, candidate) entry), ballot compaction of the
+  //      surviving entries, then their 16 group tests lane-dense ----
+  {
+    unsigned short* ent = (unsigned short*)pA;   // entry list (pA is rewritten by the prefix)
+    int nent = 0;
+    for (int eb = 0; eb < NE; eb += 64) {
+      const int e = eb + lane, q = e >> 4, cl = e & 15;
+      bool pass = false;
+      if (e < NE) {
+        mA[q * KD_CT + cbase + cl] = 0;
+        pass = kd_pass4(cmin[q], thp[cbase + cl]);
+      }
+      const unsigned long long bal = __ballot(pass);
+      if (pass) ent[nent + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)e;
+      nent += __popcll(bal);
+    }
+    wave_sync();
+    for (int i = lane; i < nent; i += 64) {
+      const int e = ent[i], q = e >> 4, cl = e & 15;
+      const uint4 t = thp[cbase + cl];
+      const int gend = min(16, Gs - q * 16);
+      unsigned int mask = 0;
+      for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], t) << k;
+      mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
+    }
+    if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
+  }
+  wave_sync();
+  // candidate-major prefix over the entries e = cl * NQ + q (a candidate's pairs contiguous);
+  // each lane keeps the prefixes of its <= 8 entries in registers for the window marks
+  const int per = (NE + 63) >> 6;                             // <= 8 (NQ <= KD_MAX_NQ)
+  const int e0 = min(NE, lane * per), e1 = min(NE, e0 + per);
+  // e / NQ = (e * magic) >> 16, exact for e <= 16 * KD_MAX_NQ
+  const unsigned int nq_magic = NQ > 0 ? (65536u + (unsigned int)NQ - 1u) / (unsigned int)NQ : 0u;
+  int PA;
+  int preE[9];
+  {
+    int cl = (int)(((unsigned int)e0 * nq_magic) >> 16), q = e0 - cl * NQ;
+    int cnt[8];
+    int loc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cnt[k] = 0;
+      if (e0 + k < e1) {
+        cnt[k] = __popc(mA[q * KD_CT + cbase + cl]);
+        if (++q == NQ) q = 0, ++cl;
+      }
+      loc += cnt[k];
+    }
+    int run = wave_scan_excl(loc, &PA);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      preE[k] = run;
+      if (e0 + k < e1) pA[e0 + k] = run;
+      run += cnt[k];
+    }
+    preE[8] = run;
+    if (lane == 0) {
+      pA[NE] = PA;
+      if (kd.counters) {
+        atomicAdd(kd.counters + 0, (unsigned long long)PA);
+        atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - c0 - cbase, CW)) * Gs);
+      }
+    }
+  }
+  wave_sync();
+  KD_T(1);
+
+  int* mb = mkB[wave];
+  int* mc = mkC[wave];
+  int carryB = -1;
+  for (int wb = 0; wb < PA; wb += 64) {
+    // ---- B: pair -> entry by marks, then the cell filter (lane = passing pair) ----
+    mb[lane] = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (preE[k + 1] > preE[k] && preE[k] >= wb && preE[k] < wb + 64) mb[preE[k] - wb] = e0 + k;
+    wave_sync();
+    const int ownB = max(wave_max_incl(mb[lane]), carryB);
+    carryB = __builtin_amdgcn_readlane(ownB, 63);
+    const int p = wb + lane;
+    unsigned int mB = 0;
+    int cg = 0;
+    if (p < PA) {
+      const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = ownB - cl * NQ;
+      const int c = cbase + cl;
+      const int g = q * 16 + kth_bit16(mA[q * KD_CT + c], p - pA[ownB]);
+      const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
+      const uint4 tq = thp[c];
+      const unsigned int tw[4] = {tq.x, tq.y, tq.z, tq.w};
+      unsigned int a[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = 0xFFFFFFFFu;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        const unsigned int tt = th16 | (th16 << 16);
+        const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+        a[0] &= kd_lt16(r1.x, tt);
+        a[1] &= kd_lt16(r1.y, tt);
+        a[2] &= kd_lt16(r1.z, tt);
+        a[3] &= kd_lt16(r1.w, tt);
+        a[4] &= kd_lt16(r2.x, tt);
+        a[5] &= kd_lt16(r2.y, tt);
+        a[6] &= kd_lt16(r2.z, tt);
+        a[7] &= kd_lt16(r2.w, tt);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mB |= (((a[i] >> 15) & 1u) | ((a[i] >> 30) & 2u)) << (2 * i);
+      cg = (c << 16) | g;
+    }
+    const int cntB = __popc(mB);
+    int EW;
+    const int pre = wave_scan_excl(cntB, &EW);
+    KD_T(2);
+    if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
+    // ---- C: term -> pair by marks (software-pipelined: the next round's owner and key
+    //      load are issued before the current round is evaluated) ----
+    int carryC = -1;
+    auto locate = [&](int cb, int& c, unsigned long long& key) {
+      mc[lane] = -1;
+      if (cntB > 0 && pre >= cb && pre < cb + 64) mc[pre - cb] = lane;
+      wave_sync();
+      const int o = max(wave_max_incl(mc[lane]), carryC);
+      carryC = __builtin_amdgcn_readlane(o, 63);
+      const int cgo = __shfl(cg, o, 64);
+      const int mo = __shfl((int)mB, o, 64);
+      const int po = __shfl(pre, o, 64);
+      wave_sync();
+      c = -1;
+      if (cb + lane < EW) {
+        c = cgo >> 16;
+        key = kd.gkeys[(size_t)(gbase + (cgo & 0xFFFF)) * 16 + kth_bit16((unsigned int)mo, cb + lane - po)];
+      }
+    };
+    int cnext = -1;
+    unsigned long long knext = 0;
+    if (EW > 0) locate(0, cnext, knext);
+    for (int cb = 0; cb < EW; cb += 64) {
+      const int c = cnext;
+      const unsigned long long key = knext;
+      if (cb + 64 < EW) locate(cb + 64, cnext, knext);
+      int rcv = -1;
+      double val[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) val[v] = 0.0;
+      if (c >= 0) {
+        double l[M], u[M];
+        K::decode(key, pt, r0, l, u);
+        double y[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) y[j] = yv[c][j];
+        if (!BWD) {
+          double prod = fmax(fmin(y[0], u[0]) - l[0], 0.0);
+#pragma unroll
+          for (int j = 1; j < M; ++j) prod *= fmax(fmin(y[j], u[j]) - l[j], 0.0);
+          val[0] = prod;
+        } else {
+          double len[M], pass[M];
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            const double raw = fmin(y[j], u[j]) - l[j];
+            len[j] = fmax(raw, 0.0);
+            const double dmin = (y[j] < u[j]) ? 1.0 : ((y[j] == u[j]) ? 0.5 : 0.0);
+            pass[j] = (raw >= 0.0) ? dmin : 0.0;
+          }
+          double pre_[M];
+          pre_[0] = 1.0;
+#pragma unroll
+          for (int j = 1; j < M; ++j) pre_[j] = pre_[j - 1] * len[j - 1];
+          val[0] = pre_[M - 1] * len[M - 1];
+          double suf = 1.0;
+#pragma unroll
+          for (int j = M - 1; j >= 0; --j) {
+            val[NV > 1 ? 1 + j : 0] = pass[j] * pre_[j] * suf;
+            suf *= len[j];
+          }
+        }
+        rcv = c;
+      }
+      KD_T(3);
+      seg_scan_wave<NV>(rcv, val);
+      const int rnext = __shfl_down(rcv, 1, 64);
+      if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[rcv][v] += val[v];
+      }
+      KD_T(4);
+    }
+    wave_sync();   // mb / mc are rewritten by the next window
+  }
+  wave_sync();
+  const size_t ss = (size_t)s * nsplit + split;
+  if (lane < CW && c0 + cbase + lane < b) part[ss * b + c0 + cbase + lane] = acc[cbase + lane][0];
+  if (BWD) {
+    for (int e = lane; e < CW * M; e += 64) {
+      const int j = e / CW, cl = e - j * CW, c = cbase + cl;
+      if (c0 + c >= b) continue;
+      const double v = acc[c][NV > 1 ? 1 + j : 0];
+      if (nsplit == 1) dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * v;
+      else dG[(ss * M + j) * b + c0 + c] = v;
+    }
+  }
+}
+
+// scan variant: 2 = hvi_kd2 (default), 1 = hvi_kd (EVR_KD=1 or evr_hvi_set_kd_variant)
+static int g_kd_variant = 0;
+static int kd_variant() {
+  if (g_kd_variant == 0) {
+    const char* e = std::getenv("EVR_KD");
+    g_kd_variant = (e && std::atoi(e) == 1) ? 1 : 2;
+  }
+  return g_kd_variant;
+}
+
 struct HviPlan {
   int tgb, bb, ctiles, nchunk, cb;
 };
@@ -803,11 +1141,20 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
   hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(b, M, st->pts_stride, G,
                                                                                      st->sorted_lo, th);
   EVR_LAUNCH_CHECK();
-  EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)Lo.bytes));
   dim3 grid(ntiles, st->S, ns);
-  hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
-                                               ns > 1 ? dgp : dG);
+  if (kd_variant() == 1) {
+    EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)Lo.bytes));
+    hvi_kd<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
+                                                 ns > 1 ? dgp : dG);
+  } else {
+    EVR_CHECK((st->max_groups + 15) / 16 <= KD_MAX_NQ, "hvi: %d kd groups per sample exceed the scan's %d",
+              st->max_groups, 16 * KD_MAX_NQ);
+    EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd2<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)Lo.bytes));
+    hvi_kd2<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
+                                                  ns > 1 ? dgp : dG);
+  }
   EVR_LAUNCH_CHECK();
   if (acq) {
     hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, ns, b, M, part, flags, acq);
@@ -950,6 +1297,12 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
                      double* work, double* dG) {
   return evr_hvi_forward_backward(stream, st, b, G, nullptr, gout, work, nullptr, dG);
+}
+
+int evr_hvi_set_kd_variant(int variant) {
+  EVR_CHECK(variant == 1 || variant == 2, "evr_hvi_set_kd_variant: variant must be 1 or 2, got %d", variant);
+  g_kd_variant = variant;
+  return 0;
 }
 
 }  // extern "C"

@@ -152,7 +152,8 @@ typedef struct {
   const double* sorted_lo;             /* S x m x pts_stride ascending lower-bound values */
   int max_groups;                      /* max_s (grp_off[s+1] - grp_off[s]) */
   /* optional scan statistics (nullable, device): [0] += passing (candidate, group) pairs,
-   * [1] += exact (cell, candidate) terms evaluated, [2] += (candidate, group) tests */
+   * [1] += exact (cell, candidate) terms evaluated, [2] += (candidate, group) tests,
+   * [3] += (candidate, 16-group chunk) entries passing the chunk pre-filter (hvi_kd2) */
   unsigned long long* scan_counters;
   /* 0: M = [Linv; G; H^T; alpha^T] (qNEHVI).  1: M carries no H^T rows (Rr = n + nb + 1) and
    * the samples have no baseline term, y_s = mu + L22 zq_s — qEHVI, where the cells come
@@ -186,6 +187,11 @@ int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const doub
 int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
                              const int* flags, const double* gout, double* work, double* acq,
                              double* dG);
+/* Sparse-scan kernel for kd-grouped cells: 2 = hvi_kd2 (default: chunk pre-filter, mark-based
+ * owner lookups), 1 = hvi_kd (the earlier kernel; also selected by EVR_KD=1).  Both give
+ * bitwise identical results; the switch exists for A/B timing and the parity test.  Plans
+ * keep the kernel they were captured with.  Process-global, not thread-safe. */
+int evr_hvi_set_kd_variant(int variant);
 /* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);

@@ -55,6 +55,62 @@ def test_kd_scan_gout_and_sample_grad():
     assert torch.allclose(d1, d2, rtol=1e-10, atol=1e-14)
 
 
+@pytest.fixture
+def kd_variant():
+    """Select the sparse-scan kernel (evr_hvi_set_kd_variant) and restore the default."""
+    from everest_amd import _native
+
+    lib = _native.load()
+    yield lambda v: _native.check(lib.evr_hvi_set_kd_variant(v), "evr_hvi_set_kd_variant")
+    lib.evr_hvi_set_kd_variant(2)
+
+
+@pytest.mark.parametrize("n,d,m,S,b", [(200, 6, 5, 128, 200), (60, 4, 3, 32, 65), (40, 3, 2, 16, 1),
+                                       (120, 6, 5, 64, 20)])
+def test_kd2_bitwise_equals_kd(kd_variant, n, d, m, S, b):
+    """hvi_kd2 (chunk pre-filter + mark-based owner lookups) visits the same pairs and terms
+    in the same order as hvi_kd: forward and fused forward+backward are bitwise equal."""
+    from everest_amd import ops
+
+    kd, dense, lo, hi, d = _pair(n, d, m, S, seed=n + 3 * m)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b + 1).uniform(size=(b, d)), device="cuda")
+    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
+    G, L22, flags = ops.qnehvi_samples_norms(kd.state, R, P, b)
+    out = {}
+    for v in (1, 2):
+        kd_variant(v)
+        a, g = ops.hvi_forward_backward(kd.state, G, b, flags)
+        out[v] = (a, g, ops.hvi_forward(kd.state, G, b, flags))
+    assert all(torch.equal(x, y) for x, y in zip(out[1], out[2]))
+    assert torch.isfinite(out[2][0]).all() and (out[2][0] >= 0).all()
+
+
+def test_kd2_bench_size_matches_tiled_scan():
+    """BASELINE configs[2] size (DTLZ2 n=512, d=6, m=5, S=256, b=512): the sparse scan equals
+    the tiled dense scan over the same compressed cells, and repeats bitwise."""
+    import bench
+    from everest_amd import ops
+
+    dev = torch.device("cuda", 0)
+    X, Y, gp, hypers, acqf, _, _ = bench.build_state(512, 6, 5, 256, dev)
+    assert acqf.box_path == "device+kd"
+    dense = ops.make_state(acqf.n, acqf.nb, acqf.S, acqf.m, gp.const, gp.ym, gp.ys, gp.kxx, acqf.zq, acqf.obj_a,
+                           acqf.obj_b, ops.Cells(acqf.cells.off, acqf.cells.counts, acqf.m, keys=acqf.cells.keys,
+                                                 pts=acqf.cells.pts, rank0=acqf.cells.rank0,
+                                                 stride=acqf.cells.stride))
+    b = 512
+    Xc = bench.candidates(b, 6, seed=2, device=dev)
+    R, P = ops.qnehvi_project(acqf.state, acqf.M, gp.cross(Xc), b)
+    G, L22, flags = ops.qnehvi_samples_norms(acqf.state, R, P, b)
+    a1, g1 = ops.hvi_forward_backward(acqf.state, G, b, flags)
+    a2, g2 = ops.hvi_forward_backward(dense, G, b, flags)
+    assert torch.allclose(a1, a2, rtol=1e-12, atol=1e-15)
+    assert torch.allclose(g1, g2, rtol=1e-10, atol=1e-13)
+    a3, g3 = ops.hvi_forward_backward(acqf.state, G, b, flags)
+    assert torch.equal(a1, a3) and torch.equal(g1, g3)
+    assert (a1 > 0).sum() > b // 2
+
+
 def test_kd_index_invariants():
     from everest_amd import ops
 
