@@ -79,49 +79,59 @@ def candidates(b: int, d: int, seed: int, device):
     return eng.draw(b, dtype=torch.float64).to(device)
 
 
-class KernelTimer:
-    """HIP events on torch's current stream (the stream every everest_amd op launches on)."""
-
-    def __init__(self):
-        self.ev = {}
-
-    def start(self, name):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        return (name, e0)
-
-    def stop(self, tok):
-        name, e0 = tok
-        e1 = torch.cuda.Event(enable_timing=True)
-        e1.record()
-        self.ev.setdefault(name, []).append((e0, e1))
-
-    def summary(self):
-        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in self.ev.items()}
-
-
-def step(acqf, Xc, timer=None):
-    """One evaluation pass: forward + backward over the candidate batch (instrumented)."""
+def op_chain(acqf, Xc):
+    """The evaluation chain op by op (the kernels the native plan runs), as closures over
+    fixed inputs so that each op can be launched repeatedly (idempotent)."""
     from everest_amd import ops
 
-    st = acqf.state
-    b = Xc.shape[0]
-    gp = acqf.gp
-    T = timer
-    tk = T.start("kernel_matrix") if T else None
+    st, gp, b = acqf.state, acqf.gp, Xc.shape[0]
     Kx = gp.cross(Xc)
-    if T: T.stop(tk); tk = T.start("proj_fwd")
     R, P = ops.qnehvi_project(st, acqf.M, Kx, b)
-    if T: T.stop(tk); tk = T.start("samples")
     G, L22, flags = ops.qnehvi_samples_norms(st, R, P, b)
-    if T: T.stop(tk); tk = T.start("hvi_fwd_bwd")
     acq, dG = ops.hvi_forward_backward(st, G, b, flags)
-    if T: T.stop(tk); tk = T.start("proj_bwd")
     dKx = ops.qnehvi_project_backward(st, acqf.M, R, L22, dG, b)
-    if T: T.stop(tk); tk = T.start("kernel_grad")
-    dX = ops.kernel_cross_grad(gp.Xn, Xc, gp.ls, dKx, gp.kind, shift2=gp.lo, scale2=gp.inv_range)
-    if T: T.stop(tk)
-    return acq, dX
+    return {
+        "kernel_matrix": lambda: gp.cross(Xc),
+        "proj_fwd": lambda: ops.qnehvi_project(st, acqf.M, Kx, b),
+        "samples": lambda: ops.qnehvi_samples_norms(st, R, P, b),
+        "hvi_fwd_bwd": lambda: ops.hvi_forward_backward(st, G, b, flags),
+        "proj_bwd": lambda: ops.qnehvi_project_backward(st, acqf.M, R, L22, dG, b),
+        "kernel_grad": lambda: ops.kernel_cross_grad(gp.Xn, Xc, gp.ls, dKx, gp.kind, shift2=gp.lo,
+                                                     scale2=gp.inv_range),
+    }
+
+
+def kernel_times(acqf, Xc, reps=10):
+    """Average device time (ms) of each op of the chain: ``reps`` launches of the op are
+    captured into one HIP graph on torch's current stream (the stream every evr_* call is
+    enqueued on) and the replay is bracketed by HIP events, so the figure is the kernels'
+    back-to-back duration, free of host enqueue gaps (it agrees with rocprofv3's per-kernel
+    averages).  Falls back to eager launches between events if capture is refused."""
+    out, how = {}, "hip-graph replay"
+    for name, f in op_chain(acqf, Xc).items():
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    f()
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            g.replay()
+            e1.record()
+        except RuntimeError:
+            how = "eager launches"
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(reps):
+                f()
+            e1.record()
+        torch.cuda.synchronize()
+        out[name] = e0.elapsed_time(e1) / reps
+    return out, how
 
 
 def scan_counts(acqf, Xc):
@@ -202,7 +212,58 @@ def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, chunk=8, budget_s=15.0):
         spent += time.perf_counter() - t0
         done += chunk
         i += 1
-    return spent, done
+    return spent, done, orc, states
+
+
+def cpu_ask_estimate(orc, states, acqf, Xc_cpu, ask, prune_sub=128, prune_samples=2048, box_samples=2):
+    """Reference-structure CPU ``QnehviStrategy.ask()`` wall time for the ask that was timed
+    on the GPU (same problem, same raw-sample and restart counts, the GPU ask's optimiser
+    evaluation count), composed from bounded samples of each phase with the oracle
+    (torch-CPU fp64, BoTorch's computation shape):
+      * prune_baseline over ``prune_sub`` of the ``prune_samples`` posterior draws (x ratio);
+      * the per-sample box decomposition of ``box_samples`` MC samples (x S);
+      * raw screening: forward-only in chunks of batch_limit (= restarts, BoFire's default),
+        two chunks timed, scaled to raw_samples;
+      * restarts: one joint forward+backward of ``restarts`` candidates (one L-BFGS-B
+        function evaluation), scaled to the GPU ask's evaluation count.
+    Returns a dict (seconds per phase, total, and the ask speedup)."""
+    from oracle import qnehvi as oq
+    from oracle.multiobjective import nondominated_cells, pareto_above_ref
+
+    out = {}
+    n, m = orc.models[0].X.shape[0], len(states)
+    Xn = orc.models[0].X
+    z = oq.base_samples(prune_sub, n, m, 7)
+    t0 = time.perf_counter()
+    oq.prune_baseline(states, Xn, orc.obj, orc.ref, z)
+    out["prune_s"] = (time.perf_counter() - t0) * prune_samples / prune_sub
+    zb = oq.base_samples(box_samples, orc.Xb.shape[0], m, 11)
+    mean_b, _ = oq.joint_posterior(states, orc.Xb)
+    obj_b = orc.obj(mean_b.unsqueeze(0) + torch.einsum("jik,skj->sij", orc.L_base, zb))
+    t0 = time.perf_counter()
+    for s in range(box_samples):
+        nondominated_cells(pareto_above_ref(obj_b[s], orc.ref), orc.ref)
+    out["box_decomposition_s"] = (time.perf_counter() - t0) * acqf.S / box_samples
+    r = ask["restarts"]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for k in range(2):
+            orc.forward(Xc_cpu[k * r:(k + 1) * r].unsqueeze(1))
+    out["raw_screening_s"] = (time.perf_counter() - t0) / (2 * r) * ask["raw_samples"]
+    x = Xc_cpu[:r].clone().requires_grad_(True)
+    t0 = time.perf_counter()
+    orc.forward(x.unsqueeze(1)).sum().backward()
+    opt_evals = ask["evals"] - ask["raw_samples"]
+    out["restarts_s"] = (time.perf_counter() - t0) / r * opt_evals
+    tot = sum(out.values())
+    out = {k: round(v, 2) for k, v in out.items()}
+    out["total_s"] = round(tot, 2)
+    out["gpu_ask_s"] = ask["ask_s"]
+    out["ask_speedup"] = round(tot / ask["ask_s"], 1)
+    out["sample"] = (f"prune {prune_sub}/{prune_samples} draws, box decomposition {box_samples}/{acqf.S} samples, "
+                     f"raw screening 2 chunks of {r}, one joint forward+backward of {r} restarts; "
+                     f"{opt_evals} optimiser evaluations from the GPU ask")
+    return out
 
 
 def _traffic(path, kernel):
@@ -285,12 +346,9 @@ def main():
     plan = acqf.plan(args.b, True)
     plan.X.copy_(Xc)
 
-    def one_step(timer=None):
-        if timer is None:
-            plan.run()
-            acq = plan.acq
-        else:                       # instrumented op-by-op chain (same kernels) for the breakdown
-            acq, _ = step(acqf, Xc, timer)
+    def one_step():
+        plan.run()
+        acq = plan.acq
         if dist is not None:
             dist.all_gather(gathered, acq)
         return acq
@@ -314,12 +372,8 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * args.b * args.steps / dt
 
-    # per-kernel device time (separate instrumented pass, events on the launch stream)
-    timer = KernelTimer()
-    for _ in range(max(5, args.steps // 2)):
-        one_step(timer)
-    torch.cuda.synchronize()
-    ktimes = timer.summary()
+    # per-kernel device time: each op of the same chain, graph-replayed between HIP events
+    ktimes, ktimes_how = kernel_times(acqf, Xc)
 
     if rank == 0:
         st = acqf.stats
@@ -336,7 +390,9 @@ def main():
             "kernel_matrix": ("hbm", 8.0 * (m * n * b + n * d + b * d + m * d), "B"),
             "proj_fwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
             "samples": ("hbm", 8.0 * m * b * (args.S + 1 + 2 * nrt) + 8.0 * args.S * m * b, "B"),
-            "hvi_fwd_bwd": ("valu", float(hvi_useful), "flop"),
+            # scan bytes with every cell read once per forward (explicit
+            # [lo, hi] rows, 16 m B per cell) + the samples + the output
+            "hvi_fwd_bwd": ("hbm", 16.0 * sum_cells * m + 8.0 * b * args.S * m + 8.0 * b, "B"),
             "proj_bwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
             "kernel_grad": ("hbm", 8.0 * (m * n * b + n * d + b * d), "B"),
         }
@@ -363,14 +419,19 @@ def main():
                 roof["traffic"] = tr["bytes_per_launch"]
                 roof["traffic_source"] = tr["source"]
         if "hvi_fwd_bwd" in kernels:
+            t = ktimes["hvi_fwd_bwd"] * 1e-3
+            kernels["hvi_fwd_bwd"]["valu_useful"] = {
+                "achieved": round(hvi_useful / t / 1e12, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(hvi_useful / t / 1e12 / PEAK_FP64_TFLOPS, 4), "work_per_launch": float(hvi_useful),
+                "note": "(6m+2) flop per evaluated (cell, candidate) term, device-counted"}
             kernels["hvi_fwd_bwd"]["scan"] = {
                 "dense_pairs": b * sum_cells, "group_tests": counts["group_tests"], "group_pairs": counts["group_pairs"],
                 "terms": counts["terms"],
                 "dense_equivalent_TFLOPs": round(b * sum_cells * (6 * m + 2) / (ktimes["hvi_fwd_bwd"] * 1e-3) / 1e12, 2)}
-        cpu = None
-        if not args.no_cpu_baseline:
+        cpu = orc = None
+        if not args.no_cpu_baseline and world == 1:
             torch.set_num_threads(min(16, os.cpu_count() or 1))
-            t_cpu, nc = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
+            t_cpu, nc, orc, ostates = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
             cpu = {"value": round(nc / t_cpu, 3), "unit": "candidates/s", "cores": torch.get_num_threads(),
                    "kind": "port", "sample": f"oracle reference-structure forward+backward over the first {nc} "
                    f"of the same {b} candidates in chunks of 8 (batch_limit), same state (n={args.n}, "
@@ -378,6 +439,8 @@ def main():
         ask = None
         if world == 1 and not args.no_ask:
             ask = ask_throughput(args.n, args.S)
+            if orc is not None:
+                cpu["ask_estimate"] = cpu_ask_estimate(orc, ostates, acqf, Xc.cpu(), ask)
         out = {
             "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
             "value": round(value, 2),
@@ -400,6 +463,7 @@ def main():
             "cpu_baseline": cpu,
             "gp_posterior_ms": round(gp_posterior_ms(device), 4),
             "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},
+            "kernel_ms_method": f"{ktimes_how} of 10 launches per op between HIP events (torch current stream)",
             "setup_s": {"gp_fit": round(t_fit, 3), "qnehvi_build": round(t_build, 3)},
             "ask": ask,
         }

@@ -510,6 +510,8 @@ __global__ __launch_bounds__(1024) void posterior_finalize_kernel(int B, int n, 
 
 int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA, const double* B,
             int ldb, long long sB, double* C, int ldc, long long sC, int batch);
+int rb_gemv_rows(hipStream_t s, int N, int K, const double* X, long long sX, const double* a, long long sa,
+                 double* y, long long sy, int batch);
 int gemm_backend_init();
 
 }  // namespace evr
@@ -649,8 +651,13 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
                                  nullptr, nullptr, Kx))
     return rc;
   if (int rc = gemm_backend_init()) return rc;
-  if (int rc = rb_gemm(s, false, n + 1, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
+  // [L^-1; alpha^T] K*: the GEMM over the n rows of L^-1 and the mean row alpha^T K* by a
+  // gemv — the (n + 1)-th row alone would add a whole row of 64-row tiles to the GEMM grid
+  if (int rc = rb_gemm(s, false, n, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
                        (long long)(n + 1) * nt, B))
+    return rc;
+  if (int rc = rb_gemv_rows(s, nt, n, Kx, (long long)n * nt, M + (size_t)n * n, (long long)(n + 1) * n,
+                            R + (size_t)n * nt, (long long)(n + 1) * nt, B))
     return rc;
   return evr_gp_posterior_finalize(stream, B, n, nt, R, c, ym, ys, kxx, noise_add, mean, var);
 }

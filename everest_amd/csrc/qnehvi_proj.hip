@@ -436,6 +436,19 @@ int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int ld
   return 0;
 }
 
+// row-major y_i = sum_k X[k][i] a[k] (X: K x N, ld N), batched: the column-major gemv y = X a
+int rb_gemv_rows(hipStream_t s, int N, int K, const double* X, long long sX, const double* a, long long sa,
+                        double* y, long long sy, int batch) {
+  rocblas_handle h = rb_handle();
+  EVR_CHECK(h, "rocBLAS handle creation failed");
+  EVR_CHECK(rocblas_set_stream(h, s) == rocblas_status_success, "rocblas_set_stream failed");
+  const double one = 1.0, zero = 0.0;
+  const rocblas_status st = rocblas_dgemv_strided_batched(h, rocblas_operation_none, N, K, &one, X, N, sX, a, 1, sa,
+                                                          &zero, y, 1, sy, batch);
+  EVR_CHECK(st == rocblas_status_success, "rocblas_dgemv_strided_batched failed (%d)", (int)st);
+  return 0;
+}
+
 int gemm_backend_init() {
   if (use_rocblas()) EVR_CHECK(rb_handle(), "rocBLAS handle creation failed");
   return 0;
@@ -456,8 +469,15 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
   const int Rr = qn_rows(st);
   const int nrt = cdiv(Rr, PT);
   if (use_rocblas()) {
-    if (int rc = rb_gemm(s, false, Rr, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R, b,
-                         (long long)Rr * b, st->m))
+    // The mean row alpha^T k is the operator's last row; kept in the GEMM it adds a 13th
+    // 64-row tile at Rr = 769 and unbalances the tile grid over the 256 CUs (MI355X,
+    // 5 x {769, 768} x 512 x 512: 54 vs 40 us).  GEMM over the first Rr - 1 rows, the mean
+    // row by a strided-batched gemv over the same K_x.
+    if (int rc = rb_gemm(s, false, Rr - 1, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R,
+                         b, (long long)Rr * b, st->m))
+      return rc;
+    if (int rc = rb_gemv_rows(s, b, st->n, Kx, (long long)st->n * b, Mm + (size_t)(Rr - 1) * st->n,
+                              (long long)Rr * st->n, R + (size_t)(Rr - 1) * b, (long long)Rr * b, st->m))
       return rc;
     qn_norms_rows<<<dim3(cdiv(b, 64), cdiv(st->n + st->nb, 64), st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, nrt, R,
                                                                                      norms);

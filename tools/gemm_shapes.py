@@ -25,7 +25,8 @@ def t_ms(fn, reps=20):
 
 out = {}
 shapes = {"fwd769": (5, 769, 512, 512), "fwd768": (5, 768, 512, 512), "fwd832": (5, 832, 512, 512),
-          "bwd769": (5, 512, 769, 512), "fwd769_b20": (5, 769, 512, 20), "fwd768_b20": (5, 768, 512, 20)}
+          "bwd769": (5, 512, 769, 512), "bwd768": (5, 512, 768, 512), "bwd512x8": (40, 64, 769, 512),
+          "fwd769_b20": (5, 769, 512, 20), "fwd768_b20": (5, 768, 512, 20)}
 for name, (B, M, K, N) in shapes.items():
     A = torch.randn(B, M, K, dtype=torch.float64, device="cuda")
     Bm = torch.randn(B, K, N, dtype=torch.float64, device="cuda")

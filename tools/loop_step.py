@@ -14,10 +14,9 @@ b = int(sys.argv[2]) if len(sys.argv) > 2 else 512
 dev = torch.device("cuda", 0)
 X, Y, gp, hypers, acqf, _, _ = bench.build_state(512, 6, 5, 256, dev)
 Xc = bench.candidates(b, 6, seed=2, device=dev)
-for _ in range(2):
-    bench.step(acqf, Xc)
-torch.cuda.synchronize()
-for _ in range(N):
-    bench.step(acqf, Xc)
+chain = bench.op_chain(acqf, Xc)
+for _ in range(2 + N):
+    for f in chain.values():
+        f()
 torch.cuda.synchronize()
 print("done")
