@@ -651,13 +651,8 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
                                  nullptr, nullptr, Kx))
     return rc;
   if (int rc = gemm_backend_init()) return rc;
-  // [L^-1; alpha^T] K*: the GEMM over the n rows of L^-1 and the mean row alpha^T K* by a
-  // gemv — the (n + 1)-th row alone would add a whole row of 64-row tiles to the GEMM grid
-  if (int rc = rb_gemm(s, false, n, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
+  if (int rc = rb_gemm(s, false, n + 1, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
                        (long long)(n + 1) * nt, B))
-    return rc;
-  if (int rc = rb_gemv_rows(s, nt, n, Kx, (long long)n * nt, M + (size_t)n * n, (long long)(n + 1) * n,
-                            R + (size_t)n * nt, (long long)(n + 1) * nt, B))
     return rc;
   return evr_gp_posterior_finalize(stream, B, n, nt, R, c, ym, ys, kxx, noise_add, mean, var);
 }

@@ -436,17 +436,24 @@ int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int ld
   return 0;
 }
 
-// row-major y_i = sum_k X[k][i] a[k] (X: K x N, ld N), batched: the column-major gemv y = X a
-int rb_gemv_rows(hipStream_t s, int N, int K, const double* X, long long sX, const double* a, long long sa,
-                        double* y, long long sy, int batch) {
-  rocblas_handle h = rb_handle();
-  EVR_CHECK(h, "rocBLAS handle creation failed");
-  EVR_CHECK(rocblas_set_stream(h, s) == rocblas_status_success, "rocblas_set_stream failed");
-  const double one = 1.0, zero = 0.0;
-  const rocblas_status st = rocblas_dgemv_strided_batched(h, rocblas_operation_none, N, K, &one, X, N, sX, a, 1, sa,
-                                                          &zero, y, 1, sy, batch);
-  EVR_CHECK(st == rocblas_status_success, "rocblas_dgemv_strided_batched failed (%d)", (int)st);
-  return 0;
+// mean row of R (the operator's last row, alpha^T K_x): 64 candidates x 4 row groups per
+// block, fixed-order sums (see proj_forward for why it is not a GEMM row)
+__global__ __launch_bounds__(256) void qn_mean_row(int n, int Rr, int b, const double* __restrict__ Mm,
+                                                   const double* __restrict__ Kx, double* __restrict__ R) {
+  __shared__ double red[4][64];
+  const int j = blockIdx.y, cx = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const double* a = Mm + ((size_t)j * Rr + (Rr - 1)) * n;
+  const double* K = Kx + (size_t)j * n * b;
+  double acc = 0.0;
+  if (c < b) {
+#pragma unroll 8
+    for (int i = rg; i < n; i += 4) acc = fma(a[i], K[(size_t)i * b + c], acc);
+  }
+  red[rg][cx] = acc;
+  __syncthreads();
+  if (rg == 0 && c < b)
+    R[((size_t)j * Rr + (Rr - 1)) * b + c] = ((red[0][cx] + red[1][cx]) + red[2][cx]) + red[3][cx];
 }
 
 int gemm_backend_init() {
@@ -472,13 +479,12 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
     // The mean row alpha^T k is the operator's last row; kept in the GEMM it adds a 13th
     // 64-row tile at Rr = 769 and unbalances the tile grid over the 256 CUs (MI355X,
     // 5 x {769, 768} x 512 x 512: 54 vs 40 us).  GEMM over the first Rr - 1 rows, the mean
-    // row by a strided-batched gemv over the same K_x.
+    // row by qn_mean_row over the same K_x (rocBLAS' batched gemv took ~20 us there).
     if (int rc = rb_gemm(s, false, Rr - 1, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R,
                          b, (long long)Rr * b, st->m))
       return rc;
-    if (int rc = rb_gemv_rows(s, b, st->n, Kx, (long long)st->n * b, Mm + (size_t)(Rr - 1) * st->n,
-                              (long long)Rr * st->n, R + (size_t)(Rr - 1) * b, (long long)Rr * b, st->m))
-      return rc;
+    qn_mean_row<<<dim3(cdiv(b, 64), st->m), 256, 0, s>>>(st->n, Rr, b, Mm, Kx, R);
+    EVR_LAUNCH_CHECK();
     qn_norms_rows<<<dim3(cdiv(b, 64), cdiv(st->n + st->nb, 64), st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, nrt, R,
                                                                                      norms);
     EVR_LAUNCH_CHECK();

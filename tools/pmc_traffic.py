@@ -23,7 +23,7 @@ OPS = [
     ("kernel_matrix", r"kmat_kernel"),
     ("proj_fwd", r"qn_proj_fwd|qn_norms_rows"),
     ("samples", r"qn_samples_norms"),
-    ("hvi_fwd_bwd", r"hvi_thresholds|hvi_kd<|hvi_tiled<|hvi_reduce_fwd|hvi_reduce_bwd"),
+    ("hvi_fwd_bwd", r"hvi_thresholds|hvi_kd2?<|hvi_tiled<|hvi_reduce_fwd|hvi_reduce_bwd"),
     ("proj_bwd", r"qn_bwd_coef|qn_proj_bwd|qn_splitk_sum|qn_gen_gr"),
     ("kernel_grad", r"kcross_grad"),
 ]
