@@ -20,8 +20,9 @@
 //      (LDS integer atomics), then ONE bitonic sort of (segment, rank, cell) keys orders
 //      every segment by its objective; segments split at 16*ceil(len/32) so every group of
 //      16 lies in one leaf;
-//   3. outputs per group of 16: keys in kd order, per-cell rank coordinates ([j][16] u16,
-//      0x7FFF padding) and the group's minimum rank per objective.
+//   3. outputs per group of 16: keys in kd order (field 0 rewritten from the rank to the point
+//      index, so the scan decodes without the rank table), per-cell rank coordinates ([j][16]
+//      u16, 0x7FFF padding) and the group's minimum rank per objective.
 // Deterministic: keys are unique (cell index in the low bits), so the order never depends
 // on thread timing.
 #include "common.hpp"
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
     const size_t gg = (size_t)(g0 + g);
     if (i < C) {
       const int cell = (int)(sb[i] & 0xFFFFu);
-      okeys[gg * 16 + w] = keys[c0 + cell];
+      const unsigned long long key = keys[c0 + cell];
+      okeys[gg * 16 + w] = K::set(key, 0, gr0[K::field(key, 0)]);   // field 0: rank -> point index
 #pragma unroll
       for (int j = 0; j < M; ++j) ork[(gg * M + j) * 16 + w] = (unsigned short)rank_of(cell, j);
     } else {

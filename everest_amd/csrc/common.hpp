@@ -159,6 +159,21 @@ struct CellKey {
       hi[j] = -bl;
     }
   }
+  // as decode, for keys whose field 0 holds the point index itself (the kd-ordered group
+  // keys written by cells_kd.hip) rather than the rank in descending first coordinate
+  __device__ static void decode_direct(unsigned long long key, const double* pt, double* lo, double* hi) {
+    int P[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) P[j] = field(key, j);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      double bl = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < j; ++k) bl = fmax(bl, pt[P[k] * M + j]);
+      lo[j] = -pt[P[j] * M + j];
+      hi[j] = -bl;
+    }
+  }
 };
 
 }  // namespace evr

@@ -670,7 +670,7 @@ __global__ __launch_bounds__(256) void hvi_kd(int b, int S, int ntiles, int nspl
             u[j] = l[j] + 0.5;
           }
         } else {
-          K::decode(key, pt, r0, l, u);
+          K::decode_direct(key, pt, l, u);   // grp_keys carry point indices (cells_kd)
         }
         double y[M];
 #pragma unroll
@@ -767,8 +767,58 @@ __device__ __forceinline__ int wave_max_incl(int x) {
   return x;
 }
 
+// LDS of hvi_kd2 beyond its static arrays: the sample's point table, the (chunk, candidate)
+// group masks and the per-wave u16 prefixes (which first hold the chunk-entry lists).  The
+// group minima stay in L2 and the kd keys carry point indices, so neither the rank table nor
+// the group table is staged: ~26 KB per workgroup instead of ~37 KB (6 instead of 4
+// workgroups per CU on the LDS budget).
+struct Kd2Lds {
+  size_t pt, mA, pA, bytes;
+};
+__host__ __device__ inline Kd2Lds kd2_lds(int stride, int M, int max_groups) {
+  Kd2Lds L;
+  const size_t nq = (size_t)(max_groups + 15) / 16;
+  size_t o = 0;
+  L.pt = o;
+  o += (size_t)stride * M * 8;
+  L.mA = o;
+  o += nq * KD_CT * 2;
+  o = (o + 15) & ~(size_t)15;
+  L.pA = o;
+  o += (KD_CT * nq + 4) * 2;
+  L.bytes = o;
+  return L;
+}
+
+// one segmented-scan step; returns whether any lane's source shared its key
+template <int CTRL, int ROWMASK, int NV>
+__device__ __forceinline__ bool seg_step_x(int key, double (&val)[NV]) {
+  const int k2 = dpp_i32<CTRL, ROWMASK>(-2, key);
+  const bool same = k2 == key;
+  if (__ballot(same) == 0ull) return false;
+  double x[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x[v] = dpp_f64<CTRL, ROWMASK>(val[v]);
+  if (same) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) val[v] += x[v];
+  }
+  return true;
+}
+// seg_scan_wave without the steps that would add nothing: segments are contiguous runs, so
+// once a row-local shift finds no lane whose source shares its key, no longer shift can; the
+// two row-broadcast steps are tested on their own.  The sums equal seg_scan_wave's when the
+// keys outside the segments are unique (idle lanes pass -3 - lane).
+template <int NV>
+__device__ __forceinline__ void seg_scan_wave_x(int key, double (&val)[NV]) {
+  if (seg_step_x<0x111, 0xF>(key, val) && seg_step_x<0x112, 0xF>(key, val) && seg_step_x<0x114, 0xF>(key, val))
+    seg_step_x<0x118, 0xF>(key, val);
+  seg_step_x<0x142, 0xA>(key, val);
+  seg_step_x<0x143, 0xC>(key, val);
+}
+
 template <int M, bool BWD>
-__global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
+__global__ __launch_bounds__(256, 6) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
                                                double* __restrict__ dG) {
@@ -780,7 +830,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   __shared__ uint4 thp[KD_CT];             // packed 16-bit thresholds (objectives >= M: 1)
   __shared__ double acc[KD_CT][NV];
   __shared__ uint4 cmin[KD_MAX_NQ];        // chunk minimum corners
-  __shared__ int mkB[4][64], mkC[4][64];   // per-wave owner marks (cell filter / evaluation)
+  __shared__ int mk[4][64];                // per-wave owner marks (cell filter, then evaluation)
   int s, tile;
   {
     const int L = blockIdx.x + ntiles * blockIdx.y;
@@ -804,18 +854,15 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   const int NQ = min(NQall, q0 + qper) - q0;                 // this workgroup's 16-group chunks
   const int gbase = kd.goff[s] + 16 * q0;
   const int Gs = min(kd.goff[s + 1] - gbase, 16 * NQ);
-  const KdLds Lo = kd_lds(stride, M, kd.max_groups);
+  const Kd2Lds Lo = kd2_lds(stride, M, kd.max_groups);
   double* pt = (double*)(kd_dyn + Lo.pt);
-  int* r0 = (int*)(kd_dyn + Lo.r0);
-  uint4* gb = (uint4*)(kd_dyn + Lo.gb);
   unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
-  int* pA = (int*)(kd_dyn + Lo.pA) + wave * (CW * NQ + 1);   // this wave's prefix array
+  unsigned short* pA = (unsigned short*)(kd_dyn + Lo.pA) + wave * (CW * NQ + 1);   // this wave's prefixes
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;   // group minimum corners (L2-resident)
 
   kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
-  kd_stage(r0, kd.rank0 + (size_t)s * stride, stride);
-  if (Gs > 0) kd_stage(gb, (const uint4*)kd.gbox + gbase, Gs);
   for (int q = tid; q < NQ; q += 256) {    // chunk minima from the same (L2-resident) bytes
-    const uint4* src = (const uint4*)kd.gbox + gbase + 16 * q;
+    const uint4* src = gmin + 16 * q;
     const int gend = min(16, Gs - 16 * q);
     uint4 mn = src[0];
     for (int k = 1; k < gend; ++k) {
@@ -857,7 +904,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   // ---- A: chunk pre-filter (lane = (chunk, candidate) entry), ballot compaction of the
   //      surviving entries, then their 16 group tests lane-dense ----
   {
-    unsigned short* ent = (unsigned short*)pA;   // entry list (pA is rewritten by the prefix)
+    unsigned short* ent = pA;   // entry list (pA is rewritten by the prefix)
     int nent = 0;
     for (int eb = 0; eb < NE; eb += 64) {
       const int e = eb + lane, q = e >> 4, cl = e & 15;
@@ -876,7 +923,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       const uint4 t = thp[cbase + cl];
       const int gend = min(16, Gs - q * 16);
       unsigned int mask = 0;
-      for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], t) << k;
+      for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gmin[q * 16 + k], t) << k;
       mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
     }
     if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
@@ -907,12 +954,12 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       preE[k] = run;
-      if (e0 + k < e1) pA[e0 + k] = run;
+      if (e0 + k < e1) pA[e0 + k] = (unsigned short)run;
       run += cnt[k];
     }
     preE[8] = run;
     if (lane == 0) {
-      pA[NE] = PA;
+      pA[NE] = (unsigned short)PA;
       if (kd.counters) {
         atomicAdd(kd.counters + 0, (unsigned long long)PA);
         atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - c0 - cbase, CW)) * Gs);
@@ -922,8 +969,8 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   wave_sync();
   KD_T(1);
 
-  int* mb = mkB[wave];
-  int* mc = mkC[wave];
+  int* mb = mk[wave];
+  int* mc = mb;   // the evaluation reuses the row once the cell filter has read it
   int carryB = -1;
   for (int wb = 0; wb < PA; wb += 64) {
     // ---- B: pair -> entry by marks, then the cell filter (lane = passing pair) ----
@@ -1002,7 +1049,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       for (int v = 0; v < NV; ++v) val[v] = 0.0;
       if (c >= 0) {
         double l[M], u[M];
-        K::decode(key, pt, r0, l, u);
+        K::decode_direct(key, pt, l, u);
         double y[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) y[j] = yv[c][j];
@@ -1035,7 +1082,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
         rcv = c;
       }
       KD_T(3);
-      seg_scan_wave<NV>(rcv, val);
+      seg_scan_wave_x<NV>(rcv >= 0 ? rcv : -3 - lane, val);
       const int rnext = __shfl_down(rcv, 1, 64);
       if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
 #pragma unroll
@@ -1150,9 +1197,10 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
   } else {
     EVR_CHECK((st->max_groups + 15) / 16 <= KD_MAX_NQ, "hvi: %d kd groups per sample exceed the scan's %d",
               st->max_groups, 16 * KD_MAX_NQ);
+    const Kd2Lds L2 = kd2_lds(st->pts_stride, M, st->max_groups);
     EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd2<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)Lo.bytes));
-    hvi_kd2<M, BWD><<<grid, 256, Lo.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
+                                (int)L2.bytes));
+    hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
                                                   ns > 1 ? dgp : dG);
   }
   EVR_LAUNCH_CHECK();

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void qn_proj_fwd_reduce(int n, int nb, int Rr,
 // ---------------------------------------------------------------------------------------
 // samples from the partial norms: thread per (candidate, output, chunk of SCH samples)
 // ---------------------------------------------------------------------------------------
-constexpr int SCH = 16;
+constexpr int SCH = 8;   // 16-sample chunks left 640 one-wave blocks at the bench shape
 
 __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int nh, int m, int b, int nrt_used,
                                                        int nrt,
@@ -436,11 +436,11 @@ int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int ld
   return 0;
 }
 
-// mean row of R (the operator's last row, alpha^T K_x): 64 candidates x 4 row groups per
+// mean row of R (the operator's last row, alpha^T K_x): 64 candidates x 16 row groups per
 // block, fixed-order sums (see proj_forward for why it is not a GEMM row)
-__global__ __launch_bounds__(256) void qn_mean_row(int n, int Rr, int b, const double* __restrict__ Mm,
+__global__ __launch_bounds__(1024) void qn_mean_row(int n, int Rr, int b, const double* __restrict__ Mm,
                                                    const double* __restrict__ Kx, double* __restrict__ R) {
-  __shared__ double red[4][64];
+  __shared__ double red[16][64];
   const int j = blockIdx.y, cx = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cx;
   const double* a = Mm + ((size_t)j * Rr + (Rr - 1)) * n;
@@ -448,12 +448,15 @@ __global__ __launch_bounds__(256) void qn_mean_row(int n, int Rr, int b, const d
   double acc = 0.0;
   if (c < b) {
 #pragma unroll 8
-    for (int i = rg; i < n; i += 4) acc = fma(a[i], K[(size_t)i * b + c], acc);
+    for (int i = rg; i < n; i += 16) acc = fma(a[i], K[(size_t)i * b + c], acc);
   }
   red[rg][cx] = acc;
   __syncthreads();
-  if (rg == 0 && c < b)
-    R[((size_t)j * Rr + (Rr - 1)) * b + c] = ((red[0][cx] + red[1][cx]) + red[2][cx]) + red[3][cx];
+  if (rg == 0 && c < b) {
+    double v = red[0][cx];
+    for (int g = 1; g < 16; ++g) v += red[g][cx];
+    R[((size_t)j * Rr + (Rr - 1)) * b + c] = v;
+  }
 }
 
 int gemm_backend_init() {
@@ -483,7 +486,7 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
     if (int rc = rb_gemm(s, false, Rr - 1, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R,
                          b, (long long)Rr * b, st->m))
       return rc;
-    qn_mean_row<<<dim3(cdiv(b, 64), st->m), 256, 0, s>>>(st->n, Rr, b, Mm, Kx, R);
+    qn_mean_row<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->n, Rr, b, Mm, Kx, R);
     EVR_LAUNCH_CHECK();
     qn_norms_rows<<<dim3(cdiv(b, 64), cdiv(st->n + st->nb, 64), st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, nrt, R,
                                                                                      norms);

@@ -146,7 +146,7 @@ typedef struct {
   /* kd-ordered cell groups (evr_cells_kd_order_device, needs the compressed cells above):
    * when grp_off is not NULL the scan runs the sparse group -> cell -> term filter */
   const int* grp_off;                  /* S + 1: group offsets, 16 cells per group */
-  const unsigned long long* grp_keys;  /* grp_off[S]*16 cell keys in kd order */
+  const unsigned long long* grp_keys;  /* grp_off[S]*16 cell keys in kd order (field 0: point index) */
   const unsigned short* grp_rank;      /* grp_off[S] x m x 16 per-cell lower-bound ranks (0x7FFF pad) */
   const unsigned short* grp_box;       /* grp_off[S] x 8: per-group minimum rank per objective */
   const double* sorted_lo;             /* S x m x pts_stride ascending lower-bound values */

@@ -120,15 +120,21 @@ def test_kd_index_invariants():
     m = cells.m
     off = cells.off.cpu().numpy()
     goff = g.goff.cpu().numpy()
-    keys = cells.keys.cpu().numpy()
-    gkeys = g.keys.cpu().numpy()
+    keys = cells.keys.cpu().numpy().view(np.uint64)
+    gkeys = g.keys.cpu().numpy().view(np.uint64)
+    # the kd keys carry the point index in field 0 where the cell keys carry its rank
+    fb = 16 if m <= 4 else (12 if m == 5 else 64 // m)
+    sh, fm = np.uint64(fb * (m - 1)), np.uint64((1 << fb) - 1)
+    rank0 = cells.rank0.cpu().numpy().reshape(cells.S, -1)
     rank = g.rank.cpu().numpy().view(np.uint16).reshape(-1, m, 16)
     box = g.box.cpu().numpy().view(np.uint16).reshape(-1, 8)
     sv = g.sorted_lo.cpu().numpy()
     for s in range(cells.S):
         C = off[s + 1] - off[s]
         assert goff[s + 1] - goff[s] == (C + 15) // 16
-        mine = np.sort(keys[off[s]:off[s + 1]])
+        kk = keys[off[s]:off[s + 1]]
+        idx = rank0[s][((kk >> sh) & fm).astype(np.int64)].astype(np.uint64)
+        mine = np.sort((kk & ~(fm << sh)) | (idx << sh))
         got = gkeys[goff[s] * 16: goff[s] * 16 + C]
         assert np.array_equal(np.sort(got), mine)                   # a permutation of the cells
         r = rank[goff[s]:goff[s + 1]]                               # groups x m x 16
