@@ -773,7 +773,7 @@ __device__ __forceinline__ int wave_max_incl(int x) {
 // the group table is staged: ~26 KB per workgroup instead of ~37 KB (6 instead of 4
 // workgroups per CU on the LDS budget).
 struct Kd2Lds {
-  size_t pt, mA, pA, bytes;
+  size_t pt, gb, mA, pA, bytes;
 };
 __host__ __device__ inline Kd2Lds kd2_lds(int stride, int M, int max_groups) {
   Kd2Lds L;
@@ -781,6 +781,9 @@ __host__ __device__ inline Kd2Lds kd2_lds(int stride, int M, int max_groups) {
   size_t o = 0;
   L.pt = o;
   o += (size_t)stride * M * 8;
+  o = (o + 15) & ~(size_t)15;
+  L.gb = o;
+  o += (size_t)max_groups * 16;
   L.mA = o;
   o += nq * KD_CT * 2;
   o = (o + 15) & ~(size_t)15;
@@ -818,7 +821,7 @@ __device__ __forceinline__ void seg_scan_wave_x(int key, double (&val)[NV]) {
 }
 
 template <int M, bool BWD>
-__global__ __launch_bounds__(256, 6) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
+__global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
                                                double* __restrict__ dG) {
@@ -858,9 +861,11 @@ __global__ __launch_bounds__(256, 6) void hvi_kd2(int b, int S, int ntiles, int 
   double* pt = (double*)(kd_dyn + Lo.pt);
   unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
   unsigned short* pA = (unsigned short*)(kd_dyn + Lo.pA) + wave * (CW * NQ + 1);   // this wave's prefixes
-  const uint4* gmin = (const uint4*)kd.gbox + gbase;   // group minimum corners (L2-resident)
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;   // group minimum corners
+  uint4* gb = (uint4*)(kd_dyn + Lo.gb);                 // ... and their LDS copy
 
   kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
+  if (Gs > 0) kd_stage(gb, gmin, Gs);
   for (int q = tid; q < NQ; q += 256) {    // chunk minima from the same (L2-resident) bytes
     const uint4* src = gmin + 16 * q;
     const int gend = min(16, Gs - 16 * q);
@@ -923,7 +928,7 @@ __global__ __launch_bounds__(256, 6) void hvi_kd2(int b, int S, int ntiles, int 
       const uint4 t = thp[cbase + cl];
       const int gend = min(16, Gs - q * 16);
       unsigned int mask = 0;
-      for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gmin[q * 16 + k], t) << k;
+      for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], t) << k;
       mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
     }
     if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
