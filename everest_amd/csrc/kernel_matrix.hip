@@ -224,7 +224,11 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
 // Block = 64 candidates (lanes; G rows read coalesced, candidates fastest) x 4 row groups
 // (waves; all lanes of a wave share the training row -> broadcast loads); the rows are
 // split over gridDim.y blocks, the per-split partials part[split][c][k] summed in a fixed
-// order by kcross_grad_reduce (bitwise reproducible).
+// order by kcross_grad_reduce (bitwise reproducible).  Rows outer, outputs inner: the G
+// loads of up to KG_B outputs of one row are issued together (the b-outer loop serialised
+// one global round trip per output: 22 us at m = 5, n = b = 512 on MI355X), 1/ls and the
+// output scales of the chunk sit in LDS.
+constexpr int KG_B = 8;
 template <int MAXD>
 __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d, int rows_per,
                                                           const double* __restrict__ X1,
@@ -241,6 +245,8 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
   const int split = blockIdx.y;
   const int i0 = split * rows_per, i1 = min(n1, i0 + rows_per);
   __shared__ double red[4][64][MAXD];
+  __shared__ double il_s[KG_B][MAXD];
+  __shared__ double os_s[KG_B];
   double x2[MAXD];
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) {
@@ -255,33 +261,53 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
   double acc[MAXD];
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) acc[k] = 0.0;
-  if (c < n2) {
-    for (int b = 0; b < B; ++b) {
-      const double* lsb = ls + (size_t)b * d;
-      const double scale = os ? os[b] : 1.0;
-      const double* Gb = G + (size_t)b * n1 * n2;
-      double il[MAXD];
+  const size_t bstride = (size_t)n1 * n2;
+  for (int b0 = 0; b0 < B; b0 += KG_B) {
+    const int nb = min(KG_B, B - b0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < nb * MAXD; t += blockDim.x) {
+      const int bb = t / MAXD, k = t % MAXD;
+      il_s[bb][k] = (k < d) ? 1.0 / ls[(size_t)(b0 + bb) * d + k] : 0.0;
+    }
+    if ((int)threadIdx.x < nb) os_s[threadIdx.x] = os ? os[b0 + threadIdx.x] : 1.0;
+    __syncthreads();
+    if (c >= n2) continue;
+    const double* Gc = G + (size_t)b0 * bstride + c;
+#pragma unroll 2
+    for (int i = i0 + ry; i < i1; i += 4) {
+      double g[KG_B];
 #pragma unroll
-      for (int k = 0; k < MAXD; ++k) il[k] = (k < d) ? 1.0 / lsb[k] : 0.0;
-      for (int i = i0 + ry; i < i1; i += 4) {
-        const double g = Gb[(size_t)i * n2 + c];
-        double diff[MAXD];
-        double d2 = 0.0;
+      for (int bb = 0; bb < KG_B; ++bb) g[bb] = (bb < nb) ? Gc[bb * bstride + (size_t)i * n2] : 0.0;
+      double x1[MAXD];
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k) {
-          if (k < d) {
-            double v = X1[(size_t)i * d + k];
-            if (sh1) v -= sh1[k];
-            if (sc1) v *= sc1[k];
-            const double df = (x2[k] - v) * il[k];
-            diff[k] = df * il[k];  // (x2 - x1)/ls^2
-            d2 = fma(df, df, d2);
-          }
+      for (int k = 0; k < MAXD; ++k) {
+        double v = 0.0;
+        if (k < d) {
+          v = X1[(size_t)i * d + k];
+          if (sh1) v -= sh1[k];
+          if (sc1) v *= sc1[k];
         }
-        const double sgl = g * scale * kernel_dscale(kind, d2);
+        x1[k] = v;
+      }
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k)
-          if (k < d) acc[k] = fma(sgl, diff[k], acc[k]);
+      for (int bb = 0; bb < KG_B; ++bb) {
+        if (bb < nb) {
+          double diff[MAXD];
+          double d2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < MAXD; ++k) {
+            if (k < d) {
+              const double il = il_s[bb][k];
+              const double df = (x2[k] - x1[k]) * il;
+              diff[k] = df * il;  // (x2 - x1)/ls^2
+              d2 = fma(df, df, d2);
+            }
+          }
+          const double sgl = g[bb] * os_s[bb] * kernel_dscale(kind, d2);
+#pragma unroll
+          for (int k = 0; k < MAXD; ++k)
+            if (k < d) acc[k] = fma(sgl, diff[k], acc[k]);
+        }
       }
     }
   }
