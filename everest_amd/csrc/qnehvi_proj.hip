@@ -255,20 +255,23 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
 
 // ---------------------------------------------------------------------------------------
 // backward coefficients of gR per (output, candidate): coef[j][0..2][c] =
-// (2 dssv, 2 dssw, s dmu); 64 candidates x 16 sample groups per block, fixed-order sum
+// (2 dssv, 2 dssw, s dmu); fixed-order sums
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void qn_bwd_coef(int S, int m, int b, const double* __restrict__ dG,
-                                                    const double* __restrict__ L22, const double* __restrict__ ys,
-                                                    const double* __restrict__ zq, const double* __restrict__ oa,
-                                                    double* __restrict__ coef) {
-  __shared__ double red[16][64][2];
-  const int j = blockIdx.y, cx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
+constexpr int BC_C = 16, BC_G = 64;   // 16 candidates x 64 sample groups: 160 workgroups at b = 512, m = 5
+__global__ __launch_bounds__(BC_C * BC_G) void qn_bwd_coef(int S, int m, int b, const double* __restrict__ dG,
+                                                          const double* __restrict__ L22,
+                                                          const double* __restrict__ ys,
+                                                          const double* __restrict__ zq,
+                                                          const double* __restrict__ oa,
+                                                          double* __restrict__ coef) {
+  __shared__ double red[BC_G][BC_C][2];
+  const int j = blockIdx.y, cx = threadIdx.x % BC_C, g = threadIdx.x / BC_C;
+  const int c = blockIdx.x * BC_C + cx;
   const double aj = oa[j];
   double dmu = 0.0, dl = 0.0;
   if (c < b) {
 #pragma unroll 4
-    for (int s = g; s < S; s += 16) {
+    for (int s = g; s < S; s += BC_G) {
       const double dy = aj * dG[((size_t)s * m + j) * b + c];
       dmu += dy;
       dl = fma(dy, zq[(size_t)s * m + j], dl);
@@ -277,10 +280,26 @@ __global__ __launch_bounds__(1024) void qn_bwd_coef(int S, int m, int b, const d
   red[g][cx][0] = dmu;
   red[g][cx][1] = dl;
   __syncthreads();
+  if (g < 8) {   // fixed order: 8 groups of 8, then the 8 partials
+    dmu = red[g * 8][cx][0];
+    dl = red[g * 8][cx][1];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      dmu += red[g * 8 + q][cx][0];
+      dl += red[g * 8 + q][cx][1];
+    }
+  }
+  __syncthreads();
+  if (g < 8) {
+    red[g][cx][0] = dmu;
+    red[g][cx][1] = dl;
+  }
+  __syncthreads();
   if (g == 0 && c < b) {
-    dmu = 0.0;
-    dl = 0.0;
-    for (int q = 0; q < 16; ++q) {
+    dmu = red[0][cx][0];
+    dl = red[0][cx][1];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
       dmu += red[q][cx][0];
       dl += red[q][cx][1];
     }
@@ -388,16 +407,18 @@ __global__ __launch_bounds__(256) void qn_norms_rows(int n, int nb, int Rr, int 
   }
 }
 
-// gR_j (Rr x b) from R, dG and the per-candidate coefficients (see the header)
+// gR_j (Rr x b) from R, dG and the per-candidate coefficients (see the header).  Grid =
+// (m * Rr rows, candidate tiles): no 64-bit division per element (the flat-index form spent
+// 8.5 us on 31 MB at m = 5, Rr = 769, b = 512 on MI355X)
 __global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int nh, int m, int b, const double* __restrict__ R,
                                                  const double* __restrict__ dG, const double* __restrict__ oa,
                                                  const double* __restrict__ coef, double* __restrict__ gR) {
   const int Rr = n + nb + nh + 1;
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long long)m * Rr * b) return;
-  const int c = (int)(e % b);
-  const long long rj = e / b;
-  const int row = (int)(rj % Rr), j = (int)(rj / Rr);
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= b) return;
+  const int rj = blockIdx.x;
+  const int j = rj / Rr, row = rj - j * Rr;
+  const size_t e = (size_t)rj * b + c;
   const double* cj = coef + (size_t)j * 3 * b;
   double v;
   if (row < n) v = R[e] * cj[c];
@@ -538,12 +559,11 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
   if (b == 0) return 0;
   const int Rr = qn_rows(st);
   double* coef = ws;
-  qn_bwd_coef<<<dim3(cdiv(b, 64), st->m), 1024, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
+  qn_bwd_coef<<<dim3(cdiv(b, BC_C), st->m), BC_C * BC_G, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
   EVR_LAUNCH_CHECK();
   if (bwd_rocblas(b)) {
     double* gR = ws + (size_t)st->m * 3 * b;
-    const long long tot = (long long)st->m * Rr * b;
-    qn_gen_gr<<<cdiv(tot, 256), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, R, dG, st->obj_a, coef, gR);
+    qn_gen_gr<<<dim3(st->m * Rr, cdiv(b, 256)), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, R, dG, st->obj_a, coef, gR);
     EVR_LAUNCH_CHECK();
     return rb_gemm(s, true, st->n, b, Rr, Mm, st->n, (long long)Rr * st->n, gR, b, (long long)Rr * b, dKx, b,
                    (long long)st->n * b, st->m);
