@@ -215,13 +215,24 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
   const int c = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y, chunk = blockIdx.z;
   if (c >= b) return;
   const long long Rr = (long long)n + nb + nh + 1;
+  const double* Rj = R + (size_t)j * Rr * b;
+  // the chunk's sample rows and z values do not depend on the norms: issue their loads
+  // first so that they overlap the partial-norm sum
+  const int s0 = chunk * SCH, ns = min(S - s0, SCH);
+  const double* h = Rj + (size_t)(n + nb) * b + c;
+  double hv[SCH], zv[SCH];
+#pragma unroll
+  for (int q = 0; q < SCH; ++q) {
+    hv[q] = (nh && q < ns) ? h[(size_t)(s0 + q) * b] : 0.0;
+    zv[q] = (q < ns) ? zq[(size_t)(s0 + q) * m + j] : 0.0;
+  }
   const double* Pj = P + (size_t)j * nrt * 2 * b;
   double ssv = 0.0, ssw = 0.0;
+#pragma unroll 4
   for (int rt = 0; rt < nrt_used; ++rt) {
     ssv += Pj[((size_t)rt * 2 + 0) * b + c];
     ssw += Pj[((size_t)rt * 2 + 1) * b + c];
   }
-  const double* Rj = R + (size_t)j * Rr * b;
   const double a = Rj[(size_t)(Rr - 1) * b + c];
   const double s = ys[j];
   const double mu = ym[j] + s * (cc[j] + a);
@@ -245,11 +256,12 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
     flags[(size_t)j * b + c] = flag;
   }
   const double A = oa[j], B0 = ob[j];
-  const double* h = Rj + (size_t)(n + nb) * b + c;
-  const int s1 = min(S, (chunk + 1) * SCH);
-  for (int si = chunk * SCH; si < s1; ++si) {
-    const double y = (nh ? mu + h[(size_t)si * b] : mu) + l22 * zq[(size_t)si * m + j];
-    G[((size_t)si * m + j) * b + c] = fma(A, y, B0);
+#pragma unroll
+  for (int q = 0; q < SCH; ++q) {
+    if (q < ns) {
+      const double y = (nh ? mu + hv[q] : mu) + l22 * zv[q];
+      G[((size_t)(s0 + q) * m + j) * b + c] = fma(A, y, B0);
+    }
   }
 }
 
