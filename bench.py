@@ -12,9 +12,11 @@ b=512 Sobol candidates already resident in HBM, run through the native evaluatio
 (everest_amd/csrc/qnehvi_plan.hip — the path ask() uses); the per-kernel breakdown comes
 from a separate instrumented pass over the same kernels launched one by one.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): every rank evaluates its own 512-candidate
-shard (weak scaling); each step ends with the RCCL all-gather of the per-shard acquisition
-values that the Boltzmann initial-condition selection needs.
+Multi-GPU (one process per GPU, RCCL): ``--gpus N`` spawns N ranks itself (or runs under
+torchrun with WORLD_SIZE = N).  Every rank evaluates its own 512-candidate shard (weak
+scaling); each step ends with the RCCL all-gather of the per-shard acquisition values that
+the Boltzmann initial-condition selection needs.  The full ask() (config
+4: 1024 raw + 20 restarts) is then timed sharded over the N ranks.
 
 Prints ONE JSON line on rank 0.
 """
@@ -155,29 +157,41 @@ def scan_counts(acqf, Xc):
     return {"group_pairs": int(c[0]), "terms": int(c[1]), "group_tests": int(c[2])}
 
 
-def gp_posterior_ms(device, reps=20):
-    """Config 2: SingleTaskGP RBF posterior (mean+var), n_train=256, d=6, 1024 test points."""
+def _event_ms(fn, reps=20, warm=3):
+    """Average device time of fn() over ``reps`` back-to-back calls, bracketed by HIP events
+    on torch's current stream (the stream every evr_* call is enqueued on)."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gp_posterior_ms(device, gp=None, n_test=1024, reps=20):
+    """GP posterior (mean + var, observation_noise=False) of 1024 Sobol test points.
+    Default: config 2 (SingleTaskGP RBF, n_train=256, d=6, one output, fixed hypers); with
+    ``gp`` the given batched model (the metric's n=512, d=6, m=5 shape from build_state)."""
     from everest_amd.gp import GPBatch, GPHyper
 
-    rng = np.random.default_rng(0)
-    X = rng.uniform(size=(256, 6))
-    y = dtlz2(X, 5)[:, :1]
-    h = GPHyper(lengthscale=np.full(6, 0.8), noise=1e-3, constant=0.0, y_mean=float(y.mean()),
-                y_std=float(y.std(ddof=1)))
-    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)  # noqa: E731
-    gp = GPBatch(t(X), t(y), [h], 0, t(np.zeros(6)), t(np.ones(6)))
-    Xs = torch.quasirandom.SobolEngine(6, scramble=True, seed=1).draw(1024, dtype=torch.float64).to(device)
-    for _ in range(3):
-        gp.posterior(Xs)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        gp.posterior(Xs)
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps * 1e3
+    if gp is None:
+        rng = np.random.default_rng(0)
+        X = rng.uniform(size=(256, 6))
+        y = dtlz2(X, 5)[:, :1]
+        h = GPHyper(lengthscale=np.full(6, 0.8), noise=1e-3, constant=0.0, y_mean=float(y.mean()),
+                    y_std=float(y.std(ddof=1)))
+        t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)  # noqa: E731
+        gp = GPBatch(t(X), t(y), [h], 0, t(np.zeros(6)), t(np.ones(6)))
+    d = gp.Xn.shape[1]
+    Xs = torch.quasirandom.SobolEngine(d, scramble=True, seed=1).draw(n_test, dtype=torch.float64).to(device)
+    return _event_ms(lambda: gp.posterior(Xs), reps=reps)
 
 
-def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, chunk=8, budget_s=15.0):
+def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, chunk=8, budget_s=12.0):
     """Reference-structure CPU restatement (oracle/, torch-CPU fp64, BoTorch computation
     shape: joint posterior over [X_base; x] per forward, per-sample cell scan, autograd
     backward) timed on the host cores over a BOUNDED sample of the same workload: chunks of
@@ -278,10 +292,12 @@ def _traffic(path, kernel):
     return ent if ent and "bytes_per_launch" in ent else None
 
 
-def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: int = 2):
-    """Full QnehviStrategy.ask() (config 4 shape on one GPU: 1024 raw Sobol candidates +
-    20 L-BFGS-B restarts, q=1) through the BoFire-compatible strategy API; returns the
-    median ask() wall time and acquisition evaluations / s (raw + optimizer evaluations)."""
+def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: int = 3, dist=None, device=None):
+    """Full QnehviStrategy.ask() (config 4 shape: 1024 raw Sobol candidates + 20 L-BFGS-B
+    restarts, q=1) through the BoFire-compatible strategy API; with ``dist`` every rank runs
+    the same strategy and ask() shards the raw screening and the joint restart evaluations
+    over the ranks (RCCL all-gathers).  Returns the median ask() wall time
+    (max over ranks) and acquisition evaluations / s (raw + optimizer evaluations)."""
     import pandas as pd
 
     import everest_amd.data_models as dm
@@ -291,23 +307,69 @@ def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: in
     bm = DTLZ2(dim=6, num_objectives=5)
     Xd = pd.DataFrame(np.random.default_rng(0).uniform(size=(n, 6)), columns=bm.domain.inputs.get_keys())
     s = strategies.map(dm.QnehviStrategy(domain=bm.domain, ref_point=bm.ref_point, seed=1, num_sobol_samples=S,
-                                         num_raw_samples=raw, num_restarts=restarts))
-    t0 = time.perf_counter()
-    s.tell(bm.f(Xd, return_complete=True))
-    torch.cuda.synchronize()
-    t_tell = time.perf_counter() - t0
-    s.ask(1)  # warm-up (first construction pays one-time allocations)
-    ts, evals = [], []
-    for _ in range(asks):
-        t0 = time.perf_counter()
-        s.ask(1)
+                                         num_raw_samples=raw, num_restarts=restarts), dist=dist)
+
+    def clock(fn):
+        if dist is not None:
+            dist.barrier()
         torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([dt], device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = tt.item()
+        return dt
+
+    t_tell = clock(lambda: s.tell(bm.f(Xd, return_complete=True)))
+    s.ask(1)  # warm-up (first construction pays one-time allocations)
+    ts, evals, phases = [], [], []
+    for _ in range(asks):
+        ts.append(clock(lambda: s.ask(1)))
         st = s.last_ask_stats
-        evals.append(st.raw_evals + st.opt_evals)
+        evals.append(st.raw_evals + getattr(st, "opt_evals_global", st.opt_evals))
+        tm = getattr(s.last_acqf, "timings", {})
+        phases.append({"construction": round(tm.get("total", 0.0), 4), "raw_screening": round(st.t_raw, 4),
+                       "restarts": round(st.t_opt, 4), "optimizer_iterations": st.opt_iters,
+                       "driver": st.chunks[0]["driver"] if st.chunks else None})
     i = int(np.argsort(ts)[len(ts) // 2])
     return {"ask_s": round(ts[i], 4), "evals": int(evals[i]), "evals_per_s": round(evals[i] / ts[i], 1),
-            "tell_s": round(t_tell, 3), "raw_samples": raw, "restarts": restarts, "mc_samples": S}
+            "tell_s": round(t_tell, 3), "raw_samples": raw, "restarts": restarts, "mc_samples": S,
+            "phases_s": phases[i], "ranks": 1 if dist is None else dist.get_world_size()}
+
+
+def _spawn_ranks(n: int) -> int:
+    """``bench.py --gpus N`` without a launcher: start N fresh ranks (one process per GPU,
+    torchrun-style env, RCCL rendezvous on 127.0.0.1) from a parent that never touches HIP,
+    stop the others if one fails, and return the first non-zero exit code (else 0)."""
+    import socket
+    import subprocess
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -326,7 +388,12 @@ def main():
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args.gpus))            # parent: no HIP call before the ranks start
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -336,6 +403,7 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=device)
+        world = dist.get_world_size()
 
     X, Y, gp, hypers, acqf, t_fit, t_build = build_state(args.n, args.d, args.m, args.S, device)
     Xc = candidates(args.b, args.d, seed=2 + rank, device=device)
@@ -374,6 +442,11 @@ def main():
 
     # per-kernel device time: each op of the same chain, graph-replayed between HIP events
     ktimes, ktimes_how = kernel_times(acqf, Xc)
+
+    # full ask() (config 4 shape; sharded over the ranks when N > 1)
+    ask = None
+    if not args.no_ask:
+        ask = ask_throughput(args.n, args.S, dist=dist, device=device)
 
     if rank == 0:
         st = acqf.stats
@@ -428,19 +501,28 @@ def main():
                 "dense_pairs": b * sum_cells, "group_tests": counts["group_tests"], "group_pairs": counts["group_pairs"],
                 "terms": counts["terms"],
                 "dense_equivalent_TFLOPs": round(b * sum_cells * (6 * m + 2) / (ktimes["hvi_fwd_bwd"] * 1e-3) / 1e12, 2)}
-        cpu = orc = None
+        cpu = None
         if not args.no_cpu_baseline and world == 1:
-            torch.set_num_threads(min(16, os.cpu_count() or 1))
+            # the job's CPU share on the box (OMP_NUM_THREADS, 16 per GPU there; the affinity
+            # mask shows the whole machine), plus a single-thread leg
+            share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            threads = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+            torch.set_num_threads(threads)
             t_cpu, nc, orc, ostates = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
             cpu = {"value": round(nc / t_cpu, 3), "unit": "candidates/s", "cores": torch.get_num_threads(),
                    "kind": "port", "sample": f"oracle reference-structure forward+backward over the first {nc} "
                    f"of the same {b} candidates in chunks of 8 (batch_limit), same state (n={args.n}, "
-                   f"n_base={acqf.nb}, S={args.S}), {t_cpu:.1f} s of CPU wall time"}
-        ask = None
-        if world == 1 and not args.no_ask:
-            ask = ask_throughput(args.n, args.S)
-            if orc is not None:
+                   f"n_base={acqf.nb}, S={args.S}), {t_cpu:.1f} s of CPU wall time",
+                   "cores_note": f"{threads} threads = this job's CPU share (OMP_NUM_THREADS; "
+                                 f"affinity mask {share}, os.cpu_count {os.cpu_count()})"}
+            torch.set_num_threads(1)
+            t1, n1, _, _ = cpu_baseline(acqf, hypers, X, Y, Xc.cpu(), budget_s=6.0)
+            cpu["single_thread"] = {"value": round(n1 / t1, 3), "unit": "candidates/s", "cores": 1,
+                                    "sample": f"{n1} candidates, {t1:.1f} s"}
+            torch.set_num_threads(threads)
+            if ask is not None:
                 cpu["ask_estimate"] = cpu_ask_estimate(orc, ostates, acqf, Xc.cpu(), ask)
+        t_post = gp_posterior_ms(device, gp=gp)
         out = {
             "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
             "value": round(value, 2),
@@ -454,14 +536,19 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (DTLZ2 d=6 m=5 train set, Sobol candidates; GPs fitted on device)",
-            "config": {"workload": "qNEHVI fwd+bwd eval pass, DTLZ2(d=6,m=5) n_train=512 S=256 b=512 q=1",
+            "config": {"workload": "qNEHVI fwd+bwd evaluation pass (the unit ask()'s raw screening and L-BFGS-B "
+                                   "restarts are made of), DTLZ2(d=6,m=5) n_train=512 S=256 b=512 q=1; "
+                                   "the full ask() rate is ask.evals_per_s",
                        "n_train": args.n, "d": args.d, "m": m, "mc_samples": args.S, "candidates_per_gpu": b,
                        "n_base": acqf.nb, "cells_total": sum_cells, "cells_max": st.max_cells,
-                       "parallelism": f"candidate-shard x{world}"},
+                       "box_decomposition": acqf.box_path, "parallelism": f"candidate-shard x{world}"},
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": cpu,
-            "gp_posterior_ms": round(gp_posterior_ms(device), 4),
+            "gp_posterior_ms": round(t_post, 4),
+            "gp_posterior": {"ms": round(t_post, 4), "shape": f"n_train={args.n} d={args.d} m={m}, 1024 test "
+                             "points, mean+var, HIP events",
+                             "config2_ms": round(gp_posterior_ms(device), 4)},
             "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},
             "kernel_ms_method": f"{ktimes_how} of 10 launches per op between HIP events (torch current stream)",
             "setup_s": {"gp_fit": round(t_fit, 3), "qnehvi_build": round(t_build, 3)},

@@ -111,6 +111,13 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_int, POINTER(c_void_p)], c_int),
     "evr_qnehvi_plan_run": ([c_void_p, c_void_p], c_int),
     "evr_qnehvi_plan_destroy": ([c_void_p], None),
+    "evr_lbfgsb_create": ([c_int, c_int, c_void_p, c_void_p, c_double, c_double, c_int, POINTER(c_void_p)], c_int),
+    "evr_lbfgsb_start": ([c_void_p, c_void_p, c_void_p], c_int),
+    "evr_lbfgsb_step": ([c_void_p, c_double, c_void_p, c_void_p], c_int),
+    "evr_lbfgsb_stats": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], None),
+    "evr_lbfgsb_destroy": ([c_void_p], None),
+    "evr_qnehvi_plan_minimize": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
+                                  c_double, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import os
+import warnings
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -61,12 +62,25 @@ def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None
     m, P, _ = O.shape
     dev = O.device
     if box_device if box_device is not None else ops.box_device_supported(P, m):
-        cells = ops.box_decompose_device(O, ref)
-        path = "device"
-        if kd_scan if kd_scan is not None else ops.kd_supported(cells):
-            ops.cells_kd_order(cells)
-            path = "device+kd"
-        return cells, path
+        try:
+            cells = ops.box_decompose_device(O, ref)
+        except ops.BoxCapacityError as e:
+            if box_device:      # explicitly requested: surface the limit
+                raise
+            warnings.warn(f"{e}; using the exact host partition", RuntimeWarning)
+            cells = None
+        if cells is not None:
+            path = "device"
+            if kd_scan if kd_scan is not None else ops.kd_supported(cells):
+                ops.cells_kd_order(cells)
+                path = "device+kd"
+            elif kd_scan is None:
+                warnings.warn(f"{int(cells.counts.max())} cells in one sample exceed the sparse kd scan's limit; "
+                              "using the dense tiled scan (~10x slower)", RuntimeWarning)
+            return cells, path
+    elif box_device is None:
+        warnings.warn(f"{P} points x {m} objectives exceed the device box decomposition's limits; "
+                      "using the host partition", RuntimeWarning)
     mask, _ = ops.pareto_mask(O, ref, dedup=True)
     lo, hi, off = ops.box_decompose(O.cpu().numpy(), ref.cpu().numpy(), mask.cpu().numpy(),
                                     num_threads or _host_threads(), layout="jis")
@@ -487,8 +501,10 @@ class QEI:
         X = X.to(device=self.dev, dtype=torch.float64).contiguous()
         R = ops.gemm(self.gp.M, self.gp.cross(X))[0]          # (n+1) x b
         acq, gR, flags = ops.qei(R, *self._scal, self.z, self.a, self.b, self.best_f, with_grad)
-        if bool(flags.any().item()):
-            raise ops.NotPSDError("qEI: posterior variance not p.d. after 3 jitter tries")
+        # NaN marks a candidate whose variance stayed not p.d. after the jitter ladder; no host
+        # sync here — optim.host_values raises NotPSDError after the (all-)gather, so every
+        # rank of a sharded evaluation raises together (as QNEHVI does)
+        acq = torch.where(flags != 0, torch.full_like(acq, math.nan), acq)
         return X, acq, gR
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:

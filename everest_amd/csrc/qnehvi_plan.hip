@@ -11,10 +11,13 @@
 // launch per iteration instead of a dozen kernel launches through the Python binding.
 // The plan copies the state / model structs; the device buffers they point to, the
 // workspace and the X / output buffers must outlive it (the Python QNEHVI object owns them).
+#include <algorithm>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "common.hpp"
+#include "lbfgsb.hpp"
 #include "../../include/everest_amd.h"
 
 namespace evr {
@@ -81,6 +84,8 @@ struct evr_qnehvi_plan {
   PlanLayout L;
   hipGraph_t graph;
   hipGraphExec_t exec;
+  double* hx;    // pinned staging of x (b x d) and [acq | dX] for evr_qnehvi_plan_minimize
+  double* hout;
 };
 
 static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
@@ -137,6 +142,8 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->L = plan_layout(st, md, b, p->backward);
   p->graph = nullptr;
   p->exec = nullptr;
+  p->hx = nullptr;
+  p->hout = nullptr;
   if (int rc = gemm_backend_init()) {
     delete p;
     return rc;
@@ -185,9 +192,78 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
+  if (p->hx) (void)hipHostFree(p->hx);
+  if (p->hout) (void)hipHostFree(p->hout);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   delete p;
+}
+
+// One evaluation of the restart batch at host x: f = -sum_r acq_r, g = -dX.
+static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g) {
+  const int b = p->b, n = b * p->md.d;
+  std::memcpy(p->hx, x, sizeof(double) * n);
+  EVR_HIP(hipMemcpyAsync((void*)p->X, p->hx, sizeof(double) * n, hipMemcpyHostToDevice, s));
+  if (int rc = evr_qnehvi_plan_run((void*)s, p)) return rc;
+  EVR_HIP(hipMemcpyAsync(p->hout, p->acq, sizeof(double) * b, hipMemcpyDeviceToHost, s));
+  EVR_HIP(hipMemcpyAsync(p->hout + b, p->dX, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  EVR_HIP(hipStreamSynchronize(s));
+  double acc = 0.0;
+  for (int r = 0; r < b; ++r) {
+    if (std::isnan(p->hout[r])) {
+      ::evr::set_error("acquisition: posterior covariance block not p.d. after the jitter ladder (NotPSDError)");
+      return EVR_ERR_NOTPSD;
+    }
+    acc += p->hout[r];
+  }
+  *f = -acc;
+  for (int i = 0; i < n; ++i) g[i] = -p->hout[b + i];
+  return 0;
+}
+
+int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0, const double* lb, const double* ub,
+                             int maxiter, int maxfun, double factr, double pgtol, int mcor, int maxls, double* x,
+                             double* acq, int* info) {
+  EVR_CHECK(p && p->backward && p->dX && x0 && lb && ub && x && acq && info && maxiter >= 1 && maxfun >= 1 &&
+                mcor >= 1 && maxls >= 1 && factr >= 0.0 && pgtol >= 0.0,
+            "evr_qnehvi_plan_minimize: bad arguments (needs a backward plan)");
+  const int b = p->b, n = b * p->md.d;
+  for (int i = 0; i < n; ++i) EVR_CHECK(!(lb[i] > ub[i]), "evr_qnehvi_plan_minimize: lower bound above upper bound");
+  hipStream_t s = (hipStream_t)stream;
+  if (!p->hx) EVR_HIP(hipHostMalloc((void**)&p->hx, sizeof(double) * n, hipHostMallocDefault));
+  if (!p->hout) EVR_HIP(hipHostMalloc((void**)&p->hout, sizeof(double) * (size_t)b * (1 + p->md.d),
+                                      hipHostMallocDefault));
+  Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
+  std::vector<double> g(n);
+  double f = 0.0;
+  int task = opt.start(x0), nit = 0, nfev = 0, status = 0;
+  // scipy's _minimize_lbfgsb driver loop
+  for (;;) {
+    if (task == LBFGSB_FG) {
+      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
+      ++nfev;
+      task = opt.step(f, g.data());
+    } else if (task == LBFGSB_NEW_X) {
+      ++nit;
+      if (nit >= maxiter || nfev > maxfun) {
+        status = 1;
+        break;
+      }
+      task = opt.step(f, g.data());
+    } else {
+      status = task == LBFGSB_ABNORMAL ? 2 : task == LBFGSB_ERROR ? 3 : 0;
+      break;
+    }
+  }
+  for (int i = 0; i < n; ++i) x[i] = std::min(ub[i], std::max(lb[i], opt.x()[i]));
+  // re-evaluate at the clipped candidates ([upstream] gen_candidates_scipy's final no-grad call)
+  if (int rc = plan_eval_host(s, p, x, &f, g.data())) return rc;
+  std::memcpy(acq, p->hout, sizeof(double) * b);
+  info[0] = nit;
+  info[1] = nfev;
+  info[2] = status;
+  info[3] = task;
+  return 0;
 }
 
 }  // extern "C"

@@ -8,6 +8,7 @@ The top-level ops are also registered as PyTorch custom ops (``torch.ops.everest
 from __future__ import annotations
 
 import ctypes
+import warnings
 from typing import Optional, Tuple
 
 import numpy as np
@@ -366,6 +367,28 @@ class QnehviPlan:
         torch.cuda.current_stream().synchronize()
         return self.host.numpy()
 
+    def minimize(self, x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int, maxfun: int = 15000,
+                 maxcor: int = 10, ftol: float = 2.220446049250313e-09, gtol: float = 1e-5, maxls: int = 20):
+        """Native L-BFGS-B over the b restarts of this (backward) plan, the whole loop in C++
+        (evr_qnehvi_plan_minimize): returns (x (b*d, clipped), acq (b) at x,
+        [iterations, evaluations, status, task]).  Raises NotPSDError on a NaN evaluation."""
+        if not self.backward:
+            raise ValueError("minimize needs a backward plan")
+        n = self.b * self.d
+        f64 = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(n))  # noqa: E731
+        x0, lb, ub = f64(x0), f64(lb), f64(ub)
+        x = np.empty(n)
+        acq = np.empty(self.b)
+        info = np.zeros(4, dtype=np.int32)
+        rc = self._lib.evr_qnehvi_plan_minimize(_stream(), self._h, x0.ctypes.data, lb.ctypes.data, ub.ctypes.data,
+                                                int(maxiter), int(maxfun), ftol / float(np.finfo(float).eps),
+                                                float(gtol), int(maxcor), int(maxls), x.ctypes.data,
+                                                acq.ctypes.data, info.ctypes.data)
+        if rc == 7:
+            raise NotPSDError(self._lib.evr_last_error().decode(errors="replace"))
+        _native.check(rc, "evr_qnehvi_plan_minimize")
+        return x, acq, info.tolist()
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
@@ -550,17 +573,27 @@ def cells_kd_order(cells: Cells) -> KdGroups:
     return cells.kd
 
 
-def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20) -> Cells:
+class BoxCapacityError(RuntimeError):
+    """The device box decomposition needs more LUB slots than its capacity / memory bound
+    (the caller falls back to the exact host partition)."""
+
+
+def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, max_cap: int = 1 << 20,
+                         max_workspace_bytes: int = 8 << 30) -> Cells:
     """Device box decomposition of every sample of O (m x n x S objective values) above ref,
     returned compressed (64-bit keys + point tables, see Cells).
 
     One host sync (the per-sample cell counts size the packed arrays and the HVI plan); a
-    sample overflowing ``cap`` LUB slots reruns the batch with 4x the capacity."""
+    sample overflowing ``cap`` LUB slots reruns the batch with 4x the capacity, up to
+    ``max_cap`` slots and ``max_workspace_bytes`` of workspace, beyond which it raises
+    BoxCapacityError."""
     O, ref = _dev(O, "O"), _dev(ref, "ref")
     m, n, S = O.shape
     dev = O.device
     while True:
         nbytes = _native.load().evr_box_device_workspace_bytes(S, n, m, cap)
+        if nbytes > max_workspace_bytes:
+            raise BoxCapacityError(f"box decomposition: {cap} LUB slots x {S} samples need {nbytes} B of workspace")
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         cs = torch.empty(2, S, dtype=torch.int32, device=dev)
         call("evr_box_decompose_device", _stream(), S, n, m, O.data_ptr(), ref.data_ptr(), cap, ws.data_ptr(),
@@ -569,7 +602,7 @@ def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, m
         if not h[1].any():
             break
         if cap >= max_cap:
-            raise RuntimeError(f"box decomposition: more than {max_cap} local upper bounds in one sample")
+            raise BoxCapacityError(f"box decomposition: more than {max_cap} local upper bounds in one sample")
         cap *= 4
     counts = h[0].astype(np.int64)
     off_h = np.zeros(S + 1, dtype=np.int64)
@@ -601,6 +634,22 @@ def _sobol_directions(dim: int) -> torch.Tensor:
     return V
 
 
+SOBOL_MAXDIM = 21201     # torch.quasirandom.SobolEngine.MAXDIM
+
+
+def _iid_normal(n: int, dim: int, seed: int, device, d0: int, nd: int, layout: int, m: int) -> torch.Tensor:
+    """[upstream] get_sampler's fallback beyond SobolEngine.MAXDIM dims: IIDNormalSampler,
+    torch.randn of the (n, dim) base-sample shape under manual_seed(seed) (CPU generator),
+    restricted to dims [d0, d0+nd) in the requested layout."""
+    warnings.warn(f"{dim} base-sample dims exceed SobolEngine.MAXDIM={SOBOL_MAXDIM}: IID normal base samples",
+                  RuntimeWarning)
+    g = torch.Generator().manual_seed(int(seed))
+    Z = torch.randn(n, dim, generator=g, dtype=torch.float64)[:, d0:d0 + nd]
+    if layout == 0:
+        return Z.contiguous().to(device)
+    return Z.reshape(n, nd // m, m).permute(2, 1, 0).contiguous().to(device)
+
+
 def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[int] = None,
                  layout: int = 0, m: int = 1) -> torch.Tensor:
     """Device draw_sobol_normal_samples(dim, n, seed) restricted to dims [d0, d0+nd).
@@ -610,6 +659,8 @@ def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[
     nd = dim - d0 if nd is None else nd
     if not (0 <= d0 and d0 + nd <= dim):
         raise ValueError("sobol_normal: dims out of range")
+    if dim > SOBOL_MAXDIM:
+        return _iid_normal(n, dim, seed, device, d0, nd, layout, m)
     V = _sobol_directions(dim).clone()
     shift = torch.empty(dim, dtype=torch.long)
     call("evr_sobol_scramble", dim, int(seed), V.data_ptr(), shift.data_ptr())

@@ -7,8 +7,12 @@ bofire/strategies/predictives/botorch.py:384-405 (q=1, return_best_only=True):
 2. the whole raw batch is evaluated in ONE device launch sequence (the reference walks it
    in chunks of ``batch_limit``);
 3. ``initialize_q_batch_nonneg`` (eta=1, alpha=1e-4) picks ``num_restarts`` starts;
-4. ``gen_candidates_scipy``: per chunk of ``batch_limit`` restarts, scipy L-BFGS-B (box) or
-   SLSQP (linear constraints) minimises -sum_r acq(x_r) with the analytic device gradient;
+4. ``gen_candidates_scipy``: per chunk of ``batch_limit`` restarts, L-BFGS-B (box) or scipy
+   SLSQP (linear constraints) minimises -sum_r acq(x_r) with the analytic device gradient.
+   L-BFGS-B is the native restatement of scipy's (csrc/lbfgsb.cpp, same iterates, checked
+   against scipy in tests/test_lbfgsb_cpu.py); on a device plan the whole loop runs in C++
+   (evr_qnehvi_plan_minimize), otherwise through ``minimize_lbfgsb`` with a Python callback.
+   ``options["optimizer"]`` / EVR_OPTIMIZER = "scipy" selects scipy's L-BFGS-B instead;
 5. candidates clamped to the bounds, re-evaluated, best restart returned.
 
 With ``dist`` (torch.distributed, one process per GPU) the raw batch is sharded over the
@@ -18,7 +22,9 @@ round-robin and the per-chunk best (value, x) pairs all-gathered (SURVEY.md §8(
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import warnings
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -42,6 +48,72 @@ class OptimizeStats:
     @property
     def candidates_evaluated(self) -> int:
         return self.raw_evals + self.opt_evals
+
+
+LBFGSB_FG, LBFGSB_NEW_X, LBFGSB_CONV_PGTOL, LBFGSB_CONV_FACTR, LBFGSB_ABNORMAL, LBFGSB_ERROR = 1, 2, 3, 4, 5, 6
+_EPS = float(np.finfo(float).eps)
+
+
+@dataclass
+class LbfgsbResult:
+    x: np.ndarray
+    fun: float
+    nit: int
+    nfev: int
+    status: int      # 0 converged, 1 iteration / evaluation limit, 2 abnormal line search
+    message: str
+
+
+_TASK_MSG = {LBFGSB_CONV_PGTOL: "CONVERGENCE: NORM OF PROJECTED GRADIENT <= PGTOL",
+             LBFGSB_CONV_FACTR: "CONVERGENCE: RELATIVE REDUCTION OF F <= FACTR*EPSMCH",
+             LBFGSB_ABNORMAL: "ABNORMAL: line search failed", LBFGSB_ERROR: "ERROR"}
+
+
+def minimize_lbfgsb(fun: Callable, x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int = 15000,
+                    maxfun: int = 15000, maxcor: int = 10, ftol: float = 2.220446049250313e-09, gtol: float = 1e-5,
+                    maxls: int = 20) -> LbfgsbResult:
+    """Bound-constrained L-BFGS-B through the native restatement (everest_amd/csrc/lbfgsb.cpp)
+    with scipy.optimize.minimize(method="L-BFGS-B", jac=True)'s defaults and driver loop:
+    ``fun(x) -> (f, g)``; stop after ``maxiter`` iterations or more than ``maxfun``
+    evaluations."""
+    from . import _native
+
+    lib = _native.load()
+    n = int(np.asarray(x0).size)
+    lo = np.ascontiguousarray(np.broadcast_to(np.asarray(lb, dtype=np.float64), (n,)))
+    hi = np.ascontiguousarray(np.broadcast_to(np.asarray(ub, dtype=np.float64), (n,)))
+    x = np.empty(n, dtype=np.float64)
+    x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(n))
+    h = ctypes.c_void_p()
+    _native.check(lib.evr_lbfgsb_create(n, int(maxcor), lo.ctypes.data, hi.ctypes.data, ftol / _EPS, float(gtol),
+                                        int(maxls), ctypes.byref(h)), "evr_lbfgsb_create")
+    try:
+        task = lib.evr_lbfgsb_start(h, x0.ctypes.data, x.ctypes.data)
+        f, g = 0.0, np.zeros(n)
+        nit = nfev = 0
+        status = 0
+        while True:
+            if task == LBFGSB_FG:
+                f, g = fun(x.copy())
+                f = float(f)
+                g = np.ascontiguousarray(np.asarray(g, dtype=np.float64).reshape(n))
+                nfev += 1
+                task = lib.evr_lbfgsb_step(h, f, g.ctypes.data, x.ctypes.data)
+            elif task == LBFGSB_NEW_X:
+                nit += 1
+                if nit >= maxiter or nfev > maxfun:
+                    status = 1
+                    msg = "STOP: TOTAL NO. OF ITERATIONS REACHED LIMIT" if nit >= maxiter else \
+                        "STOP: TOTAL NO. OF F,G EVALUATIONS EXCEEDS LIMIT"
+                    break
+                task = lib.evr_lbfgsb_step(h, f, g.ctypes.data, x.ctypes.data)
+            else:
+                status = 2 if task == LBFGSB_ABNORMAL else (3 if task == LBFGSB_ERROR else 0)
+                msg = _TASK_MSG.get(task, str(task))
+                break
+    finally:
+        lib.evr_lbfgsb_destroy(h)
+    return LbfgsbResult(x=x, fun=f, nit=nit, nfev=nfev, status=status, message=msg)
 
 
 def draw_sobol_samples(bounds: np.ndarray, n: int, seed: int) -> np.ndarray:
@@ -97,13 +169,18 @@ def hit_and_run(bounds: np.ndarray, ineq: Sequence[LinearConstraint], eq: Sequen
         N = Vt[rank:].T
     else:
         N = np.eye(d)
+    if N.shape[1] == 0:      # the equalities fix every dimension: the polytope is one point
+        return np.repeat(x[None, :], n, axis=0)
     rng = np.random.default_rng(seed)
     out = np.empty((n, d))
     total = n_burnin + n * n_thinning
     k = 0
     for it in range(total):
         r = N @ rng.standard_normal(N.shape[1])
-        r /= np.linalg.norm(r)
+        nr = np.linalg.norm(r)
+        if nr == 0.0:
+            continue
+        r /= nr
         Ar = A @ r
         slack = b - A @ x
         with np.errstate(divide="ignore"):
@@ -322,12 +399,14 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     init = initialize_q_batch if getattr(acqf, "log_acqf", False) else initialize_q_batch_nonneg
     X0, _ = init(X_raw, Y_raw, num_restarts, gen)
 
-    # 4. restarts, chunks of batch_limit, scipy on host with device value+gradient
+    # 4. restarts, chunks of batch_limit, L-BFGS-B (box) / SLSQP (linear constraints) on host
+    #    with the analytic device value+gradient
     t0 = time.perf_counter()
-    lb = np.tile(bounds[0], batch_limit)
-    ub = np.tile(bounds[1], batch_limit)
     results = []
     chunks = [(s, min(num_restarts, s + batch_limit)) for s in range(0, num_restarts, batch_limit)]
+    optimizer = options.get("optimizer") or os.environ.get("EVR_OPTIMIZER", "native")
+    if optimizer not in ("native", "scipy"):
+        raise ValueError(f"optimizer must be 'native' or 'scipy', got {optimizer!r}")
 
     def evaluate(X: np.ndarray, with_grad: bool):
         """Sharded over ranks: each rank runs its slice of the restarts on its GPU, then the
@@ -357,16 +436,22 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         host_values(torch.from_numpy(full[:, 0]))
         return full[:, 0], (full[:, 1:] if with_grad else None)
 
-    # Independent chunks (batch_limit < num_restarts) are separate scipy problems in the
+    # Independent chunks (batch_limit < num_restarts) are separate problems in the
     # reference: with at least as many chunks as ranks each rank owns whole chunks and runs
     # them with no per-iteration collective; a single joint chunk is evaluated sharded.
     own_chunks = world > 1 and len(chunks) >= world
     local_world = 1 if own_chunks else world
-    for ci, (s0, s1) in enumerate(chunks):
-        if own_chunks and ci % world != rank:
-            continue
+
+    def run_chunk(s0: int, s1: int):
         nb = s1 - s0
         x0 = X0[s0:s1].reshape(-1)
+        lbv, ubv = np.tile(bounds[0], nb), np.tile(bounds[1], nb)
+        cons = _scipy_constraints(inequality_constraints, equality_constraints, nb, d)
+        if not cons and optimizer == "native" and local_world == 1 and hasattr(acqf, "plan"):
+            # the whole L-BFGS-B loop in C++ on the device plan (no Python per iteration)
+            Xc, vals, info = acqf.plan(nb, True).minimize(x0, lbv, ubv, maxiter)
+            return vals, Xc.reshape(nb, d), {"restarts": nb, "evals": info[1], "nit": info[0], "status": info[2],
+                                             "driver": "native-plan"}
         counter = {"n": 0}
 
         def f(x):
@@ -382,20 +467,39 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             counter["n"] += 1
             return -float(a.sum()), -g.reshape(-1)
 
-        bnds = list(zip(np.tile(bounds[0], nb), np.tile(bounds[1], nb)))
-        cons = _scipy_constraints(inequality_constraints, equality_constraints, nb, d)
-        method = "SLSQP" if cons else "L-BFGS-B"
-        res = minimize(f, x0, jac=True, method=method, bounds=bnds, constraints=cons or (),
-                       options={"maxiter": maxiter})
+        if cons:
+            res = minimize(f, x0, jac=True, method="SLSQP", bounds=list(zip(lbv, ubv)), constraints=cons,
+                           options={"maxiter": maxiter})
+            drv = "scipy-slsqp"
+        elif optimizer == "native":
+            res = minimize_lbfgsb(f, x0, lbv, ubv, maxiter=maxiter)
+            drv = "native"
+        else:
+            res = minimize(f, x0, jac=True, method="L-BFGS-B", bounds=list(zip(lbv, ubv)),
+                           options={"maxiter": maxiter})
+            drv = "scipy"
         Xc = np.clip(res.x.reshape(nb, d), bounds[0], bounds[1])
         if local_world == 1:
             vals = host_values(acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)))
         else:
             vals, _ = evaluate(Xc, False)
-        stats.opt_evals += counter["n"] * nb + nb
-        stats.opt_iters += int(getattr(res, "nit", 0))
-        stats.chunks.append({"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
-                             "status": int(res.status)})
+        return vals, Xc, {"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
+                          "status": int(res.status), "driver": drv}
+
+    err: Optional[BaseException] = None
+    for ci, (s0, s1) in enumerate(chunks):
+        if own_chunks and ci % world != rank:
+            continue
+        try:
+            vals, Xc, info = run_chunk(s0, s1)
+        except Exception as e:   # noqa: BLE001 — re-raised on every rank after the exchange below
+            if not own_chunks:
+                raise
+            err = e
+            break
+        stats.opt_evals += info["evals"] * info["restarts"] + info["restarts"]
+        stats.opt_iters += info["nit"]
+        stats.chunks.append(info)
         results.append((vals, Xc))
     if results:
         vals = np.concatenate([r[0] for r in results])
@@ -404,13 +508,24 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         best_v, best_x = float(vals[k]), Xs[k]
     else:
         best_v, best_x = -np.inf, np.zeros(d)
-    if own_chunks:   # all-gather every rank's best (value, x) over RCCL; argmax (ties -> lowest rank)
-        loc = torch.tensor(np.r_[best_v, best_x], dtype=torch.float64, device=dev)
+    if own_chunks:
+        # all-gather every rank's (error flag, best value, x) over RCCL; a failure on any rank
+        # raises on every rank (no rank is left waiting in a collective); argmax, ties -> lowest rank
+        flag = 0.0 if err is None else (2.0 if _is_notpsd(err) else 1.0)
+        loc = torch.tensor(np.r_[flag, best_v, best_x], dtype=torch.float64, device=dev)
         bufs = [torch.empty_like(loc) for _ in range(world)]
         dist.all_gather(bufs, loc)
         allv = torch.stack(bufs).cpu().numpy()
-        k = int(np.argmax(allv[:, 0]))
-        best_v, best_x = float(allv[k, 0]), allv[k, 1:]
+        if (allv[:, 0] > 0).any():
+            if err is not None:
+                raise err
+            bad = [int(r) for r in np.nonzero(allv[:, 0] > 0)[0]]
+            if (allv[bad, 0] == 2.0).all():
+                from .ops import NotPSDError
+                raise NotPSDError(f"acquisition not p.d. on rank(s) {bad} (restart chunk)")
+            raise RuntimeError(f"restart optimisation failed on rank(s) {bad}")
+        k = int(np.argmax(allv[:, 1]))
+        best_v, best_x = float(allv[k, 1]), allv[k, 2:]
         cnt = torch.tensor([stats.opt_evals], dtype=torch.float64, device=dev)
         dist.all_reduce(cnt)
         stats.opt_evals_global = int(cnt.item())
@@ -418,6 +533,11 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         stats.opt_evals_global = stats.opt_evals
     stats.t_opt += time.perf_counter() - t0
     return best_x, best_v, stats
+
+
+def _is_notpsd(e: BaseException) -> bool:
+    from .ops import NotPSDError
+    return isinstance(e, NotPSDError)
 
 
 def optimize_acqf_mixed(acqf, bounds: np.ndarray, fixed_features_list: Sequence[dict], num_restarts: int,

@@ -241,6 +241,43 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* plan);
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* plan);
 
+/* ---- acquisition restarts: native L-BFGS-B ------------------------------------------
+ * Restatement of the bound-constrained L-BFGS-B (v3.0: Cauchy point, direct primal
+ * subspace step with projection / backtracking, More-Thuente line search) that
+ * scipy.optimize.minimize(method="L-BFGS-B") runs inside [upstream] botorch
+ * gen_candidates_scipy, called by optimize_acqf from
+ * bofire/strategies/predictives/botorch.py:384-405 (box bounds, no linear constraints).
+ * Host-only.  Reverse communication: evr_lbfgsb_start returns EVR_LBFGSB_FG with the
+ * (projected) x to evaluate; evr_lbfgsb_step(f, g at x) returns the next task and x.
+ * m: corrections (scipy maxcor 10), factr = ftol / eps (1e7), pgtol (1e-5), maxls (20). */
+#define EVR_LBFGSB_FG 1
+#define EVR_LBFGSB_NEW_X 2
+#define EVR_LBFGSB_CONV_PGTOL 3
+#define EVR_LBFGSB_CONV_FACTR 4
+#define EVR_LBFGSB_ABNORMAL 5
+#define EVR_LBFGSB_ERROR 6
+typedef struct evr_lbfgsb evr_lbfgsb;
+int evr_lbfgsb_create(int n, int m, const double* lb, const double* ub, double factr, double pgtol, int maxls,
+                      evr_lbfgsb** out);
+int evr_lbfgsb_start(evr_lbfgsb* h, const double* x0, double* x);
+int evr_lbfgsb_step(evr_lbfgsb* h, double f, const double* g, double* x);
+void evr_lbfgsb_stats(const evr_lbfgsb* h, int* nit, int* nfev, double* f, double* pgnorm);
+void evr_lbfgsb_destroy(evr_lbfgsb* h);
+
+/* One joint restart problem driven natively on a backward plan: minimise
+ * -sum_r acq(x_r) over the b restarts of `plan` in the box [lb, ub] (b*d host arrays each)
+ * from x0 (b*d host), with scipy's wrapper rules (stop after maxiter iterations or more
+ * than maxfun evaluations).  Each evaluation is one pinned H2D of x, one plan launch and
+ * one D2H of [acq | dX] on `stream`, with no Python in the loop.  Outputs (host): x (b*d,
+ * clipped to the box), acq (b) at x, info[4] = {iterations, evaluations, status (0
+ * converged, 1 iteration/evaluation limit, 2 abnormal line search), last task}.
+ * Returns EVR_ERR_NOTPSD when an evaluation yields NaN (a new-point posterior block not
+ * p.d. after the jitter ladder: [upstream] NotPSDError). */
+#define EVR_ERR_NOTPSD 7
+int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* plan, const double* x0, const double* lb,
+                             const double* ub, int maxiter, int maxfun, double factr, double pgtol, int m,
+                             int maxls, double* x, double* acq, int* info);
+
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+
  * with sd from psd_safe_cholesky (3 tries) of the posterior variance; gR (nullable) =

@@ -83,15 +83,21 @@ def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
     return torch.stack(means, -1), torch.stack(covs, -3)
 
 
-def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0):
+def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0, chunk: int = 0):
     """prune_inferior_points_multi_objective restated.  z_prune: S' x n x m.  Returns the
-    kept row indices (sorted, unique) into Xn."""
+    kept row indices (sorted, unique) into Xn.  ``chunk`` > 0 walks the S' draws in chunks
+    (same counts; bounds the n x n dominance tensors at BASELINE sizes)."""
     mean, cov = joint_posterior(models, Xn)                    # n x m, m x n x n
     L, _ = psd_safe_cholesky(cov)                              # m x n x n
-    Y = mean.unsqueeze(0) + torch.einsum("jik,skj->sij", L, z_prune)
-    obj = objective(Y)
-    pareto = is_non_dominated(obj, deduplicate=False) & (obj > ref).all(-1)
-    probs = pareto.to(torch.float64).mean(0)
+    Sp = z_prune.shape[0]
+    step = chunk if chunk > 0 else Sp
+    counts = torch.zeros(Xn.shape[0], dtype=torch.float64)
+    for s0 in range(0, Sp, step):
+        Y = mean.unsqueeze(0) + torch.einsum("jik,skj->sij", L, z_prune[s0:s0 + step])
+        obj = objective(Y)
+        pareto = is_non_dominated(obj, deduplicate=False) & (obj > ref).all(-1)
+        counts += pareto.to(torch.float64).sum(0)
+    probs = counts / Sp
     idx = probs.nonzero().view(-1)
     max_points = math.ceil(max_frac * Xn.shape[0])
     if idx.shape[0] > max_points:

@@ -63,3 +63,26 @@ def device_gp(X, Y, lo, hi, hyp, kind=0, device="cuda"):
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)  # noqa: E731
     Xn = t((X - lo) / (hi - lo))
     return GPBatch(Xn, t(Y), hypers, kind, t(lo), t(hi))
+
+
+def mixed_domain(n_cont: int = 4, n_cat: int = 4, levels: int = 7):
+    """BASELINE configs[4]: 4 continuous inputs + 4 categoricals x 7 levels (one-hot ->
+    d_eff = 32), one minimised output (same domain as tools/bench_config5.py)."""
+    import everest_amd.data_models as dm
+
+    cont = [dm.ContinuousInput(key=f"x{i}", bounds=(0, 1)) for i in range(n_cont)]
+    cats = [dm.CategoricalInput(key=f"c{i}", categories=[f"l{k}" for k in range(levels)]) for i in range(n_cat)]
+    out = dm.Outputs(features=[dm.ContinuousOutput(key="y", objective=dm.MinimizeObjective(w=1.0))])
+    return dm.Domain(inputs=dm.Inputs(features=cont + cats), outputs=out)
+
+
+def mixed_f(df, n_cont: int = 4, n_cat: int = 4, levels: int = 7):
+    """Synthetic response of the mixed domain: a smooth continuous part plus a random
+    per-category offset."""
+    rng = np.random.default_rng(123)
+    w = rng.normal(size=(n_cat, levels))
+    x = df[[f"x{i}" for i in range(n_cont)]].values
+    y = ((x - 0.3) ** 2).sum(1) + np.sin(3 * x[:, 0]) * x[:, 1]
+    for i in range(n_cat):
+        y = y + w[i][df[f"c{i}"].map(lambda s: int(s[1:])).values]
+    return y

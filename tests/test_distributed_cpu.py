@@ -77,3 +77,81 @@ def test_boltzmann_init_nonneg_semantics():
     assert len(Xs) == 5 and 19.0 in Xs[:, 0]            # the max is always included
     Xs, a = initialize_q_batch_nonneg(X, np.zeros(20), 5, gen)   # all non-positive -> random
     assert len(Xs) == 5
+
+
+class HostEvalAcq(OracleAcq):
+    """Stand-in with the device acquisitions' ``eval_host`` round trip (the branch the
+    single-rank GPU ask takes, optim.run_chunk) next to forward / forward_backward (the
+    branch the sharded joint evaluation takes)."""
+
+    def eval_host(self, x, backward):
+        a, g = self.forward_backward(torch.as_tensor(x))
+        return a.numpy(), (g.numpy() if backward else None)
+
+
+class FlakyAcq(OracleAcq):
+    """NaN acquisition values (a failed jitter ladder) on rank 1's restart chunks only."""
+
+    def forward_backward(self, X):
+        a, g = super().forward_backward(X)
+        if dist.is_initialized() and dist.get_rank() == 1:
+            a = torch.full_like(a, float("nan"))
+        return a, g
+
+
+def _run_generic(rank, world, port, ret, acq_name, options):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from everest_amd.optim import optimize_acqf
+
+    acq = {"host": HostEvalAcq, "flaky": FlakyAcq}[acq_name]()
+    gen = torch.Generator().manual_seed(7)
+    bounds = np.array([[0.0] * 3, [1.0] * 3])
+    try:
+        x, v, st = optimize_acqf(acq, bounds, num_restarts=4, raw_samples=64, options=options, gen=gen, dist=dist)
+        ret[rank] = ("ok", x.tolist(), v)
+    except Exception as e:  # noqa: BLE001
+        ret[rank] = ("error", type(e).__name__, str(e))
+    dist.destroy_process_group()
+
+
+def _spawn(acq_name, options, timeout=120):
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    ctx = mp.start_processes(_run_generic, args=(2, _free_port(), ret, acq_name, options), nprocs=2, join=False,
+                             start_method="spawn")
+    deadline = timeout
+    import time
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > deadline:
+            for p in ctx.processes:
+                p.kill()
+            raise AssertionError("ranks did not finish: a collective is waiting on a rank that left")
+    return dict(ret)
+
+
+def test_eval_host_branch_matches_sharded_branch():
+    """The single-process eval_host path (native L-BFGS-B, Python callback) and the 2-rank
+    sharded joint chunk (all-gather of (value, grad) per iteration) take identical steps."""
+    from everest_amd.optim import optimize_acqf
+
+    gen = torch.Generator().manual_seed(7)
+    bounds = np.array([[0.0] * 3, [1.0] * 3])
+    opts = {"batch_limit": 4, "maxiter": 200}
+    x1, v1, st1 = optimize_acqf(HostEvalAcq(), bounds, num_restarts=4, raw_samples=64, options=opts, gen=gen)
+    assert st1.chunks[0]["driver"] == "native"
+    ret = _spawn("host", opts)
+    for r in range(2):
+        status, xr, vr = ret[r]
+        assert status == "ok"
+        assert np.allclose(xr, x1, atol=1e-12) and abs(vr - v1) < 1e-14
+
+
+def test_own_chunk_failure_raises_on_every_rank():
+    """batch_limit < num_restarts: each rank optimises its own chunks with no per-iteration
+    collective; a NotPSD failure on rank 1 must raise on both ranks (not leave rank 0 waiting
+    in the final all-gather)."""
+    ret = _spawn("flaky", {"batch_limit": 1, "maxiter": 50})
+    assert ret[0][0] == "error" and ret[1][0] == "error"
+    assert ret[0][1] == "NotPSDError" and ret[1][1] == "NotPSDError"
