@@ -45,6 +45,16 @@ class EvrQnehviModel(ctypes.Structure):
     ]
 
 
+class EvrQnGeneral(ctypes.Structure):
+    _fields_ = [
+        ("q", c_int), ("m_obj", c_int),
+        ("obj_out", c_void_p), ("obj_kind", c_void_p), ("obj_p0", c_void_p), ("obj_p1", c_void_p),
+        ("n_con", c_int),
+        ("con_out", c_void_p), ("con_sign", c_void_p), ("con_thr", c_void_p), ("con_eta", c_void_p),
+        ("zq", c_void_p),
+    ]
+
+
 _SIGS = {
     "evr_version": ([], c_int),
     "evr_last_error": ([], c_char_p),
@@ -118,6 +128,11 @@ _SIGS = {
     "evr_lbfgsb_destroy": ([c_void_p], None),
     "evr_qnehvi_plan_minimize": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
                                   c_double, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "evr_qng_workspace_doubles": ([POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
+                                   POINTER(EvrQnehviModel), c_int, c_int], c_longlong),
+    "evr_qng_eval": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
+                      POINTER(EvrQnehviModel), c_int] + [c_void_p] * 5, c_int),
+    "evr_objective_general": ([c_void_p, c_int, c_int, c_int, POINTER(EvrQnGeneral)] + [c_void_p] * 4, c_int),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),

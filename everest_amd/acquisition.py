@@ -89,6 +89,27 @@ def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None
                      lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64)), "host"
 
 
+def _make_spec(m: int, obj_a, obj_b, objective, constraints) -> ops.GeneralSpec:
+    """Objective / constraint description: explicit ``objective`` [(output, kind, p0, p1)],
+    else one affine objective a_j*y_j + b_j per output."""
+    if objective is None:
+        a = np.asarray(obj_a, dtype=np.float64).reshape(-1)
+        b = np.asarray(obj_b, dtype=np.float64).reshape(-1)
+        if a.shape[0] != m or b.shape[0] != m:
+            raise ValueError(f"obj_a / obj_b need one entry per model output ({m})")
+        objective = [(j, ops.OBJ_AFFINE, a[j], b[j]) for j in range(m)]
+    return ops.GeneralSpec(m, objective, constraints or ())
+
+
+def _fast_affine(spec: ops.GeneralSpec, m: int, dev):
+    """obj_a / obj_b of the q = 1 fast path (identity placeholders when it does not apply)."""
+    f64 = dict(dtype=torch.float64, device=dev)
+    if spec.affine_identity:
+        return (torch.tensor([o[2] for o in spec.objectives], **f64),
+                torch.tensor([o[3] for o in spec.objectives], **f64))
+    return torch.ones(m, **f64), torch.zeros(m, **f64)
+
+
 @dataclass
 class ConstructionStats:
     n_train: int
@@ -109,6 +130,10 @@ class _BoxHviAcqf:
         expanded once, on the device)."""
         if not (tau_relu > 0 and tau_max > 0):
             raise ValueError("tau_relu and tau_max must be positive")
+        if not self.spec.affine_identity or self._pending_rows() is not None:
+            raise NotImplementedError("the log-space acquisitions (qLogNEHVI / qLogEHVI) run affine objectives on "
+                                      "every output, without output constraints or qEHVI pending points, on the "
+                                      "device; use qNEHVI / qEHVI for those")
         lo, hi = self.cells.explicit()
         st = _native.EvrQnehviState.from_buffer_copy(self.state)
         st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
@@ -121,8 +146,80 @@ class _BoxHviAcqf:
         self.log_acqf = True      # may be negative: optimize_acqf uses initialize_q_batch
         self._plans = {}
 
+    @property
+    def supports_plan(self) -> bool:
+        """q = 1 candidates through the fused fast path (native plan / hipGraph): every
+        output carries one affine objective and there are no output constraints."""
+        return self.spec.affine_identity
+
+    def _init_general(self, spec: ops.GeneralSpec, cells, nk: int, nb_rows: int, no_h: bool = False):
+        """States of the general evaluation (qnehvi_general.hip): model side over the m
+        outputs, scan side over the m_obj objectives and the cells."""
+        gp, m = self.gp, self.m
+        self.spec = spec
+        self._zq_cache = {}
+        if spec.affine_identity:
+            self.state_model = self.state_scan = self.state
+        else:
+            ones = torch.ones(max(m, spec.m_obj), dtype=torch.float64, device=self.dev)
+            self._dummy = (ones, torch.zeros_like(ones))
+            self.state_model = ops.make_state(nk, nb_rows, self.S, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq,
+                                              ones, ones, cells, no_h=no_h)
+            self.state_scan = ops.make_state(nk, nb_rows, self.S, spec.m_obj, ones, ones, ones, ones, self.zq,
+                                             ones, ones, cells, no_h=no_h)
+
+    def _zq(self, q: int) -> torch.Tensor:
+        """S x q x m base samples of q new points (cached per q)."""
+        z = self._zq_cache.get(q)
+        if z is None:
+            z = self._draw_zq(q).to(dtype=torch.float64, device=self.dev).reshape(self.S, q, self.m).contiguous()
+            self._zq_cache[q] = z
+        return z
+
+    def set_new_point_samples(self, q: int, z: torch.Tensor):
+        """Inject the S x q x m base samples of q new points (parity tests)."""
+        self._zq_cache[int(q)] = z.to(dtype=torch.float64, device=self.dev).reshape(self.S, q, self.m).contiguous()
+
+    def _pending_rows(self) -> Optional[torch.Tensor]:
+        return None
+
+    def _general(self, X: torch.Tensor, backward: bool, gout: Optional[torch.Tensor] = None):
+        """X: b x q x d -> (acq (b), dX b x q x d | None) through evr_qng_eval; fixed pending
+        points (qEHVI) join every candidate's joint batch."""
+        if getattr(self, "log_acqf", False):
+            raise NotImplementedError("q > 1 / output constraints / CloseToTarget for the log-space "
+                                      "acquisitions (qLogNEHVI, qLogEHVI) are not implemented on the device")
+        b, q, d = X.shape
+        Xp = self._pending_rows()
+        qq = q
+        if Xp is not None:
+            X = torch.cat([X, Xp.unsqueeze(0).expand(b, Xp.shape[0], d)], 1)
+            qq = X.shape[1]
+        if qq > 8:
+            raise ValueError(f"joint batch of {qq} points (q + pending) exceeds the device limit of 8")
+        g = self.spec.struct(qq, self._zq(qq))
+        acq, dX = ops.qng_eval(self.state_model, self.state_scan, g, self.model, X.reshape(b * qq, d).contiguous(),
+                               backward, gout)
+        if dX is not None:
+            dX = dX.view(b, qq, d)[:, :q].contiguous()
+        return acq, dX
+
+    def _split(self, X: torch.Tensor):
+        """(X as b x q x d, squeeze-back flag): 2-D input is q = 1."""
+        X = X.to(device=self.dev, dtype=torch.float64)
+        if X.dim() == 2:
+            return X.unsqueeze(1), True
+        if X.dim() != 3:
+            raise ValueError(f"candidates must be b x d or b x q x d, got {tuple(X.shape)}")
+        return X, False
+
+    def _fast(self, X3: torch.Tensor) -> bool:
+        return X3.shape[1] == 1 and self.supports_plan and self._pending_rows() is None
+
     def plan(self, b: int, backward: bool) -> ops.QnehviPlan:
         """Native evaluation plan for batch size b (cached; hipGraph unless EVR_GRAPH=0)."""
+        if not self.supports_plan:
+            raise NotImplementedError("the native plan covers q = 1 with affine objectives on every output")
         key = (int(b), bool(backward))
         p = self._plans.get(key)
         if p is None:
@@ -134,33 +231,46 @@ class _BoxHviAcqf:
         return p
 
     def forward(self, X: torch.Tensor, return_cache: bool = False):
-        """X: b x d raw (transformed) candidates on device -> acquisition values (b), through
-        the native plan (one C-ABI call); see forward_ops for the op-by-op chain."""
+        """X: b x d (q = 1) or b x q x d raw (transformed) candidates on device ->
+        acquisition values (b).  q = 1 with affine objectives runs the native plan (one C-ABI
+        call; see forward_ops for the op-by-op chain), everything else the general kernels."""
         if return_cache:
             return self.forward_ops(X, return_cache=True)
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        p = self.plan(X.shape[0], False)
-        p.X.copy_(X)
+        X3, _ = self._split(X)
+        if not self._fast(X3):
+            return self._general(X3, False)[0]
+        p = self.plan(X3.shape[0], False)
+        p.X.copy_(X3[:, 0])
         p.run()
         return p.acq.clone()
 
     def forward_backward(self, X: torch.Tensor, gout: Optional[torch.Tensor] = None):
-        """Returns (acq (b), d sum_c gout_c acq_c / dX (b x d)) through the native plan."""
+        """Returns (acq (b), d sum_c gout_c acq_c / dX (shaped like X))."""
+        X3, flat = self._split(X)
+        if not self._fast(X3):
+            acq, dX = self._general(X3, True, gout)
+            return acq, (dX[:, 0] if flat else dX)
         if gout is not None:
-            return self.forward_backward_ops(X, gout)
-        X = X.to(device=self.dev, dtype=torch.float64).contiguous()
-        p = self.plan(X.shape[0], True)
-        p.X.copy_(X)
+            acq, dX = self.forward_backward_ops(X3[:, 0], gout)
+            return acq, (dX if flat else dX.unsqueeze(1))
+        p = self.plan(X3.shape[0], True)
+        p.X.copy_(X3[:, 0])
         p.run()
-        return p.acq.clone(), p.dX.clone()
+        return p.acq.clone(), (p.dX.clone() if flat else p.dX.clone().unsqueeze(1))
 
     def eval_host(self, x: np.ndarray, backward: bool):
-        """Host round trip for the scipy optimiser: x (b x d numpy) -> (acq, dX or None)
-        numpy, one pinned H2D copy, one plan launch, one D2H copy."""
+        """Host round trip for the scipy optimiser: x (b x d or b x q x d numpy) -> (acq,
+        dX or None) numpy; q = 1 fast path: one pinned H2D copy, one plan launch, one D2H."""
         b = x.shape[0]
-        out = self.plan(b, backward).run_host(x)
-        acq = out[:b].copy()
-        return acq, (out[b:].reshape(b, -1).copy() if backward else None)
+        if x.ndim == 2 and self.supports_plan and self._pending_rows() is None:
+            out = self.plan(b, backward).run_host(x)
+            acq = out[:b].copy()
+            return acq, (out[b:].reshape(b, -1).copy() if backward else None)
+        Xt = torch.as_tensor(x, dtype=torch.float64, device=self.dev)
+        if backward:
+            a, g = self.forward_backward(Xt)
+            return a.cpu().numpy(), g.cpu().numpy()
+        return self.forward(Xt).cpu().numpy(), None
 
     def _cross(self, X: torch.Tensor) -> torch.Tensor:
         """K(X_k, normalize(X)) : m x nk x b over the training (+ pending) rows."""
@@ -211,7 +321,7 @@ class QNEHVI(_BoxHviAcqf):
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
                  num_threads: Optional[int] = None, box_device: Optional[bool] = None,
                  kd_scan: Optional[bool] = None, X_pending_raw: Optional[np.ndarray] = None,
-                 root: Optional[str] = None):
+                 root: Optional[str] = None, objective=None, constraints=()):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -219,9 +329,14 @@ class QNEHVI(_BoxHviAcqf):
         n = gp.n
         self.m, self.n, self.S = m, n, int(S)
         f64 = dict(dtype=torch.float64, device=dev)
+        spec = _make_spec(m, obj_a, obj_b, objective, constraints)
+        self.spec = spec
         self.ref = torch.as_tensor(np.asarray(ref_point, dtype=np.float64), **f64)
-        self.obj_a = torch.as_tensor(np.asarray(obj_a, dtype=np.float64), **f64)
-        self.obj_b = torch.as_tensor(np.asarray(obj_b, dtype=np.float64), **f64)
+        if self.ref.numel() != spec.m_obj:
+            raise ValueError(f"reference point has {self.ref.numel()} entries for {spec.m_obj} objectives")
+        self.obj_a, self.obj_b = _fast_affine(spec, m, dev)
+        self.sampler_seed = int(sampler_seed)
+        self._z_new_full = z_new_full
         # baseline rows -> training rows (exact match of the transformed inputs)
         X_train_raw = np.asarray(X_train_raw, dtype=np.float64)
         X_baseline_raw = np.asarray(X_baseline_raw, dtype=np.float64)
@@ -272,7 +387,7 @@ class QNEHVI(_BoxHviAcqf):
             else:
                 Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()
             Yp = ops.gemm(Lp, Zp)
-            Op = ops.objective_affine(Yp, mu_c, self.obj_a, self.obj_b)
+            Op = self._objective(Yp, mu_c)
             _, counts = ops.pareto_mask(Op, self.ref, dedup=False, want_mask=False, want_counts=True)
             probs = counts.cpu().numpy().astype(np.float64) / Zp.shape[2]
             tm["prune"] = _time.perf_counter() - t0
@@ -313,13 +428,13 @@ class QNEHVI(_BoxHviAcqf):
             else:
                 Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
             Yb = ops.gemm(self.L_base, Zb)
-            Ob = ops.objective_affine(Yb, mu_b, self.obj_a, self.obj_b)
+            Ob = self._objective(Yb, mu_b)
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
             t1 = _time.perf_counter()
             cells, self.box_path = _decompose(Ob, self.ref, box_device, kd_scan, num_threads)
             tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
-            cells = _single_cell(self.ref, S_, m)
+            cells = _single_cell(self.ref, S_, spec.m_obj)
             self.box_path = "none"
         self.cells = cells
         counts_c = cells.counts
@@ -377,6 +492,9 @@ class QNEHVI(_BoxHviAcqf):
         self.state = ops.make_state(nk, nb_rows, S_, m, gp.const, gp.ym, gp.ys, gp.kxx, self.zq, self.obj_a,
                                     self.obj_b, cells)
         self._keep = (self.zq, self.obj_a, self.obj_b)
+        self._init_general(spec, cells, nk, nb_rows)
+        if not spec.affine_identity:
+            self.state = self.state_scan
         self._lo_c = gp.lo.to(torch.float64).contiguous()
         self._scale_c = gp.inv_range.to(torch.float64).contiguous()
         self.model = _native.EvrQnehviModel(n=nk, d=gp.d, kind=gp.kind, Xn=self.Xk.data_ptr(), lengthscales=gp.ls.data_ptr(),
@@ -387,6 +505,23 @@ class QNEHVI(_BoxHviAcqf):
         tm["total"] = _time.perf_counter() - t0
         self.timings = tm
 
+
+    def _objective(self, Y: torch.Tensor, mu: torch.Tensor) -> torch.Tensor:
+        """m x P x S model samples (+ mean) -> m_obj x P x S objectives; infeasible samples
+        (output constraints) are set to the reference point."""
+        if self.spec.affine_identity:
+            return ops.objective_affine(Y, mu, self.obj_a, self.obj_b)
+        return ops.objective_general(Y, mu, self.spec, self.ref)
+
+    def _draw_zq(self, q: int) -> torch.Tensor:
+        """New-point base samples of a q-batch: rows nb .. nb+q-1 of the (nb+q)*m-dim draw of
+        the sampler seed ([upstream] _update_base_samples keeps the baseline rows)."""
+        nb, m = self.nb, self.m
+        if self._z_new_full is not None:
+            if self._z_new_full.shape[1] < nb + q:
+                raise ValueError(f"z_new_full has {self._z_new_full.shape[1]} rows, need {nb + q}")
+            return self._z_new_full[:, nb:nb + q, :]
+        return ops.sobol_normal(self.S, (nb + q) * m, self.sampler_seed, self.dev, d0=nb * m, nd=q * m)
 
 
 class QEHVI(_BoxHviAcqf):
@@ -407,31 +542,43 @@ class QEHVI(_BoxHviAcqf):
 
     def __init__(self, gp: GPBatch, Y_part: np.ndarray, ref_point, obj_a, obj_b, S: int = 512,
                  sampler_seed: int = 0, z: Optional[torch.Tensor] = None, box_device: Optional[bool] = None,
-                 kd_scan: Optional[bool] = None, num_threads: Optional[int] = None):
+                 kd_scan: Optional[bool] = None, num_threads: Optional[int] = None, objective=None,
+                 constraints=(), X_pending_raw: Optional[np.ndarray] = None):
+        """Y_part: points of the partition in objective space (m_obj columns); pending
+        points ([upstream] concatenate_pending_points) join every candidate's joint batch."""
         dev = gp.device
         self.gp, self.dev = gp, dev
         m, n = gp.B, gp.n
         self.m, self.n, self.S, self.nb, self.nk = m, n, int(S), 0, n
         f64 = dict(dtype=torch.float64, device=dev)
+        spec = _make_spec(m, obj_a, obj_b, objective, constraints)
+        self.spec = spec
+        mo = spec.m_obj
         self.ref = torch.as_tensor(np.asarray(ref_point, dtype=np.float64), **f64)
-        self.obj_a = torch.as_tensor(np.asarray(obj_a, dtype=np.float64), **f64)
-        self.obj_b = torch.as_tensor(np.asarray(obj_b, dtype=np.float64), **f64)
-        Y_part = np.asarray(Y_part, dtype=np.float64).reshape(-1, m)
+        if self.ref.numel() != mo:
+            raise ValueError(f"reference point has {self.ref.numel()} entries for {mo} objectives")
+        self.obj_a, self.obj_b = _fast_affine(spec, m, dev)
+        self.sampler_seed = int(sampler_seed)
+        Y_part = np.asarray(Y_part, dtype=np.float64).reshape(-1, mo)
         self.Xk = gp.Xn
         S_ = self.S
         if Y_part.shape[0] > 0:
-            O = torch.as_tensor(np.ascontiguousarray(Y_part.T), **f64)[:, :, None].expand(m, Y_part.shape[0], S_)
+            O = torch.as_tensor(np.ascontiguousarray(Y_part.T), **f64)[:, :, None].expand(mo, Y_part.shape[0], S_)
             cells, self.box_path = _decompose(O.contiguous(), self.ref, box_device, kd_scan, num_threads)
         else:
-            cells, self.box_path = _single_cell(self.ref, S_, m), "none"
+            cells, self.box_path = _single_cell(self.ref, S_, mo), "none"
         self.cells = cells
         cnt = cells.counts
         self.stats = ConstructionStats(n_train=n, n_base=0, total_cells=int(np.sum(cnt)),
                                        max_cells=int(cnt.max()) if len(cnt) else 0)
+        self._z1 = z
         if z is None:
             self.zq = ops.sobol_normal(S_, m, sampler_seed, dev)                  # S x m
         else:
             self.zq = z.reshape(S_, m).to(**f64).contiguous()
+        self.X_pending = None
+        if X_pending_raw is not None and np.asarray(X_pending_raw).shape[0] > 0:
+            self.X_pending = torch.as_tensor(np.asarray(X_pending_raw, dtype=np.float64).reshape(-1, gp.d), **f64)
         self.Rr = n + 1
         M = torch.empty(m, n + 1, n, **f64)
         M[:, :n].copy_(gp.Linv)
@@ -445,7 +592,19 @@ class QEHVI(_BoxHviAcqf):
                                             lengthscales=gp.ls.data_ptr(), shift=self._lo_c.data_ptr(),
                                             scale=self._scale_c.data_ptr(), M=self.M.data_ptr())
         self._plans = {}
+        self._init_general(spec, cells, n, 0, no_h=True)
+        if not spec.affine_identity:
+            self.state = self.state_scan
         torch.cuda.synchronize(dev)
+
+    def _pending_rows(self) -> Optional[torch.Tensor]:
+        return self.X_pending
+
+    def _draw_zq(self, q: int) -> torch.Tensor:
+        """S x (q*m) Sobol-normal draw of the joint batch (Sobol dim = point*m + output)."""
+        if q == 1 and self._z1 is not None:
+            return self.zq
+        return ops.sobol_normal(self.S, q * self.m, self.sampler_seed, self.dev)
 
 
 TAU_RELU = 1e-6     # [upstream] botorch.acquisition.logei.TAU_RELU

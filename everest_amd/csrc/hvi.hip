@@ -1359,3 +1359,55 @@ int evr_hvi_set_kd_variant(int variant) {
 }
 
 }  // extern "C"
+
+namespace evr {
+
+// Per-sample HVI partials for the general evaluation (qnehvi_general.hip): part = work
+// (S x nsplit x b, summed over the splits in order gives HVI_s(c)) and, with backward,
+// dG = d(sum_s HVI_s)/dG / S (gout = 1).  Linear scans only (log_hvi = 0).
+long long hvi_raw_workspace(const evr_qnehvi_state* st, int b, bool backward) {
+  if (!st || b <= 0) return 0;
+  if (st->grp_off) return hvi_kd_workspace(st, b);
+  HviPlan p = hvi_plan(st, b);
+  return (long long)st->S * p.nchunk * b * (backward ? st->m + 1 : 1);
+}
+
+int hvi_raw(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, bool backward, double* work,
+            double* dG, int* nsplit) {
+  if (int rc = hvi_check_state(st)) return rc;
+  EVR_CHECK(!st->log_hvi && work && G && nsplit && (!backward || dG), "hvi_raw: bad arguments");
+  if (b == 0) return 0;
+  int rc = 0;
+  if (st->grp_off) {
+    *nsplit = hvi_kd_nsplit(st, b);
+    if (backward) {
+#define L(MM) rc = hvi_kd_launch<MM, true>(s, st, b, G, nullptr, work, dG, nullptr, nullptr)
+      EVR_M_SWITCH(st->m, L);
+#undef L
+    } else {
+#define L(MM) rc = hvi_kd_launch<MM, false>(s, st, b, G, nullptr, work, nullptr, nullptr, nullptr)
+      EVR_M_SWITCH(st->m, L);
+#undef L
+    }
+    return rc;
+  }
+  HviPlan p = hvi_plan(st, b);
+  *nsplit = p.nchunk;
+  double* wb = work + (size_t)st->S * p.nchunk * b;
+  if (backward) {
+#define L(MM) rc = hvi_launch<MM, true>(s, st, b, p, G, work, wb)
+    EVR_M_SWITCH(st->m, L);
+#undef L
+    if (rc) return rc;
+    const long long tot = (long long)st->S * st->m * b;
+    hvi_reduce_bwd<<<cdiv(tot, 256), 256, 0, s>>>(st->S, p.nchunk, st->m, b, wb, nullptr, dG);
+    EVR_LAUNCH_CHECK();
+  } else {
+#define L(MM) rc = hvi_launch<MM, false>(s, st, b, p, G, work, nullptr)
+    EVR_M_SWITCH(st->m, L);
+#undef L
+  }
+  return rc;
+}
+
+}  // namespace evr

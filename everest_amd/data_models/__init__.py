@@ -1,6 +1,7 @@
-from .domain import (BaseModel, CategoricalInput, CloseToTargetObjective, Constraints, ConstraintNotFulfilledError,
+from .domain import (BaseModel, CategoricalInput, CloseToTargetObjective, ConstrainedObjective, Constraints, ConstraintNotFulfilledError,
                      ContinuousInput, ContinuousOutput, Domain, Inputs, LinearEqualityConstraint,
-                     LinearInequalityConstraint, MaximizeObjective, MinimizeObjective, Outputs)
+                     LinearInequalityConstraint, MaximizeObjective, MaximizeSigmoidObjective, MinimizeObjective,
+                     MinimizeSigmoidObjective, MovingMaximizeSigmoidObjective, Outputs, TargetObjective)
 from .models import (BotorchSurrogates, CategoricalEncodingEnum, CategoricalMethodEnum,
                      DimensionalityScaledLogNormalPrior, GammaPrior, LogNormalPrior, MaternKernel, NormalPrior,
                      QehviStrategy, QnehviStrategy, RandomStrategy, RBFKernel, ScalerEnum, SingleTaskGPSurrogate,

@@ -87,7 +87,64 @@ class CloseToTargetObjective(Objective):
         return -1.0 * (np.abs(np.asarray(x) - self.target_value) ** self.exponent)
 
 
-AnyObjective = Annotated[Union[MaximizeObjective, MinimizeObjective, CloseToTargetObjective],
+class ConstrainedObjective:
+    """Objectives that become BoTorch output constraints
+    (bofire/data_models/objectives/objective.py:36-37)."""
+
+
+def _sigmoid(z):
+    return 1.0 / (1.0 + np.exp(-z))
+
+
+class SigmoidObjective(Objective, ConstrainedObjective):
+    """bofire/data_models/objectives/sigmoid.py: steepness > 0, turning point tp."""
+    steepness: Annotated[float, Field(gt=0)]
+    tp: float
+    w: Annotated[float, Field(gt=0, le=1)] = 1.0
+
+
+class MaximizeSigmoidObjective(SigmoidObjective):
+    type: Literal["MaximizeSigmoidObjective"] = "MaximizeSigmoidObjective"
+
+    def __call__(self, x, x_adapt=None):
+        return _sigmoid(self.steepness * (np.asarray(x) - self.tp))
+
+
+class MinimizeSigmoidObjective(SigmoidObjective):
+    type: Literal["MinimizeSigmoidObjective"] = "MinimizeSigmoidObjective"
+
+    def __call__(self, x, x_adapt=None):
+        return 1.0 - _sigmoid(self.steepness * (np.asarray(x) - self.tp))
+
+
+class MovingMaximizeSigmoidObjective(SigmoidObjective):
+    """Turning point relative to the best observed value: tp' = max(x_adapt) + tp."""
+    type: Literal["MovingMaximizeSigmoidObjective"] = "MovingMaximizeSigmoidObjective"
+
+    def get_adjusted_tp(self, x) -> float:
+        return float(np.asarray(x).max()) + self.tp
+
+    def __call__(self, x, x_adapt):
+        return _sigmoid(self.steepness * (np.asarray(x) - self.get_adjusted_tp(x_adapt)))
+
+
+class TargetObjective(Objective, ConstrainedObjective):
+    """bofire/data_models/objectives/target.py: product of a rising sigmoid at
+    target - tolerance and a falling one at target + tolerance."""
+    type: Literal["TargetObjective"] = "TargetObjective"
+    w: Annotated[float, Field(gt=0, le=1)] = 1.0
+    target_value: float
+    tolerance: Annotated[float, Field(ge=0)]
+    steepness: Annotated[float, Field(gt=0)]
+
+    def __call__(self, x, x_adapt=None):
+        x = np.asarray(x)
+        return (_sigmoid(self.steepness * (x - (self.target_value - self.tolerance))) *
+                (1.0 - _sigmoid(self.steepness * (x - (self.target_value + self.tolerance)))))
+
+
+AnyObjective = Annotated[Union[MaximizeObjective, MinimizeObjective, CloseToTargetObjective, MaximizeSigmoidObjective,
+                               MinimizeSigmoidObjective, MovingMaximizeSigmoidObjective, TargetObjective],
                          Field(discriminator="type")]
 
 

@@ -299,6 +299,19 @@ class BotorchStrategy(Strategy):
         return self
 
 
+_MO_CONSTRAINED = ("MaximizeObjective", "MinimizeObjective", "MinimizeSigmoidObjective", "MaximizeSigmoidObjective",
+                   "TargetObjective", "CloseToTargetObjective")
+
+
+def _check_objectives(cls, domain: Domain, allowed) -> Domain:
+    """bofire/data_models/strategies/strategy.py:26-34 (is_objective_implemented)."""
+    for f in domain.outputs.get().features:
+        obj = getattr(f, "objective", None)
+        if obj is not None and type(obj).__name__ not in allowed:
+            raise ValueError(f"Objective `{type(obj)}` is not implemented for strategy `{cls.__name__}`")
+    return domain
+
+
 class MultiobjectiveStrategy(BotorchStrategy):
     @field_validator("domain")
     @classmethod
@@ -317,6 +330,12 @@ class QehviStrategy(MultiobjectiveStrategy):
     type: Literal["QehviStrategy"] = "QehviStrategy"
     num_sobol_samples: IntPowerOfTwo = 512
     ref_point: Optional[Dict[str, float]] = None
+
+    @field_validator("domain")
+    @classmethod
+    def _objectives(cls, v):
+        """bofire/data_models/strategies/predictives/qehvi.py:53-67."""
+        return _check_objectives(cls, v, ("MaximizeObjective", "MinimizeObjective"))
 
     @field_validator("num_sobol_samples")
     @classmethod
@@ -338,12 +357,24 @@ class QnehviStrategy(QehviStrategy):
     type: Literal["QnehviStrategy"] = "QnehviStrategy"
     alpha: Annotated[float, Field(ge=0, le=0.5)] = 0.0
 
+    @field_validator("domain")
+    @classmethod
+    def _objectives(cls, v):
+        """bofire/data_models/strategies/predictives/qnehvi.py:21-39."""
+        return _check_objectives(cls, v, _MO_CONSTRAINED)
+
 
 class MoboStrategy(MultiobjectiveStrategy):
     """bofire/data_models/strategies/predictives/mobo.py:24-80."""
     type: Literal["MoboStrategy"] = "MoboStrategy"
     ref_point: Optional[Dict[str, float]] = None
     acquisition_function: AnyMultiObjectiveAcquisitionFunction = Field(default_factory=qLogNEHVI)
+
+    @field_validator("domain")
+    @classmethod
+    def _objectives(cls, v):
+        """bofire/data_models/strategies/predictives/mobo.py:60-80."""
+        return _check_objectives(cls, v, _MO_CONSTRAINED)
 
     @model_validator(mode="after")
     def _ref(self):

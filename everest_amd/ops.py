@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _native
-from ._native import EvrQnehviState, call
+from ._native import EvrQnehviState, EvrQnGeneral, call
 
 KERNELS = {"rbf": 0, "matern05": 1, "matern15": 2, "matern25": 3}
 KIND_BY_NU = {0.5: 1, 1.5: 2, 2.5: 3}
@@ -328,6 +328,94 @@ def qnehvi_project_backward(st: EvrQnehviState, M: torch.Tensor, R: torch.Tensor
     call("evr_qnehvi_project_backward", _stream(), ctypes.byref(st), b, M.data_ptr(), R.data_ptr(), L22.data_ptr(),
          dG.data_ptr(), dK.data_ptr(), work.data_ptr())
     return dK
+
+
+OBJ_AFFINE, OBJ_CLOSE_TO_TARGET = 0, 1
+
+
+class GeneralSpec:
+    """Objectives over selected model outputs and output constraints for the general
+    qNEHVI / qEHVI kernels (qnehvi_general.hip, evr_qn_general).
+
+    objectives: [(output, kind, p0, p1)] — kind OBJ_AFFINE: g = p0*y + p1 (Maximize /
+    Minimize, bofire/utils/torch_tools.py:389-398), OBJ_CLOSE_TO_TARGET: g = -|y - p0|^p1
+    (:399-402).  constraints: [(output, sign, threshold, eta)] — c = sign*(y - threshold)
+    <= 0 is feasible, weight exp(sum logsigmoid(-c/eta)) (torch_tools.py:258-337)."""
+
+    def __init__(self, m_model: int, objectives, constraints=()):
+        self.m_model = int(m_model)
+        self.objectives = [(int(o), int(k), float(a), float(b)) for o, k, a, b in objectives]
+        self.constraints = [(int(o), float(sg), float(t), float(e)) for o, sg, t, e in constraints]
+        if not 1 <= len(self.objectives) <= 8 or len(self.constraints) > 16:
+            raise ValueError("general qNEHVI: 1..8 objectives and at most 16 output constraints")
+        for o, *_ in self.objectives + self.constraints:
+            if not 0 <= o < self.m_model:
+                raise ValueError(f"general qNEHVI: output index {o} outside the model's {self.m_model} outputs")
+        ob = self.objectives
+        self._arrs = (np.array([o[0] for o in ob], np.int32), np.array([o[1] for o in ob], np.int32),
+                      np.array([o[2] for o in ob], np.float64), np.array([o[3] for o in ob], np.float64))
+        cs = self.constraints or [(0, 0.0, 0.0, 1.0)]
+        self._carrs = (np.array([c[0] for c in cs], np.int32), np.array([c[1] for c in cs], np.float64),
+                       np.array([c[2] for c in cs], np.float64), np.array([c[3] for c in cs], np.float64))
+
+    @property
+    def m_obj(self) -> int:
+        return len(self.objectives)
+
+    @property
+    def affine_identity(self) -> bool:
+        """Every output carries one affine objective, in output order, and no constraints:
+        the q = 1 fast path (obj_a / obj_b fused into the sampling kernel) applies."""
+        return (not self.constraints and self.m_obj == self.m_model and
+                all(o == j and k == OBJ_AFFINE for j, (o, k, _, _) in enumerate(self.objectives)))
+
+    def struct(self, q: int = 1, zq: Optional[torch.Tensor] = None) -> EvrQnGeneral:
+        g = EvrQnGeneral()
+        g.q, g.m_obj, g.n_con = int(q), self.m_obj, len(self.constraints)
+        g.obj_out, g.obj_kind, g.obj_p0, g.obj_p1 = (a.ctypes.data for a in self._arrs)
+        g.con_out, g.con_sign, g.con_thr, g.con_eta = (a.ctypes.data for a in self._carrs)
+        g.zq = _p(zq)
+        return g
+
+    def host_objective(self, Y: np.ndarray) -> np.ndarray:
+        """Objectives of model-output rows Y (... x m_model) on the host (observed data)."""
+        cols = []
+        for o, k, a, b in self.objectives:
+            y = Y[..., o]
+            cols.append(a * y + b if k == OBJ_AFFINE else -np.abs(y - a) ** b)
+        return np.stack(cols, -1)
+
+
+def objective_general(Y: torch.Tensor, mu: Optional[torch.Tensor], spec: GeneralSpec, ref: torch.Tensor):
+    """Y: m_model x n x S (+ mu m_model x n) -> objectives m_obj x n x S, infeasible samples
+    (any constraint c > 0) set to the reference point."""
+    Y = _dev(Y, "Y")
+    m, n, S = Y.shape
+    O = torch.empty(spec.m_obj, n, S, dtype=torch.float64, device=Y.device)
+    g = spec.struct()
+    call("evr_objective_general", _stream(), m, n, S, ctypes.byref(g), Y.data_ptr(),
+         _p(None if mu is None else _dev(mu, "mu")), _dev(ref, "ref").data_ptr(), O.data_ptr())
+    return O
+
+
+def qng_eval(stm: EvrQnehviState, sth: EvrQnehviState, g: EvrQnGeneral, model: "_native.EvrQnehviModel",
+             X: torch.Tensor, backward: bool, gout: Optional[torch.Tensor] = None):
+    """General qNEHVI / qEHVI: X (b*q) x d raw candidates (point i of candidate c at row
+    c*q + i) -> acq (b) [, dX (b*q) x d]."""
+    X = _dev(X, "X")
+    q = int(g.q)
+    bq, d = X.shape
+    if bq % q:
+        raise ValueError(f"{bq} rows are not a multiple of q = {q}")
+    b = bq // q
+    lib = _native.load()
+    work = _workspace(lib.evr_qng_workspace_doubles(ctypes.byref(stm), ctypes.byref(sth), ctypes.byref(g),
+                                                    ctypes.byref(model), b, int(backward)), X.device)
+    acq = torch.empty(b, dtype=torch.float64, device=X.device)
+    dX = torch.empty_like(X) if backward else None
+    call("evr_qng_eval", _stream(), ctypes.byref(stm), ctypes.byref(sth), ctypes.byref(g), ctypes.byref(model), b,
+         X.data_ptr(), _p(None if gout is None else _dev(gout, "gout")), work.data_ptr(), acq.data_ptr(), _p(dX))
+    return acq, dX
 
 
 class QnehviPlan:

@@ -116,12 +116,15 @@ def minimize_lbfgsb(fun: Callable, x0: np.ndarray, lb: np.ndarray, ub: np.ndarra
     return LbfgsbResult(x=x, fun=f, nit=nit, nfev=nfev, status=status, message=msg)
 
 
-def draw_sobol_samples(bounds: np.ndarray, n: int, seed: int) -> np.ndarray:
-    """[upstream] botorch.utils.sampling.draw_sobol_samples (q=1)."""
+def draw_sobol_samples(bounds: np.ndarray, n: int, seed: int, q: int = 1) -> np.ndarray:
+    """[upstream] botorch.utils.sampling.draw_sobol_samples: one (q*d)-dimensional scrambled
+    Sobol draw of n points viewed as n x q x d (q = 1: n x d)."""
     lo, hi = bounds
-    eng = torch.quasirandom.SobolEngine(len(lo), scramble=True, seed=int(seed))
+    d = len(lo)
+    eng = torch.quasirandom.SobolEngine(q * d, scramble=True, seed=int(seed))
     u = eng.draw(n, dtype=torch.float64).numpy()
-    return lo + (hi - lo) * u
+    X = lo + (hi - lo) * u.reshape(n, q, d)
+    return X[:, 0] if q == 1 else X
 
 
 def _as_Ab(d: int, bounds: np.ndarray, ineq: Sequence[LinearConstraint]):
@@ -314,43 +317,52 @@ class _FixedFeatures:
         self.free = [j for j in range(d) if j not in fixed]
 
     def full_np(self, x: np.ndarray) -> np.ndarray:
-        X = np.empty((x.shape[0], self.d))
-        X[:, self.free] = x
-        X[:, self.fixed_idx] = self.fixed_val
+        X = np.empty(x.shape[:-1] + (self.d,))
+        X[..., self.free] = x
+        X[..., self.fixed_idx] = self.fixed_val
         return X
 
     def _full_t(self, X: torch.Tensor) -> torch.Tensor:
-        out = torch.empty(X.shape[0], self.d, dtype=torch.float64, device=self.dev)
-        out[:, self.free] = X.to(device=self.dev, dtype=torch.float64)
-        out[:, torch.as_tensor(self.fixed_idx, device=self.dev)] = torch.as_tensor(self.fixed_val, device=self.dev)
+        out = torch.empty(X.shape[:-1] + (self.d,), dtype=torch.float64, device=self.dev)
+        out[..., self.free] = X.to(device=self.dev, dtype=torch.float64)
+        out[..., torch.as_tensor(self.fixed_idx, device=self.dev)] = torch.as_tensor(self.fixed_val, device=self.dev)
         return out
+
+    @property
+    def supports_plan(self) -> bool:
+        return False
 
     def forward(self, X):
         return self.acqf.forward(self._full_t(X))
 
     def forward_backward(self, X):
         a, g = self.acqf.forward_backward(self._full_t(X))
-        return a, g[:, self.free]
+        return a, g[..., self.free]
 
     def eval_host(self, x: np.ndarray, backward: bool):
         if hasattr(self.acqf, "eval_host"):
             a, g = self.acqf.eval_host(self.full_np(x), backward)
-            return a, (g[:, self.free] if backward else None)
+            return a, (g[..., self.free] if backward else None)
         Xt = torch.as_tensor(self.full_np(x), dtype=torch.float64, device=self.dev)
         if backward:
             a, g = self.acqf.forward_backward(Xt)
-            return a.cpu().numpy(), g[:, self.free].cpu().numpy()
+            return a.cpu().numpy(), g[..., self.free].cpu().numpy()
         return self.acqf.forward(Xt).cpu().numpy(), None
 
 
 def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int, options: dict,
                   gen: torch.Generator, inequality_constraints: Sequence[LinearConstraint] = (),
                   equality_constraints: Sequence[LinearConstraint] = (), dist=None,
-                  stats: Optional[OptimizeStats] = None, fixed_features: Optional[dict] = None):
-    """Returns (best x (d,), best value, stats).  ``acqf`` exposes forward(X) and
-    forward_backward(X) on device tensors of raw (transformed) inputs.  ``fixed_features``
-    {column: value} are held fixed: raw samples get them set, the restarts optimise the free
-    columns only ([upstream] optimize_acqf(fixed_features=...))."""
+                  stats: Optional[OptimizeStats] = None, fixed_features: Optional[dict] = None, q: int = 1):
+    """Returns (best x, best value, stats); x is (d,) for q = 1, else the joint (q, d) batch
+    ([upstream] optimize_acqf(q=...), sequential=False).  ``acqf`` exposes forward(X) and
+    forward_backward(X) on device tensors of raw (transformed) inputs, X b x d (q = 1) or
+    b x q x d.  ``fixed_features`` {column: value} are held fixed: raw samples get them set,
+    the restarts optimise the free columns only ([upstream] optimize_acqf(fixed_features=...)).
+    Linear constraints apply to every point of a q-batch."""
+    q = int(q)
+    if q < 1:
+        raise ValueError("q must be >= 1")
     if fixed_features:
         bounds = np.asarray(bounds, dtype=np.float64)
         d_full = bounds.shape[1]
@@ -358,8 +370,9 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         wrap = _FixedFeatures(acqf, d_full, fx)
         x, v, st = optimize_acqf(wrap, bounds[:, wrap.free], num_restarts, raw_samples, options, gen,
                                  _reduce_constraints(inequality_constraints, fx, wrap.free),
-                                 _reduce_constraints(equality_constraints, fx, wrap.free), dist=dist, stats=stats)
-        return wrap.full_np(x[None, :])[0], v, st
+                                 _reduce_constraints(equality_constraints, fx, wrap.free), dist=dist, stats=stats,
+                                 q=q)
+        return wrap.full_np(x), v, st
     import time
 
     stats = stats or OptimizeStats()
@@ -375,9 +388,12 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     seed = int(torch.randint(10_000_000, (1,), generator=gen).item())
     t0 = time.perf_counter()
     if inequality_constraints or equality_constraints:
-        X_raw = hit_and_run(bounds, inequality_constraints, equality_constraints, raw_samples, seed)
+        X_raw = hit_and_run(bounds, inequality_constraints, equality_constraints, raw_samples * q, seed)
+        if q > 1:
+            X_raw = X_raw.reshape(raw_samples, q, d)
     else:
-        X_raw = draw_sobol_samples(bounds, raw_samples, seed)
+        X_raw = draw_sobol_samples(bounds, raw_samples, seed, q)
+    shp = (q, d) if q > 1 else (d,)          # one candidate (q-batch) of the acquisition
     # 2. evaluate (sharded over ranks, all-gather of the per-shard values)
     Xr = torch.as_tensor(X_raw, dtype=torch.float64, device=dev)
     if world > 1:
@@ -421,20 +437,21 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             return host_values(acqf.forward(Xt)), None
         per = math.ceil(nb / world)
         i0, i1 = min(nb, rank * per), min(nb, (rank + 1) * per)
-        loc = torch.zeros(per, 1 + d, dtype=torch.float64, device=dev)
+        nx = q * d
+        loc = torch.zeros(per, 1 + nx, dtype=torch.float64, device=dev)
         if i1 > i0:
             Xt = torch.as_tensor(X[i0:i1], dtype=torch.float64, device=dev)
             if with_grad:
                 a, g = acqf.forward_backward(Xt)
                 loc[: i1 - i0, 0] = a
-                loc[: i1 - i0, 1:] = g
+                loc[: i1 - i0, 1:] = g.reshape(i1 - i0, nx)
             else:
                 loc[: i1 - i0, 0] = acqf.forward(Xt)
         bufs = [torch.empty_like(loc) for _ in range(world)]
         dist.all_gather(bufs, loc)
         full = torch.cat(bufs)[:nb].cpu().numpy()
         host_values(torch.from_numpy(full[:, 0]))
-        return full[:, 0], (full[:, 1:] if with_grad else None)
+        return full[:, 0], (full[:, 1:].reshape((nb,) + shp) if with_grad else None)
 
     # Independent chunks (batch_limit < num_restarts) are separate problems in the
     # reference: with at least as many chunks as ranks each rank owns whole chunks and runs
@@ -445,9 +462,10 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     def run_chunk(s0: int, s1: int):
         nb = s1 - s0
         x0 = X0[s0:s1].reshape(-1)
-        lbv, ubv = np.tile(bounds[0], nb), np.tile(bounds[1], nb)
-        cons = _scipy_constraints(inequality_constraints, equality_constraints, nb, d)
-        if not cons and optimizer == "native" and local_world == 1 and hasattr(acqf, "plan"):
+        lbv, ubv = np.tile(bounds[0], nb * q), np.tile(bounds[1], nb * q)
+        cons = _scipy_constraints(inequality_constraints, equality_constraints, nb * q, d)
+        if (not cons and optimizer == "native" and local_world == 1 and q == 1
+                and getattr(acqf, "supports_plan", False)):
             # the whole L-BFGS-B loop in C++ on the device plan (no Python per iteration)
             Xc, vals, info = acqf.plan(nb, True).minimize(x0, lbv, ubv, maxiter)
             return vals, Xc.reshape(nb, d), {"restarts": nb, "evals": info[1], "nit": info[0], "status": info[2],
@@ -456,14 +474,14 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
 
         def f(x):
             if local_world == 1 and hasattr(acqf, "eval_host"):
-                a, g = acqf.eval_host(x.reshape(nb, d), True)
+                a, g = acqf.eval_host(x.reshape((nb,) + shp), True)
                 a = host_values(torch.from_numpy(a))
             elif local_world == 1:
-                Xt = torch.as_tensor(x.reshape(nb, d), dtype=torch.float64, device=dev)
+                Xt = torch.as_tensor(x.reshape((nb,) + shp), dtype=torch.float64, device=dev)
                 a, g = acqf.forward_backward(Xt)
                 a, g = host_values(a), g.cpu().numpy()
             else:
-                a, g = evaluate(x.reshape(nb, d), True)
+                a, g = evaluate(x.reshape((nb,) + shp), True)
             counter["n"] += 1
             return -float(a.sum()), -g.reshape(-1)
 
@@ -478,7 +496,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             res = minimize(f, x0, jac=True, method="L-BFGS-B", bounds=list(zip(lbv, ubv)),
                            options={"maxiter": maxiter})
             drv = "scipy"
-        Xc = np.clip(res.x.reshape(nb, d), bounds[0], bounds[1])
+        Xc = np.clip(res.x.reshape((nb,) + shp), bounds[0], bounds[1])
         if local_world == 1:
             vals = host_values(acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)))
         else:
@@ -507,12 +525,12 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         k = int(np.argmax(vals))
         best_v, best_x = float(vals[k]), Xs[k]
     else:
-        best_v, best_x = -np.inf, np.zeros(d)
+        best_v, best_x = -np.inf, np.zeros(shp)
     if own_chunks:
         # all-gather every rank's (error flag, best value, x) over RCCL; a failure on any rank
         # raises on every rank (no rank is left waiting in a collective); argmax, ties -> lowest rank
         flag = 0.0 if err is None else (2.0 if _is_notpsd(err) else 1.0)
-        loc = torch.tensor(np.r_[flag, best_v, best_x], dtype=torch.float64, device=dev)
+        loc = torch.tensor(np.r_[flag, best_v, np.ravel(best_x)], dtype=torch.float64, device=dev)
         bufs = [torch.empty_like(loc) for _ in range(world)]
         dist.all_gather(bufs, loc)
         allv = torch.stack(bufs).cpu().numpy()
@@ -525,7 +543,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
                 raise NotPSDError(f"acquisition not p.d. on rank(s) {bad} (restart chunk)")
             raise RuntimeError(f"restart optimisation failed on rank(s) {bad}")
         k = int(np.argmax(allv[:, 1]))
-        best_v, best_x = float(allv[k, 1]), allv[k, 2:]
+        best_v, best_x = float(allv[k, 1]), allv[k, 2:].reshape(shp)
         cnt = torch.tensor([stats.opt_evals], dtype=torch.float64, device=dev)
         dist.all_reduce(cnt)
         stats.opt_evals_global = int(cnt.item())
@@ -543,10 +561,14 @@ def _is_notpsd(e: BaseException) -> bool:
 def optimize_acqf_mixed(acqf, bounds: np.ndarray, fixed_features_list: Sequence[dict], num_restarts: int,
                         raw_samples: int, options: dict, gen: torch.Generator,
                         inequality_constraints: Sequence[LinearConstraint] = (),
-                        equality_constraints: Sequence[LinearConstraint] = (), dist=None):
+                        equality_constraints: Sequence[LinearConstraint] = (), dist=None, q: int = 1):
     """[upstream] botorch.optim.optimize_acqf_mixed (q = 1), as BoFire calls it for the
     EXHAUSTIVE categorical method (bofire/strategies/predictives/botorch.py:358-378): one
-    optimize_acqf per fixed-feature combination, best acquisition value wins (first on ties)."""
+    optimize_acqf per fixed-feature combination, best acquisition value wins (first on ties).
+    q > 1 (BoTorch's sequential greedy batch over re-built pending points) is not built."""
+    if q != 1:
+        raise NotImplementedError("optimize_acqf_mixed with q > 1 (sequential greedy over pending points) is "
+                                  "not implemented; use the FREE categorical method for joint batches")
     stats = OptimizeStats()
     best = (None, -np.inf)
     for ff in fixed_features_list:

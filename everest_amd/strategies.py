@@ -18,6 +18,7 @@ import pandas as pd
 import torch
 
 from . import data_models as dm
+from . import ops
 from .acquisition import QEHVI, QEI, QLogEHVI, QLogNEHVI, QNEHVI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
 from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
@@ -304,10 +305,12 @@ class BotorchStrategy(PredictiveStrategy):
         return X_train, X_pending
 
     def calc_acquisition(self, candidates: pd.DataFrame, combined: bool = False) -> np.ndarray:
+        """bofire/strategies/predictives/botorch.py:196-225: one value per candidate, or with
+        ``combined`` one joint value of the whole set as a q-batch."""
         acqf = self._get_acqfs(1)[0]
-        if combined:
-            raise NotImplementedError("combined (q>1) acquisition values are out of scope (q = 1 kernels)")
         X = torch.as_tensor(self._transform(candidates), dtype=torch.float64, device=self.model.device)
+        if combined:
+            X = X.unsqueeze(0)
         return host_values(acqf.forward(X))
 
     def _bounds(self) -> np.ndarray:
@@ -320,23 +323,22 @@ class BotorchStrategy(PredictiveStrategy):
         assert candidate_count > 0, "candidate_count has to be larger than zero."
         if self.experiments is None:
             raise ValueError("No experiments have been provided yet.")
-        if candidate_count != 1:
-            raise NotImplementedError("q > 1 joint candidate batches are not implemented in the MI355X build "
-                                      "(the device kernels evaluate q = 1)")
-        acqf = self._get_acqfs(candidate_count)[0]
+        q = int(candidate_count)
+        acqf = self._get_acqfs(q)[0]
         ineq = get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
         eq = get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
         combos = self.get_categorical_combinations()
         if len(combos) > 1:     # EXHAUSTIVE categorical method: optimize_acqf_mixed
             x, val, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts, self.num_raw_samples,
-                                                self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist)
+                                                self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
+                                                q=q)
         else:
             x, val, stats = optimize_acqf(acqf, self._bounds(), self.num_restarts, self.num_raw_samples,
                                           self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
-                                          fixed_features=combos[0] or None)
+                                          fixed_features=combos[0] or None, q=q)
         stats.best_value = val
         self.last_ask_stats = stats
-        return self._postprocess_candidates(x[None, :])
+        return self._postprocess_candidates(x.reshape(q, -1))
 
     def get_fixed_features(self) -> dict:
         """bofire/strategies/predictives/botorch.py:530-595 (continuous / one-hot part):
@@ -410,25 +412,51 @@ class _MultiobjectiveMixin:
                                                           CloseToTargetObjective])
         return (self.ref_point_mask * np.array([ref_point[k] for k in keys])).tolist()
 
-    def _objective_affine(self):
-        """g_j = a_j y_j + b_j per output (bofire/utils/torch_tools.py:384-402); the device
-        kernels take affine objectives (Maximize / Minimize with bounds)."""
-        keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
-                                                          CloseToTargetObjective])
-        if keys != self.model.output_keys:
-            raise NotImplementedError("every output must carry a Maximize/Minimize objective in this build")
-        a, b = [], []
-        for k in keys:
+    def _objective_spec(self):
+        """(objectives, constraints) over the model outputs for the device kernels:
+        get_multiobjective_objective (bofire/utils/torch_tools.py:699-727; callables :384-402)
+        and get_output_constraints (:340-381, constrained_objective2botorch :258-337)."""
+        keys = list(self.model.output_keys)
+        objectives, constraints = [], []
+        for k in self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
+                                                            CloseToTargetObjective]):
             obj = self.domain.outputs.get_by_key(k).objective
-            if not isinstance(obj, (MaximizeObjective, MinimizeObjective)):
-                raise NotImplementedError(f"objective {type(obj).__name__} has no device kernel (affine only)")
-            aa, bb = obj.affine()
-            a.append(aa)
-            b.append(bb)
-        return np.array(a), np.array(b)
+            if isinstance(obj, CloseToTargetObjective):
+                objectives.append((keys.index(k), ops.OBJ_CLOSE_TO_TARGET, obj.target_value, obj.exponent))
+            else:
+                a, b = obj.affine()
+                objectives.append((keys.index(k), ops.OBJ_AFFINE, a, b))
+        for feat in self.domain.outputs.get().features:
+            obj = getattr(feat, "objective", None)
+            if not isinstance(obj, dm.ConstrainedObjective):
+                continue
+            j = keys.index(feat.key)
+            if isinstance(obj, dm.TargetObjective):
+                eta = 1.0 / obj.steepness
+                constraints += [(j, -1.0, obj.target_value - obj.tolerance, eta),
+                                (j, 1.0, obj.target_value + obj.tolerance, eta)]
+            elif isinstance(obj, dm.MinimizeSigmoidObjective):
+                constraints.append((j, 1.0, obj.tp, 1.0 / obj.steepness))
+            elif isinstance(obj, dm.MovingMaximizeSigmoidObjective):
+                ex = self.domain.outputs.preprocess_experiments_one_valid_output(feat.key, self.experiments)
+                constraints.append((j, -1.0, obj.get_adjusted_tp(ex[feat.key].values), 1.0 / obj.steepness))
+            elif isinstance(obj, dm.MaximizeSigmoidObjective):
+                constraints.append((j, -1.0, obj.tp, 1.0 / obj.steepness))
+            else:
+                raise NotImplementedError(f"output constraint {type(obj).__name__} has no device kernel")
+        return objectives, constraints
+
+    def _objective_affine(self):
+        """a, b of g_j = a_j y_j + b_j when every output carries one affine objective (the
+        q = 1 fast path); None otherwise (the general kernels take the full description)."""
+        objectives, constraints = self._objective_spec()
+        if constraints or len(objectives) != len(self.model.output_keys) or any(
+                o != j or k != ops.OBJ_AFFINE for j, (o, k, _, _) in enumerate(objectives)):
+            return None, None
+        return np.array([o[2] for o in objectives]), np.array([o[3] for o in objectives])
 
     def _observed_outputs(self) -> np.ndarray:
-        """Valid observations of the objective outputs (n x m, model output order)."""
+        """Valid observations of every model output (n x m, model output order)."""
         df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
         return df[self.model.output_keys].values.astype(np.float64)
 
@@ -451,15 +479,16 @@ class QehviStrategy(_MultiobjectiveMixin, BotorchStrategy):
         masked observations better than the reference point (not objective-transformed)."""
         assert self.experiments is not None, "No experiments available."
         _, X_pending = self.get_acqf_input_tensors()
-        if X_pending is not None:
-            raise NotImplementedError("qEHVI with pending candidates needs q > 1 inclusion-exclusion "
-                                      "(out of scope: the device kernels evaluate q = 1)")
-        a, b = self._objective_affine()
-        train_obj = self._observed_outputs() * self.ref_point_mask
+        objectives, constraints = self._objective_spec()
+        keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
+                                                          CloseToTargetObjective])
+        df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        train_obj = df[keys].values.astype(np.float64) * self.ref_point_mask
         ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
         better = (train_obj > ref).all(axis=-1)
-        acqf = QEHVI(self.model, train_obj[better], ref, a, b, S=self.num_sobol_samples,
-                     sampler_seed=self._draw_seed())
+        acqf = QEHVI(self.model, train_obj[better], ref, None, None, S=self.num_sobol_samples,
+                     sampler_seed=self._draw_seed(), objective=objectives, constraints=constraints,
+                     X_pending_raw=X_pending)
         self.last_acqf = acqf
         return [acqf]
 
@@ -477,13 +506,14 @@ class QnehviStrategy(QehviStrategy):
         X_train, X_pending = self.get_acqf_input_tensors()
         if self.alpha != 0.0:
             raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
-        a, b = self._objective_affine()
+        objectives, constraints = self._objective_spec()
         ref = self.get_adjusted_refpoint()
         # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed
         prune_seed = self._draw_seed()
         sampler_seed = self._draw_seed()
-        acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, a, b, S=self.num_sobol_samples,
-                      sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending)
+        acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, None, None, S=self.num_sobol_samples,
+                      sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending,
+                      objective=objectives, constraints=constraints)
         self.last_acqf = acqf
         return [acqf]
 
@@ -509,22 +539,26 @@ class MoboStrategy(_MultiobjectiveMixin, BotorchStrategy):
         if getattr(af, "alpha", 0.0) != 0.0:
             raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
         X_train, X_pending = self.get_acqf_input_tensors()
-        a, b = self._objective_affine()
+        objectives, constraints = self._objective_spec()
         ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
         S = int(af.n_mc_samples)
+        kw = dict(objective=objectives, constraints=constraints)
         if isinstance(af, (dm.qEHVI, dm.qLogEHVI)):
-            if X_pending is not None:
-                raise NotImplementedError(f"{type(af).__name__} with pending candidates needs q > 1 "
-                                          "inclusion-exclusion (out of scope: the device kernels evaluate q = 1)")
+            # [upstream] get_acquisition_function: partition of objective(Y) over the feasible rows
+            spec = ops.GeneralSpec(len(self.model.output_keys), objectives, constraints)
             Y = self._observed_outputs()
+            feas = np.ones(Y.shape[0], dtype=bool)
+            for o, sg, t, _ in constraints:
+                feas &= sg * (Y[:, o] - t) <= 0
             cls = QEHVI if isinstance(af, dm.qEHVI) else QLogEHVI
-            acqf = cls(self.model, Y * a + b, ref, a, b, S=S, sampler_seed=self._draw_seed())
+            acqf = cls(self.model, spec.host_objective(Y[feas]), ref, None, None, S=S,
+                       sampler_seed=self._draw_seed(), X_pending_raw=X_pending, **kw)
         elif isinstance(af, (dm.qNEHVI, dm.qLogNEHVI)):
             prune_seed = self._draw_seed() if af.prune_baseline else 0
             sampler_seed = self._draw_seed()
             cls = QNEHVI if isinstance(af, dm.qNEHVI) else QLogNEHVI
-            acqf = cls(self.model, self.model.X_raw, X_train, ref, a, b, S=S, sampler_seed=sampler_seed,
-                       prune_baseline=af.prune_baseline, prune_seed=prune_seed, X_pending_raw=X_pending)
+            acqf = cls(self.model, self.model.X_raw, X_train, ref, None, None, S=S, sampler_seed=sampler_seed,
+                       prune_baseline=af.prune_baseline, prune_seed=prune_seed, X_pending_raw=X_pending, **kw)
         else:
             raise NotImplementedError(f"{type(af).__name__} has no device kernel in this build")
         self.last_acqf = acqf

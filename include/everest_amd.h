@@ -278,6 +278,50 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* plan, const double* 
                              const double* ub, int maxiter, int maxfun, double factr, double pgtol, int m,
                              int maxls, double* x, double* acq, int* info);
 
+/* ---- general qNEHVI / qEHVI evaluation (qnehvi_general.hip) ---------------------------
+ * q >= 1 joint candidate batches (inclusion-exclusion over the 2^q - 1 subsets of the q
+ * points), objectives over selected model outputs (Maximize / Minimize: a*y + b;
+ * CloseToTarget: -|y - t|^e) and output constraints c(y) = sign*(y_out - thr) <= 0 weighted
+ * by exp(sum logsigmoid(-c/eta)).  Replaces [upstream] qNoisyExpectedHypervolumeImprovement /
+ * qExpectedHypervolumeImprovement forward + backward with q = candidate_count
+ * (bofire/strategies/predictives/botorch.py:385), objective = get_multiobjective_objective
+ * (bofire/utils/torch_tools.py:699-727, callables :384-402) and constraints / eta from
+ * get_output_constraints (torch_tools.py:258-381, passed at
+ * bofire/strategies/predictives/qnehvi.py:28-48 and mobo.py:50-86).
+ * Model side: `stm` (m = model outputs; operator M / R layout as for q = 1, zq unused) and
+ * `md`; scan side: `sth` (m = m_obj objectives, the cells, log_hvi = 0).  X: (b*q) x d raw
+ * candidates, point i of candidate c at row c*q + i; acq: b; dX (NULL = forward only):
+ * (b*q) x d; gout (nullable, b) weights the backward.  The objective / constraint arrays are
+ * HOST arrays (copied into the launch); zq (S x q x m_model) is on the device. */
+#define EVR_OBJ_AFFINE 0
+#define EVR_OBJ_CLOSE_TO_TARGET 1
+#define EVR_QNG_MAX_Q 8
+typedef struct {
+  int q;                    /* points per candidate, 1..8 */
+  int m_obj;                /* objectives, 1..8 */
+  const int* obj_out;       /* m_obj: model output index */
+  const int* obj_kind;      /* m_obj: EVR_OBJ_* */
+  const double* obj_p0;     /* m_obj: a (affine) / target (close-to-target) */
+  const double* obj_p1;     /* m_obj: b (affine) / exponent (close-to-target) */
+  int n_con;                /* output constraints, 0..16 */
+  const int* con_out;       /* n_con: model output index */
+  const double* con_sign;   /* n_con: c = sign*(y - thr) */
+  const double* con_thr;
+  const double* con_eta;    /* n_con: sigmoid temperature (BoFire: 1/steepness) */
+  const double* zq;         /* device, S x q x m_model: base samples of the q new points */
+} evr_qn_general;
+long long evr_qng_workspace_doubles(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth,
+                                    const evr_qn_general* g, const evr_qnehvi_model* md, int b, int backward);
+int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
+                 const evr_qnehvi_model* md, int b, const double* X, const double* gout, double* work,
+                 double* acq, double* dX);
+/* Objectives of baseline / prune samples (Y: m_model x n x S plus mu: m_model x n, nullable)
+ * with hard feasibility: O[k][i][s] = g_k(y), or ref[k] where any constraint c > 0
+ * ([upstream] prune_inferior_points_multi_objective and the qNEHVI baseline partitions drop
+ * infeasible samples).  g->q / g->zq unused. */
+int evr_objective_general(void* stream, int m_model, int n, int S, const evr_qn_general* g, const double* Y,
+                          const double* mu, const double* ref, double* O);
+
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+
  * with sd from psd_safe_cholesky (3 tries) of the posterior variance; gR (nullable) =

@@ -3,7 +3,7 @@
 Reference-structure restatement (torch-CPU float64, autograd-capable) of
 ``qNoisyExpectedHypervolumeImprovement`` as BoFire builds it
 (bofire/strategies/predictives/qnehvi.py:23-53: prune_baseline=True, cache_root=True,
-alpha=0, no output constraints), of qEHVI (QehviStrategy / MoboStrategy) and of qEI
+alpha=0, output constraints / eta from get_output_constraints), of qEHVI (QehviStrategy / MoboStrategy) and of qEI
 (bofire/strategies/predictives/sobo.py:51-90).
 
 It deliberately keeps BoTorch's computation *shape*  so that it doubles as
@@ -68,6 +68,48 @@ class Objective:
         return y * self.a + self.b
 
 
+@dataclass
+class GeneralObjective:
+    """Objectives over selected outputs (get_multiobjective_objective,
+    bofire/utils/torch_tools.py:699-727): kind 0 = affine p0*y + p1 (Maximize / Minimize,
+    :389-398), kind 1 = CloseToTarget -|y - p0|^p1 (:399-402)."""
+    out: Sequence[int]
+    kind: Sequence[int]
+    p0: Sequence[float]
+    p1: Sequence[float]
+
+    def __call__(self, y):
+        cols = []
+        for o, k, a, b in zip(self.out, self.kind, self.p0, self.p1):
+            v = y[..., o]
+            cols.append(v * a + b if k == 0 else -(torch.abs(v - a) ** b))
+        return torch.stack(cols, -1)
+
+
+@dataclass
+class OutputConstraints:
+    """Output-constraint callables c(Z) = sign*(Z[..., out] - thr) with their eta
+    (constrained_objective2botorch, bofire/utils/torch_tools.py:284-315: Maximize/Minimize
+    sigmoid and Target objectives), feasible where c <= 0."""
+    out: Sequence[int]
+    sign: Sequence[float]
+    thr: Sequence[float]
+    eta: Sequence[float]
+
+    def values(self, y):
+        return torch.stack([s * (y[..., o] - t) for o, s, t in zip(self.out, self.sign, self.thr)], -1)
+
+    def feasible(self, y):
+        return (self.values(y) <= 0).all(-1)
+
+    def weight(self, y):
+        """[upstream] compute_smoothed_feasibility_indicator(log=False, fat=False): exp of the
+        sum of logsigmoid(-c / eta) over the constraints."""
+        c = self.values(y)
+        eta = torch.as_tensor(list(self.eta), dtype=c.dtype)
+        return torch.nn.functional.logsigmoid(-c / eta).sum(-1).exp()
+
+
 def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
     """Per-output joint posterior at Xn (... x p x d, normalized).  Returns mean (... x p x m)
     and cov (... x m x p x p), computed the GPyTorch way: R = K(X, Xtr) L^-T."""
@@ -83,10 +125,12 @@ def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
     return torch.stack(means, -1), torch.stack(covs, -3)
 
 
-def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0, chunk: int = 0):
+def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0, chunk: int = 0,
+                   constraints: Optional[OutputConstraints] = None):
     """prune_inferior_points_multi_objective restated.  z_prune: S' x n x m.  Returns the
     kept row indices (sorted, unique) into Xn.  ``chunk`` > 0 walks the S' draws in chunks
-    (same counts; bounds the n x n dominance tensors at BASELINE sizes)."""
+    (same counts; bounds the n x n dominance tensors at BASELINE sizes).  Infeasible samples
+    (any output constraint > 0) are set to the reference point."""
     mean, cov = joint_posterior(models, Xn)                    # n x m, m x n x n
     L, _ = psd_safe_cholesky(cov)                              # m x n x n
     Sp = z_prune.shape[0]
@@ -95,6 +139,8 @@ def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: 
     for s0 in range(0, Sp, step):
         Y = mean.unsqueeze(0) + torch.einsum("jik,skj->sij", L, z_prune[s0:s0 + step])
         obj = objective(Y)
+        if constraints is not None:
+            obj = torch.where(constraints.feasible(Y).unsqueeze(-1), obj, ref)
         pareto = is_non_dominated(obj, deduplicate=False) & (obj > ref).all(-1)
         counts += pareto.to(torch.float64).sum(0)
     probs = counts / Sp
@@ -111,19 +157,25 @@ class QNEHVI:
     Xb_n: baseline (already pruned), normalized.  z_base: S x n_b x m; z_new: S x q x m."""
 
     def __init__(self, models: List[GPState], Xb_n: torch.Tensor, objective: Objective,
-                 ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor, cells=None):
+                 ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor, cells=None,
+                 constraints: Optional[OutputConstraints] = None):
         """``cells`` (list of 2 x C x m per sample) may be injected to time the forward
-        pass alone (bench.py cpu_baseline); parity tests always build their own."""
+        pass alone (bench.py cpu_baseline); parity tests always build their own.
+        ``constraints``: baseline samples infeasible under them leave the Pareto sets (set to
+        ref), candidate areas are weighted by the smoothed feasibility."""
         self.models = models
         self.Xb = Xb_n
         self.obj = objective
         self.ref = ref
         self.z_base = z_base
         self.z_new = z_new
+        self.constraints = constraints
         mean_b, cov_b = joint_posterior(models, Xb_n)          # nb x m, m x nb x nb
         self.L_base, self.base_jitter = psd_safe_cholesky(cov_b)
         Yb = mean_b.unsqueeze(0) + torch.einsum("jik,skj->sij", self.L_base, z_base)
-        self.base_obj = objective(Yb)                          # S x nb x m
+        self.base_obj = objective(Yb)                          # S x nb x m_obj
+        if constraints is not None:
+            self.base_obj = torch.where(constraints.feasible(Yb).unsqueeze(-1), self.base_obj, ref)
         if cells is not None:
             self.cells = cells
         else:
@@ -146,8 +198,10 @@ class QNEHVI:
         s = torch.einsum("bjqk,skj->sbqj", newL, z)
         return mean[..., -q:, :].unsqueeze(0) + s
 
-    def hvi_per_sample(self, obj: torch.Tensor) -> torch.Tensor:
-        """obj: S x b x q x m -> S x b (inclusion–exclusion over q-subsets)."""
+    def hvi_per_sample(self, obj: torch.Tensor, weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """obj: S x b x q x m -> S x b (inclusion–exclusion over q-subsets); ``weights``
+        (S x b x q feasibility) multiply each subset's areas by their product over the subset
+        ([upstream] _compute_qehvi with constraints)."""
         import itertools
         S, b, q, m = obj.shape
         out = torch.zeros(S, b, **TK)
@@ -157,11 +211,16 @@ class QNEHVI:
                 for sub in itertools.combinations(range(q), i):
                     ov = obj[s][:, list(sub), :].min(dim=-2).values            # b x m
                     ln = (torch.minimum(ov.unsqueeze(-2), hi) - lo).clamp_min(0.0)
-                    out[s] = out[s] + ((-1) ** (i + 1)) * ln.prod(-1).sum(-1)
+                    area = ln.prod(-1).sum(-1)
+                    if weights is not None:
+                        area = area * weights[s][:, list(sub)].prod(-1)
+                    out[s] = out[s] + ((-1) ** (i + 1)) * area
         return out
 
     def forward(self, Xn: torch.Tensor) -> torch.Tensor:
-        return self.hvi_per_sample(self.obj(self.samples(Xn))).mean(0)
+        Y = self.samples(Xn)
+        w = None if self.constraints is None else self.constraints.weight(Y)
+        return self.hvi_per_sample(self.obj(Y), w).mean(0)
 
 
 class QEHVI:
@@ -174,8 +233,12 @@ class QEHVI:
     over q-subsets, mean over samples.  z: S x q x m (Sobol dim = point*m + output)."""
 
     def __init__(self, models: List[GPState], Y_part: torch.Tensor, objective: Objective, ref: torch.Tensor,
-                 z: torch.Tensor):
+                 z: torch.Tensor, constraints: Optional[OutputConstraints] = None,
+                 X_pending: Optional[torch.Tensor] = None):
+        """``X_pending`` (normalized) joins every candidate's joint batch ([upstream]
+        concatenate_pending_points); z then covers q + n_pending points."""
         self.models, self.obj, self.ref, self.z = models, objective, ref, z
+        self.constraints, self.X_pending = constraints, X_pending
         self.cell = nondominated_cells(pareto_above_ref(Y_part, ref), ref)
 
     def samples(self, Xn: torch.Tensor) -> torch.Tensor:
@@ -185,7 +248,11 @@ class QEHVI:
 
     def forward(self, Xn: torch.Tensor) -> torch.Tensor:
         import itertools
-        obj = self.obj(self.samples(Xn))                           # S x b x q x m
+        if self.X_pending is not None:
+            Xn = torch.cat([Xn, self.X_pending.unsqueeze(0).expand(Xn.shape[0], *self.X_pending.shape)], -2)
+        Y = self.samples(Xn)
+        obj = self.obj(Y)                                          # S x b x q x m
+        w = None if self.constraints is None else self.constraints.weight(Y)
         S, b, q, m = obj.shape
         lo, hi = self.cell[0], self.cell[1]
         out = torch.zeros(S, b, **TK)
@@ -193,7 +260,10 @@ class QEHVI:
             for sub in itertools.combinations(range(q), i):
                 ov = obj[:, :, list(sub), :].min(dim=-2).values                   # S x b x m
                 ln = (torch.minimum(ov.unsqueeze(-2), hi) - lo).clamp_min(0.0)    # S x b x C x m
-                out = out + ((-1) ** (i + 1)) * ln.prod(-1).sum(-1)
+                area = ln.prod(-1).sum(-1)
+                if w is not None:
+                    area = area * w[:, :, list(sub)].prod(-1)
+                out = out + ((-1) ** (i + 1)) * area
         return out.mean(0)
 
 

@@ -81,7 +81,11 @@ def test_config3_qnehvi_values_and_grads_match_oracle(config3):
 
 def test_config3_batch_split_equals_full_batch(config3):
     """The 512-candidate plan against 20-candidate plans (the L-BFGS restart size) on the
-    same candidates: equal up to the summation-order rounding of the group splits."""
+    same candidates: equal up to the summation-order rounding of the different GEMM /
+    split-K reductions the two batch sizes select (f64: ~1e-15 relative on R, amplified by
+    the cancellation in L22^2 = var - |L21|^2 near training points: L22 -> 0 for
+    candidates next to a baseline point, so its relative rounding grows as 1/L22: measured
+    1.4e-11 absolute on values up to ~1e-3 on MI355X; asserted against the batch's scale)."""
     import bench
 
     c = config3
@@ -91,8 +95,10 @@ def test_config3_batch_split_equals_full_batch(config3):
     parts = [acqf.forward_backward(Xc[i:i + 20]) for i in range(0, 500, 20)]
     a_p = torch.cat([p[0] for p in parts])
     g_p = torch.cat([p[1] for p in parts])
-    assert torch.allclose(a_full[:500], a_p, rtol=1e-12, atol=1e-15)
-    assert torch.allclose(g_full[:500], g_p, rtol=1e-10, atol=1e-14)
+    da = (a_full[:500] - a_p).abs().max().item()
+    assert torch.allclose(a_full[:500], a_p, rtol=1e-7, atol=1e-7 * a_full.abs().max().item()), da
+    scale = g_full.abs().max().item()
+    assert torch.allclose(g_full[:500], g_p, rtol=1e-6, atol=1e-6 * scale), (g_full[:500] - g_p).abs().max().item()
 
 
 @pytest.fixture(scope="module")
@@ -161,12 +167,20 @@ def test_config5_qei_matches_oracle(config5):
     Xc[:, 4:] = 0.0
     for i in range(4):                                     # one category per categorical
         Xc[np.arange(512), 4 + 7 * i + rng.integers(0, 7, 512)] = 1.0
-    acq, dX = acqf.forward_backward(torch.tensor(Xc, device="cuda"))
     sub = np.arange(0, 512, 16)
     x = torch.tensor((Xc[sub] - st["lo"]) / (st["hi"] - st["lo"]), requires_grad=True)
-    ref = oq.qei([o], x.unsqueeze(1), acqf.best_f, acqf.z.cpu().unsqueeze(-1), a=-1.0, bconst=0.0)
-    ref.sum().backward()
-    assert (ref.detach() > 0).sum() >= 4
-    assert torch.allclose(acq.cpu()[sub], ref.detach(), rtol=1e-6, atol=1e-10)
-    gref = x.grad / torch.tensor(st["hi"] - st["lo"])      # d/dX_raw
-    assert torch.allclose(dX.cpu()[sub], gref, rtol=1e-5, atol=1e-8 * gref.abs().max())
+    # the reference best_f, then a lowered incumbent (best_f is a plain input of the kernel):
+    # a 2048-point design leaves random candidates almost no improvement over the true best_f
+    mc, _ = ogp.posterior(o, x.detach())
+    for lowered in (False, True):
+        # lowered: the median objective mean over the checked candidates
+        acqf.best_f = float(np.median(-mc.numpy())) if lowered else best_f
+        acq, dX = acqf.forward_backward(torch.tensor(Xc, device="cuda"))
+        x.grad = None
+        ref = oq.qei([o], x.unsqueeze(1), acqf.best_f, acqf.z.cpu().unsqueeze(-1), a=-1.0, bconst=0.0)
+        ref.sum().backward()
+        if lowered:
+            assert (ref.detach() > 0).sum() >= 4
+        assert torch.allclose(acq.cpu()[sub], ref.detach(), rtol=1e-6, atol=1e-10)
+        gref = x.grad / torch.tensor(st["hi"] - st["lo"])      # d/dX_raw
+        assert torch.allclose(dX.cpu()[sub], gref, rtol=1e-5, atol=1e-8 * max(gref.abs().max().item(), 1e-30))
