@@ -55,6 +55,11 @@ class EvrQnGeneral(ctypes.Structure):
     ]
 
 
+class EvrQnehviHandle(ctypes.Structure):
+    """evr_qnehvi_handle: what torch.ops.everest_amd.qnehvi_* read (include/everest_amd.h)."""
+    _fields_ = [("stm", c_void_p), ("sth", c_void_p), ("md", c_void_p), ("g", c_void_p * 9), ("fast", c_int)]
+
+
 _SIGS = {
     "evr_version": ([], c_int),
     "evr_last_error": ([], c_char_p),

@@ -20,6 +20,7 @@ followed by the box-cell HVI scan and the mean over samples.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 import warnings
@@ -203,6 +204,41 @@ class _BoxHviAcqf:
         if dX is not None:
             dX = dX.view(b, qq, d)[:, :q].contiguous()
         return acq, dX
+
+    def _handle(self, q: int, fast: bool) -> int:
+        """Address of the evr_qnehvi_handle the torch operators read (kept alive here)."""
+        hs = self.__dict__.setdefault("_handles", {})
+        h = hs.get(fast)
+        if h is None:
+            h = _native.EvrQnehviHandle()
+            h.stm = ctypes.addressof(self.state if fast else self.state_model)
+            h.sth = ctypes.addressof(self.state if fast else self.state_scan)
+            h.md = ctypes.addressof(self.model)
+            h.fast = int(fast)
+            hs[fast] = h
+        if not fast and not h.g[q]:
+            gs = self.__dict__.setdefault("_gstructs", {})
+            gs[q] = self.spec.struct(q, self._zq(q))
+            h.g[q] = ctypes.addressof(gs[q])
+        return ctypes.addressof(h)
+
+    def __call__(self, X: torch.Tensor) -> torch.Tensor:
+        """BoTorch AcquisitionFunction protocol: X (b x q x d, or b x d for q = 1) -> acq (b),
+        differentiable through the device backward — torch.ops.everest_amd.qnehvi_forward /
+        qnehvi_backward in a torch.autograd.Function (torch_ops.QnehviFunction)."""
+        from .torch_ops import QnehviFunction
+
+        X3, _ = self._split(X)
+        if self._fast(X3):
+            return QnehviFunction.apply(X3[:, 0].contiguous(), self._handle(1, True))
+        if getattr(self, "log_acqf", False):
+            raise NotImplementedError("q > 1 for the log-space acquisitions is not implemented on the device")
+        Xp = self._pending_rows()
+        if Xp is not None:
+            X3 = torch.cat([X3, Xp.unsqueeze(0).expand(X3.shape[0], Xp.shape[0], X3.shape[2])], 1)
+        if X3.shape[1] > 8:
+            raise ValueError(f"joint batch of {X3.shape[1]} points (q + pending) exceeds the device limit of 8")
+        return QnehviFunction.apply(X3.contiguous(), self._handle(X3.shape[1], False))
 
     def _split(self, X: torch.Tensor):
         """(X as b x q x d, squeeze-back flag): 2-D input is q = 1."""

@@ -141,9 +141,13 @@ class GPBatch:
 
     def posterior(self, Xraw: torch.Tensor, observation_noise: bool = False):
         """Mean and variance (B x nt) at raw (transformed, unnormalized) inputs."""
+        from . import torch_ops
+
         Xraw = Xraw.to(device=self.device, dtype=torch.float64).contiguous()
-        return ops.gp_posterior(self.Xn, Xraw, self.lo, self.inv_range, self.ls, self.M, self.kind, self.const,
-                                self.ym, self.ys, self.kxx, self.noise if observation_noise else None)
+        # the registered operator torch.ops.everest_amd.gp_posterior (evr_gp_posterior)
+        return torch_ops.load().gp_posterior(self.Xn, Xraw, self.lo, self.inv_range, self.ls, self.M, self.kind,
+                                             self.const, self.ym, self.ys, self.kxx,
+                                             self.noise if observation_noise else None)
 
 
 # ---------------------------------------------------------------------------------------

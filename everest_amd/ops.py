@@ -3,7 +3,8 @@
 Every op runs on torch's *current* HIP stream, takes float64 device tensors, allocates
 its outputs with the torch caching allocator and never frees caller memory.  Shape,
 dtype and device errors raise (``ValueError`` / ``RuntimeError``); there is no CPU path.
-The top-level ops are also registered as PyTorch custom ops (``torch.ops.everest_amd.*``).
+The posterior, kernel matrix, Cholesky and qNEHVI entry points are also registered as PyTorch
+custom operators (``torch.ops.everest_amd.*``, everest_amd/csrc/torch_ops.cpp, everest_amd/torch_ops.py).
 """
 from __future__ import annotations
 
@@ -797,22 +798,3 @@ def device_arch(device: int = 0) -> str:
     buf = ctypes.create_string_buffer(64)
     call("evr_device_arch", device, buf, 64)
     return buf.value.decode()
-
-
-# ---------------------------------------------------------------------------------------
-# torch custom-op registrations (torch.ops.everest_amd.*)
-# ---------------------------------------------------------------------------------------
-try:
-    @torch.library.custom_op("everest_amd::kernel_matrix", mutates_args=())
-    def _op_kernel_matrix(X1: torch.Tensor, X2: torch.Tensor, lengthscales: torch.Tensor, kind: int) -> torch.Tensor:
-        return kernel_matrix(X1, X2, lengthscales, kind)
-
-    @torch.library.custom_op("everest_amd::cholesky", mutates_args=())
-    def _op_cholesky(A: torch.Tensor, jitter0: float, max_tries: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        return cholesky(A, jitter0, max_tries, raise_on_fail=False)
-
-    @torch.library.custom_op("everest_amd::tri_inv", mutates_args=())
-    def _op_tri_inv(L: torch.Tensor) -> torch.Tensor:
-        return tri_inv(L)
-except Exception:  # pragma: no cover - older torch without torch.library.custom_op
-    pass

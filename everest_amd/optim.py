@@ -483,7 +483,10 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             else:
                 a, g = evaluate(x.reshape((nb,) + shp), True)
             counter["n"] += 1
-            return -float(a.sum()), -g.reshape(-1)
+            acc = 0.0
+            for v in a.tolist():         # sequential, as evr_qnehvi_plan_minimize sums (bitwise equal paths)
+                acc += v
+            return -acc, -g.reshape(-1)
 
         if cons:
             res = minimize(f, x0, jac=True, method="SLSQP", bounds=list(zip(lbv, ubv)), constraints=cons,

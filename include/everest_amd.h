@@ -322,6 +322,19 @@ int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_sta
 int evr_objective_general(void* stream, int m_model, int n, int S, const evr_qn_general* g, const double* Y,
                           const double* mu, const double* ref, double* O);
 
+/* Handle read by the PyTorch-ROCm custom operators torch.ops.everest_amd.qnehvi_forward /
+ * qnehvi_backward (everest_amd/csrc/torch_ops.cpp; passed as an int64 address, owned by the
+ * Python acquisition object): fast != 0 -> b x d candidates through the fused q = 1 chain on
+ * (stm, md); otherwise b x q x d candidates through evr_qng_eval with g[q] (set for every q
+ * the caller evaluates; pending rows are already part of the batch). */
+typedef struct {
+  const evr_qnehvi_state* stm;
+  const evr_qnehvi_state* sth;
+  const evr_qnehvi_model* md;
+  const evr_qn_general* g[EVR_QNG_MAX_Q + 1];
+  int fast;
+} evr_qnehvi_handle;
+
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+
  * with sd from psd_safe_cholesky (3 tries) of the posterior variance; gR (nullable) =

@@ -139,7 +139,11 @@ def test_config5_cholesky_2048(config5):
     # the oracle's own kernel matrix (sq-dist expansion, GPyTorch form) at d_eff = 32
     Ko = ogp.kernel_matrix(config5["Xn"], config5["Xn"], config5["o"].lengthscale, ogp.MATERN25)
     Ko = Ko + config5["o"].noise * torch.eye(2048, dtype=torch.float64)
-    assert torch.allclose(Kc[0], Ko, rtol=1e-10, atol=1e-11)
+    err = (Kc[0] - Ko).abs()
+    k = int(err.argmax())
+    i, j = divmod(k, 2048)
+    assert torch.allclose(Kc[0], Ko, rtol=1e-10, atol=1e-11), (err.max().item(), i, j, Kc[0, i, j].item(),
+                                                               Ko[i, j].item(), config5["o"].lengthscale.min().item())
 
 
 def test_config5_posterior_matches_oracle(config5):

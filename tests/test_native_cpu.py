@@ -114,3 +114,16 @@ def test_sobol_gray_code_closed_form_matches_engine():
                 b += 1
             ref = x.to(torch.float64) / 2 ** 30
         assert torch.equal(u[k], ref), k
+
+
+def test_torch_operator_library_registers_ops():
+    """The TORCH_LIBRARY(everest_amd) operators load and register on CPU (no compute: they
+    reject CPU tensors — no CPU fallback)."""
+    from everest_amd import torch_ops
+
+    ns = torch_ops.load()
+    for name in ("kernel_matrix", "cholesky", "gp_posterior", "qnehvi_forward", "qnehvi_backward"):
+        assert hasattr(ns, name)
+    x = torch.zeros(3, 2, dtype=torch.float64)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ns.kernel_matrix(x, x, torch.ones(2, dtype=torch.float64), 0)

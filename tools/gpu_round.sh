@@ -15,7 +15,7 @@ step() {  # step <name> <timeout_s> cmd...
   echo "[$(date +%H:%M:%S)] $name rc=$rc"
   return $rc
 }
-step pytest 600 python -m pytest tests -m gpu -x -q &&
+step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
 step bench 600 python bench.py &&
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
      python bench.py --no-cpu-baseline --no-ask &&
