@@ -2,21 +2,26 @@
 """Benchmark of the qNEHVI hot path on MI355X (BASELINE.json metric: QnehviStrategy.ask()
 candidates/sec + GP posterior ms, n=512 d=6 m=5).
 
-Workload (BASELINE.json configs[2]): DTLZ2(dim=6, m=5), X_train ~
-U[0,1]^6 (n=512, seed 0), noise-free Y, reference point 1.1 -> -1.1 in objective space
-(MinimizeObjective), 5 exact RBF GPs fitted once on the device and frozen, qNEHVI built as
-BoFire builds it (prune_baseline with 2048 samples, cached root, S=256 Sobol-normal base
-samples), q=1.  A *step* = one acquisition evaluation pass (forward + analytic backward,
-the unit raw screening and the L-BFGS restarts of ask() are made of) over one batch of
-b=512 Sobol candidates already resident in HBM, run through the native evaluation plan
-(everest_amd/csrc/qnehvi_plan.hip — the path ask() uses); the per-kernel breakdown comes
-from a separate instrumented pass over the same kernels launched one by one.
+A *step* is one full ``QnehviStrategy.ask()`` of BASELINE configs[3] (SURVEY.md §8(d)
+config 4) through the BoFire-compatible API: DTLZ2(dim=6, m=5), X_train ~ U[0,1]^6 (n=512,
+seed 0), noise-free Y, reference point 1.1 -> -1.1, 5 exact RBF GPs fitted once by tell()
+on the device; each ask builds qNEHVI as BoFire does (prune_baseline over 2048 draws, cached
+root, S=256 Sobol-normal samples, exact box decompositions), screens 1024 raw Sobol
+candidates and runs 20 L-BFGS-B restarts (q=1) on the analytic device gradient.  ``value``
+= (raw samples + optimiser evaluations x batch) / ask wall time — SURVEY.md §8(d)'s
+definition of ask() candidates/s — over K timed asks after W warm-up asks.
+
+Also reported: ``eval_pass`` (one forward + backward over b=512 candidates resident in HBM
+through the native plan, the unit raw screening is made of, with its per-kernel rooflines
+and PMC traffic), the per-kernel table at the restart batch (the top-level ``roofline`` is
+its dominant op), the GP posterior of the ask's fitted model, and the CPU baseline (the
+reference-structure oracle on the host cores, composed from bounded samples of each ask
+phase).
 
 Multi-GPU (one process per GPU, RCCL): ``--gpus N`` spawns N ranks itself (or runs under
-torchrun with WORLD_SIZE = N).  Every rank evaluates its own 512-candidate shard (weak
-scaling); each step ends with the RCCL all-gather of the per-shard acquisition values that
-the Boltzmann initial-condition selection needs.  The full ask() (config
-4: 1024 raw + 20 restarts) is then timed sharded over the N ranks.
+torchrun with WORLD_SIZE = N).  One ask is sharded over the ranks (strong scaling): raw
+screening in N shards with an all-gather of the values, the restarts in N chunks
+(batch_limit = ceil(20 / N)) with one all-gather of each rank's best.
 
 Prints ONE JSON line on rank 0.
 """
@@ -292,12 +297,13 @@ def _traffic(path, kernel):
     return ent if ent and "bytes_per_launch" in ent else None
 
 
-def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: int = 3, dist=None, device=None):
-    """Full QnehviStrategy.ask() (config 4 shape: 1024 raw Sobol candidates + 20 L-BFGS-B
-    restarts, q=1) through the BoFire-compatible strategy API; with ``dist`` every rank runs
-    the same strategy and ask() shards the raw screening and the joint restart evaluations
-    over the ranks (RCCL all-gathers).  Returns the median ask() wall time
-    (max over ranks) and acquisition evaluations / s (raw + optimizer evaluations)."""
+def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=None):
+    """QnehviStrategy of config 4 (DTLZ2(6, 5), n_train = n, S MC samples, ``raw`` Sobol raw
+    samples, ``restarts`` L-BFGS-B restarts) through the BoFire-compatible API, fitted once
+    (tell).  With N ranks the restarts are split into N chunks (batch_limit = ceil(restarts
+    / N), bofire/data_models/strategies/predictives/botorch.py:101-108): each rank optimises
+    its own chunk and one RCCL all-gather picks the best; raw screening is sharded over the
+    ranks with an all-gather of the values.  Returns (strategy, tell_s)."""
     import pandas as pd
 
     import everest_amd.data_models as dm
@@ -307,37 +313,20 @@ def ask_throughput(n: int, S: int, raw: int = 1024, restarts: int = 20, asks: in
     bm = DTLZ2(dim=6, num_objectives=5)
     Xd = pd.DataFrame(np.random.default_rng(0).uniform(size=(n, 6)), columns=bm.domain.inputs.get_keys())
     s = strategies.map(dm.QnehviStrategy(domain=bm.domain, ref_point=bm.ref_point, seed=1, num_sobol_samples=S,
-                                         num_raw_samples=raw, num_restarts=restarts), dist=dist)
+                                         num_raw_samples=raw, num_restarts=restarts,
+                                         batch_limit=math.ceil(restarts / world)), dist=dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.tell(bm.f(Xd, return_complete=True))
+    torch.cuda.synchronize()
+    return s, time.perf_counter() - t0
 
-    def clock(fn):
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        fn()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        if dist is not None:
-            tt = torch.tensor([dt], device=device)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dt = tt.item()
-        return dt
 
-    t_tell = clock(lambda: s.tell(bm.f(Xd, return_complete=True)))
-    s.ask(1)  # warm-up (first construction pays one-time allocations)
-    ts, evals, phases = [], [], []
-    for _ in range(asks):
-        ts.append(clock(lambda: s.ask(1)))
-        st = s.last_ask_stats
-        evals.append(st.raw_evals + getattr(st, "opt_evals_global", st.opt_evals))
-        tm = getattr(s.last_acqf, "timings", {})
-        phases.append({"construction": round(tm.get("total", 0.0), 4), "raw_screening": round(st.t_raw, 4),
-                       "restarts": round(st.t_opt, 4), "optimizer_iterations": st.opt_iters,
-                       "driver": st.chunks[0]["driver"] if st.chunks else None})
-    i = int(np.argsort(ts)[len(ts) // 2])
-    return {"ask_s": round(ts[i], 4), "evals": int(evals[i]), "evals_per_s": round(evals[i] / ts[i], 1),
-            "tell_s": round(t_tell, 3), "raw_samples": raw, "restarts": restarts, "mc_samples": S,
-            "phases_s": phases[i], "ranks": 1 if dist is None else dist.get_world_size()}
+def _ask_evals(s) -> int:
+    """Acquisition evaluations of the last ask() over all ranks: raw samples + every
+    optimiser function evaluation x its batch (SURVEY.md §8(d) "candidates/s" of ask)."""
+    st = s.last_ask_stats
+    return int(st.raw_evals + getattr(st, "opt_evals_global", st.opt_evals))
 
 
 def _spawn_ranks(n: int) -> int:
@@ -372,18 +361,52 @@ def _spawn_ranks(n: int) -> int:
     return rc
 
 
+def _rooflines(ktimes, table):
+    out = {}
+    for k, (bound, w, unit) in table.items():
+        if k not in ktimes:
+            continue
+        t = ktimes[k] * 1e-3
+        if unit == "B":
+            ach, peak, u = w / t / 1e9, PEAK_HBM_GBS, "GB/s"
+        else:
+            ach, peak, u = w / t / 1e12, PEAK_FP64_TFLOPS, "TFLOP/s"
+        out[k] = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": u, "frac": round(ach / peak, 4),
+                  "work_per_launch": w, "launch_ms": round(ktimes[k], 4)}
+    return out
+
+
+def _work_table(acqf, b, S, m, d, sum_cells):
+    """SURVEY.md §8(d) algorithmic work per launch of each op at batch b: (bound, work, unit)."""
+    Rr, n = acqf.Rr, acqf.nk
+    nrt = math.ceil(Rr / 64)
+    return {
+        "kernel_matrix": ("hbm", 8.0 * (m * n * b + n * d + b * d + m * d), "B"),
+        "proj_fwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
+        "samples": ("hbm", 8.0 * m * b * (S + 1 + 2 * nrt) + 8.0 * S * m * b, "B"),
+        # scan bytes with every cell read once per forward (explicit [lo, hi] rows, 16 m B per
+        # cell) + the samples + the output
+        "hvi_fwd_bwd": ("hbm", 16.0 * sum_cells * m + 8.0 * b * S * m + 8.0 * b, "B"),
+        "proj_bwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
+        "kernel_grad": ("hbm", 8.0 * (m * n * b + n * d + b * d), "B"),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10, help="timed ask() calls")
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--d", type=int, default=6)
     ap.add_argument("--m", type=int, default=5)
     ap.add_argument("--S", type=int, default=256)
-    ap.add_argument("--b", type=int, default=512)
+    ap.add_argument("--raw", type=int, default=1024)
+    ap.add_argument("--restarts", type=int, default=20)
+    ap.add_argument("--b", type=int, default=512, help="candidates per rank of the evaluation pass")
+    ap.add_argument("--eval-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-ask", action="store_true", help="skip the full QnehviStrategy.ask() timing")
+    ap.add_argument("--no-eval-pass", action="store_true", help="skip the b-candidate evaluation-pass figures")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -405,154 +428,174 @@ def main():
         dist.init_process_group("nccl", device_id=device)
         world = dist.get_world_size()
 
-    X, Y, gp, hypers, acqf, t_fit, t_build = build_state(args.n, args.d, args.m, args.S, device)
-    Xc = candidates(args.b, args.d, seed=2 + rank, device=device)
-    gathered = [torch.empty(args.b, dtype=torch.float64, device=device) for _ in range(world)]
-
-    # production path: the native evaluation plan (whole chain in one C-ABI call / hipGraph),
-    # candidates already resident in its HBM input buffer
-    plan = acqf.plan(args.b, True)
-    plan.X.copy_(Xc)
-
-    def one_step():
-        plan.run()
-        acq = plan.acq
-        if dist is not None:
-            dist.all_gather(gathered, acq)
-        return acq
-
-    for _ in range(args.warmup):
-        one_step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
+    def maxed(dt):
+        if dist is None:
+            return dt
         tt = torch.tensor([dt], device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
+        return tt.item()
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    # ---- the step: one full QnehviStrategy.ask() (config 4 shape, sharded over the ranks) ----
+    s, t_tell = make_ask_strategy(args.n, args.S, args.raw, args.restarts, world, dist)
+    for _ in range(args.warmup):
+        s.ask(1)
+    sync()
+    t0 = time.perf_counter()
+    evals = 0
+    for _ in range(args.steps):
+        s.ask(1)
+        evals += _ask_evals(s)
+    sync()
+    dt = maxed(time.perf_counter() - t0)
+    value = evals / dt
     ms = dt / args.steps * 1e3
-    value = world * args.b * args.steps / dt
+    acqf_ask = s.last_acqf
+    st_ask = s.last_ask_stats
+    tm = getattr(acqf_ask, "timings", {})
+    phases = {"construction_s": round(tm.get("total", 0.0), 4), "construction": {k: round(v, 4) for k, v in tm.items()},
+              "raw_screening_s": round(st_ask.t_raw, 4), "restarts_s": round(st_ask.t_opt, 4),
+              "optimizer_iterations": st_ask.opt_iters, "evals_last_ask": _ask_evals(s),
+              "driver": st_ask.chunks[0]["driver"] if st_ask.chunks else None}
 
-    # per-kernel device time: each op of the same chain, graph-replayed between HIP events
-    ktimes, ktimes_how = kernel_times(acqf, Xc)
+    # per-op device time at the restart batch one rank evaluates per L-BFGS-B iteration
+    b_r = math.ceil(args.restarts / world)
+    Xr = candidates(b_r, args.d, seed=5 + rank, device=device)
+    kt_r, how = kernel_times(acqf_ask, Xr)
 
-    # full ask() (config 4 shape; sharded over the ranks when N > 1)
-    ask = None
-    if not args.no_ask:
-        ask = ask_throughput(args.n, args.S, dist=dist, device=device)
+    eval_pass, kernels_b = None, None
+    X = Y = hypers = acqf = None
+    if not args.no_eval_pass:
+        # ---- evaluation pass: b candidates per rank through the native plan (raw-screening unit)
+        X, Y, gp, hypers, acqf, t_fit, t_build = build_state(args.n, args.d, args.m, args.S, device)
+        Xc = candidates(args.b, args.d, seed=2 + rank, device=device)
+        gathered = [torch.empty(args.b, dtype=torch.float64, device=device) for _ in range(world)]
+        plan = acqf.plan(args.b, True)
+        plan.X.copy_(Xc)
+
+        def one_pass():
+            plan.run()
+            if dist is not None:
+                dist.all_gather(gathered, plan.acq)
+
+        for _ in range(3):
+            one_pass()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.eval_steps):
+            one_pass()
+        sync()
+        dte = maxed(time.perf_counter() - t0)
+        kt_b, _ = kernel_times(acqf, Xc)
+        if rank == 0:
+            sum_cells = acqf.stats.total_cells
+            kernels_b = _rooflines(kt_b, _work_table(acqf, args.b, args.S, args.m, args.d, sum_cells))
+            counts = scan_counts(acqf, Xc)
+            if "hvi_fwd_bwd" in kernels_b:
+                t = kt_b["hvi_fwd_bwd"] * 1e-3
+                useful = counts["terms"] * (6 * args.m + 2)
+                kernels_b["hvi_fwd_bwd"]["valu_useful"] = {
+                    "achieved": round(useful / t / 1e12, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(useful / t / 1e12 / PEAK_FP64_TFLOPS, 4), "work_per_launch": float(useful),
+                    "note": "(6m+2) flop per evaluated (cell, candidate) term, device-counted"}
+                kernels_b["hvi_fwd_bwd"]["scan"] = {
+                    "dense_pairs": args.b * sum_cells, "group_tests": counts["group_tests"],
+                    "group_pairs": counts["group_pairs"], "terms": counts["terms"]}
+                tr = _traffic(args.traffic_json, "hvi_fwd_bwd")
+                if tr is not None:
+                    kernels_b["hvi_fwd_bwd"]["traffic"] = tr["bytes_per_launch"]
+                    kernels_b["hvi_fwd_bwd"]["traffic_source"] = tr["source"]
+            eval_pass = {"value": round(world * args.b * args.eval_steps / dte, 1), "unit": "candidates/s",
+                         "ms_per_step": round(dte / args.eval_steps * 1e3, 4), "candidates_per_rank": args.b,
+                         "note": "one qNEHVI forward + analytic backward over b Sobol candidates resident in HBM "
+                                 "through the native plan (the unit raw screening and restarts are made of)",
+                         "kernel_ms": {k: round(v, 4) for k, v in kt_b.items()}, "kernels": kernels_b,
+                         "n_base": acqf.nb, "cells_total": sum_cells, "cells_max": acqf.stats.max_cells,
+                         "box_decomposition": acqf.box_path, "setup_s": {"gp_fit": round(t_fit, 3),
+                                                                         "qnehvi_build": round(t_build, 3)}}
 
     if rank == 0:
-        st = acqf.stats
-        sum_cells = st.total_cells
-        m = args.m
-        b = args.b
-        # per-kernel rooflines (SURVEY.md §8(d) work per unit x units per launch / launch time)
-        Rr, n, d = acqf.Rr, args.n, args.d
-        nrt = math.ceil(Rr / 64)
-        counts = scan_counts(acqf, Xc)
-        hvi_useful = counts["terms"] * (6 * m + 2)
-        table = {
-            # (bound, work, unit): bytes for HBM-bound kernels, flops otherwise
-            "kernel_matrix": ("hbm", 8.0 * (m * n * b + n * d + b * d + m * d), "B"),
-            "proj_fwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
-            "samples": ("hbm", 8.0 * m * b * (args.S + 1 + 2 * nrt) + 8.0 * args.S * m * b, "B"),
-            # scan bytes with every cell read once per forward (explicit
-            # [lo, hi] rows, 16 m B per cell) + the samples + the output
-            "hvi_fwd_bwd": ("hbm", 16.0 * sum_cells * m + 8.0 * b * args.S * m + 8.0 * b, "B"),
-            "proj_bwd": ("mfma", 2.0 * m * Rr * n * b, "flop"),
-            "kernel_grad": ("hbm", 8.0 * (m * n * b + n * d + b * d), "B"),
-        }
-        kernels = {}
-        for k, (bound, w, unit) in table.items():
-            if k not in ktimes:
-                continue
-            t = ktimes[k] * 1e-3
-            if unit == "B":
-                ach, peak, u = w / t / 1e9, PEAK_HBM_GBS, "GB/s"
-            else:
-                ach, peak, u = w / t / 1e12, PEAK_FP64_TFLOPS, "TFLOP/s"
-            kernels[k] = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": u,
-                          "frac": round(ach / peak, 4), "work_per_launch": w, "launch_ms": round(ktimes[k], 4)}
-        dom = max(ktimes, key=ktimes.get)
+        sum_cells_r = acqf_ask.stats.total_cells
+        kernels_r = _rooflines(kt_r, _work_table(acqf_ask, b_r, args.S, args.m, args.d, sum_cells_r))
+        dom = max(kt_r, key=kt_r.get)
         roof = None
-        if dom in kernels:
-            r = kernels[dom]
+        if dom in kernels_r:
+            r = kernels_r[dom]
             roof = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"],
                     "unit": r["unit"], "frac": r["frac"], "traffic": None,
-                    "algorithmic_work_per_launch": r["work_per_launch"], "launch_ms": r["launch_ms"]}
-            tr = _traffic(args.traffic_json, dom)
+                    "algorithmic_work_per_launch": r["work_per_launch"], "launch_ms": r["launch_ms"],
+                    "batch": f"{b_r} restart candidates (one L-BFGS-B evaluation of this rank's chunk)"}
+            tr = _traffic(args.traffic_json, f"{dom}@b{b_r}")
             if tr is not None:
                 roof["traffic"] = tr["bytes_per_launch"]
                 roof["traffic_source"] = tr["source"]
-        if "hvi_fwd_bwd" in kernels:
-            t = ktimes["hvi_fwd_bwd"] * 1e-3
-            kernels["hvi_fwd_bwd"]["valu_useful"] = {
-                "achieved": round(hvi_useful / t / 1e12, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(hvi_useful / t / 1e12 / PEAK_FP64_TFLOPS, 4), "work_per_launch": float(hvi_useful),
-                "note": "(6m+2) flop per evaluated (cell, candidate) term, device-counted"}
-            kernels["hvi_fwd_bwd"]["scan"] = {
-                "dense_pairs": b * sum_cells, "group_tests": counts["group_tests"], "group_pairs": counts["group_pairs"],
-                "terms": counts["terms"],
-                "dense_equivalent_TFLOPs": round(b * sum_cells * (6 * m + 2) / (ktimes["hvi_fwd_bwd"] * 1e-3) / 1e12, 2)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            # the job's CPU share on the box (OMP_NUM_THREADS, 16 per GPU there; the affinity
-            # mask shows the whole machine), plus a single-thread leg
             share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
             threads = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
             torch.set_num_threads(threads)
-            t_cpu, nc, orc, ostates = cpu_baseline(acqf, hypers, X, Y, Xc.cpu())
-            cpu = {"value": round(nc / t_cpu, 3), "unit": "candidates/s", "cores": torch.get_num_threads(),
-                   "kind": "port", "sample": f"oracle reference-structure forward+backward over the first {nc} "
-                   f"of the same {b} candidates in chunks of 8 (batch_limit), same state (n={args.n}, "
-                   f"n_base={acqf.nb}, S={args.S}), {t_cpu:.1f} s of CPU wall time",
-                   "cores_note": f"{threads} threads = this job's CPU share (OMP_NUM_THREADS; "
-                                 f"affinity mask {share}, os.cpu_count {os.cpu_count()})"}
+            if X is None:
+                X, Y, gp, hypers, acqf, _, _ = build_state(args.n, args.d, args.m, args.S, device)
+            Xcc = candidates(max(args.b, 2 * args.restarts), args.d, seed=2, device=device).cpu()
+            t_cpu, nc, orc, ostates = cpu_baseline(acqf, hypers, X, Y, Xcc, budget_s=6.0)
+            ask_info = {"restarts": args.restarts, "raw_samples": args.raw, "evals": _ask_evals(s),
+                        "ask_s": round(ms * 1e-3, 4)}
+            est = cpu_ask_estimate(orc, ostates, acqf, Xcc, ask_info)
+            cpu = {"value": round(ask_info["evals"] / est["total_s"], 2), "unit": "candidates/s", "cores": threads,
+                   "kind": "port",
+                   "sample": "reference-structure QnehviStrategy.ask() on the host (oracle/, torch-CPU fp64, "
+                             "BoTorch's computation shape) for the same ask: " + est["sample"] +
+                             f"; {est['total_s']} s estimated per ask",
+                   "ask_estimate": est,
+                   "eval_pass_cpu": {"value": round(nc / t_cpu, 3), "unit": "candidates/s",
+                                     "sample": f"forward+backward of {nc} candidates in chunks of 8, {t_cpu:.1f} s"},
+                   "cores_note": f"{threads} threads = this job's CPU share (OMP_NUM_THREADS; affinity mask "
+                                 f"{share}, os.cpu_count {os.cpu_count()})"}
             torch.set_num_threads(1)
-            t1, n1, _, _ = cpu_baseline(acqf, hypers, X, Y, Xc.cpu(), budget_s=6.0)
-            cpu["single_thread"] = {"value": round(n1 / t1, 3), "unit": "candidates/s", "cores": 1,
-                                    "sample": f"{n1} candidates, {t1:.1f} s"}
+            t1, n1, _, _ = cpu_baseline(acqf, hypers, X, Y, Xcc, budget_s=4.0)
+            cpu["eval_pass_cpu"]["single_thread"] = {"value": round(n1 / t1, 3), "cores": 1,
+                                                     "sample": f"{n1} candidates, {t1:.1f} s"}
             torch.set_num_threads(threads)
-            if ask is not None:
-                cpu["ask_estimate"] = cpu_ask_estimate(orc, ostates, acqf, Xc.cpu(), ask)
-        t_post = gp_posterior_ms(device, gp=gp)
+        gp_ask = s.model
+        t_post = gp_posterior_ms(device, gp=gp_ask)
         out = {
             "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
-            "value": round(value, 2),
+            "value": round(value, 1),
             "unit": "candidates/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms, 4),
+            "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (DTLZ2 d=6 m=5 train set, Sobol candidates; GPs fitted on device)",
-            "config": {"workload": "qNEHVI fwd+bwd evaluation pass (the unit ask()'s raw screening and L-BFGS-B "
-                                   "restarts are made of), DTLZ2(d=6,m=5) n_train=512 S=256 b=512 q=1; "
-                                   "the full ask() rate is ask.evals_per_s",
-                       "n_train": args.n, "d": args.d, "m": m, "mc_samples": args.S, "candidates_per_gpu": b,
-                       "n_base": acqf.nb, "cells_total": sum_cells, "cells_max": st.max_cells,
-                       "box_decomposition": acqf.box_path, "parallelism": f"candidate-shard x{world}"},
+            "data": "synthetic (DTLZ2 d=6 m=5 train set; GPs fitted on device by tell())",
+            "config": {"workload": "full QnehviStrategy.ask() of BASELINE configs[3] (config 4): DTLZ2(d=6,m=5), "
+                                   f"n_train={args.n}, S={args.S} MC samples, {args.raw} raw Sobol candidates + "
+                                   f"{args.restarts} L-BFGS-B restarts, q=1; value = (raw + optimiser "
+                                   "evaluations x batch) / ask wall time, SURVEY.md §8(d)",
+                       "n_train": args.n, "d": args.d, "m": args.m, "mc_samples": args.S, "raw_samples": args.raw,
+                       "restarts": args.restarts, "batch_limit": math.ceil(args.restarts / world),
+                       "parallelism": f"restart chunks + raw-screening shards over {world} rank(s)"},
             "roofline": roof,
-            "kernels": kernels,
+            "kernels": kernels_r,
+            "kernel_ms": {k: round(v, 4) for k, v in kt_r.items()},
+            "kernel_ms_method": f"{how} of 10 launches per op between HIP events (torch current stream), "
+                                f"batch {b_r}",
+            "ask": {"ask_s": round(ms * 1e-3, 4), "evals_per_ask": round(evals / args.steps, 1), "tell_s": round(t_tell, 3),
+                    "phases_last_ask": phases, "n_base": acqf_ask.nb, "cells_total": sum_cells_r,
+                    "box_decomposition": acqf_ask.box_path},
+            "eval_pass": eval_pass,
             "cpu_baseline": cpu,
             "gp_posterior_ms": round(t_post, 4),
-            "gp_posterior": {"ms": round(t_post, 4), "shape": f"n_train={args.n} d={args.d} m={m}, 1024 test "
-                             "points, mean+var, HIP events",
+            "gp_posterior": {"ms": round(t_post, 4), "shape": f"n_train={args.n} d={args.d} m={args.m} (the ask's "
+                             "fitted model), 1024 test points, mean+var, HIP events",
                              "config2_ms": round(gp_posterior_ms(device), 4)},
-            "kernel_ms": {k: round(v, 4) for k, v in ktimes.items()},
-            "kernel_ms_method": f"{ktimes_how} of 10 launches per op between HIP events (torch current stream)",
-            "setup_s": {"gp_fit": round(t_fit, 3), "qnehvi_build": round(t_build, 3)},
-            "ask": ask,
         }
         print(json.dumps(out))
     if dist is not None:

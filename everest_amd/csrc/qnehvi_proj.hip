@@ -451,6 +451,8 @@ static bool use_rocblas() {
 static rocblas_handle rb_handle() {
   thread_local rocblas_handle h = nullptr;
   if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
+  // bitwise-reproducible results: no atomics-based split-K in the Tensile kernels
+  if (h) (void)rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);
   return h;
 }
 

@@ -100,6 +100,8 @@ class Strategy:
 
     def __init__(self, data_model):
         self.domain = data_model.domain
+        # bofire/strategies/strategy.py:26: `seed or random` — a seed of 0 counts as no seed
+        # (draws a random one), as in the reference
         self.seed = data_model.seed or int(np.random.default_rng().integers(1000))
         self.rng = np.random.default_rng(self.seed)
         self._experiments: Optional[pd.DataFrame] = None

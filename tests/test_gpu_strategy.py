@@ -15,7 +15,7 @@ from oracle import gp as ogp
 pytestmark = pytest.mark.gpu
 
 
-def _dtlz2_experiments(n=10, dim=6, m=2, seed=0):
+def _dtlz2_experiments(n=10, dim=6, m=2, seed=17):
     bench = DTLZ2(dim=dim, num_objectives=m)
     rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=seed))
     X = rnd.ask(n)
@@ -112,7 +112,7 @@ def test_detergent_readme_loop():
     """README.md:82-104 loop (config 1): 2 initial random points + 4 ask/tell rounds with the
     two linear inequality constraints (SLSQP restarts on hit-and-run raw samples)."""
     bench = Detergent()
-    rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=0))
+    rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=19))
     exps = bench.f(rnd.ask(2), return_complete=True)
     s = strategies.map(dm.QnehviStrategy(domain=bench.domain, seed=7, num_sobol_samples=64,
                                          num_raw_samples=128, num_restarts=4))

@@ -50,7 +50,7 @@ def f(df):
 def main(n=2048, b=512, method="FREE"):
     dev = torch.device("cuda", 0)
     dom = domain()
-    rnd = strategies.map(dm.RandomStrategy(domain=dom, seed=0))
+    rnd = strategies.map(dm.RandomStrategy(domain=dom, seed=13))
     X = rnd.ask(n)
     exps = X.copy()
     exps["y"] = f(X)

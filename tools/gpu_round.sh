@@ -18,10 +18,15 @@ step() {  # step <name> <timeout_s> cmd...
 step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
 step bench 600 python bench.py &&
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-     python bench.py --no-cpu-baseline --no-ask &&
+     python bench.py --no-cpu-baseline --no-eval-pass &&
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
      --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 &&
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
      --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 &&
-python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json"
+step pmc_fetch20 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch20" -o run --output-format csv \
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
+step pmc_write20 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write20" -o run --output-format csv \
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
+python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" &&
+python tools/pmc_traffic.py "$OUT/pmc_fetch20" "$OUT/pmc_write20" "$OUT/hbm_traffic.json" "@b20"
 echo "done rc=$?"

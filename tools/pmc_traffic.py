@@ -9,7 +9,9 @@ by position: the one after kmat_kernel is the forward projection, the one after 
 the backward); a step starts at each kmat_kernel dispatch; the per-launch figure of an op
 is its summed bytes per step, averaged over the last PMC_LAST steps.
 
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> [out.json]
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> [out.json] [suffix]
+(suffix, e.g. "@b20" for a tools/loop_step.py N 20 pass: keys become op@b20 and are merged into
+an existing out.json)
 """
 import csv
 import glob
@@ -65,9 +67,13 @@ def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                                  "hbm_traffic.json")
+    suffix = sys.argv[4] if len(sys.argv) > 4 else ""
     fs, names = per_step(fdir, "FETCH_SIZE")
     ws, _ = per_step(wdir, "WRITE_SIZE")
     res = {}
+    if suffix and os.path.exists(out):
+        with open(out) as fi:
+            res = json.load(fi)
     for op, _ in OPS:
         f = [s.get(op, 0.0) for s in fs]
         w = [s.get(op, 0.0) for s in ws]
@@ -75,12 +81,12 @@ def main():
             continue
         fb = 2.0 * sum(f) / len(f)
         wb = sum(w) / len(w) if w else 0.0
-        res[op] = {"bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb, "steps": len(f),
+        res[op + suffix] = {"bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb, "steps": len(f),
                    "kernels": sorted(names[op]),
                    "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE per step of tools/loop_step.py"}
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
-    print(json.dumps({k: v["bytes_per_launch"] for k, v in res.items()}))
+    print(json.dumps({k: v["bytes_per_launch"] for k, v in res.items() if k.endswith(suffix) or not suffix}))
 
 
 if __name__ == "__main__":
