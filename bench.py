@@ -462,9 +462,17 @@ def main():
               "optimizer_iterations": st_ask.opt_iters, "evals_last_ask": _ask_evals(s),
               "driver": st_ask.chunks[0]["driver"] if st_ask.chunks else None}
 
-    # per-op device time at the restart batch one rank evaluates per L-BFGS-B iteration
+    # per-op device time at the restart batch one rank evaluates per L-BFGS-B iteration, on
+    # the candidates the restarts converged to (the scan's work depends on where the
+    # candidates sit: optimised points dominate more cells than random ones)
     b_r = math.ceil(args.restarts / world)
-    Xr = candidates(b_r, args.d, seed=5 + rank, device=device)
+    if st_ask.restart_X is not None and st_ask.restart_X.shape[0] == b_r:
+        Xr = torch.as_tensor(np.ascontiguousarray(st_ask.restart_X.reshape(b_r, -1)), dtype=torch.float64,
+                             device=device)
+        xr_note = "the last ask's optimised restart candidates"
+    else:
+        Xr = candidates(b_r, args.d, seed=5 + rank, device=device)
+        xr_note = "Sobol candidates"
     kt_r, how = kernel_times(acqf_ask, Xr)
 
     eval_pass, kernels_b = None, None
@@ -586,7 +594,7 @@ def main():
             "kernels": kernels_r,
             "kernel_ms": {k: round(v, 4) for k, v in kt_r.items()},
             "kernel_ms_method": f"{how} of 10 launches per op between HIP events (torch current stream), "
-                                f"batch {b_r}",
+                                f"batch {b_r}: {xr_note}",
             "ask": {"ask_s": round(ms * 1e-3, 4), "evals_per_ask": round(evals / args.steps, 1), "tell_s": round(t_tell, 3),
                     "phases_last_ask": phases, "n_base": acqf_ask.nb, "cells_total": sum_cells_r,
                     "box_decomposition": acqf_ask.box_path},

@@ -12,7 +12,9 @@
 // The plan copies the state / model structs; the device buffers they point to, the
 // workspace and the X / output buffers must outlive it (the Python QNEHVI object owns them).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <new>
 #include <vector>
 
@@ -28,7 +30,22 @@ size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b);
 int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double* Mm, const double* R,
                   const double* L22, const double* dG, double* dKx, double* ws);
 int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
-                  double* L22, int* flags);
+                  double* L22, int* flags, int tile_rows);
+bool qs_applies(const evr_qnehvi_state* st, int b, int d);
+size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
+size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
+int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+               double* R, double* P);
+int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX);
+constexpr int QS_TILE_ROWS = 16;
+
+// b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
+// EVR_SMALL=0 keeps the 64 x 64-tile path for A/B timing and the parity test
+static bool small_path(const evr_qnehvi_state* st, int b, int d) {
+  const char* e = std::getenv("EVR_SMALL");   // read per plan (plans are built once per batch size)
+  return !(e && std::string(e) == "0") && qs_applies(st, b, d);
+}
 size_t kcross_grad_ws_doubles(int n1, int n2, int d);
 int gemm_backend_init();
 int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
@@ -37,7 +54,8 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
                        double* work);
 
 struct PlanLayout {
-  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, bytes;
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, bytes;
+  bool small;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -51,19 +69,24 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     o += al256(bytes);
     return r;
   };
+  L.small = small_path(st, b, md->d);
   L.Kx = take(8 * m * n * b);
   L.R = take(8 * m * Rr * b);
-  L.P = take(8 * m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b);
-  L.Wf = take(8 * proj_forward_ws_doubles(st, b));
+  L.P = take(8 * (L.small ? qs_norms_doubles(st, b) : m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b));
+  L.Wf = take(8 * (L.small ? 0 : proj_forward_ws_doubles(st, b)));
   L.G = take(8 * (size_t)st->S * m * b);
   L.L22 = take(8 * m * b);
   L.flags = take(4 * m * b);
   L.hvi = take(8 * (size_t)evr_hvi_workspace_doubles(st, b, backward));
   if (backward) {
     L.dG = take(8 * (size_t)st->S * m * b);
-    L.bws = take(8 * proj_backward_ws_doubles(st, b));
-    L.dKx = take(8 * m * n * b);
-    L.kg = take(8 * kcross_grad_ws_doubles(st->n, b, md->d));
+    if (L.small) {
+      L.dxp = take(8 * qs_dxp_doubles(st, b, md->d));
+    } else {
+      L.bws = take(8 * proj_backward_ws_doubles(st, b));
+      L.dKx = take(8 * m * n * b);
+      L.kg = take(8 * kcross_grad_ws_doubles(st->n, b, md->d));
+    }
   }
   L.bytes = o;
   return L;
@@ -100,16 +123,22 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   double* L22 = (double*)(w + p->L.L22);
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
-  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
-                                 md->lengthscales, nullptr, nullptr, Kx))
+  const bool small = p->L.small;
+  if (small) {   // K_x is built inside qs_fwd
+    if (int rc = qs_forward(s, st, md, b, p->X, R, P)) return rc;
+  } else if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift,
+                                        md->scale, md->lengthscales, nullptr, nullptr, Kx)) {
     return rc;
-  if (int rc = proj_forward(s, st, b, md->M, Kx, R, P, p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr))
+  } else if (int rc = proj_forward(s, st, b, md->M, Kx, R, P,
+                                   p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr)) {
     return rc;
-  if (int rc = samples_norms(s, st, b, R, P, G, L22, flags)) return rc;
+  }
+  if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : 64)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
   double* dG = (double*)(w + p->L.dG);
-  double* dKx = (double*)(w + p->L.dKx);
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
+  if (small) return qs_backward(s, st, md, b, p->X, R, L22, dG, (double*)(w + p->L.dxp), p->dX);
+  double* dKx = (double*)(w + p->L.dKx);
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;
   return kcross_grad_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
                             md->lengthscales, nullptr, dKx, p->dX, (double*)(w + p->L.kg));

@@ -597,11 +597,11 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 }
 
 int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
-                  double* L22, int* flags) {
+                  double* L22, int* flags, int tile_rows) {
   if (b == 0) return 0;
   const int Rr = qn_rows(st);
-  const int nrt = cdiv(Rr, PT);
-  const int nrt_used = cdiv(st->n + st->nb, PT);
+  const int nrt = cdiv(Rr, tile_rows);   // partial-norm tiles (64 rows here, 16 in qnehvi_small.hip)
+  const int nrt_used = cdiv(st->n + st->nb, tile_rows);
   dim3 grid(cdiv(b, 64), st->m, cdiv(st->S, SCH));
   qn_samples_norms<<<grid, 64, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, nrt_used, nrt, norms, R, st->c, st->ym, st->ys,
                                         st->kxx, st->zq, st->obj_a, st->obj_b, G, L22, flags);
@@ -640,7 +640,7 @@ int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const do
 int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* norms,
                              double* G, double* L22, int* flags) {
   EVR_CHECK(st && R && norms && G && L22 && flags && b >= 0, "evr_qnehvi_samples_norms: bad arguments");
-  return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags);
+  return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags, PT);
 }
 
 long long evr_qnehvi_project_backward_workspace_doubles(const evr_qnehvi_state* st, int b) {

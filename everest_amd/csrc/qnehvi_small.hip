@@ -1,0 +1,377 @@
+// Small-batch (b <= 32) projections of the qNEHVI evaluation chain — the L-BFGS-B restart
+// batch of ask() (BoFire: num_restarts candidates per optimiser evaluation,
+// bofire/strategies/predictives/botorch.py:384-405; 20 in BASELINE configs[3]).
+//
+// At b = 20 the operator M (m x Rr x n, 15.7 MB at the bench shape) is the only large
+// operand: both GEMMs are HBM streams over M with a 20-column right-hand side, not
+// MFMA-bound contractions.  The 64 x 64-tile paths (rocBLAS forward, split-K MFMA backward)
+// spent 19 + 25 us there plus five helper launches (mean row, norms, gR coefficients,
+// split-K sum, cross-gradient reduction).  Here:
+//   qs_fwd:  one workgroup per (16 rows of M_j, output j): K_x staged in LDS in 256-row
+//            chunks, v_mfma_f64_16x16x4 with a per-lane contiguous 128 B slice of each M row
+//            (the contraction index is permuted per lane, identically in A and B), the four
+//            waves' k-quarters reduced in a fixed order; epilogue writes R and the per-tile
+//            partial sums of squares the sampling kernel reads.
+//   qs_bwd:  one workgroup per (16 columns of M_j, output j): the gR coefficients (reduced
+//            over the S samples in a fixed order), gR generated in the B fetch from R, dG and
+//            the coefficients, dK_x = M_j^T gR by MFMA, and in the epilogue the cross-
+//            covariance gradient of the tile's 16 training rows (dK_x never reaches HBM).
+//   qs_dx_reduce: dX = sum over the (output, tile) partials in a fixed order.
+// Every reduction order is fixed: results are bitwise reproducible.
+#include <algorithm>
+
+#include "common.hpp"
+#include "../../include/everest_amd.h"
+
+using double4_t = __attribute__((ext_vector_type(4))) double;
+
+namespace evr {
+
+constexpr int QS_B = 32;     // max candidates
+constexpr int QS_FR = 16;    // rows of M per forward workgroup
+constexpr int QS_KC = 256;   // K_x rows staged per chunk
+constexpr int QS_BI = 16;    // columns of M (training rows) per backward workgroup
+constexpr int QS_MAXD = 8;   // input dims handled in registers by the backward epilogue
+
+__device__ __forceinline__ double4_t mfma4(double a, double b, double4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------
+// forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, int d, int kind,
+                                              const double* __restrict__ M, const double* __restrict__ Xn,
+                                              const double* __restrict__ X, const double* __restrict__ shift,
+                                              const double* __restrict__ scale, const double* __restrict__ ls,
+                                              double* __restrict__ R, double* __restrict__ P, int ntile) {
+  constexpr int MP = QS_KC + 4;                  // padded row of the staged M tile
+  __shared__ double Ms[QS_FR][MP];               // 16 x 256 slice of M_j (33 KB)
+  __shared__ double Ks[QS_KC][QS_B];             // 256 x 32 slice of K_x,j (64 KB), built here
+  __shared__ double Us[QS_KC][QS_MAXD + 1];      // the chunk's training rows / lengthscale
+  __shared__ double Uc[QS_B][QS_MAXD + 1];       // normalised candidates / lengthscale
+  __shared__ double red[4][QS_FR][QS_B + 1];
+  const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const double* Mj = M + (size_t)j * Rr * n;
+  const double* lsj = ls + (size_t)j * d;
+  double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  // coalesced chunk loads into registers (a wave reads 512 contiguous bytes of one M row per
+  // instruction; the chunk's training rows are one contiguous range), staged in LDS
+  // afterwards; the next chunk's loads are issued before the current chunk's MFMAs
+  constexpr int XL = QS_KC * QS_MAXD / 256;
+  double mv[QS_FR], xv[XL];
+  auto load = [&](int kc) {
+    const int kn = min(QS_KC, n - kc);
+#pragma unroll
+    for (int u = 0; u < QS_FR; ++u) {
+      const int r = r0 + u;
+      mv[u] = (r < Rr && tid < kn) ? Mj[(size_t)r * n + kc + tid] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < XL; ++u) {
+      const int e = u * 256 + tid;
+      xv[u] = e < kn * d ? Xn[(size_t)kc * d + e] : 0.0;
+    }
+  };
+  load(0);
+  if (tid < QS_B * QS_MAXD) {
+    const int c = tid / QS_MAXD, t = tid - c * QS_MAXD;
+    double v = 0.0;
+    if (c < b && t < d) {
+      v = X[(size_t)c * d + t];
+      if (shift) v -= shift[t];
+      if (scale) v *= scale[t];
+      v *= 1.0 / lsj[t];
+    }
+    Uc[c][t] = v;
+  }
+  constexpr int KW = QS_KC / 4;   // k per wave and chunk
+  for (int kc = 0; kc < n; kc += QS_KC) {
+    const int kn = min(QS_KC, n - kc);
+    __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
+#pragma unroll
+    for (int u = 0; u < QS_FR; ++u) Ms[u][tid] = mv[u];
+#pragma unroll
+    for (int u = 0; u < XL; ++u) {
+      const int e = u * 256 + tid;
+      if (e < kn * d) {
+        const int k = e / d, t = e - k * d;
+        Us[k][t] = xv[u] * (1.0 / lsj[t]);
+      }
+    }
+    __syncthreads();
+    if (kc + QS_KC < n) load(kc + QS_KC);
+    // K_x chunk: k(x_train, x_c) from explicit differences, as kmat_kernel (bitwise equal)
+    for (int e = tid; e < QS_KC * QS_B; e += 256) {
+      const int k = e / QS_B, c = e - k * QS_B;
+      double v = 0.0;
+      if (k < kn && c < b) {
+        double acc = 0.0;
+        for (int t = 0; t < d; ++t) {
+          const double df = Us[k][t] - Uc[c][t];
+          acc = fma(df, df, acc);
+        }
+        v = kernel_value(kind, acc);
+      }
+      Ks[k][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < KW / 4; ++t) {
+      const int k = wave * KW + 4 * t + kq;
+      const double a = Ms[i][k];
+      acc0 = mfma4(a, Ks[k][i], acc0);
+      acc1 = mfma4(a, Ks[k][i + 16], acc1);
+    }
+  }
+  // D map of v_mfma_f64_16x16x4: register q of lane l holds D[4q + (l >> 4)][l & 15]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[wave][4 * q + kq][i] = acc0[q];
+    red[wave][4 * q + kq][16 + i] = acc1[q];
+  }
+  __syncthreads();
+  {
+    const int rr = tid >> 4, cp = tid & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = cp + 16 * h;
+      const double v = ((red[0][rr][c] + red[1][rr][c]) + red[2][rr][c]) + red[3][rr][c];
+      if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
+      red[0][rr][c] = v;   // own slot only: read back by the norms below after the barrier
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * QS_B) {
+    const int cls = tid / QS_B, c = tid - cls * QS_B;
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < QS_FR; ++rr) {
+      const int r = r0 + rr;
+      const bool in = cls == 0 ? r < n : (r >= n && r < n + nb);
+      if (in) s = fma(red[0][rr][c], red[0][rr][c], s);
+    }
+    if (c < b) P[(((size_t)j * ntile + tile) * 2 + cls) * b + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// backward: per (16 training rows i0.., output j): coefficients, dK_x tile = M_j^T gR (MFMA),
+// cross-covariance gradient partial dXp[j*ntile + tile][c][k].  gR rows come from R (rows
+// < n + nb, times the per-candidate coefficients), a_j dG (sample rows) or the coefficient
+// itself (mean row); the chunk of 128 rows of M (16 columns) and of the gR sources is loaded
+// with coalesced row segments, the coefficients applied while staging in LDS.
+// ---------------------------------------------------------------------------------------
+constexpr int QS_RC = 128;   // rows of M per backward chunk
+__global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
+                                              const double* __restrict__ M, const double* __restrict__ R,
+                                              const double* __restrict__ dG, const double* __restrict__ L22,
+                                              const double* __restrict__ ys, const double* __restrict__ zq,
+                                              const double* __restrict__ oa, const double* __restrict__ Xn,
+                                              const double* __restrict__ X, const double* __restrict__ shift,
+                                              const double* __restrict__ scale, const double* __restrict__ ls,
+                                              double* __restrict__ dXp, int ntile, int rows_per) {
+  __shared__ double cf[3][QS_B];
+  __shared__ double red[8][QS_B][2];
+  __shared__ double Ms[QS_RC][QS_BI + 1];
+  __shared__ double Bs[QS_RC][QS_B + 1];
+  __shared__ double dk[4][QS_BI][QS_B + 1];
+  __shared__ double gx[8][QS_B][QS_MAXD];
+  const int tile = blockIdx.x, j = blockIdx.y, z = blockIdx.z, i0 = tile * QS_BI;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Rr = n + nb + nh + 1;
+  const int rbeg = z * rows_per, rend = min(Rr, rbeg + rows_per);   // this split's rows of M
+  const double aj = oa[j], sj = ys[j];
+  const double* Mj = M + (size_t)j * Rr * n;
+  const double* Rj = R + (size_t)j * Rr * b;
+  // chunk loads: M[r][i0 + col] (a wave covers 4 rows x 128 B), gR source (row, candidate)
+  constexpr int ML = QS_RC * QS_BI / 256, BL = QS_RC * QS_B / 256;
+  double mv[ML], bv[BL];
+  auto load = [&](int rc) {
+#pragma unroll
+    for (int u = 0; u < ML; ++u) {
+      const int e = u * 256 + tid, rr = e / QS_BI, cc = e % QS_BI, r = rc + rr;
+      mv[u] = (r < rend && i0 + cc < n) ? Mj[(size_t)r * n + i0 + cc] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < BL; ++u) {
+      const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
+      const double* src = nullptr;
+      if (c < b && r < rend && r < Rr - 1)
+        src = r < n + nb ? Rj + (size_t)r * b + c : dG + ((size_t)(r - n - nb) * m + j) * b + c;
+      bv[u] = src ? *src : 0.0;
+    }
+  };
+  load(rbeg);
+  // 1. gR coefficients of this output (qn_bwd_coef's algebra): dmu = sum_s a dG, dl = sum_s a dG z
+  {
+    const int c = tid & (QS_B - 1), g = tid >> 5;   // 8 sample groups
+    double dmu = 0.0, dl = 0.0;
+    if (c < b) {
+      constexpr int CU = 16;   // loads of 16 samples in flight, summed in sample order
+      for (int s0 = g; s0 < S; s0 += 8 * CU) {
+        double dv[CU], zv[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int s = s0 + 8 * u;
+          dv[u] = s < S ? dG[((size_t)s * m + j) * b + c] : 0.0;
+          zv[u] = s < S ? zq[(size_t)s * m + j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const double dy = aj * dv[u];
+          dmu += dy;
+          dl = fma(dy, zv[u], dl);
+        }
+      }
+    }
+    red[g][c][0] = dmu;
+    red[g][c][1] = dl;
+    __syncthreads();
+    if (tid < QS_B) {
+      double u = red[0][tid][0], v = red[0][tid][1];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) {
+        u += red[q][tid][0];
+        v += red[q][tid][1];
+      }
+      const double dbr = tid < b ? v / (2.0 * L22[(size_t)j * b + tid]) : 0.0;
+      cf[0][tid] = -2.0 * sj * sj * dbr;
+      cf[1][tid] = -2.0 * dbr;
+      cf[2][tid] = sj * u;
+    }
+  }
+  // 2. dK tile: D[i][c] = sum_r M[r][i0 + i] gR[r][c] over chunks of 128 rows
+  const int i = lane & 15, kq = lane >> 4;
+  double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  for (int rc = rbeg; rc < rend; rc += QS_RC) {
+    __syncthreads();   // coefficients ready / the previous chunk's MFMAs are done with Ms, Bs
+#pragma unroll
+    for (int u = 0; u < ML; ++u) {
+      const int e = u * 256 + tid;
+      Ms[e / QS_BI][e % QS_BI] = mv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < BL; ++u) {
+      const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
+      double v = bv[u];
+      if (r < n) v *= cf[0][c];
+      else if (r < n + nb) v *= cf[1][c];
+      else if (r < n + nb + nh) v *= aj;
+      else v = (r == Rr - 1 && r < rend && c < b) ? cf[2][c] : 0.0;
+      Bs[rr][c] = v;
+    }
+    __syncthreads();
+    if (rc + QS_RC < rend) load(rc + QS_RC);
+#pragma unroll
+    for (int t = 0; t < QS_RC / 16; ++t) {
+      const int rr = wave * (QS_RC / 4) + 4 * t + kq;
+      const double a = Ms[rr][i];
+      acc0 = mfma4(a, Bs[rr][i], acc0);
+      acc1 = mfma4(a, Bs[rr][i + 16], acc1);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    dk[wave][4 * q + kq][i] = acc0[q];
+    dk[wave][4 * q + kq][16 + i] = acc1[q];
+  }
+  __syncthreads();
+  // 3. cross-covariance gradient of the tile's rows: thread (candidate c, row group g of 8),
+  //    rows i0 + g and i0 + g + 8; dX_c += dK[i][c] dk(x_i, x_c)/dx_c (normalized units)
+  {
+    const int c = tid & (QS_B - 1), g = tid >> 5;
+    double acc[QS_MAXD];
+#pragma unroll
+    for (int k = 0; k < QS_MAXD; ++k) acc[k] = 0.0;
+    if (c < b) {
+      double xc[QS_MAXD], il[QS_MAXD];
+#pragma unroll
+      for (int k = 0; k < QS_MAXD; ++k) {
+        xc[k] = k < d ? (X[(size_t)c * d + k] - (shift ? shift[k] : 0.0)) * (scale ? scale[k] : 1.0) : 0.0;
+        il[k] = k < d ? 1.0 / ls[(size_t)j * d + k] : 0.0;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ii = g + 8 * h, irow = i0 + ii;
+        if (irow >= n) continue;
+        const double gk = ((dk[0][ii][c] + dk[1][ii][c]) + dk[2][ii][c]) + dk[3][ii][c];
+        double diff[QS_MAXD], d2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < QS_MAXD; ++k) {
+          const double df = k < d ? (xc[k] - Xn[(size_t)irow * d + k]) * il[k] : 0.0;
+          diff[k] = df * il[k];
+          d2 = fma(df, df, d2);
+        }
+        const double sgl = gk * kernel_dscale(kind, d2);
+#pragma unroll
+        for (int k = 0; k < QS_MAXD; ++k) acc[k] = fma(sgl, diff[k], acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < QS_MAXD; ++k) gx[g][c][k] = acc[k];
+    __syncthreads();
+    if (tid < QS_B * QS_MAXD) {
+      const int cc = tid / QS_MAXD, k = tid - cc * QS_MAXD;
+      double v = gx[0][cc][k];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v += gx[q][cc][k];
+      if (cc < b && k < d) dXp[((((size_t)j * gridDim.z + z) * ntile + tile) * b + cc) * d + k] = v;
+    }
+  }
+}
+
+// one wave per dX element: lane-strided partial sums, then a fixed xor-butterfly
+__global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
+                                                   const double* __restrict__ scale, double* __restrict__ dX) {
+  const int e = blockIdx.x, lane = threadIdx.x;
+  const int k = e % d;
+  double v = 0.0;
+  for (int p = lane; p < np; p += 64) v += dXp[(size_t)p * b * d + e];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) dX[e] = v * (scale ? scale[k] : 1.0);
+}
+
+// ---- launchers (qnehvi_plan.hip) ------------------------------------------------------
+bool qs_applies(const evr_qnehvi_state* st, int b, int d) { return b >= 1 && b <= QS_B && d <= QS_MAXD && st->m >= 1; }
+
+int qs_ntile_fwd(const evr_qnehvi_state* st) { return cdiv(qn_rows(st), QS_FR); }
+
+size_t qs_norms_doubles(const evr_qnehvi_state* st, int b) { return (size_t)st->m * qs_ntile_fwd(st) * 2 * b; }
+
+// backward row splits: enough workgroups (>= ~512) that each walks at most two 128-row chunks
+static int qs_zsplit(const evr_qnehvi_state* st) {
+  const int tiles = cdiv(st->n, QS_BI) * st->m;
+  return std::max(1, std::min(cdiv(qn_rows(st), QS_RC), cdiv(640, tiles)));
+}
+
+size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
+  return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
+}
+
+int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+               double* R, double* P) {
+  const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
+  qs_fwd<<<dim3(nt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, md->d, md->kind, md->M, md->Xn, X, md->shift,
+                                        md->scale, md->lengthscales, R, P, nt);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX) {
+  const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
+  const int rows_per = cdiv(cdiv(qn_rows(st), zs), 16) * 16;
+  qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
+                                            L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
+                                            md->lengthscales, dXp, nt, rows_per);
+  EVR_LAUNCH_CHECK();
+  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace evr

@@ -243,3 +243,127 @@ def fit_single(Xn: torch.Tensor, y_raw: np.ndarray, kind: int, ls_prior, noise_p
             nz = max(float(prior_sample_np(nzp, rng, 1)[0]) if nzp else 1e-3, MIN_INFERRED_NOISE_LEVEL)
             x0 = np.concatenate([[nz, 0.0], np.log(np.expm1(ls))])
     raise RuntimeError(f"GP fit failed after {max_attempts} attempts: {last_err}")
+
+
+# ---------------------------------------------------------------------------------------
+# lock-step fit of several outputs on shared inputs: one batched MLL launch chain per round
+# ---------------------------------------------------------------------------------------
+class MLLBatch:
+    """MLL / n (+ hyperpriors) value and gradient of B GPs sharing Xn (one per output),
+    evaluated for any subset of the outputs in one batched launch chain (kernel matrices,
+    psd_safe Cholesky + inverse, alpha, W = alpha alpha^T - K^-1, lengthscale gradients, the
+    scalar terms) and one device->host copy.  Returns None for a member whose Cholesky stays
+    not p.d. after the jitter ladder (NotPSDError of that fit)."""
+
+    def __init__(self, Xn: torch.Tensor, Ys: np.ndarray, kind: int, ls_prior, noise_prior):
+        self.Xn = Xn.contiguous()
+        self.n, self.d = Xn.shape
+        self.kind = kind
+        self.Y = torch.as_tensor(np.asarray(Ys, dtype=np.float64), device=Xn.device)   # B x n (standardized)
+        self.ls_prior = _prior(ls_prior)
+        self.noise_prior = _prior(noise_prior)
+
+    def __call__(self, idx: Sequence[int], xs: Sequence[np.ndarray]):
+        n, d, dev = self.n, self.d, self.Xn.device
+        xs = np.stack([np.asarray(x, dtype=np.float64) for x in xs])
+        noise, const, raw = xs[:, 0], xs[:, 1], xs[:, 2:]
+        ls = softplus_np(raw)
+        ls_t = torch.as_tensor(ls, device=dev)
+        Ky = ops.kernel_matrix(self.Xn, self.Xn, ls_t, self.kind, diag_add=torch.as_tensor(noise, device=dev))
+        L, Linv, _, info = ops.cholesky_inverse(Ky, 1e-8, 3, raise_on_fail=False)
+        it = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=dev)
+        r = (self.Y[it] - torch.as_tensor(const, device=dev)[:, None]).unsqueeze(-1).contiguous()   # B x n x 1
+        v = ops.gemm(Linv, r)
+        alpha = ops.gemm(Linv, v, transA=True)
+        W = ops.gemm(alpha, alpha, transB=True)
+        ops.gemm(Linv, Linv, transA=True, alpha=-1.0, beta=1.0, out=W)
+        gls = ops.kernel_lengthscale_grad(self.Xn, ls_t, W, self.kind)
+        terms = ops.mll_terms(L, Linv, r[..., 0].contiguous(), alpha[..., 0].contiguous())
+        host = torch.cat([terms.reshape(-1), gls.reshape(-1), info.to(torch.float64)]).cpu().numpy()
+        B = len(idx)
+        terms_h = host[:5 * B].reshape(B, 5)
+        gls_h = host[5 * B:5 * B + B * d].reshape(B, d)
+        info_h = host[5 * B + B * d:]
+        out = []
+        for k in range(B):
+            if info_h[k] != 0 or not np.all(np.isfinite(terms_h[k])):
+                out.append(None)
+                continue
+            logdet, quad, trKinv, sum_a, sum_a2 = terms_h[k]
+            ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * math.log(2 * math.pi)
+            d_noise = 0.5 * (sum_a2 - trKinv)
+            d_const = sum_a
+            d_ls = 0.5 * gls_h[k]
+            if self.ls_prior is not None:
+                ll += float(np.sum(prior_logpdf_np(self.ls_prior, ls[k])))
+                d_ls = d_ls + prior_dlogpdf_np(self.ls_prior, ls[k])
+            if self.noise_prior is not None:
+                ll += float(prior_logpdf_np(self.noise_prior, noise[k]))
+                d_noise += float(prior_dlogpdf_np(self.noise_prior, noise[k]))
+            g = np.concatenate([[d_noise, d_const], d_ls * sigmoid_np(raw[k])]) / n
+            out.append((ll / n, g))
+        return out
+
+
+def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_prior=(-4.0, 1.0),
+              max_attempts: int = 10, seed: int = 0, options: Optional[dict] = None,
+              standardize: bool = True) -> List[GPHyper]:
+    """fit_single for the B columns of ``Y_raw`` (n x B) on shared inputs, in lock-step: each
+    output runs its own L-BFGS-B (the native restatement of scipy's, csrc/lbfgsb.cpp; same
+    start, bounds and NotPSDError retries with prior samples as fit_single), and every round
+    evaluates the outputs that asked for a function value in ONE batched MLL launch chain.
+    The fits stay independent problems, as in the reference's per-surrogate
+    fit_gpytorch_mll (bofire/surrogates/single_task_gp.py:70-71)."""
+    from .optim import lbfgsb_steps
+
+    Y_raw = np.asarray(Y_raw, dtype=np.float64).reshape(Xn.shape[0], -1)
+    B, d = Y_raw.shape[1], Xn.shape[1]
+    opts = dict(options or {})
+    maxiter, maxfun = int(opts.get("maxiter", 15000)), int(opts.get("maxfun", 15000))
+    stats, Ys = [], []
+    for b in range(B):
+        ym, ys = standardize_params(Y_raw[:, b]) if standardize else (0.0, 1.0)
+        stats.append((ym, ys))
+        Ys.append((Y_raw[:, b] - ym) / ys)
+    lsp, nzp = _prior(ls_prior), _prior(noise_prior)
+    ev = MLLBatch(Xn, np.stack(Ys), kind, lsp, nzp)
+    if nzp is not None and nzp[0] == "lognormal":
+        noise0 = math.exp(nzp[1] - nzp[2] ** 2)
+    elif nzp is not None and nzp[0] == "gamma" and nzp[1] > 1:
+        noise0 = (nzp[1] - 1) / nzp[2]
+    else:
+        noise0 = 2 * MIN_INFERRED_NOISE_LEVEL
+    noise0 = max(noise0, MIN_INFERRED_NOISE_LEVEL)
+    lb = np.r_[MIN_INFERRED_NOISE_LEVEL, -np.inf, np.full(d, -np.inf)]
+    ub = np.full(d + 2, np.inf)
+    rngs = [np.random.default_rng(seed) for _ in range(B)]
+    attempts = [0] * B
+
+    def start(x0):
+        gen = lbfgsb_steps(x0, lb, ub, maxiter, maxfun)
+        return gen, next(gen)
+
+    runs = {b: start(np.concatenate([[noise0, 0.0], np.zeros(d)])) for b in range(B)}
+    result = {}
+    while runs:
+        idx = sorted(runs)
+        vals = ev(idx, [runs[b][1] for b in idx])
+        for b, v in zip(idx, vals):
+            gen, _ = runs[b]
+            if v is None:        # NotPSDError: sample_all_priors, then retry (max_attempts)
+                gen.close()
+                attempts[b] += 1
+                if attempts[b] >= max_attempts:
+                    raise RuntimeError(f"GP fit of output {b} failed after {max_attempts} attempts (NotPSDError)")
+                ls = prior_sample_np(lsp, rngs[b], d) if lsp else np.full(d, math.log(2.0))
+                nz = max(float(prior_sample_np(nzp, rngs[b], 1)[0]) if nzp else 1e-3, MIN_INFERRED_NOISE_LEVEL)
+                runs[b] = start(np.concatenate([[nz, 0.0], np.log(np.expm1(ls))]))
+                continue
+            f, g = v
+            try:
+                runs[b] = (gen, gen.send((-f, -g)))
+            except StopIteration as stop:
+                result[b] = stop.value.x
+                del runs[b]
+    return [GPHyper(lengthscale=softplus_np(result[b][2:]), noise=float(result[b][0]), constant=float(result[b][1]),
+                    y_mean=stats[b][0], y_std=stats[b][1]) for b in range(B)]

@@ -44,6 +44,8 @@ class OptimizeStats:
     t_raw: float = 0.0
     t_opt: float = 0.0
     chunks: List[dict] = field(default_factory=list)
+    restart_X: Optional[np.ndarray] = None    # this rank's optimised restart candidates (last chunk)
+    init_X: Optional[np.ndarray] = None       # the Boltzmann initial conditions
 
     @property
     def candidates_evaluated(self) -> int:
@@ -76,6 +78,20 @@ def minimize_lbfgsb(fun: Callable, x0: np.ndarray, lb: np.ndarray, ub: np.ndarra
     with scipy.optimize.minimize(method="L-BFGS-B", jac=True)'s defaults and driver loop:
     ``fun(x) -> (f, g)``; stop after ``maxiter`` iterations or more than ``maxfun``
     evaluations."""
+    gen = lbfgsb_steps(x0, lb, ub, maxiter, maxfun, maxcor, ftol, gtol, maxls)
+    x = next(gen)
+    try:
+        while True:
+            x = gen.send(fun(x))
+    except StopIteration as stop:
+        return stop.value
+
+
+def lbfgsb_steps(x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int = 15000, maxfun: int = 15000,
+                 maxcor: int = 10, ftol: float = 2.220446049250313e-09, gtol: float = 1e-5, maxls: int = 20):
+    """minimize_lbfgsb as a generator: yields each x to evaluate and receives ``(f, g)``
+    through ``send``; returns the LbfgsbResult (StopIteration.value).  Lets independent
+    problems advance in lock-step with one batched device evaluation per round (gp.fit_batch)."""
     from . import _native
 
     lib = _native.load()
@@ -94,7 +110,7 @@ def minimize_lbfgsb(fun: Callable, x0: np.ndarray, lb: np.ndarray, ub: np.ndarra
         status = 0
         while True:
             if task == LBFGSB_FG:
-                f, g = fun(x.copy())
+                f, g = yield x.copy()
                 f = float(f)
                 g = np.ascontiguousarray(np.asarray(g, dtype=np.float64).reshape(n))
                 nfev += 1
@@ -414,6 +430,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     # 3. Boltzmann initial conditions
     init = initialize_q_batch if getattr(acqf, "log_acqf", False) else initialize_q_batch_nonneg
     X0, _ = init(X_raw, Y_raw, num_restarts, gen)
+    stats.init_X = X0
 
     # 4. restarts, chunks of batch_limit, L-BFGS-B (box) / SLSQP (linear constraints) on host
     #    with the analytic device value+gradient
@@ -521,6 +538,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         stats.opt_evals += info["evals"] * info["restarts"] + info["restarts"]
         stats.opt_iters += info["nit"]
         stats.chunks.append(info)
+        stats.restart_X = Xc
         results.append((vals, Xc))
     if results:
         vals = np.concatenate([r[0] for r in results])

@@ -105,27 +105,32 @@ class SingleTaskGPSurrogate:
     # ---- fit -------------------------------------------------------------------------
     def fit(self, experiments: pd.DataFrame, options: Optional[dict] = None):
         """TrainableSurrogate.fit (bofire/surrogates/trainable.py:24-42): valid rows of this output."""
+        X, Y = self._fit_data(experiments)
+        self._fit(X, Y, options)
+
+    def _fit_data(self, experiments: pd.DataFrame):
         key = self.output_key
         df = experiments
         if f"valid_{key}" in df:
             df = df[df[f"valid_{key}"] > 0]
         df = df.dropna(subset=[key])
-        X = df[self.inputs.get_keys()]
-        Y = df[[key]]
-        self._fit(X, Y, options)
+        return df[self.inputs.get_keys()], df[[key]]
 
-    def _fit(self, X: pd.DataFrame, Y: pd.DataFrame, options: Optional[dict] = None):
-        dev = device()
+    def _fit_problem(self, X: pd.DataFrame, Y: pd.DataFrame) -> dict:
+        """Everything the MLL fit needs: transformed inputs, bounds, targets, kernel, priors."""
         Xt = self.transform_inputs(X)
         lo, hi = self._bounds(X)
-        Xn = torch.as_tensor((Xt - lo) / (hi - lo), dtype=torch.float64, device=dev)
-        y = Y.values[:, 0].astype(np.float64)
-        kind = kernel_kind(self.kernel)
-        ls_prior = map_prior(getattr(self.kernel, "lengthscale_prior", None), Xt.shape[1])
-        noise_prior = map_prior(self.noise_prior, 1)
-        standardize = self.output_scaler == ScalerEnum.STANDARDIZE
-        hyp = fit_single(Xn, y, kind, ls_prior, noise_prior, standardize=standardize, options=options)
-        self._set_state(Xt, y, lo, hi, kind, hyp)
+        return dict(Xt=Xt, lo=lo, hi=hi, y=Y.values[:, 0].astype(np.float64), kind=kernel_kind(self.kernel),
+                    ls_prior=map_prior(getattr(self.kernel, "lengthscale_prior", None), Xt.shape[1]),
+                    noise_prior=map_prior(self.noise_prior, 1),
+                    standardize=self.output_scaler == ScalerEnum.STANDARDIZE)
+
+    def _fit(self, X: pd.DataFrame, Y: pd.DataFrame, options: Optional[dict] = None):
+        pb = self._fit_problem(X, Y)
+        Xn = torch.as_tensor((pb["Xt"] - pb["lo"]) / (pb["hi"] - pb["lo"]), dtype=torch.float64, device=device())
+        hyp = fit_single(Xn, pb["y"], pb["kind"], pb["ls_prior"], pb["noise_prior"], standardize=pb["standardize"],
+                         options=options)
+        self._set_state(pb["Xt"], pb["y"], pb["lo"], pb["hi"], pb["kind"], hyp)
 
     def _set_state(self, Xt, y, lo, hi, kind, hyp: GPHyper):
         self.state = dict(X=np.asarray(Xt), y=np.asarray(y), lo=np.asarray(lo), hi=np.asarray(hi), kind=int(kind),
@@ -187,16 +192,42 @@ class BotorchSurrogates:
 
     def fit(self, experiments: pd.DataFrame):
         """Fits the per-output GPs (independent problems, as in the reference's sequential
-        loop) concurrently: one host thread and one HIP stream per output, so the small,
-        latency-bound MLL kernels of the outputs overlap on the device.  Every fit is
-        deterministic on its own stream, so the hyperparameters do not depend on the overlap.
-        EVR_FIT_THREADS=1 restores the sequential loop."""
+        loop, bofire/surrogates/botorch_surrogates.py).  Outputs observed on the same rows with
+        the same kernel, priors and scalers (the usual case) are fitted in lock-step by
+        gp.fit_batch: one L-BFGS-B per output, one batched MLL launch chain per round.  Others
+        run concurrently, one host thread and one HIP stream per output (EVR_FIT_THREADS=1:
+        sequentially); EVR_FIT_BATCH=0 disables the lock-step fit."""
         import os
         from concurrent.futures import ThreadPoolExecutor
 
-        workers = int(os.environ.get("EVR_FIT_THREADS", "0") or 0) or len(self.surrogates)
-        if workers <= 1 or len(self.surrogates) <= 1 or not torch.cuda.is_available():
-            for s in self.surrogates:
+        from .gp import fit_batch
+
+        rest = list(self.surrogates)
+        if os.environ.get("EVR_FIT_BATCH", "1") != "0" and len(rest) > 1 and torch.cuda.is_available():
+            probs = [(s, s._fit_problem(*s._fit_data(experiments))) for s in rest]
+            groups = {}
+            for s, pb in probs:
+                key = (pb["Xt"].shape, pb["Xt"].tobytes(), pb["lo"].tobytes(), pb["hi"].tobytes(), pb["kind"],
+                       pb["ls_prior"], pb["noise_prior"], pb["standardize"])
+                groups.setdefault(key, []).append((s, pb))
+            rest = []
+            for members in groups.values():
+                if len(members) == 1:
+                    rest.append(members[0][0])
+                    continue
+                pb0 = members[0][1]
+                Xn = torch.as_tensor((pb0["Xt"] - pb0["lo"]) / (pb0["hi"] - pb0["lo"]), dtype=torch.float64,
+                                     device=device())
+                hyps = fit_batch(Xn, np.stack([pb["y"] for _, pb in members], 1), pb0["kind"], pb0["ls_prior"],
+                                 pb0["noise_prior"], standardize=pb0["standardize"])
+                for (s, pb), h in zip(members, hyps):
+                    s._set_state(pb["Xt"], pb["y"], pb["lo"], pb["hi"], pb["kind"], h)
+            if not rest:
+                return
+
+        workers = int(os.environ.get("EVR_FIT_THREADS", "0") or 0) or len(rest)
+        if workers <= 1 or len(rest) <= 1 or not torch.cuda.is_available():
+            for s in rest:
                 s.fit(experiments)
             return
         dev = device()
@@ -207,8 +238,8 @@ class BotorchSurrogates:
                 s.fit(experiments)
             stream.synchronize()
 
-        with ThreadPoolExecutor(max_workers=min(workers, len(self.surrogates))) as ex:
-            for f in [ex.submit(run, s) for s in self.surrogates]:
+        with ThreadPoolExecutor(max_workers=min(workers, len(rest))) as ex:
+            for f in [ex.submit(run, s) for s in rest]:
                 f.result()
 
     def compatibilize(self, inputs, outputs) -> GPBatch:
