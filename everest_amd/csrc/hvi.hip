@@ -209,23 +209,26 @@ __global__ __launch_bounds__(HV_THREADS) void hvi_tiled(int b, int nchunk, int C
   }
 }
 
-// acq[c] = (1/S) sum_{s, chunk} work[s][chunk][c] — block of 16 candidates x 16 partial
-// groups, fixed-order tree over the groups (bitwise reproducible).  A candidate whose
-// new-point Cholesky block failed (flags[j][c] != 0 for some j) gets NaN.
+// acq[c] = (1/S) sum_{s, chunk} work[s][chunk][c] — block of CX candidates x 256/CX partial
+// groups, fixed-order tree over the groups (bitwise reproducible for a given CX; CX = 4 for
+// the b <= 32 restart batches, whose wave-split scans leave S x 8 partials per candidate).
+// A candidate whose new-point Cholesky block failed (flags[j][c] != 0 for some j) gets NaN.
+template <int CX>
 __global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, int m, const double* __restrict__ work,
                                                       const int* __restrict__ flags, double* __restrict__ acq) {
-  __shared__ double red[16][17];
-  const int cx = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cx;
+  constexpr int G = 256 / CX;
+  __shared__ double red[G][CX + 1];
+  const int cx = threadIdx.x % CX, g = threadIdx.x / CX;
+  const int c = blockIdx.x * CX + cx;
   const int tot = S * nchunk;
   double sum = 0.0;
   if (c < b) {
 #pragma unroll 8
-    for (int k = g; k < tot; k += 16) sum += work[(size_t)k * b + c];
+    for (int k = g; k < tot; k += G) sum += work[(size_t)k * b + c];
   }
   red[g][cx] = sum;
   __syncthreads();
-  for (int o = 8; o > 0; o >>= 1) {
+  for (int o = G / 2; o > 0; o >>= 1) {
     if (g < o) red[g][cx] += red[g + o][cx];
     __syncthreads();
   }
@@ -235,6 +238,14 @@ __global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, 
       for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + c] != 0;
     acq[c] = bad ? nan("") : red[0][cx] / (double)S;
   }
+}
+
+static void hvi_reduce_fwd_launch(hipStream_t s, int S, int nchunk, int b, int m, const double* work,
+                                  const int* flags, double* acq) {
+  if (b <= 32)
+    hvi_reduce_fwd<4><<<cdiv(b, 4), 256, 0, s>>>(S, nchunk, b, m, work, flags, acq);
+  else
+    hvi_reduce_fwd<16><<<cdiv(b, 16), 256, 0, s>>>(S, nchunk, b, m, work, flags, acq);
 }
 
 // dG[s][j][c] = gout[c]/S * sum_chunk work[s][chunk][j][c]
@@ -824,7 +835,7 @@ template <int M, bool BWD>
 __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
-                                               double* __restrict__ dG) {
+                                               double* __restrict__ dG, int W) {
   constexpr int NV = BWD ? M + 1 : 1;
   constexpr int CW = KD_CT / 4;            // candidates per wave
   using K = CellKey<M>;
@@ -846,7 +857,9 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       tile = blockIdx.x;
     }
   }
-  const int c0 = tile * KD_CT, tid = threadIdx.x;
+  // W waves share one 16-candidate group and split its chunks (small candidate batches:
+  // the L-BFGS restarts), so a tile holds 64 / W candidates
+  const int c0 = tile * (KD_CT / W), tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int stride = kd.stride;
   KD_T0();
@@ -855,6 +868,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   const int qper = (NQall + nsplit - 1) / nsplit;
   const int q0 = min(NQall, split * qper);
   const int NQ = min(NQall, q0 + qper) - q0;                 // this workgroup's 16-group chunks
+  int qw0 = 0, NQw = NQ;                                     // this wave's share (set below)
   const int gbase = kd.goff[s] + 16 * q0;
   const int Gs = min(kd.goff[s + 1] - gbase, 16 * NQ);
   const Kd2Lds Lo = kd2_lds(stride, M, kd.max_groups);
@@ -902,9 +916,17 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   for (int e = tid; e < KD_CT * NV; e += 256) (&acc[0][0])[e] = 0.0;
   __syncthreads();
   KD_T(0);
-  const int cbase = wave * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
+  const int wsub = wave % W;
+  const int cbase = (wave / W) * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
+  const int aslot = wave * CW;         // ... and its accumulator rows
   if (c0 + cbase >= b) return;
-  const int NE = CW * NQ;
+  {   // this wave's share of the workgroup's chunks
+    const int qpw = (NQ + W - 1) / W;
+    const int qa = min(NQ, wsub * qpw);
+    qw0 = qa;
+    NQw = min(NQ, qa + qpw) - qa;
+  }
+  const int NE = CW * NQw;
 
   // ---- A: chunk pre-filter (lane = (chunk, candidate) entry), ballot compaction of the
   //      surviving entries, then their 16 group tests lane-dense ----
@@ -912,7 +934,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     unsigned short* ent = pA;   // entry list (pA is rewritten by the prefix)
     int nent = 0;
     for (int eb = 0; eb < NE; eb += 64) {
-      const int e = eb + lane, q = e >> 4, cl = e & 15;
+      const int e = eb + lane, q = qw0 + (e >> 4), cl = e & 15;
       bool pass = false;
       if (e < NE) {
         mA[q * KD_CT + cbase + cl] = 0;
@@ -924,7 +946,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     }
     wave_sync();
     for (int i = lane; i < nent; i += 64) {
-      const int e = ent[i], q = e >> 4, cl = e & 15;
+      const int e = ent[i], q = qw0 + (e >> 4), cl = e & 15;
       const uint4 t = thp[cbase + cl];
       const int gend = min(16, Gs - q * 16);
       unsigned int mask = 0;
@@ -934,24 +956,24 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
   }
   wave_sync();
-  // candidate-major prefix over the entries e = cl * NQ + q (a candidate's pairs contiguous);
+  // candidate-major prefix over the entries e = cl * NQw + q (a candidate's pairs contiguous);
   // each lane keeps the prefixes of its <= 8 entries in registers for the window marks
   const int per = (NE + 63) >> 6;                             // <= 8 (NQ <= KD_MAX_NQ)
   const int e0 = min(NE, lane * per), e1 = min(NE, e0 + per);
   // e / NQ = (e * magic) >> 16, exact for e <= 16 * KD_MAX_NQ
-  const unsigned int nq_magic = NQ > 0 ? (65536u + (unsigned int)NQ - 1u) / (unsigned int)NQ : 0u;
+  const unsigned int nq_magic = NQw > 0 ? (65536u + (unsigned int)NQw - 1u) / (unsigned int)NQw : 0u;
   int PA;
   int preE[9];
   {
-    int cl = (int)(((unsigned int)e0 * nq_magic) >> 16), q = e0 - cl * NQ;
+    int cl = (int)(((unsigned int)e0 * nq_magic) >> 16), q = e0 - cl * NQw;
     int cnt[8];
     int loc = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       cnt[k] = 0;
       if (e0 + k < e1) {
-        cnt[k] = __popc(mA[q * KD_CT + cbase + cl]);
-        if (++q == NQ) q = 0, ++cl;
+        cnt[k] = __popc(mA[(qw0 + q) * KD_CT + cbase + cl]);
+        if (++q == NQw) q = 0, ++cl;
       }
       loc += cnt[k];
     }
@@ -990,7 +1012,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     unsigned int mB = 0;
     int cg = 0;
     if (p < PA) {
-      const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = ownB - cl * NQ;
+      const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = qw0 + ownB - cl * NQw;
       const int c = cbase + cl;
       const int g = q * 16 + kth_bit16(mA[q * KD_CT + c], p - pA[ownB]);
       const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
@@ -1091,21 +1113,22 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       const int rnext = __shfl_down(rcv, 1, 64);
       if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) acc[rcv][v] += val[v];
+        for (int v = 0; v < NV; ++v) acc[rcv - cbase + aslot][v] += val[v];
       }
       KD_T(4);
     }
     wave_sync();   // mb / mc are rewritten by the next window
   }
   wave_sync();
-  const size_t ss = (size_t)s * nsplit + split;
-  if (lane < CW && c0 + cbase + lane < b) part[ss * b + c0 + cbase + lane] = acc[cbase + lane][0];
+  const int nst = nsplit * W;   // partial splits: workgroup splits x wave splits
+  const size_t ss = ((size_t)s * nsplit + split) * W + wsub;
+  if (lane < CW && c0 + cbase + lane < b) part[ss * b + c0 + cbase + lane] = acc[aslot + lane][0];
   if (BWD) {
     for (int e = lane; e < CW * M; e += 64) {
       const int j = e / CW, cl = e - j * CW, c = cbase + cl;
       if (c0 + c >= b) continue;
-      const double v = acc[c][NV > 1 ? 1 + j : 0];
-      if (nsplit == 1) dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * v;
+      const double v = acc[aslot + cl][NV > 1 ? 1 + j : 0];
+      if (nst == 1) dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * v;
       else dG[(ss * M + j) * b + c0 + c] = v;
     }
   }
@@ -1168,16 +1191,24 @@ static HviKd hvi_kd_of(const evr_qnehvi_state* st) {
                st->pts_stride, st->max_groups, st->scan_counters};
 }
 
+// waves sharing one 16-candidate group in hvi_kd2 (chunks split between them): the
+// restart batches (b <= 32) would leave 2-3 of the 4 waves idle otherwise
+static int hvi_kd_wsplit(int b) {
+  if (kd_variant() != 2) return 1;
+  return b <= 16 ? 4 : (b <= 32 ? 2 : 1);
+}
+
 // group-range splits per sample: fill ~1024 workgroups at small candidate batches
 static int hvi_kd_nsplit(const evr_qnehvi_state* st, int b) {
-  const int tiles = cdiv(b, KD_CT) * st->S;
+  const int tiles = cdiv(b, KD_CT / hvi_kd_wsplit(b)) * st->S;
   const int nq = (st->max_groups + 15) / 16;
   return std::max(1, std::min(std::min(cdiv(1024, tiles), 8), std::max(nq, 1)));
 }
 
-// workspace (doubles): S x ns x b partials | S x M x b int thresholds | (ns > 1) S x ns x M x b dG partials
+// workspace (doubles): S x ns x b partials | S x M x b int thresholds | (ns > 1) S x ns x M x b dG
+// partials, ns counting workgroup x wave splits
 static long long hvi_kd_workspace(const evr_qnehvi_state* st, int b) {
-  const long long ns = hvi_kd_nsplit(st, b);
+  const long long ns = (long long)hvi_kd_nsplit(st, b) * hvi_kd_wsplit(b);
   return (long long)st->S * ns * b + ((long long)st->S * st->m * b + 1) / 2 +
          (ns > 1 ? (long long)st->S * ns * st->m * b : 0);
 }
@@ -1186,14 +1217,16 @@ template <int M, bool BWD>
 static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
                          double* part, double* dG, const int* flags, double* acq) {
   const KdLds Lo = kd_lds(st->pts_stride, M, st->max_groups);
-  const int ntiles = cdiv(b, KD_CT);
-  const int ns = hvi_kd_nsplit(st, b);
+  const int W = hvi_kd_wsplit(b);
+  const int ntiles = cdiv(b, KD_CT / W);
+  const int nsb = hvi_kd_nsplit(st, b);   // workgroup splits
+  const int ns = nsb * W;                 // partial splits (workgroup x wave)
   int* th = (int*)(part + (size_t)st->S * ns * b);   // workspace: thresholds, then dG partials
   double* dgp = (double*)(th + (((size_t)st->S * M * b + 1) & ~(size_t)1));
   hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(b, M, st->pts_stride, G,
                                                                                      st->sorted_lo, th);
   EVR_LAUNCH_CHECK();
-  dim3 grid(ntiles, st->S, ns);
+  dim3 grid(ntiles, st->S, nsb);
   if (kd_variant() == 1) {
     EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)Lo.bytes));
@@ -1205,12 +1238,12 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
     const Kd2Lds L2 = kd2_lds(st->pts_stride, M, st->max_groups);
     EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd2<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)L2.bytes));
-    hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, ns, G, th, hvi_kd_of(st), gout, part,
-                                                  ns > 1 ? dgp : dG);
+    hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, nsb, G, th, hvi_kd_of(st), gout, part,
+                                                  ns > 1 ? dgp : dG, W);
   }
   EVR_LAUNCH_CHECK();
   if (acq) {
-    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, ns, b, M, part, flags, acq);
+    hvi_reduce_fwd_launch(s, st->S, ns, b, M, part, flags, acq);
     EVR_LAUNCH_CHECK();
   }
   if (BWD && ns > 1) {
@@ -1310,7 +1343,7 @@ int evr_hvi_forward(void* stream, const evr_qnehvi_state* st, int b, const doubl
   EVR_M_SWITCH(st->m, L);
 #undef L
   if (rc) return rc;
-  hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, p.nchunk, b, st->m, work, flags, acq);
+  hvi_reduce_fwd_launch(s, st->S, p.nchunk, b, st->m, work, flags, acq);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -1338,7 +1371,7 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
 #undef L
   if (rc) return rc;
   if (acq) {
-    hvi_reduce_fwd<<<cdiv(b, 16), 256, 0, s>>>(st->S, p.nchunk, b, st->m, wf, flags, acq);
+    hvi_reduce_fwd_launch(s, st->S, p.nchunk, b, st->m, wf, flags, acq);
     EVR_LAUNCH_CHECK();
   }
   const long long tot = (long long)st->S * st->m * b;
@@ -1379,7 +1412,7 @@ int hvi_raw(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, b
   if (b == 0) return 0;
   int rc = 0;
   if (st->grp_off) {
-    *nsplit = hvi_kd_nsplit(st, b);
+    *nsplit = hvi_kd_nsplit(st, b) * hvi_kd_wsplit(b);
     if (backward) {
 #define L(MM) rc = hvi_kd_launch<MM, true>(s, st, b, G, nullptr, work, dG, nullptr, nullptr)
       EVR_M_SWITCH(st->m, L);

@@ -34,7 +34,7 @@ int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 bool qs_applies(const evr_qnehvi_state* st, int b, int d);
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
-int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX);
@@ -124,11 +124,11 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
   const bool small = p->L.small;
-  if (small) {   // K_x is built inside qs_fwd
-    if (int rc = qs_forward(s, st, md, b, p->X, R, P)) return rc;
-  } else if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift,
-                                        md->scale, md->lengthscales, nullptr, nullptr, Kx)) {
+  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+                                 md->lengthscales, nullptr, nullptr, Kx))
     return rc;
+  if (small) {
+    if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;
   } else if (int rc = proj_forward(s, st, b, md->M, Kx, R, P,
                                    p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr)) {
     return rc;

@@ -7,8 +7,9 @@
 // MFMA-bound contractions.  The 64 x 64-tile paths (rocBLAS forward, split-K MFMA backward)
 // spent 19 + 25 us there plus five helper launches (mean row, norms, gR coefficients,
 // split-K sum, cross-gradient reduction).  Here:
-//   qs_fwd:  one workgroup per (16 rows of M_j, output j): K_x staged in LDS in 256-row
-//            chunks, v_mfma_f64_16x16x4 with a per-lane contiguous 128 B slice of each M row
+//   qs_fwd:  one workgroup per (16 rows of M_j, output j): K_x (kmat_kernel, once per
+//            output: computing it inside every row tile costs 49x the f64 exp) staged in LDS
+//            in 256-row chunks, v_mfma_f64_16x16x4 with a per-lane contiguous 128 B slice of each M row
 //            (the contraction index is permuted per lane, identically in A and B), the four
 //            waves' k-quarters reduced in a fixed order; epilogue writes R and the per-tile
 //            partial sums of squares the sampling kernel reads.
@@ -40,28 +41,24 @@ __device__ __forceinline__ double4_t mfma4(double a, double b, double4_t c) {
 // ---------------------------------------------------------------------------------------
 // forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, int d, int kind,
-                                              const double* __restrict__ M, const double* __restrict__ Xn,
-                                              const double* __restrict__ X, const double* __restrict__ shift,
-                                              const double* __restrict__ scale, const double* __restrict__ ls,
-                                              double* __restrict__ R, double* __restrict__ P, int ntile) {
+__global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
+                                              const double* __restrict__ Kx, double* __restrict__ R,
+                                              double* __restrict__ P, int ntile) {
   constexpr int MP = QS_KC + 4;                  // padded row of the staged M tile
   __shared__ double Ms[QS_FR][MP];               // 16 x 256 slice of M_j (33 KB)
-  __shared__ double Ks[QS_KC][QS_B];             // 256 x 32 slice of K_x,j (64 KB), built here
-  __shared__ double Us[QS_KC][QS_MAXD + 1];      // the chunk's training rows / lengthscale
-  __shared__ double Uc[QS_B][QS_MAXD + 1];       // normalised candidates / lengthscale
+  __shared__ double Ks[QS_KC][QS_B + 1];         // 256 x b slice of K_x,j (66 KB)
   __shared__ double red[4][QS_FR][QS_B + 1];
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, kq = lane >> 4;
   const double* Mj = M + (size_t)j * Rr * n;
-  const double* lsj = ls + (size_t)j * d;
+  const double* Kj = Kx + (size_t)j * n * b;
   double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
   // coalesced chunk loads into registers (a wave reads 512 contiguous bytes of one M row per
-  // instruction; the chunk's training rows are one contiguous range), staged in LDS
-  // afterwards; the next chunk's loads are issued before the current chunk's MFMAs
-  constexpr int XL = QS_KC * QS_MAXD / 256;
-  double mv[QS_FR], xv[XL];
+  // instruction; the chunk's K_x rows are one contiguous run of kn x b doubles), staged in
+  // LDS afterwards; the next chunk's loads are issued before the current chunk's MFMAs.
+  // K_x rows past the end of a partial chunk are zero (M's are too, but 0 x garbage is not 0).
+  double mv[QS_FR], kv[QS_B];
   auto load = [&](int kc) {
     const int kn = min(QS_KC, n - kc);
 #pragma unroll
@@ -70,58 +67,29 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, int 
       mv[u] = (r < Rr && tid < kn) ? Mj[(size_t)r * n + kc + tid] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < XL; ++u) {
+    for (int u = 0; u < QS_B; ++u) {
       const int e = u * 256 + tid;
-      xv[u] = e < kn * d ? Xn[(size_t)kc * d + e] : 0.0;
+      kv[u] = (u < b && e < kn * b) ? Kj[(size_t)kc * b + e] : 0.0;
     }
   };
   load(0);
-  if (tid < QS_B * QS_MAXD) {
-    const int c = tid / QS_MAXD, t = tid - c * QS_MAXD;
-    double v = 0.0;
-    if (c < b && t < d) {
-      v = X[(size_t)c * d + t];
-      if (shift) v -= shift[t];
-      if (scale) v *= scale[t];
-      v *= 1.0 / lsj[t];
-    }
-    Uc[c][t] = v;
-  }
   constexpr int KW = QS_KC / 4;   // k per wave and chunk
   for (int kc = 0; kc < n; kc += QS_KC) {
-    const int kn = min(QS_KC, n - kc);
     __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
 #pragma unroll
     for (int u = 0; u < QS_FR; ++u) Ms[u][tid] = mv[u];
 #pragma unroll
-    for (int u = 0; u < XL; ++u) {
+    for (int u = 0; u < QS_B; ++u) {
       const int e = u * 256 + tid;
-      if (e < kn * d) {
-        const int k = e / d, t = e - k * d;
-        Us[k][t] = xv[u] * (1.0 / lsj[t]);
-      }
+      if (u < b) Ks[e / b][e % b] = kv[u];   // e < 256 b: every row of the chunk, columns < b
     }
     __syncthreads();
     if (kc + QS_KC < n) load(kc + QS_KC);
-    // K_x chunk: k(x_train, x_c) from explicit differences, as kmat_kernel (bitwise equal)
-    for (int e = tid; e < QS_KC * QS_B; e += 256) {
-      const int k = e / QS_B, c = e - k * QS_B;
-      double v = 0.0;
-      if (k < kn && c < b) {
-        double acc = 0.0;
-        for (int t = 0; t < d; ++t) {
-          const double df = Us[k][t] - Uc[c][t];
-          acc = fma(df, df, acc);
-        }
-        v = kernel_value(kind, acc);
-      }
-      Ks[k][c] = v;
-    }
-    __syncthreads();
 #pragma unroll
     for (int t = 0; t < KW / 4; ++t) {
       const int k = wave * KW + 4 * t + kq;
       const double a = Ms[i][k];
+      // columns >= b of Ks are never written: they only reach D's columns >= b (not stored)
       acc0 = mfma4(a, Ks[k][i], acc0);
       acc1 = mfma4(a, Ks[k][i + 16], acc1);
     }
@@ -175,14 +143,21 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
                                               double* __restrict__ dXp, int ntile, int rows_per) {
   __shared__ double cf[3][QS_B];
   __shared__ double red[8][QS_B][2];
-  __shared__ double Ms[QS_RC][QS_BI + 1];
-  __shared__ double Bs[QS_RC][QS_B + 1];
-  __shared__ double dk[4][QS_BI][QS_B + 1];
-  __shared__ double gx[8][QS_B][QS_MAXD];
+  // the chunk tiles and the epilogue's reduction buffers share one LDS region (~53 KB per
+  // workgroup, two resident per CU)
+  constexpr int MS_SZ = QS_RC * (QS_BI + 1), BS_SZ = QS_RC * (QS_B + 1);
+  constexpr int DK_SZ = 4 * QS_BI * (QS_B + 1), GX_SZ = 8 * QS_B * QS_MAXD;
+  static_assert(DK_SZ + GX_SZ <= MS_SZ + BS_SZ, "epilogue buffers alias the chunk tiles");
+  __shared__ double lds[MS_SZ + BS_SZ];
+  auto Ms = reinterpret_cast<double(*)[QS_BI + 1]>(lds);
+  auto Bs = reinterpret_cast<double(*)[QS_B + 1]>(lds + MS_SZ);
+  auto dk = reinterpret_cast<double(*)[QS_BI][QS_B + 1]>(lds);
+  auto gx = reinterpret_cast<double(*)[QS_B][QS_MAXD]>(lds + DK_SZ);
   const int tile = blockIdx.x, j = blockIdx.y, z = blockIdx.z, i0 = tile * QS_BI;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Rr = n + nb + nh + 1;
-  const int rbeg = z * rows_per, rend = min(Rr, rbeg + rows_per);   // this split's rows of M
+  // this split's rows of M; the mean row (Rr - 1, a rank-1 term) is added in the epilogue
+  const int rbeg = z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
   const double aj = oa[j], sj = ys[j];
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Rj = R + (size_t)j * Rr * b;
@@ -199,7 +174,7 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
     for (int u = 0; u < BL; ++u) {
       const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
       const double* src = nullptr;
-      if (c < b && r < rend && r < Rr - 1)
+      if (c < b && r < rend)
         src = r < n + nb ? Rj + (size_t)r * b + c : dG + ((size_t)(r - n - nb) * m + j) * b + c;
       bv[u] = src ? *src : 0.0;
     }
@@ -259,8 +234,7 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       double v = bv[u];
       if (r < n) v *= cf[0][c];
       else if (r < n + nb) v *= cf[1][c];
-      else if (r < n + nb + nh) v *= aj;
-      else v = (r == Rr - 1 && r < rend && c < b) ? cf[2][c] : 0.0;
+      else v *= aj;
       Bs[rr][c] = v;
     }
     __syncthreads();
@@ -273,6 +247,7 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       acc1 = mfma4(a, Bs[rr][i + 16], acc1);
     }
   }
+  __syncthreads();   // all waves are done with Ms, Bs (dk aliases them)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     dk[wave][4 * q + kq][i] = acc0[q];
@@ -297,7 +272,8 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       for (int h = 0; h < 2; ++h) {
         const int ii = g + 8 * h, irow = i0 + ii;
         if (irow >= n) continue;
-        const double gk = ((dk[0][ii][c] + dk[1][ii][c]) + dk[2][ii][c]) + dk[3][ii][c];
+        double gk = ((dk[0][ii][c] + dk[1][ii][c]) + dk[2][ii][c]) + dk[3][ii][c];
+        if (z == 0) gk = fma(Mj[(size_t)(Rr - 1) * n + irow], cf[2][c], gk);   // mean row
         double diff[QS_MAXD], d2 = 0.0;
 #pragma unroll
         for (int k = 0; k < QS_MAXD; ++k) {
@@ -342,21 +318,27 @@ int qs_ntile_fwd(const evr_qnehvi_state* st) { return cdiv(qn_rows(st), QS_FR); 
 
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b) { return (size_t)st->m * qs_ntile_fwd(st) * 2 * b; }
 
-// backward row splits: enough workgroups (>= ~512) that each walks at most two 128-row chunks
+// backward row splits over the Rr - 1 non-mean rows: as many as keep every workgroup resident
+// at once (two per CU), in whole 128-row chunks
 static int qs_zsplit(const evr_qnehvi_state* st) {
-  const int tiles = cdiv(st->n, QS_BI) * st->m;
-  return std::max(1, std::min(cdiv(qn_rows(st), QS_RC), cdiv(640, tiles)));
+  const int tiles = cdiv(st->n, QS_BI) * st->m, nch = cdiv(qn_rows(st) - 1, QS_RC);
+  const int zs = std::max(1, std::min(nch, 512 / std::max(1, tiles)));
+  return cdiv(nch, cdiv(nch, zs));
+}
+
+static int qs_rows_per(const evr_qnehvi_state* st) {
+  const int nch = cdiv(qn_rows(st) - 1, QS_RC);
+  return cdiv(nch, qs_zsplit(st)) * QS_RC;
 }
 
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
   return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
 }
 
-int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P) {
   const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
-  qs_fwd<<<dim3(nt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, md->d, md->kind, md->M, md->Xn, X, md->shift,
-                                        md->scale, md->lengthscales, R, P, nt);
+  qs_fwd<<<dim3(nt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, md->M, Kx, R, P, nt);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -364,7 +346,7 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
-  const int rows_per = cdiv(cdiv(qn_rows(st), zs), 16) * 16;
+  const int rows_per = qs_rows_per(st);
   qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
                                             md->lengthscales, dXp, nt, rows_per);

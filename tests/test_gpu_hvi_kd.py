@@ -69,7 +69,9 @@ def kd_variant():
                                        (120, 6, 5, 64, 20)])
 def test_kd2_bitwise_equals_kd(kd_variant, n, d, m, S, b):
     """hvi_kd2 (chunk pre-filter + mark-based owner lookups) visits the same pairs and terms
-    in the same order as hvi_kd: forward and fused forward+backward are bitwise equal."""
+    in the same order as hvi_kd: forward and fused forward+backward are bitwise equal — for
+    b > 32; smaller batches split a candidate group's chunks over 2 or 4 waves (one more
+    partial per split, summed in a fixed order by the reduction): equal to 1e-13."""
     from everest_amd import ops
 
     kd, dense, lo, hi, d = _pair(n, d, m, S, seed=n + 3 * m)
@@ -81,7 +83,13 @@ def test_kd2_bitwise_equals_kd(kd_variant, n, d, m, S, b):
         kd_variant(v)
         a, g = ops.hvi_forward_backward(kd.state, G, b, flags)
         out[v] = (a, g, ops.hvi_forward(kd.state, G, b, flags))
-    assert all(torch.equal(x, y) for x, y in zip(out[1], out[2]))
+    if b > 32:
+        assert all(torch.equal(x, y) for x, y in zip(out[1], out[2]))
+    else:
+        for x, y in zip(out[1], out[2]):
+            assert torch.allclose(y, x, rtol=1e-13, atol=1e-16 * max(1.0, x.abs().max().item()))
+        a2, g2 = ops.hvi_forward_backward(kd.state, G, b, flags)     # repeats bitwise
+        assert torch.equal(a2, out[2][0]) and torch.equal(g2, out[2][1])
     assert torch.isfinite(out[2][0]).all() and (out[2][0] >= 0).all()
 
 
