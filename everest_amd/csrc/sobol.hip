@@ -16,8 +16,8 @@
 //     scaled by 2^-30 (point 0 goes through float32 as SobolEngine._first_point does), then
 //     the inverse-normal transform with torch's calc_erfinv (rational seed + 2 Newton steps).
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
-#include <random>
 #include <thread>
 #include <vector>
 
@@ -101,6 +101,48 @@ __global__ __launch_bounds__(256) void sobol_normal_kernel(int n, int nd, int d0
   out[idx] = z;
 }
 
+// The mt19937 stream of torch.Generator().manual_seed(seed) (std::mt19937 seeding) as raw
+// (untempered) state words, block after block of 624, each block twisted straight from the
+// previous one into the output (three vectorisable segments).  Only the lowest bit of each
+// tempered draw is used; tempering is linear over GF(2), so that bit is parity(word & mask),
+// evaluated by the consumers in parallel.  Same bits as std::mt19937 (tests compare the
+// scrambled engine state with torch.quasirandom.SobolEngine's).
+struct MtWords {
+  static constexpr int N = 624, Mo = 397;
+  static uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  static uint32_t lsb_mask() {
+    uint32_t mask = 0;
+    for (int k = 0; k < 32; ++k) mask |= (temper(1u << k) & 1u) << k;
+    return mask;
+  }
+  static uint32_t step(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  // out: ceil(n / 624) * 624 words; *done (if given) publishes the words written so far
+  static void generate(uint32_t seed, size_t n, uint32_t* out, std::atomic<size_t>* done = nullptr) {
+    uint32_t init[N];
+    init[0] = seed;
+    for (int i = 1; i < N; ++i) init[i] = 1812433253u * (init[i - 1] ^ (init[i - 1] >> 30)) + (uint32_t)i;
+    const uint32_t* o = init;
+    for (size_t blk = 0; blk * N < n; ++blk) {
+      uint32_t* w = out + blk * N;
+      for (int i = 0; i < N - Mo; ++i) w[i] = step(o[i], o[i + 1], o[i + Mo]);
+      for (int i = N - Mo; i < N - 1; ++i) w[i] = step(o[i], o[i + 1], w[i + Mo - N]);
+      w[N - 1] = step(o[N - 1], w[0], w[Mo - 1]);
+      o = w;
+      if (done && (blk & 15) == 15) done->store((blk + 1) * N, std::memory_order_release);
+    }
+    if (done) done->store((n + N - 1) / N * N, std::memory_order_release);
+  }
+};
+
 }  // namespace evr
 
 using namespace evr;
@@ -109,47 +151,63 @@ extern "C" {
 
 int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long* shift) {
   EVR_CHECK(dim >= 1 && V && shift, "evr_sobol_scramble: bad arguments");
-  std::mt19937 mt((uint32_t)(seed & 0xffffffffull));
-  for (int d = 0; d < dim; ++d) {
-    long long s = 0;
-    for (int b = 0; b < SOBOL_MAXBIT; ++b) s |= (long long)(mt() & 1u) << b;
-    shift[d] = s;
-  }
-  // lower-triangular scrambling matrices, one row per bit: ltm_dots[d][p] = sum_{k<=p}
-  // bit(d,p,k) 2^(29-k) with the diagonal forced to 1.
-  std::vector<uint32_t> dots((size_t)dim * SOBOL_MAXBIT);
-  for (int d = 0; d < dim; ++d)
-    for (int p = 0; p < SOBOL_MAXBIT; ++p) {
-      uint32_t r = 0;
-      for (int k = 0; k < SOBOL_MAXBIT; ++k) {
-        const uint32_t bit = mt() & 1u;
-        if (k < p && bit) r |= 1u << (SOBOL_MAXBIT - 1 - k);
-      }
-      r |= 1u << (SOBOL_MAXBIT - 1 - p);
-      dots[(size_t)d * SOBOL_MAXBIT + p] = r;
-    }
+  // the stream: shift bits (dim x 30), then the scrambling-matrix bits (dim x 30 x 30); the
+  // raw words are generated serially by this thread while the workers, one dimension range
+  // each, start as soon as the words of their range are published
+  const size_t nshift = (size_t)dim * SOBOL_MAXBIT, per_dim = (size_t)SOBOL_MAXBIT * SOBOL_MAXBIT;
+  const size_t ndraw = nshift + (size_t)dim * per_dim;
+  // per-thread buffer, kept between calls (an ask() scrambles ~10 MB of draws three times)
+  thread_local std::vector<uint32_t> words;
+  const size_t nw = (ndraw + MtWords::N - 1) / MtWords::N * MtWords::N;
+  if (words.size() < nw) words.resize(nw);
+  const uint32_t mask = MtWords::lsb_mask();
+  const uint32_t* wp = words.data();   // the caller's buffer (a thread_local name would
+                                       // resolve to each worker's own, empty instance)
+  auto bit = [wp, mask](size_t i) { return (uint32_t)__builtin_parity(wp[i] & mask); };
   auto work = [&](int dbeg, int dend) {
+    uint32_t col[SOBOL_MAXBIT];
     for (int d = dbeg; d < dend; ++d) {
-      const uint32_t* ld = &dots[(size_t)d * SOBOL_MAXBIT];
+      long long sh = 0;
+      for (int b = 0; b < SOBOL_MAXBIT; ++b) sh |= (long long)bit((size_t)d * SOBOL_MAXBIT + b) << b;
+      shift[d] = sh;
+      // lower-triangular scrambling matrix L (row p: bits k < p drawn, diagonal 1, upper
+      // triangle consumed and discarded); the scrambled direction number has bit 29 - p =
+      // parity(row_p & v) with row_p's bit 29 - k = L[p][k].  Stored by columns: col[b] is
+      // the output pattern of input bit b = 29 - k, so the product is an XOR over v's set bits.
+      const size_t bd = nshift + (size_t)d * per_dim;
+      for (int k = 0; k < SOBOL_MAXBIT; ++k) col[SOBOL_MAXBIT - 1 - k] = 1u << (SOBOL_MAXBIT - 1 - k);
+      for (int p = 1; p < SOBOL_MAXBIT; ++p)
+        for (int k = 0; k < p; ++k)
+          col[SOBOL_MAXBIT - 1 - k] |= bit(bd + p * SOBOL_MAXBIT + k) << (SOBOL_MAXBIT - 1 - p);
       for (int j = 0; j < SOBOL_MAXBIT; ++j) {
-        const uint32_t v = (uint32_t)V[(size_t)d * SOBOL_MAXBIT + j];
-        long long t2 = 0;
-        for (int p = SOBOL_MAXBIT - 1, l = 0; p >= 0; --p, ++l)
-          t2 |= (long long)(__builtin_popcount(ld[p] & v) & 1) << l;
+        uint32_t v = (uint32_t)V[(size_t)d * SOBOL_MAXBIT + j] & ((1u << SOBOL_MAXBIT) - 1u), t2 = 0;
+        while (v) {
+          t2 ^= col[__builtin_ctz(v)];
+          v &= v - 1;
+        }
         V[(size_t)d * SOBOL_MAXBIT + j] = t2;
       }
     }
   };
-  const int nth = dim >= 512 ? 8 : 1;
+  const uint32_t seed32 = (uint32_t)(seed & 0xffffffffull);
+  const int nth = dim >= 256 ? 8 : 1;
   if (nth == 1) {
+    MtWords::generate(seed32, ndraw, words.data());
     work(0, dim);
   } else {
+    std::atomic<size_t> done{0};
     std::vector<std::thread> th;
     const int per = (dim + nth - 1) / nth;
     for (int i = 0; i < nth; ++i) {
       const int a = i * per, b = std::min(dim, a + per);
-      if (a < b) th.emplace_back(work, a, b);
+      if (a < b)
+        th.emplace_back([&, a, b] {
+          const size_t need = nshift + (size_t)b * per_dim;
+          while (done.load(std::memory_order_acquire) < need) std::this_thread::yield();
+          work(a, b);
+        });
     }
+    MtWords::generate(seed32, ndraw, words.data(), &done);
     for (auto& t : th) t.join();
   }
   return 0;
