@@ -296,7 +296,8 @@ class _BoxHviAcqf:
 
     def eval_host(self, x: np.ndarray, backward: bool):
         """Host round trip for the scipy optimiser: x (b x d or b x q x d numpy) -> (acq,
-        dX or None) numpy; q = 1 fast path: one pinned H2D copy, one plan launch, one D2H."""
+        dX or None) numpy; q = 1 fast path: one evr_qnehvi_plan_eval_host (x and the results
+        through pinned host memory inside the plan's host graph)."""
         b = x.shape[0]
         if x.ndim == 2 and self.supports_plan and self._pending_rows() is None:
             out = self.plan(b, backward).run_host(x)

@@ -13,6 +13,7 @@
 // workspace and the X / output buffers must outlive it (the Python QNEHVI object owns them).
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <new>
@@ -107,9 +108,41 @@ struct evr_qnehvi_plan {
   PlanLayout L;
   hipGraph_t graph;
   hipGraphExec_t exec;
-  double* hx;    // pinned staging of x (b x d) and [acq | dX] for evr_qnehvi_plan_minimize
-  double* hout;
+  // host-driven evaluations (evr_qnehvi_plan_minimize): fine-grained pinned buffers read and
+  // written by kernels of a second graph [copy-in, chain, copy-out], so one evaluation is one
+  // graph launch and a spin on a completion word (no blit copies, no stream synchronise)
+  double* hx;                    // x (b x d), then the evaluation's sequence number (u64)
+  double* hout;                  // acq (b), dX (b x d), then the completion word (u64)
+  hipGraph_t hgraph;
+  hipGraphExec_t hexec;
+  unsigned long long seq;
 };
+
+namespace evr {
+
+__global__ __launch_bounds__(256) void plan_copy_in(int n, const double* __restrict__ hx, double* __restrict__ X) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) X[i] = hx[i];
+}
+
+// acq and dX to the host buffer, then (after every thread's system-scope fence) the
+// evaluation's sequence number into the completion word the host spins on
+__global__ __launch_bounds__(256) void plan_copy_out(int b, int n, const double* __restrict__ acq,
+                                                     const double* __restrict__ dX, const double* hx,
+                                                     double* hout) {
+  for (int i = threadIdx.x; i < b; i += 256) hout[i] = acq[i];
+  if (dX)
+    for (int i = threadIdx.x; i < n; i += 256) hout[b + i] = dX[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long seq = *(volatile const unsigned long long*)(hx + n);
+    __threadfence_system();
+    *(volatile unsigned long long*)(hout + b + n) = seq;
+  }
+}
+
+}  // namespace evr
 
 static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   const evr_qnehvi_state* st = &p->st;
@@ -173,6 +206,9 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->exec = nullptr;
   p->hx = nullptr;
   p->hout = nullptr;
+  p->hgraph = nullptr;
+  p->hexec = nullptr;
+  p->seq = 0;
   if (int rc = gemm_backend_init()) {
     delete p;
     return rc;
@@ -221,6 +257,8 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
+  if (p->hexec) (void)hipGraphExecDestroy(p->hexec);
+  if (p->hgraph) (void)hipGraphDestroy(p->hgraph);
   if (p->hx) (void)hipHostFree(p->hx);
   if (p->hout) (void)hipHostFree(p->hout);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
@@ -228,15 +266,69 @@ void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   delete p;
 }
 
+// The host-evaluation buffers and graph, built on first use.
+static int plan_host_setup(evr_qnehvi_plan* p) {
+  if (p->hexec) return 0;
+  const int b = p->b, n = b * p->md.d;
+  if (!p->hx)
+    EVR_HIP(hipHostMalloc((void**)&p->hx, sizeof(double) * (n + 1), hipHostMallocMapped | hipHostMallocCoherent));
+  if (!p->hout)
+    EVR_HIP(hipHostMalloc((void**)&p->hout, sizeof(double) * ((size_t)b * (1 + p->md.d) + 1),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(p->hx, 0, sizeof(double) * (n + 1));
+  std::memset(p->hout, 0, sizeof(double) * ((size_t)b * (1 + p->md.d) + 1));
+  double *dhx = nullptr, *dhout = nullptr;
+  EVR_HIP(hipHostGetDevicePointer((void**)&dhx, p->hx, 0));
+  EVR_HIP(hipHostGetDevicePointer((void**)&dhout, p->hout, 0));
+  hipStream_t cs = nullptr;
+  EVR_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
+  if (!rc) {
+    plan_copy_in<<<cdiv(n, 256), 256, 0, cs>>>(n, dhx, (double*)p->X);
+    rc = plan_chain(cs, p);
+    if (!rc) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
+  }
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(cs, &g);
+  (void)hipStreamDestroy(cs);
+  if (!rc && e == hipSuccess && g && hipGraphInstantiate(&p->hexec, g, nullptr, nullptr, 0) == hipSuccess) {
+    p->hgraph = g;
+    return 0;
+  }
+  if (g) (void)hipGraphDestroy(g);
+  p->hexec = nullptr;
+  const std::string why = last_error();
+  EVR_CHECK(false, "qnehvi plan: host-evaluation graph capture failed (%s)", why.c_str());
+}
+
+// One evaluation at host x (b x d); [acq | dX] left in p->hout.
+static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
+  const int b = p->b, n = b * p->md.d;
+  if (int rc = plan_host_setup(p)) return rc;
+  std::memcpy(p->hx, x, sizeof(double) * n);
+  const unsigned long long seq = ++p->seq;
+  std::memcpy(p->hx + n, &seq, sizeof(seq));
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  EVR_HIP(hipGraphLaunch(p->hexec, s));
+  // spin on the completion word; every 256 polls ask the stream whether it has drained (a
+  // faulted or failed launch ends the wait with its error instead of spinning forever)
+  volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
+  for (unsigned k = 1; *done != seq; ++k) {
+    if ((k & 255) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipErrorNotReady) continue;
+      EVR_HIP(q);
+      if (*done != seq) EVR_CHECK(false, "qnehvi plan: evaluation finished without its completion word");
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  return 0;
+}
+
 // One evaluation of the restart batch at host x: f = -sum_r acq_r, g = -dX.
 static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g) {
   const int b = p->b, n = b * p->md.d;
-  std::memcpy(p->hx, x, sizeof(double) * n);
-  EVR_HIP(hipMemcpyAsync((void*)p->X, p->hx, sizeof(double) * n, hipMemcpyHostToDevice, s));
-  if (int rc = evr_qnehvi_plan_run((void*)s, p)) return rc;
-  EVR_HIP(hipMemcpyAsync(p->hout, p->acq, sizeof(double) * b, hipMemcpyDeviceToHost, s));
-  EVR_HIP(hipMemcpyAsync(p->hout + b, p->dX, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-  EVR_HIP(hipStreamSynchronize(s));
+  if (int rc = plan_eval_raw(s, p, x)) return rc;
   double acc = 0.0;
   for (int r = 0; r < b; ++r) {
     if (std::isnan(p->hout[r])) {
@@ -250,6 +342,13 @@ static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, do
   return 0;
 }
 
+int evr_qnehvi_plan_eval_host(void* stream, evr_qnehvi_plan* p, const double* x, double* out) {
+  EVR_CHECK(p && x && out, "evr_qnehvi_plan_eval_host: bad arguments");
+  if (int rc = plan_eval_raw((hipStream_t)stream, p, x)) return rc;
+  std::memcpy(out, p->hout, sizeof(double) * (size_t)p->b * (p->backward ? 1 + p->md.d : 1));
+  return 0;
+}
+
 int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0, const double* lb, const double* ub,
                              int maxiter, int maxfun, double factr, double pgtol, int mcor, int maxls, double* x,
                              double* acq, int* info) {
@@ -259,9 +358,6 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   const int b = p->b, n = b * p->md.d;
   for (int i = 0; i < n; ++i) EVR_CHECK(!(lb[i] > ub[i]), "evr_qnehvi_plan_minimize: lower bound above upper bound");
   hipStream_t s = (hipStream_t)stream;
-  if (!p->hx) EVR_HIP(hipHostMalloc((void**)&p->hx, sizeof(double) * n, hipHostMallocDefault));
-  if (!p->hout) EVR_HIP(hipHostMalloc((void**)&p->hout, sizeof(double) * (size_t)b * (1 + p->md.d),
-                                      hipHostMallocDefault));
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;

@@ -435,8 +435,7 @@ class QnehviPlan:
         self.work = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
         self.acq = self.out[:b]
         self.dX = self.out[b:].view(b, d)
-        self.host = torch.empty(b * (1 + d), dtype=torch.float64, pin_memory=True)
-        self.xhost = torch.empty(b, d, dtype=torch.float64, pin_memory=True)
+        self.host = torch.zeros(b * (1 + d), dtype=torch.float64)
         h = ctypes.c_void_p()
         call("evr_qnehvi_plan_create", _stream(), ctypes.byref(st), ctypes.byref(model), b, int(backward),
              self.X.data_ptr(), self.work.data_ptr(), self.acq.data_ptr(),
@@ -448,13 +447,12 @@ class QnehviPlan:
         call("evr_qnehvi_plan_run", _stream(), self._h)
 
     def run_host(self, x: np.ndarray) -> np.ndarray:
-        """x (b x d numpy) -> host copy of [acq | dX] (one H2D, one graph launch, one D2H)."""
-        self.xhost.numpy()[...] = x
-        self.X.copy_(self.xhost, non_blocking=True)
-        self.run()
-        self.host.copy_(self.out, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return self.host.numpy()
+        """x (b x d numpy) -> host [acq | dX] (evr_qnehvi_plan_eval_host: one graph launch
+        reading x from and writing the results to pinned host memory)."""
+        xh = np.ascontiguousarray(x, dtype=np.float64).reshape(self.b, self.d)
+        out = self.host.numpy()
+        call("evr_qnehvi_plan_eval_host", _stream(), self._h, xh.ctypes.data, out.ctypes.data)
+        return out
 
     def minimize(self, x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int, maxfun: int = 15000,
                  maxcor: int = 10, ftol: float = 2.220446049250313e-09, gtol: float = 1e-5, maxls: int = 20):

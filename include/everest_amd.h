@@ -239,6 +239,12 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
                            int backward, const double* X, void* work, double* acq, double* dX, int use_graph,
                            evr_qnehvi_plan** out);
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* plan);
+/* One evaluation at host x (b x d): out (host) = [acq (b) | dX (b x d, backward plans)].
+ * Runs a second graph [copy-in from fine-grained pinned memory, the chain, copy-out + a
+ * completion word] and spins on that word: no blit copies and no stream synchronise per
+ * evaluation (the hot loop of evr_qnehvi_plan_minimize; botorch's per-evaluation
+ * forward+backward of gen_candidates_scipy's objective). */
+int evr_qnehvi_plan_eval_host(void* stream, evr_qnehvi_plan* plan, const double* x, double* out);
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* plan);
 
 /* ---- acquisition restarts: native L-BFGS-B ------------------------------------------
@@ -267,8 +273,8 @@ void evr_lbfgsb_destroy(evr_lbfgsb* h);
 /* One joint restart problem driven natively on a backward plan: minimise
  * -sum_r acq(x_r) over the b restarts of `plan` in the box [lb, ub] (b*d host arrays each)
  * from x0 (b*d host), with scipy's wrapper rules (stop after maxiter iterations or more
- * than maxfun evaluations).  Each evaluation is one pinned H2D of x, one plan launch and
- * one D2H of [acq | dX] on `stream`, with no Python in the loop.  Outputs (host): x (b*d,
+ * than maxfun evaluations).  Each evaluation is one evr_qnehvi_plan_eval_host on `stream`,
+ * with no Python in the loop.  Outputs (host): x (b*d,
  * clipped to the box), acq (b) at x, info[4] = {iterations, evaluations, status (0
  * converged, 1 iteration/evaluation limit, 2 abnormal line search), last task}.
  * Returns EVR_ERR_NOTPSD when an evaluation yields NaN (a new-point posterior block not

@@ -63,3 +63,24 @@ def test_native_lbfgsb_tracks_scipy_on_the_acquisition():
     # same algorithm: the optimum agrees to the line-search tolerance scale
     assert abs(v1 - v2) <= 1e-6 * max(1.0, abs(v2))
     assert np.allclose(x1, x2, atol=1e-4)
+
+
+@pytest.mark.parametrize("backward", [False, True])
+def test_plan_eval_host_matches_device_evaluation(backward):
+    """evr_qnehvi_plan_eval_host (x from / [acq | dX] to pinned host memory inside the graph,
+    completion word instead of a stream synchronise) returns exactly the device chain's
+    values, evaluation after evaluation."""
+    acqf, lo, hi = _acqf()
+    rng = np.random.default_rng(9)
+    b, d = 8, len(lo)
+    p = acqf.plan(b, backward)
+    for _ in range(5):
+        x = lo + (hi - lo) * rng.uniform(size=(b, d))
+        out = p.run_host(x).copy()
+        Xd = torch.tensor(x, device="cuda")
+        if backward:
+            a, g = acqf.forward_backward(Xd)
+            assert np.array_equal(out[b:].reshape(b, d), g.cpu().numpy())
+        else:
+            a = acqf.forward(Xd)
+        assert np.array_equal(out[:b], a.cpu().numpy())
