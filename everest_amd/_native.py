@@ -143,6 +143,7 @@ _SIGS = {
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),
     "evr_sobol_scramble": ([c_int, ctypes.c_ulonglong, c_void_p, c_void_p], c_int),
+    "evr_sobol_scramble_range": ([c_int, ctypes.c_ulonglong, c_int, c_int, c_void_p, c_void_p], c_int),
     "evr_sobol_normal": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
 }
 

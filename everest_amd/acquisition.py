@@ -34,10 +34,32 @@ from . import _native, ops
 from .gp import GPBatch
 
 
-def sobol_base_samples(S: int, n_points: int, m: int, seed: int, device) -> torch.Tensor:
+def sobol_base_samples(S: int, n_points: int, m: int, seed: int, device, scrambled=None) -> torch.Tensor:
     """Device Sobol-normal base samples in the GEMM-ready layout m x n_points x S
     ([upstream] draw_sobol_normal_samples(n_points*m, S, seed), Sobol dim = point*m + output)."""
-    return ops.sobol_normal(S, n_points * m, seed, device, layout=1, m=m)
+    return ops.sobol_normal(S, n_points * m, seed, device, layout=1, m=m, scrambled=scrambled)
+
+
+_SCRAMBLE_POOL = None
+
+
+def _prefetch_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = None):
+    """Start ops.sobol_scramble on a worker thread (the host half of a Sobol draw overlaps the
+    device work queued meanwhile and the other draws); returns a future, or None for an empty
+    range."""
+    global _SCRAMBLE_POOL
+    nd = dim - d0 if nd is None else nd
+    if nd <= 0:
+        return None
+    if _SCRAMBLE_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _SCRAMBLE_POOL = ThreadPoolExecutor(max_workers=3, thread_name_prefix="evr-sobol")
+    return _SCRAMBLE_POOL.submit(ops.sobol_scramble, dim, seed, d0, nd)
+
+
+def _result(fut):
+    return None if fut is None else fut.result()
 
 
 def _host_threads() -> int:
@@ -402,6 +424,8 @@ class QNEHVI(_BoxHviAcqf):
         import time as _time
         tm = {}
         t0 = _time.perf_counter()
+        fut_prune = (_prefetch_scramble(len(base_rows) * m, prune_seed)
+                     if prune_baseline and z_prune is None else None)
         # ---- joint posterior at the training (+ pending) inputs, shared by prune and baseline
         K = ops.kernel_matrix(self.Xk, self.Xk, gp.ls, gp.kind) if npend else gp.kernel_train(noise=False)
         Kt = K[:, :, :n].contiguous() if npend else K                      # m x nk x n
@@ -420,7 +444,7 @@ class QNEHVI(_BoxHviAcqf):
             nc = cand.shape[0]
             Lp, _, _ = ops.cholesky(Sig_c, 1e-8, 3)
             if z_prune is None:
-                Zp = sobol_base_samples(prune_samples, nc, m, prune_seed, dev)   # m x nc x S'
+                Zp = sobol_base_samples(prune_samples, nc, m, prune_seed, dev, _result(fut_prune))  # m x nc x S'
             else:
                 Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()
             Yp = ops.gemm(Lp, Zp)
@@ -442,23 +466,26 @@ class QNEHVI(_BoxHviAcqf):
         self.nb = nb
         self.base_rows = base_rows
         idx = torch.as_tensor(base_rows, device=dev)
+        S_ = self.S
+        fut_q = _prefetch_scramble((nb + 1) * m, sampler_seed, nb * m, m) if z_new_full is None else None
+        fut_b = _prefetch_scramble(nb_t * m, sampler_seed) if nb > 0 and z_base_full is None else None
 
         # ---- baseline posterior root, samples, box decomposition ----------------------
         if nb > 0:
             Sig_b = Sig[:, idx][:, :, idx].contiguous()
             self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
-        S_ = self.S
         # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed;
         # pending rows from the (nb_t+n_p)*m-dimensional draw ([upstream] _update_base_samples
         # keeps the earlier rows of the base sampler, the same seed draws the new ones)
         if z_new_full is None:
-            self.zq = ops.sobol_normal(S_, (nb + 1) * m, sampler_seed, dev, d0=nb * m, nd=m)   # S x m
+            self.zq = ops.sobol_normal(S_, (nb + 1) * m, sampler_seed, dev, d0=nb * m, nd=m,
+                                       scrambled=_result(fut_q))                           # S x m
         else:
             self.zq = z_new_full[:, nb, :].to(**f64).contiguous()
         if nb > 0:
             if z_base_full is None:
-                Zb = sobol_base_samples(S_, nb_t, m, sampler_seed, dev)              # m x nb x S
+                Zb = sobol_base_samples(S_, nb_t, m, sampler_seed, dev, _result(fut_b))   # m x nb x S
                 if npend:
                     Zp_ = ops.sobol_normal(S_, nb * m, sampler_seed, dev, d0=nb_t * m, nd=npend * m, layout=1, m=m)
                     Zb = torch.cat([Zb, Zp_], 1).contiguous()

@@ -7,6 +7,8 @@
 // Replaces the [upstream] torch/LAPACK calls behind GPyTorch's Cholesky / solves
 // (Appendix A.4).
 #include <cmath>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "common.hpp"
@@ -347,26 +349,13 @@ __device__ __forceinline__ double4_t mm16(const double (*M1)[BNB + 1], int pr, i
   return acc;
 }
 
-__global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* __restrict__ Lm, long long sL, int ldl,
-                                                        double* __restrict__ Dinv, long long sD,
-                                                        int* __restrict__ info) {
-  const int b = blockIdx.x;
-  if (info[b]) return;
-  double* L = Lm + b * sL;
-  double* Di = Dinv + b * sD;
-  const int nb = min(BNB, n - k0);
-  __shared__ double A[BNB][BNB + 1];
-  __shared__ double X[BNB][BNB + 1];
-  __shared__ double colj[CP], erow[CP], piv[CP];
-  __shared__ int fail;
+// Factor the 64x64 block A (LDS, lower triangle, padding rows/cols as the identity) in
+// place into L_kk and its inverse into X (zeroed by the caller).  All 256 threads; returns
+// the first failing local pivot index or -1 (uniform over the workgroup).
+__device__ __forceinline__ int factor_diag64(double (*A)[BNB + 1], double (*X)[BNB + 1], double* colj, double* erow, double* piv,
+                             int* fail) {
   const int tid = threadIdx.x, wave = tid >> 6;
-  for (int e = tid; e < BNB * BNB; e += 256) {
-    const int i = e >> 6, c = e & 63;
-    // padding rows / columns beyond nb factor as the identity
-    A[i][c] = (i < nb && c <= i) ? L[(size_t)(k0 + i) * ldl + k0 + c] : (i == c ? 1.0 : 0.0);
-    X[i][c] = 0.0;
-  }
-  if (tid == 0) fail = -1;
+  if (tid == 0) *fail = -1;
   __syncthreads();
   CHOL_T0(0)
   for (int p = 0; p < BNB / CP; ++p) {
@@ -374,11 +363,11 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
     CHOL_T0(1)
     if (wave == 0) {
       const int bad = panel_factor16(A, X, c0, colj, erow, piv);
-      if (bad >= 0 && (tid & 63) == 0) fail = c0 + bad;
+      if (bad >= 0 && (tid & 63) == 0) *fail = c0 + bad;
     }
     __syncthreads();
     CHOL_T(1)
-    if (fail >= 0) break;
+    if (*fail >= 0) break;
     const int r0 = c0 + CP, R = BNB - r0;
     if (R == 0) break;
     CHOL_T0(2)
@@ -413,11 +402,9 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
     CHOL_T(3)
   }
   CHOL_T(0)
+  const int f = *fail;
+  if (f >= 0) return f;
   CHOL_T0(4)
-  if (fail >= 0) {
-    if (fail < nb && tid == 0) info[b] = k0 + fail + 1;
-    if (fail < nb) return;
-  }
   // inv(L) off-diagonal blocks by distance dd = i - j: wave pr owns the pair (pr + dd, pr);
   // T = sum_k L_ik X_kj stays in the accumulator, which is already the B fragment of X_ii T
   for (int dd = 1; dd < BNB / CP; ++dd) {
@@ -439,7 +426,14 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
     __syncthreads();
   }
   CHOL_T(4)
-  for (int e = tid; e < BNB * BNB; e += 256) {
+  return -1;
+}
+
+// store a factored diagonal block: L_kk (rows/cols < nb, lower) and inv(L_kk) (identity
+// padding beyond nb, ld BNB)
+__device__ __forceinline__ void store_diag64(const double (*A)[BNB + 1], const double (*X)[BNB + 1], int nb, double* L, int ldl,
+                             int k0, double* Di) {
+  for (int e = threadIdx.x; e < BNB * BNB; e += 256) {
     const int i = e >> 6, c = e & 63;
     if (i < nb && c < nb) {
       L[(size_t)(k0 + i) * ldl + k0 + c] = (c <= i) ? A[i][c] : 0.0;
@@ -448,6 +442,283 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* _
       Di[(size_t)i * BNB + c] = (i == c) ? 1.0 : 0.0;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void chol_diag_kernel(int n, int k0, double* __restrict__ Lm, long long sL, int ldl,
+                                                        double* __restrict__ Dinv, long long sD,
+                                                        int* __restrict__ info) {
+  const int b = blockIdx.x;
+  if (info[b]) return;
+  double* L = Lm + b * sL;
+  double* Di = Dinv + b * sD;
+  const int nb = min(BNB, n - k0);
+  __shared__ double A[BNB][BNB + 1];
+  __shared__ double X[BNB][BNB + 1];
+  __shared__ double colj[CP], erow[CP], piv[CP];
+  __shared__ int fail;
+  const int tid = threadIdx.x;
+  {
+    double v[16];   // all loads in flight before the LDS stores
+    const int c = tid & 63, i0 = tid >> 6;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = 4 * u + i0;
+      // padding rows / columns beyond nb factor as the identity
+      v[u] = (i < nb && c <= i) ? L[(size_t)(k0 + i) * ldl + k0 + c] : (i == c ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      A[4 * u + i0][c] = v[u];
+      X[4 * u + i0][c] = 0.0;
+    }
+  }
+  const int f = factor_diag64(A, X, colj, erow, piv, &fail);
+  if (f >= 0) {
+    if (f < nb && tid == 0) info[b] = k0 + f + 1;
+    if (f < nb) return;
+  }
+  store_diag64(A, X, nb, L, ldl, k0, Di);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused right-looking steps (one launch per 64-column block instead of three):
+//   chol_step_kernel(k): one workgroup per trailing lower tile (I, J) of step k.  Each
+//     recomputes the two panel tiles it needs, P_I = A_Ik inv(L_kk)^T and P_J, from the
+//     un-normalised panel (still in L) and Dinv_k, applies C_IJ -= P_I P_J^T, and the
+//     workgroup of the next diagonal tile (k+1, k+1) — whose update is then complete —
+//     factors it at once (L_k+1,k+1 and its inverse).  k = -1 factors block 0 only.
+//   chol_panel_kernel: after the last step, every off-diagonal tile L_IK = A_IK Dinv_K^T in
+//     place (the panels stay un-normalised while later steps still read them).
+// Workgroups of one launch never read what another writes, so no inter-workgroup sync.
+// ---------------------------------------------------------------------------------------
+// quadrant of the 64x64 product P Q^T (P, Q row-major LDS tiles): wave (wr, wc) owns rows
+// wr*32.., cols wc*32..; acc[bi][bj] in the MFMA D layout.
+__device__ __forceinline__ void mm64_nt(const double (*P)[BNB + 1], const double (*Q)[BNB + 1], int wr, int wc,
+                                        double4_t (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+  for (int kk = 0; kk < BNB; kk += 4) {
+    const double a0 = P[wr + i][kk + kq], a1 = P[wr + 16 + i][kk + kq];
+    const double b0 = Q[wc + i][kk + kq], b1 = Q[wc + 16 + i][kk + kq];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+}
+
+// tile (row block r0, col block c0) of the matrix into LDS (rows >= n zero).  All 16 loads
+// of a thread are issued before the first LDS store (a load -> store loop would wait on
+// every load in turn); a wave reads 512 contiguous bytes of one row per instruction.
+__device__ __forceinline__ void load_tile64(double (*T)[BNB + 1], const double* L, int ldl, int n, int r0, int c0) {
+  double v[16];
+  const int c = threadIdx.x & 63, i0 = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int i = 4 * u + i0;
+    v[u] = (r0 + i < n && c0 + c < n) ? L[(size_t)(r0 + i) * ldl + c0 + c] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) T[4 * u + i0][c] = v[u];
+}
+
+__device__ __forceinline__ void load_dinv64(double (*T)[BNB + 1], const double* Di) {
+  double v[16];
+  const int c = threadIdx.x & 63, i0 = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) v[u] = Di[(4 * u + i0) * BNB + c];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) T[4 * u + i0][c] = v[u];
+}
+
+// write a wave's quadrant accumulators into an LDS tile (row-major)
+__device__ __forceinline__ void put_quadrant(double (*T)[BNB + 1], int wr, int wc, const double4_t (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[wr + bi * 16 + rq + 4 * r][wc + bj * 16 + col] = acc[bi][bj][r];
+}
+
+__global__ __launch_bounds__(256) void chol_step_kernel(int n, int k, double* __restrict__ Lm, long long sL, int ldl,
+                                                        double* __restrict__ Dinv, long long sD,
+                                                        int* __restrict__ info) {
+  const int b = blockIdx.y;
+  if (info[b]) return;
+  double* L = Lm + b * sL;
+  __shared__ double TI[BNB][BNB + 1];
+  __shared__ double TJ[BNB][BNB + 1];
+  __shared__ double TD[BNB][BNB + 1];
+  __shared__ double colj[CP], erow[CP], piv[CP];
+  __shared__ int fail;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
+  int I = 0, J = 0;   // trailing tile (lower, row-major enumeration)
+  {
+    const int t = blockIdx.x;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    J = t - I * (I + 1) / 2;
+  }
+  const int r0 = (k + 1 + I) * BNB, c0 = (k + 1 + J) * BNB;
+  double4_t acc[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  // C quadrant straight into the accumulator layout
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
+        acc[bi][bj][r] = (row < n && cc < n) ? L[(size_t)row * ldl + cc] : 0.0;
+      }
+  if (k >= 0) {
+    const int p0 = k * BNB;
+    const double* Dk = Dinv + b * sD + (size_t)k * BNB * BNB;
+    load_tile64(TI, L, ldl, n, r0, p0);
+    if (I != J) load_tile64(TJ, L, ldl, n, c0, p0);
+    load_dinv64(TD, Dk);
+    __syncthreads();
+    // panel tiles P = A_panel Dinv_k^T, written back over their LDS source
+    double4_t pi[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+    double4_t pj[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+    mm64_nt(TI, TD, wr, wc, pi);
+    if (I != J) mm64_nt(TJ, TD, wr, wc, pj);
+    __syncthreads();
+    put_quadrant(TI, wr, wc, pi);
+    if (I != J) put_quadrant(TJ, wr, wc, pj);
+    __syncthreads();
+    double4_t u[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+    mm64_nt(TI, I != J ? TJ : TI, wr, wc, u);
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[bi][bj][r] = acc[bi][bj][r] + (-1.0) * u[bi][bj][r];
+  }
+  if (I != 0 || J != 0) {   // plain trailing tile: store (lower triangle of a diagonal tile)
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
+          if (row < n && cc < n && (I != J || cc <= row)) L[(size_t)row * ldl + cc] = acc[bi][bj][r];
+        }
+    return;
+  }
+  // the next diagonal block: factor it now (padding rows / columns beyond nb as the identity)
+  const int nb = min(BNB, n - r0);
+  __syncthreads();   // TI / TJ free
+  put_quadrant(TI, wr, wc, acc);
+  __syncthreads();
+  for (int e = tid; e < BNB * BNB; e += 256) {
+    const int i = e >> 6, c = e & 63;
+    TI[i][c] = (i < nb && c < nb) ? (c <= i ? TI[i][c] : 0.0) : (i == c ? 1.0 : 0.0);
+    TJ[i][c] = 0.0;
+  }
+  const int f = factor_diag64(TI, TJ, colj, erow, piv, &fail);
+  if (f >= 0) {
+    if (f < nb && tid == 0) info[b] = r0 + f + 1;
+    if (f < nb) return;
+  }
+  store_diag64(TI, TJ, nb, L, ldl, r0, Dinv + b * sD + (size_t)(k + 1) * BNB * BNB);
+}
+
+// off-diagonal tiles (I > K): L_IK = A_IK Dinv_K^T in place
+__global__ __launch_bounds__(256) void chol_panel_kernel(int n, double* __restrict__ Lm, long long sL, int ldl,
+                                                         const double* __restrict__ Dinv, long long sD,
+                                                         const int* __restrict__ info) {
+  const int b = blockIdx.y;
+  if (info[b]) return;
+  double* L = Lm + b * sL;
+  __shared__ double TA[BNB][BNB + 1];
+  __shared__ double TD[BNB][BNB + 1];
+  int I = 1, K = 0;
+  {
+    const int t = blockIdx.x;   // strictly lower tiles, row-major: row I has I tiles
+    while (I * (I + 1) / 2 <= t) ++I;
+    K = t - I * (I - 1) / 2;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
+  load_tile64(TA, L, ldl, n, I * BNB, K * BNB);
+  load_dinv64(TD, Dinv + b * sD + (size_t)K * BNB * BNB);
+  __syncthreads();
+  double4_t p[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  mm64_nt(TA, TD, wr, wc, p);
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = I * BNB + wr + bi * 16 + rq + 4 * r, cc = K * BNB + wc + bj * 16 + col;
+        if (row < n && cc < n) L[(size_t)row * ldl + cc] = p[bi][bj][r];
+      }
+}
+
+// ---------------------------------------------------------------------------------------
+// Triangular inverse by block rows, one launch per row i (instead of two GEMMs):
+//   X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj   for every j < i (one workgroup each),
+// X_ii = Dinv_i and zeros above the diagonal placed beforehand (place_diag_blocks_kernel).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tri_inv_row_kernel(int n, int i, const double* __restrict__ Lm, long long sL,
+                                                          int ldl, const double* __restrict__ Dinv, long long sD,
+                                                          double* __restrict__ Xm, long long sX, int ldx,
+                                                          const int* __restrict__ skip) {
+  const int b = blockIdx.y, j = blockIdx.x;
+  if (skip && skip[b]) return;
+  const double* L = Lm + b * sL;
+  double* X = Xm + b * sX;
+  __shared__ double TA[BNB][BNB + 1];
+  __shared__ double TB[BNB][BNB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4, li = lane & 15,
+            kq = lane >> 4;
+  double4_t t[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  for (int k = j; k < i; ++k) {
+    __syncthreads();
+    load_tile64(TA, L, ldl, n, i * BNB, k * BNB);      // L_ik
+    load_tile64(TB, X, ldx, n, k * BNB, j * BNB);      // X_kj
+    __syncthreads();
+    // T += L_ik X_kj  (B operand X[kk][c])
+#pragma unroll 4
+    for (int kk = 0; kk < BNB; kk += 4) {
+      const double a0 = TA[wr + li][kk + kq], a1 = TA[wr + 16 + li][kk + kq];
+      const double b0 = TB[kk + kq][wc + li], b1 = TB[kk + kq][wc + 16 + li];
+      t[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t[0][0], 0, 0, 0);
+      t[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t[0][1], 0, 0, 0);
+      t[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, t[1][0], 0, 0, 0);
+      t[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t[1][1], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  put_quadrant(TB, wr, wc, t);                          // T
+  load_dinv64(TA, Dinv + b * sD + (size_t)i * BNB * BNB);
+  __syncthreads();
+  double4_t y[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+#pragma unroll 4
+  for (int kk = 0; kk < BNB; kk += 4) {
+    const double a0 = TA[wr + li][kk + kq], a1 = TA[wr + 16 + li][kk + kq];
+    const double b0 = TB[kk + kq][wc + li], b1 = TB[kk + kq][wc + 16 + li];
+    y[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, y[0][0], 0, 0, 0);
+    y[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, y[0][1], 0, 0, 0);
+    y[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, y[1][0], 0, 0, 0);
+    y[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, y[1][1], 0, 0, 0);
+  }
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * BNB + wr + bi * 16 + rq + 4 * r, cc = j * BNB + wc + bj * 16 + col;
+        if (row < n && cc < n) X[(size_t)row * ldx + cc] = -y[bi][bj][r];
+      }
 }
 
 // Inverse of every 64x64 diagonal block of a given lower-triangular L (grid (blocks, batch)):
@@ -542,9 +813,29 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
 }
 
 // One blocked factorisation attempt of every batch member (jitter already in L's diagonal).
+// Default: the fused steps (nblk + 1 launches); EVR_CHOL=v1 keeps the diag / panel GEMM /
+// trailing GEMM sequence (3 launches per block) for A/B timing and the parity test.
+static bool chol_v1() {
+  const char* e = std::getenv("EVR_CHOL");
+  return e && e[0] == 'v' && e[1] == '1' && e[2] == 0;
+}
+
 int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long sL, double* Dinv, int* info) {
   const int nblk = (n + BNB - 1) / BNB;
   const long long sD = (long long)nblk * BNB * BNB;
+  if (!chol_v1()) {
+    for (int k = -1; k < nblk - 1; ++k) {
+      const int T = nblk - 1 - k;   // trailing tile rows (block 0 alone for k = -1)
+      const int tiles = k < 0 ? 1 : T * (T + 1) / 2;
+      chol_step_kernel<<<dim3(tiles, batch), 256, 0, s>>>(n, k, L, sL, ldl, Dinv, sD, info);
+      EVR_LAUNCH_CHECK();
+    }
+    if (nblk > 1) {
+      chol_panel_kernel<<<dim3(nblk * (nblk - 1) / 2, batch), 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, info);
+      EVR_LAUNCH_CHECK();
+    }
+    return 0;
+  }
   for (int kb = 0; kb < nblk; ++kb) {
     const int k0 = kb * BNB, nb = std::min(BNB, n - k0), r0 = k0 + nb, t = n - r0;
     double* Dk = Dinv + (size_t)kb * BNB * BNB;
@@ -563,7 +854,7 @@ int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long 
   return 0;
 }
 
-// X = L^-1 from L and the diagonal-block inverses (block forward substitution with GEMMs).
+// X = L^-1 from L and the diagonal-block inverses (block forward substitution).
 int tri_inv_blocked(hipStream_t s, int batch, int n, const double* L, int ldl, long long sL, const double* Dinv,
                     double* X, int ldx, long long sX, double* T, const int* skip) {
   const int nblk = (n + BNB - 1) / BNB;
@@ -571,6 +862,13 @@ int tri_inv_blocked(hipStream_t s, int batch, int n, const double* L, int ldl, l
   dim3 g1(cdiv((long long)n * n, 256), batch);
   place_diag_blocks_kernel<<<g1, 256, 0, s>>>(n, Dinv, sD, X, sX, ldx);
   EVR_LAUNCH_CHECK();
+  if (!chol_v1()) {
+    for (int i = 1; i < nblk; ++i) {
+      tri_inv_row_kernel<<<dim3(i, batch), 256, 0, s>>>(n, i, L, sL, ldl, Dinv, sD, X, sX, ldx, skip);
+      EVR_LAUNCH_CHECK();
+    }
+    return 0;
+  }
   const long long sT = (long long)BNB * n;
   for (int i = 1; i < nblk; ++i) {
     const int r0 = i * BNB, rb = std::min(BNB, n - r0);

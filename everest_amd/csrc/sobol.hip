@@ -150,7 +150,12 @@ using namespace evr;
 extern "C" {
 
 int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long* shift) {
-  EVR_CHECK(dim >= 1 && V && shift, "evr_sobol_scramble: bad arguments");
+  return evr_sobol_scramble_range(dim, seed, 0, dim, V, shift);
+}
+
+int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, long long* V, long long* shift) {
+  EVR_CHECK(dim >= 1 && V && shift && d0 >= 0 && nd >= 1 && d0 + nd <= dim,
+            "evr_sobol_scramble_range: bad arguments");
   // the stream: shift bits (dim x 30), then the scrambling-matrix bits (dim x 30 x 30); the
   // raw words are generated serially by this thread while the workers, one dimension range
   // each, start as soon as the words of their range are published
@@ -164,12 +169,13 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
   const uint32_t* wp = words.data();   // the caller's buffer (a thread_local name would
                                        // resolve to each worker's own, empty instance)
   auto bit = [wp, mask](size_t i) { return (uint32_t)__builtin_parity(wp[i] & mask); };
+  // dimensions [d0, d0 + nd) only; V / shift hold those dimensions (row d - d0)
   auto work = [&](int dbeg, int dend) {
     uint32_t col[SOBOL_MAXBIT];
     for (int d = dbeg; d < dend; ++d) {
       long long sh = 0;
       for (int b = 0; b < SOBOL_MAXBIT; ++b) sh |= (long long)bit((size_t)d * SOBOL_MAXBIT + b) << b;
-      shift[d] = sh;
+      shift[d - d0] = sh;
       // lower-triangular scrambling matrix L (row p: bits k < p drawn, diagonal 1, upper
       // triangle consumed and discarded); the scrambled direction number has bit 29 - p =
       // parity(row_p & v) with row_p's bit 29 - k = L[p][k].  Stored by columns: col[b] is
@@ -180,26 +186,28 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
         for (int k = 0; k < p; ++k)
           col[SOBOL_MAXBIT - 1 - k] |= bit(bd + p * SOBOL_MAXBIT + k) << (SOBOL_MAXBIT - 1 - p);
       for (int j = 0; j < SOBOL_MAXBIT; ++j) {
-        uint32_t v = (uint32_t)V[(size_t)d * SOBOL_MAXBIT + j] & ((1u << SOBOL_MAXBIT) - 1u), t2 = 0;
+        uint32_t v = (uint32_t)V[(size_t)(d - d0) * SOBOL_MAXBIT + j] & ((1u << SOBOL_MAXBIT) - 1u), t2 = 0;
         while (v) {
           t2 ^= col[__builtin_ctz(v)];
           v &= v - 1;
         }
-        V[(size_t)d * SOBOL_MAXBIT + j] = t2;
+        V[(size_t)(d - d0) * SOBOL_MAXBIT + j] = t2;
       }
     }
   };
   const uint32_t seed32 = (uint32_t)(seed & 0xffffffffull);
-  const int nth = dim >= 256 ? 8 : 1;
+  // the stream must be generated through the last requested dimension's matrix bits
+  const size_t nneed = nshift + (size_t)(d0 + nd) * per_dim;
+  const int nth = nd >= 256 ? 8 : 1;
   if (nth == 1) {
-    MtWords::generate(seed32, ndraw, words.data());
-    work(0, dim);
+    MtWords::generate(seed32, nneed, words.data());
+    work(d0, d0 + nd);
   } else {
     std::atomic<size_t> done{0};
     std::vector<std::thread> th;
-    const int per = (dim + nth - 1) / nth;
+    const int per = (nd + nth - 1) / nth;
     for (int i = 0; i < nth; ++i) {
-      const int a = i * per, b = std::min(dim, a + per);
+      const int a = d0 + i * per, b = std::min(d0 + nd, a + per);
       if (a < b)
         th.emplace_back([&, a, b] {
           const size_t need = nshift + (size_t)b * per_dim;
@@ -207,7 +215,7 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
           work(a, b);
         });
     }
-    MtWords::generate(seed32, ndraw, words.data(), &done);
+    MtWords::generate(seed32, nneed, words.data(), &done);
     for (auto& t : th) t.join();
   }
   return 0;

@@ -737,27 +737,44 @@ def _iid_normal(n: int, dim: int, seed: int, device, d0: int, nd: int, layout: i
     return Z.reshape(n, nd // m, m).permute(2, 1, 0).contiguous().to(device)
 
 
+def sobol_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = None):
+    """Host half of draw_sobol_normal_samples: the scrambled direction numbers (nd x 30) and
+    shifts (nd) of dims [d0, d0+nd) of SobolEngine(dim, scramble=True, seed) (CPU int64
+    tensors; evr_sobol_scramble_range).  None beyond SOBOL_MAXDIM (IID fallback).  Releases the
+    GIL: the acquisition prefetches it on a worker thread."""
+    nd = dim - d0 if nd is None else nd
+    if not (0 <= d0 and nd >= 1 and d0 + nd <= dim):
+        raise ValueError("sobol_scramble: dims out of range")
+    if dim > SOBOL_MAXDIM:
+        return None
+    V = _sobol_directions(dim)[d0:d0 + nd].clone()
+    shift = torch.empty(nd, dtype=torch.long)
+    call("evr_sobol_scramble_range", dim, int(seed), d0, nd, V.data_ptr(), shift.data_ptr())
+    return V, shift
+
+
 def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[int] = None,
-                 layout: int = 0, m: int = 1) -> torch.Tensor:
+                 layout: int = 0, m: int = 1, scrambled=None) -> torch.Tensor:
     """Device draw_sobol_normal_samples(dim, n, seed) restricted to dims [d0, d0+nd).
 
     layout 0 -> n x nd; layout 1 -> m x (nd/m) x n (sample index fastest, the GEMM-ready
-    layout of the baseline / prune samples: dim t = point*m + output)."""
+    layout of the baseline / prune samples: dim t = point*m + output).  ``scrambled``: the
+    (V, shift) of sobol_scramble(dim, seed, d0, nd) when already computed."""
     nd = dim - d0 if nd is None else nd
     if not (0 <= d0 and d0 + nd <= dim):
         raise ValueError("sobol_normal: dims out of range")
     if dim > SOBOL_MAXDIM:
         return _iid_normal(n, dim, seed, device, d0, nd, layout, m)
-    V = _sobol_directions(dim).clone()
-    shift = torch.empty(dim, dtype=torch.long)
-    call("evr_sobol_scramble", dim, int(seed), V.data_ptr(), shift.data_ptr())
-    Vd = V.to(device, non_blocking=False)
-    sd = shift.to(device)
     if layout == 0:
         out = torch.empty(n, nd, dtype=torch.float64, device=device)
     else:
         out = torch.empty(m, nd // m, n, dtype=torch.float64, device=device)
-    call("evr_sobol_normal", _stream(), n, nd, d0, Vd.data_ptr(), sd.data_ptr(), layout, m, out.data_ptr())
+    if nd == 0:
+        return out
+    V, shift = scrambled if scrambled is not None else sobol_scramble(dim, seed, d0, nd)
+    Vd = V.to(device, non_blocking=False)
+    sd = shift.to(device)
+    call("evr_sobol_normal", _stream(), n, nd, 0, Vd.data_ptr(), sd.data_ptr(), layout, m, out.data_ptr())
     return out
 
 

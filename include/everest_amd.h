@@ -425,6 +425,10 @@ int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int*
  * .shift.  evr_sobol_normal (device): normal samples of points 0..n-1, dims [d0, d0+nd):
  * layout 0 -> out[k*nd + t]; layout 1 -> out[(o*np + p)*n + k] with t = p*m + o, np = nd/m. */
 int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long* shift);
+/* The same for dimensions [d0, d0 + nd) of the dim-dimensional engine only: V (nd x 30) and
+ * shift (nd) hold those dimensions (the stream is still drawn through dimension d0 + nd - 1;
+ * the per-dimension work is skipped for the others). */
+int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, long long* V, long long* shift);
 int evr_sobol_normal(void* stream, int n, int nd, int d0, const long long* V, const long long* shift,
                      int layout, int m, double* out);
 

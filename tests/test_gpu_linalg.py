@@ -151,3 +151,43 @@ def test_kernel_matrix_wide_mfma(d, kind):
         # a rounded expansion would leave d2 ~ 1e-15, i.e. r ~ 3e-8 there
         assert torch.allclose(torch.diagonal(Ks[b]), torch.diagonal(Rs), rtol=0, atol=2.0 ** -49)
         assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
+
+
+@pytest.mark.parametrize("n", [64, 65, 130, 513, 1024])
+def test_fused_cholesky_inverse_matches_torch_and_v1(n, monkeypatch):
+    """The fused Cholesky (one launch per 64-column block: panel recompute + trailing update +
+    factor of the next diagonal block, then the in-place panel pass) and the one-launch-per-
+    row triangular inverse, against torch and against the three-launch-per-block v1 path."""
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(n)
+    A = torch.randn(3, n, n + 5, generator=g, dtype=torch.float64)
+    A = A @ A.transpose(1, 2) / n + 1e-2 * torch.eye(n, dtype=torch.float64)
+    L, Li, jit, info = ops.cholesky_inverse(_t(A))
+    ref = torch.linalg.cholesky(A)
+    assert info.cpu().eq(0).all() and jit.cpu().eq(0).all()
+    assert torch.allclose(L.cpu(), ref, rtol=1e-10, atol=1e-11 * ref.abs().max().item())
+    assert torch.allclose(Li.cpu(), torch.linalg.inv(ref), rtol=1e-8, atol=1e-9 * torch.linalg.inv(ref).abs().max().item())
+    assert torch.equal(torch.triu(L, 1).cpu(), torch.zeros_like(ref)) and torch.equal(torch.triu(Li, 1).cpu(), torch.zeros_like(ref))
+    monkeypatch.setenv("EVR_CHOL", "v1")
+    L1, Li1, _, _ = ops.cholesky_inverse(_t(A))
+    assert torch.allclose(L, L1, rtol=1e-12, atol=1e-13 * ref.abs().max().item())
+    assert torch.allclose(Li, Li1, rtol=1e-10, atol=1e-11 * Li1.abs().max().item())
+
+
+def test_fused_cholesky_failure_and_ladder():
+    """A member failing in a late diagonal block of the fused path reports the same pivot
+    index as v1 and gets the same jitter (psd_safe_cholesky per-member ladder)."""
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(3)
+    V = torch.randn(2, 200, 150, generator=g, dtype=torch.float64)
+    A = V @ V.transpose(1, 2)                      # rank 150 of 200: fails past block 2
+    A[0] = A[0] + torch.eye(200, dtype=torch.float64)
+    _, _, info = ops.cholesky(_t(A), 1e-8, 0, raise_on_fail=False)
+    inf = info.cpu().tolist()
+    assert inf[0] == 0 and (inf[1] == 0 or inf[1] > 128)
+    L, jit, info = ops.cholesky(_t(A), 1e-8, 3, raise_on_fail=False)
+    Lr, jr = ogp.psd_safe_cholesky(A)
+    assert torch.allclose(jit.cpu(), jr)
+    assert torch.allclose(L.cpu(), Lr, atol=1e-7)
