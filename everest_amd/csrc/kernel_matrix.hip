@@ -446,6 +446,9 @@ __global__ __launch_bounds__(256) void mll_terms_kernel(int n, const double* __r
                                                         const double* __restrict__ r,
                                                         const double* __restrict__ alpha,
                                                         double* __restrict__ part) {
+  // chunk ch: ||Linv||_F^2 over a contiguous 1/MT_CHUNKS of the n x n elements (the upper
+  // triangle is exactly zero), 8 loads in flight per thread; the O(n) terms of rows
+  // [ch*rc, ch*rc + rc) one row per thread
   const int b = blockIdx.x, ch = blockIdx.y;
   const int tid = threadIdx.x;
   const double* Lb = L + (size_t)b * n * n;
@@ -453,29 +456,36 @@ __global__ __launch_bounds__(256) void mll_terms_kernel(int n, const double* __r
   const double* rb = r + (size_t)b * n;
   const double* ab = alpha + (size_t)b * n;
   double t[5] = {0, 0, 0, 0, 0};
-  for (int i = ch; i < n; i += MT_CHUNKS) {
-    for (int j = tid; j <= i; j += 256) {
-      const double v = Ib[(size_t)i * n + j];
-      t[2] = fma(v, v, t[2]);
+  const size_t nn = (size_t)n * n, per = (nn + MT_CHUNKS - 1) / MT_CHUNKS;
+  const size_t beg = ch * per, end = min(nn, beg + per);
+  for (size_t e0 = beg + tid; e0 < end; e0 += 8 * 256) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t e = e0 + (size_t)u * 256;
+      v[u] = e < end ? Ib[e] : 0.0;
     }
-    if (tid == 0) {
-      t[0] += log(Lb[(size_t)i * n + i]);
-      t[1] = fma(rb[i], ab[i], t[1]);
-      t[3] += ab[i];
-      t[4] = fma(ab[i], ab[i], t[4]);
-    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[2] = fma(v[u], v[u], t[2]);
   }
-  __shared__ double red[256];
-  for (int q = 0; q < 5; ++q) {
-    red[tid] = t[q];
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
-    }
-    if (tid == 0) part[((size_t)b * MT_CHUNKS + ch) * 5 + q] = red[0];
+  const int rc = (n + MT_CHUNKS - 1) / MT_CHUNKS;
+  for (int i = ch * rc + tid; i < min(n, ch * rc + rc); i += 256) {
+    t[0] += log(Lb[(size_t)i * n + i]);
+    t[1] = fma(rb[i], ab[i], t[1]);
+    t[3] += ab[i];
+    t[4] = fma(ab[i], ab[i], t[4]);
+  }
+  __shared__ double red[5][256];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) red[q][tid] = t[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) red[q][tid] += red[q][tid + o];
     __syncthreads();
   }
+  if (tid < 5) part[((size_t)b * MT_CHUNKS + ch) * 5 + tid] = red[tid][0];
 }
 
 __global__ void mll_terms_finalize(int B, const double* __restrict__ part, double* __restrict__ out) {
@@ -543,6 +553,18 @@ int gemm_backend_init();
 }  // namespace evr
 
 using namespace evr;
+
+namespace evr {
+// graph-capturable MLL terms (mll_plan.hip): chunk partials only, reduced by the caller
+size_t mll_terms_part_doubles(int B) { return (size_t)B * MT_CHUNKS * 5; }
+int mll_terms_chunks() { return MT_CHUNKS; }
+int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const double* Linv, const double* r,
+                       const double* alpha, double* part) {
+  mll_terms_kernel<<<dim3(B, MT_CHUNKS), 256, 0, s>>>(n, L, Linv, r, alpha, part);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+}  // namespace evr
 
 extern "C" {
 
@@ -633,6 +655,7 @@ int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, con
   EVR_LAUNCH_CHECK();
   return 0;
 }
+
 
 int evr_gp_mll_terms(void* stream, int B, int n, const double* L, const double* Linv, const double* r,
                      const double* alpha, double* out) {

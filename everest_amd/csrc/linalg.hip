@@ -282,7 +282,34 @@ __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// cross-lane helpers (f64 as two dwords): readlane (uniform result) and a DPP quad broadcast
+// of lane s of every 4-lane group
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, l), hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ int quad_bcast32(int v, int s) {
+  switch (s) {   // quad_perm [s, s, s, s]
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xf, 0xf, false);
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xf, 0xf, false);
+    default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xf, 0xf, false);
+  }
+}
+
+__device__ __forceinline__ double quad_bcast_f64(double v, int s) {
+  const long long x = __double_as_longlong(v);
+  const int lo = quad_bcast32((int)x, s), hi = quad_bcast32((int)(x >> 32), s);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
+// Lane (row r, quad q) holds A[r][q + 4k].  Per pivot step the pivot comes by readlane (a
+// uniform scalar: its reciprocal starts at once and the failure test is a scalar branch),
+// the lane's own row entry A[r][j] by a DPP quad broadcast, and only the column entries of
+// the other rows (A[c][j]) and the finished inverse row go through LDS.
 // Returns the first failing local pivot index or -1 (uniform over the wave).
 __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
                                               double* erow, double* piv) {
@@ -297,13 +324,13 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   int bad = -1;
 #pragma unroll
   for (int j = 0; j < CP; ++j) {
-    if (q == (j & 3)) colj[r] = a[j >> 2];            // pivot column (unnormalised)
+    const double p = readlane_f64(a[j >> 2], 4 * j + (j & 3));   // A[j][j] (unnormalised pivot)
+    const double arj = quad_bcast_f64(a[j >> 2], j & 3);          // A[r][j]
+    if (q == (j & 3)) colj[r] = a[j >> 2];                        // pivot column for the other rows
     if (r == j) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) erow[q + 4 * k] = e[k];   // inverse row j (final)
+      for (int k = 0; k < 4; ++k) erow[q + 4 * k] = e[k];         // inverse row j (final)
     }
-    lds_wave_sync();
-    const double p = colj[j];
     if (!(p > 0.0)) {
       bad = j;
       break;
@@ -312,7 +339,8 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     double ip = __builtin_amdgcn_rcp(p);            // + 2 Newton steps (pivots are normal, > 0)
     ip = fma(ip, fma(-p, ip, 1.0), ip);
     ip = fma(ip, fma(-p, ip, 1.0), ip);
-    const double m = colj[r] * ip;
+    lds_wave_sync();
+    const double m = arj * ip;
     const bool below = r > j;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -325,6 +353,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     __builtin_amdgcn_wave_barrier();   // one wave: LDS ops complete in order; keep the compiler's order
   }
   if (bad >= 0) return bad;
+  lds_wave_sync();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int c = q + 4 * k;
@@ -932,6 +961,29 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
   return rc;
 }
 }  // namespace
+
+namespace evr {
+// Graph-capturable pieces for the MLL plan (mll_plan.hip): one psd_safe_cholesky attempt
+// with the jitter vector already on the device (no host sync, no allocation) followed by the
+// triangular inverse, and the GEMM without the split-K workspace allocation.
+int chol_inverse_attempt(hipStream_t s, int batch, int n, const double* A, double* L, double* Linv, double* Dinv,
+                         double* T, const double* jit_d, int* info_d) {
+  EVR_HIP(hipMemsetAsync(info_d, 0, sizeof(int) * batch, s));
+  dim3 g1(cdiv((long long)n * n, 256), batch);
+  chol_init_kernel<<<g1, 256, 0, s>>>(n, A, (long long)n * n, n, L, (long long)n * n, n, jit_d);
+  EVR_LAUNCH_CHECK();
+  if (int rc = chol_blocked(s, batch, n, L, n, (long long)n * n, Dinv, info_d)) return rc;
+  return tri_inv_blocked(s, batch, n, L, n, (long long)n * n, Dinv, Linv, n, (long long)n * n, T, info_d);
+}
+
+size_t chol_inverse_dinv_doubles(int batch, int n) { return (size_t)batch * cdiv(n, BNB) * BNB * BNB; }
+
+int gemm_plain(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alpha, const double* A, int lda,
+               long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
+               int batch) {
+  return launch_gemm(s, tA, tB, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, 0, nullptr, false);
+}
+}  // namespace evr
 
 using namespace evr;
 

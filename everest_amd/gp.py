@@ -12,14 +12,16 @@ so that posteriors for all outputs are one batched launch.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-from . import ops
+from . import _native, ops
 
 MIN_INFERRED_NOISE_LEVEL = 1e-4
 
@@ -262,12 +264,12 @@ class MLLBatch:
         self.Y = torch.as_tensor(np.asarray(Ys, dtype=np.float64), device=Xn.device)   # B x n (standardized)
         self.ls_prior = _prior(ls_prior)
         self.noise_prior = _prior(noise_prior)
+        self.use_plan = os.environ.get("EVR_MLL_PLAN", "1") != "0"
+        self._plan = None
 
-    def __call__(self, idx: Sequence[int], xs: Sequence[np.ndarray]):
-        n, d, dev = self.n, self.d, self.Xn.device
-        xs = np.stack([np.asarray(x, dtype=np.float64) for x in xs])
-        noise, const, raw = xs[:, 0], xs[:, 1], xs[:, 2:]
-        ls = softplus_np(raw)
+    def _eval_ops(self, idx, ls, noise, const):
+        """The op-by-op chain with the psd_safe_cholesky jitter ladder (host arrays)."""
+        dev = self.Xn.device
         ls_t = torch.as_tensor(ls, device=dev)
         Ky = ops.kernel_matrix(self.Xn, self.Xn, ls_t, self.kind, diag_add=torch.as_tensor(noise, device=dev))
         L, Linv, _, info = ops.cholesky_inverse(Ky, 1e-8, 3, raise_on_fail=False)
@@ -279,7 +281,54 @@ class MLLBatch:
         ops.gemm(Linv, Linv, transA=True, alpha=-1.0, beta=1.0, out=W)
         gls = ops.kernel_lengthscale_grad(self.Xn, ls_t, W, self.kind)
         terms = ops.mll_terms(L, Linv, r[..., 0].contiguous(), alpha[..., 0].contiguous())
-        host = torch.cat([terms.reshape(-1), gls.reshape(-1), info.to(torch.float64)]).cpu().numpy()
+        return torch.cat([terms.reshape(-1), gls.reshape(-1), info.to(torch.float64)]).cpu().numpy()
+
+    def _eval_plan(self, idx, ls, noise, const):
+        """All members through the native MLL plan (evr_mll_plan_eval: one graph launch);
+        members outside idx keep their last parameters.  None when an active member's
+        attempt-0 factor fails (the caller takes the ladder path)."""
+        Bt, d = self.Y.shape[0], self.d
+        if self._plan is None:
+            h = ctypes.c_void_p()
+            ops.call("evr_mll_plan_create", ops._stream(), int(self.kind), Bt, self.n, d, self.Xn.data_ptr(),
+                     self.Y.data_ptr(), ctypes.byref(h))
+            self._plan = h
+            self._lib = _native.load()
+            self._params = np.empty((Bt, d + 2))
+            self._params[:, :d] = ls[0]
+            self._params[:, d] = noise[0]
+            self._params[:, d + 1] = const[0]
+            self._pout = np.empty(Bt * (5 + d + 1))
+        P = self._params
+        for k, b in enumerate(idx):
+            P[b, :d], P[b, d], P[b, d + 1] = ls[k], noise[k], const[k]
+        flat = np.concatenate([P[:, :d].reshape(-1), P[:, d], P[:, d + 1]])
+        _native.check(self._lib.evr_mll_plan_eval(ops._stream(), self._plan, flat.ctypes.data, self._pout.ctypes.data),
+                      "evr_mll_plan_eval")
+        o = self._pout
+        terms, gls, info = o[:5 * Bt].reshape(Bt, 5), o[5 * Bt:5 * Bt + Bt * d].reshape(Bt, d), o[5 * Bt + Bt * d:]
+        ii = np.asarray(idx, dtype=np.int64)
+        if np.any(info[ii] != 0):
+            return None
+        return np.concatenate([terms[ii].reshape(-1), gls[ii].reshape(-1), info[ii]])
+
+    def __del__(self):
+        h = getattr(self, "_plan", None)
+        if h is not None and getattr(self, "_lib", None) is not None:
+            try:
+                self._lib.evr_mll_plan_destroy(h)
+            except Exception:
+                pass
+            self._plan = None
+
+    def __call__(self, idx: Sequence[int], xs: Sequence[np.ndarray]):
+        n, d = self.n, self.d
+        xs = np.stack([np.asarray(x, dtype=np.float64) for x in xs])
+        noise, const, raw = xs[:, 0], xs[:, 1], xs[:, 2:]
+        ls = softplus_np(raw)
+        host = self._eval_plan(idx, ls, noise, const) if self.use_plan else None
+        if host is None:
+            host = self._eval_ops(idx, ls, noise, const)
         B = len(idx)
         terms_h = host[:5 * B].reshape(B, 5)
         gls_h = host[5 * B:5 * B + B * d].reshape(B, d)

@@ -67,6 +67,22 @@ int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, con
 int evr_gp_mll_terms(void* stream, int B, int n, const double* L, const double* Linv,
                      const double* r, const double* alpha, double* out);
 
+/* Native MLL plan for the GP fit: B exact GPs sharing the normalised inputs Xn (n x d,
+ * device, must outlive the plan) with standardised targets Y (B x n, device, copied).  One
+ * evr_mll_plan_eval is one hipGraph launch computing, per member b, with params (host) =
+ * [lengthscales (B x d) | noise (B) | constant (B)]:
+ *   out (host) = [terms (B x 5) as evr_gp_mll_terms | gls (B x d) as
+ *                 evr_kernel_lengthscale_grad with W = alpha alpha^T - K^-1 | info (B)]
+ * for K = k(Xn, Xn; ls_b) + noise_b I (psd_safe_cholesky attempt 0: a member with
+ * info != 0 needs the jitter ladder, i.e. the unfused path).  Replaces the per-evaluation
+ * op chain of the ExactMarginalLogLikelihood closure inside [upstream] fit_gpytorch_mll
+ * (bofire/surrogates/single_task_gp.py:70-71). */
+typedef struct evr_mll_plan evr_mll_plan;
+int evr_mll_plan_create(void* stream, int kind, int B, int n, int d, const double* Xn, const double* Y,
+                        evr_mll_plan** out);
+int evr_mll_plan_eval(void* stream, evr_mll_plan* plan, const double* params, double* out);
+void evr_mll_plan_destroy(evr_mll_plan* plan);
+
 /* ---- dense float64 linear algebra --------------------------------------------------- */
 int evr_gemm_f64(void* stream, int transA, int transB, int M, int N, int K, double alpha,
                  const double* A, int lda, long long strideA, const double* B, int ldb,

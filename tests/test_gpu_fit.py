@@ -61,3 +61,37 @@ def test_strategy_tell_uses_batched_fit(monkeypatch):
         hyps[mode] = [sur.state["lengthscale"] for sur in s.surrogates.surrogates]
     for a, b in zip(hyps["1"], hyps["0"]):
         assert np.allclose(a, b, rtol=2e-2)
+
+
+@pytest.mark.parametrize("kind", [0, 3])
+def test_mll_plan_matches_op_chain(kind, monkeypatch):
+    """evr_mll_plan (one graph launch per MLL evaluation of all outputs) against the op-by-op
+    chain with the jitter ladder, for subsets of the outputs, and the ladder fallback when an
+    active member's plain factorisation fails (duplicated inputs, zero noise)."""
+    from everest_amd.gp import MLLBatch
+
+    rng = np.random.default_rng(5)
+    n, d, m = 150, 4, 3
+    X = rng.uniform(size=(n, d))
+    X[100:110] = X[:10]                                   # duplicates: singular without noise
+    Y = dtlz2(X, m)
+    Ys = (Y - Y.mean(0)) / Y.std(0)
+    Xn = torch.tensor(X, device="cuda")
+    prior = (math.sqrt(2) + 0.5 * math.log(d), math.sqrt(3))
+    ev = MLLBatch(Xn, Ys.T.copy(), kind, prior, (-4.0, 1.0))
+    ref = MLLBatch(Xn, Ys.T.copy(), kind, prior, (-4.0, 1.0))
+    ref.use_plan = False
+    xs = [np.r_[1e-2 * (j + 1), 0.1 * j, rng.normal(size=d)] for j in range(m)]
+    for idx in ([0, 1, 2], [1], [2, 0]):
+        got = ev(idx, [xs[j] for j in idx])
+        want = ref(idx, [xs[j] for j in idx])
+        for (v1, g1), (v2, g2) in zip(got, want):
+            assert abs(v1 - v2) <= 1e-10 * max(1.0, abs(v2))
+            assert np.allclose(g1, g2, rtol=1e-8, atol=1e-10)
+    bad = [np.r_[1e-13, 0.0, rng.normal(size=d)] for _ in range(m)]
+    got = ev([1], [bad[1]])
+    want = ref([1], [bad[1]])
+    assert (got[0] is None) == (want[0] is None)
+    if got[0] is not None:
+        a, b = got[0][0], want[0][0]
+        assert (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-6 * max(1.0, abs(b))
