@@ -125,6 +125,14 @@ _SIGS = {
     "evr_qnehvi_plan_create": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_int, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, POINTER(c_void_p)], c_int),
     "evr_qnehvi_plan_run": ([c_void_p, c_void_p], c_int),
+    "evr_qnehvi_small_applies": ([POINTER(EvrQnehviState), c_int, c_int], c_int),
+    "evr_qnehvi_small_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int, c_int], ctypes.c_longlong),
+    "evr_qnehvi_small_forward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
+                                  c_void_p, c_void_p], c_int),
+    "evr_qnehvi_small_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p], c_int),
+    "evr_qnehvi_small_backward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "evr_mll_plan_create": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_mll_plan_eval": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "evr_mll_plan_destroy": ([c_void_p], None),

@@ -357,3 +357,41 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
 }
 
 }  // namespace evr
+
+using namespace evr;
+
+namespace evr {
+int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* norms, double* G,
+                  double* L22, int* flags, int tile_rows);
+}
+
+extern "C" {
+
+int evr_qnehvi_small_applies(const evr_qnehvi_state* st, int b, int d) { return st && qs_applies(st, b, d) ? 1 : 0; }
+
+long long evr_qnehvi_small_workspace_doubles(const evr_qnehvi_state* st, int b, int d, int which) {
+  if (!st || !qs_applies(st, b, d)) return 0;
+  return which == 0 ? (long long)qs_norms_doubles(st, b) : (long long)qs_dxp_doubles(st, b, d);
+}
+
+int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                             const double* Kx, double* R, double* P) {
+  EVR_CHECK(st && md && Kx && R && P && qs_applies(st, b, md->d), "evr_qnehvi_small_forward: bad arguments");
+  return qs_forward((hipStream_t)stream, st, md, b, Kx, R, P);
+}
+
+int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,
+                             double* G, double* L22, int* flags) {
+  EVR_CHECK(st && R && P && G && L22 && flags && b >= 1 && b <= QS_B, "evr_qnehvi_small_samples: bad arguments");
+  return samples_norms((hipStream_t)stream, st, b, R, P, G, L22, flags, QS_FR);
+}
+
+int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                              const double* X, const double* R, const double* L22, const double* dG, double* dXp,
+                              double* dX) {
+  EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
+            "evr_qnehvi_small_backward: bad arguments");
+  return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX);
+}
+
+}  // extern "C"

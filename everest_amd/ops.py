@@ -9,6 +9,7 @@ custom operators (``torch.ops.everest_amd.*``, everest_amd/csrc/torch_ops.cpp, e
 from __future__ import annotations
 
 import ctypes
+import os
 import warnings
 from typing import Optional, Tuple
 
@@ -329,6 +330,49 @@ def qnehvi_project_backward(st: EvrQnehviState, M: torch.Tensor, R: torch.Tensor
     call("evr_qnehvi_project_backward", _stream(), ctypes.byref(st), b, M.data_ptr(), R.data_ptr(), L22.data_ptr(),
          dG.data_ptr(), dK.data_ptr(), work.data_ptr())
     return dK
+
+
+def qnehvi_small_applies(st: EvrQnehviState, b: int, d: int) -> bool:
+    """Whether the native plan runs the b <= 32 restart-batch kernels (qnehvi_small.hip) for
+    this batch (EVR_SMALL=0 disables them, as in the plan)."""
+    return (os.environ.get("EVR_SMALL", "1") != "0"
+            and bool(_native.load().evr_qnehvi_small_applies(ctypes.byref(st), int(b), int(d))))
+
+
+def qnehvi_small_forward(st: EvrQnehviState, model, Kx: torch.Tensor, b: int):
+    """Restart-batch projection: R = M Kx and 16-row-tile partial norms (qs_fwd)."""
+    dev = Kx.device
+    lib = _native.load()
+    Rr = st.n + st.nb + (0 if st.no_h else st.S) + 1
+    R = torch.empty(st.m, Rr, b, dtype=torch.float64, device=dev)
+    P = _workspace(lib.evr_qnehvi_small_workspace_doubles(ctypes.byref(st), b, model.d, 0), dev)
+    call("evr_qnehvi_small_forward", _stream(), ctypes.byref(st), ctypes.byref(model), b,
+         _dev(Kx, "Kx").data_ptr(), R.data_ptr(), P.data_ptr())
+    return R, P
+
+
+def qnehvi_small_samples(st: EvrQnehviState, R: torch.Tensor, P: torch.Tensor, b: int):
+    dev = R.device
+    G = torch.empty(st.S, st.m, b, dtype=torch.float64, device=dev)
+    L22 = torch.empty(st.m, b, dtype=torch.float64, device=dev)
+    flags = torch.empty(st.m, b, dtype=torch.int32, device=dev)
+    call("evr_qnehvi_small_samples", _stream(), ctypes.byref(st), b, R.data_ptr(), P.data_ptr(), G.data_ptr(),
+         L22.data_ptr(), flags.data_ptr())
+    return G, L22, flags
+
+
+def qnehvi_small_backward(st: EvrQnehviState, model, X: torch.Tensor, R: torch.Tensor, L22: torch.Tensor,
+                          dG: torch.Tensor, b: int) -> torch.Tensor:
+    """Restart-batch backward: dX (b x d) = d sum acq / dX with the cross-covariance gradient
+    fused into the M^T gR product (qs_bwd + qs_dx_reduce)."""
+    dev = R.device
+    lib = _native.load()
+    dXp = _workspace(lib.evr_qnehvi_small_workspace_doubles(ctypes.byref(st), b, model.d, 1), dev)
+    dX = torch.empty(b, model.d, dtype=torch.float64, device=dev)
+    call("evr_qnehvi_small_backward", _stream(), ctypes.byref(st), ctypes.byref(model), b,
+         _dev(X, "X").contiguous().data_ptr(), R.data_ptr(), L22.data_ptr(), dG.data_ptr(), dXp.data_ptr(),
+         dX.data_ptr())
+    return dX
 
 
 OBJ_AFFINE, OBJ_CLOSE_TO_TARGET = 0, 1

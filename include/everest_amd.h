@@ -254,6 +254,19 @@ long long evr_qnehvi_plan_workspace_bytes(const evr_qnehvi_state* st, const evr_
 int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
                            int backward, const double* X, void* work, double* acq, double* dX, int use_graph,
                            evr_qnehvi_plan** out);
+/* The b <= 32 (restart-batch) pieces of the plan chain, exposed op by op for measurement and
+ * parity tests (qnehvi_small.hip): small_forward R, P (16-row norm tiles) from Kx; small_samples
+ * G, L22, flags from them; small_backward dX (b x d, the cross-covariance gradient fused) from
+ * R, L22, dG and the candidates X.  workspace_doubles(which = 0: P, 1: dXp). */
+int evr_qnehvi_small_applies(const evr_qnehvi_state* st, int b, int d);
+long long evr_qnehvi_small_workspace_doubles(const evr_qnehvi_state* st, int b, int d, int which);
+int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                             const double* Kx, double* R, double* P);
+int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,
+                             double* G, double* L22, int* flags);
+int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                              const double* X, const double* R, const double* L22, const double* dG, double* dXp,
+                              double* dX);
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* plan);
 /* One evaluation at host x (b x d): out (host) = [acq (b) | dX (b x d, backward plans)].
  * Runs a second graph [copy-in from fine-grained pinned memory, the chain, copy-out + a
