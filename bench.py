@@ -365,7 +365,7 @@ def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=
     for _ in range(2):      # cold (first GPU work of the process: module loads, plan captures), then warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        s.tell(exps)
+        s.tell(exps, replace=True)      # the same n training points both times
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     return s, times

@@ -97,3 +97,27 @@ def test_small_batch_kernels_match_tile_path(split, monkeypatch):
         assert torch.allclose(g1, g0, rtol=1e-8, atol=1e-11 * g0.abs().max()), (g1 - g0).abs().max()
         a2, g2 = q.forward_backward(Xc)                 # repeat: bitwise
         assert torch.equal(a2, a1) and torch.equal(g2, g1)
+
+
+def test_small_batch_ops_equal_plan():
+    """The b <= 32 pieces exposed through the C-ABI (evr_qnehvi_small_forward / _samples /
+    _backward, what bench.py times per op) chained by hand give the plan's values bitwise."""
+    from everest_amd import ops
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 120, 5, 3, 64
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=23)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=2, prune_seed=3,
+               prune_samples=256)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(4).uniform(size=(13, d)), device="cuda")
+    b = Xc.shape[0]
+    st, md = q.state, q.model
+    assert ops.qnehvi_small_applies(st, b, d)
+    Kx = gp.cross(Xc)
+    R, P = ops.qnehvi_small_forward(st, md, Kx, b)
+    G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
+    acq, dG = ops.hvi_forward_backward(st, G, b, flags)
+    dX = ops.qnehvi_small_backward(st, md, Xc, R, L22, dG, b)
+    a_ref, g_ref = q.forward_backward(Xc)
+    assert torch.equal(acq, a_ref) and torch.equal(dX, g_ref)
