@@ -369,8 +369,11 @@ class Inputs(_Features):
 
     def transform(self, experiments: pd.DataFrame, specs: Dict[str, str]) -> pd.DataFrame:
         """bofire/data_models/domain/features.py:493-533 (ONE_HOT only)."""
+        feats = self.get().features
+        if all(isinstance(f, ContinuousInput) for f in feats):
+            return experiments[[f.key for f in feats]].astype("float64")
         parts = []
-        for feat in self.get().features:
+        for feat in feats:
             s = experiments[feat.key]
             if isinstance(feat, CategoricalInput):
                 if specs.get(feat.key) != "ONE_HOT":
@@ -422,11 +425,33 @@ class Inputs(_Features):
         return experiments
 
     def validate_candidates(self, candidates: pd.DataFrame) -> pd.DataFrame:
-        for feat in self.get().features:
+        """Per-feature checks of ContinuousInput / CategoricalInput.validate_candidental, the
+        continuous columns' bounds tested in one array pass (same errors, same order)."""
+        feats = self.get().features
+        for feat in feats:
             if feat.key not in candidates:
                 raise ValueError(f"no col for input feature `{feat.key}`")
-            candidates[feat.key] = feat.validate_candidental(candidates[feat.key])
-        return candidates[self.get_keys()]
+        dtypes = candidates.dtypes
+        cont = [f for f in feats if isinstance(f, ContinuousInput)]
+        if cont:
+            for f in cont:
+                if not pd.api.types.is_numeric_dtype(dtypes[f.key]):
+                    raise ValueError(f"not all values of input feature `{f.key}` are numerical")
+            vals = candidates[[f.key for f in cont]].to_numpy(dtype=np.float64)
+            lo = np.array([f.lower_bound for f in cont]) - 1e-6
+            hi = np.array([f.upper_bound for f in cont]) + 1e-6
+            bad = ((vals < lo) | (vals > hi)).any(axis=0)
+            for f, b in zip(cont, bad):
+                if b:
+                    raise ValueError(f"not all values of input feature `{f.key}` are inside the bounds "
+                                     f"[{f.lower_bound}, {f.upper_bound}]")
+        for feat in feats:
+            if isinstance(feat, ContinuousInput):
+                if dtypes[feat.key] != np.float64:
+                    candidates[feat.key] = candidates[feat.key].astype("float64")
+            else:
+                candidates[feat.key] = feat.validate_candidental(candidates[feat.key])
+        return candidates[[f.key for f in feats]]
 
 
 class Outputs(_Features):
@@ -466,12 +491,15 @@ class Outputs(_Features):
                                                  output_feature_keys: Optional[List[str]] = None) -> pd.DataFrame:
         """bofire/data_models/domain/features.py:951-974."""
         keys = output_feature_keys or self.get_keys()
-        clean = experiments
+        # one row mask (valid_<key> > 0 for every key that has the column, no NaN in the
+        # output columns) and one selection instead of a filtered copy per key
+        keep = np.ones(len(experiments), dtype=bool)
         for k in keys:
             vk = f"valid_{k}"
-            if vk in clean:
-                clean = clean[clean[vk] > 0]
-        return clean.dropna(subset=keys)
+            if vk in experiments:
+                keep &= np.asarray(experiments[vk] > 0, dtype=bool)
+        keep &= ~experiments[list(keys)].isna().to_numpy().any(axis=1)
+        return experiments if keep.all() else experiments[keep]
 
     def validate_experiments(self, experiments: pd.DataFrame) -> pd.DataFrame:
         for feat in self.features:
@@ -584,7 +612,7 @@ class Domain(BaseModel):
                             raise_validation_error: bool = True) -> pd.DataFrame:
         """bofire/data_models/domain/domain.py:417-459."""
         cand = self.inputs.validate_candidates(candidates.copy())
-        if not self.constraints.is_fulfilled(cand, tol=tol).all():
+        if len(self.constraints) and not self.constraints.is_fulfilled(cand, tol=tol).all():
             if raise_validation_error:
                 raise ConstraintNotFulfilledError(f"Constraints not fulfilled: {cand}")
             warnings.warn("Not all constraints are fulfilled.")

@@ -293,18 +293,34 @@ class BotorchStrategy(PredictiveStrategy):
         mean, var = self.model.posterior(X, observation_noise=True)
         return mean.T.cpu().numpy(), np.sqrt(var.T.cpu().numpy())
 
+    def _valid_experiments(self) -> pd.DataFrame:
+        """preprocess_experiments_all_valid_outputs of the current experiments, computed once
+        per experiments frame (tell / set / add replace the frame object)."""
+        c = getattr(self, "_valid_cache", None)
+        if c is not None and c[0] is self._experiments:
+            return c[1]
+        v = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        self._valid_cache = (self._experiments, v)
+        self._xtrain_cache = None
+        return v
+
     def has_sufficient_experiments(self) -> bool:
         if self.experiments is None:
             return False
-        return len(self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)) > 1
+        return len(self._valid_experiments()) > 1
 
     def get_acqf_input_tensors(self):
         """bofire/strategies/predictives/botorch.py:696-724."""
-        ex = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
-        clean = ex.drop_duplicates(subset=self.domain.inputs.get_keys(), keep="first")
-        X_train = self._transform(clean)
+        ex = self._valid_experiments()
+        c = getattr(self, "_xtrain_cache", None)
+        if c is not None and c[0] is ex:
+            X_train = c[1]
+        else:
+            clean = ex.drop_duplicates(subset=self.domain.inputs.get_keys(), keep="first")
+            X_train = self._transform(clean)
+            self._xtrain_cache = (ex, X_train)
         X_pending = self._transform(self.candidates) if self.candidates is not None else None
-        return X_train, X_pending
+        return X_train.copy(), X_pending
 
     def calc_acquisition(self, candidates: pd.DataFrame, combined: bool = False) -> np.ndarray:
         """bofire/strategies/predictives/botorch.py:196-225: one value per candidate, or with
@@ -406,7 +422,7 @@ class _MultiobjectiveMixin:
     def get_adjusted_refpoint(self) -> List[float]:
         assert self.experiments is not None, "No experiments available."
         if self.ref_point is None:
-            df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+            df = self._valid_experiments()
             ref_point = infer_ref_point(self.domain, experiments=df, return_masked=False)
         else:
             ref_point = self.ref_point
@@ -459,7 +475,7 @@ class _MultiobjectiveMixin:
 
     def _observed_outputs(self) -> np.ndarray:
         """Valid observations of every model output (n x m, model output order)."""
-        df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        df = self._valid_experiments()
         return df[self.model.output_keys].values.astype(np.float64)
 
     def _draw_seed(self) -> int:
@@ -484,7 +500,7 @@ class QehviStrategy(_MultiobjectiveMixin, BotorchStrategy):
         objectives, constraints = self._objective_spec()
         keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
                                                           CloseToTargetObjective])
-        df = self.domain.outputs.preprocess_experiments_all_valid_outputs(self.experiments)
+        df = self._valid_experiments()
         train_obj = df[keys].values.astype(np.float64) * self.ref_point_mask
         ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
         better = (train_obj > ref).all(axis=-1)
