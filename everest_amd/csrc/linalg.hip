@@ -7,6 +7,8 @@
 // Replaces the [upstream] torch/LAPACK calls behind GPyTorch's Cholesky / solves
 // (Appendix A.4).
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -806,6 +808,35 @@ __global__ void place_diag_blocks_kernel(int n, const double* __restrict__ Dinv,
 namespace {
 using namespace evr;
 
+// Per-stream scratch of the jitter ladder (diagonal-block inverses, the inverse's row
+// products, jitter and info vectors), grown on demand and reused: the ladder synchronises
+// its stream before returning, so the next call on that stream may overwrite it.  A
+// hipMallocAsync / hipFreeAsync pair per call cost up to ~1.4 ms at 5 x 512 once the pool
+// had released its memory.
+struct LadderScratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+static int stream_scratch(int slot, hipStream_t s, size_t bytes, void** out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, LadderScratch> pool;   // one entry per (use, stream), never freed
+  std::lock_guard<std::mutex> lock(mu);
+  LadderScratch& e = pool[{slot, s}];
+  if (e.bytes < bytes) {
+    if (e.p) EVR_HIP(hipFree(e.p));
+    e.p = nullptr;
+    e.bytes = 0;
+    EVR_HIP(hipMalloc(&e.p, bytes));
+    e.bytes = bytes;
+  }
+  *out = e.p;
+  return 0;
+}
+
+static int ladder_scratch(hipStream_t s, size_t bytes, void** out) { return stream_scratch(0, s, bytes, out); }
+static int gemm_scratch(hipStream_t s, size_t bytes, void** out) { return stream_scratch(1, s, bytes, out); }
+
 int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alpha, const double* A, int lda,
                 long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
                 int batch, int lower_only = 0, const int* skip = nullptr, bool allow_split = false) {
@@ -821,7 +852,20 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
   const int kchunk = ksplit > 1 ? cdiv(cdiv(K, ksplit), GK) * GK : std::max(K, 1);
   if (ksplit > 1) ksplit = cdiv(K, kchunk);
   double* W = nullptr;
-  if (ksplit > 1) EVR_HIP(hipMallocAsync((void**)&W, sizeof(double) * (size_t)ksplit * batch * M * N, s));
+  bool pooled = false;
+  if (ksplit > 1) {
+    // split-K partials: the stream's reusable scratch (stream order protects it), or a
+    // stream-ordered allocation while the stream is being captured into a graph
+    const size_t wbytes = sizeof(double) * (size_t)ksplit * batch * M * N;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    EVR_HIP(hipStreamIsCapturing(s, &cap));
+    if (cap == hipStreamCaptureStatusNone) {
+      if (int rc = gemm_scratch(s, wbytes, (void**)&W)) return rc;
+      pooled = true;
+    } else {
+      EVR_HIP(hipMallocAsync((void**)&W, wbytes, s));
+    }
+  }
   dim3 grid(cdiv(N, GT), cdiv(M, GT), batch * ksplit);
 #define G_(TA_, TB_)                                                                                       \
   gemm_f64_kernel<TA_, TB_><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \
@@ -836,7 +880,7 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
     dim3 g2(cdiv((long long)M * N, 256), batch);
     gemm_splitk_reduce<<<g2, 256, 0, s>>>(M, N, batch, ksplit, alpha, W, beta, C, ldc, sC);
     EVR_LAUNCH_CHECK();
-    EVR_HIP(hipFreeAsync(W, s));
+    if (!pooled) EVR_HIP(hipFreeAsync(W, s));
   }
   return 0;
 }
@@ -924,10 +968,16 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
   const size_t tbytes = Linv ? sizeof(double) * (size_t)batch * BNB * n : 0;
   double *Dinv = nullptr, *T = nullptr, *jit_d = nullptr;
   int* info_d = nullptr;
-  EVR_HIP(hipMallocAsync((void**)&Dinv, dbytes, s));
-  if (tbytes) EVR_HIP(hipMallocAsync((void**)&T, tbytes, s));
-  EVR_HIP(hipMallocAsync((void**)&jit_d, sizeof(double) * batch, s));
-  EVR_HIP(hipMallocAsync((void**)&info_d, sizeof(int) * batch, s));
+  {
+    const size_t a = (dbytes + 255) & ~(size_t)255, t = (tbytes + 255) & ~(size_t)255;
+    const size_t j = (sizeof(double) * batch + 255) & ~(size_t)255;
+    unsigned char* base = nullptr;
+    if (int rc = ladder_scratch(s, a + t + j + sizeof(int) * batch, (void**)&base)) return rc;
+    Dinv = (double*)base;
+    T = tbytes ? (double*)(base + a) : nullptr;
+    jit_d = (double*)(base + a + t);
+    info_d = (int*)(base + a + t + j);
+  }
   std::vector<double> jit(batch, 0.0);
   std::vector<int> info(batch, 0);
   int rc = 0;
@@ -953,11 +1003,7 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
     if (jitter_used) EVR_HIP(hipMemcpyAsync(jitter_used, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
     if (info_out) EVR_HIP(hipMemcpyAsync(info_out, info_d, sizeof(int) * batch, hipMemcpyDeviceToDevice, s));
   }
-  EVR_HIP(hipStreamSynchronize(s));  // host vectors above must outlive the async copies
-  (void)hipFreeAsync(Dinv, s);
-  if (T) (void)hipFreeAsync(T, s);
-  (void)hipFreeAsync(jit_d, s);
-  (void)hipFreeAsync(info_d, s);
+  EVR_HIP(hipStreamSynchronize(s));  // host vectors and the stream's scratch must outlive the work
   return rc;
 }
 }  // namespace

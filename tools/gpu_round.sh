@@ -24,9 +24,9 @@ step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --outpu
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
      --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 &&
 step pmc_fetch20 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch20" -o run --output-format csv \
-     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|qs_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
 step pmc_write20 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write20" -o run --output-format csv \
-     --kernel-include-regex "hvi_|kmat_kernel|qn_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
+     --kernel-include-regex "hvi_|kmat_kernel|qn_|qs_|kcross_grad|Cijk" -- python tools/loop_step.py 10 20 &&
 python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" &&
 python tools/pmc_traffic.py "$OUT/pmc_fetch20" "$OUT/pmc_write20" "$OUT/hbm_traffic.json" "@b20" &&
 step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
