@@ -835,9 +835,9 @@ template <int M, bool BWD>
 __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
-                                               double* __restrict__ dG, int W) {
+                                               double* __restrict__ dG, int W, int balance) {
   constexpr int NV = BWD ? M + 1 : 1;
-  constexpr int CW = KD_CT / 4;            // candidates per wave
+  constexpr int CW = KD_CT / 4;            // candidate slots per wave
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kd_dyn[];
   __shared__ double yv[KD_CT][M];
@@ -861,6 +861,13 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   // the L-BFGS restarts), so a tile holds 64 / W candidates
   const int c0 = tile * (KD_CT / W), tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  // slot -> candidate: the tile's 4 / W groups of 16 slots each take gsz = ceil(candidates of
+  // the tile / groups) candidates, so a split tile (small batches) is balanced across its
+  // wave groups (at b = 20: 10 + 10 instead of 16 + 4); full tiles map slot = candidate
+  const int ngr = 4 / W;
+  const int gsz = (W > 1 && balance) ? min(CW, (min(KD_CT / W, b - c0) + ngr - 1) / ngr) : CW;
+  auto cand = [&](int c) { return c0 + (c >> 4) * gsz + (c & 15); };
+  auto valid = [&](int c) { return (c & 15) < gsz && cand(c) < b; };
   const int stride = kd.stride;
   KD_T0();
   const int split = blockIdx.z;
@@ -895,10 +902,10 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   }
   for (int e = tid; e < KD_CT * M; e += 256) {
     const int j = e / KD_CT, c = e - j * KD_CT;
-    yv[c][j] = (c0 + c < b) ? G[((size_t)s * M + j) * b + c0 + c] : -INFINITY;
+    yv[c][j] = valid(c) ? G[((size_t)s * M + j) * b + cand(c)] : -INFINITY;
   }
   if (tid < KD_CT) {
-    const bool in = c0 + tid < b;
+    const bool in = valid(tid);
     unsigned int w[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -906,7 +913,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int j = 2 * q + h;
-        const unsigned int t = (j < M) ? (in ? (unsigned int)thg[((size_t)s * M + j) * b + c0 + tid] : 0u) : 1u;
+        const unsigned int t = (j < M) ? (in ? (unsigned int)thg[((size_t)s * M + j) * b + cand(tid)] : 0u) : 1u;
         v |= t << (16 * h);
       }
       w[q] = v;
@@ -919,7 +926,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   const int wsub = wave % W;
   const int cbase = (wave / W) * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
   const int aslot = wave * CW;         // ... and its accumulator rows
-  if (c0 + cbase >= b) return;
+  if (!valid(cbase)) return;
   {   // this wave's share of the workgroup's chunks
     const int qpw = (NQ + W - 1) / W;
     const int qa = min(NQ, wsub * qpw);
@@ -989,7 +996,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       pA[NE] = (unsigned short)PA;
       if (kd.counters) {
         atomicAdd(kd.counters + 0, (unsigned long long)PA);
-        atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - c0 - cbase, CW)) * Gs);
+        atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - cand(cbase), gsz)) * Gs);
       }
     }
   }
@@ -1122,14 +1129,15 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   wave_sync();
   const int nst = nsplit * W;   // partial splits: workgroup splits x wave splits
   const size_t ss = ((size_t)s * nsplit + split) * W + wsub;
-  if (lane < CW && c0 + cbase + lane < b) part[ss * b + c0 + cbase + lane] = acc[aslot + lane][0];
+  if (lane < CW && valid(cbase + lane)) part[ss * b + cand(cbase + lane)] = acc[aslot + lane][0];
   if (BWD) {
     for (int e = lane; e < CW * M; e += 64) {
       const int j = e / CW, cl = e - j * CW, c = cbase + cl;
-      if (c0 + c >= b) continue;
+      if (!valid(c)) continue;
+      const int gc = cand(c);
       const double v = acc[aslot + cl][NV > 1 ? 1 + j : 0];
-      if (nst == 1) dG[((size_t)s * M + j) * b + c0 + c] = (gout ? gout[c0 + c] : 1.0) / (double)S * v;
-      else dG[(ss * M + j) * b + c0 + c] = v;
+      if (nst == 1) dG[((size_t)s * M + j) * b + gc] = (gout ? gout[gc] : 1.0) / (double)S * v;
+      else dG[(ss * M + j) * b + gc] = v;
     }
   }
 }
@@ -1238,8 +1246,12 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
     const Kd2Lds L2 = kd2_lds(st->pts_stride, M, st->max_groups);
     EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd2<M, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)L2.bytes));
+    static const int balance = [] {   // EVR_KD_BALANCE=0: 16-slot groups filled in order (A/B)
+      const char* e = std::getenv("EVR_KD_BALANCE");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
     hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, nsb, G, th, hvi_kd_of(st), gout, part,
-                                                  ns > 1 ? dgp : dG, W);
+                                                  ns > 1 ? dgp : dG, W, balance);
   }
   EVR_LAUNCH_CHECK();
   if (acq) {
