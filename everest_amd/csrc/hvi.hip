@@ -214,12 +214,13 @@ __global__ __launch_bounds__(HV_THREADS) void hvi_tiled(int b, int nchunk, int C
 // the b <= 32 restart batches, whose wave-split scans leave S x 8 partials per candidate).
 // A candidate whose new-point Cholesky block failed (flags[j][c] != 0 for some j) gets NaN.
 template <int CX>
-__global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, int m, const double* __restrict__ work,
-                                                      const int* __restrict__ flags, double* __restrict__ acq) {
+__device__ __forceinline__ void reduce_fwd_body(int blk, int S, int nchunk, int b, int m,
+                                                const double* __restrict__ work, const int* __restrict__ flags,
+                                                double* __restrict__ acq) {
   constexpr int G = 256 / CX;
   __shared__ double red[G][CX + 1];
   const int cx = threadIdx.x % CX, g = threadIdx.x / CX;
-  const int c = blockIdx.x * CX + cx;
+  const int c = blk * CX + cx;
   const int tot = S * nchunk;
   double sum = 0.0;
   if (c < b) {
@@ -240,6 +241,38 @@ __global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, 
   }
 }
 
+template <int CX>
+__global__ __launch_bounds__(256) void hvi_reduce_fwd(int S, int nchunk, int b, int m, const double* __restrict__ work,
+                                                      const int* __restrict__ flags, double* __restrict__ acq) {
+  reduce_fwd_body<CX>(blockIdx.x, S, nchunk, b, m, work, flags, acq);
+}
+
+// dG[s][j][c] = gout[c]/S * sum_chunk work[s][chunk][j][c] (elementwise; nchunk loads in flight)
+__device__ __forceinline__ void reduce_bwd_body(int blk, int S, int nchunk, int M, int b,
+                                                const double* __restrict__ work, const double* __restrict__ gout,
+                                                double* __restrict__ dG) {
+  const long long e = (long long)blk * 256 + threadIdx.x;
+  if (e >= (long long)S * M * b) return;
+  const int c = (int)(e % b);
+  const int j = (int)((e / b) % M);
+  const int s = (int)(e / ((long long)b * M));
+  double sum = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < nchunk; ++k) sum += work[(((size_t)s * nchunk + k) * M + j) * b + c];
+  dG[e] = (gout ? gout[c] : 1.0) / (double)S * sum;
+}
+
+// both reductions of a forward + backward scan in one launch: blocks [0, nf) reduce the
+// values (CX candidates each), the rest the sample gradients
+template <int CX>
+__global__ __launch_bounds__(256) void hvi_reduce_fb(int S, int nchunk, int b, int m, int nf,
+                                                     const double* __restrict__ work, const int* __restrict__ flags,
+                                                     double* __restrict__ acq, const double* __restrict__ dwork,
+                                                     const double* __restrict__ gout, double* __restrict__ dG) {
+  if ((int)blockIdx.x < nf) reduce_fwd_body<CX>(blockIdx.x, S, nchunk, b, m, work, flags, acq);
+  else reduce_bwd_body(blockIdx.x - nf, S, nchunk, m, b, dwork, gout, dG);
+}
+
 static void hvi_reduce_fwd_launch(hipStream_t s, int S, int nchunk, int b, int m, const double* work,
                                   const int* flags, double* acq) {
   if (b <= 32)
@@ -248,17 +281,9 @@ static void hvi_reduce_fwd_launch(hipStream_t s, int S, int nchunk, int b, int m
     hvi_reduce_fwd<16><<<cdiv(b, 16), 256, 0, s>>>(S, nchunk, b, m, work, flags, acq);
 }
 
-// dG[s][j][c] = gout[c]/S * sum_chunk work[s][chunk][j][c]
 __global__ void hvi_reduce_bwd(int S, int nchunk, int M, int b, const double* __restrict__ work,
                                const double* __restrict__ gout, double* __restrict__ dG) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long long)S * M * b) return;
-  const int c = (int)(e % b);
-  const int j = (int)((e / b) % M);
-  const int s = (int)(e / ((long long)b * M));
-  double sum = 0.0;
-  for (int k = 0; k < nchunk; ++k) sum += work[(((size_t)s * nchunk + k) * M + j) * b + c];
-  dG[e] = (gout ? gout[c] : 1.0) / (double)S * sum;
+  reduce_bwd_body(blockIdx.x, S, nchunk, M, b, work, gout, dG);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1254,6 +1279,19 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
                                                   ns > 1 ? dgp : dG, W, balance);
   }
   EVR_LAUNCH_CHECK();
+  if (acq && BWD && ns > 1) {   // one launch for both reductions
+    const long long tot = (long long)st->S * M * b;
+    const int nb = (int)cdiv(tot, 256);
+    if (b <= 32) {
+      const int nf = cdiv(b, 4);
+      hvi_reduce_fb<4><<<nf + nb, 256, 0, s>>>(st->S, ns, b, M, nf, part, flags, acq, dgp, gout, dG);
+    } else {
+      const int nf = cdiv(b, 16);
+      hvi_reduce_fb<16><<<nf + nb, 256, 0, s>>>(st->S, ns, b, M, nf, part, flags, acq, dgp, gout, dG);
+    }
+    EVR_LAUNCH_CHECK();
+    return 0;
+  }
   if (acq) {
     hvi_reduce_fwd_launch(s, st->S, ns, b, M, part, flags, acq);
     EVR_LAUNCH_CHECK();

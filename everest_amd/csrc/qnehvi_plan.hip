@@ -38,7 +38,8 @@ size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                const double* R, const double* L22, const double* dG, double* dXp, double* dX);
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
+                double* hout, const double* seqp, unsigned int* counter);
 constexpr int QS_TILE_ROWS = 16;
 
 // b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
@@ -116,14 +117,11 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
+  unsigned int* counter;         // blocks-done counter of the fused copy-out (device)
 };
 
 namespace evr {
 
-__global__ __launch_bounds__(256) void plan_copy_in(int n, const double* __restrict__ hx, double* __restrict__ X) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) X[i] = hx[i];
-}
 
 // acq and dX to the host buffer, then (after every thread's system-scope fence) the
 // evaluation's sequence number into the completion word the host spins on
@@ -144,7 +142,11 @@ __global__ __launch_bounds__(256) void plan_copy_out(int b, int n, const double*
 
 }  // namespace evr
 
-static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
+// The chain on candidates X (device buffer, or in the host graph the pinned host buffer
+// itself).  Host mode (hout): the b <= 32 backward's dX reduction also writes [acq | dX] and
+// the completion word to hout (*done = 1); otherwise the caller appends a copy-out kernel.
+static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, double* hout = nullptr,
+                      const double* seqp = nullptr, unsigned int* counter = nullptr, int* done = nullptr) {
   const evr_qnehvi_state* st = &p->st;
   const evr_qnehvi_model* md = &p->md;
   const int b = p->b, m = st->m, n = st->n, d = md->d;
@@ -157,7 +159,7 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
   const bool small = p->L.small;
-  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                  md->lengthscales, nullptr, nullptr, Kx))
     return rc;
   if (small) {
@@ -170,10 +172,13 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p) {
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
   double* dG = (double*)(w + p->L.dG);
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
-  if (small) return qs_backward(s, st, md, b, p->X, R, L22, dG, (double*)(w + p->L.dxp), p->dX);
+  if (small) {
+    if (done) *done = hout ? 1 : 0;
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter);
+  }
   double* dKx = (double*)(w + p->L.dKx);
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;
-  return kcross_grad_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, p->X, md->shift, md->scale,
+  return kcross_grad_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                             md->lengthscales, nullptr, dKx, p->dX, (double*)(w + p->L.kg));
 }
 
@@ -209,6 +214,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->hgraph = nullptr;
   p->hexec = nullptr;
   p->seq = 0;
+  p->counter = nullptr;
   if (int rc = gemm_backend_init()) {
     delete p;
     return rc;
@@ -223,7 +229,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
     }
     int rc = 0;
     if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = 1;
-    if (!rc) rc = plan_chain(cs, p);
+    if (!rc) rc = plan_chain(cs, p, p->X);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(cs, &g);
     if (!rc && e == hipSuccess && g) {
@@ -252,7 +258,7 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
     EVR_HIP(hipGraphLaunch(p->exec, s));
     return 0;
   }
-  return plan_chain(s, p);
+  return plan_chain(s, p, p->X);
 }
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
@@ -261,6 +267,7 @@ void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (p->hgraph) (void)hipGraphDestroy(p->hgraph);
   if (p->hx) (void)hipHostFree(p->hx);
   if (p->hout) (void)hipHostFree(p->hout);
+  if (p->counter) (void)hipFree(p->counter);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   delete p;
@@ -280,13 +287,19 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   double *dhx = nullptr, *dhout = nullptr;
   EVR_HIP(hipHostGetDevicePointer((void**)&dhx, p->hx, 0));
   EVR_HIP(hipHostGetDevicePointer((void**)&dhout, p->hout, 0));
+  if (!p->counter) {
+    EVR_HIP(hipMalloc((void**)&p->counter, sizeof(unsigned int)));
+    EVR_HIP(hipMemset(p->counter, 0, sizeof(unsigned int)));
+  }
   hipStream_t cs = nullptr;
   EVR_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
   if (!rc) {
-    plan_copy_in<<<cdiv(n, 256), 256, 0, cs>>>(n, dhx, (double*)p->X);
-    rc = plan_chain(cs, p);
-    if (!rc) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
+    // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
+    // writes the results and the completion word itself, other chains end in plan_copy_out
+    int done = 0;
+    rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
+    if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
   }
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);

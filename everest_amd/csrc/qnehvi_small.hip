@@ -161,6 +161,15 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
   const double aj = oa[j], sj = ys[j];
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Rj = R + (size_t)j * Rr * b;
+  // the epilogue's candidate coordinates (normalised) and inverse lengthscales, loaded first:
+  // X may be the plan's pinned host buffer (PCIe latency, hidden behind the main loop)
+  double xc[QS_MAXD];
+  {
+    const int c = tid & (QS_B - 1);
+#pragma unroll
+    for (int k = 0; k < QS_MAXD; ++k)
+      xc[k] = (c < b && k < d) ? (X[(size_t)c * d + k] - (shift ? shift[k] : 0.0)) * (scale ? scale[k] : 1.0) : 0.0;
+  }
   // chunk loads: M[r][i0 + col] (a wave covers 4 rows x 128 B), gR source (row, candidate)
   constexpr int ML = QS_RC * QS_BI / 256, BL = QS_RC * QS_B / 256;
   double mv[ML], bv[BL];
@@ -262,12 +271,9 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
 #pragma unroll
     for (int k = 0; k < QS_MAXD; ++k) acc[k] = 0.0;
     if (c < b) {
-      double xc[QS_MAXD], il[QS_MAXD];
+      double il[QS_MAXD];
 #pragma unroll
-      for (int k = 0; k < QS_MAXD; ++k) {
-        xc[k] = k < d ? (X[(size_t)c * d + k] - (shift ? shift[k] : 0.0)) * (scale ? scale[k] : 1.0) : 0.0;
-        il[k] = k < d ? 1.0 / ls[(size_t)j * d + k] : 0.0;
-      }
+      for (int k = 0; k < QS_MAXD; ++k) il[k] = k < d ? 1.0 / ls[(size_t)j * d + k] : 0.0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ii = g + 8 * h, irow = i0 + ii;
@@ -299,16 +305,37 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
   }
 }
 
-// one wave per dX element: lane-strided partial sums, then a fixed xor-butterfly
+// one wave per dX element: lane-strided partial sums, then a fixed xor-butterfly.  Host mode
+// (hout != nullptr, the plan's host graph): every block also writes its dX element (and the
+// first b blocks acq) to the pinned host buffer; after a system-scope fence each block counts
+// itself done, and the last one resets the counter and writes the evaluation's sequence
+// number into the completion word the host spins on (no separate copy-out kernel).
 __global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
-                                                   const double* __restrict__ scale, double* __restrict__ dX) {
+                                                   const double* __restrict__ scale, double* __restrict__ dX,
+                                                   const double* __restrict__ acq, double* hout,
+                                                   const double* seqp, unsigned int* counter) {
   const int e = blockIdx.x, lane = threadIdx.x;
   const int k = e % d;
   double v = 0.0;
   for (int p = lane; p < np; p += 64) v += dXp[(size_t)p * b * d + e];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) dX[e] = v * (scale ? scale[k] : 1.0);
+  if (lane == 0) {
+    const double r = v * (scale ? scale[k] : 1.0);
+    dX[e] = r;
+    if (hout) {
+      hout[b + e] = r;
+      if (e < b) hout[e] = acq[e];
+      __threadfence_system();
+      const unsigned int prev = atomicAdd(counter, 1u);
+      if (prev == gridDim.x - 1) {
+        atomicExch(counter, 0u);
+        const unsigned long long seq = *(volatile const unsigned long long*)seqp;
+        __threadfence_system();
+        *(volatile unsigned long long*)(hout + b + (size_t)b * d) = seq;
+      }
+    }
+  }
 }
 
 // ---- launchers (qnehvi_plan.hip) ------------------------------------------------------
@@ -344,14 +371,15 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
 }
 
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                const double* R, const double* L22, const double* dG, double* dXp, double* dX) {
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
+                double* hout, const double* seqp, unsigned int* counter) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
   qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
                                             md->lengthscales, dXp, nt, rows_per);
   EVR_LAUNCH_CHECK();
-  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX);
+  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -391,7 +419,7 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
                               double* dX) {
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
-  return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX);
+  return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr);
 }
 
 }  // extern "C"
