@@ -424,6 +424,15 @@ class QNEHVI(_BoxHviAcqf):
         import time as _time
         tm = {}
         t0 = _time.perf_counter()
+        _probe_on = os.environ.get("EVR_CONSTRUCTION_PROBES") == "1"   # diagnosis: synchronised split times
+        _last = [t0]
+
+        def probe(name):
+            if _probe_on:
+                torch.cuda.synchronize(dev)
+                t = _time.perf_counter()
+                tm["probe_" + name] = t - _last[0]
+                _last[0] = t
         fut_prune = (_prefetch_scramble(len(base_rows) * m, prune_seed)
                      if prune_baseline and z_prune is None else None)
         # ---- joint posterior at the training (+ pending) inputs, shared by prune and baseline
@@ -434,6 +443,7 @@ class QNEHVI(_BoxHviAcqf):
         A = ops.gemm(gp.Linv, K[:, :n].contiguous() if npend else K)      # L^-1 K  (m x n x nk)
         Sig = ops.gemm(A, A, transA=True, alpha=-1.0, beta=1.0, out=K)    # K - A^T A (in place)
         ops.scale_batched(Sig, (gp.ys ** 2).contiguous())                 # unstandardize
+        probe("joint_posterior")
 
         # ---- prune_inferior_points_multi_objective --------------------------------------
         probs = None
@@ -443,10 +453,12 @@ class QNEHVI(_BoxHviAcqf):
             mu_c = mu_train[:, cand].contiguous()
             nc = cand.shape[0]
             Lp, _, _ = ops.cholesky(Sig_c, 1e-8, 3)
+            probe("prune_chol")
             if z_prune is None:
                 Zp = sobol_base_samples(prune_samples, nc, m, prune_seed, dev, _result(fut_prune))  # m x nc x S'
             else:
                 Zp = z_prune.to(dev).permute(2, 1, 0).contiguous()
+            probe("prune_sobol")
             Yp = ops.gemm(Lp, Zp)
             Op = self._objective(Yp, mu_c)
             _, counts = ops.pareto_mask(Op, self.ref, dedup=False, want_mask=False, want_counts=True)
@@ -475,6 +487,7 @@ class QNEHVI(_BoxHviAcqf):
             Sig_b = Sig[:, idx][:, :, idx].contiguous()
             self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
+            probe("baseline_chol")
         # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed;
         # pending rows from the (nb_t+n_p)*m-dimensional draw ([upstream] _update_base_samples
         # keeps the earlier rows of the base sampler, the same seed draws the new ones)
@@ -491,6 +504,7 @@ class QNEHVI(_BoxHviAcqf):
                     Zb = torch.cat([Zb, Zp_], 1).contiguous()
             else:
                 Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
+            probe("baseline_sobol")
             Yb = ops.gemm(self.L_base, Zb)
             Ob = self._objective(Yb, mu_b)
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
@@ -500,6 +514,7 @@ class QNEHVI(_BoxHviAcqf):
         else:  # no baseline: one cell [ref, inf)
             cells = _single_cell(self.ref, S_, spec.m_obj)
             self.box_path = "none"
+        probe("box")
         self.cells = cells
         counts_c = cells.counts
         self.stats = ConstructionStats(n_train=n, n_base=nb, total_cells=int(np.sum(counts_c)),
@@ -545,7 +560,9 @@ class QNEHVI(_BoxHviAcqf):
                 V = ops.gemm(E, Lp)                                              # nb x nk
                 Iv = ops.gemm(V, V, transA=True)                                 # V^T V
                 Iv.diagonal(dim1=-2, dim2=-1)[:, :n] += 1.0                      # + D0
+                probe("root_gemms")
                 Lv, _, _ = ops.cholesky(Iv, 1e-8, 3)
+                probe("root_chol")
                 ops.gemm_into(M[:, :nk], Lv, Lpi, transA=True)                   # C = Lv^T Lp^-1
             else:
                 M[:, nk:nk + nb].copy_(E)
@@ -564,6 +581,7 @@ class QNEHVI(_BoxHviAcqf):
         self.model = _native.EvrQnehviModel(n=nk, d=gp.d, kind=gp.kind, Xn=self.Xk.data_ptr(), lengthscales=gp.ls.data_ptr(),
                                             shift=self._lo_c.data_ptr(), scale=self._scale_c.data_ptr(),
                                             M=self.M.data_ptr())
+        probe("operator")
         self._plans = {}
         torch.cuda.synchronize(dev)
         tm["total"] = _time.perf_counter() - t0
