@@ -1,3 +1,4 @@
+#include <algorithm>
 // qNEHVI (q = 1) device kernels on gfx950: cached-Cholesky sampling, box-cell hypervolume
 // improvement scan (forward + backward), Pareto / prune masks.
 //
@@ -178,6 +179,53 @@ __global__ void pareto_kernel(int S, int n, const double* __restrict__ O, const 
   if (counts && nd) atomicAdd(&counts[i], 1);
 }
 
+// The same test with the points of SB samples staged in LDS (loads of SB contiguous samples
+// per (objective, point)); a thread walks point i's dominance scan over LDS broadcasts
+// instead of n dependent L2 loads per (sample, point).
+template <int M>
+__global__ __launch_bounds__(256) void pareto_lds_kernel(int S, int n, int SB, const double* __restrict__ O,
+                                                         const double* __restrict__ ref, int dedup,
+                                                         unsigned char* __restrict__ mask, int* __restrict__ counts) {
+  extern __shared__ double pts[];   // [SB][n][M]
+  const int s0 = blockIdx.x * SB, sb = min(SB, S - s0);
+  const int tot = M * n * sb;
+  for (int e = threadIdx.x; e < tot; e += 256) {
+    const int j = e / (n * sb), rem = e - j * n * sb, k = rem / sb, ss = rem - k * sb;
+    pts[((size_t)ss * n + k) * M + j] = O[((size_t)j * n + k) * S + s0 + ss];
+  }
+  double rj[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) rj[j] = ref[j];
+  __syncthreads();
+  for (int p = threadIdx.x; p < sb * n; p += 256) {
+    const int ss = p / n, i = p - ss * n;
+    const double* P = pts + (size_t)ss * n * M;
+    double yi[M];
+    bool better = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      yi[j] = P[i * M + j];
+      better &= yi[j] > rj[j];
+    }
+    bool nd = better;
+    for (int k = 0; k < n && nd; ++k) {
+      if (k == i) continue;
+      bool ge = true, gt = false, eq = true;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const double v = P[k * M + j];
+        ge &= v >= yi[j];
+        gt |= v > yi[j];
+        eq &= v == yi[j];
+      }
+      if (ge && gt) nd = false;
+      if (dedup && eq && k < i) nd = false;
+    }
+    if (mask) mask[(size_t)(s0 + ss) * n + i] = nd ? 1 : 0;
+    if (counts && nd) atomicAdd(&counts[i], 1);
+  }
+}
+
 // -------------------------------------------------------------------------------------
 // qEI (q = 1, one output): plain MC sampling f_s = mu + sigma z_s with psd_safe_cholesky
 // (3 jitter tries) on the 1x1 posterior covariance; acq = mean_s (a f_s + b - best_f)_+.
@@ -323,10 +371,25 @@ int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const do
   EVR_CHECK(S >= 1 && n >= 0, "evr_pareto_mask: bad sizes");
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(cdiv(S, 64), n);
-#define L(MM) pareto_kernel<MM><<<grid, 64, 0, s>>>(S, n, O, ref, dedup, mask, counts)
-  EVR_DISPATCH_M(m, L);
+  constexpr size_t kLds = 96 * 1024;
+  const size_t per = (size_t)n * m * sizeof(double);
+  if (per <= kLds) {   // samples staged in LDS, as many per block as fit (at most 4)
+    const int SB = (int)std::min<size_t>(4, kLds / per);
+    const size_t bytes = per * SB;
+#define L(MM)                                                                                            \
+  do {                                                                                                   \
+    EVR_HIP(hipFuncSetAttribute((const void*)pareto_lds_kernel<MM>,                                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));                \
+    pareto_lds_kernel<MM><<<cdiv(S, SB), 256, bytes, s>>>(S, n, SB, O, ref, dedup, mask, counts);       \
+  } while (0)
+    EVR_DISPATCH_M(m, L);
 #undef L
+  } else {
+    dim3 grid(cdiv(S, 64), n);
+#define L(MM) pareto_kernel<MM><<<grid, 64, 0, s>>>(S, n, O, ref, dedup, mask, counts)
+    EVR_DISPATCH_M(m, L);
+#undef L
+  }
   EVR_LAUNCH_CHECK();
   return 0;
 }

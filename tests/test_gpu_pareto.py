@@ -1,0 +1,44 @@
+"""evr_pareto_mask (prune_inferior_points' per-sample Pareto test and the partitions'
+non-dominated filter) against a direct numpy statement of the rule, for the LDS-staged
+kernel and the per-point fallback (points of one sample beyond the LDS budget), with ties,
+duplicates and dedup on/off."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference(O, ref, dedup):
+    m, n, S = O.shape
+    mask = np.zeros((S, n), dtype=np.uint8)
+    for s in range(S):
+        Y = O[:, :, s].T
+        better = (Y > ref).all(1)
+        ge = (Y[None, :, :] >= Y[:, None, :]).all(2)      # [i, k]: k >= i everywhere
+        gt = (Y[None, :, :] > Y[:, None, :]).any(2)
+        dom = (ge & gt)
+        np.fill_diagonal(dom, False)
+        nd = better & ~dom.any(1)
+        if dedup:
+            eq = (Y[None, :, :] == Y[:, None, :]).all(2)
+            dup = np.tril(eq, -1).any(1)                  # an earlier identical point
+            nd &= ~dup
+        mask[s] = nd
+    return mask
+
+
+@pytest.mark.parametrize("m,n,S", [(5, 300, 37), (3, 64, 130), (2, 1000, 9), (5, 2600, 3)])
+@pytest.mark.parametrize("dedup", [False, True])
+def test_pareto_mask_matches_rule(m, n, S, dedup):
+    from everest_amd import ops
+
+    rng = np.random.default_rng(n + S)
+    O = np.round(rng.normal(size=(m, n, S)), 1)          # coarse grid: ties and duplicates
+    O[:, 5, :] = O[:, 3, :]                              # exact duplicate points
+    ref = np.full(m, -1.5)
+    mask, counts = ops.pareto_mask(torch.tensor(O, device="cuda"), torch.tensor(ref, device="cuda"), dedup,
+                                   want_mask=True, want_counts=True)
+    want = _reference(O, ref, dedup)
+    assert np.array_equal(mask.cpu().numpy(), want)
+    assert np.array_equal(counts.cpu().numpy(), want.sum(0))
