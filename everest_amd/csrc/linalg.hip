@@ -711,11 +711,28 @@ __global__ __launch_bounds__(256) void tri_inv_row_kernel(int n, int i, const do
   const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4, li = lane & 15,
             kq = lane >> 4;
   double4_t t[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  // the next step's tiles are loaded into registers while the current step's MFMAs run
+  double ra[16], rb[16];
+  const int tc = tid & 63, ti0 = tid >> 6;
+  auto fetch = [&](int k) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = 4 * u + ti0;
+      const int ra_row = i * BNB + r, ra_col = k * BNB + tc, rb_row = k * BNB + r, rb_col = j * BNB + tc;
+      ra[u] = (ra_row < n && ra_col < n) ? L[(size_t)ra_row * ldl + ra_col] : 0.0;
+      rb[u] = (rb_row < n && rb_col < n) ? X[(size_t)rb_row * ldx + rb_col] : 0.0;
+    }
+  };
+  fetch(j);
   for (int k = j; k < i; ++k) {
     __syncthreads();
-    load_tile64(TA, L, ldl, n, i * BNB, k * BNB);      // L_ik
-    load_tile64(TB, X, ldx, n, k * BNB, j * BNB);      // X_kj
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      TA[4 * u + ti0][tc] = ra[u];                    // L_ik
+      TB[4 * u + ti0][tc] = rb[u];                    // X_kj
+    }
     __syncthreads();
+    if (k + 1 < i) fetch(k + 1);
     // T += L_ik X_kj  (B operand X[kk][c])
 #pragma unroll 4
     for (int kk = 0; kk < BNB; kk += 4) {
