@@ -208,18 +208,29 @@ __global__ __launch_bounds__(256) void pareto_lds_kernel(int S, int n, int SB, c
       better &= yi[j] > rj[j];
     }
     bool nd = better;
-    for (int k = 0; k < n && nd; ++k) {
-      if (k == i) continue;
-      bool ge = true, gt = false, eq = true;
+    // 8 points per step: their 8 x M LDS loads are in flight together (the early exit is
+    // taken per step; the outcome equals the point-by-point scan's)
+    constexpr int U = 8;
+    for (int k0 = 0; k0 < n && nd; k0 += U) {
+      double v[U][M];
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const double v = P[k * M + j];
-        ge &= v >= yi[j];
-        gt |= v > yi[j];
-        eq &= v == yi[j];
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[u][j] = (k0 + u < n) ? P[(k0 + u) * M + j] : 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        if (k >= n || k == i) continue;
+        bool ge = true, gt = false, eq = true;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          ge &= v[u][j] >= yi[j];
+          gt |= v[u][j] > yi[j];
+          eq &= v[u][j] == yi[j];
+        }
+        if (ge && gt) nd = false;
+        if (dedup && eq && k < i) nd = false;
       }
-      if (ge && gt) nd = false;
-      if (dedup && eq && k < i) nd = false;
     }
     if (mask) mask[(size_t)(s0 + ss) * n + i] = nd ? 1 : 0;
     if (counts && nd) atomicAdd(&counts[i], 1);
