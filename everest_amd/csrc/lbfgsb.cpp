@@ -69,6 +69,20 @@ double dot(const double* a, const double* b, int n) {
   return s;
 }
 
+// four interleaved partial sums (vectorisable), combined in a fixed order
+double dot4(const double* a, const double* b, int n) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int i = 0;
+  for (; i + 3 < n; i += 4) {
+    s0 += a[i] * b[i];
+    s1 += a[i + 1] * b[i + 1];
+    s2 += a[i + 2] * b[i + 2];
+    s3 += a[i + 3] * b[i + 3];
+  }
+  for (; i < n; ++i) s0 += a[i] * b[i];
+  return (s0 + s1) + (s2 + s3);
+}
+
 }  // namespace
 
 Lbfgsb::Lbfgsb(int n, int m, const double* lb, const double* ub, double factr, double pgtol, int maxls)
@@ -179,12 +193,17 @@ int Lbfgsb::cauchy(std::vector<double>& xcp, std::vector<double>& c) {
   const int col = col_, col2 = 2 * col;
   xcp = x_;
   c.assign(col2, 0.0);
-  std::vector<double> p(col2, 0.0), v(col2), wbp(col2);
+  std::vector<double>& p = sc_p_;
+  std::vector<double>& v = sc_v_;
+  std::vector<double>& wbp = sc_wbp_;
+  p.assign(col2, 0.0);
+  v.assign(col2, 0.0);
+  wbp.assign(col2, 0.0);
   std::vector<double>& d = d_;
   bool bnded = true;
   int nfree = n_ + 1, nbreak = 0;
-  std::vector<std::pair<double, int>> bp;
-  bp.reserve(n_);
+  std::vector<std::pair<double, int>>& bp = sc_bp_;
+  bp.clear();
   double f1 = 0.0;
   for (int i = 0; i < n_; ++i) {
     const double neggi = -g_[i];
@@ -234,16 +253,21 @@ int Lbfgsb::cauchy(std::vector<double>& xcp, std::vector<double>& c) {
     f2 -= dot(v.data(), p.data(), col2);
   }
   double dtm = -f1 / f2, tsum = 0.0;
-  std::stable_sort(bp.begin(), bp.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
-    return a.first < b.first;
-  });
+  // breakpoints in ascending (t, index) order — the order of a stable sort by t — popped
+  // lazily from a heap (as [cauchy]'s hpsolb): the search usually stops after a few
+  const auto later = [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+    return a.first > b.first || (a.first == b.first && a.second > b.second);
+  };
+  std::make_heap(bp.begin(), bp.end(), later);
   int nleft = nbreak;
   double tj = 0.0;
   bool all_fixed = false;
   for (int k = 0; k < nbreak; ++k) {
+    std::pop_heap(bp.begin(), bp.end() - k, later);
+    const std::pair<double, int> next = bp[nbreak - 1 - k];
     const double tj0 = tj;
-    tj = bp[k].first;
-    const int ibp = bp[k].second;
+    tj = next.first;
+    const int ibp = next.second;
     const double dt = tj - tj0;
     if (dtm < dt) break;
     tsum += dt;
@@ -307,14 +331,17 @@ int Lbfgsb::cauchy(std::vector<double>& xcp, std::vector<double>& c) {
 // backtracking step along the subspace direction.  z holds x^cp on entry.
 void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
   const int col = col_, col2 = 2 * col;
-  std::vector<int> ind;
-  ind.reserve(n_);
+  std::vector<int>& ind = sc_ind_;
+  ind.clear();
   for (int i = 0; i < n_; ++i)
     if (iwhere_[i] <= 0) ind.push_back(i);
   const int nsub = (int)ind.size();
   if (nsub == 0 || col == 0) return;
   // r = -Z^T (theta (z - x) + g - W M c)
-  std::vector<double> mc(col2), r(nsub);
+  std::vector<double>& mc = sc_mc_;
+  std::vector<double>& r = sc_r_;
+  mc.assign(col2, 0.0);
+  r.assign(nsub, 0.0);
   bmv(c.data(), mc.data());
   for (int a = 0; a < nsub; ++a) {
     const int k = ind[a];
@@ -326,7 +353,10 @@ void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
     r[a] = s;
   }
   // d = (Z^T B Z)^-1 r = r / theta + W_F (M^-1 - W_F^T W_F / theta)^-1 W_F^T r / theta^2
-  std::vector<double> N(minv_lu_.size()), wv(col2, 0.0);
+  std::vector<double>& N = sc_N_;
+  std::vector<double>& wv = sc_wv_;
+  N.assign(minv_lu_.size(), 0.0);
+  wv.assign(col2, 0.0);
   {
     // rebuild M^-1 (the LU holds its factors) and subtract W_F^T W_F / theta
     const int k2 = col2;
@@ -342,23 +372,41 @@ void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
         N[(size_t)(col + i) * k2 + col + j] = theta_ * s;
       }
     }
-    std::vector<double> wk(col2);
-    for (int a = 0; a < nsub; ++a) {
-      const int k = ind[a];
-      for (int j = 0; j < col; ++j) {
-        const int pj = col_index(j);
-        wk[j] = wy_[(size_t)pj * n_ + k];
-        wk[col + j] = theta_ * ws_[(size_t)pj * n_ + k];
+    // W_F (col2 x nsub, rows contiguous) gathered once; then W_F^T r and the symmetric
+    // W_F^T W_F / theta as row dot products (vectorisable) instead of nsub rank-1 updates
+    std::vector<double>& WF = wf_;
+    WF.resize((size_t)k2 * nsub);
+    for (int j = 0; j < col; ++j) {
+      const int pj = col_index(j);
+      const double* wyr = &wy_[(size_t)pj * n_];
+      const double* wsr = &ws_[(size_t)pj * n_];
+      double* a1 = &WF[(size_t)j * nsub];
+      double* a2 = &WF[(size_t)(col + j) * nsub];
+      if (nsub == n_) {
+        for (int a = 0; a < nsub; ++a) {
+          a1[a] = wyr[a];
+          a2[a] = theta_ * wsr[a];
+        }
+      } else {
+        for (int a = 0; a < nsub; ++a) {
+          a1[a] = wyr[ind[a]];
+          a2[a] = theta_ * wsr[ind[a]];
+        }
       }
-      for (int i = 0; i < k2; ++i) {
-        wv[i] += wk[i] * r[a];
-        const double wi = wk[i] / theta_;
-        for (int j = 0; j < k2; ++j) N[(size_t)i * k2 + j] -= wi * wk[j];
+    }
+    for (int i = 0; i < k2; ++i) {
+      const double* wi = &WF[(size_t)i * nsub];
+      wv[i] = dot4(wi, r.data(), nsub);
+      for (int j = i; j < k2; ++j) {
+        const double gij = dot4(wi, &WF[(size_t)j * nsub], nsub) / theta_;
+        N[(size_t)i * k2 + j] -= gij;
+        if (j != i) N[(size_t)j * k2 + i] -= gij;
       }
     }
   }
-  std::vector<int> piv;
-  std::vector<double> dsub(nsub);
+  std::vector<int>& piv = sc_piv_;
+  std::vector<double>& dsub = sc_dsub_;
+  dsub.assign(nsub, 0.0);
   if (lu_factor(N, piv, col2)) {
     lu_solve(N, piv, col2, wv.data());
     for (int a = 0; a < nsub; ++a) {
@@ -374,7 +422,8 @@ void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
     for (int a = 0; a < nsub; ++a) dsub[a] = r[a] / theta_;   // B = theta I on the subspace
   }
   // projection of x^cp + d onto the box
-  const std::vector<double> xp = z;
+  std::vector<double>& xp = sc_xp_;
+  xp = z;
   bool hit = false;
   for (int a = 0; a < nsub; ++a) {
     const int k = ind[a];
