@@ -118,6 +118,7 @@ struct evr_qnehvi_plan {
   hipGraphExec_t hexec;
   unsigned long long seq;
   unsigned int* counter;         // blocks-done counter of the fused copy-out (device)
+  int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
 };
 
 namespace evr {
@@ -219,41 +220,40 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
     delete p;
     return rc;
   }
-  if (use_graph) {
-    hipStream_t s = (hipStream_t)stream;
-    // capture on a private stream so the caller's stream (torch's) never enters capture mode
-    hipStream_t cs = nullptr;
-    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
-      delete p;
-      EVR_CHECK(false, "evr_qnehvi_plan_create: hipStreamCreate failed");
-    }
-    int rc = 0;
-    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = 1;
-    if (!rc) rc = plan_chain(cs, p, p->X);
-    hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(cs, &g);
-    if (!rc && e == hipSuccess && g) {
-      if (hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0) == hipSuccess) p->graph = g;
-      else rc = 1;
-    } else {
-      rc = rc ? rc : 1;
-    }
-    (void)hipStreamDestroy(cs);
-    if (rc) {
-      if (g) (void)hipGraphDestroy(g);
-      delete p;
-      const std::string why = last_error();
-      EVR_CHECK(false, "evr_qnehvi_plan_create: graph capture failed (%s)", why.c_str());
-    }
-    (void)s;
-  }
+  // the device-mode graph is captured on the second run (a plan evaluated once — the raw
+  // screening chunks — or only host-driven — the restarts, which use the host graph — never
+  // pays for a capture and an instantiation)
+  p->use_graph = use_graph ? 1 : 0;
+  p->nrun = 0;
+  (void)stream;
   *out = p;
   return 0;
+}
+
+// Capture the device-mode chain into p->exec (private stream: the caller's stream, torch's,
+// never enters capture mode).  On failure the plan keeps running the chain eagerly.
+static void plan_capture(evr_qnehvi_plan* p) {
+  p->use_graph = 0;
+  hipStream_t cs = nullptr;
+  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return;
+  int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
+  if (!rc) rc = plan_chain(cs, p, p->X);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(cs, &g);
+  if (!rc && e == hipSuccess && g && hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0) == hipSuccess) {
+    p->graph = g;
+  } else {
+    if (g) (void)hipGraphDestroy(g);
+    p->exec = nullptr;
+    (void)hipGetLastError();
+  }
+  (void)hipStreamDestroy(cs);
 }
 
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
   EVR_CHECK(p, "evr_qnehvi_plan_run: null plan");
   hipStream_t s = (hipStream_t)stream;
+  if (!p->exec && p->use_graph && p->nrun++ >= 1) plan_capture(p);
   if (p->exec) {
     EVR_HIP(hipGraphLaunch(p->exec, s));
     return 0;
