@@ -155,6 +155,10 @@ _SIGS = {
                                   c_int),
     "evr_sobol_scramble": ([c_int, ctypes.c_ulonglong, c_void_p, c_void_p], c_int),
     "evr_sobol_scramble_range": ([c_int, ctypes.c_ulonglong, c_int, c_int, c_void_p, c_void_p], c_int),
+    "evr_sobol_stream_words": ([c_int], ctypes.c_longlong),
+    "evr_sobol_stream_create": ([ctypes.c_ulonglong, ctypes.c_longlong, c_void_p], c_int),
+    "evr_sobol_scramble_stream": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+    "evr_sobol_stream_destroy": ([c_void_p], None),
     "evr_sobol_normal": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
 }
 

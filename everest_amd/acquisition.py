@@ -58,6 +58,25 @@ def _prefetch_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = Non
     return _SCRAMBLE_POOL.submit(ops.sobol_scramble, dim, seed, d0, nd)
 
 
+def _submit(fn, *args):
+    global _SCRAMBLE_POOL
+    if _SCRAMBLE_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _SCRAMBLE_POOL = ThreadPoolExecutor(max_workers=3, thread_name_prefix="evr-sobol")
+    return _SCRAMBLE_POOL.submit(fn, *args)
+
+
+def _prefetch_from_stream(fut_stream, dim: int, d0: int = 0, nd: Optional[int] = None):
+    """Scramble dims [d0, d0+nd) of a dim-dimensional draw from a seed stream a worker is
+    generating (fut_stream).  The future's result is None when the stream cannot serve the
+    draw; ops.sobol_normal then scrambles (or falls back to IID normals) itself."""
+    nd = dim - d0 if nd is None else nd
+    if nd <= 0:
+        return None
+    return _submit(lambda: fut_stream.result().scramble(dim, d0, nd))
+
+
 def _result(fut):
     return None if fut is None else fut.result()
 
@@ -435,6 +454,17 @@ class QNEHVI(_BoxHviAcqf):
                 _last[0] = t
         fut_prune = (_prefetch_scramble(len(base_rows) * m, prune_seed)
                      if prune_baseline and z_prune is None else None)
+        # the sampler seed's raw stream covers the new-point and baseline draws of every
+        # possible pruning outcome (draws of one seed are prefixes of one stream): start it now,
+        # scramble the needed dimension ranges once the pruned baseline size is known
+        max_dim = (len(base_rows) + npend + 1) * m
+        def _stream_job(after=fut_prune):
+            if after is not None:      # after the prune draw, which is needed first
+                after.result()
+            return ops.SobolStream(int(sampler_seed), max_dim)
+
+        fut_stream = (_submit(_stream_job)
+                      if max_dim <= ops.SOBOL_MAXDIM and (z_new_full is None or z_base_full is None) else None)
         # ---- joint posterior at the training (+ pending) inputs, shared by prune and baseline
         K = ops.kernel_matrix(self.Xk, self.Xk, gp.ls, gp.kind) if npend else gp.kernel_train(noise=False)
         Kt = K[:, :, :n].contiguous() if npend else K                      # m x nk x n
@@ -479,8 +509,13 @@ class QNEHVI(_BoxHviAcqf):
         self.base_rows = base_rows
         idx = torch.as_tensor(base_rows, device=dev)
         S_ = self.S
-        fut_q = _prefetch_scramble((nb + 1) * m, sampler_seed, nb * m, m) if z_new_full is None else None
-        fut_b = _prefetch_scramble(nb_t * m, sampler_seed) if nb > 0 and z_base_full is None else None
+        if fut_stream is not None:
+            fut_q = _prefetch_from_stream(fut_stream, (nb + 1) * m, nb * m, m) if z_new_full is None else None
+            fut_b = (_prefetch_from_stream(fut_stream, nb_t * m)
+                     if nb > 0 and nb_t > 0 and z_base_full is None else None)
+        else:
+            fut_q = _prefetch_scramble((nb + 1) * m, sampler_seed, nb * m, m) if z_new_full is None else None
+            fut_b = _prefetch_scramble(nb_t * m, sampler_seed) if nb > 0 and z_base_full is None else None
 
         # ---- baseline posterior root, samples, box decomposition ----------------------
         if nb > 0:

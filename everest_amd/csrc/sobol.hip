@@ -17,6 +17,8 @@
 //     the inverse-normal transform with torch's calc_erfinv (rational seed + 2 Newton steps).
 #include <algorithm>
 #include <atomic>
+#include <functional>
+#include <new>
 #include <cstdint>
 #include <thread>
 #include <vector>
@@ -166,23 +168,18 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
   return evr_sobol_scramble_range(dim, seed, 0, dim, V, shift);
 }
 
-int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, long long* V, long long* shift) {
-  EVR_CHECK(dim >= 1 && V && shift && d0 >= 0 && nd >= 1 && d0 + nd <= dim,
-            "evr_sobol_scramble_range: bad arguments");
-  // the stream: shift bits (dim x 30), then the scrambling-matrix bits (dim x 30 x 30); the
-  // raw words are generated serially by this thread while the workers, one dimension range
-  // each, start as soon as the words of their range are published
+}  // extern "C"
+
+namespace evr {
+// Dimensions [d0, d0 + nd) of a dim-dimensional engine from the raw words wp of its seed's
+// stream: shift bits (dim x 30), then the scrambling-matrix bits (dim x 30 x 30).  With
+// `done`, the words are still being generated: each worker waits until its range is in.
+static void scramble_apply(const uint32_t* wp, int dim, int d0, int nd, long long* V, long long* shift,
+                           const std::function<void()>& producer, std::atomic<size_t>* done) {
   const size_t nshift = (size_t)dim * SOBOL_MAXBIT, per_dim = (size_t)SOBOL_MAXBIT * SOBOL_MAXBIT;
-  const size_t ndraw = nshift + (size_t)dim * per_dim;
-  // per-thread buffer, kept between calls (an ask() scrambles ~10 MB of draws three times)
-  thread_local std::vector<uint32_t> words;
-  const size_t nw = (ndraw + MtWords::N - 1) / MtWords::N * MtWords::N;
-  if (words.size() < nw) words.resize(nw);
   const uint32_t mask = MtWords::lsb_mask();
-  const uint32_t* wp = words.data();   // the caller's buffer (a thread_local name would
-                                       // resolve to each worker's own, empty instance)
   auto bit = [wp, mask](size_t i) { return (uint32_t)__builtin_parity(wp[i] & mask); };
-  // dimensions [d0, d0 + nd) only; V / shift hold those dimensions (row d - d0)
+  // V / shift hold the requested dimensions (row d - d0)
   auto work = [&](int dbeg, int dend) {
     uint32_t col[SOBOL_MAXBIT];
     for (int d = dbeg; d < dend; ++d) {
@@ -208,31 +205,83 @@ int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, l
       }
     }
   };
-  const uint32_t seed32 = (uint32_t)(seed & 0xffffffffull);
-  // the stream must be generated through the last requested dimension's matrix bits
-  const size_t nneed = nshift + (size_t)(d0 + nd) * per_dim;
   const int nth = nd >= 256 ? 8 : 1;
   if (nth == 1) {
-    MtWords::generate(seed32, nneed, words.data());
+    if (producer) producer();
     work(d0, d0 + nd);
-  } else {
-    std::atomic<size_t> done{0};
-    std::vector<std::thread> th;
-    const int per = (nd + nth - 1) / nth;
-    for (int i = 0; i < nth; ++i) {
-      const int a = d0 + i * per, b = std::min(d0 + nd, a + per);
-      if (a < b)
-        th.emplace_back([&, a, b] {
-          const size_t need = nshift + (size_t)b * per_dim;
-          while (done.load(std::memory_order_acquire) < need) std::this_thread::yield();
-          work(a, b);
-        });
-    }
-    MtWords::generate(seed32, nneed, words.data(), &done);
-    for (auto& t : th) t.join();
+    return;
   }
+  std::vector<std::thread> th;
+  const int per = (nd + nth - 1) / nth;
+  for (int i = 0; i < nth; ++i) {
+    const int a = d0 + i * per, b = std::min(d0 + nd, a + per);
+    if (a < b)
+      th.emplace_back([&, a, b] {
+        if (done) {
+          const size_t need = nshift + (size_t)b * per_dim;
+          while (done->load(std::memory_order_acquire) < need) std::this_thread::yield();
+        }
+        work(a, b);
+      });
+  }
+  if (producer) producer();
+  for (auto& t : th) t.join();
+}
+}  // namespace evr
+
+struct evr_sobol_stream {
+  std::vector<uint32_t> words;
+  size_t n;
+};
+
+extern "C" {
+
+int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, long long* V, long long* shift) {
+  EVR_CHECK(dim >= 1 && V && shift && d0 >= 0 && nd >= 1 && d0 + nd <= dim,
+            "evr_sobol_scramble_range: bad arguments");
+  // the raw words are generated serially by this thread while the workers, one dimension
+  // range each, start as soon as the words of their range are published; the stream is
+  // needed through the last requested dimension's matrix bits
+  const size_t nshift = (size_t)dim * SOBOL_MAXBIT, per_dim = (size_t)SOBOL_MAXBIT * SOBOL_MAXBIT;
+  const size_t nneed = nshift + (size_t)(d0 + nd) * per_dim;
+  // per-thread buffer, kept between calls (an ask() scrambles ~10 MB of draws three times)
+  thread_local std::vector<uint32_t> words;
+  const size_t nw = (nneed + MtWords::N - 1) / MtWords::N * MtWords::N;
+  if (words.size() < nw) words.resize(nw);
+  uint32_t* wp = words.data();   // the caller's buffer (a thread_local name would resolve to
+                                 // each worker's own, empty instance)
+  const uint32_t seed32 = (uint32_t)(seed & 0xffffffffull);
+  std::atomic<size_t> done{0};
+  scramble_apply(wp, dim, d0, nd, V, shift, [&] { MtWords::generate(seed32, nneed, wp, &done); }, &done);
   return 0;
 }
+
+long long evr_sobol_stream_words(int dim) {
+  return dim >= 1 ? (long long)dim * SOBOL_MAXBIT * (1 + SOBOL_MAXBIT) : 0;
+}
+
+int evr_sobol_stream_create(unsigned long long seed, long long nwords, evr_sobol_stream** out) {
+  EVR_CHECK(out && nwords >= 1, "evr_sobol_stream_create: bad arguments");
+  evr_sobol_stream* st = new (std::nothrow) evr_sobol_stream();
+  EVR_CHECK(st, "evr_sobol_stream_create: out of host memory");
+  st->n = (size_t)nwords;
+  st->words.resize((st->n + MtWords::N - 1) / MtWords::N * MtWords::N);
+  MtWords::generate((uint32_t)(seed & 0xffffffffull), st->n, st->words.data());
+  *out = st;
+  return 0;
+}
+
+int evr_sobol_scramble_stream(const evr_sobol_stream* st, int dim, int d0, int nd, long long* V, long long* shift) {
+  EVR_CHECK(st && dim >= 1 && V && shift && d0 >= 0 && nd >= 1 && d0 + nd <= dim,
+            "evr_sobol_scramble_stream: bad arguments");
+  const size_t nshift = (size_t)dim * SOBOL_MAXBIT, per_dim = (size_t)SOBOL_MAXBIT * SOBOL_MAXBIT;
+  EVR_CHECK(nshift + (size_t)(d0 + nd) * per_dim <= st->n,
+            "evr_sobol_scramble_stream: stream of %zu words too short for %d dims", st->n, dim);
+  scramble_apply(st->words.data(), dim, d0, nd, V, shift, nullptr, nullptr);
+  return 0;
+}
+
+void evr_sobol_stream_destroy(evr_sobol_stream* st) { delete st; }
 
 int evr_sobol_normal(void* stream, int n, int nd, int d0, const long long* V, const long long* shift, int layout,
                      int m, double* out) {

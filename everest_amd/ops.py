@@ -797,6 +797,40 @@ def sobol_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = None):
     return V, shift
 
 
+class SobolStream:
+    """The raw mt19937 stream of one seed, long enough for draws of up to ``max_dim``
+    dimensions (evr_sobol_stream_create; releases the GIL, so it can be generated on a worker
+    thread before the draw's dimension count is known)."""
+
+    def __init__(self, seed: int, max_dim: int):
+        lib = _native.load()
+        self._lib = lib
+        self.seed, self.max_dim = int(seed), int(max_dim)
+        h = ctypes.c_void_p()
+        call("evr_sobol_stream_create", self.seed, lib.evr_sobol_stream_words(self.max_dim), ctypes.byref(h))
+        self._h = h
+
+    def scramble(self, dim: int, d0: int = 0, nd: Optional[int] = None):
+        """(V, shift) of dims [d0, d0+nd) of SobolEngine(dim, scramble=True, seed) — as
+        sobol_scramble — or None beyond SOBOL_MAXDIM / this stream's length."""
+        nd = dim - d0 if nd is None else nd
+        if dim > SOBOL_MAXDIM or dim > self.max_dim or nd < 1:
+            return None
+        V = _sobol_directions(dim)[d0:d0 + nd].clone()
+        shift = torch.empty(nd, dtype=torch.long)
+        call("evr_sobol_scramble_stream", self._h, dim, d0, nd, V.data_ptr(), shift.data_ptr())
+        return V, shift
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None:
+            try:
+                self._lib.evr_sobol_stream_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
 def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[int] = None,
                  layout: int = 0, m: int = 1, scrambled=None) -> torch.Tensor:
     """Device draw_sobol_normal_samples(dim, n, seed) restricted to dims [d0, d0+nd).

@@ -458,6 +458,15 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
  * shift (nd) hold those dimensions (the stream is still drawn through dimension d0 + nd - 1;
  * the per-dimension work is skipped for the others). */
 int evr_sobol_scramble_range(int dim, unsigned long long seed, int d0, int nd, long long* V, long long* shift);
+/* The same in two steps: generate a seed's raw stream once (evr_sobol_stream_words(dim)
+ * words cover every draw of up to dim dimensions; the draws of one seed at different
+ * dimension counts are prefixes of the same stream), then scramble dimension ranges of any
+ * dim it covers.  Lets the host start the stream before the dimension count is known. */
+typedef struct evr_sobol_stream evr_sobol_stream;
+long long evr_sobol_stream_words(int dim);
+int evr_sobol_stream_create(unsigned long long seed, long long nwords, evr_sobol_stream** out);
+int evr_sobol_scramble_stream(const evr_sobol_stream* st, int dim, int d0, int nd, long long* V, long long* shift);
+void evr_sobol_stream_destroy(evr_sobol_stream* st);
 int evr_sobol_normal(void* stream, int n, int nd, int d0, const long long* V, const long long* shift,
                      int layout, int m, double* out);
 
