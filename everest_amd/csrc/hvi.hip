@@ -492,7 +492,15 @@ __device__ __forceinline__ int wave_scan_excl(int v, int* total) {
 // phase timers of the instrumented build (EVR_KD_PROF=1): per-wave clock deltas summed into
 // counters[4 + phase] (0 stage, 1 group filter + prefix, 2 cell filter, 3 term evaluation,
 // 4 segmented scan + accumulate)
-#define KD_T0() long long kd_t = EVR_KD_PROF ? clock64() : 0
+#define KD_T0() long long kd_t = EVR_KD_PROF ? clock64() : 0; const long long kd_ts = kd_t
+// longest wave (counters[9]) and waves timed (counters[10]) of the instrumented build
+#define KD_TEND()                                                                     \
+  do {                                                                                \
+    if (EVR_KD_PROF && kd.counters && (threadIdx.x & 63) == 0) {                     \
+      atomicMax(kd.counters + 9, (unsigned long long)(clock64() - kd_ts));            \
+      atomicAdd(kd.counters + 10, 1ull);                                              \
+    }                                                                                 \
+  } while (0)
 #define KD_T(ph)                                                                      \
   do {                                                                                \
     if (EVR_KD_PROF && kd.counters) {                                                 \
@@ -860,7 +868,7 @@ template <int M, bool BWD>
 __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
-                                               double* __restrict__ dG, int W, int balance) {
+                                               double* __restrict__ dG, int W, int balance, int ilv) {
   constexpr int NV = BWD ? M + 1 : 1;
   constexpr int CW = KD_CT / 4;            // candidate slots per wave
   using K = CellKey<M>;
@@ -895,14 +903,30 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   auto valid = [&](int c) { return (c & 15) < gsz && cand(c) < b; };
   const int stride = kd.stride;
   KD_T0();
+  // The sample's 16-group chunks are dealt to the nsplit workgroups (and within one to its W
+  // waves) round-robin when ilv is set: the kd order keeps a candidate's dominated cells in
+  // neighbouring chunks, so contiguous ranges would leave most of a sample's terms to one or
+  // two of its splits.  Workgroup-local chunk ql is the sample's chunk q0 + ql * qstep.
   const int split = blockIdx.z;
-  const int NQall = (kd.goff[s + 1] - kd.goff[s] + 15) >> 4;
-  const int qper = (NQall + nsplit - 1) / nsplit;
-  const int q0 = min(NQall, split * qper);
-  const int NQ = min(NQall, q0 + qper) - q0;                 // this workgroup's 16-group chunks
-  int qw0 = 0, NQw = NQ;                                     // this wave's share (set below)
-  const int gbase = kd.goff[s] + 16 * q0;
-  const int Gs = min(kd.goff[s + 1] - gbase, 16 * NQ);
+  const int Gsamp = kd.goff[s + 1] - kd.goff[s];
+  const int NQall = (Gsamp + 15) >> 4;
+  int q0, NQ, qstep;
+  if (ilv) {
+    q0 = split;
+    qstep = nsplit;
+    NQ = split < NQall ? (NQall - split + nsplit - 1) / nsplit : 0;
+  } else {
+    const int qper = (NQall + nsplit - 1) / nsplit;
+    q0 = min(NQall, split * qper);
+    qstep = 1;
+    NQ = min(NQall, q0 + qper) - q0;                         // this workgroup's 16-group chunks
+  }
+  auto qgl = [&](int ql) { return q0 + ql * qstep; };       // workgroup-local -> sample chunk
+  auto gend_of = [&](int ql) { return min(16, Gsamp - 16 * qgl(ql)); };
+  int qw0 = 0, NQw = NQ, qwst = 1;                           // this wave's share (set below)
+  const int gbase = kd.goff[s];
+  // groups of this workgroup's chunks (the sample's last chunk may be short)
+  const int Gs = 16 * NQ - ((NQ > 0 && qgl(NQ - 1) == NQall - 1) ? 16 * NQall - Gsamp : 0);
   const Kd2Lds Lo = kd2_lds(stride, M, kd.max_groups);
   double* pt = (double*)(kd_dyn + Lo.pt);
   unsigned short* mA = (unsigned short*)(kd_dyn + Lo.mA);
@@ -911,10 +935,17 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   uint4* gb = (uint4*)(kd_dyn + Lo.gb);                 // ... and their LDS copy
 
   kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
-  if (Gs > 0) kd_stage(gb, gmin, Gs);
+  if (!ilv) {
+    if (Gs > 0) kd_stage(gb, gmin + 16 * q0, Gs);
+  } else {
+    for (int e = tid; e < 16 * NQ; e += 256) {
+      const int g = 16 * qgl(e >> 4) + (e & 15);
+      if (g < Gsamp) gb[e] = gmin[g];
+    }
+  }
   for (int q = tid; q < NQ; q += 256) {    // chunk minima from the same (L2-resident) bytes
-    const uint4* src = gmin + 16 * q;
-    const int gend = min(16, Gs - 16 * q);
+    const uint4* src = gmin + 16 * qgl(q);
+    const int gend = gend_of(q);
     uint4 mn = src[0];
     for (int k = 1; k < gend; ++k) {
       const uint4 v = src[k];
@@ -952,7 +983,11 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   const int cbase = (wave / W) * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
   const int aslot = wave * CW;         // ... and its accumulator rows
   if (!valid(cbase)) return;
-  {   // this wave's share of the workgroup's chunks
+  if (ilv) {   // this wave's share of the workgroup's chunks: local chunk qw0 + k * qwst
+    qw0 = wsub;
+    qwst = W;
+    NQw = wsub < NQ ? (NQ - wsub + W - 1) / W : 0;
+  } else {
     const int qpw = (NQ + W - 1) / W;
     const int qa = min(NQ, wsub * qpw);
     qw0 = qa;
@@ -966,7 +1001,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     unsigned short* ent = pA;   // entry list (pA is rewritten by the prefix)
     int nent = 0;
     for (int eb = 0; eb < NE; eb += 64) {
-      const int e = eb + lane, q = qw0 + (e >> 4), cl = e & 15;
+      const int e = eb + lane, q = qw0 + (e >> 4) * qwst, cl = e & 15;
       bool pass = false;
       if (e < NE) {
         mA[q * KD_CT + cbase + cl] = 0;
@@ -978,9 +1013,9 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     }
     wave_sync();
     for (int i = lane; i < nent; i += 64) {
-      const int e = ent[i], q = qw0 + (e >> 4), cl = e & 15;
+      const int e = ent[i], q = qw0 + (e >> 4) * qwst, cl = e & 15;
       const uint4 t = thp[cbase + cl];
-      const int gend = min(16, Gs - q * 16);
+      const int gend = gend_of(q);
       unsigned int mask = 0;
       for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], t) << k;
       mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
@@ -1004,7 +1039,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     for (int k = 0; k < 8; ++k) {
       cnt[k] = 0;
       if (e0 + k < e1) {
-        cnt[k] = __popc(mA[(qw0 + q) * KD_CT + cbase + cl]);
+        cnt[k] = __popc(mA[(qw0 + q * qwst) * KD_CT + cbase + cl]);
         if (++q == NQw) q = 0, ++cl;
       }
       loc += cnt[k];
@@ -1044,9 +1079,9 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     unsigned int mB = 0;
     int cg = 0;
     if (p < PA) {
-      const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = qw0 + ownB - cl * NQw;
+      const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = qw0 + (ownB - cl * NQw) * qwst;
       const int c = cbase + cl;
-      const int g = q * 16 + kth_bit16(mA[q * KD_CT + c], p - pA[ownB]);
+      const int g = 16 * qgl(q) + kth_bit16(mA[q * KD_CT + c], p - pA[ownB]);   // the sample's group
       const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
       const uint4 tq = thp[c];
       const unsigned int tw[4] = {tq.x, tq.y, tq.z, tq.w};
@@ -1152,6 +1187,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     wave_sync();   // mb / mc are rewritten by the next window
   }
   wave_sync();
+  KD_TEND();
   const int nst = nsplit * W;   // partial splits: workgroup splits x wave splits
   const size_t ss = ((size_t)s * nsplit + split) * W + wsub;
   if (lane < CW && valid(cbase + lane)) part[ss * b + cand(cbase + lane)] = acc[aslot + lane][0];
@@ -1235,7 +1271,12 @@ static int hvi_kd_wsplit(int b) {
 static int hvi_kd_nsplit(const evr_qnehvi_state* st, int b) {
   const int tiles = cdiv(b, KD_CT / hvi_kd_wsplit(b)) * st->S;
   const int nq = (st->max_groups + 15) / 16;
-  return std::max(1, std::min(std::min(cdiv(1024, tiles), 8), std::max(nq, 1)));
+  static const int wgs = [] {   // EVR_KD_WGS: workgroups to fill (tuning knob, default 1024)
+    const char* e = std::getenv("EVR_KD_WGS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 1024;
+  }();
+  return std::max(1, std::min(std::min(cdiv(wgs, tiles), 16), std::max(nq, 1)));
 }
 
 // workspace (doubles): S x ns x b partials | S x M x b int thresholds | (ns > 1) S x ns x M x b dG
@@ -1275,8 +1316,14 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
       const char* e = std::getenv("EVR_KD_BALANCE");
       return (e && e[0] == '0') ? 0 : 1;
     }();
+    // round-robin chunks for the wave-split restart batches (b <= 32); larger batches keep
+    // contiguous ranges (bitwise equal to hvi_kd).  EVR_KD_ILV=0: contiguous everywhere (A/B)
+    static const int ilv = [] {
+      const char* e = std::getenv("EVR_KD_ILV");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
     hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, nsb, G, th, hvi_kd_of(st), gout, part,
-                                                  ns > 1 ? dgp : dG, W, balance);
+                                                  ns > 1 ? dgp : dG, W, balance, ilv && W > 1);
   }
   EVR_LAUNCH_CHECK();
   if (acq && BWD && ns > 1) {   // one launch for both reductions
