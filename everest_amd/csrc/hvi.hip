@@ -492,18 +492,35 @@ __device__ __forceinline__ int wave_scan_excl(int v, int* total) {
 // phase timers of the instrumented build (EVR_KD_PROF=1): per-wave clock deltas summed into
 // counters[4 + phase] (0 stage, 1 group filter + prefix, 2 cell filter, 3 term evaluation,
 // 4 segmented scan + accumulate)
-#define KD_T0() long long kd_t = EVR_KD_PROF ? clock64() : 0; const long long kd_ts = kd_t
+#define KD_T0() long long kd_t = EVR_KD_PROF ? clock64() : 0; const long long kd_ts = kd_t; \
+  const unsigned long long kd_w0 = EVR_KD_PROF ? wall_clock64() : 0; \
+  unsigned long long kd_wst = 0, kd_wpf = 0; long long kd_np = 0, kd_nt = 0
+#define KD_WSTAMP(v) do { if (EVR_KD_PROF == 2) v = wall_clock64(); } while (0)
 // longest wave (counters[9]) and waves timed (counters[10]) of the instrumented build
 #define KD_TEND()                                                                     \
   do {                                                                                \
     if (EVR_KD_PROF && kd.counters && (threadIdx.x & 63) == 0) {                     \
-      atomicMax(kd.counters + 9, (unsigned long long)(clock64() - kd_ts));            \
-      atomicAdd(kd.counters + 10, 1ull);                                              \
+      if (EVR_KD_PROF == 1) {                                                         \
+        atomicMax(kd.counters + 9, (unsigned long long)(clock64() - kd_ts));          \
+        atomicAdd(kd.counters + 10, 1ull);                                            \
+      }                                                                               \
+      /* per-wave record (counters[16 + 8 w ...]): wall-clock start, staged, prefixed, */ \
+      /* end, sample, split, group pairs, terms (EVR_KD_PROF=2)                        */ \
+      const size_t kd_gw = ((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6); \
+      unsigned long long* kd_r = kd.counters + 16 + 8 * kd_gw;                         \
+      kd_r[0] = kd_w0;                                                                \
+      kd_r[1] = kd_wst;                                                               \
+      kd_r[2] = kd_wpf;                                                               \
+      kd_r[3] = wall_clock64();                                                       \
+      kd_r[4] = (unsigned long long)s;                                                \
+      kd_r[5] = (unsigned long long)blockIdx.z;                                       \
+      kd_r[6] = (unsigned long long)kd_np;                                            \
+      kd_r[7] = (unsigned long long)kd_nt;                                            \
     }                                                                                 \
   } while (0)
 #define KD_T(ph)                                                                      \
   do {                                                                                \
-    if (EVR_KD_PROF && kd.counters) {                                                 \
+    if (EVR_KD_PROF == 1 && kd.counters) {                                            \
       const long long kd_n = clock64();                                               \
       if ((threadIdx.x & 63) == 0) atomicAdd(kd.counters + 4 + (ph), (unsigned long long)(kd_n - kd_t)); \
       kd_t = kd_n;                                                                    \
@@ -935,26 +952,24 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   uint4* gb = (uint4*)(kd_dyn + Lo.gb);                 // ... and their LDS copy
 
   kd_stage(pt, kd.pts + (size_t)s * stride * M, stride * M);
-  if (!ilv) {
-    if (Gs > 0) kd_stage(gb, gmin + 16 * q0, Gs);
-  } else {
-    for (int e = tid; e < 16 * NQ; e += 256) {
-      const int g = 16 * qgl(e >> 4) + (e & 15);
-      if (g < Gsamp) gb[e] = gmin[g];
+  // group minima into LDS and, from the same registers, each chunk's minimum corner by a
+  // 16-lane xor-shuffle reduction (a chunk's 16 groups sit in 16 consecutive lanes): one
+  // round of independent loads instead of a 16-step dependent loop per chunk
+  for (int e = tid; e < 16 * NQ; e += 256) {
+    const int q = e >> 4, g = 16 * qgl(q) + (e & 15);
+    uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);   // identity of the packed u16 minimum
+    if (g < Gsamp) {
+      v = gmin[g];
+      gb[e] = v;
     }
-  }
-  for (int q = tid; q < NQ; q += 256) {    // chunk minima from the same (L2-resident) bytes
-    const uint4* src = gmin + 16 * qgl(q);
-    const int gend = gend_of(q);
-    uint4 mn = src[0];
-    for (int k = 1; k < gend; ++k) {
-      const uint4 v = src[k];
-      mn.x = pk_min_u16(mn.x, v.x);
-      mn.y = pk_min_u16(mn.y, v.y);
-      mn.z = pk_min_u16(mn.z, v.z);
-      mn.w = pk_min_u16(mn.w, v.w);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      v.x = pk_min_u16(v.x, (unsigned int)__shfl_xor((int)v.x, o, 64));
+      v.y = pk_min_u16(v.y, (unsigned int)__shfl_xor((int)v.y, o, 64));
+      v.z = pk_min_u16(v.z, (unsigned int)__shfl_xor((int)v.z, o, 64));
+      v.w = pk_min_u16(v.w, (unsigned int)__shfl_xor((int)v.w, o, 64));
     }
-    cmin[q] = mn;
+    if ((e & 15) == 0) cmin[q] = v;
   }
   for (int e = tid; e < KD_CT * M; e += 256) {
     const int j = e / KD_CT, c = e - j * KD_CT;
@@ -979,6 +994,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   for (int e = tid; e < KD_CT * NV; e += 256) (&acc[0][0])[e] = 0.0;
   __syncthreads();
   KD_T(0);
+  KD_WSTAMP(kd_wst);
   const int wsub = wave % W;
   const int cbase = (wave / W) * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
   const int aslot = wave * CW;         // ... and its accumulator rows
@@ -1020,7 +1036,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], t) << k;
       mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
     }
-    if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
+    if (EVR_KD_PROF != 2 && kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
   }
   wave_sync();
   // candidate-major prefix over the entries e = cl * NQw + q (a candidate's pairs contiguous);
@@ -1054,7 +1070,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     preE[8] = run;
     if (lane == 0) {
       pA[NE] = (unsigned short)PA;
-      if (kd.counters) {
+      if (EVR_KD_PROF != 2 && kd.counters) {
         atomicAdd(kd.counters + 0, (unsigned long long)PA);
         atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - cand(cbase), gsz)) * Gs);
       }
@@ -1062,6 +1078,8 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   }
   wave_sync();
   KD_T(1);
+  KD_WSTAMP(kd_wpf);
+  if (EVR_KD_PROF == 2) kd_np = PA;
 
   int* mb = mk[wave];
   int* mc = mb;   // the evaluation reuses the row once the cell filter has read it
@@ -1110,7 +1128,8 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     int EW;
     const int pre = wave_scan_excl(cntB, &EW);
     KD_T(2);
-    if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
+    if (EVR_KD_PROF == 2) kd_nt += EW;
+    if (EVR_KD_PROF != 2 && kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
     // ---- C: term -> pair by marks (software-pipelined: the next round's owner and key
     //      load are issued before the current round is evaluated) ----
     int carryC = -1;
@@ -1130,13 +1149,18 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
         key = kd.gkeys[(size_t)(gbase + (cgo & 0xFFFF)) * 16 + kth_bit16((unsigned int)mo, cb + lane - po)];
       }
     };
-    int cnext = -1;
-    unsigned long long knext = 0;
+    // two rounds in flight: round r + 2's owner and key load are issued before round r is
+    // evaluated (one round's evaluation is shorter than an L2/MALL key-load latency)
+    int cnext = -1, cnext2 = -1;
+    unsigned long long knext = 0, knext2 = 0;
     if (EW > 0) locate(0, cnext, knext);
+    if (EW > 64) locate(64, cnext2, knext2);
     for (int cb = 0; cb < EW; cb += 64) {
       const int c = cnext;
       const unsigned long long key = knext;
-      if (cb + 64 < EW) locate(cb + 64, cnext, knext);
+      cnext = cnext2;
+      knext = knext2;
+      if (cb + 128 < EW) locate(cb + 128, cnext2, knext2);
       int rcv = -1;
       double val[NV];
 #pragma unroll
