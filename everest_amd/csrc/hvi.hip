@@ -854,6 +854,16 @@ __host__ __device__ inline Kd2Lds kd2_lds(int stride, int M, int max_groups) {
   return L;
 }
 
+// DPP move with an undefined old value (no zero-initialised destination): only read by lanes
+// whose source lane exists — there the key move below carries the source's key, elsewhere the
+// old -2, which matches no key
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64_u(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)x, CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, ROWMASK, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 // one segmented-scan step; returns whether any lane's source shared its key
 template <int CTRL, int ROWMASK, int NV>
 __device__ __forceinline__ bool seg_step_x(int key, double (&val)[NV]) {
@@ -862,7 +872,7 @@ __device__ __forceinline__ bool seg_step_x(int key, double (&val)[NV]) {
   if (__ballot(same) == 0ull) return false;
   double x[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) x[v] = dpp_f64<CTRL, ROWMASK>(val[v]);
+  for (int v = 0; v < NV; ++v) x[v] = dpp_f64_u<CTRL, ROWMASK>(val[v]);
   if (same) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) val[v] += x[v];
@@ -1143,24 +1153,19 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       const int mo = __shfl((int)mB, o, 64);
       const int po = __shfl(pre, o, 64);
       wave_sync();
-      c = -1;
-      if (cb + lane < EW) {
-        c = cgo >> 16;
-        key = kd.gkeys[(size_t)(gbase + (cgo & 0xFFFF)) * 16 + kth_bit16((unsigned int)mo, cb + lane - po)];
-      }
+      // the key load is issued by every lane (past the end: the sample's first key), so each
+      // locate issues exactly one load and the compiler can count them across rounds
+      const bool in = cb + lane < EW;
+      c = in ? (cgo >> 16) : -1;
+      const size_t kidx = in ? (size_t)(gbase + (cgo & 0xFFFF)) * 16 + kth_bit16((unsigned int)mo, cb + lane - po)
+                             : (size_t)gbase * 16;
+      key = kd.gkeys[kidx];
     };
-    // two rounds in flight: round r + 2's owner and key load are issued before round r is
-    // evaluated (one round's evaluation is shorter than an L2/MALL key-load latency)
-    int cnext = -1, cnext2 = -1;
-    unsigned long long knext = 0, knext2 = 0;
-    if (EW > 0) locate(0, cnext, knext);
-    if (EW > 64) locate(64, cnext2, knext2);
-    for (int cb = 0; cb < EW; cb += 64) {
-      const int c = cnext;
-      const unsigned long long key = knext;
-      cnext = cnext2;
-      knext = knext2;
-      if (cb + 128 < EW) locate(cb + 128, cnext2, knext2);
+    // Rounds alternate between two (owner, key) buffers: round r + 2's owner and key load are
+    // issued into the buffer round r has just consumed, so the load is in flight while round
+    // r + 1 is evaluated.  (A buffer copied from a register with a load in flight would make
+    // the compiler wait for that load at the loop head.)
+    auto term_round = [&](const int c, const unsigned long long key) {
       int rcv = -1;
       double val[NV];
 #pragma unroll
@@ -1207,6 +1212,20 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
         for (int v = 0; v < NV; ++v) acc[rcv - cbase + aslot][v] += val[v];
       }
       KD_T(4);
+    };
+    // Every path through the loop issues the same loads in the same order (locates past the
+    // end are dummies), so the wait before a round's first key use counts only its own load.
+    if (EW > 0) {
+      int cA = -1, cB = -1;
+      unsigned long long kA = 0, kB = 0;
+      locate(0, cA, kA);
+      locate(64, cB, kB);
+      for (int cb = 0; cb < EW; cb += 128) {
+        term_round(cA, kA);
+        locate(cb + 128, cA, kA);
+        if (cb + 64 < EW) term_round(cB, kB);
+        locate(cb + 192, cB, kB);
+      }
     }
     wave_sync();   // mb / mc are rewritten by the next window
   }
