@@ -22,3 +22,5 @@ torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("cumulative").print_stats(45)
+st.sort_stats("tottime").print_stats(40)
+st.print_callers("ops.py.*cholesky|_native.py.*call|method .cpu.|method .item.|method .tolist.")
