@@ -224,8 +224,18 @@ __device__ __forceinline__ void reduce_fwd_body(int blk, int S, int nchunk, int 
   const int tot = S * nchunk;
   double sum = 0.0;
   if (c < b) {
+    // 32 partials per thread in flight at once (the restart batch: S x 8 partials over 64
+    // groups), summed in the same sequential order as the plain loop
+    int k = g;
+    for (; k + 31 * G < tot; k += 32 * G) {
+      double x[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) x[u] = work[(size_t)(k + u * G) * b + c];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) sum += x[u];
+    }
 #pragma unroll 8
-    for (int k = g; k < tot; k += G) sum += work[(size_t)k * b + c];
+    for (; k < tot; k += G) sum += work[(size_t)k * b + c];
   }
   red[g][cx] = sum;
   __syncthreads();

@@ -316,8 +316,18 @@ __global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const d
                                                    const double* seqp, unsigned int* counter) {
   const int e = blockIdx.x, lane = threadIdx.x;
   const int k = e % d;
+  // the lane's first 8 partials loaded together, then summed in the loop's order
+  double x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int p = lane + 64 * u;
+    x[u] = p < np ? dXp[(size_t)p * b * d + e] : 0.0;
+  }
   double v = 0.0;
-  for (int p = lane; p < np; p += 64) v += dXp[(size_t)p * b * d + e];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (lane + 64 * u < np) v += x[u];
+  for (int p = lane + 512; p < np; p += 64) v += dXp[(size_t)p * b * d + e];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if (lane == 0) {
