@@ -256,6 +256,20 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       acc1 = mfma4(a, Bs[rr][i + 16], acc1);
     }
   }
+  // the epilogue's training rows and mean-row entries, loaded before the dk exchange so their
+  // latency overlaps it: thread (candidate c, row group g) uses rows i0 + g and i0 + g + 8
+  double xr[2][QS_MAXD], mrow[2];
+  {
+    const int g = tid >> 5;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int irow = i0 + g + 8 * h;
+      const bool in = irow < n;
+#pragma unroll
+      for (int k = 0; k < QS_MAXD; ++k) xr[h][k] = (in && k < d) ? Xn[(size_t)irow * d + k] : 0.0;
+      mrow[h] = (in && z == 0) ? Mj[(size_t)(Rr - 1) * n + irow] : 0.0;
+    }
+  }
   __syncthreads();   // all waves are done with Ms, Bs (dk aliases them)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -279,11 +293,11 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
         const int ii = g + 8 * h, irow = i0 + ii;
         if (irow >= n) continue;
         double gk = ((dk[0][ii][c] + dk[1][ii][c]) + dk[2][ii][c]) + dk[3][ii][c];
-        if (z == 0) gk = fma(Mj[(size_t)(Rr - 1) * n + irow], cf[2][c], gk);   // mean row
+        if (z == 0) gk = fma(mrow[h], cf[2][c], gk);   // mean row
         double diff[QS_MAXD], d2 = 0.0;
 #pragma unroll
         for (int k = 0; k < QS_MAXD; ++k) {
-          const double df = k < d ? (xc[k] - Xn[(size_t)irow * d + k]) * il[k] : 0.0;
+          const double df = k < d ? (xc[k] - xr[h][k]) * il[k] : 0.0;
           diff[k] = df * il[k];
           d2 = fma(df, df, d2);
         }
