@@ -1,4 +1,6 @@
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 // qNEHVI (q = 1) device kernels on gfx950: cached-Cholesky sampling, box-cell hypervolume
 // improvement scan (forward + backward), Pareto / prune masks.
 //
@@ -237,6 +239,93 @@ __global__ __launch_bounds__(256) void pareto_lds_kernel(int S, int n, int SB, c
   }
 }
 
+// The same test with an exact f32 pre-filter: rounding to f32 is monotone, so
+// f32(v) < f32(y) in some objective proves v < y there and k can neither dominate nor
+// duplicate i.  Only the (k, i) pairs that pass every objective in f32 (a dominator, a
+// duplicate or a near-tie) are decided in f64 — f64 compares issue at a quarter of the f32
+// rate and were the bound of pareto_lds_kernel.  LDS: the points as f64 [SB][n][M] for the
+// exact test and as f32 [SB][M][npad] (objective-major, 8-aligned runs of k) for the filter.
+template <int M>
+__global__ __launch_bounds__(256) void pareto_f32_kernel(int S, int n, int npad, int SB, const double* __restrict__ O,
+                                                         const double* __restrict__ ref, int dedup,
+                                                         unsigned char* __restrict__ mask, int* __restrict__ counts) {
+  extern __shared__ double pts[];   // [SB][n][M] f64, then [SB][M][npad] f32
+  float* ptf = reinterpret_cast<float*>(pts + (size_t)SB * n * M);
+  const int s0 = blockIdx.x * SB, sb = min(SB, S - s0);
+  const int tot = M * n * sb;
+  for (int e = threadIdx.x; e < tot; e += 256) {
+    const int j = e / (n * sb), rem = e - j * n * sb, k = rem / sb, ss = rem - k * sb;
+    const double v = O[((size_t)j * n + k) * S + s0 + ss];
+    pts[((size_t)ss * n + k) * M + j] = v;
+    ptf[((size_t)ss * M + j) * npad + k] = (float)v;
+  }
+  for (int e = threadIdx.x; e < sb * M * (npad - n); e += 256) {   // padding: never passes
+    const int r = e / (npad - n), k = n + (e - r * (npad - n));
+    ptf[(size_t)r * npad + k] = -INFINITY;
+  }
+  double rj[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) rj[j] = ref[j];
+  __syncthreads();
+  for (int p = threadIdx.x; p < sb * n; p += 256) {
+    const int ss = p / n, i = p - ss * n;
+    const double* P = pts + (size_t)ss * n * M;
+    const float* F = ptf + (size_t)ss * M * npad;
+    double yi[M];
+    float yf[M];
+    bool better = true;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      yi[j] = P[i * M + j];
+      yf[j] = (float)yi[j];
+      better &= yi[j] > rj[j];
+    }
+    bool nd = better;
+    for (int k0 = 0; k0 < n && nd; k0 += 8) {
+      float4 va[M], vb[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        va[j] = *reinterpret_cast<const float4*>(F + (size_t)j * npad + k0);
+        vb[j] = *reinterpret_cast<const float4*>(F + (size_t)j * npad + k0 + 4);
+      }
+      float mn[8];
+      mn[0] = va[0].x - yf[0]; mn[1] = va[0].y - yf[0]; mn[2] = va[0].z - yf[0]; mn[3] = va[0].w - yf[0];
+      mn[4] = vb[0].x - yf[0]; mn[5] = vb[0].y - yf[0]; mn[6] = vb[0].z - yf[0]; mn[7] = vb[0].w - yf[0];
+#pragma unroll
+      for (int j = 1; j < M; ++j) {
+        mn[0] = fminf(mn[0], va[j].x - yf[j]); mn[1] = fminf(mn[1], va[j].y - yf[j]);
+        mn[2] = fminf(mn[2], va[j].z - yf[j]); mn[3] = fminf(mn[3], va[j].w - yf[j]);
+        mn[4] = fminf(mn[4], vb[j].x - yf[j]); mn[5] = fminf(mn[5], vb[j].y - yf[j]);
+        mn[6] = fminf(mn[6], vb[j].z - yf[j]); mn[7] = fminf(mn[7], vb[j].w - yf[j]);
+      }
+      // candidate bits: every objective >= in f32 (fminf drops NaN operands, so a NaN only
+      // sends the pair to the exact test, which rejects it)
+      unsigned int cand = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cand |= (unsigned int)(mn[u] >= 0.0f && k0 + u != i && k0 + u < n) << u;
+      while (cand) {
+        const int u = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const int k = k0 + u;
+        bool ge = true, gt = false, eq = true;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const double v = P[k * M + j];
+          ge &= v >= yi[j];
+          gt |= v > yi[j];
+          eq &= v == yi[j];
+        }
+        if ((ge && gt) || (dedup && eq && k < i)) {
+          nd = false;
+          cand = 0;
+        }
+      }
+    }
+    if (mask) mask[(size_t)(s0 + ss) * n + i] = nd ? 1 : 0;
+    if (counts && nd) atomicAdd(&counts[i], 1);
+  }
+}
+
 // -------------------------------------------------------------------------------------
 // qEI (q = 1, one output): plain MC sampling f_s = mu + sigma z_s with psd_safe_cholesky
 // (3 jitter tries) on the 1x1 posterior covariance; acq = mean_s (a f_s + b - best_f)_+.
@@ -384,7 +473,27 @@ int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const do
   hipStream_t s = (hipStream_t)stream;
   constexpr size_t kLds = 96 * 1024;
   const size_t per = (size_t)n * m * sizeof(double);
-  if (per <= kLds) {   // samples staged in LDS, as many per block as fit (at most 4)
+  // f32 pre-filter variant (EVR_PARETO=f64 keeps the f64-only scan): f64 + f32 copies of
+  // SB samples per block, SB chosen so that two blocks fit a CU's LDS
+  static const int f32_filter = [] {
+    const char* e = std::getenv("EVR_PARETO");
+    return (e && std::string(e) == "f64") ? 0 : 1;
+  }();
+  const int npad = (n + 7) & ~7;
+  const size_t per2 = (size_t)n * m * sizeof(double) + (size_t)npad * m * sizeof(float);
+  constexpr size_t kLds2 = 78 * 1024;
+  if (f32_filter && per2 <= kLds2) {
+    const int SB = (int)std::min<size_t>(4, kLds2 / per2);
+    const size_t bytes = per2 * SB;
+#define L(MM)                                                                                            \
+  do {                                                                                                   \
+    EVR_HIP(hipFuncSetAttribute((const void*)pareto_f32_kernel<MM>,                                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));                \
+    pareto_f32_kernel<MM><<<cdiv(S, SB), 256, bytes, s>>>(S, n, npad, SB, O, ref, dedup, mask, counts);  \
+  } while (0)
+    EVR_DISPATCH_M(m, L);
+#undef L
+  } else if (per <= kLds) {   // samples staged in LDS, as many per block as fit (at most 4)
     const int SB = (int)std::min<size_t>(4, kLds / per);
     const size_t bytes = per * SB;
 #define L(MM)                                                                                            \

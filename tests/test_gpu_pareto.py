@@ -28,13 +28,18 @@ def _reference(O, ref, dedup):
     return mask
 
 
-@pytest.mark.parametrize("m,n,S", [(5, 300, 37), (3, 64, 130), (2, 1000, 9), (5, 2600, 3)])
+@pytest.mark.parametrize("m,n,S", [(5, 300, 37), (3, 64, 130), (2, 1000, 9), (5, 2600, 3), (5, 509, 11)])
 @pytest.mark.parametrize("dedup", [False, True])
-def test_pareto_mask_matches_rule(m, n, S, dedup):
+@pytest.mark.parametrize("near", [False, True])
+def test_pareto_mask_matches_rule(m, n, S, dedup, near):
+    """near: values a few f64 ulps apart, equal after rounding to f32 — the f32 pre-filter
+    passes those pairs and the exact f64 test has to decide them."""
     from everest_amd import ops
 
     rng = np.random.default_rng(n + S)
     O = np.round(rng.normal(size=(m, n, S)), 1)          # coarse grid: ties and duplicates
+    if near:
+        O = O + rng.integers(-2, 3, size=O.shape) * np.spacing(np.abs(O) + 1.0)
     O[:, 5, :] = O[:, 3, :]                              # exact duplicate points
     ref = np.full(m, -1.5)
     mask, counts = ops.pareto_mask(torch.tensor(O, device="cuda"), torch.tensor(ref, device="cuda"), dedup,
