@@ -102,6 +102,8 @@ _SIGS = {
     "evr_add_selection": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_box_decompose": ([c_int, c_int, c_int, c_void_p, c_longlong, c_longlong, c_longlong, c_void_p,
                            c_void_p, c_int, POINTER(c_void_p)], c_int),
+    "evr_box_decompose_approx": ([c_int, c_int, c_int, c_void_p, c_longlong, c_longlong, c_longlong, c_void_p,
+                                  c_void_p, c_double, c_int, POINTER(c_void_p)], c_int),
     "evr_cells_total": ([c_void_p], c_longlong),
     "evr_cells_copy": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "evr_cells_free": ([c_void_p], None),

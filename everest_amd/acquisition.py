@@ -97,13 +97,19 @@ def _single_cell(ref: torch.Tensor, S: int, m: int) -> ops.Cells:
                      hi=torch.full((S, m), math.inf, dtype=torch.float64, device=dev))
 
 
-def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None, num_threads=None):
-    """Exact non-dominated box decomposition above ref of every sample of O (m x P x S):
-    device kernel + kd ordering, or the native host partition beyond the device limits.
-    Returns (cells, path)."""
+def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None, num_threads=None,
+               alpha: float = 0.0):
+    """Non-dominated box decomposition above ref of every sample of O (m x P x S): exact
+    (device kernel + kd ordering, or the native host partition beyond the device limits), or
+    for alpha > 0 with m > 2 the approximate partition of [upstream]
+    NondominatedPartitioning(alpha) (host, explicit cells for the tiled scan; BoTorch's own
+    partition for that case is a host loop too).  Returns (cells, path)."""
     m, P, _ = O.shape
     dev = O.device
-    if box_device if box_device is not None else ops.box_device_supported(P, m):
+    approx = alpha > 0.0 and m > 2
+    if approx and box_device:
+        raise ValueError("the device box decomposition is exact only (alpha = 0)")
+    if not approx and (box_device if box_device is not None else ops.box_device_supported(P, m)):
         try:
             cells = ops.box_decompose_device(O, ref)
         except ops.BoxCapacityError as e:
@@ -120,15 +126,16 @@ def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None
                 warnings.warn(f"{int(cells.counts.max())} cells in one sample exceed the sparse kd scan's limit; "
                               "using the dense tiled scan (~10x slower)", RuntimeWarning)
             return cells, path
-    elif box_device is None:
+    elif not approx and box_device is None:
         warnings.warn(f"{P} points x {m} objectives exceed the device box decomposition's limits; "
                       "using the host partition", RuntimeWarning)
     mask, _ = ops.pareto_mask(O, ref, dedup=True)
     lo, hi, off = ops.box_decompose(O.cpu().numpy(), ref.cpu().numpy(), mask.cpu().numpy(),
-                                    num_threads or _host_threads(), layout="jis")
+                                    num_threads or _host_threads(), layout="jis", alpha=alpha if approx else 0.0)
     f64 = dict(dtype=torch.float64, device=dev)
     return ops.Cells(torch.as_tensor(off, dtype=torch.int32, device=dev), np.diff(off), m,
-                     lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64)), "host"
+                     lo=torch.as_tensor(lo, **f64), hi=torch.as_tensor(hi, **f64)), \
+        ("host-approx" if approx else "host")
 
 
 def _make_spec(m: int, obj_a, obj_b, objective, constraints) -> ops.GeneralSpec:
@@ -399,7 +406,7 @@ class QNEHVI(_BoxHviAcqf):
                  z_base_full: Optional[torch.Tensor] = None, z_new_full: Optional[torch.Tensor] = None,
                  num_threads: Optional[int] = None, box_device: Optional[bool] = None,
                  kd_scan: Optional[bool] = None, X_pending_raw: Optional[np.ndarray] = None,
-                 root: Optional[str] = None, objective=None, constraints=()):
+                 root: Optional[str] = None, objective=None, constraints=(), alpha: float = 0.0):
         dev = gp.device
         self.gp = gp
         self.dev = dev
@@ -544,7 +551,7 @@ class QNEHVI(_BoxHviAcqf):
             Ob = self._objective(Yb, mu_b)
             tm["baseline"] = _time.perf_counter() - t0 - tm.get("prune", 0.0)
             t1 = _time.perf_counter()
-            cells, self.box_path = _decompose(Ob, self.ref, box_device, kd_scan, num_threads)
+            cells, self.box_path = _decompose(Ob, self.ref, box_device, kd_scan, num_threads, alpha)
             tm["box_decomposition"] = _time.perf_counter() - t1
         else:  # no baseline: one cell [ref, inf)
             cells = _single_cell(self.ref, S_, spec.m_obj)
@@ -660,9 +667,10 @@ class QEHVI(_BoxHviAcqf):
     def __init__(self, gp: GPBatch, Y_part: np.ndarray, ref_point, obj_a, obj_b, S: int = 512,
                  sampler_seed: int = 0, z: Optional[torch.Tensor] = None, box_device: Optional[bool] = None,
                  kd_scan: Optional[bool] = None, num_threads: Optional[int] = None, objective=None,
-                 constraints=(), X_pending_raw: Optional[np.ndarray] = None):
+                 constraints=(), X_pending_raw: Optional[np.ndarray] = None, alpha: float = 0.0):
         """Y_part: points of the partition in objective space (m_obj columns); pending
-        points ([upstream] concatenate_pending_points) join every candidate's joint batch."""
+        points ([upstream] concatenate_pending_points) join every candidate's joint batch;
+        alpha > 0: [upstream] NondominatedPartitioning(alpha) instead of the exact partition."""
         dev = gp.device
         self.gp, self.dev = gp, dev
         m, n = gp.B, gp.n
@@ -681,7 +689,7 @@ class QEHVI(_BoxHviAcqf):
         S_ = self.S
         if Y_part.shape[0] > 0:
             O = torch.as_tensor(np.ascontiguousarray(Y_part.T), **f64)[:, :, None].expand(mo, Y_part.shape[0], S_)
-            cells, self.box_path = _decompose(O.contiguous(), self.ref, box_device, kd_scan, num_threads)
+            cells, self.box_path = _decompose(O.contiguous(), self.ref, box_device, kd_scan, num_threads, alpha)
         else:
             cells, self.box_path = _single_cell(self.ref, S_, mo), "none"
         self.cells = cells

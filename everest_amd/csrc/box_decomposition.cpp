@@ -1,5 +1,5 @@
-// Host-side exact box decomposition of the non-dominated region, one MC sample per task,
-// parallel over samples with std::thread.
+// Host-side box decomposition of the non-dominated region (exact, or BoTorch's approximate
+// partition for alpha > 0), one MC sample per task, parallel over samples with std::thread.
 //
 // Restates [upstream] BoTorch FastNondominatedPartitioning (alpha = 0, used by BoFire's
 // qNEHVI, bofire/strategies/predictives/qnehvi.py:50): local upper bounds U(N) of the
@@ -94,8 +94,100 @@ void update_lub(LUB& L, const double* z, std::vector<size_t>& A, std::vector<dou
   L.Z.insert(L.Z.end(), newZ.begin(), newZ.end());
 }
 
+// Approximate partition (alpha > 0, m > 2): [upstream] BoTorch NondominatedPartitioning.
+// _partition_space, the binary partitioning of Couckuyt, Deschrijver & Dhaene (2014), in the
+// minimisation space z = -g.  Coordinates are indices into the augmented front sorted per
+// objective: 0 = the ideal point (per-objective minimum of the front), 1..P = the front in
+// ascending (stable) order, P+1 = the reference point.  A cell [l, u] (index pairs) is
+//   accepted  if its upper corner is not dominated: every front point p has some j with
+//             value(u)_j <= p_j;
+//   split     if only its lower corner passes that test (the cell straddles the front), it is
+//             wider than one index step in some objective and its volume exceeds alpha times
+//             the volume between the ideal and reference points: along the objective of the
+//             largest index span, the upper half loses round-half-even(span / 2) steps and the
+//             lower half gains the rest;
+//   dropped   otherwise (dominated, or straddling but too small: the approximation).
+// Accepted cells are reported with index 0 mapped to -inf (upstream get_hypercell_bounds), so
+// in maximisation space a cell touching the ideal side is unbounded above.
+void approx_cells(int m, const std::vector<double>& Zf, int P, const double* Rn, double alpha,
+                  std::vector<double>& lo_tmp, std::vector<double>& hi_tmp) {
+  const double inf = std::numeric_limits<double>::infinity();
+  // aug[j][k]: k-th smallest augmented value of objective j (k = 0..P+1)
+  std::vector<std::vector<double>> aug(m, std::vector<double>(P + 2));
+  std::vector<int> ord(P);
+  double total = 1.0;
+  for (int j = 0; j < m; ++j) {
+    for (int i = 0; i < P; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return Zf[a * m + j] < Zf[b * m + j]; });
+    for (int k = 0; k < P; ++k) aug[j][k + 1] = Zf[ord[k] * m + j];
+    aug[j][0] = P ? aug[j][1] : Rn[j];
+    aug[j][P + 1] = Rn[j];
+    total *= Rn[j] - aug[j][0];
+  }
+  auto undominated = [&](const std::vector<int>& c) {   // c: m indices
+    for (int i = 0; i < P; ++i) {
+      bool some = false;
+      for (int j = 0; j < m && !some; ++j) some = aug[j][c[j]] <= Zf[i * m + j];
+      if (!some) return false;
+    }
+    return true;
+  };
+  auto emit = [&](const std::vector<int>& l, const std::vector<int>& u) {
+    bool ok = true;
+    const size_t b = lo_tmp.size();
+    for (int j = 0; j < m; ++j) {
+      const double zl = l[j] == 0 ? -inf : aug[j][l[j]], zu = aug[j][u[j]];
+      lo_tmp.push_back(-zu);
+      hi_tmp.push_back(-zl);
+      ok &= zu > zl;
+    }
+    if (!ok) {   // empty cell (tied front values): no volume
+      lo_tmp.resize(b);
+      hi_tmp.resize(b);
+    }
+  };
+  std::vector<std::vector<int>> stack;   // each: 2m indices (lower, upper)
+  std::vector<int> cell(2 * m);
+  for (int j = 0; j < m; ++j) {
+    cell[j] = 0;
+    cell[m + j] = P + 1;
+  }
+  stack.push_back(cell);
+  std::vector<int> l(m), u(m);
+  while (!stack.empty()) {
+    cell = stack.back();
+    stack.pop_back();
+    for (int j = 0; j < m; ++j) {
+      l[j] = cell[j];
+      u[j] = cell[m + j];
+    }
+    if (P == 0 || undominated(u)) {
+      emit(l, u);
+      continue;
+    }
+    if (!undominated(l)) continue;
+    int longest = 0, span = -1;
+    double vol = 1.0;
+    for (int j = 0; j < m; ++j) {
+      const int dj = u[j] - l[j];
+      if (dj > span) {   // first maximum, as torch.max
+        span = dj;
+        longest = j;
+      }
+      vol *= aug[j][u[j]] - aug[j][l[j]];
+    }
+    if (span <= 1 || !(vol / total > alpha)) continue;
+    const int h1 = (int)std::nearbyint(span / 2.0), h2 = span - h1;
+    std::vector<int> c1 = cell, c2 = cell;
+    c1[m + longest] -= h1;
+    c2[longest] += h2;
+    stack.push_back(std::move(c1));
+    stack.push_back(std::move(c2));
+  }
+}
+
 void decompose_one(int n, int m, const double* obj, long long si, long long sj, const unsigned char* mask,
-                   const double* ref, std::vector<double>& lo_out, std::vector<double>& hi_out) {
+                   const double* ref, double alpha, std::vector<double>& lo_out, std::vector<double>& hi_out) {
   // candidate points: masked & better than ref
   std::vector<int> cand;
   cand.reserve(n);
@@ -125,10 +217,17 @@ void decompose_one(int n, int m, const double* obj, long long si, long long sj, 
     }
     if (nd) pts.push_back(i);
   }
-  LUB L;
-  L.m = m;
   std::vector<double> R(m);
   for (int j = 0; j < m; ++j) R[j] = -ref[j];
+  std::vector<double> lo_tmp, hi_tmp;
+  if (alpha > 0.0 && m > 2) {
+    std::vector<double> Zf(pts.size() * m);
+    for (size_t a = 0; a < pts.size(); ++a)
+      for (int j = 0; j < m; ++j) Zf[a * m + j] = -obj[pts[a] * si + j * sj];
+    approx_cells(m, Zf, (int)pts.size(), R.data(), alpha, lo_tmp, hi_tmp);
+  } else {
+  LUB L;
+  L.m = m;
   init_lub(L, R);
   std::vector<double> nU, nZ, z(m);
   std::vector<size_t> A;
@@ -137,7 +236,6 @@ void decompose_one(int n, int m, const double* obj, long long si, long long sj, 
     update_lub(L, z.data(), A, nU, nZ);
   }
   const size_t K = L.K();
-  std::vector<double> lo_tmp, hi_tmp;
   lo_tmp.reserve(K * m);
   hi_tmp.reserve(K * m);
   std::vector<double> lw(m), up(m);
@@ -155,6 +253,7 @@ void decompose_one(int n, int m, const double* obj, long long si, long long sj, 
     if (!ok) continue;
     lo_tmp.insert(lo_tmp.end(), lw.begin(), lw.end());
     hi_tmp.insert(hi_tmp.end(), up.begin(), up.end());
+  }
   }
   // Cells sorted by their first lower bound (ties: remaining coordinates) so that a device
   // thread's neighbouring cells share a tight lower envelope (tile skip test in hvi.hip).
@@ -182,7 +281,13 @@ extern "C" {
 
 int evr_box_decompose(int S, int n, int m, const double* obj, long long ss, long long si, long long sj,
                       const unsigned char* mask, const double* ref, int num_threads, evr_cells** out) {
-  if (!out || !obj || !ref || S < 1 || n < 0 || m < 1) {
+  return evr_box_decompose_approx(S, n, m, obj, ss, si, sj, mask, ref, 0.0, num_threads, out);
+}
+
+int evr_box_decompose_approx(int S, int n, int m, const double* obj, long long ss, long long si, long long sj,
+                             const unsigned char* mask, const double* ref, double alpha, int num_threads,
+                             evr_cells** out) {
+  if (!out || !obj || !ref || S < 1 || n < 0 || m < 1 || !(alpha >= 0.0 && alpha < std::numeric_limits<double>::infinity())) {
     evr::set_error("evr_box_decompose: bad arguments");
     return 2;
   }
@@ -198,7 +303,7 @@ int evr_box_decompose(int S, int n, int m, const double* obj, long long ss, long
     for (;;) {
       const int s = next.fetch_add(1);
       if (s >= S) break;
-      decompose_one(n, m, obj + (size_t)s * ss, si, sj, mask ? mask + (size_t)s * n : nullptr, ref, c->lo[s],
+      decompose_one(n, m, obj + (size_t)s * ss, si, sj, mask ? mask + (size_t)s * n : nullptr, ref, alpha, c->lo[s],
                     c->hi[s]);
     }
   };

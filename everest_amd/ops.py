@@ -857,9 +857,10 @@ def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[
 
 
 def box_decompose(obj: np.ndarray, ref: np.ndarray, mask: Optional[np.ndarray] = None, num_threads: int = 0,
-                  layout: str = "jis"):
+                  layout: str = "jis", alpha: float = 0.0):
     """Host box decomposition.  obj: float64 numpy array, layout 'jis' (m x n x S) or 'sij'
-    (S x n x m).  Returns (lo [C x m], hi [C x m], off [S+1]) numpy arrays."""
+    (S x n x m).  alpha > 0 (m > 2): the approximate partition of [upstream]
+    NondominatedPartitioning(alpha).  Returns (lo [C x m], hi [C x m], off [S+1]) numpy arrays."""
     lib = _native.load()
     obj = np.ascontiguousarray(obj, dtype=np.float64)
     if layout == "jis":
@@ -873,9 +874,10 @@ def box_decompose(obj: np.ndarray, ref: np.ndarray, mask: Optional[np.ndarray] =
     ref = np.ascontiguousarray(ref, dtype=np.float64)
     mk = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
     handle = ctypes.c_void_p()
-    _native.check(lib.evr_box_decompose(S, n, m, obj.ctypes.data, ss, si, sj,
-                                        None if mk is None else mk.ctypes.data, ref.ctypes.data, int(num_threads),
-                                        ctypes.byref(handle)), "evr_box_decompose")
+    _native.check(lib.evr_box_decompose_approx(S, n, m, obj.ctypes.data, ss, si, sj,
+                                               None if mk is None else mk.ctypes.data, ref.ctypes.data,
+                                               float(alpha), int(num_threads), ctypes.byref(handle)),
+                  "evr_box_decompose_approx")
     try:
         total = lib.evr_cells_total(handle)
         lo = np.empty((total, m), dtype=np.float64)

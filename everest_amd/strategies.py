@@ -522,8 +522,6 @@ class QnehviStrategy(QehviStrategy):
         """bofire/strategies/predictives/qnehvi.py:23-53."""
         assert self.experiments is not None, "No experiments available."
         X_train, X_pending = self.get_acqf_input_tensors()
-        if self.alpha != 0.0:
-            raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
         objectives, constraints = self._objective_spec()
         ref = self.get_adjusted_refpoint()
         # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed
@@ -531,7 +529,7 @@ class QnehviStrategy(QehviStrategy):
         sampler_seed = self._draw_seed()
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, None, None, S=self.num_sobol_samples,
                       sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending,
-                      objective=objectives, constraints=constraints)
+                      objective=objectives, constraints=constraints, alpha=self.alpha)
         self.last_acqf = acqf
         return [acqf]
 
@@ -554,13 +552,12 @@ class MoboStrategy(_MultiobjectiveMixin, BotorchStrategy):
         assert self.is_fitted is True, "Model not trained."
         assert self.experiments is not None, "No experiments available."
         af = self.acquisition_function
-        if getattr(af, "alpha", 0.0) != 0.0:
-            raise NotImplementedError("approximate partitioning (alpha > 0) is out of scope")
         X_train, X_pending = self.get_acqf_input_tensors()
         objectives, constraints = self._objective_spec()
         ref = np.asarray(self.get_adjusted_refpoint(), dtype=np.float64)
         S = int(af.n_mc_samples)
-        kw = dict(objective=objectives, constraints=constraints)
+        # mobo.py:83 passes the data model's alpha to get_acquisition_function
+        kw = dict(objective=objectives, constraints=constraints, alpha=float(af.alpha))
         if isinstance(af, (dm.qEHVI, dm.qLogEHVI)):
             # [upstream] get_acquisition_function: partition of objective(Y) over the feasible rows
             spec = ops.GeneralSpec(len(self.model.output_keys), objectives, constraints)

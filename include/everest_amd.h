@@ -405,6 +405,13 @@ typedef struct evr_cells evr_cells;
 int evr_box_decompose(int S, int n, int m, const double* obj, long long ss, long long si,
                       long long sj, const unsigned char* mask, const double* ref, int num_threads,
                       evr_cells** out);
+/* alpha > 0 (finite) with m > 2: the approximate partition of [upstream] BoTorch
+ * NondominatedPartitioning(alpha) (bofire/strategies/predictives/qnehvi.py:50 passes the data
+ * model's alpha, bofire/data_models/strategies/predictives/qnehvi.py:19); alpha = 0 or m <= 2
+ * is the exact partition above. */
+int evr_box_decompose_approx(int S, int n, int m, const double* obj, long long ss, long long si,
+                             long long sj, const unsigned char* mask, const double* ref, double alpha,
+                             int num_threads, evr_cells** out);
 long long evr_cells_total(const evr_cells* c);
 int evr_cells_copy(const evr_cells* c, double* lo, double* hi, int* off);
 void evr_cells_free(evr_cells* c);

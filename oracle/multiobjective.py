@@ -105,6 +105,60 @@ def nondominated_cells(pareto_Y: torch.Tensor, ref: torch.Tensor) -> torch.Tenso
     return torch.stack([lower[keep], upper[keep]], 0)
 
 
+def approximate_cells(pareto_Y: torch.Tensor, ref: torch.Tensor, alpha: float) -> torch.Tensor:
+    """[upstream] NondominatedPartitioning(ref, Y, alpha)._partition_space +
+    get_hypercell_bounds for m > 2 (BoFire passes alpha at
+    bofire/strategies/predictives/qnehvi.py:50 and mobo.py:83): binary partitioning over
+    indices of the augmented front, minimisation frame z = -y.  Index 0 is the ideal point
+    (per-objective minimum of the front; -inf in the reported bounds), 1..P the front sorted
+    per objective (stable), P+1 the reference point.  A cell whose upper corner no front point
+    dominates is kept; one whose lower corner passes is split along its widest index span
+    (upper half minus round(span / 2), lower half plus the rest) while some span exceeds 1 and
+    its volume / (ref - ideal volume) exceeds alpha, else dropped.  Returns 2 x C x m
+    (maximisation lower, upper) in stack-pop order.  Parity unpinned: BoTorch is not
+    available here; the ideal-point volume normaliser is this restatement's reading."""
+    m = ref.shape[0]
+    Z = -pareto_Y
+    P = Z.shape[0]
+    Rn = -ref
+    idx = torch.argsort(Z, dim=0, stable=True)
+    aug = torch.empty(P + 2, m, **TK)
+    for j in range(m):
+        aug[1:P + 1, j] = Z[idx[:, j], j]
+    aug[0] = aug[1] if P else Rn
+    aug[P + 1] = Rn
+    total = float((Rn - aug[0]).prod())
+    ar = torch.arange(m)
+    out = []
+    stack = [torch.stack([torch.zeros(m, dtype=torch.long), torch.full((m,), P + 1, dtype=torch.long)])]
+
+    def undominated(corner):
+        return bool((corner <= Z).any(dim=-1).all()) if P else True
+
+    while stack:
+        cell = stack.pop()
+        vals = aug[cell, ar]                       # 2 x m
+        if undominated(vals[1]):
+            lo_z = vals[0].clone()
+            lo_z[cell[0] == 0] = -float("inf")
+            out.append(torch.stack([-vals[1], -lo_z]))
+        elif undominated(vals[0]):
+            dist = cell[1] - cell[0]
+            vol = float((vals[1] - vals[0]).prod())
+            if bool((dist > 1).any()) and vol / total > alpha:
+                span, j = int(dist.max()), int(torch.argmax(dist))
+                h1 = int(round(span / 2.0))
+                for b, delta in ((1, -h1), (0, span - h1)):
+                    c = cell.clone()
+                    c[b, j] += delta
+                    stack.append(c)
+    if not out:
+        return torch.empty(2, 0, m, **TK)
+    cells = torch.stack(out, 1)
+    keep = (cells[1] > cells[0]).all(-1)
+    return cells[:, keep]
+
+
 def hvi_from_cells(y: torch.Tensor, cells: torch.Tensor) -> torch.Tensor:
     """q=1 HVI of points y (... x m) w.r.t. cells (2 x C x m)."""
     lo, hi = cells[0], cells[1]

@@ -29,7 +29,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from .gp import GPState, TK, kernel_matrix, psd_safe_cholesky
-from .multiobjective import is_non_dominated, nondominated_cells, pareto_above_ref
+from .multiobjective import approximate_cells, is_non_dominated, nondominated_cells, pareto_above_ref
 
 
 def draw_sobol_normal_samples(d: int, n: int, seed: int) -> torch.Tensor:
@@ -158,11 +158,13 @@ class QNEHVI:
 
     def __init__(self, models: List[GPState], Xb_n: torch.Tensor, objective: Objective,
                  ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor, cells=None,
-                 constraints: Optional[OutputConstraints] = None):
+                 constraints: Optional[OutputConstraints] = None, alpha: float = 0.0):
         """``cells`` (list of 2 x C x m per sample) may be injected to time the forward
         pass alone (bench.py cpu_baseline); parity tests always build their own.
         ``constraints``: baseline samples infeasible under them leave the Pareto sets (set to
-        ref), candidate areas are weighted by the smoothed feasibility."""
+        ref), candidate areas are weighted by the smoothed feasibility.
+        ``alpha`` > 0 (m > 2): [upstream] NondominatedPartitioning(alpha)'s approximate cells
+        (bofire/strategies/predictives/qnehvi.py:50)."""
         self.models = models
         self.Xb = Xb_n
         self.obj = objective
@@ -179,8 +181,9 @@ class QNEHVI:
         if cells is not None:
             self.cells = cells
         else:
-            self.cells = [nondominated_cells(pareto_above_ref(self.base_obj[s], ref), ref)
-                          for s in range(z_base.shape[0])]
+            part = ((lambda P: approximate_cells(P, ref, alpha)) if alpha > 0 and ref.shape[0] > 2
+                    else (lambda P: nondominated_cells(P, ref)))
+            self.cells = [part(pareto_above_ref(self.base_obj[s], ref)) for s in range(z_base.shape[0])]
 
     def samples(self, Xn: torch.Tensor) -> torch.Tensor:
         """Xn: b x q x d normalized -> samples S x b x q x m (sample_cached_cholesky)."""

@@ -51,7 +51,7 @@ def test_mll_value_and_grad(kind):
     assert np.allclose(g, t.grad.numpy(), rtol=1e-7, atol=1e-9)
 
 
-def _matched_qnehvi(n, d, m, S, seed, prune, nprune=64):
+def _matched_qnehvi(n, d, m, S, seed, prune, nprune=64, alpha=0.0):
     from everest_amd.acquisition import QNEHVI
 
     X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=seed)
@@ -68,9 +68,9 @@ def _matched_qnehvi(n, d, m, S, seed, prune, nprune=64):
     nb = idx.shape[0]
     zb = oq.base_samples(S, nb, m, 7)
     zn = oq.base_samples(S, nb + 1, m, 7)
-    orc = oq.QNEHVI(ost, Xn[idx], objective, torch.tensor(ref), zb, zn[:, nb:nb + 1, :])
+    orc = oq.QNEHVI(ost, Xn[idx], objective, torch.tensor(ref), zb, zn[:, nb:nb + 1, :], alpha=alpha)
     dq = QNEHVI(gp, X, X, ref, obj_a, obj_b, S=S, prune_baseline=prune, z_prune=zp, z_base_full=zb,
-                z_new_full=zn, prune_samples=nprune)
+                z_new_full=zn, prune_samples=nprune, alpha=alpha)
     return X, lo, hi, orc, dq, idx
 
 
@@ -96,6 +96,26 @@ def test_qnehvi_forward_backward_parity(n, d, m, S, prune):
     assert torch.allclose(dX.cpu()[1:], xt.grad[1:], rtol=1e-5, atol=1e-7)
     # total cells equal (same partition algorithm) and per-sample HVI of the device cells
     assert dq.stats.total_cells == sum(c.shape[1] for c in orc.cells)
+
+
+@pytest.mark.parametrize("n,d,m,alpha", [(40, 4, 3, 0.01), (50, 5, 4, 0.001)])
+def test_qnehvi_approximate_partition_parity(n, d, m, alpha):
+    """alpha > 0 ([upstream] NondominatedPartitioning(alpha), bofire qnehvi.py:50): the host
+    approximate cells through the tiled device scan vs the oracle on its own approximate cells;
+    the approximation can only lower the value."""
+    X, lo, hi, orc, dq, idx = _matched_qnehvi(n, d, m, 16, seed=n + 1, prune=True, alpha=alpha)
+    assert dq.box_path == "host-approx"
+    assert dq.stats.total_cells == sum(c.shape[1] for c in orc.cells)
+    rng = np.random.default_rng(6)
+    Xc = lo + (hi - lo) * rng.uniform(size=(29, d))
+    acq, dX = dq.forward_backward(torch.tensor(Xc, device="cuda"))
+    xt = torch.tensor(Xc, requires_grad=True)
+    r = orc.forward(((xt - torch.tensor(lo)) / torch.tensor(hi - lo)).unsqueeze(1))
+    r.sum().backward()
+    assert torch.allclose(acq.cpu(), r.detach(), rtol=1e-6, atol=1e-9)
+    assert torch.allclose(dX.cpu(), xt.grad, rtol=1e-5, atol=1e-7)
+    _, _, _, _, dq0, _ = _matched_qnehvi(n, d, m, 16, seed=n + 1, prune=True)
+    assert (acq <= dq0.forward(torch.tensor(Xc, device="cuda")) + 1e-12).all()
 
 
 def test_qnehvi_large_batch_consistency():

@@ -46,6 +46,24 @@ def test_qnehvi_tell_ask_dtlz2(use_ref_point):
     assert st.raw_evals == 256 and st.opt_evals > 0
 
 
+@pytest.mark.parametrize("mobo", [False, True])
+def test_qnehvi_ask_approximate_partition(mobo):
+    """QnehviStrategy(alpha=...) / MoboStrategy(qNEHVI(alpha=...)) at m = 3: the acquisition
+    takes the approximate partition (bofire qnehvi.py:50, mobo.py:83) and ask() completes."""
+    bench, exps = _dtlz2_experiments(n=14, m=3, seed=5)
+    kw = dict(domain=bench.domain, ref_point=bench.ref_point, seed=4)
+    if mobo:
+        dmod = dm.MoboStrategy(acquisition_function=dm.qNEHVI(alpha=0.02, n_mc_samples=64), **kw)
+    else:
+        dmod = dm.QnehviStrategy(alpha=0.02, num_sobol_samples=64, num_raw_samples=128, num_restarts=2, **kw)
+    s = strategies.map(dmod)
+    s.tell(exps)
+    cand = s.ask(1)
+    assert len(cand) == 1 and s.last_acqf.box_path == "host-approx"
+    for k in bench.domain.inputs.get_keys():
+        assert 0.0 <= cand[k].iloc[0] <= 1.0
+
+
 def test_qnehvi_ask_add_pending():
     """ask(add_pending=True) stores the candidate; the next ask() folds it into the baseline
     (X_pending, bofire/strategies/predictives/qnehvi.py:47), which removes its improvement."""

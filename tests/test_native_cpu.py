@@ -127,3 +127,55 @@ def test_torch_operator_library_registers_ops():
     x = torch.zeros(3, 2, dtype=torch.float64)
     with pytest.raises((RuntimeError, NotImplementedError)):
         ns.kernel_matrix(x, x, torch.ones(2, dtype=torch.float64), 0)
+
+
+def _sorted_cells(lo, hi):
+    rows = np.concatenate([lo, hi], 1)
+    return rows[np.lexsort(rows.T[::-1])]
+
+
+@pytest.mark.parametrize("m,n,alpha", [(3, 25, 1e-3), (3, 40, 0.05), (4, 30, 0.01), (5, 20, 0.2)])
+def test_host_approximate_partition_matches_oracle(m, n, alpha):
+    """alpha > 0: evr_box_decompose_approx vs the oracle's restatement of [upstream]
+    NondominatedPartitioning(alpha) — the same cell set, bit for bit; the approximation only
+    drops volume (HVI <= exact) and alpha -> 0 recovers the exact partition."""
+    from everest_amd import ops
+    from oracle.multiobjective import approximate_cells, hvi_from_cells, nondominated_cells, pareto_above_ref
+
+    rng = np.random.default_rng(7 * m + n)
+    S = 3
+    obj = -rng.uniform(size=(S, n, m))
+    obj[:, 4] = obj[:, 1]
+    ref = -1.1 * np.ones(m)
+    lo, hi, off = ops.box_decompose(obj, ref, None, 2, layout="sij", alpha=alpha)
+    lo0, hi0, off0 = ops.box_decompose(obj, ref, None, 2, layout="sij")
+    y = torch.tensor(-rng.uniform(size=(64, m)) * 0.9)
+    for s in range(S):
+        pf = pareto_above_ref(torch.tensor(obj[s]), torch.tensor(ref))
+        c = approximate_cells(pf, torch.tensor(ref), alpha)
+        a, b = off[s], off[s + 1]
+        assert b - a == c.shape[1]
+        assert np.array_equal(_sorted_cells(lo[a:b], hi[a:b]), _sorted_cells(c[0].numpy(), c[1].numpy()))
+        mine = torch.stack([torch.tensor(lo[a:b]), torch.tensor(hi[a:b])])
+        exact = torch.stack([torch.tensor(lo0[off0[s]:off0[s + 1]]), torch.tensor(hi0[off0[s]:off0[s + 1]])])
+        h, h0 = hvi_from_cells(y, mine), hvi_from_cells(y, exact)
+        assert (h <= h0 + 1e-14).all()
+        c_full = approximate_cells(pf, torch.tensor(ref), 0.0)       # no approximation: exact region
+        assert torch.allclose(hvi_from_cells(y, c_full), hvi_from_cells(y, nondominated_cells(pf, torch.tensor(ref))),
+                              atol=1e-13, rtol=0)
+
+
+def test_approximate_partition_m2_is_exact_and_alpha_bounds():
+    """m = 2 takes the exact partition whatever alpha ([upstream] _partition_space_2d);
+    a negative or non-finite alpha is refused."""
+    from everest_amd import _native, ops
+
+    rng = np.random.default_rng(3)
+    obj = -rng.uniform(size=(2, 20, 2))
+    ref = -1.1 * np.ones(2)
+    a = ops.box_decompose(obj, ref, None, 1, layout="sij", alpha=0.3)
+    b = ops.box_decompose(obj, ref, None, 1, layout="sij")
+    assert all(np.array_equal(x, z) for x, z in zip(a, b))
+    with pytest.raises(RuntimeError, match="bad arguments"):
+        ops.box_decompose(obj, ref, None, 1, layout="sij", alpha=-0.1)
+    assert hasattr(_native.load(), "evr_box_decompose_approx")
