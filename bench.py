@@ -589,6 +589,21 @@ def main():
                          "box_decomposition": acqf.box_path, "setup_s": {"gp_fit": round(t_fit, 3),
                                                                          "qnehvi_build": round(t_build, 3)}}
 
+    qlog = None
+    if not args.no_eval_pass and rank == 0:
+        # ---- qLogNEHVI (MoboStrategy's default acquisition) on the same fitted GPs: the dense
+        # log-space scan (hvi_log.hip) over every cell, forward + backward, HIP events
+        from everest_amd.acquisition import QLogNEHVI
+
+        qa = QLogNEHVI(gp, X, X, -1.1 * np.ones(args.m), -np.ones(args.m), np.zeros(args.m), S=args.S,
+                       sampler_seed=1234, prune_baseline=True, prune_seed=4321)
+        qlog = {"note": "qLogNEHVI forward + backward (dense fat-smoothed log scan over all cells), same GPs and "
+                        "seeds as eval_pass; device time between HIP events incl. any host syncs",
+                "cells_total": qa.stats.total_cells, "box_decomposition": qa.box_path}
+        for bb, XX in ((args.b, Xc), (b_r, Xr)):
+            qlog[f"b{bb}_ms"] = round(_event_ms(lambda: qa.forward_backward(XX), reps=10), 4)
+        del qa
+
     if rank == 0:
         sum_cells_r = acqf_ask.stats.total_cells
         kernels_r = _rooflines(kt_r, _work_table(acqf_ask, b_r, args.S, args.m, args.d, sum_cells_r))
@@ -663,6 +678,7 @@ def main():
                     "phases_last_ask": phases, "n_base": acqf_ask.nb, "cells_total": sum_cells_r,
                     "box_decomposition": acqf_ask.box_path},
             "eval_pass": eval_pass,
+            "qlognehvi": qlog,
             "linalg": cholesky_figures(device),
             "cpu_baseline": cpu,
             "gp_posterior_ms": round(t_post, 4),
