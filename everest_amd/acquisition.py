@@ -759,6 +759,30 @@ class QLogEHVI(QEHVI):
         self._use_log_scan(tau_relu, tau_max)
 
 
+class QEIJoint(QEHVI):
+    """Device qEI over joint batches — q > 1 candidates and/or pending points ([upstream]
+    qExpectedImprovement with X_pending, bofire/strategies/predictives/sobo.py:51-90;
+    optimize_acqf(q=...) at botorch.py:385).  With one objective, the region above any
+    reference r < best_f not dominated by best_f is the single cell [best_f, inf), and the
+    hypervolume improvement of q samples over it is max_i (g(y_i) - best_f)_+ — exactly qEI's
+    integrand.  So the joint posterior of the q (+ pending) points, its psd_safe q x q root,
+    the subset scan and their analytic backward are the general qEHVI kernels at m = 1
+    (``qg_*``), with best_f = max over X_train of g(posterior mean) as in QEI and the
+    S x (q + n_pending) Sobol-normal draw of the sampler seed."""
+
+    def __init__(self, gp: GPBatch, X_train_raw: np.ndarray, obj_a: float, obj_b: float, S: int = 512,
+                 seed: int = 0, X_pending_raw: Optional[np.ndarray] = None):
+        if gp.B != 1:
+            raise ValueError("QEIJoint takes a single-output model")
+        Xt = torch.as_tensor(np.asarray(X_train_raw, dtype=np.float64), device=gp.device)
+        mean, _ = gp.posterior(Xt)
+        best_f = float((float(obj_a) * mean[0] + float(obj_b)).max().item())
+        super().__init__(gp, np.array([[best_f]]), [best_f - 1.0], [float(obj_a)], [float(obj_b)], S=S,
+                         sampler_seed=seed, box_device=False, X_pending_raw=X_pending_raw)
+        self.best_f = best_f
+        self.a, self.b = float(obj_a), float(obj_b)
+
+
 class QEI:
     """Device qEI (q = 1, one output) — [upstream] qExpectedImprovement as built by
     ``get_acquisition_function("qEI", ...)`` from SoboStrategy._get_acqfs

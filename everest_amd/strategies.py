@@ -19,7 +19,7 @@ import torch
 
 from . import data_models as dm
 from . import ops
-from .acquisition import QEHVI, QEI, QLogEHVI, QLogNEHVI, QNEHVI
+from .acquisition import QEHVI, QEI, QEIJoint, QLogEHVI, QLogNEHVI, QNEHVI
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
 from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
 from .surrogates import BotorchSurrogates, device
@@ -325,7 +325,7 @@ class BotorchStrategy(PredictiveStrategy):
     def calc_acquisition(self, candidates: pd.DataFrame, combined: bool = False) -> np.ndarray:
         """bofire/strategies/predictives/botorch.py:196-225: one value per candidate, or with
         ``combined`` one joint value of the whole set as a q-batch."""
-        acqf = self._get_acqfs(1)[0]
+        acqf = self._get_acqfs(len(candidates) if combined else 1)[0]
         X = torch.as_tensor(self._transform(candidates), dtype=torch.float64, device=self.model.device)
         if combined:
             X = X.unsqueeze(0)
@@ -595,10 +595,12 @@ class SoboStrategy(BotorchStrategy):
             raise NotImplementedError("single-output SOBO only")
         a, b = target.objective.affine()
         X_train, X_pending = self.get_acqf_input_tensors()
-        if X_pending is not None:
-            raise NotImplementedError("pending candidates are not yet supported on the device path")
         seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
-        return [QEI(self.model, X_train, a, b, S=int(self.acquisition_function.n_mc_samples), seed=seed)]
+        S = int(self.acquisition_function.n_mc_samples)
+        if X_pending is None and n == 1:
+            return [QEI(self.model, X_train, a, b, S=S, seed=seed)]
+        # joint batches (q > 1) and pending points (sobo.py:72 passes X_pending)
+        return [QEIJoint(self.model, X_train, a, b, S=S, seed=seed, X_pending_raw=X_pending)]
 
 
 STRATEGY_MAP = {

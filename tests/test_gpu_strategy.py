@@ -172,6 +172,62 @@ def test_sobo_qei_matern_parity():
     assert torch.allclose(dX.cpu(), x.grad, rtol=1e-6, atol=1e-9)
 
 
+def _sobo_qei_strategy(seed=11):
+    bench, exps = _dtlz2_experiments(n=25, dim=4, m=2, seed=seed)
+    dom = dm.Domain(inputs=bench.domain.inputs,
+                    outputs=dm.Outputs(features=[dm.ContinuousOutput(key="f_0",
+                                                                      objective=dm.MinimizeObjective(w=1.0))]))
+    spec = dm.SingleTaskGPSurrogate(inputs=dom.inputs, outputs=dom.outputs, kernel=dm.MaternKernel(nu=2.5))
+    s = strategies.map(dm.SoboStrategy(domain=dom, acquisition_function=dm.qEI(n_mc_samples=128), seed=3,
+                                       surrogate_specs=dm.BotorchSurrogates(surrogates=[spec]),
+                                       num_raw_samples=64, num_restarts=2))
+    s.tell(exps[dom.inputs.get_keys() + ["f_0", "valid_f_0"]])
+    st = s.surrogates.surrogates[0].state
+    o = ogp.GPState(X=torch.tensor(st["X"]), y=torch.tensor((st["y"] - st["y_mean"]) / st["y_std"]),
+                    lengthscale=torch.tensor(st["lengthscale"]), noise=st["noise"], constant=st["constant"],
+                    y_mean=st["y_mean"], y_std=st["y_std"], kind=ogp.MATERN25)
+    return s, dom, o
+
+
+@pytest.mark.parametrize("q,npend", [(3, 0), (1, 2), (2, 1)])
+def test_qei_joint_batch_parity(q, npend):
+    """qEI over joint batches (q > 1, pending points: sobo.py:51-90 with X_pending) through the
+    m = 1 general qEHVI kernels vs the oracle's joint-posterior qEI (psd_safe q x q root,
+    mean_s max_i (g - best_f)_+), values and gradients on the same base samples."""
+    from everest_amd.acquisition import QEI, QEIJoint
+    from oracle import qnehvi as oq
+
+    s, dom, o = _sobo_qei_strategy()
+    X_train, _ = s.get_acqf_input_tensors()
+    rng = np.random.default_rng(q * 10 + npend)
+    Xp = rng.uniform(size=(npend, 4)) if npend else None
+    acqf = QEIJoint(s.model, X_train, -1.0, 0.0, S=128, seed=9, X_pending_raw=Xp)
+    assert abs(acqf.best_f - QEI(s.model, X_train, -1.0, 0.0, S=8).best_f) == 0.0
+    qq = q + npend
+    z = acqf._zq(qq).reshape(128, qq).cpu()
+    Xc = rng.uniform(size=(12, q, 4))
+    x = torch.tensor(Xc, requires_grad=True)
+    xf = torch.cat([x, torch.tensor(Xp).unsqueeze(0).expand(12, npend, 4)], 1) if npend else x
+    ref = oq.qei([o], xf, acqf.best_f, z, a=-1.0, bconst=0.0)
+    ref.sum().backward()
+    acq, dX = acqf.forward_backward(torch.tensor(Xc, device="cuda"))
+    assert torch.allclose(acq.cpu(), ref.detach(), rtol=1e-6, atol=1e-10)
+    assert torch.allclose(dX.cpu().reshape(12, q, 4), x.grad, rtol=1e-5, atol=1e-8)
+
+
+def test_sobo_ask_joint_and_pending():
+    """SoboStrategy.ask(2) optimises one joint q = 2 batch; ask(add_pending=True) then folds the
+    pending candidate into the next qEI (which no longer raises)."""
+    s, dom, _ = _sobo_qei_strategy(seed=4)
+    c2 = s.ask(2)
+    assert len(c2) == 2
+    v = s.calc_acquisition(c2[dom.inputs.get_keys()], combined=True)
+    assert v.shape == (1,) and v[0] >= 0
+    c1 = s.ask(1, add_pending=True)
+    c1b = s.ask(1)
+    assert len(c1b) == 1 and not np.allclose(c1[dom.inputs.get_keys()].values, c1b[dom.inputs.get_keys()].values)
+
+
 def test_qnehvi_ask_joint_batch_and_combined_value():
     """ask(candidate_count=3): one joint q = 3 optimisation (optimize_acqf(q=...),
     bofire/strategies/predictives/botorch.py:385); calc_acquisition(combined=True) scores the
