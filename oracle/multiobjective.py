@@ -67,7 +67,9 @@ def compute_local_upper_bounds(U, Z, z):
     mask = torch.ones(m, dtype=torch.bool)
     for j in range(m):
         mask[j] = False
-        zmax = AZ[:, mask, j].max(dim=-1).values
+        # m = 1: no other defining points, the projection is always admissible
+        zmax = (AZ[:, mask, j].max(dim=-1).values if m > 1
+                else torch.full((A.shape[0],), -float("inf"), dtype=A.dtype))
         add = z[j] >= zmax
         if add.any():
             uj = A[add].clone()

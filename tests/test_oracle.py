@@ -165,3 +165,29 @@ def test_log_hvi_oracle_tends_to_log_qnehvi():
     far = torch.full((1, 1, 3), 1.0)
     lv = oq.QLogNEHVI(ost, Xn, obj, torch.tensor(ref), zb, zn).forward(far)
     assert torch.isfinite(lv).all()
+
+
+@pytest.mark.parametrize("q,npend", [(1, 0), (3, 0), (2, 2)])
+def test_qei_is_one_objective_qehvi_over_best_f_cell(q, npend):
+    """The identity QEIJoint rests on: with one objective, qEHVI over the partition of
+    {best_f} (a single cell [best_f, inf) above any ref < best_f) equals qEI with that best_f
+    on the same base samples, pending points included."""
+    X, Y, lo, hi, hyp = make_problem(n=20, d=3, m=1, seed=q + 3 * npend)
+    st = oracle_states(X, Y, lo, hi, hyp)
+    a, b0 = -1.0, 0.0
+    Xn = torch.tensor((X - lo) / (hi - lo))
+    mean, _ = ogp.posterior(st[0], Xn)
+    best_f = float((a * mean + b0).max())
+    qq = q + npend
+    z = oq.base_samples(64, qq, 1, 5)                                   # S x qq x 1
+    rng = np.random.default_rng(1)
+    Xp = torch.tensor(rng.uniform(size=(npend, 3))) if npend else None
+    f64 = dict(dtype=torch.float64)
+    qe = oq.QEHVI(st, torch.tensor([[best_f]], **f64), oq.Objective(torch.tensor([a], **f64), torch.tensor([b0], **f64)),
+                  torch.tensor([best_f - 1.0], **f64), z, X_pending=Xp)
+    Xc = torch.tensor(rng.uniform(size=(9, q, 3)))
+    v_hvi = qe.forward(Xc)
+    Xf = torch.cat([Xc, Xp.unsqueeze(0).expand(9, npend, 3)], 1) if npend else Xc
+    v_ei = oq.qei(st, Xf, best_f, z[..., 0], a=a, bconst=b0)
+    # inclusion-exclusion over the q-subsets cancels terms: equal up to rounding
+    assert torch.allclose(v_hvi, v_ei, rtol=1e-10, atol=1e-13)
