@@ -191,3 +191,14 @@ def test_qei_is_one_objective_qehvi_over_best_f_cell(q, npend):
     v_ei = oq.qei(st, Xf, best_f, z[..., 0], a=a, bconst=b0)
     # inclusion-exclusion over the q-subsets cancels terms: equal up to rounding
     assert torch.allclose(v_hvi, v_ei, rtol=1e-10, atol=1e-13)
+
+
+def test_log_fatplus_cutoff_is_exact():
+    """hvi_log.hip drops exp(x) / log1p(exp(x)) from log fatplus below x = -60: on a dense
+    grid to -1e8 both F = softplus(x) + 0.1 / (1 + x^2) and the derivative numerator
+    sigmoid(x) - 0.2 x / (1 + x^2)^2 round to the same doubles without the exp term."""
+    x = -np.concatenate([np.linspace(60.0, 745.0, 400001), np.geomspace(60.0, 1e8, 200001)])
+    e = np.exp(x)
+    c = 1.0 / (1.0 + x * x)
+    assert np.array_equal(np.log1p(e) + 0.1 * c, 0.0 + 0.1 * c)
+    assert np.array_equal(e / (1.0 + e) - 0.2 * x * c * c, 0.0 - 0.2 * x * c * c)
