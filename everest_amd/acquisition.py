@@ -198,8 +198,10 @@ class _BoxHviAcqf:
     @property
     def supports_plan(self) -> bool:
         """q = 1 candidates through the fused fast path (native plan / hipGraph): every
-        output carries one affine objective and there are no output constraints."""
-        return self.spec.affine_identity
+        output carries one affine objective, there are no output constraints, and no pending
+        points join the candidates' joint batch (qEHVI / qEI X_pending; qNEHVI folds its
+        pending points into the baseline, so its plan sees them)."""
+        return self.spec.affine_identity and self._pending_rows() is None
 
     def _init_general(self, spec: ops.GeneralSpec, cells, nk: int, nb_rows: int, no_h: bool = False):
         """States of the general evaluation (qnehvi_general.hip): model side over the m

@@ -250,7 +250,9 @@ __global__ __launch_bounds__(256) void pareto_f32_kernel(int S, int n, int npad,
                                                          const double* __restrict__ ref, int dedup,
                                                          unsigned char* __restrict__ mask, int* __restrict__ counts) {
   extern __shared__ double pts[];   // [SB][n][M] f64, then [SB][M][npad] f32
-  float* ptf = reinterpret_cast<float*>(pts + (size_t)SB * n * M);
+  // the f32 copy starts on a 16-byte boundary (float4 loads): round the f64 region up to
+  // an even number of doubles
+  float* ptf = reinterpret_cast<float*>(pts + (((size_t)SB * n * M + 1) & ~(size_t)1));
   const int s0 = blockIdx.x * SB, sb = min(SB, S - s0);
   const int tot = M * n * sb;
   for (int e = threadIdx.x; e < tot; e += 256) {
@@ -288,21 +290,22 @@ __global__ __launch_bounds__(256) void pareto_f32_kernel(int S, int n, int npad,
         va[j] = *reinterpret_cast<const float4*>(F + (size_t)j * npad + k0);
         vb[j] = *reinterpret_cast<const float4*>(F + (size_t)j * npad + k0 + 4);
       }
-      float mn[8];
-      mn[0] = va[0].x - yf[0]; mn[1] = va[0].y - yf[0]; mn[2] = va[0].z - yf[0]; mn[3] = va[0].w - yf[0];
-      mn[4] = vb[0].x - yf[0]; mn[5] = vb[0].y - yf[0]; mn[6] = vb[0].z - yf[0]; mn[7] = vb[0].w - yf[0];
+      // candidate bits: every objective >= in f32.  Direct compares (not the sign of a
+      // difference): f32 rounding is monotone, so v >= y in f64 implies f32(v) >= f32(y),
+      // infinities included; a NaN fails the compare here and in the exact test alike.
+      bool ge8[8];
 #pragma unroll
-      for (int j = 1; j < M; ++j) {
-        mn[0] = fminf(mn[0], va[j].x - yf[j]); mn[1] = fminf(mn[1], va[j].y - yf[j]);
-        mn[2] = fminf(mn[2], va[j].z - yf[j]); mn[3] = fminf(mn[3], va[j].w - yf[j]);
-        mn[4] = fminf(mn[4], vb[j].x - yf[j]); mn[5] = fminf(mn[5], vb[j].y - yf[j]);
-        mn[6] = fminf(mn[6], vb[j].z - yf[j]); mn[7] = fminf(mn[7], vb[j].w - yf[j]);
+      for (int u = 0; u < 8; ++u) ge8[u] = k0 + u != i && k0 + u < n;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        ge8[0] &= va[j].x >= yf[j]; ge8[1] &= va[j].y >= yf[j];
+        ge8[2] &= va[j].z >= yf[j]; ge8[3] &= va[j].w >= yf[j];
+        ge8[4] &= vb[j].x >= yf[j]; ge8[5] &= vb[j].y >= yf[j];
+        ge8[6] &= vb[j].z >= yf[j]; ge8[7] &= vb[j].w >= yf[j];
       }
-      // candidate bits: every objective >= in f32 (fminf drops NaN operands, so a NaN only
-      // sends the pair to the exact test, which rejects it)
       unsigned int cand = 0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) cand |= (unsigned int)(mn[u] >= 0.0f && k0 + u != i && k0 + u < n) << u;
+      for (int u = 0; u < 8; ++u) cand |= (unsigned int)ge8[u] << u;
       while (cand) {
         const int u = __builtin_ctz(cand);
         cand &= cand - 1;
@@ -484,7 +487,7 @@ int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const do
   constexpr size_t kLds2 = 78 * 1024;
   if (f32_filter && per2 <= kLds2) {
     const int SB = (int)std::min<size_t>(4, kLds2 / per2);
-    const size_t bytes = per2 * SB;
+    const size_t bytes = (((size_t)SB * n * m + 1) & ~(size_t)1) * sizeof(double) + (size_t)SB * npad * m * sizeof(float);
 #define L(MM)                                                                                            \
   do {                                                                                                   \
     EVR_HIP(hipFuncSetAttribute((const void*)pareto_f32_kernel<MM>,                                       \

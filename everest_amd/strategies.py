@@ -494,10 +494,13 @@ class QehviStrategy(_MultiobjectiveMixin, BotorchStrategy):
 
     def _get_acqfs(self, n) -> List[QEHVI]:
         """bofire/strategies/predictives/qehvi.py:37-79: the partition is built from the
-        masked observations better than the reference point (not objective-transformed)."""
+        masked observations better than the reference point (not objective-transformed).
+        Like the reference (qehvi.py:67-75 passes objective and X_pending only), output
+        constraints do not enter qEHVI here; QnehviStrategy and MoboStrategy pass them."""
         assert self.experiments is not None, "No experiments available."
         _, X_pending = self.get_acqf_input_tensors()
-        objectives, constraints = self._objective_spec()
+        objectives, _ = self._objective_spec()
+        constraints = ()
         keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
                                                           CloseToTargetObjective])
         df = self._valid_experiments()

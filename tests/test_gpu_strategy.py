@@ -283,9 +283,35 @@ def test_qehvi_pending_joint_batch():
     c2 = s.ask(1, add_pending=True)
     acqf = s.last_acqf
     assert acqf.X_pending is not None and acqf.X_pending.shape[0] == 1
-    # (c2 may repeat c1: at x = pending the joint block is singular and the pending point's
-    # samples switch to the candidate's base-sample row, a different QMC estimate of its own
-    # improvement — the reference's sample_cached_cholesky behaves the same)
-    v = acqf.forward(torch.tensor(s._transform(c2), device=acqf.dev))
-    assert torch.isfinite(v).all() and float(v[0]) > 0
+    # the pending point must reach the restarts' optimiser: not the pending-free q = 1 plan
+    assert not acqf.supports_plan
+    st = s.last_ask_stats
+    assert st.chunks and all(ch["driver"] != "native-plan" for ch in st.chunks)
+    v2 = acqf.forward(torch.tensor(s._transform(c2), device=acqf.dev))
+    v1 = acqf.forward(torch.tensor(s._transform(c1), device=acqf.dev))
+    assert torch.isfinite(v2).all() and float(v2[0]) > 0
+    # the returned best value is the acquisition with the pending point at the candidate
+    assert abs(float(v2[0]) - st.best_value) <= 1e-9 * max(1.0, abs(st.best_value))
+    keys = bench.domain.inputs.get_keys()
+    assert not np.allclose(c1[keys].values, c2[keys].values) or float(v2[0]) >= float(v1[0]) - 1e-12
     assert len(s.candidates) == 2
+
+
+def test_qehvi_strategy_ignores_output_constraints():
+    """QehviStrategy builds qExpectedHypervolumeImprovement without constraints / eta
+    (bofire/strategies/predictives/qehvi.py:67-75); QnehviStrategy passes them
+    (qnehvi.py:28-51)."""
+    bench, exps = _dtlz2_experiments(n=16, m=3, seed=9)
+    outs = dm.Outputs(features=[
+        dm.ContinuousOutput(key="f_0", objective=dm.MinimizeObjective(w=1.0)),
+        dm.ContinuousOutput(key="f_1", objective=dm.MinimizeObjective(w=1.0)),
+        dm.ContinuousOutput(key="f_2", objective=dm.MaximizeSigmoidObjective(tp=0.2, steepness=50.0))])
+    dom = dm.Domain(inputs=bench.domain.inputs, outputs=outs)
+    kw = dict(domain=dom, seed=2, num_sobol_samples=64, num_raw_samples=128, num_restarts=2)
+    s = strategies.map(dm.QehviStrategy(**kw))
+    s.tell(exps)
+    acqf = s._get_acqfs(1)[0]
+    assert acqf.spec.constraints == [] and acqf.spec.m_obj == 2
+    s2 = strategies.map(dm.QnehviStrategy(**kw))
+    s2.tell(exps)
+    assert len(s2._get_acqfs(1)[0].spec.constraints) == 1
