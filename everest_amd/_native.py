@@ -152,6 +152,7 @@ _SIGS = {
     "evr_qng_eval": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
                       POINTER(EvrQnehviModel), c_int] + [c_void_p] * 5, c_int),
     "evr_objective_general": ([c_void_p, c_int, c_int, c_int, POINTER(EvrQnGeneral)] + [c_void_p] * 4, c_int),
+    "evr_objective_weights": ([c_void_p, c_int, c_int, POINTER(EvrQnGeneral)] + [c_void_p] * 3, c_int),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),
     "evr_cells_kd_order_device": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 7,
                                   c_int),

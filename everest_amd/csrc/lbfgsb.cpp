@@ -626,6 +626,19 @@ int Lbfgsb::step(double f, const double* g) {
       return begin_iteration();
     }
     case S_LNSRCH: {
+      bool finite = std::isfinite(f);
+      for (int i = 0; i < n_ && finite; ++i) finite = std::isfinite(g[i]);
+      if (!finite) {
+        // a trial point with a non-finite value or gradient (an overflowing kernel gradient,
+        // a NaN from the objective) is rejected: the More-Thuente search restarts from the
+        // iterate with a 10x shorter step (counted against maxls like any other trial), so no
+        // NaN ever enters the iterate, the curvature pairs or the bracket
+        f_ = fold_;
+        g_ = r_;
+        stp_ *= 0.1;
+        ls_task_ = 0;
+        return ls_continue();
+      }
       f_ = f;
       std::copy(g, g + n_, g_.begin());
       return ls_continue();

@@ -526,6 +526,21 @@ __global__ void qg_objective_kernel(int n, int S, QgObj o, const double* __restr
   for (int k = 0; k < o.mo; ++k) O[((size_t)k * n + i) * S + s] = feas ? qg_obj(o, k, y(o.oo[k])) : ref[k];
 }
 
+// ---------------------------------------------------------------------------------------
+// objective values and smoothed feasibility weights of model-output rows, through the same
+// per-point function (qg_point) the general scan applies to every sample: G[k][i] = g_k(y_i),
+// W[i] = exp(sum_c logsigmoid(-c(y_i) / eta_c)).  Y: m_model x n (output-major).
+// ---------------------------------------------------------------------------------------
+__global__ void qg_weights_kernel(int n, QgObj o, const double* __restrict__ Y, double* __restrict__ G,
+                                  double* __restrict__ W) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double g[QG_MAXM], w;
+  qg_point(o, Y + i, (size_t)n, g, w);
+  for (int k = 0; k < o.mo; ++k) G[(size_t)k * n + i] = g[k];
+  W[i] = w;
+}
+
 static int qg_params(const evr_qn_general* g, int m_model, QgObj* o) {
   EVR_CHECK(g && g->m_obj >= 1 && g->m_obj <= QG_MAXM && g->n_con >= 0 && g->n_con <= QG_MAXC && m_model >= 1 &&
                 m_model <= QG_MAXM && g->obj_out && g->obj_kind && g->obj_p0 && g->obj_p1 &&
@@ -721,4 +736,16 @@ int evr_objective_general(void* stream, int m_model, int n, int S, const evr_qn_
   return 0;
 }
 
+int evr_objective_weights(void* stream, int m_model, int n, const evr_qn_general* g, const double* Y, double* G,
+                          double* W) {
+  QgObj o;
+  if (int rc = qg_params(g, m_model, &o)) return rc;
+  EVR_CHECK(Y && G && W && n >= 0, "evr_objective_weights: bad arguments");
+  if (n == 0) return 0;
+  qg_weights_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(n, o, Y, G, W);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // extern "C"
+

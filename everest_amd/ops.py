@@ -422,6 +422,16 @@ class GeneralSpec:
         g.zq = _p(zq)
         return g
 
+    def host_weights(self, Y: np.ndarray) -> np.ndarray:
+        """Smoothed feasibility weights exp(sum_c logsigmoid(-c / eta)) of model-output rows Y
+        (... x m_model) on the host ([upstream] compute_smoothed_feasibility_indicator,
+        fat=False); 1 without constraints."""
+        lw = np.zeros(Y.shape[:-1])
+        for o, sg, t, eta in self.constraints:
+            x = -sg * (Y[..., o] - t) / eta
+            lw += np.minimum(x, 0.0) - np.log1p(np.exp(-np.abs(x)))
+        return np.exp(lw)
+
     def host_objective(self, Y: np.ndarray) -> np.ndarray:
         """Objectives of model-output rows Y (... x m_model) on the host (observed data)."""
         cols = []
@@ -441,6 +451,20 @@ def objective_general(Y: torch.Tensor, mu: Optional[torch.Tensor], spec: General
     call("evr_objective_general", _stream(), m, n, S, ctypes.byref(g), Y.data_ptr(),
          _p(None if mu is None else _dev(mu, "mu")), _dev(ref, "ref").data_ptr(), O.data_ptr())
     return O
+
+
+def objective_weights(Y: torch.Tensor, spec: GeneralSpec):
+    """Y: m_model x n model-output rows on device -> (objectives m_obj x n, feasibility
+    weights n) through the general scan's per-point device function (evr_objective_weights)."""
+    Y = _dev(Y, "Y")
+    m, n = Y.shape
+    if m != spec.m_model:
+        raise ValueError(f"Y has {m} outputs, the spec {spec.m_model}")
+    G = torch.empty(spec.m_obj, n, dtype=torch.float64, device=Y.device)
+    W = torch.empty(n, dtype=torch.float64, device=Y.device)
+    g = spec.struct()
+    call("evr_objective_weights", _stream(), m, n, ctypes.byref(g), Y.data_ptr(), G.data_ptr(), W.data_ptr())
+    return G, W
 
 
 def qng_eval(stm: EvrQnehviState, sth: EvrQnehviState, g: EvrQnGeneral, model: "_native.EvrQnehviModel",

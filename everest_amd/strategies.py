@@ -11,7 +11,7 @@ acquisition evaluations of ``ask()`` (everest_amd/optim.py).
 from __future__ import annotations
 
 import warnings
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import pandas as pd
@@ -415,6 +415,59 @@ class BotorchStrategy(PredictiveStrategy):
         raise NotImplementedError
 
 
+def objective_term(objective, idx: int):
+    """get_objective_callable (bofire/utils/torch_tools.py:384-402) as the device kernels'
+    objective description (output, kind, p0, p1): Maximize / Minimize -> the affine
+    g = a*y + b of (y - lb) / (ub - lb) (negated for Minimize), CloseToTarget ->
+    g = -|y - target|^exponent."""
+    if isinstance(objective, CloseToTargetObjective):
+        return (int(idx), ops.OBJ_CLOSE_TO_TARGET, float(objective.target_value), float(objective.exponent))
+    if isinstance(objective, (MaximizeObjective, MinimizeObjective)):
+        a, b = objective.affine()
+        return (int(idx), ops.OBJ_AFFINE, float(a), float(b))
+    raise NotImplementedError(f"objective {type(objective).__name__} has no device kernel")
+
+
+def constrained_objective_terms(objective, idx: int, x_adapt=None):
+    """constrained_objective2botorch (bofire/utils/torch_tools.py:258-337) as the device
+    kernels' constraint description: one (output, sign, threshold, eta) per BoTorch
+    constraint callable c(Z) = sign * (Z[..., idx] - threshold), feasible for c <= 0, with
+    eta = 1 / steepness; the device weight is exp(sum_c logsigmoid(-c / eta))
+    ([upstream] compute_smoothed_feasibility_indicator, fat=False)."""
+    if not isinstance(objective, dm.ConstrainedObjective) or not hasattr(objective, "steepness"):
+        raise NotImplementedError(f"output constraint {type(objective).__name__} has no device kernel")
+    eta = 1.0 / objective.steepness
+    if isinstance(objective, dm.MovingMaximizeSigmoidObjective):
+        if x_adapt is None:
+            raise ValueError("MovingMaximizeSigmoidObjective needs x_adapt (the observed values)")
+        return [(int(idx), -1.0, float(np.asarray(x_adapt).max()) + objective.tp, eta)]
+    if isinstance(objective, dm.MaximizeSigmoidObjective):
+        return [(int(idx), -1.0, float(objective.tp), eta)]
+    if isinstance(objective, dm.MinimizeSigmoidObjective):
+        return [(int(idx), 1.0, float(objective.tp), eta)]
+    if isinstance(objective, dm.TargetObjective):
+        return [(int(idx), -1.0, objective.target_value - objective.tolerance, eta),
+                (int(idx), 1.0, objective.target_value + objective.tolerance, eta)]
+    raise NotImplementedError(f"output constraint {type(objective).__name__} has no device kernel")
+
+
+def get_output_constraints(outputs, experiments: pd.DataFrame, output_keys: Sequence[str]):
+    """get_output_constraints (bofire/utils/torch_tools.py:340-381): the constraint terms of
+    every output with a constrained objective, in output order, each over its model output
+    index in ``output_keys``; a moving turning point adapts to that output's valid
+    observations.  The etas are the terms' last field."""
+    constraints = []
+    for feat in outputs.get().features:
+        obj = getattr(feat, "objective", None)
+        if not isinstance(obj, dm.ConstrainedObjective):
+            continue
+        x_adapt = None
+        if isinstance(obj, dm.MovingMaximizeSigmoidObjective):
+            x_adapt = outputs.preprocess_experiments_one_valid_output(feat.key, experiments)[feat.key].values
+        constraints += constrained_objective_terms(obj, list(output_keys).index(feat.key), x_adapt)
+    return constraints
+
+
 class _MultiobjectiveMixin:
     """Reference point and objective handling shared by the hypervolume strategies
     (bofire/strategies/predictives/qehvi.py:87-110, mobo.py:92-115)."""
@@ -438,30 +491,8 @@ class _MultiobjectiveMixin:
         objectives, constraints = [], []
         for k in self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
                                                             CloseToTargetObjective]):
-            obj = self.domain.outputs.get_by_key(k).objective
-            if isinstance(obj, CloseToTargetObjective):
-                objectives.append((keys.index(k), ops.OBJ_CLOSE_TO_TARGET, obj.target_value, obj.exponent))
-            else:
-                a, b = obj.affine()
-                objectives.append((keys.index(k), ops.OBJ_AFFINE, a, b))
-        for feat in self.domain.outputs.get().features:
-            obj = getattr(feat, "objective", None)
-            if not isinstance(obj, dm.ConstrainedObjective):
-                continue
-            j = keys.index(feat.key)
-            if isinstance(obj, dm.TargetObjective):
-                eta = 1.0 / obj.steepness
-                constraints += [(j, -1.0, obj.target_value - obj.tolerance, eta),
-                                (j, 1.0, obj.target_value + obj.tolerance, eta)]
-            elif isinstance(obj, dm.MinimizeSigmoidObjective):
-                constraints.append((j, 1.0, obj.tp, 1.0 / obj.steepness))
-            elif isinstance(obj, dm.MovingMaximizeSigmoidObjective):
-                ex = self.domain.outputs.preprocess_experiments_one_valid_output(feat.key, self.experiments)
-                constraints.append((j, -1.0, obj.get_adjusted_tp(ex[feat.key].values), 1.0 / obj.steepness))
-            elif isinstance(obj, dm.MaximizeSigmoidObjective):
-                constraints.append((j, -1.0, obj.tp, 1.0 / obj.steepness))
-            else:
-                raise NotImplementedError(f"output constraint {type(obj).__name__} has no device kernel")
+            objectives.append(objective_term(self.domain.outputs.get_by_key(k).objective, keys.index(k)))
+        constraints = get_output_constraints(self.domain.outputs, self.experiments, keys)
         return objectives, constraints
 
     def _objective_affine(self):

@@ -356,6 +356,14 @@ int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_sta
  * infeasible samples).  g->q / g->zq unused. */
 int evr_objective_general(void* stream, int m_model, int n, int S, const evr_qn_general* g, const double* Y,
                           const double* mu, const double* ref, double* O);
+/* Objective values and smoothed feasibility weights of model-output rows (Y: m_model x n,
+ * output-major) through the per-point function the general scan applies to every MC sample:
+ * G[k][i] = g_k(y_i) (get_objective_callable, bofire/utils/torch_tools.py:384-402) and
+ * W[i] = exp(sum_c logsigmoid(-c(y_i) / eta_c)) ([upstream] compute_smoothed_feasibility_indicator
+ * over the constrained_objective2botorch callables, torch_tools.py:258-337; W = 1 without
+ * constraints).  g->q / g->zq unused. */
+int evr_objective_weights(void* stream, int m_model, int n, const evr_qn_general* g, const double* Y, double* G,
+                          double* W);
 
 /* Handle read by the PyTorch-ROCm custom operators torch.ops.everest_amd.qnehvi_forward /
  * qnehvi_backward (everest_amd/csrc/torch_ops.cpp; passed as an int64 address, owned by the

@@ -91,6 +91,51 @@ qe = QehviStrategy(domain=det.domain)
 out["qehvi_defaults"] = {"num_sobol_samples": qe.num_sobol_samples, "ref_point": qe.ref_point,
                          "type": qe.type}
 
+
+# objective callables and smoothed feasibility (the known-answer tests of
+# tests/bofire/utils/test_torch_tools.py:105-139 and :1064-1104): the reference's own
+# objective __call__ values on fixed samples.  The build's device objective g(y) must equal
+# __call__ for the objectives get_objective_callable turns into MC objectives, and its
+# feasibility weight exp(sum logsigmoid(-c/eta)) over the constraints
+# constrained_objective2botorch makes must equal __call__ for the constrained ones.
+from bofire.data_models.objectives.api import (CloseToTargetObjective, MaximizeSigmoidObjective,
+                                               MinimizeSigmoidObjective, MovingMaximizeSigmoidObjective,
+                                               TargetObjective)
+
+rng = np.random.default_rng(105)
+samples = rng.uniform(size=50) * 5.0                  # test_torch_tools.py:130: rand(50, 3) * 5, column 1
+x_adapt = rng.uniform(size=10) * 3.0                  # :132
+callables = []
+for obj in (MaximizeObjective(w=0.5), MinimizeObjective(w=0.5), CloseToTargetObjective(target_value=2.0, exponent=1.0, w=0.5),
+            CloseToTargetObjective(target_value=2.0, exponent=2.0, w=0.5),
+            MaximizeObjective(w=1.0, bounds=[-1.0, 3.0]), MinimizeObjective(w=1.0, bounds=[0.5, 4.0]),
+            MaximizeSigmoidObjective(steepness=1.0, tp=1.0, w=0.5), MinimizeSigmoidObjective(steepness=1.0, tp=1.0, w=0.5),
+            TargetObjective(target_value=2.0, steepness=1.0, tolerance=1e-3, w=0.5),
+            MovingMaximizeSigmoidObjective(steepness=1, tp=-1, w=1)):
+    callables.append({"objective": json.loads(obj.model_dump_json()),
+                      "values": np.asarray(obj(samples, x_adapt=x_adapt), dtype=np.float64).tolist()})
+out["objective_callables"] = {"samples": samples.tolist(), "x_adapt": x_adapt.tolist(), "cases": callables}
+
+xf = np.linspace(0, 30, 500)                           # :1079
+xa = np.array([1.0, 2.0, 3.0])                         # :1074
+feas = []
+for obj in (MaximizeSigmoidObjective(w=1, tp=15, steepness=0.5), MinimizeSigmoidObjective(w=1, tp=15, steepness=0.5),
+            TargetObjective(w=1, target_value=15, steepness=2, tolerance=5),
+            MovingMaximizeSigmoidObjective(w=1, tp=-1, steepness=0.5)):
+    feas.append({"objective": json.loads(obj.model_dump_json()),
+                 "values": np.asarray(obj(xf, x_adapt=xa), dtype=np.float64).tolist()})
+out["smoothed_feasibility"] = {"x": xf.tolist(), "x_adapt": xa.tolist(), "cases": feas}
+
+# get_output_constraints etas (:546-581): outputs of1 Maximize, of2 MaximizeSigmoid(steepness 2),
+# of3 Target(steepness 4) -> etas [0.5, 0.25, 0.25] (the test's literal; the etas are
+# 1/steepness per constraint, two constraints for a TargetObjective)
+of1 = ContinuousOutput(key="of1", objective=MaximizeObjective(w=1.0))
+of2 = ContinuousOutput(key="of2", objective=MaximizeSigmoidObjective(w=1.0, tp=0, steepness=2))
+of3 = ContinuousOutput(key="of3", objective=TargetObjective(w=1.0, tolerance=2, target_value=5, steepness=4))
+out["output_constraint_etas"] = {
+    "orders": [[json.loads(f.model_dump_json()) for f in fs] for fs in ((of1, of2, of3), (of2, of1, of3))],
+    "etas": [0.5, 0.25, 0.25]}
+
 with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_datamodels.json"), "w") as f:
     json.dump(out, f, indent=1)
 print("wrote reference_datamodels.json")

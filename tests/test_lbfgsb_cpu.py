@@ -78,3 +78,30 @@ def test_converged_at_start_and_fixed_variables():
 def test_bad_bounds_raise():
     with pytest.raises(RuntimeError):
         minimize_lbfgsb(_rosen, np.zeros(2), np.ones(2), np.zeros(2))
+
+
+@pytest.mark.parametrize("which", ["value", "gradient"])
+def test_nonfinite_trial_points_are_rejected(which):
+    """A line-search trial whose value or gradient is not finite (an overflowing MLL
+    gradient during the GP fit) is rejected and the search retried with a shorter step: no
+    NaN reaches an iterate, the optimum of the finite region is found."""
+    seen = []
+
+    def fun(x):
+        seen.append(x.copy())
+        f, g = float(np.sum((x - 3.0) ** 2)), 2.0 * (x - 3.0)
+        if np.any(x > 2.5):
+            if which == "value":
+                f = float("nan")
+            else:
+                g = np.full_like(x, np.inf)
+        else:
+            f += float(np.sum(np.exp(-20.0 * (2.5 - x))))       # a wall at 2.5
+            g = g - 20.0 * np.exp(-20.0 * (2.5 - x)) * -1.0
+        return f, g
+
+    x0 = np.zeros(3)
+    r = minimize_lbfgsb(fun, x0, np.full(3, -np.inf), np.full(3, np.inf), maxiter=200)
+    assert all(np.all(np.isfinite(x)) for x in seen)
+    assert np.all(np.isfinite(r.x)) and np.isfinite(r.fun)
+    assert np.all(r.x <= 2.5) and np.all(r.x > 2.0)
