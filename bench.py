@@ -19,9 +19,11 @@ reference-structure oracle on the host cores, composed from bounded samples of e
 phase).
 
 Multi-GPU (one process per GPU, RCCL): ``--gpus N`` spawns N ranks itself (or runs under
-torchrun with WORLD_SIZE = N).  One ask is sharded over the ranks (strong scaling): raw
-screening in N shards with an all-gather of the values, the restarts in N chunks
-(batch_limit = ceil(20 / N)) with one all-gather of each rank's best.
+torchrun with WORLD_SIZE = N).  One ask is sharded over the ranks (strong scaling) and stays
+the same problem at every N: raw screening in N shards with an all-gather of the values; the
+20 restarts remain ONE joint L-BFGS-B problem (batch_limit = num_restarts, BoFire's default),
+run replicated on every rank, each rank evaluating its slice of the restarts per iteration
+and all-gathering (value, gradient).
 
 Prints ONE JSON line on rank 0.
 """
@@ -345,10 +347,10 @@ def _traffic(path, kernel):
 def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=None):
     """QnehviStrategy of config 4 (DTLZ2(6, 5), n_train = n, S MC samples, ``raw`` Sobol raw
     samples, ``restarts`` L-BFGS-B restarts) through the BoFire-compatible API, fitted once
-    (tell).  With N ranks the restarts are split into N chunks (batch_limit = ceil(restarts
-    / N), bofire/data_models/strategies/predictives/botorch.py:101-108): each rank optimises
-    its own chunk and one RCCL all-gather picks the best; raw screening is sharded over the
-    ranks with an all-gather of the values.  Returns (strategy, tell_s)."""
+    (tell).  batch_limit = restarts at every N (the data model's default,
+    bofire/data_models/strategies/predictives/botorch.py:101-108): one joint problem whose
+    evaluations the ranks shard; raw screening is sharded over the ranks with an all-gather of
+    the values.  Returns (strategy, tell_s)."""
     import pandas as pd
 
     import everest_amd.data_models as dm
@@ -359,7 +361,7 @@ def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=
     Xd = pd.DataFrame(np.random.default_rng(0).uniform(size=(n, 6)), columns=bm.domain.inputs.get_keys())
     s = strategies.map(dm.QnehviStrategy(domain=bm.domain, ref_point=bm.ref_point, seed=1, num_sobol_samples=S,
                                          num_raw_samples=raw, num_restarts=restarts,
-                                         batch_limit=math.ceil(restarts / world)), dist=dist)
+                                         batch_limit=restarts), dist=dist)
     exps = bm.f(Xd, return_complete=True)
     times = []
     for _ in range(2):      # cold (first GPU work of the process: module loads, plan captures), then warm
@@ -482,19 +484,27 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EVR_DIST_BACKEND=gloo: a multi-rank rehearsal of the sharded path on fewer GPUs than
+    # ranks (ranks share devices round-robin, exchanges through host memory); default RCCL
+    backend = os.environ.get("EVR_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
         world = dist.get_world_size()
 
     def maxed(dt):
         if dist is None:
             return dt
-        tt = torch.tensor([dt], device=device)
+        tt = torch.tensor([dt], device=device if backend != "gloo" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return tt.item()
 
@@ -528,11 +538,12 @@ def main():
     # per-op device time at the restart batch one rank evaluates per L-BFGS-B iteration, on
     # the candidates the restarts converged to (the scan's work depends on where the
     # candidates sit: optimised points dominate more cells than random ones)
-    b_r = math.ceil(args.restarts / world)
-    if st_ask.restart_X is not None and st_ask.restart_X.shape[0] == b_r:
-        Xr = torch.as_tensor(np.ascontiguousarray(st_ask.restart_X.reshape(b_r, -1)), dtype=torch.float64,
+    sl = st_ask.restart_slice
+    b_r = (sl.stop - sl.start) if sl is not None else math.ceil(args.restarts / world)
+    if st_ask.restart_X is not None and sl is not None and b_r > 0:
+        Xr = torch.as_tensor(np.ascontiguousarray(st_ask.restart_X[sl].reshape(b_r, -1)), dtype=torch.float64,
                              device=device)
-        xr_note = "the last ask's optimised restart candidates"
+        xr_note = "the last ask's optimised restart candidates (this rank's slice)"
     else:
         Xr = candidates(b_r, args.d, seed=5 + rank, device=device)
         xr_note = "Sobol candidates"
@@ -551,7 +562,10 @@ def main():
         def one_pass():
             plan.run()
             if dist is not None:
-                dist.all_gather(gathered, plan.acq)
+                if backend == "gloo":
+                    dist.all_gather([g.cpu() for g in gathered], plan.acq.cpu())
+                else:
+                    dist.all_gather(gathered, plan.acq)
 
         for _ in range(3):
             one_pass()
@@ -666,8 +680,10 @@ def main():
                                    f"{args.restarts} L-BFGS-B restarts, q=1; value = (raw + optimiser "
                                    "evaluations x batch) / ask wall time, SURVEY.md §8(d)",
                        "n_train": args.n, "d": args.d, "m": args.m, "mc_samples": args.S, "raw_samples": args.raw,
-                       "restarts": args.restarts, "batch_limit": math.ceil(args.restarts / world),
-                       "parallelism": f"restart chunks + raw-screening shards over {world} rank(s)"},
+                       "restarts": args.restarts, "batch_limit": args.restarts,
+                       "parallelism": (f"one joint L-BFGS-B problem over {args.restarts} restarts, evaluation "
+                                       f"sharded over {world} rank(s) (all-gather per iteration) + raw-screening "
+                                       "shards" if world > 1 else "1 rank")},
             "roofline": roof,
             "kernels": kernels_r,
             "kernel_ms": {k: round(v, 4) for k, v in kt_r.items()},

@@ -17,8 +17,12 @@ bofire/strategies/predictives/botorch.py:384-405 (q=1, return_best_only=True):
 
 With ``dist`` (torch.distributed, one process per GPU) the raw batch is sharded over the
 ranks and the per-shard acquisition values are all-gathered (RCCL over xGMI) so that every
-rank runs the identical Boltzmann selection; restart chunks are then distributed
-round-robin and the per-chunk best (value, x) pairs all-gathered.
+rank runs the identical Boltzmann selection.  The restart chunks stay the reference's
+problems (batch_limit restarts optimised jointly): with at least as many chunks as ranks
+each rank owns whole chunks; with fewer, the ranks form one group per chunk that runs the
+chunk's optimiser replicated and evaluates it sharded, all-gathering (value, gradient) once
+per evaluation — BoFire's default batch_limit = num_restarts is one joint problem over all
+ranks.  The per-rank best (value, x) pairs are all-gathered at the end.
 """
 from __future__ import annotations
 
@@ -44,7 +48,8 @@ class OptimizeStats:
     t_raw: float = 0.0
     t_opt: float = 0.0
     chunks: List[dict] = field(default_factory=list)
-    restart_X: Optional[np.ndarray] = None    # this rank's optimised restart candidates (last chunk)
+    restart_X: Optional[np.ndarray] = None    # the optimised restart candidates of this rank's last chunk
+    restart_slice: Optional[slice] = None     # the rows of restart_X this rank evaluates
     init_X: Optional[np.ndarray] = None       # the Boltzmann initial conditions
 
     @property
@@ -399,6 +404,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     maxiter = int(options.get("maxiter", 2000))
     world = dist.get_world_size() if dist is not None else 1
     rank = dist.get_rank() if dist is not None else 0
+    cdev = comm_device(dist, dev)
 
     # 1. raw samples (seeded from the strategy's torch generator -> identical on every rank)
     seed = int(torch.randint(10_000_000, (1,), generator=gen).item())
@@ -415,9 +421,9 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     if world > 1:
         per = math.ceil(raw_samples / world)
         lo_i, hi_i = rank * per, min(raw_samples, (rank + 1) * per)
-        part = torch.zeros(per, dtype=torch.float64, device=dev)
+        part = torch.zeros(per, dtype=torch.float64, device=cdev)
         if hi_i > lo_i:
-            part[: hi_i - lo_i] = acqf.forward(Xr[lo_i:hi_i])
+            part[: hi_i - lo_i] = acqf.forward(Xr[lo_i:hi_i]).to(cdev)
         bufs = [torch.empty_like(part) for _ in range(world)]
         dist.all_gather(bufs, part)
         Y_raw = torch.cat(bufs)[:raw_samples]
@@ -440,65 +446,29 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     optimizer = options.get("optimizer") or os.environ.get("EVR_OPTIMIZER", "native")
     if optimizer not in ("native", "scipy"):
         raise ValueError(f"optimizer must be 'native' or 'scipy', got {optimizer!r}")
+    # chunk -> ranks: every chunk is the reference's own problem (batch_limit restarts
+    # optimised jointly); with at least as many chunks as ranks each rank owns whole chunks
+    # (no per-iteration collective), with fewer the ranks form one group per chunk and each
+    # group evaluates its chunk sharded
+    layout = restart_layout(len(chunks), world)
+    if world > 1:
+        _Shard.ensure_groups(dist, layout)
 
-    def evaluate(X: np.ndarray, with_grad: bool):
-        """Sharded over ranks: each rank runs its slice of the restarts on its GPU, then the
-        (value[, grad]) slices are all-gathered so that every rank holds identical bytes and
-        the replicated host optimiser takes identical steps."""
-        nb = X.shape[0]
-        if world == 1:
-            Xt = torch.as_tensor(X, dtype=torch.float64, device=dev)
-            if with_grad:
-                a, g = acqf.forward_backward(Xt)
-                return host_values(a), g.cpu().numpy()
-            return host_values(acqf.forward(Xt)), None
-        per = math.ceil(nb / world)
-        i0, i1 = min(nb, rank * per), min(nb, (rank + 1) * per)
-        nx = q * d
-        loc = torch.zeros(per, 1 + nx, dtype=torch.float64, device=dev)
-        if i1 > i0:
-            Xt = torch.as_tensor(X[i0:i1], dtype=torch.float64, device=dev)
-            if with_grad:
-                a, g = acqf.forward_backward(Xt)
-                loc[: i1 - i0, 0] = a
-                loc[: i1 - i0, 1:] = g.reshape(i1 - i0, nx)
-            else:
-                loc[: i1 - i0, 0] = acqf.forward(Xt)
-        bufs = [torch.empty_like(loc) for _ in range(world)]
-        dist.all_gather(bufs, loc)
-        full = torch.cat(bufs)[:nb].cpu().numpy()
-        host_values(torch.from_numpy(full[:, 0]))
-        return full[:, 0], (full[:, 1:].reshape((nb,) + shp) if with_grad else None)
-
-    # Independent chunks (batch_limit < num_restarts) are separate problems in the
-    # reference: with at least as many chunks as ranks each rank owns whole chunks and runs
-    # them with no per-iteration collective; a single joint chunk is evaluated sharded.
-    own_chunks = world > 1 and len(chunks) >= world
-    local_world = 1 if own_chunks else world
-
-    def run_chunk(s0: int, s1: int):
+    def run_chunk(s0: int, s1: int, shard: "_Shard"):
         nb = s1 - s0
         x0 = X0[s0:s1].reshape(-1)
         lbv, ubv = np.tile(bounds[0], nb * q), np.tile(bounds[1], nb * q)
         cons = _scipy_constraints(inequality_constraints, equality_constraints, nb * q, d)
-        if (not cons and optimizer == "native" and local_world == 1 and q == 1
+        if (not cons and optimizer == "native" and shard.k == 1 and q == 1
                 and getattr(acqf, "supports_plan", False)):
             # the whole L-BFGS-B loop in C++ on the device plan (no Python per iteration)
             Xc, vals, info = acqf.plan(nb, True).minimize(x0, lbv, ubv, maxiter)
             return vals, Xc.reshape(nb, d), {"restarts": nb, "evals": info[1], "nit": info[0], "status": info[2],
-                                             "driver": "native-plan"}
+                                             "driver": "native-plan", "local_batch": nb}
         counter = {"n": 0}
 
         def f(x):
-            if local_world == 1 and hasattr(acqf, "eval_host"):
-                a, g = acqf.eval_host(x.reshape((nb,) + shp), True)
-                a = host_values(torch.from_numpy(a))
-            elif local_world == 1:
-                Xt = torch.as_tensor(x.reshape((nb,) + shp), dtype=torch.float64, device=dev)
-                a, g = acqf.forward_backward(Xt)
-                a, g = host_values(a), g.cpu().numpy()
-            else:
-                a, g = evaluate(x.reshape((nb,) + shp), True)
+            a, g = shard.evaluate(acqf, x.reshape((nb,) + shp), True)
             counter["n"] += 1
             acc = 0.0
             for v in a.tolist():         # sequential, as evr_qnehvi_plan_minimize sums (bitwise equal paths)
@@ -516,29 +486,32 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             res = minimize(f, x0, jac=True, method="L-BFGS-B", bounds=list(zip(lbv, ubv)),
                            options={"maxiter": maxiter})
             drv = "scipy"
+        if shard.k > 1:
+            drv += f"-sharded{shard.k}"
         Xc = np.clip(res.x.reshape((nb,) + shp), bounds[0], bounds[1])
-        if local_world == 1:
-            vals = host_values(acqf.forward(torch.as_tensor(Xc, dtype=torch.float64, device=dev)))
-        else:
-            vals, _ = evaluate(Xc, False)
+        vals, _ = shard.evaluate(acqf, Xc, False)
         return vals, Xc, {"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
-                          "status": int(res.status), "driver": drv}
+                          "status": int(res.status), "driver": drv, "local_batch": shard.local_size(nb)}
 
     err: Optional[BaseException] = None
     for ci, (s0, s1) in enumerate(chunks):
-        if own_chunks and ci % world != rank:
+        ranks = layout[ci]
+        if rank not in ranks:
             continue
+        shard = _Shard(dist, ranks, rank, world, cdev)
         try:
-            vals, Xc, info = run_chunk(s0, s1)
+            vals, Xc, info = run_chunk(s0, s1, shard)
         except Exception as e:   # noqa: BLE001 — re-raised on every rank after the exchange below
-            if not own_chunks:
+            if world == 1:
                 raise
             err = e
             break
-        stats.opt_evals += info["evals"] * info["restarts"] + info["restarts"]
+        if shard.idx == 0:        # each chunk's work is counted once, by its group's first rank
+            stats.opt_evals += info["evals"] * info["restarts"] + info["restarts"]
         stats.opt_iters += info["nit"]
         stats.chunks.append(info)
         stats.restart_X = Xc
+        stats.restart_slice = shard.slice_of(s1 - s0)
         results.append((vals, Xc))
     if results:
         vals = np.concatenate([r[0] for r in results])
@@ -547,11 +520,11 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         best_v, best_x = float(vals[k]), Xs[k]
     else:
         best_v, best_x = -np.inf, np.zeros(shp)
-    if own_chunks:
+    if world > 1:
         # all-gather every rank's (error flag, best value, x) over RCCL; a failure on any rank
         # raises on every rank (no rank is left waiting in a collective); argmax, ties -> lowest rank
         flag = 0.0 if err is None else (2.0 if _is_notpsd(err) else 1.0)
-        loc = torch.tensor(np.r_[flag, best_v, np.ravel(best_x)], dtype=torch.float64, device=dev)
+        loc = torch.tensor(np.r_[flag, best_v, np.ravel(best_x)], dtype=torch.float64, device=cdev)
         bufs = [torch.empty_like(loc) for _ in range(world)]
         dist.all_gather(bufs, loc)
         allv = torch.stack(bufs).cpu().numpy()
@@ -565,13 +538,118 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
             raise RuntimeError(f"restart optimisation failed on rank(s) {bad}")
         k = int(np.argmax(allv[:, 1]))
         best_v, best_x = float(allv[k, 1]), allv[k, 2:].reshape(shp)
-        cnt = torch.tensor([stats.opt_evals], dtype=torch.float64, device=dev)
+        cnt = torch.tensor([stats.opt_evals], dtype=torch.float64, device=cdev)
         dist.all_reduce(cnt)
         stats.opt_evals_global = int(cnt.item())
     else:
         stats.opt_evals_global = stats.opt_evals
     stats.t_opt += time.perf_counter() - t0
     return best_x, best_v, stats
+
+
+def comm_device(dist, dev):
+    """Where the exchange buffers live: the GPU for RCCL ("nccl"), the host for gloo (the
+    CPU tests, and multi-rank rehearsals sharing one GPU)."""
+    if dist is None or not dist.is_initialized():
+        return dev
+    return torch.device("cpu") if dist.get_backend() == "gloo" else dev
+
+
+def restart_layout(n_chunks: int, world: int) -> List[Tuple[int, ...]]:
+    """Ranks that optimise each restart chunk.  Chunks >= ranks: chunk c on rank c mod N
+    alone; fewer chunks than ranks: the ranks split into one contiguous group per chunk
+    (sizes differ by at most one), so no rank idles; a single chunk (BoFire's default
+    batch_limit = num_restarts) is one joint problem evaluated by every rank."""
+    if world <= 1:
+        return [(0,)] * n_chunks
+    if n_chunks >= world:
+        return [(c % world,) for c in range(n_chunks)]
+    out, r = [], 0
+    for c in range(n_chunks):
+        sz = world // n_chunks + (1 if c < world % n_chunks else 0)
+        out.append(tuple(range(r, r + sz)))
+        r += sz
+    return out
+
+
+_GROUPS: dict = {}
+
+
+class _Shard:
+    """One rank's part of a restart chunk optimised by the rank group ``ranks``: every member
+    runs the same host optimiser on identical bytes (replicated, deterministic), evaluates its
+    slice of the chunk's restarts on its GPU, and the (value[, gradient]) slices are
+    all-gathered in the group (RCCL over xGMI) once per optimiser evaluation."""
+
+    def __init__(self, dist, ranks: Tuple[int, ...], rank: int, world: int, dev):
+        self.dist, self.ranks, self.dev = dist, tuple(ranks), dev
+        self.k = len(self.ranks)
+        self.idx = self.ranks.index(rank)
+        self.pg = None
+        if 1 < self.k < world:
+            key = self.ranks
+            if key not in _GROUPS:
+                # new_group is collective over the world: every rank creates every group of the
+                # layout in the same order (restart_layout is a function of (chunks, world) only)
+                raise RuntimeError("restart group not created")
+            self.pg = _GROUPS[key]
+
+    @staticmethod
+    def ensure_groups(dist, layout):
+        for ranks in layout:
+            if len(ranks) > 1 and len(ranks) < dist.get_world_size() and tuple(ranks) not in _GROUPS:
+                _GROUPS[tuple(ranks)] = dist.new_group(list(ranks))
+
+    def _bounds(self, nb: int):
+        sizes = [nb // self.k + (1 if i < nb % self.k else 0) for i in range(self.k)]
+        starts = np.cumsum([0] + sizes)
+        return sizes, starts
+
+    def slice_of(self, nb: int) -> slice:
+        sizes, starts = self._bounds(nb)
+        return slice(int(starts[self.idx]), int(starts[self.idx + 1]))
+
+    def local_size(self, nb: int) -> int:
+        return self._bounds(nb)[0][self.idx]
+
+    def evaluate(self, acqf, X: np.ndarray, with_grad: bool):
+        """(values (nb,), gradients shaped like X | None) of the whole chunk X on every member."""
+        nb = X.shape[0]
+        if self.k == 1:
+            return _local_eval(acqf, X, with_grad)
+        sizes, starts = self._bounds(nb)
+        per = max(sizes)
+        nx = int(np.prod(X.shape[1:]))
+        i0, i1 = int(starts[self.idx]), int(starts[self.idx + 1])
+        loc = np.zeros((per, 1 + nx))
+        if i1 > i0:
+            a, g = _local_eval(acqf, X[i0:i1], with_grad, check=False)
+            loc[: i1 - i0, 0] = a
+            if with_grad:
+                loc[: i1 - i0, 1:] = g.reshape(i1 - i0, nx)
+        lt = torch.as_tensor(loc, device=self.dev)
+        bufs = [torch.empty_like(lt) for _ in range(self.k)]
+        self.dist.all_gather(bufs, lt, group=self.pg)
+        full = np.concatenate([b.cpu().numpy()[:sz] for b, sz in zip(bufs, sizes)])
+        host_values(torch.from_numpy(full[:, 0]))
+        return full[:, 0], (full[:, 1:].reshape(X.shape) if with_grad else None)
+
+
+def _local_eval(acqf, X: np.ndarray, with_grad: bool, check: bool = True):
+    """This rank's evaluation of X (numpy) -> (values, gradients | None) numpy: one native plan
+    round trip (eval_host) where the acquisition has it, else the device ops."""
+    if hasattr(acqf, "eval_host"):
+        a, g = acqf.eval_host(X, with_grad)
+    else:
+        Xt = torch.as_tensor(X, dtype=torch.float64, device=acqf.dev)
+        if with_grad:
+            a, g = acqf.forward_backward(Xt)
+            a, g = a.cpu().numpy(), g.cpu().numpy()
+        else:
+            a, g = acqf.forward(Xt).cpu().numpy(), None
+    if check:
+        host_values(torch.from_numpy(np.asarray(a)))
+    return np.asarray(a), g
 
 
 def _is_notpsd(e: BaseException) -> bool:

@@ -155,3 +155,76 @@ def test_own_chunk_failure_raises_on_every_rank():
     ret = _spawn("flaky", {"batch_limit": 1, "maxiter": 50})
     assert ret[0][0] == "error" and ret[1][0] == "error"
     assert ret[0][1] == "NotPSDError" and ret[1][1] == "NotPSDError"
+
+
+def test_restart_layout_no_idle_ranks():
+    """Chunks >= ranks: whole chunks per rank; fewer chunks: one contiguous rank group per
+    chunk, sizes within one, every rank used (the N = 6 / 8 case of 20 restarts in chunks)."""
+    from everest_amd.optim import restart_layout
+
+    assert restart_layout(1, 8) == [tuple(range(8))]
+    assert restart_layout(3, 8) == [(0, 1, 2), (3, 4, 5), (6, 7)]
+    assert restart_layout(7, 8) == [(0, 1), (2,), (3,), (4,), (5,), (6,), (7,)]
+    assert restart_layout(5, 3) == [(0,), (1,), (2,), (0,), (1,)]
+    for c in range(1, 12):
+        for w in range(1, 10):
+            lay = restart_layout(c, w)
+            assert len(lay) == c
+            used = sorted(r for g in lay for r in g)
+            if c < w:
+                assert used == list(range(w))             # no idle rank
+                sz = [len(g) for g in lay]
+                assert max(sz) - min(sz) <= 1
+
+
+def _run_layout(rank, world, port, ret, acq_name, restarts, batch_limit):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from everest_amd.optim import optimize_acqf
+
+    acq = {"plain": OracleAcq, "host": HostEvalAcq}[acq_name]()
+    gen = torch.Generator().manual_seed(11)
+    bounds = np.array([[0.0] * 3, [1.0] * 3])
+    try:
+        x, v, st = optimize_acqf(acq, bounds, num_restarts=restarts, raw_samples=64,
+                                 options={"batch_limit": batch_limit, "maxiter": 200}, gen=gen, dist=dist)
+        ret[rank] = ("ok", x.tolist(), v, st.opt_evals_global, [c["driver"] for c in st.chunks])
+    except Exception as e:  # noqa: BLE001
+        ret[rank] = ("error", type(e).__name__, str(e))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("restarts,batch_limit,acq_name", [(5, 5, "host"), (5, 2, "plain"), (6, 1, "host")])
+def test_sharded_layouts_match_single_process(world, restarts, batch_limit, acq_name):
+    """The reference's problem at every world size: one joint chunk (batch_limit =
+    num_restarts) evaluated by all ranks, chunks >= ranks owned whole, and chunks < ranks
+    evaluated by rank groups — best (x, value) and the global evaluation count equal the
+    single-process run."""
+    from everest_amd.optim import optimize_acqf
+
+    acq = {"plain": OracleAcq, "host": HostEvalAcq}[acq_name]()
+    gen = torch.Generator().manual_seed(11)
+    bounds = np.array([[0.0] * 3, [1.0] * 3])
+    x1, v1, st1 = optimize_acqf(acq, bounds, num_restarts=restarts, raw_samples=64,
+                                options={"batch_limit": batch_limit, "maxiter": 200}, gen=gen)
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    ctx = mp.start_processes(_run_layout, args=(world, _free_port(), ret, acq_name, restarts, batch_limit),
+                             nprocs=world, join=False, start_method="spawn")
+    import time
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > 240:
+            for p in ctx.processes:
+                p.kill()
+            raise AssertionError("ranks did not finish")
+    ret = dict(ret)
+    n_chunks = -(-restarts // batch_limit)
+    for r in range(world):
+        status, xr, vr, evals, drivers = ret[r]
+        assert status == "ok", ret[r]
+        assert np.allclose(xr, x1, atol=1e-12) and abs(vr - v1) < 1e-14
+        assert evals == st1.opt_evals_global
+    if n_chunks < world:
+        assert any("sharded" in dv for r in range(world) for dv in ret[r][4])

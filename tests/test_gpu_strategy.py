@@ -299,8 +299,9 @@ def test_qehvi_pending_joint_batch():
 
 def test_qehvi_strategy_ignores_output_constraints():
     """QehviStrategy builds qExpectedHypervolumeImprovement without constraints / eta
-    (bofire/strategies/predictives/qehvi.py:67-75); QnehviStrategy passes them
-    (qnehvi.py:28-51)."""
+    (bofire/strategies/predictives/qehvi.py:67-75) and its data model admits no constrained
+    objective (data_models/strategies/predictives/qehvi.py:54-70); QnehviStrategy passes the
+    output constraints (qnehvi.py:28-51)."""
     bench, exps = _dtlz2_experiments(n=16, m=3, seed=9)
     outs = dm.Outputs(features=[
         dm.ContinuousOutput(key="f_0", objective=dm.MinimizeObjective(w=1.0)),
@@ -308,10 +309,14 @@ def test_qehvi_strategy_ignores_output_constraints():
         dm.ContinuousOutput(key="f_2", objective=dm.MaximizeSigmoidObjective(tp=0.2, steepness=50.0))])
     dom = dm.Domain(inputs=bench.domain.inputs, outputs=outs)
     kw = dict(domain=dom, seed=2, num_sobol_samples=64, num_raw_samples=128, num_restarts=2)
-    s = strategies.map(dm.QehviStrategy(**kw))
-    s.tell(exps)
-    acqf = s._get_acqfs(1)[0]
-    assert acqf.spec.constraints == [] and acqf.spec.m_obj == 2
+    with pytest.raises(ValueError):
+        dm.QehviStrategy(**kw)
     s2 = strategies.map(dm.QnehviStrategy(**kw))
     s2.tell(exps)
     assert len(s2._get_acqfs(1)[0].spec.constraints) == 1
+    # the plain two-objective QehviStrategy runs the fused q = 1 plan (affine objectives only)
+    s = strategies.map(dm.QehviStrategy(domain=bench.domain, ref_point=bench.ref_point, seed=2,
+                                        num_sobol_samples=64, num_raw_samples=128, num_restarts=2))
+    s.tell(exps)
+    acqf = s._get_acqfs(1)[0]
+    assert acqf.spec.constraints == [] and acqf.supports_plan
