@@ -55,10 +55,6 @@ class EvrQnGeneral(ctypes.Structure):
     ]
 
 
-class EvrQnehviHandle(ctypes.Structure):
-    """evr_qnehvi_handle: what torch.ops.everest_amd.qnehvi_* read (include/everest_amd.h)."""
-    _fields_ = [("stm", c_void_p), ("sth", c_void_p), ("md", c_void_p), ("g", c_void_p * 9), ("fast", c_int)]
-
 
 _SIGS = {
     "evr_version": ([], c_int),
@@ -131,6 +127,8 @@ _SIGS = {
     "evr_qnehvi_small_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int, c_int], ctypes.c_longlong),
     "evr_qnehvi_small_forward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
                                   c_void_p, c_void_p], c_int),
+    "evr_qnehvi_small_forward_x": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
+                                    c_void_p, c_void_p], c_int),
     "evr_qnehvi_small_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p], c_int),
     "evr_qnehvi_small_backward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,

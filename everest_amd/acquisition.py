@@ -255,22 +255,57 @@ class _BoxHviAcqf:
             dX = dX.view(b, qq, d)[:, :q].contiguous()
         return acq, dX
 
-    def _handle(self, q: int, fast: bool) -> int:
-        """Address of the evr_qnehvi_handle the torch operators read (kept alive here)."""
-        hs = self.__dict__.setdefault("_handles", {})
-        h = hs.get(fast)
-        if h is None:
-            h = _native.EvrQnehviHandle()
-            h.stm = ctypes.addressof(self.state if fast else self.state_model)
-            h.sth = ctypes.addressof(self.state if fast else self.state_scan)
-            h.md = ctypes.addressof(self.model)
-            h.fast = int(fast)
-            hs[fast] = h
-        if not fast and not h.g[q]:
-            gs = self.__dict__.setdefault("_gstructs", {})
-            gs[q] = self.spec.struct(q, self._zq(q))
-            h.g[q] = ctypes.addressof(gs[q])
-        return ctypes.addressof(h)
+    def _device_tensors(self):
+        """Every device tensor the acquisition (and its model and cells) holds: the state /
+        model structs point into these, so the torch-side acquisition object keeps them alive."""
+        out, seen = [], set()
+
+        def walk(v, depth=0):
+            if isinstance(v, torch.Tensor):
+                if v.device.type == "cuda" and id(v) not in seen:
+                    seen.add(id(v))
+                    out.append(v)
+            elif isinstance(v, (list, tuple)) and depth < 3:
+                for x in v:
+                    walk(x, depth + 1)
+            elif isinstance(v, dict) and depth < 3:
+                for x in v.values():
+                    walk(x, depth + 1)
+        for obj in (self, self.gp, getattr(self, "cells", None)):
+            if obj is not None:
+                for k, v in vars(obj).items():
+                    if k not in ("_torch_acqs", "_plans"):
+                        walk(v)
+        return out
+
+    def _torch_acq(self, q: int, fast: bool):
+        """The torch.classes.everest_amd.QnehviAcq behind torch.ops.everest_amd.qnehvi_*
+        (torch_ops.cpp): owns copies of the state / model structs, references to every device
+        tensor they point into, and a plan cache across calls (cached here per path)."""
+        from . import torch_ops
+
+        torch_ops.load()
+        cache = self.__dict__.setdefault("_torch_acqs", {})
+        acq = cache.get(fast)
+        if acq is None:
+            def raw(st):
+                return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8)
+            stm = self.state if fast else self.state_model
+            sth = self.state if fast else self.state_scan
+            acq = torch.classes.everest_amd.QnehviAcq(raw(stm), raw(sth), raw(self.model), bool(fast),
+                                                      self._device_tensors())
+            acq._general_q = set()
+            cache[fast] = acq
+        if not fast and q not in acq._general_q:
+            spec = self.spec
+            oo, ok, p0, p1 = spec._arrs
+            cons = spec.constraints
+            co = torch.tensor([c[0] for c in cons], dtype=torch.int32)
+            cs, ct, ce = (torch.tensor([c[k] for c in cons], dtype=torch.float64) for k in (1, 2, 3))
+            acq.set_general(int(q), torch.from_numpy(oo), torch.from_numpy(ok), torch.from_numpy(p0),
+                            torch.from_numpy(p1), co, cs, ct, ce, self._zq(q))
+            acq._general_q.add(q)
+        return acq
 
     def __call__(self, X: torch.Tensor) -> torch.Tensor:
         """BoTorch AcquisitionFunction protocol: X (b x q x d, or b x d for q = 1) -> acq (b),
@@ -280,7 +315,7 @@ class _BoxHviAcqf:
 
         X3, _ = self._split(X)
         if self._fast(X3):
-            return QnehviFunction.apply(X3[:, 0].contiguous(), self._handle(1, True))
+            return QnehviFunction.apply(X3[:, 0].contiguous(), self._torch_acq(1, True))
         if getattr(self, "log_acqf", False):
             raise NotImplementedError("q > 1 for the log-space acquisitions is not implemented on the device")
         Xp = self._pending_rows()
@@ -288,7 +323,7 @@ class _BoxHviAcqf:
             X3 = torch.cat([X3, Xp.unsqueeze(0).expand(X3.shape[0], Xp.shape[0], X3.shape[2])], 1)
         if X3.shape[1] > 8:
             raise ValueError(f"joint batch of {X3.shape[1]} points (q + pending) exceeds the device limit of 8")
-        return QnehviFunction.apply(X3.contiguous(), self._handle(X3.shape[1], False))
+        return QnehviFunction.apply(X3.contiguous(), self._torch_acq(X3.shape[1], False))
 
     def _split(self, X: torch.Tensor):
         """(X as b x q x d, squeeze-back flag): 2-D input is q = 1."""
@@ -529,7 +564,9 @@ class QNEHVI(_BoxHviAcqf):
         # ---- baseline posterior root, samples, box decomposition ----------------------
         if nb > 0:
             Sig_b = Sig[:, idx][:, :, idx].contiguous()
-            self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
+            # L_base and its inverse in one blocked pass: G = L_base^-1 E below is then one
+            # GEMM (a 64-row-block forward substitution kept 40 workgroups busy for ~0.5 ms)
+            self.L_base, Lb_inv, self.base_jitter, _ = ops.cholesky_inverse(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
             probe("baseline_chol")
         # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed;
@@ -590,7 +627,7 @@ class QNEHVI(_BoxHviAcqf):
                 E = torch.cat([E, torch.zeros(m, nb, npend, **f64)], 2).contiguous()
             ops.add_selection(E, idx.to(torch.int32), None)                      # + P
             ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
-            ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
+            E = ops.gemm(Lb_inv, E)                                              # G = L_base^-1 E
             ops.gemm_into(M[:, nk + nb_rows:nk + nb_rows + S_], Zb, E, transA=True)   # H^T = Z^T G
             if fused:
                 Lp = torch.zeros(m, nk, nk, **f64)

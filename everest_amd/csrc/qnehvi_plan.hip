@@ -37,6 +37,8 @@ size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
+int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                 double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
                 double* hout, const double* seqp, unsigned int* counter);
@@ -72,7 +74,7 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     return r;
   };
   L.small = small_path(st, b, md->d);
-  L.Kx = take(8 * m * n * b);
+  L.Kx = take(L.small ? 0 : 8 * m * n * b);
   L.R = take(8 * m * Rr * b);
   L.P = take(8 * (L.small ? qs_norms_doubles(st, b) : m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b));
   L.Wf = take(8 * (L.small ? 0 : proj_forward_ws_doubles(st, b)));
@@ -160,11 +162,12 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
   const bool small = p->L.small;
-  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
-                                 md->lengthscales, nullptr, nullptr, Kx))
-    return rc;
   if (small) {
-    if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;
+    // the restart batch: K_x generated inside the projection (qs_fwd_x, no kmat launch)
+    if (int rc = qs_forward_x(s, st, md, b, X, R, P)) return rc;
+  } else if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
+                                        md->lengthscales, nullptr, nullptr, Kx)) {
+    return rc;
   } else if (int rc = proj_forward(s, st, b, md->M, Kx, R, P,
                                    p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr)) {
     return rc;

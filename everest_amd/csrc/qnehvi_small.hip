@@ -44,7 +44,9 @@ __device__ __forceinline__ double4_t mfma4(double a, double b, double4_t c) {
 __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
                                               const double* __restrict__ Kx, double* __restrict__ R,
                                               double* __restrict__ P, int ntile) {
-  constexpr int MP = QS_KC + 4;                  // padded row of the staged M tile
+  // padded row of the staged M tile: 2 MP = 4 (mod 64 dwords) puts the 16 rows x 2
+  // k-quarters of a ds_read_b64 lane half on 32 distinct bank pairs (conflict-free)
+  constexpr int MP = QS_KC + 2;
   __shared__ double Ms[QS_FR][MP];               // 16 x 256 slice of M_j (33 KB)
   __shared__ double Ks[QS_KC][QS_B + 1];         // 256 x b slice of K_x,j (66 KB)
   __shared__ double red[4][QS_FR][QS_B + 1];
@@ -109,6 +111,130 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
       const double v = ((red[0][rr][c] + red[1][rr][c]) + red[2][rr][c]) + red[3][rr][c];
       if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
       red[0][rr][c] = v;   // own slot only: read back by the norms below after the barrier
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * QS_B) {
+    const int cls = tid / QS_B, c = tid - cls * QS_B;
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < QS_FR; ++rr) {
+      const int r = r0 + rr;
+      const bool in = cls == 0 ? r < n : (r >= n && r < n + nb);
+      if (in) s = fma(red[0][rr][c], red[0][rr][c], s);
+    }
+    if (c < b) P[(((size_t)j * ntile + tile) * 2 + cls) * b + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// forward with the cross-covariance generated in the B fetch (the restart batch of the native
+// plan): as qs_fwd, but each chunk's K_x rows are computed by the workgroup itself —
+// thread t owns training row kc + t and forms k(x_t, x_c) for the b candidates with
+// kmat_kernel's arithmetic (normalised / lengthscale-divided coordinates, explicit
+// differences, fma accumulation in coordinate order, the same kernel_value), so R is bitwise
+// the kmat_kernel + qs_fwd result, without the separate launch or K_x's HBM round trip.
+// The candidates (b x d raw, possibly the plan's pinned host buffer) are read once per
+// workgroup.  LDS: the M tile padded as in qs_fwd; the K tile's rows of 32 doubles hold
+// column c at c ^ 16 (k & 1), so the MFMA B reads of rows k, k+1 (one ds_read_b64 lane
+// half) fall on the two halves of the bank row; each lane starts its row's columns at
+// lane mod b so the K stores spread over the banks.
+// ---------------------------------------------------------------------------------------
+template <int KIND>
+__global__ __launch_bounds__(256) void qs_fwd_x(int n, int nb, int Rr, int b, int d, const double* __restrict__ M,
+                                                const double* __restrict__ Xn, const double* X,
+                                                const double* __restrict__ shift, const double* __restrict__ scale,
+                                                const double* __restrict__ ls, double* __restrict__ R,
+                                                double* __restrict__ P, int ntile) {
+  constexpr int MP = QS_KC + 2;
+  constexpr int UP = QS_MAXD + 1;                // candidate rows padded: per-lane rows conflict-free
+  __shared__ double Ms[QS_FR][MP];
+  __shared__ double Ks[QS_KC][QS_B];
+  __shared__ double uc[QS_B][UP];
+  __shared__ double red[4][QS_FR][QS_B + 1];
+  const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const double* Mj = M + (size_t)j * Rr * n;
+  const double* lsj = ls + (size_t)j * d;
+  double mv[QS_FR];
+  double xt[QS_MAXD];
+  auto load = [&](int kc) {
+    const int kn = min(QS_KC, n - kc);
+#pragma unroll
+    for (int u = 0; u < QS_FR; ++u) {
+      const int r = r0 + u;
+      mv[u] = (r < Rr && tid < kn) ? Mj[(size_t)r * n + kc + tid] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < QS_MAXD; ++k) xt[k] = (tid < kn && k < d) ? Xn[(size_t)(kc + tid) * d + k] : 0.0;
+  };
+  load(0);
+  // candidates, normalised and divided by the lengthscales (kmat_kernel's B operand)
+  if (tid < b * d) {
+    const int c = tid / d, k = tid - c * d;
+    double w = X[(size_t)c * d + k];
+    if (shift) w -= shift[k];
+    if (scale) w *= scale[k];
+    uc[c][k] = w * (1.0 / lsj[k]);
+  }
+  double il[QS_MAXD];
+#pragma unroll
+  for (int k = 0; k < QS_MAXD; ++k) il[k] = k < d ? 1.0 / lsj[k] : 0.0;
+  const int rot = lane % b;
+  double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  constexpr int KW = QS_KC / 4;
+  for (int kc = 0; kc < n; kc += QS_KC) {
+    const int kn = min(QS_KC, n - kc);
+    __syncthreads();   // uc written / the previous chunk's MFMAs are done with Ms, Ks
+#pragma unroll
+    for (int u = 0; u < QS_FR; ++u) Ms[u][tid] = mv[u];
+    {
+      // this thread's training row kc + tid, then its b kernel values (rows past the end: 0)
+      double ut[QS_MAXD];
+#pragma unroll
+      for (int k = 0; k < QS_MAXD; ++k) ut[k] = xt[k] * il[k];
+      const int sw = 16 * (tid & 1);
+      for (int cc = 0; cc < b; ++cc) {
+        int c = cc + rot;
+        if (c >= b) c -= b;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < QS_MAXD; ++k) {
+          if (k < d) {
+            const double df = ut[k] - uc[c][k];
+            acc = fma(df, df, acc);
+          }
+        }
+        Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND, acc) : 0.0;
+      }
+    }
+    __syncthreads();
+    if (kc + QS_KC < n) load(kc + QS_KC);
+#pragma unroll
+    for (int t = 0; t < KW / 4; ++t) {
+      const int k = wave * KW + 4 * t + kq;
+      const double a = Ms[i][k];
+      const int sw = 16 * (k & 1);
+      // columns >= b of Ks are never written: they only reach D's columns >= b (not stored)
+      acc0 = mfma4(a, Ks[k][i ^ sw], acc0);
+      acc1 = mfma4(a, Ks[k][(i + 16) ^ sw], acc1);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[wave][4 * q + kq][i] = acc0[q];
+    red[wave][4 * q + kq][16 + i] = acc1[q];
+  }
+  __syncthreads();
+  {
+    const int rr = tid >> 4, cp = tid & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = cp + 16 * h;
+      const double v = ((red[0][rr][c] + red[1][rr][c]) + red[2][rr][c]) + red[3][rr][c];
+      if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
+      red[0][rr][c] = v;
     }
   }
   __syncthreads();
@@ -394,6 +520,24 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
   return 0;
 }
 
+int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                 double* R, double* P) {
+  const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
+  const dim3 g(nt, st->m);
+#define GO(K_)                                                                                                  \
+  qs_fwd_x<K_><<<g, 256, 0, s>>>(st->n, st->nb, Rr, b, md->d, md->M, md->Xn, X, md->shift, md->scale,           \
+                                 md->lengthscales, R, P, nt)
+  switch (md->kind) {
+    case RBF: GO(RBF); break;
+    case MATERN05: GO(MATERN05); break;
+    case MATERN15: GO(MATERN15); break;
+    default: GO(MATERN25); break;
+  }
+#undef GO
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
                 double* hout, const double* seqp, unsigned int* counter) {
@@ -430,6 +574,13 @@ int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr
                              const double* Kx, double* R, double* P) {
   EVR_CHECK(st && md && Kx && R && P && qs_applies(st, b, md->d), "evr_qnehvi_small_forward: bad arguments");
   return qs_forward((hipStream_t)stream, st, md, b, Kx, R, P);
+}
+
+int evr_qnehvi_small_forward_x(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                               const double* X, double* R, double* P) {
+  EVR_CHECK(st && md && X && R && P && qs_applies(st, b, md->d) && md->Xn && md->M && md->lengthscales,
+            "evr_qnehvi_small_forward_x: bad arguments");
+  return qs_forward_x((hipStream_t)stream, st, md, b, X, R, P);
 }
 
 int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,

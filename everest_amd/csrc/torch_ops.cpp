@@ -9,7 +9,13 @@
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/custom_class.h>
 #include <torch/library.h>
+
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
 
 #include "../../include/everest_amd.h"
 
@@ -110,55 +116,161 @@ std::tuple<at::Tensor, at::Tensor> gp_posterior(const at::Tensor& Xn_, const at:
   return {mean, var};
 }
 
-const evr_qnehvi_handle* handle_of(int64_t h) {
-  TORCH_CHECK(h != 0, "qnehvi: null handle");
-  return reinterpret_cast<const evr_qnehvi_handle*>(h);
-}
+// ---------------------------------------------------------------------------------------
+// The acquisition behind torch.ops.everest_amd.qnehvi_*: a registered torch class that OWNS
+// what the device chain reads — private copies of the state / model / objective structs and
+// references to every device tensor they point into (so the tensors live as long as the
+// object) — and caches one native plan per (batch size, backward) across calls.
+// ---------------------------------------------------------------------------------------
+struct QnehviAcq : torch::CustomClassHolder {
+  evr_qnehvi_state stm{}, sth{};
+  evr_qnehvi_model md{};
+  bool fast = false;
+  std::vector<at::Tensor> keep;
+  struct General {
+    evr_qn_general g{};
+    std::vector<int> oo, ok, co;
+    std::vector<double> p0, p1, cs, ct, ce;
+    at::Tensor zq;
+  };
+  std::map<int64_t, std::unique_ptr<General>> gens;
+  struct Plan {
+    evr_qnehvi_plan* p = nullptr;
+    at::Tensor work, X, acq, dX;
+  };
+  std::map<std::pair<int64_t, bool>, Plan> plans;
+  int64_t n_evals = 0;
 
-// (acq, dX | undefined) of the acquisition at X through the handle
-std::tuple<at::Tensor, at::Tensor> qnehvi_eval(int64_t h, const at::Tensor& X_, bool backward) {
-  const evr_qnehvi_handle* H = handle_of(h);
-  auto X = dev64(X_, "X");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  hipStream_t s = cur_stream();
-  if (H->fast) {
-    TORCH_CHECK(X.dim() == 2 && X.size(1) == H->md->d, "qnehvi (q = 1 fast path): X must be b x d");
-    const int b = (int)X.size(0);
+  template <class T>
+  static T from_bytes(const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.device().is_cpu() && t.scalar_type() == at::kByte && t.numel() == (int64_t)sizeof(T),
+                "QnehviAcq: ", what, " must be a CPU uint8 tensor of ", sizeof(T), " bytes");
+    T v;
+    std::memcpy(&v, t.contiguous().data_ptr(), sizeof(T));
+    return v;
+  }
+
+  QnehviAcq(const at::Tensor& stm_b, const at::Tensor& sth_b, const at::Tensor& md_b, bool fast_,
+            std::vector<at::Tensor> keep_)
+      : fast(fast_), keep(std::move(keep_)) {
+    stm = from_bytes<evr_qnehvi_state>(stm_b, "model-side state");
+    sth = from_bytes<evr_qnehvi_state>(sth_b, "scan-side state");
+    md = from_bytes<evr_qnehvi_model>(md_b, "model");
+    TORCH_CHECK(md.M && md.Xn && md.lengthscales && md.n == stm.n && md.d >= 1, "QnehviAcq: inconsistent model");
+  }
+
+  ~QnehviAcq() override {
+    for (auto& kv : plans) evr_qnehvi_plan_destroy(kv.second.p);
+  }
+
+  // objective / constraint description and base samples of q-point candidates (general path)
+  void set_general(int64_t q, const at::Tensor& oo, const at::Tensor& ok, const at::Tensor& p0, const at::Tensor& p1,
+                   const at::Tensor& co, const at::Tensor& cs, const at::Tensor& ct, const at::Tensor& ce,
+                   const at::Tensor& zq) {
+    TORCH_CHECK(q >= 1 && q <= EVR_QNG_MAX_Q, "QnehviAcq.set_general: q = ", q, " outside 1..", EVR_QNG_MAX_Q);
+    auto ints = [](const at::Tensor& t) {
+      auto c = t.to(at::kCPU, at::kInt).contiguous();
+      return std::vector<int>(c.data_ptr<int>(), c.data_ptr<int>() + c.numel());
+    };
+    auto dbls = [](const at::Tensor& t) {
+      auto c = t.to(at::kCPU, at::kDouble).contiguous();
+      return std::vector<double>(c.data_ptr<double>(), c.data_ptr<double>() + c.numel());
+    };
+    auto G = std::make_unique<General>();
+    G->oo = ints(oo);
+    G->ok = ints(ok);
+    G->co = ints(co);
+    G->p0 = dbls(p0);
+    G->p1 = dbls(p1);
+    G->cs = dbls(cs);
+    G->ct = dbls(ct);
+    G->ce = dbls(ce);
+    TORCH_CHECK(G->ok.size() == G->oo.size() && G->p0.size() == G->oo.size() && G->p1.size() == G->oo.size() &&
+                    G->cs.size() == G->co.size() && G->ct.size() == G->co.size() && G->ce.size() == G->co.size(),
+                "QnehviAcq.set_general: inconsistent objective / constraint arrays");
+    G->zq = dev64(zq, "zq");
+    G->g.q = (int)q;
+    G->g.m_obj = (int)G->oo.size();
+    G->g.obj_out = G->oo.data();
+    G->g.obj_kind = G->ok.data();
+    G->g.obj_p0 = G->p0.data();
+    G->g.obj_p1 = G->p1.data();
+    G->g.n_con = (int)G->co.size();
+    G->g.con_out = G->co.empty() ? nullptr : G->co.data();
+    G->g.con_sign = G->cs.empty() ? nullptr : G->cs.data();
+    G->g.con_thr = G->ct.empty() ? nullptr : G->ct.data();
+    G->g.con_eta = G->ce.empty() ? nullptr : G->ce.data();
+    G->g.zq = G->zq.data_ptr<double>();
+    gens[q] = std::move(G);
+  }
+
+  Plan& plan(int64_t b, bool backward, const at::Tensor& like, hipStream_t s) {
+    auto key = std::make_pair(b, backward);
+    auto it = plans.find(key);
+    if (it != plans.end()) return it->second;
+    Plan P;
+    P.X = at::empty({b, (int64_t)md.d}, like.options());
+    P.acq = at::empty({b}, like.options());
+    P.dX = backward ? at::empty({b, (int64_t)md.d}, like.options()) : at::Tensor();
+    P.work = at::empty({std::max<long long>(evr_qnehvi_plan_workspace_bytes(&stm, &md, (int)b, backward), 1)},
+                       like.options().dtype(at::kByte));
+    check(evr_qnehvi_plan_create(s, &stm, &md, (int)b, backward, P.X.data_ptr<double>(), P.work.data_ptr(),
+                                 P.acq.data_ptr<double>(), backward ? P.dX.data_ptr<double>() : nullptr, 1, &P.p),
+          "qnehvi_plan_create");
+    return plans.emplace(key, std::move(P)).first->second;
+  }
+
+  // (acq, dX | undefined) at X: q = 1 on the fused chain through a cached plan (one graph
+  // launch from its second use), q-point candidates through evr_qng_eval
+  std::tuple<at::Tensor, at::Tensor> eval(const at::Tensor& X_, bool backward) {
+    auto X = dev64(X_, "X");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+    hipStream_t s = cur_stream();
+    if (fast) {
+      TORCH_CHECK(X.dim() == 2 && X.size(1) == md.d, "qnehvi (q = 1 fast path): X must be b x d");
+      const int64_t b = X.size(0);
+      if (b == 0) return {at::empty({0}, X.options()), backward ? at::empty_like(X) : at::Tensor()};
+      Plan& P = plan(b, backward, X, s);
+      P.X.copy_(X);
+      check(evr_qnehvi_plan_run(s, P.p), "qnehvi_plan_run");
+      ++n_evals;
+      return {P.acq.clone(), backward ? P.dX.clone() : at::Tensor()};
+    }
+    TORCH_CHECK(X.dim() == 3 && X.size(2) == md.d, "qnehvi (general path): X must be b x q x d");
+    const int64_t b = X.size(0), q = X.size(1);
+    auto it = gens.find(q);
+    TORCH_CHECK(it != gens.end(), "qnehvi: no objective description / base samples set for q = ", q);
+    const evr_qn_general* g = &it->second->g;
     auto acq = at::empty({b}, X.options());
     at::Tensor dX = backward ? at::empty_like(X) : at::Tensor();
     if (b == 0) return {acq, dX};
-    auto work = at::empty({std::max<long long>(evr_qnehvi_plan_workspace_bytes(H->stm, H->md, b, backward), 1)},
-                          X.options().dtype(at::kByte));
-    evr_qnehvi_plan* plan = nullptr;
-    check(evr_qnehvi_plan_create(s, H->stm, H->md, b, backward, X.data_ptr<double>(), work.data_ptr(),
-                                 acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr, 0, &plan),
-          "qnehvi_plan_create");
-    const int rc = evr_qnehvi_plan_run(s, plan);
-    evr_qnehvi_plan_destroy(plan);
-    check(rc, "qnehvi_plan_run");
+    auto work = scratch(evr_qng_workspace_doubles(&stm, &sth, g, &md, (int)b, backward), X);
+    check(evr_qng_eval(s, &stm, &sth, g, &md, (int)b, X.data_ptr<double>(), nullptr, work.data_ptr<double>(),
+                       acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr),
+          "qng_eval");
+    ++n_evals;
     return {acq, dX};
   }
-  TORCH_CHECK(X.dim() == 3 && X.size(2) == H->md->d, "qnehvi (general path): X must be b x q x d");
-  const int64_t b = X.size(0), q = X.size(1), d = X.size(2);
-  TORCH_CHECK(q >= 1 && q <= EVR_QNG_MAX_Q && H->g[q], "qnehvi: no base samples prepared for q = ", q);
-  auto acq = at::empty({b}, X.options());
-  at::Tensor dX = backward ? at::empty_like(X) : at::Tensor();
-  if (b == 0) return {acq, dX};
-  auto work = scratch(evr_qng_workspace_doubles(H->stm, H->sth, H->g[q], H->md, (int)b, backward), X);
-  check(evr_qng_eval(s, H->stm, H->sth, H->g[q], H->md, (int)b, X.data_ptr<double>(), nullptr,
-                     work.data_ptr<double>(), acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr),
-        "qng_eval");
-  (void)d;
-  return {acq, dX};
+
+  int64_t evals() const { return n_evals; }
+  int64_t cached_plans() const { return (int64_t)plans.size(); }
+};
+
+using AcqPtr = c10::intrusive_ptr<QnehviAcq>;
+
+at::Tensor qnehvi_forward(const AcqPtr& acq, const at::Tensor& X) { return std::get<0>(acq->eval(X, false)); }
+
+// (acq, d acq_c / dX_c): one chain for the value and the analytic gradient
+std::tuple<at::Tensor, at::Tensor> qnehvi_forward_backward(const AcqPtr& acq, const at::Tensor& X) {
+  return acq->eval(X, true);
 }
 
-at::Tensor qnehvi_forward(int64_t h, const at::Tensor& X) { return std::get<0>(qnehvi_eval(h, X, false)); }
-
 // d(sum_c grad_out_c acq_c)/dX: candidates are independent, so the per-candidate gradient
-// of the device backward is scaled by grad_out
-at::Tensor qnehvi_backward(int64_t h, const at::Tensor& X, const at::Tensor& grad_out_) {
+// of the device backward is scaled by grad_out (re-runs the chain; the autograd wrapper uses
+// qnehvi_forward_backward's saved gradient instead)
+at::Tensor qnehvi_backward(const AcqPtr& acq, const at::Tensor& X, const at::Tensor& grad_out_) {
   auto g = dev64(grad_out_, "grad_out");
-  auto dX = std::get<1>(qnehvi_eval(h, X, true));
+  auto dX = std::get<1>(acq->eval(X, true));
   TORCH_CHECK(g.numel() == dX.size(0), "qnehvi_backward: grad_out must have one entry per candidate");
   std::vector<int64_t> shape(dX.dim(), 1);
   shape[0] = dX.size(0);
@@ -168,13 +280,19 @@ at::Tensor qnehvi_backward(int64_t h, const at::Tensor& X, const at::Tensor& gra
 }  // namespace
 
 TORCH_LIBRARY(everest_amd, m) {
+  m.class_<QnehviAcq>("QnehviAcq")
+      .def(torch::init<at::Tensor, at::Tensor, at::Tensor, bool, std::vector<at::Tensor>>())
+      .def("set_general", &QnehviAcq::set_general)
+      .def("evals", &QnehviAcq::evals)
+      .def("cached_plans", &QnehviAcq::cached_plans);
   m.def("kernel_matrix(Tensor X1, Tensor X2, Tensor lengthscales, int kind) -> Tensor");
   m.def("cholesky(Tensor A, float jitter0, int max_tries) -> (Tensor, Tensor, Tensor)");
   m.def("tri_inv(Tensor L) -> Tensor");
   m.def("gp_posterior(Tensor Xn, Tensor X, Tensor shift, Tensor scale, Tensor lengthscales, Tensor M, int kind, "
         "Tensor c, Tensor ym, Tensor ys, Tensor kxx, Tensor? noise) -> (Tensor, Tensor)");
-  m.def("qnehvi_forward(int handle, Tensor X) -> Tensor");
-  m.def("qnehvi_backward(int handle, Tensor X, Tensor grad_out) -> Tensor");
+  m.def("qnehvi_forward(__torch__.torch.classes.everest_amd.QnehviAcq acq, Tensor X) -> Tensor");
+  m.def("qnehvi_forward_backward(__torch__.torch.classes.everest_amd.QnehviAcq acq, Tensor X) -> (Tensor, Tensor)");
+  m.def("qnehvi_backward(__torch__.torch.classes.everest_amd.QnehviAcq acq, Tensor X, Tensor grad_out) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(everest_amd, CUDA, m) {
@@ -183,5 +301,6 @@ TORCH_LIBRARY_IMPL(everest_amd, CUDA, m) {
   m.impl("tri_inv", &tri_inv);
   m.impl("gp_posterior", &gp_posterior);
   m.impl("qnehvi_forward", &qnehvi_forward);
+  m.impl("qnehvi_forward_backward", &qnehvi_forward_backward);
   m.impl("qnehvi_backward", &qnehvi_backward);
 }

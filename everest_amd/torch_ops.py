@@ -7,8 +7,10 @@ AcquisitionFunction.forward protocols called at bofire/strategies/predictives/bo
     torch.ops.everest_amd.kernel_matrix(X1, X2, lengthscales, kind) -> K (B x n1 x n2)
     torch.ops.everest_amd.cholesky(A, jitter0, max_tries) -> (L, jitter, info)
     torch.ops.everest_amd.gp_posterior(Xn, X, shift, scale, ls, M, kind, c, ym, ys, kxx, noise?)
-    torch.ops.everest_amd.qnehvi_forward(handle, X) -> acq
-    torch.ops.everest_amd.qnehvi_backward(handle, X, grad_out) -> dX
+    torch.classes.everest_amd.QnehviAcq(state, scan_state, model, fast, keep)  (owns state + plans)
+    torch.ops.everest_amd.qnehvi_forward(acq, X) -> acq values
+    torch.ops.everest_amd.qnehvi_forward_backward(acq, X) -> (acq values, dX)
+    torch.ops.everest_amd.qnehvi_backward(acq, X, grad_out) -> dX
 
 No fallback: a missing library raises NativeLibraryError."""
 from __future__ import annotations
@@ -39,16 +41,24 @@ def load():
 
 
 class QnehviFunction(torch.autograd.Function):
-    """acq = qNEHVI / qEHVI(X) through torch.ops.everest_amd.qnehvi_forward with the analytic
-    device backward (qnehvi_backward) as its gradient."""
+    """acq = qNEHVI / qEHVI(X) through the torch operators on a
+    torch.classes.everest_amd.QnehviAcq (which owns the acquisition state and caches its
+    plans).  When X needs a gradient the forward runs qnehvi_forward_backward — ONE device
+    chain for the value and the analytic gradient — and saves dX; backward only scales it by
+    grad_out (candidates are independent)."""
 
     @staticmethod
-    def forward(ctx, X: torch.Tensor, handle: int):
-        ctx.save_for_backward(X)
-        ctx.handle = handle
-        return load().qnehvi_forward(handle, X)
+    def forward(ctx, X: torch.Tensor, acq):
+        ops = load()
+        if ctx.needs_input_grad[0]:
+            a, dX = ops.qnehvi_forward_backward(acq, X)
+            ctx.save_for_backward(dX)
+            return a
+        ctx.save_for_backward(None)
+        return ops.qnehvi_forward(acq, X)
 
     @staticmethod
     def backward(ctx, grad_out: torch.Tensor):
-        (X,) = ctx.saved_tensors
-        return load().qnehvi_backward(ctx.handle, X, grad_out.contiguous()), None
+        (dX,) = ctx.saved_tensors
+        shape = (dX.shape[0],) + (1,) * (dX.dim() - 1)
+        return dX * grad_out.reshape(shape), None

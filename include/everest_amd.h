@@ -262,6 +262,11 @@ int evr_qnehvi_small_applies(const evr_qnehvi_state* st, int b, int d);
 long long evr_qnehvi_small_workspace_doubles(const evr_qnehvi_state* st, int b, int d, int which);
 int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
                              const double* Kx, double* R, double* P);
+/* As evr_qnehvi_small_forward with the cross-covariance generated inside the projection from
+ * the raw candidates X (b x d; the native plan's restart-batch path): R and P bitwise equal
+ * to kernel_matrix + evr_qnehvi_small_forward. */
+int evr_qnehvi_small_forward_x(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
+                               const double* X, double* R, double* P);
 int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,
                              double* G, double* L22, int* flags);
 int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
@@ -365,18 +370,10 @@ int evr_objective_general(void* stream, int m_model, int n, int S, const evr_qn_
 int evr_objective_weights(void* stream, int m_model, int n, const evr_qn_general* g, const double* Y, double* G,
                           double* W);
 
-/* Handle read by the PyTorch-ROCm custom operators torch.ops.everest_amd.qnehvi_forward /
- * qnehvi_backward (everest_amd/csrc/torch_ops.cpp; passed as an int64 address, owned by the
- * Python acquisition object): fast != 0 -> b x d candidates through the fused q = 1 chain on
- * (stm, md); otherwise b x q x d candidates through evr_qng_eval with g[q] (set for every q
- * the caller evaluates; pending rows are already part of the batch). */
-typedef struct {
-  const evr_qnehvi_state* stm;
-  const evr_qnehvi_state* sth;
-  const evr_qnehvi_model* md;
-  const evr_qn_general* g[EVR_QNG_MAX_Q + 1];
-  int fast;
-} evr_qnehvi_handle;
+/* The PyTorch-ROCm operators torch.ops.everest_amd.qnehvi_* (everest_amd/csrc/torch_ops.cpp)
+ * take a torch.classes.everest_amd.QnehviAcq: it copies the evr_qnehvi_state /
+ * evr_qnehvi_model / evr_qn_general structs, holds references to the device tensors they
+ * point into, and caches one plan per batch size (no raw addresses cross the boundary). */
 
 /* ---- qEI (q = 1, single output) -----------------------------------------------------
  * R = [Linv; alpha^T] K(Xtr, x) ((n+1) x b).  acq[c] = mean_s (a*(mu + sd*z_s) + b - best_f)_+

@@ -116,6 +116,9 @@ def test_small_batch_ops_equal_plan():
     assert ops.qnehvi_small_applies(st, b, d)
     Kx = gp.cross(Xc)
     R, P = ops.qnehvi_small_forward(st, md, Kx, b)
+    # the plan's projection generates K_x itself: bitwise the kernel_matrix + projection pair
+    R2, P2 = ops.qnehvi_small_forward_x(st, md, Xc, b)
+    assert torch.equal(R, R2) and torch.equal(P, P2)
     G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
     acq, dG = ops.hvi_forward_backward(st, G, b, flags)
     dX = ops.qnehvi_small_backward(st, md, Xc, R, L22, dG, b)

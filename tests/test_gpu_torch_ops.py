@@ -84,6 +84,38 @@ def test_qnehvi_autograd_function(general, q):
     assert torch.allclose(X.grad, g_ref * w.view(wshape), rtol=1e-12, atol=1e-30)
 
 
+def test_autograd_launches_the_chain_once_and_caches_plans():
+    """acqf(X).sum().backward() runs ONE device chain (qnehvi_forward_backward in the
+    autograd forward, the saved dX scaled in backward), the torch-side acquisition caches its
+    plan across calls, and it keeps the device state alive on its own."""
+    import gc
+
+    acqf, lo, hi = _acqf(False)
+    rng = np.random.default_rng(9)
+    Xc = torch.tensor(lo + (hi - lo) * rng.uniform(size=(11, 4)), device="cuda")
+    a_ref, g_ref = acqf.forward_backward(Xc)
+    tacq = acqf._torch_acq(1, True)
+    n0 = tacq.evals()
+    for k in range(3):
+        X = Xc.clone().requires_grad_(True)
+        acqf(X).sum().backward()
+        assert tacq.evals() == n0 + k + 1          # one chain per forward + backward
+        assert torch.equal(X.grad, g_ref)
+    assert tacq.cached_plans() == 1
+    with torch.no_grad():
+        v = acqf(Xc)                                # value only: no gradient chain
+    assert torch.equal(v, a_ref) and tacq.evals() == n0 + 4 and tacq.cached_plans() == 2
+    # the torch object owns its state: drop every Python reference to the acquisition
+    ops = __import__("everest_amd.torch_ops", fromlist=["load"]).load()
+    del acqf
+    gc.collect()
+    torch.cuda.empty_cache()
+    junk = torch.randn(1 << 22, dtype=torch.float64, device="cuda")   # reuse freed memory
+    a2, g2 = ops.qnehvi_forward_backward(tacq, Xc)
+    assert torch.equal(a2, a_ref) and torch.equal(g2, g_ref)
+    del junk
+
+
 def test_surrogate_dumps_loads_round_trip():
     import everest_amd.data_models as dm
     from everest_amd import strategies, surrogates

@@ -122,8 +122,10 @@ def test_torch_operator_library_registers_ops():
     from everest_amd import torch_ops
 
     ns = torch_ops.load()
-    for name in ("kernel_matrix", "cholesky", "gp_posterior", "qnehvi_forward", "qnehvi_backward"):
+    for name in ("kernel_matrix", "cholesky", "gp_posterior", "qnehvi_forward", "qnehvi_forward_backward",
+                 "qnehvi_backward"):
         assert hasattr(ns, name)
+    assert hasattr(torch.classes.everest_amd, "QnehviAcq")
     x = torch.zeros(3, 2, dtype=torch.float64)
     with pytest.raises((RuntimeError, NotImplementedError)):
         ns.kernel_matrix(x, x, torch.ones(2, dtype=torch.float64), 0)
