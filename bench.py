@@ -332,6 +332,75 @@ def cpu_ask_estimate(orc, states, acqf, Xc_cpu, ask, prune_sub=128, prune_sample
     return out
 
 
+class _OracleAcqf:
+    """The oracle's reference-structure qNEHVI (torch-CPU fp64) behind optimize_acqf's
+    acquisition protocol: forward in chunks of ``chunk`` candidates (BoTorch evaluates the raw
+    samples in batch_limit chunks), forward_backward by autograd over the joint restart batch
+    (gen_candidates_scipy's acq(X).sum().backward())."""
+
+    dev = torch.device("cpu")
+
+    def __init__(self, orc, chunk):
+        self.orc, self.chunk = orc, chunk
+
+    def forward(self, X):
+        with torch.no_grad():
+            return torch.cat([self.orc.forward(X[i:i + self.chunk].unsqueeze(1))
+                              for i in range(0, X.shape[0], self.chunk)])
+
+    def forward_backward(self, X):
+        x = X.detach().clone().requires_grad_(True)
+        v = self.orc.forward(x.unsqueeze(1))
+        v.sum().backward()
+        return v.detach(), x.grad
+
+
+def cpu_full_ask(s, restarts, raw, S, seed=0):
+    """One FULL, un-extrapolated reference-structure QnehviStrategy.ask() on the host cores
+    (oracle/, torch-CPU fp64, BoTorch's computation shape) for the ask the GPU times: prune
+    over 2048 posterior draws, S per-sample Python box decompositions, ``raw`` raw samples in
+    chunks of batch_limit, then scipy L-BFGS-B over the joint ``restarts`` problem with the
+    autograd gradient, on the GPU ask's fitted GPs.  Returns a dict of phase times and
+    evaluation counts (minutes of CPU work: run with --cpu-full-ask, not by default)."""
+    from everest_amd.optim import optimize_acqf
+    from oracle import gp as ogp
+    from oracle import qnehvi as oq
+
+    states = []
+    for sur in s.surrogates.surrogates:
+        st = sur.state
+        states.append(ogp.GPState(X=torch.tensor((st["X"] - st["lo"]) / (st["hi"] - st["lo"])),
+                                  y=torch.tensor((st["y"] - st["y_mean"]) / st["y_std"]),
+                                  lengthscale=torch.tensor(st["lengthscale"]), noise=st["noise"],
+                                  constant=st["constant"], y_mean=st["y_mean"], y_std=st["y_std"]))
+    m = len(states)
+    Xn = states[0].X
+    obj = oq.Objective(-torch.ones(m, dtype=torch.float64), torch.zeros(m, dtype=torch.float64))
+    ref = torch.tensor(s.get_adjusted_refpoint(), dtype=torch.float64)
+    out = {}
+    t0 = time.perf_counter()
+    zp = oq.base_samples(2048, Xn.shape[0], m, seed + 1)
+    idx, _ = oq.prune_baseline(states, Xn, obj, ref, zp, chunk=32)
+    out["prune_s"] = time.perf_counter() - t0
+    nb = int(idx.shape[0])
+    t1 = time.perf_counter()
+    zb = oq.base_samples(S, nb, m, seed + 2)
+    zn = oq.base_samples(S, nb + 1, m, seed + 2)[:, nb:nb + 1]
+    orc = oq.QNEHVI(states, Xn[idx], obj, ref, zb, zn)
+    out["baseline_and_box_decomposition_s"] = time.perf_counter() - t1
+    gen = torch.Generator().manual_seed(seed)
+    bounds = np.array([[0.0] * Xn.shape[1], [1.0] * Xn.shape[1]])
+    x, v, st = optimize_acqf(_OracleAcqf(orc, restarts), bounds, restarts, raw,
+                             {"batch_limit": restarts, "maxiter": 2000, "optimizer": "scipy"}, gen)
+    out["raw_screening_s"] = st.t_raw
+    out["restarts_s"] = st.t_opt
+    out["total_s"] = time.perf_counter() - t0
+    out.update(n_base=nb, cells_total=int(sum(c.shape[1] for c in orc.cells)), raw_evals=st.raw_evals,
+               opt_evals=st.opt_evals, optimizer_iterations=st.opt_iters, best_value=v,
+               candidates_per_s=round((st.raw_evals + st.opt_evals) / out["total_s"], 3))
+    return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}
+
+
 def _traffic(path, kernel):
     """Per-launch HBM bytes of ``kernel`` from the committed PMC summary (FETCH_SIZE doubled
     per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE), or None."""
@@ -471,6 +540,8 @@ def main():
     ap.add_argument("--b", type=int, default=512, help="candidates per rank of the evaluation pass")
     ap.add_argument("--eval-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full-ask", default=None, metavar="JSON",
+                    help="also run one FULL reference-structure ask on the host (minutes) and write it to JSON")
     ap.add_argument("--no-eval-pass", action="store_true", help="skip the b-candidate evaluation-pass figures")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
@@ -655,6 +726,20 @@ def main():
                                      "sample": f"forward+backward of {nc} candidates in chunks of 8, {t_cpu:.1f} s"},
                    "cores_note": f"{threads} threads = this job's CPU share (OMP_NUM_THREADS; affinity mask "
                                  f"{share}, os.cpu_count {os.cpu_count()})"}
+            full_path = args.cpu_full_ask or os.path.join(ROOT, "profiles", "cpu_full_ask.json")
+            if args.cpu_full_ask:
+                full = cpu_full_ask(s, args.restarts, args.raw, args.S)
+                full.update(cores=threads, gpu_ask_s=round(ms * 1e-3, 4))
+                with open(args.cpu_full_ask, "w") as f:
+                    json.dump(full, f, indent=1)
+            try:
+                with open(full_path) as f:
+                    full = json.load(f)
+                cpu["full_ask_measured"] = dict(full, source=os.path.relpath(full_path, ROOT),
+                                                note="one complete un-extrapolated reference-structure ask on the "
+                                                     "host cores (bench.py --cpu-full-ask)")
+            except (OSError, ValueError):
+                pass
             torch.set_num_threads(1)
             t1, n1, _, _ = cpu_baseline(acqf, hypers, X, Y, Xcc, budget_s=4.0)
             cpu["eval_pass_cpu"]["single_thread"] = {"value": round(n1 / t1, 3), "cores": 1,
