@@ -149,6 +149,10 @@ _SIGS = {
                                    POINTER(EvrQnehviModel), c_int, c_int], c_longlong),
     "evr_qng_eval": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
                       POINTER(EvrQnehviModel), c_int] + [c_void_p] * 5, c_int),
+    "evr_qlog_workspace_doubles": ([POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
+                                    POINTER(EvrQnehviModel), c_int, c_int], ctypes.c_longlong),
+    "evr_qlog_eval": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),
+                       POINTER(EvrQnehviModel), c_int] + [c_void_p] * 5, c_int),
     "evr_objective_general": ([c_void_p, c_int, c_int, c_int, POINTER(EvrQnGeneral)] + [c_void_p] * 4, c_int),
     "evr_objective_weights": ([c_void_p, c_int, c_int, POINTER(EvrQnGeneral)] + [c_void_p] * 3, c_int),
     "evr_cells_kd_limits": ([c_int, c_int, c_int, c_void_p], c_int),

@@ -175,22 +175,26 @@ class _BoxHviAcqf:
 
     def _use_log_scan(self, tau_relu: float, tau_max: float):
         """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
-        dense kernel of hvi_log.hip over the explicit cell bounds (compressed cells are
-        expanded once, on the device)."""
+        q = 1 affine fast path runs the dense kernel of hvi_log.hip, every other case
+        (output constraints, CloseToTarget / selected outputs, q > 1, qLogEHVI pending points)
+        the general log scan (evr_qlog_eval), both over the explicit cell bounds (compressed
+        cells are expanded once, on the device)."""
         if not (tau_relu > 0 and tau_max > 0):
             raise ValueError("tau_relu and tau_max must be positive")
-        if not self.spec.affine_identity or self._pending_rows() is not None:
-            raise NotImplementedError("the log-space acquisitions (qLogNEHVI / qLogEHVI) run affine objectives on "
-                                      "every output, without output constraints or qEHVI pending points, on the "
-                                      "device; use qNEHVI / qEHVI for those")
         lo, hi = self.cells.explicit()
-        st = _native.EvrQnehviState.from_buffer_copy(self.state)
-        st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
-        st.cell_keys = st.cell_pts = st.cell_rank0 = None
-        st.grp_off = st.grp_keys = st.grp_rank = st.grp_box = st.sorted_lo = None
-        st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
+
+        def logify(src):
+            st = _native.EvrQnehviState.from_buffer_copy(src)
+            st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
+            st.cell_keys = st.cell_pts = st.cell_rank0 = None
+            st.grp_off = st.grp_keys = st.grp_rank = st.grp_box = st.sorted_lo = None
+            st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
+            return st
         self._log_cells = (lo, hi)
-        self.state = st
+        self.state_scan = logify(self.state_scan)
+        self.state = logify(self.state)
+        if self.spec.affine_identity:
+            self.state_model = self.state
         self.tau_relu, self.tau_max = float(tau_relu), float(tau_max)
         self.log_acqf = True      # may be negative: optimize_acqf uses initialize_q_batch
         self._plans = {}
@@ -237,9 +241,6 @@ class _BoxHviAcqf:
     def _general(self, X: torch.Tensor, backward: bool, gout: Optional[torch.Tensor] = None):
         """X: b x q x d -> (acq (b), dX b x q x d | None) through evr_qng_eval; fixed pending
         points (qEHVI) join every candidate's joint batch."""
-        if getattr(self, "log_acqf", False):
-            raise NotImplementedError("q > 1 / output constraints / CloseToTarget for the log-space "
-                                      "acquisitions (qLogNEHVI, qLogEHVI) are not implemented on the device")
         b, q, d = X.shape
         Xp = self._pending_rows()
         qq = q
@@ -249,8 +250,9 @@ class _BoxHviAcqf:
         if qq > 8:
             raise ValueError(f"joint batch of {qq} points (q + pending) exceeds the device limit of 8")
         g = self.spec.struct(qq, self._zq(qq))
-        acq, dX = ops.qng_eval(self.state_model, self.state_scan, g, self.model, X.reshape(b * qq, d).contiguous(),
-                               backward, gout)
+        ev = ops.qlog_eval if getattr(self, "log_acqf", False) else ops.qng_eval
+        acq, dX = ev(self.state_model, self.state_scan, g, self.model, X.reshape(b * qq, d).contiguous(),
+                     backward, gout)
         if dX is not None:
             dX = dX.view(b, qq, d)[:, :q].contiguous()
         return acq, dX
@@ -293,7 +295,7 @@ class _BoxHviAcqf:
             stm = self.state if fast else self.state_model
             sth = self.state if fast else self.state_scan
             acq = torch.classes.everest_amd.QnehviAcq(raw(stm), raw(sth), raw(self.model), bool(fast),
-                                                      self._device_tensors())
+                                                      bool(getattr(self, "log_acqf", False)), self._device_tensors())
             acq._general_q = set()
             cache[fast] = acq
         if not fast and q not in acq._general_q:
@@ -316,8 +318,6 @@ class _BoxHviAcqf:
         X3, _ = self._split(X)
         if self._fast(X3):
             return QnehviFunction.apply(X3[:, 0].contiguous(), self._torch_acq(1, True))
-        if getattr(self, "log_acqf", False):
-            raise NotImplementedError("q > 1 for the log-space acquisitions is not implemented on the device")
         Xp = self._pending_rows()
         if Xp is not None:
             X3 = torch.cat([X3, Xp.unsqueeze(0).expand(X3.shape[0], Xp.shape[0], X3.shape[2])], 1)

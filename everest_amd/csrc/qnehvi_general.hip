@@ -623,6 +623,322 @@ static int qg_check(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, co
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Log-space general scan: [upstream] qLogExpectedHypervolumeImprovement._compute_log_qehvi
+// (fat = True; shared by qLogNoisyExpectedHypervolumeImprovement) for q-point candidates,
+// objectives over selected outputs and output constraints — MoboStrategy's default
+// acquisition (bofire/strategies/predictives/mobo.py:47-90).  Per MC sample s, candidate c,
+// explicit cell [l, u] of the sample's partition and q-subset T:
+//   a_ik   = log fatplus(g_k(y_i) - l_k; tau_relu)
+//   z_k(T) = fatmin_{i in T} a_ik                       (tau_max)
+//   A(T)   = sum_k fatmin(z_k(T), log(min(u_k, 1e10) - l_k)) + sum_{i in T} lf_i
+//   cell   = logdiffexp(logsumexp_{|T| odd} A(T), logsumexp_{|T| even} A(T))
+//   LSE_sc = logsumexp_cells cell,   acq_c = logmeanexp_s LSE_sc
+// lf_i = sum_t logsigmoid(-c_t(y_i) / eta_t) (log feasibility).  A workgroup owns (sample,
+// CT candidates, range of cells); the cells are staged through LDS with their log lengths;
+// each thread keeps an online log-sum-exp over its cells with Q (m_obj + 1) gradient slots
+// (d / d g_ik and d / d lf_i), merged over the thread groups and splits in a fixed order.
+// The backward walks the subsets a second time with the cell's final odd / even sums:
+// d cell / d A(T) = +-exp(A(T) - cell).
+// ---------------------------------------------------------------------------------------
+constexpr int QL_THREADS = 256, QL_CHUNK = 128;
+
+// fat-min over the members of subset T of x[0..Q) and its partials (members only)
+template <int Q>
+__device__ __forceinline__ double ql_fatmin_set(unsigned T, const double* x, double t, double* dz) {
+  double xmin = INFINITY;
+  int am = 0;
+#pragma unroll
+  for (int i = 0; i < Q; ++i)
+    if ((T >> i & 1) && x[i] < xmin) {
+      xmin = x[i];
+      am = i;
+    }
+  if (!(T & (T - 1))) {   // a single point: exactly x
+    if (dz)
+#pragma unroll
+      for (int i = 0; i < Q; ++i) dz[i] = (int)i == am ? 1.0 : 0.0;
+    return xmin;
+  }
+  double S = 0.0, sp = 0.0;
+  double pp[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    pp[i] = 0.0;
+    if (T >> i & 1) {
+      const double u = (x[i] - xmin) / t;
+      const double p = 2.0 / (2.0 + u * (2.0 + u));
+      S += p;
+      pp[i] = (1.0 + u) * p * p;   // -pareto'(u)
+      if (i != am) sp += pp[i];
+    }
+  }
+  if (dz) {
+#pragma unroll
+    for (int i = 0; i < Q; ++i) dz[i] = (T >> i & 1) ? (i == am ? 1.0 - sp / S : pp[i] / S) : 0.0;
+  }
+  return xmin - t * log(S);
+}
+
+template <int MM, int Q, bool BWD>
+__global__ __launch_bounds__(QL_THREADS) void qlog_scan(int b, int nsplit, int CT, int CB, QgObj o,
+                                                        const double* __restrict__ Y,
+                                                        const int* __restrict__ off, const double* __restrict__ lo,
+                                                        const double* __restrict__ hi, double tr, double tm,
+                                                        double* __restrict__ out) {
+  constexpr int NG = Q * (MM + 1);
+  constexpr int NO = 2 + (BWD ? NG : 0);
+  constexpr unsigned NSUB = (1u << Q) - 1u;
+  __shared__ double Ls[QL_CHUNK][MM];
+  __shared__ double Ws[QL_CHUNK][MM];
+  __shared__ double red[QL_THREADS / 2][NO];   // tree merge of the thread groups (GR a power of two)
+  const int s = blockIdx.y, split = blockIdx.z, tid = threadIdx.x;
+  const int mo = o.mo, bq = b * Q;
+  const int GR = QL_THREADS / CT;
+  const int cl = tid % CT, g = tid / CT;
+  const int c = blockIdx.x * CT + cl;
+  // this thread's candidate: objectives and log feasibility of its Q points
+  double gv[Q][MM], lf[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    lf[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < MM; ++k) gv[i][k] = 0.0;
+    if (c < b) {
+      double gg[QG_MAXM], w;
+      qg_point(o, Y + (size_t)s * o.m * bq + (size_t)c * Q + i, (size_t)bq, gg, w);
+      double l = 0.0;
+      for (int t = 0; t < o.nc; ++t) {
+        const double cval = o.cs[t] * (Y[((size_t)s * o.m + o.co[t]) * bq + (size_t)c * Q + i] - o.ct[t]);
+        l += qg_logsig(-cval / o.ce[t]);
+      }
+      lf[i] = l;
+#pragma unroll
+      for (int k = 0; k < MM; ++k) gv[i][k] = k < mo ? gg[k] : 0.0;
+    }
+  }
+  LseState<NG, BWD> st;
+  st.init();
+  const int k0 = off[s] + split * CB;
+  const int k1 = min(off[s + 1], k0 + CB);
+  for (int ks = k0; ks < k1; ks += QL_CHUNK) {
+    const int nc = min(QL_CHUNK, k1 - ks);
+    __syncthreads();
+    for (int e = tid; e < nc * mo; e += QL_THREADS) {
+      const int cell = e / mo, j = e - cell * mo;
+      const double l = lo[(size_t)ks * mo + e];
+      const double u = fmin(hi[(size_t)ks * mo + e], HL_UMAX);
+      Ls[cell][j] = l;
+      Ws[cell][j] = log(u - l);
+    }
+    __syncthreads();
+    if (c >= b) continue;
+    for (int kc = g; kc < nc; kc += GR) {
+      double a[Q][MM], da[Q][MM];
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int k = 0; k < MM; ++k) {
+          a[i][k] = 0.0;
+          da[i][k] = 0.0;
+          if (k < mo) a[i][k] = log_fatplus(gv[i][k] - Ls[kc][k], tr, BWD ? &da[i][k] : nullptr);
+        }
+      // forward: online log-sum-exp of the odd / even subsets
+      double mp = -INFINITY, sp = 0.0, mn = -INFINITY, sn = 0.0;
+      for (unsigned T = 1; T <= NSUB; ++T) {
+        double A = 0.0;
+#pragma unroll
+        for (int k = 0; k < MM; ++k) {
+          if (k >= mo) continue;
+          double xk[Q];
+#pragma unroll
+          for (int i = 0; i < Q; ++i) xk[i] = a[i][k];
+          const double z = ql_fatmin_set<Q>(T, xk, tm, nullptr);
+          A += fatmin2(z, Ws[kc][k], tm, nullptr);
+        }
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+          if (T >> i & 1) A += lf[i];
+        if (A == -INFINITY) continue;
+        double& m_ = (__builtin_popcount(T) & 1) ? mp : mn;
+        double& s_ = (__builtin_popcount(T) & 1) ? sp : sn;
+        if (A > m_) {
+          s_ = fma(s_, exp(m_ - A), 1.0);
+          m_ = A;
+        } else {
+          s_ += exp(A - m_);
+        }
+      }
+      if (sp == 0.0) continue;
+      const double la = mp + log(sp), lb = sn > 0.0 ? mn + log(sn) : -INFINITY;
+      if (!(la > lb)) continue;
+      const double d = lb - la;
+      const double cell = la + (d > -0.6931471805599453 ? log(-expm1(d)) : log1p(-exp(d)));
+      double gcell[BWD ? NG : 1];
+      if (BWD) {
+        double ga[Q][MM], glf[Q];
+#pragma unroll
+        for (int i = 0; i < Q; ++i) {
+          glf[i] = 0.0;
+#pragma unroll
+          for (int k = 0; k < MM; ++k) ga[i][k] = 0.0;
+        }
+        for (unsigned T = 1; T <= NSUB; ++T) {
+          double A = 0.0, dl[MM], dzk[MM][Q];
+#pragma unroll
+          for (int k = 0; k < MM; ++k) {
+            dl[k] = 0.0;
+            if (k >= mo) continue;
+            double xk[Q];
+#pragma unroll
+            for (int i = 0; i < Q; ++i) xk[i] = a[i][k];
+            const double z = ql_fatmin_set<Q>(T, xk, tm, dzk[k]);
+            A += fatmin2(z, Ws[kc][k], tm, &dl[k]);
+          }
+#pragma unroll
+          for (int i = 0; i < Q; ++i)
+            if (T >> i & 1) A += lf[i];
+          if (A == -INFINITY) continue;
+          const double cT = ((__builtin_popcount(T) & 1) ? 1.0 : -1.0) * exp(A - cell);
+#pragma unroll
+          for (int i = 0; i < Q; ++i) {
+            if (!(T >> i & 1)) continue;
+            glf[i] += cT;
+#pragma unroll
+            for (int k = 0; k < MM; ++k)
+              if (k < mo) ga[i][k] = fma(cT * dl[k], dzk[k][i], ga[i][k]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < Q; ++i) {
+#pragma unroll
+          for (int k = 0; k < MM; ++k) gcell[i * (MM + 1) + k] = ga[i][k] * da[i][k];
+          gcell[i * (MM + 1) + MM] = glf[i];
+        }
+      }
+      st.add(cell, gcell);
+    }
+  }
+  for (int h = GR / 2; h >= 1; h /= 2) {   // fixed pairing: deterministic
+    __syncthreads();
+    if (g >= h && g < 2 * h) {
+      double* r = red[(g - h) * CT + cl];
+      r[0] = st.m;
+      r[1] = st.s0;
+      if (BWD) {
+#pragma unroll
+        for (int j = 0; j < NG; ++j) r[2 + j] = st.g[j];
+      }
+    }
+    __syncthreads();
+    if (g < h) {
+      const double* r = red[g * CT + cl];
+      st.merge(r[0], r[1], r + 2);
+    }
+  }
+  if (g == 0 && c < b) {
+    double* ob = out + ((size_t)s * nsplit + split) * NO * b;
+    ob[c] = st.m;
+    ob[(size_t)b + c] = st.s0;
+    if (BWD) {
+#pragma unroll
+      for (int j = 0; j < NG; ++j) ob[(size_t)(2 + j) * b + c] = st.g[j];
+    }
+  }
+}
+
+// thread per candidate: merge the splits per sample -> LSE_sc (split 0's m slot), the
+// normalised gradient slots (g / s0) in split 0, acq_c = logmeanexp_s; w_s (slot s0 of split
+// 0) = gout softmax_s weight for the backward; NaN where the new-point Cholesky failed
+template <int MM, int Q, bool BWD>
+__global__ void qlog_reduce(int b, int S, int nsplit, int m, double* __restrict__ ws, const int* __restrict__ flags,
+                            const double* __restrict__ gout, double* __restrict__ acq) {
+  constexpr int NG = Q * (MM + 1);
+  constexpr int NO = 2 + (BWD ? NG : 0);
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  double mx = -INFINITY;
+  for (int s = 0; s < S; ++s) {
+    double* o = ws + (size_t)s * nsplit * NO * b;
+    LseState<NG, BWD> st;
+    st.m = o[c];
+    st.s0 = o[(size_t)b + c];
+    if (BWD)
+      for (int j = 0; j < NG; ++j) st.g[j] = o[(size_t)(2 + j) * b + c];
+    for (int q = 1; q < nsplit; ++q) {
+      const double* r = o + (size_t)q * NO * b;
+      double g2[BWD ? NG : 1];
+      if (BWD)
+        for (int j = 0; j < NG; ++j) g2[j] = r[(size_t)(2 + j) * b + c];
+      st.merge(r[c], r[(size_t)b + c], g2);
+    }
+    const double lse = (st.s0 > 0.0) ? st.m + log(st.s0) : -INFINITY;
+    o[c] = lse;
+    if (BWD)
+      for (int j = 0; j < NG; ++j) o[(size_t)(2 + j) * b + c] = (st.s0 > 0.0) ? st.g[j] / st.s0 : 0.0;
+    mx = fmax(mx, lse);
+  }
+  double sum = 0.0;
+  if (mx > -INFINITY)
+    for (int s = 0; s < S; ++s) sum += exp(ws[(size_t)s * nsplit * NO * b + c] - mx);
+  const double lme = (mx > -INFINITY) ? mx + log(sum) - log((double)S) : -INFINITY;
+  bool bad = false;
+  for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + c] != 0;
+  acq[c] = bad ? nan("") : lme;
+  if (BWD) {
+    const double go = gout ? gout[c] : 1.0;
+    for (int s = 0; s < S; ++s) {
+      double* o = ws + (size_t)s * nsplit * NO * b;
+      o[(size_t)b + c] = (lme > -INFINITY) ? go * exp(o[c] - lme) / (double)S : 0.0;
+    }
+  }
+}
+
+// thread per (sample, point): dY[s][j][p] from the weighted gradient slots through the
+// objectives and the log feasibility (d logsigmoid(x)/dx = sigmoid(-x))
+template <int MM, int Q>
+__global__ void qlog_dy(int b, int S, int nsplit, QgObj o, const double* __restrict__ Y,
+                        const double* __restrict__ ws, double* __restrict__ dY) {
+  constexpr int NG = Q * (MM + 1);
+  constexpr int NO = 2 + NG;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int bq = b * Q;
+  if (e >= (long long)S * bq) return;
+  const int s = (int)(e / bq), p = (int)(e % bq), c = p / Q, i = p % Q;
+  const double* ob = ws + (size_t)s * nsplit * NO * b;
+  const double w = ob[(size_t)b + c];
+  const double* Ys = Y + (size_t)s * o.m * bq + p;
+  double dy[QG_MAXM];
+  for (int j = 0; j < QG_MAXM; ++j) dy[j] = 0.0;
+  for (int k = 0; k < o.mo; ++k) {
+    const int jj = o.oo[k];
+    dy[jj] += w * ob[(size_t)(2 + i * (MM + 1) + k) * b + c] * qg_dobj(o, k, Ys[(size_t)jj * bq]);
+  }
+  const double glf = w * ob[(size_t)(2 + i * (MM + 1) + MM) * b + c];
+  for (int t = 0; t < o.nc; ++t) {
+    const int jj = o.co[t];
+    const double cval = o.cs[t] * (Ys[(size_t)jj * bq] - o.ct[t]);
+    dy[jj] += glf * qg_sig(cval / o.ce[t]) * (-o.cs[t] / o.ce[t]);
+  }
+  for (int j = 0; j < o.m; ++j) dY[((size_t)s * o.m + j) * bq + p] = dy[j];
+}
+
+struct QlPlan {
+  int CT, nsplit, CB;
+};
+
+static QlPlan ql_plan(const evr_qnehvi_state* sth, int b) {
+  QlPlan p;
+  p.CT = b >= 48 ? 64 : (b > 16 ? 32 : 16);
+  const int ctiles = cdiv(b, p.CT);
+  const int maxc = std::max(sth->max_cells, 1);
+  const int want = std::max(1, cdiv(2048, (long long)ctiles * sth->S));
+  p.nsplit = std::min(want, cdiv(maxc, QL_CHUNK));
+  p.CB = cdiv(cdiv(maxc, p.nsplit), QL_CHUNK) * QL_CHUNK;
+  p.nsplit = cdiv(maxc, p.CB);
+  return p;
+}
+
 #define QG_SWITCH(q, MACRO)                                                             \
   switch (q) {                                                                          \
     case 1: MACRO(1); break;                                                            \
@@ -635,6 +951,47 @@ static int qg_check(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, co
     case 8: MACRO(8); break;                                                            \
     default: EVR_CHECK(false, "qnehvi_general: q = %d not supported", q);               \
   }
+
+struct QlLayout {
+  size_t Kx, R, P, Wf, Y, Lq, flags, LW, dY, cf, dKqq, cm, gR, dKx, kg, total;
+  QlPlan plan;
+  int MM;
+};
+
+static QlLayout ql_layout(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, int q, int d, int b,
+                          bool backward) {
+  QlLayout L{};
+  const size_t m = stm->m, n = stm->n, S = stm->S, bq = (size_t)b * q;
+  const size_t Rr = (size_t)qn_rows(stm);
+  L.MM = sth->m <= 4 ? 4 : 8;
+  L.plan = ql_plan(sth, b);
+  const size_t NO = 2 + (backward ? (size_t)q * (L.MM + 1) : 0);
+  size_t o = 0;
+  auto take = [&](size_t doubles) {
+    const size_t r = o;
+    o += (doubles + 31) & ~(size_t)31;
+    return r;
+  };
+  L.Kx = take(m * n * bq);
+  L.R = take(m * Rr * bq);
+  L.P = take(m * (size_t)evr_qnehvi_norms_rows(stm) * 2 * bq);
+  L.Wf = take(proj_forward_ws_doubles(stm, (int)bq));
+  L.Y = take(S * m * bq);
+  L.Lq = take(m * b * q * q);
+  L.flags = take((m * b + 1) / 2);
+  L.LW = take(S * (size_t)L.plan.nsplit * NO * b);
+  if (backward) {
+    L.dY = take(S * m * bq);
+    L.cf = take(m * b * q * q);
+    L.dKqq = take(m * b * q * q);
+    L.cm = take(m * bq);
+    L.gR = take(m * Rr * bq);
+    L.dKx = take(m * n * bq);
+    L.kg = take(kcross_grad_ws_doubles((int)n, (int)bq, d));
+  }
+  L.total = o;
+  return L;
+}
 
 }  // namespace evr
 
@@ -744,6 +1101,111 @@ int evr_objective_weights(void* stream, int m_model, int n, const evr_qn_general
   if (n == 0) return 0;
   qg_weights_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(n, o, Y, G, W);
   EVR_LAUNCH_CHECK();
+  return 0;
+}
+
+long long evr_qlog_workspace_doubles(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
+                                     const evr_qnehvi_model* md, int b, int backward) {
+  if (!stm || !sth || !g || !md || b <= 0 || g->q < 1 || g->q > EVR_QNG_MAX_Q) return 0;
+  return (long long)ql_layout(stm, sth, g->q, md->d, b, backward != 0).total;
+}
+
+int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
+                  const evr_qnehvi_model* md, int b, const double* X, const double* gout, double* work, double* acq,
+                  double* dX) {
+  EVR_CHECK(stm && sth && g && md, "evr_qlog_eval: null argument");
+  EVR_CHECK(g->q >= 1 && g->q <= EVR_QNG_MAX_Q, "evr_qlog_eval: q = %d outside 1..%d", g->q, EVR_QNG_MAX_Q);
+  EVR_CHECK(sth->m == g->m_obj && sth->S == stm->S && sth->cell_lo && sth->cell_hi && sth->cell_off,
+            "evr_qlog_eval: the scan state must carry m = m_obj objectives, the same S and explicit cells");
+  EVR_CHECK(sth->tau_relu > 0.0 && sth->tau_max > 0.0, "evr_qlog_eval: tau_relu / tau_max must be positive");
+  EVR_CHECK(md->n == stm->n && md->d >= 1 && md->M && md->Xn && md->lengthscales && g->zq && stm->c && stm->ym &&
+                stm->ys && stm->kxx,
+            "evr_qlog_eval: inconsistent model / state");
+  EVR_CHECK(X && work && acq && b >= 0, "evr_qlog_eval: bad arguments");
+  if (b == 0) return 0;
+  QgObj o;
+  if (int rc = qg_params(g, stm->m, &o)) return rc;
+  if (int rc = gemm_backend_init()) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int q = g->q, m = stm->m, n = stm->n, d = md->d, S = stm->S;
+  const int bq = b * q;
+  const bool backward = dX != nullptr;
+  const QlLayout L = ql_layout(stm, sth, q, d, b, backward);
+  double* w = work;
+  double* Kx = w + L.Kx;
+  double* R = w + L.R;
+  double* Y = w + L.Y;
+  double* Lq = w + L.Lq;
+  int* flags = (int*)(w + L.flags);
+  double* LW = w + L.LW;
+  const QgDims dm{n, stm->nb, qn_nh(stm), S, m, b};
+  if (int rc = evr_kernel_matrix(s, md->kind, m, n, bq, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
+                                 md->lengthscales, nullptr, nullptr, Kx))
+    return rc;
+  if (int rc = proj_forward(s, stm, bq, md->M, Kx, R, w + L.P, L.Wf != L.Y ? w + L.Wf : nullptr)) return rc;
+  const QlPlan& P = L.plan;
+  const dim3 grid(cdiv(b, P.CT), S, P.nsplit);
+#define GO(QQ)                                                                                                    \
+  qg_gram_samples<QQ><<<dim3(b, m), 256, 0, s>>>(dm, md->kind, d, R, X, md->lengthscales, md->shift, md->scale,    \
+                                                 stm->c, stm->ym, stm->ys, stm->kxx, g->zq, Y, Lq, flags);        \
+  EVR_LAUNCH_CHECK();                                                                                             \
+  if (L.MM == 4) {                                                                                                \
+    if (backward) qlog_scan<4, QQ, true><<<grid, QL_THREADS, 0, s>>>(b, P.nsplit, P.CT, P.CB, o, Y, sth->cell_off,  \
+                                                                 sth->cell_lo, sth->cell_hi, sth->tau_relu,       \
+                                                                 sth->tau_max, LW);                               \
+    else qlog_scan<4, QQ, false><<<grid, QL_THREADS, 0, s>>>(b, P.nsplit, P.CT, P.CB, o, Y, sth->cell_off,          \
+                                                          sth->cell_lo, sth->cell_hi, sth->tau_relu, sth->tau_max, \
+                                                          LW);                                                    \
+    EVR_LAUNCH_CHECK();                                                                                           \
+    if (backward) qlog_reduce<4, QQ, true><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
+    else qlog_reduce<4, QQ, false><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
+    EVR_LAUNCH_CHECK();                                                                                           \
+    if (backward) qlog_dy<4, QQ><<<cdiv((long long)S * bq, 256), 256, 0, s>>>(b, S, P.nsplit, o, Y, LW, w + L.dY); \
+  } else {                                                                                                        \
+    if (backward) qlog_scan<8, QQ, true><<<grid, QL_THREADS, 0, s>>>(b, P.nsplit, P.CT, P.CB, o, Y, sth->cell_off,  \
+                                                                 sth->cell_lo, sth->cell_hi, sth->tau_relu,       \
+                                                                 sth->tau_max, LW);                               \
+    else qlog_scan<8, QQ, false><<<grid, QL_THREADS, 0, s>>>(b, P.nsplit, P.CT, P.CB, o, Y, sth->cell_off,          \
+                                                          sth->cell_lo, sth->cell_hi, sth->tau_relu, sth->tau_max, \
+                                                          LW);                                                    \
+    EVR_LAUNCH_CHECK();                                                                                           \
+    if (backward) qlog_reduce<8, QQ, true><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
+    else qlog_reduce<8, QQ, false><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
+    EVR_LAUNCH_CHECK();                                                                                           \
+    if (backward) qlog_dy<8, QQ><<<cdiv((long long)S * bq, 256), 256, 0, s>>>(b, S, P.nsplit, o, Y, LW, w + L.dY); \
+  }                                                                                                               \
+  EVR_LAUNCH_CHECK()
+  QG_SWITCH(q, GO);
+#undef GO
+  if (!backward) return 0;
+  double* dY = w + L.dY;
+  double* cf = w + L.cf;
+  double* dKqq = w + L.dKqq;
+  double* cm = w + L.cm;
+  double* gR = w + L.gR;
+  double* dKx = w + L.dKx;
+  const int Rr = qn_rows(stm);
+#define GO(QQ)                                                                                                   \
+  qg_samples_bwd<QQ><<<dim3(b, m), 256, 0, s>>>(dm, dY, g->zq, Lq, stm->ys, cf, dKqq, cm);                        \
+  EVR_LAUNCH_CHECK();                                                                                            \
+  qg_gen_gr<QQ><<<dim3(m * Rr, cdiv(bq, 256)), 256, 0, s>>>(dm, R, dY, cf, cm, stm->ys, gR);                      \
+  EVR_LAUNCH_CHECK()
+  QG_SWITCH(q, GO);
+#undef GO
+  if (int rc = rb_gemm(s, true, n, bq, Rr, md->M, n, (long long)Rr * n, gR, bq, (long long)Rr * bq, dKx, bq,
+                       (long long)n * bq, m))
+    return rc;
+  if (int rc = kcross_grad_launch(s, md->kind, m, n, bq, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
+                                  md->lengthscales, nullptr, dKx, dX, w + L.kg))
+    return rc;
+  if (q > 1) {
+#define GO(QQ)                                                                                                   \
+  qg_kqq_grad<QQ><<<cdiv(bq, 64), 64, 0, s>>>(b, m, d, md->kind, X, md->lengthscales, md->shift, md->scale,       \
+                                              stm->kxx, dKqq, dX);                                               \
+  EVR_LAUNCH_CHECK()
+    QG_SWITCH(q, GO);
+#undef GO
+  }
   return 0;
 }
 

@@ -150,9 +150,11 @@ struct QnehviAcq : torch::CustomClassHolder {
     return v;
   }
 
-  QnehviAcq(const at::Tensor& stm_b, const at::Tensor& sth_b, const at::Tensor& md_b, bool fast_,
+  bool log_scan = false;   // general path through evr_qlog_eval (qLogNEHVI / qLogEHVI)
+
+  QnehviAcq(const at::Tensor& stm_b, const at::Tensor& sth_b, const at::Tensor& md_b, bool fast_, bool log_,
             std::vector<at::Tensor> keep_)
-      : fast(fast_), keep(std::move(keep_)) {
+      : fast(fast_), keep(std::move(keep_)), log_scan(log_) {
     stm = from_bytes<evr_qnehvi_state>(stm_b, "model-side state");
     sth = from_bytes<evr_qnehvi_state>(sth_b, "scan-side state");
     md = from_bytes<evr_qnehvi_model>(md_b, "model");
@@ -244,10 +246,17 @@ struct QnehviAcq : torch::CustomClassHolder {
     auto acq = at::empty({b}, X.options());
     at::Tensor dX = backward ? at::empty_like(X) : at::Tensor();
     if (b == 0) return {acq, dX};
-    auto work = scratch(evr_qng_workspace_doubles(&stm, &sth, g, &md, (int)b, backward), X);
-    check(evr_qng_eval(s, &stm, &sth, g, &md, (int)b, X.data_ptr<double>(), nullptr, work.data_ptr<double>(),
-                       acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr),
-          "qng_eval");
+    if (log_scan) {
+      auto work = scratch(evr_qlog_workspace_doubles(&stm, &sth, g, &md, (int)b, backward), X);
+      check(evr_qlog_eval(s, &stm, &sth, g, &md, (int)b, X.data_ptr<double>(), nullptr, work.data_ptr<double>(),
+                          acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr),
+            "qlog_eval");
+    } else {
+      auto work = scratch(evr_qng_workspace_doubles(&stm, &sth, g, &md, (int)b, backward), X);
+      check(evr_qng_eval(s, &stm, &sth, g, &md, (int)b, X.data_ptr<double>(), nullptr, work.data_ptr<double>(),
+                         acq.data_ptr<double>(), backward ? dX.data_ptr<double>() : nullptr),
+            "qng_eval");
+    }
     ++n_evals;
     return {acq, dX};
   }
@@ -281,7 +290,7 @@ at::Tensor qnehvi_backward(const AcqPtr& acq, const at::Tensor& X, const at::Ten
 
 TORCH_LIBRARY(everest_amd, m) {
   m.class_<QnehviAcq>("QnehviAcq")
-      .def(torch::init<at::Tensor, at::Tensor, at::Tensor, bool, std::vector<at::Tensor>>())
+      .def(torch::init<at::Tensor, at::Tensor, at::Tensor, bool, bool, std::vector<at::Tensor>>())
       .def("set_general", &QnehviAcq::set_general)
       .def("evals", &QnehviAcq::evals)
       .def("cached_plans", &QnehviAcq::cached_plans);

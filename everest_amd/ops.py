@@ -501,6 +501,26 @@ def qng_eval(stm: EvrQnehviState, sth: EvrQnehviState, g: EvrQnGeneral, model: "
     return acq, dX
 
 
+def qlog_eval(stm: EvrQnehviState, sth: EvrQnehviState, g: EvrQnGeneral, model: "_native.EvrQnehviModel",
+              X: torch.Tensor, backward: bool, gout: Optional[torch.Tensor] = None):
+    """Log-space general qLogNEHVI / qLogEHVI (evr_qlog_eval): X (b*q) x d raw candidates ->
+    acq (b) [, dX (b*q) x d]; ``sth`` carries the explicit cells and tau_relu / tau_max."""
+    X = _dev(X, "X")
+    q = int(g.q)
+    bq, d = X.shape
+    if bq % q:
+        raise ValueError(f"{bq} rows are not a multiple of q = {q}")
+    b = bq // q
+    lib = _native.load()
+    work = _workspace(lib.evr_qlog_workspace_doubles(ctypes.byref(stm), ctypes.byref(sth), ctypes.byref(g),
+                                                     ctypes.byref(model), b, int(backward)), X.device)
+    acq = torch.empty(b, dtype=torch.float64, device=X.device)
+    dX = torch.empty_like(X) if backward else None
+    call("evr_qlog_eval", _stream(), ctypes.byref(stm), ctypes.byref(sth), ctypes.byref(g), ctypes.byref(model), b,
+         X.data_ptr(), _p(None if gout is None else _dev(gout, "gout")), work.data_ptr(), acq.data_ptr(), _p(dX))
+    return acq, dX
+
+
 class QnehviPlan:
     """Native evaluation plan of the whole qNEHVI chain for a fixed batch size b
     (qnehvi_plan.hip): persistent device buffers X (b x d), out = [acq (b) | dX (b x d)] and

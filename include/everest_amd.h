@@ -355,6 +355,18 @@ long long evr_qng_workspace_doubles(const evr_qnehvi_state* stm, const evr_qnehv
 int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
                  const evr_qnehvi_model* md, int b, const double* X, const double* gout, double* work,
                  double* acq, double* dX);
+/* Log-space general evaluation ([upstream] qLogExpectedHypervolumeImprovement._compute_log_qehvi,
+ * fat = True; qLogNEHVI / qLogEHVI, MoboStrategy's default, bofire/strategies/predictives/
+ * mobo.py:47-90): as evr_qng_eval, with `sth` carrying EXPLICIT cells (cell_lo / cell_hi /
+ * cell_off) and tau_relu / tau_max; per cell the q-subset areas are combined in log space
+ * (log fatplus improvements, fat-min over the subset's points and with the log cell lengths,
+ * log feasibilities summed over the subset, odd minus even sizes by logdiffexp), logsumexp
+ * over the cells, logmeanexp over the samples. */
+long long evr_qlog_workspace_doubles(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
+                                     const evr_qnehvi_model* md, int b, int backward);
+int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, const evr_qn_general* g,
+                  const evr_qnehvi_model* md, int b, const double* X, const double* gout, double* work,
+                  double* acq, double* dX);
 /* Objectives of baseline / prune samples (Y: m_model x n x S plus mu: m_model x n, nullable)
  * with hard feasibility: O[k][i][s] = g_k(y), or ref[k] where any constraint c > 0
  * ([upstream] prune_inferior_points_multi_objective and the qNEHVI baseline partitions drop

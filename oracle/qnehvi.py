@@ -323,32 +323,96 @@ def logmeanexp(x: torch.Tensor, dim: int) -> torch.Tensor:
     return torch.logsumexp(x, dim=dim) - math.log(x.shape[dim])
 
 
+def logdiffexp(log_a: torch.Tensor, log_b: torch.Tensor) -> torch.Tensor:
+    """log(exp(a) - exp(b)) for b <= a (safe_math.logdiffexp: a + log1mexp(b - a));
+    -inf where the difference is not positive (a cell whose smoothed odd and even subset sums
+    cancel contributes nothing instead of a NaN)."""
+    d = log_b - log_a
+    l1m = torch.where(d > -math.log(2.0), torch.log(-torch.expm1(d)), torch.log1p(-torch.exp(d)))
+    out = log_a + l1m
+    return torch.where((log_a > log_b) & torch.isfinite(log_a), out, torch.full_like(out, -math.inf))
+
+
+def log_qehvi_cells(obj: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, tau_relu: float, tau_max: float,
+                    log_feas: Optional[torch.Tensor] = None):
+    """[upstream] qLogExpectedHypervolumeImprovement._compute_log_qehvi (fat = True) for one
+    MC sample: obj b x q x m, cells lo / hi C x m, log_feas (b x q, log feasibility of each
+    point, or None) -> b.  Per cell and q-subset T: the log improvement log fatplus(g_i - l)
+    of every point, its fat-min over the points of T, the fat-min with log(min(u, 1e10) - l),
+    summed over the objectives (+ sum of log feasibilities over T); logsumexp over the subsets
+    of each size, odd sizes added and even sizes subtracted (logdiffexp), logsumexp over
+    the cells.  q = 1 equals log_hvi_cells."""
+    import itertools
+    b, q, m = obj.shape
+    log_len = (hi.clamp_max(UPPER_CLAMP) - lo).log()                           # C x m
+    pos = torch.full((b, lo.shape[0]), -math.inf, **TK)
+    neg = torch.full((b, lo.shape[0]), -math.inf, **TK)
+    for i in range(1, q + 1):
+        subs = list(itertools.combinations(range(q), i))
+        idx = torch.tensor(subs)                                               # n_i x i
+        o = obj[:, idx, :]                                                     # b x n_i x i x m
+        li = fatplus(o.unsqueeze(1) - lo[None, :, None, None, :], tau_relu).log()   # b x C x n_i x i x m
+        li = fatmin(li, dim=-2, tau=tau_max)                                   # b x C x n_i x m
+        ll = log_len[None, :, None, :].expand_as(li)
+        lens = fatmin(torch.stack([li, ll], -1), dim=-1, tau=tau_max)          # b x C x n_i x m
+        area = lens.sum(-1)                                                    # b x C x n_i
+        if log_feas is not None:
+            area = area + log_feas[:, idx].sum(-1).unsqueeze(1)
+        la = torch.logsumexp(area, dim=-1)                                     # b x C
+        if i % 2 == 1:
+            pos = torch.logaddexp(pos, la)
+        else:
+            neg = torch.logaddexp(neg, la)
+    return torch.logsumexp(logdiffexp(pos, neg), dim=-1)
+
+
+def log_feasibility(constraints: Optional[OutputConstraints], Y: torch.Tensor):
+    """Sum of logsigmoid(-c / eta) over the output constraints (None without constraints).
+    [upstream] compute_smoothed_feasibility_indicator(log=True) with fat = True uses a
+    fat-tailed sigmoid here; its exact form is not restated offline, so this build uses the
+    logistic one (fat = False) — parity unpinned."""
+    if constraints is None:
+        return None
+    c = constraints.values(Y)
+    eta = torch.as_tensor(list(constraints.eta), dtype=c.dtype)
+    return torch.nn.functional.logsigmoid(-c / eta).sum(-1)
+
+
 class QLogNEHVI(QNEHVI):
-    """qLogNEHVI (q = 1): the qNEHVI samples and per-sample cells, log-space fat-smoothed HVI,
-    logmeanexp over the samples."""
+    """qLogNEHVI: the qNEHVI samples and per-sample cells, log-space fat-smoothed HVI with
+    inclusion–exclusion over q-subsets (log_qehvi_cells), output-constraint log
+    feasibilities, logmeanexp over the samples."""
 
     def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
         super().__init__(*args, **kw)
         self.tau_relu, self.tau_max = tau_relu, tau_max
 
     def forward(self, Xn: torch.Tensor) -> torch.Tensor:
-        obj = self.obj(self.samples(Xn))                                     # S x b x 1 x m
-        lse = torch.stack([log_hvi_cells(obj[s, :, 0], self.cells[s][0], self.cells[s][1], self.tau_relu,
-                                         self.tau_max) for s in range(obj.shape[0])])
+        Y = self.samples(Xn)                                                  # S x b x q x m_model
+        obj = self.obj(Y)
+        lf = log_feasibility(self.constraints, Y)
+        lse = torch.stack([log_qehvi_cells(obj[s], self.cells[s][0], self.cells[s][1], self.tau_relu,
+                                           self.tau_max, None if lf is None else lf[s])
+                           for s in range(obj.shape[0])])
         return logmeanexp(lse, 0)
 
 
 class QLogEHVI(QEHVI):
-    """qLogEHVI (q = 1): the qEHVI samples and fixed partition, log-space fat-smoothed HVI."""
+    """qLogEHVI: the qEHVI samples (pending points joined) and fixed partition, log-space
+    fat-smoothed HVI over q-subsets."""
 
     def __init__(self, *args, tau_relu: float = TAU_RELU, tau_max: float = TAU_MAX_MO, **kw):
         super().__init__(*args, **kw)
         self.tau_relu, self.tau_max = tau_relu, tau_max
 
     def forward(self, Xn: torch.Tensor) -> torch.Tensor:
-        obj = self.obj(self.samples(Xn))[:, :, 0]                            # S x b x m
-        lse = torch.stack([log_hvi_cells(obj[s], self.cell[0], self.cell[1], self.tau_relu, self.tau_max)
-                           for s in range(obj.shape[0])])
+        if self.X_pending is not None:
+            Xn = torch.cat([Xn, self.X_pending.unsqueeze(0).expand(Xn.shape[0], *self.X_pending.shape)], -2)
+        Y = self.samples(Xn)
+        obj = self.obj(Y)
+        lf = log_feasibility(self.constraints, Y)
+        lse = torch.stack([log_qehvi_cells(obj[s], self.cell[0], self.cell[1], self.tau_relu, self.tau_max,
+                                           None if lf is None else lf[s]) for s in range(obj.shape[0])])
         return logmeanexp(lse, 0)
 
 

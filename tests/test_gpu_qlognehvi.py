@@ -105,3 +105,126 @@ def test_mobo_default_qlognehvi_tell_ask():
         assert 0.0 <= cand[k].iloc[0] <= 1.0
     vals = s.calc_acquisition(cand[bench.domain.inputs.get_keys()])
     assert np.isfinite(vals).all()
+
+
+# ---- general log path (evr_qlog_eval): q > 1, objectives over selected outputs /
+#      CloseToTarget, output constraints (log feasibility), qLogEHVI pending points ----------
+def _general_log(n, d, m, S, seed, q, objective=None, constraints=None, ref=None, nprune=64, ls_scale=1.0):
+    from everest_amd.acquisition import QLogNEHVI
+
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=seed)
+    for h in hyp:
+        h["lengthscale"] = h["lengthscale"] * ls_scale
+    ost = oracle_states(X, Y, lo, hi, hyp)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    if objective is None:
+        objective = [(j, 0, -1.0, 0.0) for j in range(m)]
+    mo = len(objective)
+    ref = -1.1 * np.ones(mo) if ref is None else np.asarray(ref, dtype=np.float64)
+    oobj = oq.GeneralObjective(*[list(t) for t in zip(*objective)])
+    ocon = None if not constraints else oq.OutputConstraints(*[list(t) for t in zip(*constraints)])
+    Xn = torch.tensor((X - lo) / (hi - lo))
+    zp = oq.base_samples(nprune, n, m, 11)
+    idx, _ = oq.prune_baseline(ost, Xn, oobj, torch.tensor(ref), zp, constraints=ocon)
+    nb = idx.shape[0]
+    zb = oq.base_samples(S, nb, m, 7)
+    zn = oq.base_samples(S, nb + q, m, 7)
+    orc = oq.QLogNEHVI(ost, Xn[idx], oobj, torch.tensor(ref), zb, zn[:, nb:nb + q, :], constraints=ocon)
+    dq = QLogNEHVI(gp, X, X, ref, None, None, S=S, prune_baseline=True, z_prune=zp, z_base_full=zb,
+                   z_new_full=zn, prune_samples=nprune, objective=objective, constraints=constraints or ())
+    return X, lo, hi, orc, dq
+
+
+def _check_general(dq, orc, lo, hi, Xc, atol=1e-9, gtol=1e-6):
+    acq, dX = dq.forward_backward(torch.tensor(Xc, device="cuda"))
+    xt = torch.tensor(Xc, requires_grad=True)
+    xn = (xt - torch.tensor(lo)) / torch.tensor(hi - lo)
+    ref = orc.forward(xn if xn.dim() == 3 else xn.unsqueeze(1))
+    ref.sum().backward()
+    assert torch.isfinite(ref).all() and torch.isfinite(acq).all()
+    assert torch.allclose(acq.cpu(), ref.detach(), rtol=1e-9, atol=atol), (acq.cpu() - ref.detach()).abs().max()
+    g = dX.cpu()
+    assert g.shape == xt.grad.shape
+    assert torch.allclose(g, xt.grad, rtol=gtol, atol=1e-9 * xt.grad.abs().max()), (g - xt.grad).abs().max()
+    fwd = dq.forward(torch.tensor(Xc, device="cuda"))
+    assert torch.allclose(fwd, acq, rtol=1e-12, atol=1e-12)
+    return acq
+
+
+def test_qlognehvi_general_q1_equals_fast_path():
+    """The general log scan at q = 1 with affine objectives reproduces the dense q = 1 kernel."""
+    X, lo, hi, orc, dq = _general_log(40, 4, 3, 16, seed=41, q=1)
+    assert dq.supports_plan
+    Xt = torch.tensor(lo + (hi - lo) * np.random.default_rng(2).uniform(size=(19, 4)), device="cuda")
+    a_fast, g_fast = dq.forward_backward(Xt)
+    a_gen, g_gen = dq._general(Xt.unsqueeze(1), True)
+    assert torch.allclose(a_gen, a_fast, rtol=1e-11, atol=1e-11)
+    assert torch.allclose(g_gen[:, 0], g_fast, rtol=1e-8, atol=1e-11 * g_fast.abs().max())
+
+
+@pytest.mark.parametrize("q", [2, 3])
+def test_qlognehvi_joint_batches(q):
+    X, lo, hi, orc, dq = _general_log(30, 3, 2, 12, seed=30 + q, q=q)
+    Xc = lo + (hi - lo) * np.random.default_rng(q).uniform(size=(9, q, 3))
+    _check_general(dq, orc, lo, hi, Xc)
+
+
+@pytest.mark.parametrize("q", [1, 2])
+def test_qlognehvi_constraints_close_to_target(q):
+    """MoboStrategy's default on a constrained domain: Minimize output 0, CloseToTarget on
+    output 1, a MaximizeSigmoid-style constraint on output 2 and a bound on output 0."""
+    objective = [(0, 0, -1.0, 0.0), (1, 1, 0.5, 1.5)]
+    constraints = [(2, -1.0, 0.3, 0.05), (0, 1.0, 0.9, 0.1)]
+    X, lo, hi, orc, dq = _general_log(45, 4, 3, 16, seed=19 + q, q=q, objective=objective,
+                                      constraints=constraints, ref=[-1.1, -1.0])
+    assert not dq.supports_plan
+    rng = np.random.default_rng(71)
+    Xc = lo + (hi - lo) * rng.uniform(size=(11, q, 4) if q > 1 else (11, 4))
+    _check_general(dq, orc, lo, hi, Xc)
+
+
+def test_qlogehvi_pending_joint_batch():
+    """qLogEHVI with a pending point joined to every candidate's batch (q = 1 + 1 pending)."""
+    from everest_amd.acquisition import QLogEHVI
+
+    n, d, m, S, q = 30, 3, 2, 16, 1
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=13)
+    ost = oracle_states(X, Y, lo, hi, hyp)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    a, b = -np.ones(m), np.zeros(m)
+    ref = -1.1 * np.ones(m)
+    Ypart = Y * a + b
+    Ypart = Ypart[(Ypart > ref).all(-1)]
+    Xp = lo + (hi - lo) * np.random.default_rng(3).uniform(size=(1, d))
+    z = oq.base_samples(S, q + 1, m, 5)
+    dq = QLogEHVI(gp, Ypart, ref, a, b, S=S, X_pending_raw=Xp)
+    dq.set_new_point_samples(q + 1, z)
+    assert not dq.supports_plan
+    orc = oq.QLogEHVI(ost, torch.tensor(Ypart), oq.Objective(torch.tensor(a), torch.tensor(b)), torch.tensor(ref), z,
+                      X_pending=torch.tensor((Xp - lo) / (hi - lo)))
+    Xc = lo + (hi - lo) * np.random.default_rng(8).uniform(size=(9, d))
+    _check_general(dq, orc, lo, hi, Xc)
+
+
+def test_mobo_default_constrained_ask_joint_batch():
+    """MoboStrategy() (default qLogNEHVI) on a domain with an output constraint and
+    CloseToTarget: ask(2) (one joint q = 2 problem) and ask(add_pending=True) run on the
+    device."""
+    bench = DTLZ2(dim=5, num_objectives=3)
+    rnd = strategies.map(dm.RandomStrategy(domain=bench.domain, seed=6))
+    exps = bench.f(rnd.ask(14), return_complete=True)
+    outs = dm.Outputs(features=[
+        dm.ContinuousOutput(key="f_0", objective=dm.MinimizeObjective(w=1.0)),
+        dm.ContinuousOutput(key="f_1", objective=dm.CloseToTargetObjective(target_value=0.4, exponent=2.0)),
+        dm.ContinuousOutput(key="f_2", objective=dm.MaximizeSigmoidObjective(tp=0.2, steepness=50.0))])
+    dom = dm.Domain(inputs=bench.domain.inputs, outputs=outs)
+    s = strategies.map(dm.MoboStrategy(domain=dom, seed=3, num_raw_samples=128, num_restarts=2,
+                                       acquisition_function=dm.qLogNEHVI(n_mc_samples=32)))
+    s.tell(exps)
+    cand = s.ask(2)
+    assert len(cand) == 2
+    v = s.calc_acquisition(cand[dom.inputs.get_keys()], combined=True)
+    assert v.shape == (1,) and np.isfinite(v).all()
+    c1 = s.ask(1, add_pending=True)
+    c2 = s.ask(1)
+    assert len(c1) == 1 and len(c2) == 1

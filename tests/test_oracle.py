@@ -202,3 +202,47 @@ def test_log_fatplus_cutoff_is_exact():
     c = 1.0 / (1.0 + x * x)
     assert np.array_equal(np.log1p(e) + 0.1 * c, 0.0 + 0.1 * c)
     assert np.array_equal(e / (1.0 + e) - 0.2 * x * c * c, 0.0 - 0.2 * x * c * c)
+
+
+@pytest.mark.parametrize("q", [1, 2, 3])
+def test_log_qehvi_subsets_tend_to_log_exact_hvi(q):
+    """The q-subset log restatement (log_qehvi_cells: logsumexp per subset size, odd minus
+    even by logdiffexp) tends to log of the exact inclusion–exclusion HVI as the
+    temperatures go to 0, equals log_hvi_cells at q = 1, and a log feasibility of 0 changes
+    nothing."""
+    import itertools
+
+    g = torch.Generator().manual_seed(q)
+    m = 3
+    P = torch.rand(12, m, dtype=torch.float64, generator=g)
+    ref = torch.zeros(m, dtype=torch.float64)
+    lo, hi = omo.nondominated_cells(omo.pareto_above_ref(P, ref), ref)
+    obj = torch.rand(6, q, m, dtype=torch.float64, generator=g) * 1.2
+    la = oq.log_qehvi_cells(obj, lo, hi, 1e-10, 1e-7)
+    ex = torch.zeros(6, dtype=torch.float64)
+    for i in range(1, q + 1):
+        for sub in itertools.combinations(range(q), i):
+            ov = obj[:, list(sub)].min(1).values
+            ex += (-1) ** (i + 1) * (torch.minimum(ov.unsqueeze(1), hi) - lo).clamp_min(0).prod(-1).sum(-1)
+    pos = ex > 1e-6
+    assert pos.sum() >= 2
+    assert torch.allclose(la.exp()[pos], ex[pos], rtol=1e-5)
+    assert (la.exp()[~pos] < 1e-5).all()
+    if q == 1:
+        assert torch.equal(oq.log_qehvi_cells(obj, lo, hi, 1e-6, 1e-3), oq.log_hvi_cells(obj[:, 0], lo, hi, 1e-6, 1e-3))
+    zero = torch.zeros(6, q, dtype=torch.float64)
+    assert torch.equal(oq.log_qehvi_cells(obj, lo, hi, 1e-6, 1e-3, zero), oq.log_qehvi_cells(obj, lo, hi, 1e-6, 1e-3))
+    # a log feasibility lf on every point scales the single-point areas by exp(lf): q = 1 shifts by lf
+    if q == 1:
+        lf = torch.full((6, 1), -0.7, dtype=torch.float64)
+        assert torch.allclose(oq.log_qehvi_cells(obj, lo, hi, 1e-6, 1e-3, lf),
+                              oq.log_qehvi_cells(obj, lo, hi, 1e-6, 1e-3) - 0.7, rtol=0, atol=1e-12)
+
+
+def test_logdiffexp():
+    a = torch.tensor([0.0, -1.0, 2.0, -math.inf, 1.0], dtype=torch.float64)
+    b = torch.tensor([-1.0, -math.inf, 2.0, -math.inf, -1e-12], dtype=torch.float64)
+    out = oq.logdiffexp(a, b)
+    assert torch.allclose(out[:2], torch.log(torch.exp(a[:2]) - torch.exp(b[:2])))
+    assert out[2] == -math.inf and out[3] == -math.inf
+    assert torch.allclose(out[4], torch.log(-torch.expm1(b[4] - a[4])) + a[4])
