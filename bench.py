@@ -96,15 +96,15 @@ def op_chain(acqf, Xc):
     st, gp, b = acqf.state, acqf.gp, Xc.shape[0]
     Kx = gp.cross(Xc)
     if ops.qnehvi_small_applies(st, b, Xc.shape[1]):
-        # restart batches: the plan's b <= 32 kernels (the cross-covariance is generated inside
-        # proj_fwd and its gradient fused into proj_bwd, so there is no kernel_matrix /
-        # kernel_grad op)
+        # restart batches: the plan's b <= 32 kernels (the cross-covariance gradient is fused
+        # into proj_bwd there, so there is no separate kernel_grad op)
         md = acqf.model
-        R, P = ops.qnehvi_small_forward_x(st, md, Xc, b)
+        R, P = ops.qnehvi_small_forward(st, md, Kx, b)
         G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
         acq, dG = ops.hvi_forward_backward(st, G, b, flags)
         return {
-            "proj_fwd": lambda: ops.qnehvi_small_forward_x(st, md, Xc, b),
+            "kernel_matrix": lambda: gp.cross(Xc),
+            "proj_fwd": lambda: ops.qnehvi_small_forward(st, md, Kx, b),
             "samples": lambda: ops.qnehvi_small_samples(st, R, P, b),
             "hvi_fwd_bwd": lambda: ops.hvi_forward_backward(st, G, b, flags),
             "proj_bwd": lambda: ops.qnehvi_small_backward(st, md, Xc, R, L22, dG, b),
@@ -508,8 +508,8 @@ def _work_table(acqf, b, S, m, d, sum_cells):
         # the samples' gradient and writes dX (cross-covariance gradient fused)
         nrt16 = math.ceil(Rr / 16)
         return {
-            # M streamed once; K_x is generated in the kernel (its bytes never reach HBM)
-            "proj_fwd": ("hbm", 8.0 * (m * Rr * n + n * d + b * d + m * Rr * b + 2 * m * nrt16 * b), "B"),
+            "kernel_matrix": ("hbm", 8.0 * (m * n * b + n * d + b * d + m * d), "B"),
+            "proj_fwd": ("hbm", 8.0 * (m * Rr * n + m * n * b + m * Rr * b + 2 * m * nrt16 * b), "B"),
             "samples": ("hbm", 8.0 * m * b * (S + 1 + 2 * nrt16) + 8.0 * S * m * b, "B"),
             "hvi_fwd_bwd": ("hbm", 16.0 * sum_cells * m + 8.0 * b * S * m + 8.0 * b, "B"),
             "proj_bwd": ("hbm", 8.0 * (m * Rr * n + m * Rr * b + S * m * b + n * d + b * d), "B"),

@@ -296,9 +296,9 @@ class _BoxHviAcqf:
             sth = self.state if fast else self.state_scan
             acq = torch.classes.everest_amd.QnehviAcq(raw(stm), raw(sth), raw(self.model), bool(fast),
                                                       bool(getattr(self, "log_acqf", False)), self._device_tensors())
-            acq._general_q = set()
             cache[fast] = acq
-        if not fast and q not in acq._general_q:
+        done = self.__dict__.setdefault("_torch_general_q", set())
+        if not fast and q not in done:
             spec = self.spec
             oo, ok, p0, p1 = spec._arrs
             cons = spec.constraints
@@ -306,7 +306,7 @@ class _BoxHviAcqf:
             cs, ct, ce = (torch.tensor([c[k] for c in cons], dtype=torch.float64) for k in (1, 2, 3))
             acq.set_general(int(q), torch.from_numpy(oo), torch.from_numpy(ok), torch.from_numpy(p0),
                             torch.from_numpy(p1), co, cs, ct, ce, self._zq(q))
-            acq._general_q.add(q)
+            done.add(q)
         return acq
 
     def __call__(self, X: torch.Tensor) -> torch.Tensor:
@@ -564,9 +564,7 @@ class QNEHVI(_BoxHviAcqf):
         # ---- baseline posterior root, samples, box decomposition ----------------------
         if nb > 0:
             Sig_b = Sig[:, idx][:, :, idx].contiguous()
-            # L_base and its inverse in one blocked pass: G = L_base^-1 E below is then one
-            # GEMM (a 64-row-block forward substitution kept 40 workgroups busy for ~0.5 ms)
-            self.L_base, Lb_inv, self.base_jitter, _ = ops.cholesky_inverse(Sig_b, 1e-8, 3)
+            self.L_base, self.base_jitter, _ = ops.cholesky(Sig_b, 1e-8, 3)
             mu_b = mu_train[:, idx].contiguous()
             probe("baseline_chol")
         # the new point's samples come from a (nb+1)*m-dimensional draw of the same seed;
@@ -627,7 +625,7 @@ class QNEHVI(_BoxHviAcqf):
                 E = torch.cat([E, torch.zeros(m, nb, npend, **f64)], 2).contiguous()
             ops.add_selection(E, idx.to(torch.int32), None)                      # + P
             ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
-            E = ops.gemm(Lb_inv, E)                                              # G = L_base^-1 E
+            ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
             ops.gemm_into(M[:, nk + nb_rows:nk + nb_rows + S_], Zb, E, transA=True)   # H^T = Z^T G
             if fused:
                 Lp = torch.zeros(m, nk, nk, **f64)

@@ -59,7 +59,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
 
 struct PlanLayout {
   size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, bytes;
-  bool small;
+  bool small, fused_kx;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -74,7 +74,11 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     return r;
   };
   L.small = small_path(st, b, md->d);
-  L.Kx = take(L.small ? 0 : 8 * m * n * b);
+  {
+    const char* e = std::getenv("EVR_FUSED_KX");
+    L.fused_kx = L.small && e && std::string(e) == "1";
+  }
+  L.Kx = take(L.fused_kx ? 0 : 8 * m * n * b);
   L.R = take(8 * m * Rr * b);
   L.P = take(8 * (L.small ? qs_norms_doubles(st, b) : m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b));
   L.Wf = take(8 * (L.small ? 0 : proj_forward_ws_doubles(st, b)));
@@ -162,12 +166,16 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
   const bool small = p->L.small;
-  if (small) {
-    // the restart batch: K_x generated inside the projection (qs_fwd_x, no kmat launch)
+  if (small && p->L.fused_kx) {
+    // K_x generated inside the projection (qs_fwd_x, EVR_FUSED_KX=1): measured slower than
+    // the separate kmat launch at b = 20 (29 vs 12.8 + 4.8 us; each of the 49 row tiles of an
+    // output recomputes the whole K_x,j at one wave per SIMD), kept for A/B
     if (int rc = qs_forward_x(s, st, md, b, X, R, P)) return rc;
   } else if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                         md->lengthscales, nullptr, nullptr, Kx)) {
     return rc;
+  } else if (small) {
+    if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;
   } else if (int rc = proj_forward(s, st, b, md->M, Kx, R, P,
                                    p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr)) {
     return rc;

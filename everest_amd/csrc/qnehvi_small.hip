@@ -195,18 +195,34 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int n, int nb, int Rr, int b, in
 #pragma unroll
       for (int k = 0; k < QS_MAXD; ++k) ut[k] = xt[k] * il[k];
       const int sw = 16 * (tid & 1);
-      for (int cc = 0; cc < b; ++cc) {
-        int c = cc + rot;
-        if (c >= b) c -= b;
-        double acc = 0.0;
+      // all b squared distances first, then the b kernel values: fully unrolled so the LDS
+      // reads and the exp table loads of different candidates are in flight together (one
+      // wave per SIMD here: nothing else hides their latency)
+      double d2v[QS_B];
 #pragma unroll
-        for (int k = 0; k < QS_MAXD; ++k) {
-          if (k < d) {
-            const double df = ut[k] - uc[c][k];
-            acc = fma(df, df, acc);
+      for (int cc = 0; cc < QS_B; ++cc) {
+        d2v[cc] = 0.0;
+        if (cc < b) {
+          int c = cc + rot;
+          if (c >= b) c -= b;
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < QS_MAXD; ++k) {
+            if (k < d) {
+              const double df = ut[k] - uc[c][k];
+              acc = fma(df, df, acc);
+            }
           }
+          d2v[cc] = acc;
         }
-        Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND, acc) : 0.0;
+      }
+#pragma unroll
+      for (int cc = 0; cc < QS_B; ++cc) {
+        if (cc < b) {
+          int c = cc + rot;
+          if (c >= b) c -= b;
+          Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND, d2v[cc]) : 0.0;
+        }
       }
     }
     __syncthreads();
