@@ -1274,17 +1274,34 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
     __syncthreads();
     if (kd_last) {
       __threadfence();
+      // each thread's partials are loaded 16 at a time before they are summed (in split order):
+      // a load -> add chain would pay the L2 latency once per partial on this critical tail
       if (BWD) {
         for (int e = tid; e < M * b; e += 256) {
           const int j = e / b, c = e - j * b;
           double v = 0.0;
-          for (int k = 0; k < nst; ++k) v += dG[((((size_t)s * nst + k) * M) + j) * b + c];
+          for (int k0 = 0; k0 < nst; k0 += 16) {
+            double x[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              x[u] = k0 + u < nst ? dG[((((size_t)s * nst + k0 + u) * M) + j) * b + c] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              if (k0 + u < nst) v += x[u];
+          }
           dGf[((size_t)s * M + j) * b + c] = (gout ? gout[c] : 1.0) / (double)S * v;
         }
       }
       for (int c = tid; c < b; c += 256) {
         double v = 0.0;
-        for (int k = 0; k < nst; ++k) v += part[((size_t)s * nst + k) * b + c];
+        for (int k0 = 0; k0 < nst; k0 += 16) {
+          double x[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) x[u] = k0 + u < nst ? part[((size_t)s * nst + k0 + u) * b + c] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (k0 + u < nst) v += x[u];
+        }
         part[(size_t)s * nst * b + c] = v;
       }
       __threadfence();
@@ -1295,8 +1312,16 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
         __threadfence();
         const int c = tid & 31, g = tid >> 5;
         double v = 0.0;
-        if (c < b)
-          for (int s2 = g; s2 < S; s2 += 8) v += part[(size_t)s2 * nst * b + c];
+        if (c < b) {
+          for (int s0 = g; s0 < S; s0 += 8 * 32) {
+            double x[32];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) x[u] = s0 + 8 * u < S ? part[(size_t)(s0 + 8 * u) * nst * b + c] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 32; ++u)
+              if (s0 + 8 * u < S) v += x[u];
+          }
+        }
         kd_red[g][c] = v;
         __syncthreads();
         if (tid < 32 && c < b) {

@@ -664,10 +664,11 @@ def optimize_acqf_mixed(acqf, bounds: np.ndarray, fixed_features_list: Sequence[
     """[upstream] botorch.optim.optimize_acqf_mixed (q = 1), as BoFire calls it for the
     EXHAUSTIVE categorical method (bofire/strategies/predictives/botorch.py:358-378): one
     optimize_acqf per fixed-feature combination, best acquisition value wins (first on ties).
-    q > 1 (BoTorch's sequential greedy batch over re-built pending points) is not built."""
+    q > 1 is BoTorch's sequential greedy over pending points, which needs the acquisition
+    rebuilt with the chosen rows pending: BotorchStrategy._ask_mixed_sequential drives it."""
     if q != 1:
-        raise NotImplementedError("optimize_acqf_mixed with q > 1 (sequential greedy over pending points) is "
-                                  "not implemented; use the FREE categorical method for joint batches")
+        raise ValueError("optimize_acqf_mixed runs q = 1 rounds; q > 1 is the strategy's sequential greedy "
+                         "(BotorchStrategy._ask_mixed_sequential)")
     stats = OptimizeStats()
     best = (None, -np.inf)
     for ff in fixed_features_list:

@@ -320,6 +320,9 @@ class BotorchStrategy(PredictiveStrategy):
             X_train = self._transform(clean)
             self._xtrain_cache = (ex, X_train)
         X_pending = self._transform(self.candidates) if self.candidates is not None else None
+        extra = getattr(self, "_extra_pending", None)
+        if extra is not None and len(extra):
+            X_pending = extra if X_pending is None else np.concatenate([X_pending, extra], 0)
         return X_train.copy(), X_pending
 
     def calc_acquisition(self, candidates: pd.DataFrame, combined: bool = False) -> np.ndarray:
@@ -342,10 +345,20 @@ class BotorchStrategy(PredictiveStrategy):
         if self.experiments is None:
             raise ValueError("No experiments have been provided yet.")
         q = int(candidate_count)
-        acqf = self._get_acqfs(q)[0]
         ineq = get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
         eq = get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
         combos = self.get_categorical_combinations()
+        if len(combos) > 1 and q > 1:
+            # EXHAUSTIVE categoricals with a batch: [upstream] optimize_acqf_mixed(q > 1) is a
+            # sequential greedy — q rounds of the q = 1 mixed optimisation, each round's winner
+            # added to the acquisition's pending points (acq_function.set_X_pending) — so the
+            # acquisition is rebuilt per round with the same seeds (the generator is rewound)
+            # and the chosen rows as extra pending points
+            x, val, stats = self._ask_mixed_sequential(q, combos, ineq, eq)
+            stats.best_value = val
+            self.last_ask_stats = stats
+            return self._postprocess_candidates(x.reshape(q, -1))
+        acqf = self._get_acqfs(q)[0]
         if len(combos) > 1:     # EXHAUSTIVE categorical method: optimize_acqf_mixed
             x, val, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts, self.num_raw_samples,
                                                 self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
@@ -357,6 +370,28 @@ class BotorchStrategy(PredictiveStrategy):
         stats.best_value = val
         self.last_ask_stats = stats
         return self._postprocess_candidates(x.reshape(q, -1))
+
+    def _ask_mixed_sequential(self, q: int, combos, ineq, eq):
+        """optimize_acqf_mixed with q > 1 (botorch.optim.optimize_mixed, sequential branch):
+        returns (q x d candidates, list of the rounds' values, stats of the last round)."""
+        seed_state = self.gen.get_state()
+        chosen, values = [], []
+        stats = None
+        try:
+            for _ in range(q):
+                gen_state = self.gen.get_state()
+                self.gen.set_state(seed_state)            # same acquisition seeds every round
+                self._extra_pending = np.asarray(chosen) if chosen else None
+                acqf = self._get_acqfs(1)[0]
+                self.gen.set_state(gen_state)             # the optimiser's draws continue
+                x, v, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts,
+                                                  self.num_raw_samples, self._get_optimizer_options(), self.gen, ineq,
+                                                  eq, dist=self.dist, q=1)
+                chosen.append(np.asarray(x, dtype=np.float64).reshape(-1))
+                values.append(v)
+        finally:
+            self._extra_pending = None
+        return np.stack(chosen), values, stats
 
     def get_fixed_features(self) -> dict:
         """bofire/strategies/predictives/botorch.py:530-595 (continuous / one-hot part):

@@ -46,3 +46,36 @@ def test_categorical_ask(method):
         Xt = X.cpu().numpy()[0]
         assert set(np.unique(Xt[2:])) <= {0.0, 1.0}                  # exact one-hot
         assert s.last_ask_stats.raw_evals == 6 * 64
+
+
+def test_exhaustive_batch_is_sequential_greedy():
+    """EXHAUSTIVE categoricals with ask(2): [upstream] optimize_acqf_mixed(q = 2) runs two
+    q = 1 mixed optimisations, the first winner pending in the second (the qEI becomes a
+    joint qEI over the candidate and the pending row); the second round's value is the joint
+    acquisition at both rows."""
+    from everest_amd.acquisition import QEIJoint
+
+    dom = _domain()
+    spec = dm.SingleTaskGPSurrogate(inputs=dom.inputs, outputs=dom.outputs, kernel=dm.MaternKernel(nu=2.5))
+    s = strategies.map(dm.SoboStrategy(domain=dom, acquisition_function=dm.qEI(), seed=4,
+                                       surrogate_specs=dm.BotorchSurrogates(surrogates=[spec]),
+                                       categorical_method="EXHAUSTIVE", num_raw_samples=64, num_restarts=2))
+    s.tell(_exps(dom))
+    c = s.ask(2)
+    assert len(c) == 2
+    for k in range(2):
+        assert c["c0"].iloc[k] in ("a", "b", "c") and c["c1"].iloc[k] in ("u", "w")
+    X = s._transform(c)
+    assert not np.allclose(X[0], X[1])
+    vals = s.last_ask_stats.best_value
+    assert len(vals) == 2 and all(np.isfinite(vals))
+    # round 2 was optimised with row 1 pending: its value is the joint qEI of the two rows
+    s._extra_pending = X[:1]
+    gen_state = s.gen.get_state()
+    try:
+        acqf = s._get_acqfs(1)[0]
+    finally:
+        s._extra_pending = None
+        s.gen.set_state(gen_state)
+    assert isinstance(acqf, QEIJoint)
+    assert s.candidates is None
