@@ -113,15 +113,18 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
 // distance loop of kmat_kernel (2 flop per coordinate per entry) was the bound at d = 32.
 using kd4_t = __attribute__((ext_vector_type(4))) double;
 
-template <int DP, int KIND>
+template <int DP, int KIND, int EPI>
 __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
                                                         const double* __restrict__ X1, const double* __restrict__ sh1,
                                                         const double* __restrict__ sc1, const double* __restrict__ X2,
                                                         const double* __restrict__ sh2, const double* __restrict__ sc2,
                                                         const double* __restrict__ ls, const double* __restrict__ os,
                                                         const double* __restrict__ dg, double* __restrict__ K) {
-  __shared__ double As[DP][KT + 2];
-  __shared__ double Bs[DP][KT + 2];
+  // operand tiles As / Bs; EPI 1 / 2 reuse the same storage for the output tile
+  constexpr int OPS = 2 * DP * (KT + 2), OUT = EPI ? KT * (KT + 1) : 0;
+  __shared__ double smem[OPS > OUT ? OPS : OUT];
+  double (*As)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem);
+  double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
   __shared__ double na[KT], nb2[KT];
   __shared__ int eqr[KT];   // diagonal tiles: row r of both operands bitwise identical
   const int gx = gridDim.x, gy = gridDim.y;
@@ -204,20 +207,55 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n1 * n2;
   const int col = lane & 15, rq = lane >> 4;
+  if (EPI == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+        const int gi = i0 + li, gj = j0 + lj;
+        if (gi < n1 && gj < n2) {
+          double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+          if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
+          double v = scale * kernel_value(KIND, d2);
+          if (gi == gj) v += dadd;
+          Kb[(size_t)gi * n2 + gj] = v;
+        }
+      }
+    return;
+  }
+  // EPI 1 / 2: the tile's values go through LDS (aliasing the operand tiles, whose MFMA reads
+  // are done) so that every store instruction writes one contiguous 512-byte row segment
+  // (EPI 2: non-temporal stores — the output is not re-read by this kernel)
+  double vals[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
       const int gi = i0 + li, gj = j0 + lj;
-      if (gi < n1 && gj < n2) {
-        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-        if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
-        double v = scale * kernel_value(KIND, d2);
-        if (gi == gj) v += dadd;
-        Kb[(size_t)gi * n2 + gj] = v;
-      }
+      double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+      if (gi == gj && eqr[li]) d2 = 0.0;
+      double v = scale * kernel_value(KIND, d2);
+      if (gi == gj) v += dadd;
+      vals[4 * q + r] = v;
     }
+  __syncthreads();   // every wave is done with As / Bs
+  double (*T)[KT + 1] = reinterpret_cast<double (*)[KT + 1]>(smem);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[4 * q + r];
+  __syncthreads();
+  const int gj = j0 + lane;
+#pragma unroll 4
+  for (int rr = wave; rr < KT; rr += 4) {
+    const int gi = i0 + rr;
+    if (gi < n1 && gj < n2) {
+      if (EPI == 2) __builtin_nontemporal_store(T[rr][lane], Kb + (size_t)gi * n2 + gj);
+      else Kb[(size_t)gi * n2 + gj] = T[rr][lane];
+    }
+  }
 }
 
 // dX2[c][k] = sum_b sum_i G[b][i][c] * dk_b(x1_i, x2_c)/dx2_ck.
@@ -578,9 +616,21 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
-#define KMK(DP_, K_)                                                                                        \
-  kmat_mfma_kernel<DP_, K_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                 lengthscales, outputscale, diag_add, K)
+    static const int epi = [] {   // EVR_KMAT_EPI: 0 direct D-layout stores, 1 LDS rows, 2 + non-temporal
+      const char* e = getenv("EVR_KMAT_EPI");
+      const int v = e ? atoi(e) : 0;
+      return (v >= 0 && v <= 2) ? v : 0;
+    }();
+#define KMK(DP_, K_)                                                                                          \
+  if (epi == 0)                                                                                               \
+    kmat_mfma_kernel<DP_, K_, 0><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                      lengthscales, outputscale, diag_add, K);                 \
+  else if (epi == 1)                                                                                          \
+    kmat_mfma_kernel<DP_, K_, 1><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                      lengthscales, outputscale, diag_add, K);                 \
+  else                                                                                                        \
+    kmat_mfma_kernel<DP_, K_, 2><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                      lengthscales, outputscale, diag_add, K)
 #define KM(DP_)                         \
   if (kind == RBF) KMK(DP_, RBF);           \
   else if (kind == MATERN05) KMK(DP_, MATERN05); \

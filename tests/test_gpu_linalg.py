@@ -153,13 +153,17 @@ def test_kernel_matrix_wide_mfma(d, kind):
         assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
 
 
+@pytest.mark.parametrize("variant", ["la", "rl"])
 @pytest.mark.parametrize("n", [64, 65, 130, 513, 1024])
-def test_fused_cholesky_inverse_matches_torch_and_v1(n, monkeypatch):
-    """The fused Cholesky (one launch per 64-column block: panel recompute + trailing update +
-    factor of the next diagonal block, then the in-place panel pass) and the one-launch-per-
-    row triangular inverse, against torch and against the three-launch-per-block v1 path."""
+def test_fused_cholesky_inverse_matches_torch_and_v1(n, variant, monkeypatch):
+    """The one-launch-per-block Cholesky variants — "la" (default: final panels, the next
+    block column normalised in the same launch after the diagonal factor's flag) and "rl"
+    (panel recomputed by every consumer, in-place panel pass at the end) — and the one-
+    launch-per-row triangular inverse, against torch and against the three-launch-per-block
+    v1 path."""
     from everest_amd import ops
 
+    monkeypatch.setenv("EVR_CHOL", variant)
     g = torch.Generator().manual_seed(n)
     A = torch.randn(3, n, n + 5, generator=g, dtype=torch.float64)
     A = A @ A.transpose(1, 2) / n + 1e-2 * torch.eye(n, dtype=torch.float64)
@@ -175,11 +179,14 @@ def test_fused_cholesky_inverse_matches_torch_and_v1(n, monkeypatch):
     assert torch.allclose(Li, Li1, rtol=1e-10, atol=1e-11 * Li1.abs().max().item())
 
 
-def test_fused_cholesky_failure_and_ladder():
-    """A member failing in a late diagonal block of the fused path reports the same pivot
-    index as v1 and gets the same jitter (psd_safe_cholesky per-member ladder)."""
+@pytest.mark.parametrize("variant", ["la", "rl", "v1"])
+def test_fused_cholesky_failure_and_ladder(variant, monkeypatch):
+    """A member failing in a late diagonal block reports a pivot index past block 2 and gets
+    the psd_safe_cholesky per-member jitter; in the look-ahead variant the waiting column
+    tiles of the failing member must see the flag and exit (no hang)."""
     from everest_amd import ops
 
+    monkeypatch.setenv("EVR_CHOL", variant)
     g = torch.Generator().manual_seed(3)
     V = torch.randn(2, 200, 150, generator=g, dtype=torch.float64)
     A = V @ V.transpose(1, 2)                      # rank 150 of 200: fails past block 2

@@ -1,5 +1,5 @@
 """Batched Cholesky / Cholesky+inverse timing (HIP events, device-resident input), fused
-path vs EVR_CHOL=v1, with TF/s against the f64 MFMA peak.  One JSON line.
+look-ahead (la, default) vs fused right-looking (rl) vs v1, with TF/s against the f64 MFMA peak.  One JSON line.
 Flops: n^3/3 per factorisation, + n^3/3 for the triangular inverse."""
 import json
 import os
@@ -35,11 +35,8 @@ def run(n, B, inverse, reps):
 
 def main():
     out = {}
-    for ver in ("fused", "v1"):
-        if ver == "v1":
-            os.environ["EVR_CHOL"] = "v1"
-        else:
-            os.environ.pop("EVR_CHOL", None)
+    for ver in ("la", "rl", "v1"):
+        os.environ["EVR_CHOL"] = ver
         for n, B, inv in ((512, 5, False), (512, 5, True), (1024, 5, False), (2048, 1, False), (2048, 1, True),
                           (4096, 1, False)):
             out[f"{ver}/n{n}b{B}{'_inv' if inv else ''}"] = run(n, B, inv, 20 if n <= 1024 else 5)
@@ -49,8 +46,7 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1:      # one configuration: ver n B inv (for rocprofv3 runs)
         ver, n, B, inv = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4] == "1"
-        if ver == "v1":
-            os.environ["EVR_CHOL"] = "v1"
+        os.environ["EVR_CHOL"] = ver
         print(json.dumps(run(n, B, inv, 20)))
     else:
         main()

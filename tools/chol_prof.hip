@@ -6,6 +6,10 @@
 #include <vector>
 #include "../everest_amd/csrc/linalg.hip"
 
+namespace evr {
+void set_error(const char*, ...) {}
+}
+
 int main() {
   const int n = 64, reps = 200;
   std::vector<double> A(n * n);
