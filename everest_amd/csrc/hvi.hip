@@ -438,13 +438,9 @@ __device__ __forceinline__ unsigned int kd_lt16(unsigned int w, unsigned int t) 
 // t[s][j][c] = #{point rows p of sample s : lower-bound value_j(p) <= G[s][j][c]} (binary
 // search in the sample's ascending values, staged in LDS); one workgroup per (j, s).
 __global__ __launch_bounds__(256) void hvi_thresholds(int b, int M, int stride, const double* __restrict__ G,
-                                                      const double* __restrict__ sorted_lo, int* __restrict__ th,
-                                                      unsigned int* __restrict__ cnt, int ncnt) {
+                                                      const double* __restrict__ sorted_lo, int* __restrict__ th) {
   extern __shared__ double thv[];
   const int j = blockIdx.x, s = blockIdx.y;
-  // the scan's completion counters (fused reductions) start every evaluation at zero
-  if (cnt && j == 0 && s == 0)
-    for (int e = threadIdx.x; e < ncnt; e += 256) cnt[e] = 0u;
   const double* src = sorted_lo + ((size_t)s * M + j) * stride;
   for (int e = threadIdx.x; e < stride; e += 256) thv[e] = src[e];
   __syncthreads();
@@ -909,9 +905,7 @@ template <int M, bool BWD>
 __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsplit, const double* __restrict__ G,
                                                const int* __restrict__ thg, HviKd kd,
                                                const double* __restrict__ gout, double* __restrict__ part,
-                                               double* __restrict__ dG, int W, int balance, int ilv,
-                                               unsigned int* __restrict__ cnt, const int* __restrict__ flags,
-                                               double* __restrict__ acq, double* __restrict__ dGf) {
+                                               double* __restrict__ dG, int W, int balance, int ilv) {
   constexpr int NV = BWD ? M + 1 : 1;
   constexpr int CW = KD_CT / 4;            // candidate slots per wave
   using K = CellKey<M>;
@@ -1024,7 +1018,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   const int wsub = wave % W;
   const int cbase = (wave / W) * CW;   // this wave's candidates: cbase .. cbase + 15 (tile-local)
   const int aslot = wave * CW;         // ... and its accumulator rows
-  if (valid(cbase)) {   // (waves without candidates skip to the fused tail)
+  if (!valid(cbase)) return;
   if (ilv) {   // this wave's share of the workgroup's chunks: local chunk qw0 + k * qwst
     qw0 = wsub;
     qwst = W;
@@ -1247,6 +1241,7 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   }
   wave_sync();
   KD_TEND();
+  const int nst = nsplit * W;   // partial splits: workgroup splits x wave splits
   const size_t ss = ((size_t)s * nsplit + split) * W + wsub;
   if (lane < CW && valid(cbase + lane)) part[ss * b + cand(cbase + lane)] = acc[aslot + lane][0];
   if (BWD) {
@@ -1255,84 +1250,8 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
       if (!valid(c)) continue;
       const int gc = cand(c);
       const double v = acc[aslot + cl][NV > 1 ? 1 + j : 0];
-      if (nsplit * W == 1) dG[((size_t)s * M + j) * b + gc] = (gout ? gout[gc] : 1.0) / (double)S * v;
+      if (nst == 1) dG[((size_t)s * M + j) * b + gc] = (gout ? gout[gc] : 1.0) / (double)S * v;
       else dG[(ss * M + j) * b + gc] = v;
-    }
-  }
-  }   // valid(cbase)
-  const int nst = nsplit * W;   // partial splits: workgroup splits x wave splits
-  if (cnt) {
-    // fused reductions of the small (split) batches, replacing the hvi_reduce_fb launch: the
-    // last workgroup of a sample (device-scope counter cnt[s]) sums its nst partials in split
-    // order — dG[s] exactly as hvi_reduce_bwd, the values into split slot 0 — and the last
-    // sample's workgroup (cnt[S]) forms acq = sum_s / S in a fixed 8-group order
-    __shared__ unsigned int kd_last;
-    __shared__ double kd_red[8][32];
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) kd_last = (atomicAdd(&cnt[s], 1u) == (unsigned)(gridDim.x * gridDim.z) - 1u) ? 1u : 0u;
-    __syncthreads();
-    if (kd_last) {
-      __threadfence();
-      // each thread's partials are loaded 16 at a time before they are summed (in split order):
-      // a load -> add chain would pay the L2 latency once per partial on this critical tail
-      if (BWD) {
-        for (int e = tid; e < M * b; e += 256) {
-          const int j = e / b, c = e - j * b;
-          double v = 0.0;
-          for (int k0 = 0; k0 < nst; k0 += 16) {
-            double x[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-              x[u] = k0 + u < nst ? dG[((((size_t)s * nst + k0 + u) * M) + j) * b + c] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-              if (k0 + u < nst) v += x[u];
-          }
-          dGf[((size_t)s * M + j) * b + c] = (gout ? gout[c] : 1.0) / (double)S * v;
-        }
-      }
-      for (int c = tid; c < b; c += 256) {
-        double v = 0.0;
-        for (int k0 = 0; k0 < nst; k0 += 16) {
-          double x[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = k0 + u < nst ? part[((size_t)s * nst + k0 + u) * b + c] : 0.0;
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            if (k0 + u < nst) v += x[u];
-        }
-        part[(size_t)s * nst * b + c] = v;
-      }
-      __threadfence();
-      __syncthreads();
-      if (tid == 0) kd_last = (atomicAdd(&cnt[S], 1u) == (unsigned)S - 1u) ? 1u : 0u;
-      __syncthreads();
-      if (kd_last) {
-        __threadfence();
-        const int c = tid & 31, g = tid >> 5;
-        double v = 0.0;
-        if (c < b) {
-          for (int s0 = g; s0 < S; s0 += 8 * 32) {
-            double x[32];
-#pragma unroll
-            for (int u = 0; u < 32; ++u) x[u] = s0 + 8 * u < S ? part[(size_t)(s0 + 8 * u) * nst * b + c] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 32; ++u)
-              if (s0 + 8 * u < S) v += x[u];
-          }
-        }
-        kd_red[g][c] = v;
-        __syncthreads();
-        if (tid < 32 && c < b) {
-          const double tot = ((kd_red[0][c] + kd_red[1][c]) + (kd_red[2][c] + kd_red[3][c])) +
-                             ((kd_red[4][c] + kd_red[5][c]) + (kd_red[6][c] + kd_red[7][c]));
-          bool bad = false;
-          if (flags)
-            for (int j = 0; j < M; ++j) bad |= flags[(size_t)j * b + c] != 0;
-          acq[c] = bad ? nan("") : tot / (double)S;
-        }
-      }
     }
   }
 }
@@ -1418,17 +1337,7 @@ static int hvi_kd_nsplit(const evr_qnehvi_state* st, int b) {
 static long long hvi_kd_workspace(const evr_qnehvi_state* st, int b) {
   const long long ns = (long long)hvi_kd_nsplit(st, b) * hvi_kd_wsplit(b);
   return (long long)st->S * ns * b + ((long long)st->S * st->m * b + 1) / 2 +
-         (ns > 1 ? (long long)st->S * ns * st->m * b + (st->S + 2) / 2 + 1 : 0);
-}
-
-// the fused reductions of hvi_kd2 (last-workgroup tails) replace hvi_reduce_fb for the small
-// split batches; EVR_KD_FUSE=0 keeps the separate launch (A/B)
-static bool kd_fuse() {
-  static const int f = [] {
-    const char* e = std::getenv("EVR_KD_FUSE");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return f != 0;
+         (ns > 1 ? (long long)st->S * ns * st->m * b : 0);
 }
 
 template <int M, bool BWD>
@@ -1439,12 +1348,10 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
   const int ntiles = cdiv(b, KD_CT / W);
   const int nsb = hvi_kd_nsplit(st, b);   // workgroup splits
   const int ns = nsb * W;                 // partial splits (workgroup x wave)
-  int* th = (int*)(part + (size_t)st->S * ns * b);   // workspace: thresholds, then dG partials, counters
+  int* th = (int*)(part + (size_t)st->S * ns * b);   // workspace: thresholds, then dG partials
   double* dgp = (double*)(th + (((size_t)st->S * M * b + 1) & ~(size_t)1));
-  unsigned int* cnt = ns > 1 ? (unsigned int*)(dgp + (size_t)st->S * ns * M * b) : nullptr;
-  const bool fuse = kd_variant() == 2 && ns > 1 && acq && b <= 32 && kd_fuse();
-  hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(
-      b, M, st->pts_stride, G, st->sorted_lo, th, fuse ? cnt : nullptr, st->S + 1);
+  hvi_thresholds<<<dim3(M, st->S), 256, (size_t)st->pts_stride * sizeof(double), s>>>(b, M, st->pts_stride, G,
+                                                                                     st->sorted_lo, th);
   EVR_LAUNCH_CHECK();
   dim3 grid(ntiles, st->S, nsb);
   if (kd_variant() == 1) {
@@ -1469,11 +1376,9 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
       return (e && e[0] == '0') ? 0 : 1;
     }();
     hvi_kd2<M, BWD><<<grid, 256, L2.bytes, s>>>(b, st->S, ntiles, nsb, G, th, hvi_kd_of(st), gout, part,
-                                                  ns > 1 ? dgp : dG, W, balance, ilv && W > 1,
-                                                  fuse ? cnt : nullptr, flags, acq, dG);
+                                                  ns > 1 ? dgp : dG, W, balance, ilv && W > 1);
   }
   EVR_LAUNCH_CHECK();
-  if (fuse) return 0;
   if (acq && BWD && ns > 1) {   // one launch for both reductions
     const long long tot = (long long)st->S * M * b;
     const int nb = (int)cdiv(tot, 256);

@@ -1019,16 +1019,16 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
 }
 
 // One blocked factorisation attempt of every batch member (jitter already in L's diagonal).
-// Default: the look-ahead steps (nblk launches, chol_la_kernel); EVR_CHOL=rl the fused
-// right-looking steps that recompute the panel per consumer (nblk + 1 launches); EVR_CHOL=v1
-// the diag / panel GEMM / trailing GEMM sequence (3 launches per block).  A/B timing and
-// the parity tests.
+// Default: the fused right-looking steps that recompute the panel per consumer (nblk + 1
+// launches); EVR_CHOL=la the look-ahead steps (nblk launches, chol_la_kernel; measured slower:
+// 1.43 vs 1.29 ms at n = 2048, profiles/r03/b); EVR_CHOL=v1 the diag / panel GEMM / trailing
+// GEMM sequence (3 launches per block).  A/B timing and the parity tests.
 static int chol_variant() {   // 0 look-ahead, 1 fused right-looking, 2 v1 (read per call: tests switch it)
   const char* e = std::getenv("EVR_CHOL");
-  if (!e) return 0;
+  if (!e) return 1;
   if (!std::strcmp(e, "v1")) return 2;
-  if (!std::strcmp(e, "rl")) return 1;
-  return 0;
+  if (!std::strcmp(e, "la")) return 0;
+  return 1;
 }
 static bool chol_v1() { return chol_variant() == 2; }
 

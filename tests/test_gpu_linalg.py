@@ -156,9 +156,9 @@ def test_kernel_matrix_wide_mfma(d, kind):
 @pytest.mark.parametrize("variant", ["la", "rl"])
 @pytest.mark.parametrize("n", [64, 65, 130, 513, 1024])
 def test_fused_cholesky_inverse_matches_torch_and_v1(n, variant, monkeypatch):
-    """The one-launch-per-block Cholesky variants — "la" (default: final panels, the next
-    block column normalised in the same launch after the diagonal factor's flag) and "rl"
-    (panel recomputed by every consumer, in-place panel pass at the end) — and the one-
+    """The one-launch-per-block Cholesky variants — "rl" (default: panel recomputed by every
+    consumer, in-place panel pass at the end) and "la" (final panels, the next block column
+    normalised in the same launch after the diagonal factor's flag) — and the one-
     launch-per-row triangular inverse, against torch and against the three-launch-per-block
     v1 path."""
     from everest_amd import ops
