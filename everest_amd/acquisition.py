@@ -175,7 +175,8 @@ class _BoxHviAcqf:
 
     def _use_log_scan(self, tau_relu: float, tau_max: float):
         """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
-        q = 1 affine fast path runs the dense kernel of hvi_log.hip, every other case
+        q = 1 affine fast path runs hvi_log.hip (the tabulated keyed kernel over compressed
+        cells, the dense kernel over explicit ones), every other case
         (output constraints, CloseToTarget / selected outputs, q > 1, qLogEHVI pending points)
         the general log scan (evr_qlog_eval), both over the explicit cell bounds (compressed
         cells are expanded once, on the device)."""
@@ -186,7 +187,8 @@ class _BoxHviAcqf:
         def logify(src):
             st = _native.EvrQnehviState.from_buffer_copy(src)
             st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
-            st.cell_keys = st.cell_pts = st.cell_rank0 = None
+            # compressed cells stay: the q = 1 scan tabulates log fatplus over the point table
+            # (hvi_logk_kernel); the general log scan reads the explicit rows
             st.grp_off = st.grp_keys = st.grp_rank = st.grp_box = st.sorted_lo = None
             st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
             return st

@@ -218,6 +218,98 @@ __device__ __forceinline__ double fatmin2(double a, double b, double t, double* 
   return fmin(a, b) - t * log(1.0 + p);
 }
 
+// ---- table-driven f64 log1p / log / exp for the keyed log scan (hvi_logk_kernel): the
+// OCML routines cost ~100 instructions each and there are ~7 per (cell, candidate).  The
+// tables live in the caller's LDS (FastLogTabs::fill once per workgroup); results stay
+// within ~2 ulps of the libm values.
+struct FastLogTabs {
+  double2 li[65];  // (log1p(i / 64), 1 / (1 + i / 64)): one 16-byte LDS read per log1p
+  double et[64];   // 2^(j / 64)
+  __device__ void fill(int tid, int nthreads) {
+    for (int i = tid; i < 65; i += nthreads) {
+      li[i] = make_double2(log1p(i / 64.0), 1.0 / (1.0 + i / 64.0));
+      if (i < 64) et[i] = exp2(i / 64.0);
+    }
+  }
+};
+
+// 1 / d for d in [1, 2^1000]: hardware reciprocal seed + two Newton steps (<= 1 ulp, no
+// scaling / fixup sequence: d is never denormal, infinite or zero here)
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+// log1p(p) for p in [0, 1]: log1p(i / 64) + log1p(r), r = (p - i / 64) / (1 + i / 64) in
+// [0, 1/64) by its Taylor series to r^8 (truncation < 3e-18)
+__device__ __forceinline__ double log1p_tab(double p, const FastLogTabs& T) {
+  const int i = min(64, (int)(p * 64.0));
+  const double2 L = T.li[i];
+  const double r = (p - i * (1.0 / 64.0)) * L.y;
+  double q = -1.0 / 8.0;
+  q = fma(q, r, 1.0 / 7.0);
+  q = fma(q, r, -1.0 / 6.0);
+  q = fma(q, r, 1.0 / 5.0);
+  q = fma(q, r, -1.0 / 4.0);
+  q = fma(q, r, 1.0 / 3.0);
+  q = fma(q, r, -1.0 / 2.0);
+  q = fma(q, r, 1.0);
+  return fma(q, r, L.x);
+}
+
+// log(w), w > 0 finite (w <= 0: -inf): w = m 2^e with m in [1, 2)
+__device__ __forceinline__ double log_tab(double w, const FastLogTabs& T) {
+  if (!(w > 0.0)) return -INFINITY;
+  int e;
+  const double m = 2.0 * frexp(w, &e);   // frexp: [0.5, 1)
+  constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+  const double e1 = (double)(e - 1);
+  return fma(e1, LN2_HI, fma(e1, LN2_LO, log1p_tab(m - 1.0, T)));
+}
+
+// exp(x) for x <= 0 (x < -745.2: 0): x = k ln2 / 64 + r, |r| <= ln2 / 128, 2^(k/64) from
+// the table, expm1(r) by its Taylor series to r^6
+__device__ __forceinline__ double exp_tab_neg(double x, const FastLogTabs& T) {
+  if (x < -745.2) return 0.0;
+  constexpr double K64 = 92.33248261689365951;   // 64 / ln 2
+  constexpr double C_HI = 1.08304246962070465088e-02, C_LO = 2.98155597433513719e-12;   // ln2 / 64
+  const double kd = rint(x * K64);
+  const int k = (int)kd;
+  const double r = fma(-kd, C_LO, fma(-kd, C_HI, x));
+  double q = 1.0 / 720.0;
+  q = fma(q, r, 1.0 / 120.0);
+  q = fma(q, r, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  const double t = T.et[k & 63];
+  return ldexp(fma(t * r, q, t), k >> 6);
+}
+
+// fatmin for the tabulated keyed scan: x scaled by 1 / t, one division for 2 / q and the
+// derivative's 1 / (1 + p) (q = 2 + 2x + x^2: p = 2 / q, 1 / (1 + p) = q / (q + 2)), log1p —
+// within a few ulps of fatmin2
+__device__ __forceinline__ double fatmin_fast(double a, double b, double t, double it, double* da,
+                                              const FastLogTabs& T) {
+  if (b == -INFINITY) {
+    *da = 0.0;
+    return -INFINITY;
+  }
+  const double x = fabs(a - b) * it;
+  const double q = fma(x, 2.0 + x, 2.0);
+  const double qq = q * (q + 2.0);
+  // x = inf (a or b infinite): q(q+2) = inf, p = dq = 0 as the divided form gives
+  const bool big = isinf(qq);
+  const double w = big ? 0.0 : rcp_nr(qq);
+  const double p = big ? 0.0 : 2.0 * (q + 2.0) * w;
+  const double dq = big ? 0.0 : 4.0 * (1.0 + x) * w;   // -pareto'(x) / (1 + pareto(x))
+  *da = (a < b) ? 1.0 - dq : dq;
+  return fmin(a, b) - t * log1p_tab(p, T);
+}
+
 // online log-sum-exp with M gradient slots (running max m, s0 = sum exp(a - m),
 // g_j = sum exp(a - m) da/dtheta_j)
 template <int M, bool BWD>
@@ -229,18 +321,19 @@ struct LseState {
 #pragma unroll
     for (int j = 0; j < (BWD ? M : 1); ++j) g[j] = 0.0;
   }
+  // one exp on either branch (exp(-|a - m|) is exp(m - a) for a new maximum, exp(a - m)
+  // otherwise, bitwise), so lanes that disagree on the branch do not pay two
   __device__ void add(double a, const double* da) {
     if (a == -INFINITY) return;
+    const double e = exp(-fabs(a - m));   // 0 when m = -inf
     if (a > m) {
-      const double r = exp(m - a);   // 0 when m = -inf
-      s0 = fma(s0, r, 1.0);
+      s0 = fma(s0, e, 1.0);
       if (BWD) {
 #pragma unroll
-        for (int j = 0; j < M; ++j) g[j] = fma(g[j], r, da[j]);
+        for (int j = 0; j < M; ++j) g[j] = fma(g[j], e, da[j]);
       }
       m = a;
     } else {
-      const double e = exp(a - m);
       s0 += e;
       if (BWD) {
 #pragma unroll

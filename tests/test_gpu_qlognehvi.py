@@ -228,3 +228,27 @@ def test_mobo_default_constrained_ask_joint_batch():
     c1 = s.ask(1, add_pending=True)
     c2 = s.ask(1)
     assert len(c1) == 1 and len(c2) == 1
+
+
+@pytest.mark.parametrize("m,prune", [(2, False), (3, True), (5, True)])
+def test_qlog_keyed_scan_matches_dense(m, prune, monkeypatch):
+    """The tabulated scan over compressed cells (hvi_logk_kernel: log fatplus once per
+    (candidate, objective, point), lam once per cell) against the dense kernel over the same
+    cells expanded to explicit rows (EVR_LOG=dense): equal up to the summation order of the
+    online log-sum-exp; forward-only and fused forward + backward plans agree bitwise."""
+    X, lo, hi, orc, dq = _matched(48, 4, m, 32, seed=3 + m, prune=prune)
+    assert dq.cells.keys is not None and dq.state.cell_keys
+    rng = np.random.default_rng(m)
+    for b in (1, 5, 20, 67):
+        Xc = torch.tensor(lo + (hi - lo) * rng.uniform(size=(b, 4)), device="cuda")
+        dq._plans = {}
+        a_k, g_k = dq.forward_backward(Xc)
+        f_k = dq.forward(Xc)
+        monkeypatch.setenv("EVR_LOG", "dense")
+        dq._plans = {}
+        a_d, g_d = dq.forward_backward(Xc)
+        monkeypatch.delenv("EVR_LOG")
+        dq._plans = {}
+        assert torch.allclose(a_k, a_d, rtol=1e-12, atol=1e-12), (a_k - a_d).abs().max()
+        assert torch.allclose(g_k, g_d, rtol=1e-10, atol=1e-12 * g_d.abs().max()), (g_k - g_d).abs().max()
+        assert torch.equal(f_k, a_k)
