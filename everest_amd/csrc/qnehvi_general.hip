@@ -847,18 +847,23 @@ __global__ __launch_bounds__(QL_THREADS) void qlog_scan(int b, int nsplit, int C
   }
 }
 
-// thread per candidate: merge the splits per sample -> LSE_sc (split 0's m slot), the
-// normalised gradient slots (g / s0) in split 0, acq_c = logmeanexp_s; w_s (slot s0 of split
-// 0) = gout softmax_s weight for the backward; NaN where the new-point Cholesky failed
+// workgroup per candidate, thread per sample: merge the splits per sample -> LSE_sc (split
+// 0's m slot), the normalised gradient slots (g / s0) in split 0; acq_c = logmeanexp_s by
+// fixed-order tree reductions (max, sum of exp); w_s (slot s0 of split 0) = gout softmax_s
+// weight for the backward; NaN where the new-point Cholesky failed.  (A thread per
+// candidate walking the S samples serially paid the load latency S times over.)
+constexpr int QLR_THREADS = 256;
+
 template <int MM, int Q, bool BWD>
-__global__ void qlog_reduce(int b, int S, int nsplit, int m, double* __restrict__ ws, const int* __restrict__ flags,
-                            const double* __restrict__ gout, double* __restrict__ acq) {
+__global__ __launch_bounds__(QLR_THREADS) void qlog_reduce(int b, int S, int nsplit, int m, double* __restrict__ ws,
+                                                           const int* __restrict__ flags,
+                                                           const double* __restrict__ gout, double* __restrict__ acq) {
   constexpr int NG = Q * (MM + 1);
   constexpr int NO = 2 + (BWD ? NG : 0);
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= b) return;
-  double mx = -INFINITY;
-  for (int s = 0; s < S; ++s) {
+  __shared__ double rd[QLR_THREADS];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double mloc = -INFINITY;
+  for (int s = tid; s < S; s += QLR_THREADS) {
     double* o = ws + (size_t)s * nsplit * NO * b;
     LseState<NG, BWD> st;
     st.m = o[c];
@@ -876,18 +881,34 @@ __global__ void qlog_reduce(int b, int S, int nsplit, int m, double* __restrict_
     o[c] = lse;
     if (BWD)
       for (int j = 0; j < NG; ++j) o[(size_t)(2 + j) * b + c] = (st.s0 > 0.0) ? st.g[j] / st.s0 : 0.0;
-    mx = fmax(mx, lse);
+    mloc = fmax(mloc, lse);
   }
-  double sum = 0.0;
+  rd[tid] = mloc;
+  for (int h = QLR_THREADS / 2; h > 0; h >>= 1) {
+    __syncthreads();
+    if (tid < h) rd[tid] = fmax(rd[tid], rd[tid + h]);
+  }
+  __syncthreads();
+  const double mx = rd[0];
+  __syncthreads();
+  double sl = 0.0;
   if (mx > -INFINITY)
-    for (int s = 0; s < S; ++s) sum += exp(ws[(size_t)s * nsplit * NO * b + c] - mx);
-  const double lme = (mx > -INFINITY) ? mx + log(sum) - log((double)S) : -INFINITY;
-  bool bad = false;
-  for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + c] != 0;
-  acq[c] = bad ? nan("") : lme;
+    for (int s = tid; s < S; s += QLR_THREADS) sl += exp(ws[(size_t)s * nsplit * NO * b + c] - mx);
+  rd[tid] = sl;
+  for (int h = QLR_THREADS / 2; h > 0; h >>= 1) {
+    __syncthreads();
+    if (tid < h) rd[tid] += rd[tid + h];
+  }
+  __syncthreads();
+  const double lme = (mx > -INFINITY) ? mx + log(rd[0]) - log((double)S) : -INFINITY;
+  if (tid == 0) {
+    bool bad = false;
+    for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + c] != 0;
+    acq[c] = bad ? nan("") : lme;
+  }
   if (BWD) {
     const double go = gout ? gout[c] : 1.0;
-    for (int s = 0; s < S; ++s) {
+    for (int s = tid; s < S; s += QLR_THREADS) {
       double* o = ws + (size_t)s * nsplit * NO * b;
       o[(size_t)b + c] = (lme > -INFINITY) ? go * exp(o[c] - lme) / (double)S : 0.0;
     }
@@ -1157,8 +1178,8 @@ int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_st
                                                           sth->cell_lo, sth->cell_hi, sth->tau_relu, sth->tau_max, \
                                                           LW);                                                    \
     EVR_LAUNCH_CHECK();                                                                                           \
-    if (backward) qlog_reduce<4, QQ, true><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
-    else qlog_reduce<4, QQ, false><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
+    if (backward) qlog_reduce<4, QQ, true><<<b, QLR_THREADS, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
+    else qlog_reduce<4, QQ, false><<<b, QLR_THREADS, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
     EVR_LAUNCH_CHECK();                                                                                           \
     if (backward) qlog_dy<4, QQ><<<cdiv((long long)S * bq, 256), 256, 0, s>>>(b, S, P.nsplit, o, Y, LW, w + L.dY); \
   } else {                                                                                                        \
@@ -1169,8 +1190,8 @@ int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_st
                                                           sth->cell_lo, sth->cell_hi, sth->tau_relu, sth->tau_max, \
                                                           LW);                                                    \
     EVR_LAUNCH_CHECK();                                                                                           \
-    if (backward) qlog_reduce<8, QQ, true><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
-    else qlog_reduce<8, QQ, false><<<cdiv(b, 64), 64, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
+    if (backward) qlog_reduce<8, QQ, true><<<b, QLR_THREADS, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);    \
+    else qlog_reduce<8, QQ, false><<<b, QLR_THREADS, 0, s>>>(b, S, P.nsplit, m, LW, flags, gout, acq);           \
     EVR_LAUNCH_CHECK();                                                                                           \
     if (backward) qlog_dy<8, QQ><<<cdiv((long long)S * bq, 256), 256, 0, s>>>(b, S, P.nsplit, o, Y, LW, w + L.dY); \
   }                                                                                                               \
