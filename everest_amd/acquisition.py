@@ -249,8 +249,9 @@ class _BoxHviAcqf:
         if Xp is not None:
             X = torch.cat([X, Xp.unsqueeze(0).expand(b, Xp.shape[0], d)], 1)
             qq = X.shape[1]
-        if qq > 8:
-            raise ValueError(f"joint batch of {qq} points (q + pending) exceeds the device limit of 8")
+        if qq > ops.QNG_MAX_Q:
+            raise ValueError(f"joint batch of {qq} points (q + pending) exceeds the device limit of {ops.QNG_MAX_Q} "
+                             f"(the inclusion-exclusion runs over all 2^q - 1 subsets)")
         g = self.spec.struct(qq, self._zq(qq))
         ev = ops.qlog_eval if getattr(self, "log_acqf", False) else ops.qng_eval
         acq, dX = ev(self.state_model, self.state_scan, g, self.model, X.reshape(b * qq, d).contiguous(),
@@ -323,8 +324,9 @@ class _BoxHviAcqf:
         Xp = self._pending_rows()
         if Xp is not None:
             X3 = torch.cat([X3, Xp.unsqueeze(0).expand(X3.shape[0], Xp.shape[0], X3.shape[2])], 1)
-        if X3.shape[1] > 8:
-            raise ValueError(f"joint batch of {X3.shape[1]} points (q + pending) exceeds the device limit of 8")
+        if X3.shape[1] > ops.QNG_MAX_Q:
+            raise ValueError(f"joint batch of {X3.shape[1]} points (q + pending) exceeds the device limit of "
+                             f"{ops.QNG_MAX_Q} (the inclusion-exclusion runs over all 2^q - 1 subsets)")
         return QnehviFunction.apply(X3.contiguous(), self._torch_acq(X3.shape[1], False))
 
     def _split(self, X: torch.Tensor):

@@ -78,6 +78,29 @@ __device__ __constant__ static const double kExp2J64[64] = {
     1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951,
 };
 
+// exp_k with the 2^(j/64) table read from T (an LDS copy, kexp_stage): a per-lane indexed
+// __constant__ read is a vector memory load, and on gfx9 vmcnt retires loads and stores in
+// issue order, so in a store-heavy epilogue every table load also waited for the stores
+// issued before it.  Same arithmetic as exp_k: bitwise equal.
+__device__ __forceinline__ double exp_k_t(double x, const double* __restrict__ T) {
+  x = x < -760.0 ? -760.0 : x;
+  const double kd = __builtin_rint(x * 92.33248261689366);
+  const int k = (int)kd;
+  double r = fma(kd, -0.010830424696249145, x);
+  r = fma(kd, -3.623510646634843e-19, r);
+  double q = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+  q = fma(q, r, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  const double p = fma(q, r * r, r);
+  const double t = T[k & 63];
+  return __builtin_ldexp(fma(t, p, t), k >> 6);
+}
+// copy of kExp2J64 into a workgroup's LDS (callers __syncthreads before use)
+__device__ __forceinline__ void kexp_stage(double* T, int tid, int nthreads) {
+  for (int i = tid; i < 64; i += nthreads) T[i] = kExp2J64[i];
+}
+
 __device__ __forceinline__ double exp_k(double x) {
   x = x < -760.0 ? -760.0 : x;
   const double kd = __builtin_rint(x * 92.33248261689366);
@@ -114,6 +137,27 @@ __device__ __forceinline__ double kernel_value(int kind, double d2) {
   }
   const double s = 2.23606797749979 * d;
   return (1.0 + s + (5.0 / 3.0) * d2) * exp_k(-s);
+}
+// kernel_value with the exp table in LDS (bitwise equal)
+__device__ __forceinline__ double kernel_value_t(int kind, double d2, const double* __restrict__ T) {
+  if (kind == RBF) return exp_k_t(-0.5 * d2, T);
+  const double d = sqrt(fmax(d2, 1e-30));
+  if (kind == MATERN05) return exp_k_t(-d, T);
+  if (kind == MATERN15) {
+    const double s = 1.7320508075688772 * d;
+    return (1.0 + s) * exp_k_t(-s, T);
+  }
+  const double s = 2.23606797749979 * d;
+  return (1.0 + s + (5.0 / 3.0) * d2) * exp_k_t(-s, T);
+}
+__device__ __forceinline__ double kernel_dscale_t(int kind, double d2, const double* __restrict__ T) {
+  if (kind == RBF) return -exp_k_t(-0.5 * d2, T);
+  if (d2 < 1e-30) return 0.0;
+  const double d = sqrt(d2);
+  if (kind == MATERN05) return -exp_k_t(-d, T) / d;
+  if (kind == MATERN15) return -3.0 * exp_k_t(-1.7320508075688772 * d, T);
+  const double s = 2.23606797749979 * d;
+  return -(5.0 / 3.0) * (1.0 + s) * exp_k_t(-s, T);
 }
 
 // dk/d(x_d) = kernel_dscale(kind, d2) * (x_d - x'_d) / ls_d^2   (x in lengthscale units

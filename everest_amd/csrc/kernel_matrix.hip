@@ -65,6 +65,8 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
       Bt[r * ld + k] = w * il;
     }
   }
+  __shared__ double kexp[64];
+  kexp_stage(kexp, tid, 256);
   __syncthreads();
   const int tx = tid & 15, ty = tid >> 4;
   double acc[RA][4];
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
     for (int c = 0; c < 4; ++c) {
       const int j = j0 + tx + 16 * c;
       if (j < n2) {
-        double v = scale * kernel_value(KIND, acc[a][c]);
+        double v = scale * kernel_value_t(KIND, acc[a][c], kexp);
         if (i == j) v += dadd;
         Kb[(size_t)i * n2 + j] = v;
       }
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
   __shared__ double na[KT], nb2[KT];
   __shared__ int eqr[KT];   // diagonal tiles: row r of both operands bitwise identical
+  __shared__ double kexp[64];
   const int gx = gridDim.x, gy = gridDim.y;
   const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   const int bx = t % gx, by = (t / gx) % gy, b = t / (gx * gy);
@@ -173,6 +176,7 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
       Bs[k][r] = c;
     }
   }
+  kexp_stage(kexp, tid, 256);
   __syncthreads();
   if (tid < 2 * KT) {
     const int r = tid & (KT - 1);
@@ -217,7 +221,7 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
         if (gi < n1 && gj < n2) {
           double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
           if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
-          double v = scale * kernel_value(KIND, d2);
+          double v = scale * kernel_value_t(KIND, d2, kexp);
           if (gi == gj) v += dadd;
           Kb[(size_t)gi * n2 + gj] = v;
         }
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
       const int gi = i0 + li, gj = j0 + lj;
       double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
       if (gi == gj && eqr[li]) d2 = 0.0;
-      double v = scale * kernel_value(KIND, d2);
+      double v = scale * kernel_value_t(KIND, d2, kexp);
       if (gi == gj) v += dadd;
       vals[4 * q + r] = v;
     }
@@ -255,6 +259,134 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
       if (EPI == 2) __builtin_nontemporal_store(T[rr][lane], Kb + (size_t)gi * n2 + gj);
       else Kb[(size_t)gi * n2 + gj] = T[rr][lane];
     }
+  }
+}
+
+// Persistent form of kmat_mfma_kernel for large outputs (DP = 16 / 32 / 64): a workgroup
+// walks tiles t = blockIdx.x, + gridDim.x, ...  The next tile's operand rows (and its
+// lengthscales) are loaded into registers right after the current tile's MFMAs, before the
+// current epilogue's stores, so the stores of tile t drain while tile t + 1's loads are in
+// flight (vmcnt retires in issue order: loads issued after the stores would wait for them).
+// One-shot launches leave every workgroup in the same phase — all staging, then all
+// storing — and the output stream never overlaps the operand fetch.  Values bitwise equal
+// kmat_mfma_kernel's (same staging arithmetic, MFMA order and epilogue).
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void kmat_mfma_pers(int n1, int n2, int d, int B, const double* __restrict__ X1,
+                                                      const double* __restrict__ sh1, const double* __restrict__ sc1,
+                                                      const double* __restrict__ X2, const double* __restrict__ sh2,
+                                                      const double* __restrict__ sc2, const double* __restrict__ ls,
+                                                      const double* __restrict__ os, const double* __restrict__ dg,
+                                                      double* __restrict__ K) {
+  static_assert(256 % DP == 0, "one coordinate per thread");
+  constexpr int NE = KT * DP / 256;   // operand elements per thread and operand
+  __shared__ double As[DP][KT + 2], Bs[DP][KT + 2];
+  __shared__ double na[KT], nb2[KT];
+  __shared__ int eqr[KT];
+  __shared__ double kexp[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int gx = (n2 + KT - 1) / KT, gy = (n1 + KT - 1) / KT, T = gx * gy * B;
+  const int k = tid % DP, r0 = tid / DP;   // this thread's coordinate; rows r0 + (256 / DP) t
+  constexpr int RS = 256 / DP;
+  // batch-independent normalisation of coordinate k
+  const bool kin = k < d;
+  const double s1 = (kin && sh1) ? sh1[k] : 0.0, c1 = (kin && sc1) ? sc1[k] : 1.0;
+  const double s2 = (kin && sh2) ? sh2[k] : 0.0, c2 = (kin && sc2) ? sc2[k] : 1.0;
+  kexp_stage(kexp, tid, 256);
+  double v[NE], w[NE], lk = 1.0;
+  auto fetch = [&](int t) {
+    const int b = t / (gx * gy), rem = t - b * gx * gy, i0 = (rem / gx) * KT, j0 = (rem % gx) * KT;
+    lk = kin ? ls[(size_t)b * d + k] : 1.0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int r = r0 + RS * e;
+      v[e] = (kin && i0 + r < n1) ? X1[(size_t)(i0 + r) * d + k] : 0.0;
+      w[e] = (kin && j0 + r < n2) ? X2[(size_t)(j0 + r) * d + k] : 0.0;
+    }
+  };
+  int t = blockIdx.x;
+  if (t < T) fetch(t);
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int i = lane & 15, kq = lane >> 4, col = lane & 15, rq = lane >> 4;
+  for (; t < T; t += gridDim.x) {
+    const int b = t / (gx * gy), rem = t - b * gx * gy, i0 = (rem / gx) * KT, j0 = (rem % gx) * KT;
+    {
+      const double il = 1.0 / lk;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int r = r0 + RS * e;
+        double a = 0.0, c = 0.0;
+        if (kin) {
+          if (i0 + r < n1) {
+            a = v[e];
+            if (sh1) a -= s1;
+            if (sc1) a *= c1;
+            a *= il;
+          }
+          if (j0 + r < n2) {
+            c = w[e];
+            if (sh2) c -= s2;
+            if (sc2) c *= c2;
+            c *= il;
+          }
+        }
+        As[k][r] = a;
+        Bs[k][r] = c;
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * KT) {
+      const int rr = tid & (KT - 1);
+      double sq = 0.0;
+      if (tid < KT) {
+        int eq = 1;
+        for (int kk = 0; kk < DP; ++kk) {
+          sq = fma(As[kk][rr], As[kk][rr], sq);
+          eq &= As[kk][rr] == Bs[kk][rr];
+        }
+        na[rr] = sq;
+        eqr[rr] = eq;
+      } else {
+        for (int kk = 0; kk < DP; ++kk) sq = fma(Bs[kk][rr], Bs[kk][rr], sq);
+        nb2[rr] = sq;
+      }
+    }
+    kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int kk = 0; kk < DP; kk += 4) {
+      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
+      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+    }
+    if (t + (int)gridDim.x < T) fetch(t + gridDim.x);   // next tile's loads ahead of this tile's stores
+    __syncthreads();   // na / nb2 / eqr; every wave's As / Bs reads are done
+    const double scale = os ? os[b] : 1.0;
+    const double dadd = dg ? dg[b] : 0.0;
+    double* Kb = K + (size_t)b * n1 * n2;
+    double vals[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+        const int gi = i0 + li, gj = j0 + lj;
+        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+        if (gi == gj && eqr[li]) d2 = 0.0;
+        double val = scale * kernel_value_t(KIND, d2, kexp);
+        if (gi == gj) val += dadd;
+        vals[4 * q + r] = val;
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+        const int gi = i0 + li, gj = j0 + lj;
+        if (gi < n1 && gj < n2) Kb[(size_t)gi * n2 + gj] = vals[4 * q + r];
+      }
+    __syncthreads();   // na / nb2 / eqr are rewritten by the next tile
   }
 }
 
@@ -616,6 +748,31 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
+    // EVR_KMAT_PERS=<n>: the persistent pipelined form with n workgroups per CU (opt-in:
+    // measured slower at config 5, 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — fewer
+    // resident waves hide less latency than the load / store overlap gains)
+    static const int pers = [] {
+      const char* e = getenv("EVR_KMAT_PERS");
+      return e ? atoi(e) : 0;
+    }();
+    const long long tiles = (long long)grid.x * grid.y * grid.z;
+    if (pers > 0 && d != 48 && d <= 64 && tiles >= 4LL * 256) {
+      const int nwg = (int)std::min<long long>(tiles, 256LL * pers);
+#define KP(DP_, K_) kmat_mfma_pers<DP_, K_><<<nwg, 256, 0, s>>>(n1, n2, d, B, X1, shift1, scale1, X2, shift2, scale2, \
+                                                               lengthscales, outputscale, diag_add, K)
+#define KPD(DP_)                                    \
+  if (kind == RBF) KP(DP_, RBF);                    \
+  else if (kind == MATERN05) KP(DP_, MATERN05);     \
+  else if (kind == MATERN15) KP(DP_, MATERN15);     \
+  else KP(DP_, MATERN25)
+      if (d <= 16) { KPD(16); }
+      else if (d <= 32) { KPD(32); }
+      else { KPD(64); }
+#undef KPD
+#undef KP
+      EVR_LAUNCH_CHECK();
+      return 0;
+    }
     static const int epi = [] {   // EVR_KMAT_EPI: 0 direct D-layout stores, 1 LDS rows, 2 + non-temporal
       const char* e = getenv("EVR_KMAT_EPI");
       const int v = e ? atoi(e) : 0;

@@ -970,6 +970,10 @@ static QlPlan ql_plan(const evr_qnehvi_state* sth, int b) {
     case 6: MACRO(6); break;                                                            \
     case 7: MACRO(7); break;                                                            \
     case 8: MACRO(8); break;                                                            \
+    case 9: MACRO(9); break;                                                            \
+    case 10: MACRO(10); break;                                                          \
+    case 11: MACRO(11); break;                                                          \
+    case 12: MACRO(12); break;                                                          \
     default: EVR_CHECK(false, "qnehvi_general: q = %d not supported", q);               \
   }
 

@@ -384,6 +384,9 @@ class Inputs(_Features):
         return pd.concat(parts, axis=1)
 
     def inverse_transform(self, transformed: pd.DataFrame, specs: Dict[str, str]) -> pd.DataFrame:
+        feats = self.get().features
+        if all(isinstance(f, ContinuousInput) for f in feats):
+            return transformed[[f.key for f in feats]]
         parts = []
         for feat in self.get().features:
             if isinstance(feat, CategoricalInput):
@@ -478,13 +481,23 @@ class Outputs(_Features):
         return [f.key for f in self.get_by_objective(includes, excludes, exact).features]
 
     def __call__(self, experiments: pd.DataFrame, experiments_adapt=None, predictions: bool = False) -> pd.DataFrame:
-        """Desirabilities (bofire/data_models/domain/features.py:783-835)."""
+        """Desirabilities (bofire/data_models/domain/features.py:783-848): objective values of
+        every output with an objective, the adaptive objectives (MovingMaximizeSigmoid) fed
+        with the non-null observed values of experiments_adapt.  The objectives run on the
+        column arrays and the frame is built once (same values, same column names)."""
+        if predictions and experiments_adapt is None:
+            raise ValueError("If predictions are used, `experiments_adapt` has to be provided.")
+        adapt = experiments if experiments_adapt is None else experiments_adapt
         cols = {}
         for feat in self.get().features:
             if feat.objective is None:
                 continue
             col = f"{feat.key}_pred" if predictions else feat.key
-            cols[f"{feat.key}_des"] = feat(experiments[col])
+            x = experiments[col].to_numpy(dtype=np.float64)
+            xa = None
+            if isinstance(feat.objective, MovingMaximizeSigmoidObjective):
+                xa = adapt[feat.key].dropna().to_numpy(dtype=np.float64)
+            cols[f"{feat.key}_des"] = np.asarray(feat.objective(x, xa), dtype=np.float64)
         return pd.DataFrame(cols, index=experiments.index)
 
     def preprocess_experiments_all_valid_outputs(self, experiments: pd.DataFrame,

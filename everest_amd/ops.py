@@ -28,6 +28,10 @@ class NotPSDError(RuntimeError):
     linear_operator NotPSDError, caught by fit_gpytorch_mll's retries)."""
 
 
+# joint batch limit of the general q-point kernels (include/everest_amd.h EVR_QNG_MAX_Q): the
+# [upstream] inclusion-exclusion enumerates all 2^q - 1 subsets of the q (+ pending) points
+QNG_MAX_Q = 12
+
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 

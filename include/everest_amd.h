@@ -335,7 +335,7 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* plan, const double* 
  * HOST arrays (copied into the launch); zq (S x q x m_model) is on the device. */
 #define EVR_OBJ_AFFINE 0
 #define EVR_OBJ_CLOSE_TO_TARGET 1
-#define EVR_QNG_MAX_Q 8
+#define EVR_QNG_MAX_Q 12
 typedef struct {
   int q;                    /* points per candidate, 1..8 */
   int m_obj;                /* objectives, 1..8 */

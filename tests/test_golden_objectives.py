@@ -123,3 +123,20 @@ def test_device_weights_several_outputs_and_constraints():
     Gd, Wd = ops.objective_weights(torch.tensor(Y, device="cuda"), spec)
     np.testing.assert_allclose(Gd.cpu().numpy(), spec.host_objective(Y.T).T, rtol=1e-13, atol=1e-15)
     np.testing.assert_allclose(Wd.cpu().numpy(), spec.host_weights(Y.T), rtol=1e-13, atol=1e-15)
+
+
+def test_outputs_desirabilities_match_reference_callables():
+    """Outputs.__call__(predictions=True) — the `{key}_des` columns of ask()/predict() —
+    equals the reference objective values for every golden objective, the adaptive ones
+    (MovingMaximizeSigmoid) fed with the non-null observed values of experiments_adapt
+    (bofire/data_models/domain/features.py:783-848)."""
+    for k, (obj, x, xa, ref) in enumerate(_callable_cases()):
+        feat = dm.ContinuousOutput(key=f"y{k}", objective=obj)
+        outs = dm.Outputs(features=[feat])
+        pred = pd.DataFrame({f"y{k}_pred": x, f"y{k}_sd": np.zeros_like(x)})
+        adapt = pd.DataFrame({f"y{k}": np.concatenate([xa, [np.nan]])})
+        des = outs(pred, experiments_adapt=adapt, predictions=True)
+        assert list(des.columns) == [f"y{k}_des"]
+        np.testing.assert_allclose(des[f"y{k}_des"].to_numpy(), ref, rtol=1e-12, atol=1e-15)
+    with pytest.raises(ValueError, match="experiments_adapt"):
+        outs(pred, predictions=True)

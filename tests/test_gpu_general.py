@@ -132,3 +132,23 @@ def test_qehvi_joint_batch_with_pending():
                    X_pending=torch.tensor((Xp - lo) / (hi - lo)))
     Xc = lo + (hi - lo) * np.random.default_rng(8).uniform(size=(9, q, d))
     _check(dq, orc, lo, hi, Xc)
+
+
+@pytest.mark.parametrize("q", [9, 10])
+def test_qnehvi_joint_batch_above_eight(q):
+    """q > 8 (the reference passes optimize_acqf(q=candidate_count) with no cap): 2^q - 1
+    subsets through the same kernels (QG Q = 9..12), against the oracle's inclusion-exclusion."""
+    X, lo, hi, orc, dq, _ = _setup(24, 3, 2, 8, seed=90 + q, q=q, prune=True, ls_scale=0.5)
+    Xc = lo + (hi - lo) * np.random.default_rng(q).uniform(size=(3, q, 3))
+    _check(dq, orc, lo, hi, Xc)
+
+
+def test_joint_batch_limit_message():
+    """Beyond the device limit the error names the limit (the subset count is 2^q - 1)."""
+    from everest_amd import ops
+
+    X, lo, hi, orc, dq, _ = _setup(20, 3, 2, 8, seed=3, q=2, prune=False)
+    q = ops.QNG_MAX_Q + 1
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(0).uniform(size=(1, q, 3)), device="cuda")
+    with pytest.raises(ValueError, match=f"device limit of {ops.QNG_MAX_Q}"):
+        dq.forward(Xc)
