@@ -104,12 +104,18 @@ def op_chain(acqf, Xc):
         md = acqf.model
         R, P = ops.qnehvi_small_forward(st, md, Kx, b)
         G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
-        acq, dG = ops.hvi_forward_backward(st, G, b, flags)
+        if ops.hvi_restart_fb_applies(st, b):
+            # the plan's one-launch restart scan (hvi_kd3: thresholds + scan + split reduction)
+            _, dG = ops.hvi_restart_fb(st, G, b)
+            scan = lambda: ops.hvi_restart_fb(st, G, b)   # noqa: E731
+        else:
+            _, dG = ops.hvi_forward_backward(st, G, b, flags)
+            scan = lambda: ops.hvi_forward_backward(st, G, b, flags)   # noqa: E731
         return {
             "kernel_matrix": lambda: gp.cross(Xc),
             "proj_fwd": lambda: ops.qnehvi_small_forward(st, md, Kx, b),
             "samples": lambda: ops.qnehvi_small_samples(st, R, P, b),
-            "hvi_fwd_bwd": lambda: ops.hvi_forward_backward(st, G, b, flags),
+            "hvi_fwd_bwd": scan,
             "proj_bwd": lambda: ops.qnehvi_small_backward(st, md, Xc, R, L22, dG, b),
         }
     R, P = ops.qnehvi_project(st, acqf.M, Kx, b)

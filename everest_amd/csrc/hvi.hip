@@ -1256,6 +1256,344 @@ __global__ __launch_bounds__(256) void hvi_kd2(int b, int S, int ntiles, int nsp
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// hvi_kd3 — the restart-batch (b <= 32) forward + backward scan in ONE launch: one workgroup
+// per sample holds the sample's nz <= 4 group-range splits (hvi_kd2's count: 4 at S = 256, 2
+// at S = 512) as 256-thread sub-workgroups, each running hvi_kd2's filter / window / term loop on its
+// round-robin share of the 16-group chunks.  What the three-launch chain spread over kernels
+// is done in LDS:
+//   * the thresholds t_j(y_c) (hvi_thresholds) by binary search in the sample's ascending
+//     lower bounds, staged once for all splits together with the point table;
+//   * the split partials (hvi_reduce_fb's backward half): after one barrier every (candidate,
+//     value) sums its splits x wave-split partials in hvi_kd2's partial order, so dG is
+//     bitwise the kd2 + reduce_fb result; the per-sample values (sval[s][c]) are left for the
+//     dX reduction kernel, which forms acq = mean over samples (qs_dx_reduce).
+// ---------------------------------------------------------------------------------------
+constexpr int KD3_NZ = 4;   // splits (sub-workgroups) per sample
+
+struct Kd3Lds {
+  size_t pt, th, zb, gb, mA, pA, per_z, bytes;
+  int nqz;
+};
+__host__ __device__ inline Kd3Lds kd3_lds(int stride, int M, int max_groups, int nz) {
+  Kd3Lds L;
+  const int nq = (max_groups + 15) / 16;
+  L.nqz = (nq + nz - 1) / nz;   // chunks of one split (round-robin share)
+  size_t o = 0;
+  L.pt = o;
+  o += (size_t)stride * M * 8;
+  L.th = o;
+  o += (size_t)stride * M * 8;
+  o = (o + 15) & ~(size_t)15;
+  L.zb = o;
+  // per split: group minima (16 per chunk), (chunk, candidate) masks, per-wave u16 prefixes
+  L.gb = 0;
+  size_t p = (size_t)L.nqz * 16 * 16;
+  L.mA = p;
+  p += (size_t)L.nqz * KD_CT * 2;
+  p = (p + 15) & ~(size_t)15;
+  L.pA = p;
+  p += ((size_t)KD_CT * L.nqz + 4) * 2;
+  L.per_z = (p + 15) & ~(size_t)15;
+  L.bytes = o + L.per_z * nz;
+  return L;
+}
+
+template <int M>
+__global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const double* __restrict__ G, HviKd kd,
+                                                double* __restrict__ sval, double* __restrict__ dG, int W,
+                                                int balance) {
+  constexpr int NV = M + 1;
+  constexpr int CW = KD_CT / 4;   // candidate slots per wave
+  using K = CellKey<M>;
+  extern __shared__ __align__(16) unsigned char kd_dyn[];
+  __shared__ double yv[KD_CT][M];
+  __shared__ __align__(16) unsigned short ths[KD_CT][8];   // packed thresholds (objectives >= M: 1)
+  __shared__ double acc[KD3_NZ][KD_CT][NV];
+  __shared__ uint4 cmin[KD3_NZ][KD_MAX_NQ];
+  __shared__ int mk[KD3_NZ][4][64];
+  const int s = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;   // nth = 256 nz
+  const int z = tid >> 8, t = tid & 255, lane = t & 63, wave = t >> 6;
+  const int ngr = 4 / W;
+  const int gsz = (W > 1 && balance) ? min(CW, (min(KD_CT / W, b) + ngr - 1) / ngr) : CW;
+  auto cand = [&](int c) { return (c >> 4) * gsz + (c & 15); };
+  auto valid = [&](int c) { return (c & 15) < gsz && cand(c) < b; };
+  const int stride = kd.stride;
+  const Kd3Lds Lo = kd3_lds(stride, M, kd.max_groups, nz);
+  double* pt = (double*)(kd_dyn + Lo.pt);
+  double* thv = (double*)(kd_dyn + Lo.th);
+  unsigned char* zbase = kd_dyn + Lo.zb + Lo.per_z * z;
+  uint4* gb = (uint4*)(zbase + Lo.gb);
+  unsigned short* mA = (unsigned short*)(zbase + Lo.mA);
+  const int Gsamp = kd.goff[s + 1] - kd.goff[s];
+  const int NQall = (Gsamp + 15) >> 4;
+  // this split's chunks: the sample's chunk z + ql * nz (round-robin, as hvi_kd2's ilv)
+  const bool zin = z < nz;
+  const int NQ = (zin && z < NQall) ? (NQall - z + nz - 1) / nz : 0;
+  auto qgl = [&](int ql) { return z + ql * nz; };
+  auto gend_of = [&](int ql) { return min(16, Gsamp - 16 * qgl(ql)); };
+  const int gbase = kd.goff[s];
+  const int Gs = 16 * NQ - ((NQ > 0 && qgl(NQ - 1) == NQall - 1) ? 16 * NQall - Gsamp : 0);
+  unsigned short* pA = (unsigned short*)(zbase + Lo.pA) + wave * (CW * NQ + 1);
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;
+
+  // ---- staging (all splits): point table, ascending lower bounds, candidate values ----
+  {
+    const double* src = kd.pts + (size_t)s * stride * M;
+    const double* srt = kd.sv + (size_t)s * M * stride;
+    const int n = stride * M;
+    for (int e = tid; e < n; e += nth) {
+      const double a = src[e], c = srt[e];
+      pt[e] = a;
+      thv[e] = c;
+    }
+  }
+  for (int e = t; e < 16 * NQ; e += 256) {
+    const int q = e >> 4, g = 16 * qgl(q) + (e & 15);
+    uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (g < Gsamp) {
+      v = gmin[g];
+      gb[e] = v;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      v.x = pk_min_u16(v.x, (unsigned int)__shfl_xor((int)v.x, o, 64));
+      v.y = pk_min_u16(v.y, (unsigned int)__shfl_xor((int)v.y, o, 64));
+      v.z = pk_min_u16(v.z, (unsigned int)__shfl_xor((int)v.z, o, 64));
+      v.w = pk_min_u16(v.w, (unsigned int)__shfl_xor((int)v.w, o, 64));
+    }
+    if ((e & 15) == 0) cmin[z][q] = v;
+  }
+  for (int e = tid; e < KD_CT * M; e += nth) {
+    const int j = e / KD_CT, c = e - j * KD_CT;
+    yv[c][j] = valid(c) ? G[((size_t)s * M + j) * b + cand(c)] : -INFINITY;
+  }
+  for (int e = tid; e < KD3_NZ * KD_CT * NV; e += nth) (&acc[0][0][0])[e] = 0.0;
+  __syncthreads();
+  // thresholds: t_j = #{rows with lower-bound value <= y_j} (hvi_thresholds' search)
+  if (tid < KD_CT * 8) {
+    const int c = tid >> 3, j = tid & 7;
+    unsigned short v = 1;
+    if (j < M) {
+      v = 0;
+      if (valid(c)) {
+        const double y = yv[c][j];
+        const double* tv = thv + (size_t)j * stride;
+        int lo = 0, hi = stride;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (tv[mid] <= y) lo = mid + 1;
+          else hi = mid;
+        }
+        v = (unsigned short)lo;
+      }
+    }
+    ths[c][j] = v;
+  }
+  __syncthreads();
+  const uint4* thp = reinterpret_cast<const uint4*>(&ths[0][0]);
+  const int wsub = wave % W;
+  const int cbase = (wave / W) * CW;
+  const int aslot = wave * CW;
+  double (*accz)[NV] = acc[z];
+  if (zin && valid(cbase)) {
+    const int qw0 = wsub, qwst = W;
+    const int NQw = wsub < NQ ? (NQ - wsub + W - 1) / W : 0;
+    const int NE = CW * NQw;
+    // ---- A: chunk pre-filter, ballot compaction, lane-dense group tests ----
+    {
+      unsigned short* ent = pA;
+      int nent = 0;
+      for (int eb = 0; eb < NE; eb += 64) {
+        const int e = eb + lane, q = qw0 + (e >> 4) * qwst, cl = e & 15;
+        bool pass = false;
+        if (e < NE) {
+          mA[q * KD_CT + cbase + cl] = 0;
+          pass = kd_pass4(cmin[z][q], thp[cbase + cl]);
+        }
+        const unsigned long long bal = __ballot(pass);
+        if (pass) ent[nent + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)e;
+        nent += __popcll(bal);
+      }
+      wave_sync();
+      for (int i = lane; i < nent; i += 64) {
+        const int e = ent[i], q = qw0 + (e >> 4) * qwst, cl = e & 15;
+        const uint4 tt = thp[cbase + cl];
+        const int gend = gend_of(q);
+        unsigned int mask = 0;
+        for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], tt) << k;
+        mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
+      }
+      if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
+    }
+    wave_sync();
+    const int per = (NE + 63) >> 6;
+    const int e0 = min(NE, lane * per), e1 = min(NE, e0 + per);
+    const unsigned int nq_magic = NQw > 0 ? (65536u + (unsigned int)NQw - 1u) / (unsigned int)NQw : 0u;
+    int PA;
+    int preE[9];
+    {
+      int cl = (int)(((unsigned int)e0 * nq_magic) >> 16), q = e0 - cl * NQw;
+      int cnt[8];
+      int loc = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        cnt[k] = 0;
+        if (e0 + k < e1) {
+          cnt[k] = __popc(mA[(qw0 + q * qwst) * KD_CT + cbase + cl]);
+          if (++q == NQw) q = 0, ++cl;
+        }
+        loc += cnt[k];
+      }
+      int run = wave_scan_excl(loc, &PA);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        preE[k] = run;
+        if (e0 + k < e1) pA[e0 + k] = (unsigned short)run;
+        run += cnt[k];
+      }
+      preE[8] = run;
+      if (lane == 0) {
+        pA[NE] = (unsigned short)PA;
+        if (kd.counters) {
+          atomicAdd(kd.counters + 0, (unsigned long long)PA);
+          atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - cand(cbase), gsz)) * Gs);
+        }
+      }
+    }
+    wave_sync();
+    int* mb = mk[z][wave];
+    int* mc = mb;
+    int carryB = -1;
+    for (int wb = 0; wb < PA; wb += 64) {
+      // ---- B: pair -> entry by marks, cell filter ----
+      mb[lane] = -1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (preE[k + 1] > preE[k] && preE[k] >= wb && preE[k] < wb + 64) mb[preE[k] - wb] = e0 + k;
+      wave_sync();
+      const int ownB = max(wave_max_incl(mb[lane]), carryB);
+      carryB = __builtin_amdgcn_readlane(ownB, 63);
+      const int p = wb + lane;
+      unsigned int mB = 0;
+      int cg = 0;
+      if (p < PA) {
+        const int cl = (int)(((unsigned int)ownB * nq_magic) >> 16), q = qw0 + (ownB - cl * NQw) * qwst;
+        const int c = cbase + cl;
+        const int g = 16 * qgl(q) + kth_bit16(mA[q * KD_CT + c], p - pA[ownB]);
+        const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
+        const uint4 tq = thp[c];
+        const unsigned int tw[4] = {tq.x, tq.y, tq.z, tq.w};
+        unsigned int a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+          const unsigned int tt = th16 | (th16 << 16);
+          const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+          a[0] &= kd_lt16(r1.x, tt);
+          a[1] &= kd_lt16(r1.y, tt);
+          a[2] &= kd_lt16(r1.z, tt);
+          a[3] &= kd_lt16(r1.w, tt);
+          a[4] &= kd_lt16(r2.x, tt);
+          a[5] &= kd_lt16(r2.y, tt);
+          a[6] &= kd_lt16(r2.z, tt);
+          a[7] &= kd_lt16(r2.w, tt);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mB |= (((a[i] >> 15) & 1u) | ((a[i] >> 30) & 2u)) << (2 * i);
+        cg = (c << 16) | g;
+      }
+      const int cntB = __popc(mB);
+      int EW;
+      const int pre = wave_scan_excl(cntB, &EW);
+      if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
+      // ---- C: term -> pair by marks, pipelined key loads, terms, segmented sums ----
+      int carryC = -1;
+      auto locate = [&](int cb, int& c, unsigned long long& key) {
+        mc[lane] = -1;
+        if (cntB > 0 && pre >= cb && pre < cb + 64) mc[pre - cb] = lane;
+        wave_sync();
+        const int o = max(wave_max_incl(mc[lane]), carryC);
+        carryC = __builtin_amdgcn_readlane(o, 63);
+        const int cgo = __shfl(cg, o, 64);
+        const int mo = __shfl((int)mB, o, 64);
+        const int po = __shfl(pre, o, 64);
+        wave_sync();
+        const bool in = cb + lane < EW;
+        c = in ? (cgo >> 16) : -1;
+        const size_t kidx = in ? (size_t)(gbase + (cgo & 0xFFFF)) * 16 + kth_bit16((unsigned int)mo, cb + lane - po)
+                               : (size_t)gbase * 16;
+        key = kd.gkeys[kidx];
+      };
+      auto term_round = [&](const int c, const unsigned long long key) {
+        int rcv = -1;
+        double val[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) val[v] = 0.0;
+        if (c >= 0) {
+          double l[M], u[M];
+          K::decode_direct(key, pt, l, u);
+          double y[M];
+#pragma unroll
+          for (int j = 0; j < M; ++j) y[j] = yv[c][j];
+          double len[M], pass[M];
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            const double raw = fmin(y[j], u[j]) - l[j];
+            len[j] = fmax(raw, 0.0);
+            const double dmin = (y[j] < u[j]) ? 1.0 : ((y[j] == u[j]) ? 0.5 : 0.0);
+            pass[j] = (raw >= 0.0) ? dmin : 0.0;
+          }
+          double pre_[M];
+          pre_[0] = 1.0;
+#pragma unroll
+          for (int j = 1; j < M; ++j) pre_[j] = pre_[j - 1] * len[j - 1];
+          val[0] = pre_[M - 1] * len[M - 1];
+          double suf = 1.0;
+#pragma unroll
+          for (int j = M - 1; j >= 0; --j) {
+            val[1 + j] = pass[j] * pre_[j] * suf;
+            suf *= len[j];
+          }
+          rcv = c;
+        }
+        seg_scan_wave_x<NV>(rcv >= 0 ? rcv : -3 - lane, val);
+        const int rnext = __shfl_down(rcv, 1, 64);
+        if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) accz[rcv - cbase + aslot][v] += val[v];
+        }
+      };
+      if (EW > 0) {
+        int cA = -1, cB = -1;
+        unsigned long long kA = 0, kB = 0;
+        locate(0, cA, kA);
+        locate(64, cB, kB);
+        for (int cb = 0; cb < EW; cb += 128) {
+          term_round(cA, kA);
+          locate(cb + 128, cA, kA);
+          if (cb + 64 < EW) term_round(cB, kB);
+          locate(cb + 192, cB, kB);
+        }
+      }
+      wave_sync();
+    }
+  }
+  __syncthreads();
+  // ---- split partials, summed in hvi_kd2's partial order (split-major, wave-split minor) ----
+  for (int e = tid; e < b * NV; e += nth) {
+    const int v = e / b, gc = e - v * b;
+    const int gi = gc / gsz, i = gc - gi * gsz;   // slot group and slot of candidate gc
+    double sum = 0.0;
+    for (int zz = 0; zz < nz; ++zz)
+      for (int ws = 0; ws < W; ++ws) sum += acc[zz][(gi * W + ws) * CW + i][v];
+    if (v == 0) sval[(size_t)s * b + gc] = sum;
+    else dG[((size_t)s * M + (v - 1)) * b + gc] = 1.0 / (double)S * sum;
+  }
+}
+
 // scan variant: 2 = hvi_kd2 (default), 1 = hvi_kd (EVR_KD=1 or evr_hvi_set_kd_variant)
 static int g_kd_variant = 0;
 static int kd_variant() {
@@ -1404,6 +1742,42 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
   return 0;
 }
 
+// hvi_kd3 (one launch: thresholds, scan, split reduction) for the restart batches: kd cells,
+// b <= 32, the kd2 variant, and its LDS within budget.  EVR_KD3=0 keeps the three-launch
+// chain (A/B).
+static bool hvi_kd3_applies(const evr_qnehvi_state* st, int b) {
+  static const bool on = [] {
+    const char* e = std::getenv("EVR_KD3");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !st || st->log_hvi || !st->grp_off || b < 1 || b > 32 || kd_variant() != 2 || st->m < 1 || st->m > 8)
+    return false;
+  if ((st->max_groups + 15) / 16 > KD_MAX_NQ) return false;
+  // the splits of hvi_kd2's launch (at most 4 sub-workgroups; S >= 256 at these batches)
+  const int nz = hvi_kd_nsplit(st, b);
+  return nz <= KD3_NZ && kd3_lds(st->pts_stride, st->m, st->max_groups, nz).bytes <= 128 * 1024;
+}
+
+template <int M>
+static int hvi_kd3_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
+                          double* dG) {
+  const int W = hvi_kd_wsplit(b);
+  // the same split count as hvi_kd2's launch (bitwise equal dG); one 256-thread
+  // sub-workgroup per split
+  const int nz = hvi_kd_nsplit(st, b);
+  EVR_CHECK(nz >= 1 && nz <= KD3_NZ, "hvi_kd3: %d splits exceed %d sub-workgroups", nz, KD3_NZ);
+  EVR_CHECK(cdiv(b, KD_CT / W) == 1, "hvi_kd3: %d candidates exceed one tile", b);
+  const Kd3Lds L = kd3_lds(st->pts_stride, M, st->max_groups, nz);
+  static const int balance = [] {
+    const char* e = std::getenv("EVR_KD_BALANCE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  EVR_HIP(hipFuncSetAttribute((const void*)hvi_kd3<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes));
+  hvi_kd3<M><<<st->S, 256 * nz, L.bytes, s>>>(b, st->S, nz, G, hvi_kd_of(st), sval, dG, W, balance);
+  EVR_LAUNCH_CHECK();
+  return 0;
+}
+
 static HviCells hvi_cells(const evr_qnehvi_state* st) {
   return HviCells{st->cell_lo, st->cell_hi, st->cell_off, st->cell_keys, st->cell_pts, st->cell_rank0,
                   st->pts_stride};
@@ -1528,6 +1902,20 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
   hvi_reduce_bwd<<<cdiv(tot, 256), 256, 0, s>>>(st->S, p.nchunk, st->m, b, wb, gout, dG);
   EVR_LAUNCH_CHECK();
   return 0;
+}
+
+int evr_hvi_restart_fb_applies(const evr_qnehvi_state* st, int b) { return hvi_kd3_applies(st, b) ? 1 : 0; }
+
+int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* sval,
+                       double* dG) {
+  if (int rc = hvi_check_state(st)) return rc;
+  EVR_CHECK(G && sval && dG && hvi_kd3_applies(st, b),
+            "evr_hvi_restart_fb: bad arguments or the state / batch is not a kd restart batch (b <= 32)");
+  int rc = 0;
+#define L(MM) rc = hvi_kd3_launch<MM>((hipStream_t)stream, st, b, G, sval, dG)
+  EVR_M_SWITCH(st->m, L);
+#undef L
+  return rc;
 }
 
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,

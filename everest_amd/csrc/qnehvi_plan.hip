@@ -40,8 +40,8 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
 int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                  double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
-                double* hout, const double* seqp, unsigned int* counter);
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
+                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags);
 constexpr int QS_TILE_ROWS = 16;
 
 // b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
@@ -59,7 +59,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
 
 struct PlanLayout {
   size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, bytes;
-  bool small, fused_kx;
+  bool small, fused_kx, fused_scan;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -78,6 +78,7 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     const char* e = std::getenv("EVR_FUSED_KX");
     L.fused_kx = L.small && e && std::string(e) == "1";
   }
+  L.fused_scan = L.small && backward && evr_hvi_restart_fb_applies(st, b);
   L.Kx = take(L.fused_kx ? 0 : 8 * m * n * b);
   L.R = take(8 * m * Rr * b);
   L.P = take(8 * (L.small ? qs_norms_doubles(st, b) : m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b));
@@ -183,10 +184,19 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : 64)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
   double* dG = (double*)(w + p->L.dG);
+  if (small && p->L.fused_scan) {
+    // one launch for thresholds + scan + split reduction (hvi_kd3); the per-sample values in
+    // the scan workspace become acq inside the dX reduction
+    if (int rc = evr_hvi_restart_fb(s, st, b, G, hw, dG)) return rc;
+    if (done) *done = hout ? 1 : 0;
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+                       hw, flags);
+  }
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (small) {
     if (done) *done = hout ? 1 : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter);
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+                       nullptr, nullptr);
   }
   double* dKx = (double*)(w + p->L.dKx);
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;

@@ -466,12 +466,39 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
 // first b blocks acq) to the pinned host buffer; after a system-scope fence each block counts
 // itself done, and the last one resets the counter and writes the evaluation's sequence
 // number into the completion word the host spins on (no separate copy-out kernel).
+//
+// With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the first b
+// blocks also form acq[c] = mean over the S samples (lane-strided, then the butterfly; NaN
+// for a candidate whose new-point Cholesky failed) and write it to acq.
 __global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
                                                    const double* __restrict__ scale, double* __restrict__ dX,
-                                                   const double* __restrict__ acq, double* hout,
-                                                   const double* seqp, unsigned int* counter) {
+                                                   double* __restrict__ acq, double* hout,
+                                                   const double* seqp, unsigned int* counter,
+                                                   const double* __restrict__ sval, int S, int m,
+                                                   const int* __restrict__ flags) {
   const int e = blockIdx.x, lane = threadIdx.x;
   const int k = e % d;
+  double av = 0.0;
+  if (sval && e < b) {
+    double x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = lane + 64 * u;
+      x[u] = s < S ? sval[(size_t)s * b + e] : 0.0;
+    }
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < S) a += x[u];
+    for (int s = lane + 256; s < S; s += 64) a += sval[(size_t)s * b + e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    bool bad = false;
+    if (flags)
+      for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + e] != 0;
+    av = bad ? nan("") : a / (double)S;
+    if (lane == 0) acq[e] = av;
+  }
   // the lane's first 8 partials loaded together, then summed in the loop's order
   double x[8];
 #pragma unroll
@@ -491,7 +518,7 @@ __global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const d
     dX[e] = r;
     if (hout) {
       hout[b + e] = r;
-      if (e < b) hout[e] = acq[e];
+      if (e < b) hout[e] = sval ? av : acq[e];
       __threadfence_system();
       const unsigned int prev = atomicAdd(counter, 1u);
       if (prev == gridDim.x - 1) {
@@ -555,15 +582,16 @@ int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mod
 }
 
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                const double* R, const double* L22, const double* dG, double* dXp, double* dX, const double* acq,
-                double* hout, const double* seqp, unsigned int* counter) {
+                const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
+                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
   qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
                                             md->lengthscales, dXp, nt, rows_per);
   EVR_LAUNCH_CHECK();
-  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter);
+  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter, sval,
+                                     st->S, st->m, flags);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -610,7 +638,8 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
                               double* dX) {
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
-  return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr);
+  return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, nullptr);
 }
 
 }  // extern "C"

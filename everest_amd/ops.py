@@ -635,6 +635,20 @@ def hvi_forward_backward(st: EvrQnehviState, G: torch.Tensor, b: int, flags: Opt
     return acq, dG
 
 
+def hvi_restart_fb_applies(st: EvrQnehviState, b: int) -> bool:
+    return bool(_native.load().evr_hvi_restart_fb_applies(ctypes.byref(st), int(b)))
+
+
+def hvi_restart_fb(st: EvrQnehviState, G: torch.Tensor, b: int):
+    """The restart-batch scan in one launch (hvi_kd3, b <= 32): (per-sample values S x b,
+    dG = dHVI/dG / S); acq = mean_over_samples(values)."""
+    S = int(st.S)
+    sval = torch.empty(S, b, dtype=torch.float64, device=G.device)
+    dG = torch.empty_like(G)
+    call("evr_hvi_restart_fb", _stream(), ctypes.byref(st), b, G.data_ptr(), sval.data_ptr(), dG.data_ptr())
+    return sval, dG
+
+
 def qnehvi_samples_backward(st: EvrQnehviState, R, L22, dG, b: int):
     gR = torch.empty_like(R)
     call("evr_qnehvi_samples_backward", _stream(), ctypes.byref(st), b, R.data_ptr(), L22.data_ptr(), dG.data_ptr(),

@@ -158,3 +158,28 @@ def test_kd_index_invariants():
     flat = rank[goff[0]:goff[1]].transpose(0, 2, 1).reshape(-1, m)[:C]
     lo_rank = np.stack([sv[0, j, flat[:, j]] for j in range(m)], 1)
     assert np.array_equal(np.sort(lo_rank, axis=0), np.sort(lo_x[:C], axis=0))
+
+
+@pytest.mark.parametrize("n,d,m,S,b", [(120, 6, 5, 256, 20), (60, 4, 3, 256, 7), (40, 3, 2, 512, 1),
+                                       (200, 6, 5, 512, 32), (90, 5, 4, 256, 16), (80, 4, 1, 1024, 3)])
+def test_restart_fused_scan_equals_three_launch_chain(n, d, m, S, b):
+    """hvi_kd3 (thresholds, scan and split reduction in one launch, the restart batches) against
+    hvi_thresholds + hvi_kd2 + hvi_reduce_fb on the same samples: dG bitwise equal (same
+    partials, same order), acq = mean of the per-sample values equal to 1e-14."""
+    from everest_amd import ops
+
+    kd, dense, lo, hi, d = _pair(n, d, m, S, seed=n + 5 * m)
+    assert ops.hvi_restart_fb_applies(kd.state, b)
+    assert not ops.hvi_restart_fb_applies(kd.state, 33) and not ops.hvi_restart_fb_applies(dense.state, b)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b + 2).uniform(size=(b, d)), device="cuda")
+    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
+    G, L22, flags = ops.qnehvi_samples_norms(kd.state, R, P, b)
+    a1, d1 = ops.hvi_forward_backward(kd.state, G, b, flags)
+    sval, d2 = ops.hvi_restart_fb(kd.state, G, b)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+    a2 = ops.mean_over_samples(sval)
+    assert torch.allclose(a1, a2, rtol=1e-14, atol=1e-300)
+    assert torch.isfinite(a1).all() and (b < 7 or (a1 > 0).any())
+    sval2, d3 = ops.hvi_restart_fb(kd.state, G, b)
+    assert torch.equal(sval, sval2) and torch.equal(d2, d3)      # bitwise reproducible

@@ -105,7 +105,7 @@ def test_small_batch_ops_equal_plan():
     from everest_amd import ops
     from everest_amd.acquisition import QNEHVI
 
-    n, d, m, S = 120, 5, 3, 64
+    n, d, m, S = 120, 5, 3, 256
     X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=23)
     gp = device_gp(X, Y, lo, hi, hyp)
     q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=2, prune_seed=3,
@@ -120,7 +120,14 @@ def test_small_batch_ops_equal_plan():
     R2, P2 = ops.qnehvi_small_forward_x(st, md, Xc, b)
     assert torch.equal(R, R2) and torch.equal(P, P2)
     G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
+    # the plan's restart scan is hvi_kd3 (one launch; dG bitwise the three-launch chain's), its
+    # acq the sample mean formed inside the dX reduction (summation order differs: 1e-14)
+    assert ops.hvi_restart_fb_applies(st, b)
     acq, dG = ops.hvi_forward_backward(st, G, b, flags)
-    dX = ops.qnehvi_small_backward(st, md, Xc, R, L22, dG, b)
+    sval, dG3 = ops.hvi_restart_fb(st, G, b)
+    assert torch.equal(dG, dG3)
+    dX = ops.qnehvi_small_backward(st, md, Xc, R, L22, dG3, b)
     a_ref, g_ref = q.forward_backward(Xc)
-    assert torch.equal(acq, a_ref) and torch.equal(dX, g_ref)
+    assert torch.equal(dX, g_ref)
+    assert torch.allclose(acq, a_ref, rtol=1e-14, atol=0) and torch.allclose(ops.mean_over_samples(sval), a_ref,
+                                                                               rtol=1e-14, atol=0)
