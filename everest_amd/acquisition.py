@@ -629,16 +629,20 @@ class QNEHVI(_BoxHviAcqf):
                 E = torch.cat([E, torch.zeros(m, nb, npend, **f64)], 2).contiguous()
             ops.add_selection(E, idx.to(torch.int32), None)                      # + P
             ops.scale_batched(E, (gp.ys ** 2).contiguous())                      # s^2 (...)
-            ops.trsm(self.L_base, E)                                             # G = L_base^-1 E
+            # G = L_base^-1 E by forward substitution (an explicit inverse of the ill-conditioned
+            # baseline root loses digits the near-training-point L22 cancellation exposes)
+            ops.trsm(self.L_base, E)
             ops.gemm_into(M[:, nk + nb_rows:nk + nb_rows + S_], Zb, E, transA=True)   # H^T = Z^T G
             if fused:
-                Lp = torch.zeros(m, nk, nk, **f64)
-                Lp[:, :n, :n].copy_(gp.L)
-                Lpi = torch.zeros(m, nk, nk, **f64)
-                Lpi[:, :n, :n].copy_(gp.Linv)
                 if npend:
+                    Lp = torch.zeros(m, nk, nk, **f64)
+                    Lp[:, :n, :n].copy_(gp.L)
+                    Lpi = torch.zeros(m, nk, nk, **f64)
+                    Lpi[:, :n, :n].copy_(gp.Linv)
                     Lp[:, n:, n:].copy_(torch.eye(npend, **f64))
                     Lpi[:, n:, n:].copy_(torch.eye(npend, **f64))
+                else:   # Lp = L, Lp^-1 = L^-1 (no padded copies)
+                    Lp, Lpi = gp.L, gp.Linv
                 ops.scale_batched(E, (1.0 / gp.ys).contiguous())                 # G / s
                 V = ops.gemm(E, Lp)                                              # nb x nk
                 Iv = ops.gemm(V, V, transA=True)                                 # V^T V

@@ -1,6 +1,8 @@
 // Native L-BFGS-B — see lbfgsb.hpp for what is restated and from where.
 #include "lbfgsb.hpp"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cmath>
 #include <limits>
@@ -81,6 +83,75 @@ double dot4(const double* a, const double* b, int n) {
   }
   for (; i < n; ++i) s0 += a[i] * b[i];
   return (s0 + s1) + (s2 + s3);
+}
+
+// The subspace step's W_F^T r and symmetric W_F^T W_F (k x k, rows of W_F contiguous, length
+// n): every entry is dot4's arithmetic exactly (the four interleaved partial sums, the scalar
+// tail into the first, (s0 + s1) + (s2 + s3)), so results do not depend on the path taken.
+// gram[i * k + j] for j >= i only.
+void gram_base(const double* W, int k, int n, const double* r, double* wv, double* gram) {
+  for (int i = 0; i < k; ++i) {
+    const double* wi = W + (size_t)i * n;
+    wv[i] = dot4(wi, r, n);
+    for (int j = i; j < k; ++j) gram[(size_t)i * k + j] = dot4(wi, W + (size_t)j * n, n);
+  }
+}
+
+// AVX2 clone (no FMA, so no contraction: the same roundings as dot4): one 4-lane register per
+// dot holds (s0, s1, s2, s3); row i is loaded once per block of four columns.
+__attribute__((target("avx2"))) inline double gram_finish(__m256d acc, const double* a, const double* b, int n4,
+                                                          int n) {
+  alignas(32) double l[4];
+  _mm256_store_pd(l, acc);
+  for (int t = n4; t < n; ++t) l[0] += a[t] * b[t];
+  return (l[0] + l[1]) + (l[2] + l[3]);
+}
+
+__attribute__((target("avx2"))) void gram_avx2(const double* W, int k, int n, const double* r, double* wv,
+                                               double* gram) {
+  const int n4 = n & ~3;
+  auto finish = [n4, n](__m256d acc, const double* a, const double* b) __attribute__((target("avx2"))) {
+    return gram_finish(acc, a, b, n4, n);
+  };
+  for (int i = 0; i < k; ++i) {
+    const double* wi = W + (size_t)i * n;
+    {
+      __m256d acc = _mm256_setzero_pd();
+      for (int t = 0; t < n4; t += 4) acc = _mm256_add_pd(acc, _mm256_mul_pd(_mm256_loadu_pd(wi + t), _mm256_loadu_pd(r + t)));
+      wv[i] = finish(acc, wi, r);
+    }
+    int j = i;
+    for (; j + 3 < k; j += 4) {
+      const double* b0 = W + (size_t)j * n;
+      const double* b1 = b0 + n;
+      const double* b2 = b1 + n;
+      const double* b3 = b2 + n;
+      __m256d a0 = _mm256_setzero_pd(), a1 = a0, a2 = a0, a3 = a0;
+      for (int t = 0; t < n4; t += 4) {
+        const __m256d x = _mm256_loadu_pd(wi + t);
+        a0 = _mm256_add_pd(a0, _mm256_mul_pd(x, _mm256_loadu_pd(b0 + t)));
+        a1 = _mm256_add_pd(a1, _mm256_mul_pd(x, _mm256_loadu_pd(b1 + t)));
+        a2 = _mm256_add_pd(a2, _mm256_mul_pd(x, _mm256_loadu_pd(b2 + t)));
+        a3 = _mm256_add_pd(a3, _mm256_mul_pd(x, _mm256_loadu_pd(b3 + t)));
+      }
+      gram[(size_t)i * k + j] = finish(a0, wi, b0);
+      gram[(size_t)i * k + j + 1] = finish(a1, wi, b1);
+      gram[(size_t)i * k + j + 2] = finish(a2, wi, b2);
+      gram[(size_t)i * k + j + 3] = finish(a3, wi, b3);
+    }
+    for (; j < k; ++j) {
+      const double* bj = W + (size_t)j * n;
+      __m256d acc = _mm256_setzero_pd();
+      for (int t = 0; t < n4; t += 4) acc = _mm256_add_pd(acc, _mm256_mul_pd(_mm256_loadu_pd(wi + t), _mm256_loadu_pd(bj + t)));
+      gram[(size_t)i * k + j] = finish(acc, wi, bj);
+    }
+  }
+}
+
+void gram(const double* W, int k, int n, const double* r, double* wv, double* g) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) gram_avx2(W, k, n, r, wv, g);
+  else gram_base(W, k, n, r, wv, g);
 }
 
 }  // namespace
@@ -394,15 +465,15 @@ void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
         }
       }
     }
-    for (int i = 0; i < k2; ++i) {
-      const double* wi = &WF[(size_t)i * nsub];
-      wv[i] = dot4(wi, r.data(), nsub);
+    std::vector<double>& GG = sc_gram_;
+    GG.resize((size_t)k2 * k2);
+    gram(WF.data(), k2, nsub, r.data(), wv.data(), GG.data());
+    for (int i = 0; i < k2; ++i)
       for (int j = i; j < k2; ++j) {
-        const double gij = dot4(wi, &WF[(size_t)j * nsub], nsub) / theta_;
+        const double gij = GG[(size_t)i * k2 + j] / theta_;
         N[(size_t)i * k2 + j] -= gij;
         if (j != i) N[(size_t)j * k2 + i] -= gij;
       }
-    }
   }
   std::vector<int>& piv = sc_piv_;
   std::vector<double>& dsub = sc_dsub_;

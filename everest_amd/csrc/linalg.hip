@@ -230,6 +230,80 @@ __global__ __launch_bounds__(256) void trsm_kernel(int n, int nrhs, const double
   }
 }
 
+// Forward substitution L X = B (lower, no transpose) for n <= TS_MAXN, 16 right-hand-side
+// columns per workgroup: 5 x 512 columns give 160 workgroups (trsm_kernel's 64-column tiles
+// gave 40, each walking its blocks alone: 0.47 ms at n = 280).  Wave w solves columns
+// 4w .. 4w + 3; within a wave, 16 lanes share a column, lane rg owning rows rg + 16a of the
+// current 64-row block.  Solved rows stay in LDS for the later blocks' updates.  Per row the
+// subtractions run in trsm_kernel's order (earlier blocks' q ascending, then the diagonal
+// block's q ascending) with the same contractions, and the division last: bitwise its result.
+constexpr int TS_C = 16, TS_MAXN = 512;
+__global__ __launch_bounds__(256) void trsm16_kernel(int n, int nrhs, const double* __restrict__ Lm, long long sL,
+                                                     int ldl, double* __restrict__ Bm, long long sB, int ldb) {
+  const double* L = Lm + blockIdx.y * sL;
+  double* B = Bm + blockIdx.y * sB;
+  const int c0 = blockIdx.x * TS_C;
+  __shared__ double Lt[TT][TT + 1];
+  extern __shared__ double Xs[];   // (nblk * 64) x 16: solved rows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rg = lane & 15, cl = wave * 4 + (lane >> 4), col = c0 + cl;
+  const bool cin = col < nrhs;
+  const int nblk = (n + TT - 1) / TT;
+  for (int bi = 0; bi < nblk; ++bi) {
+    const int r0 = bi * TT;
+    double acc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int r = r0 + rg + 16 * a;
+      acc[a] = (r < n && cin) ? B[(size_t)r * ldb + col] : 0.0;
+    }
+    for (int bj = 0; bj < bi; ++bj) {
+      const int s0 = bj * TT;
+      __syncthreads();   // Lt reuse
+      for (int e = tid; e < TT * TT; e += 256) {
+        const int rr = e >> 6, cc = e & 63;
+        const int gr = r0 + rr, gc = s0 + cc;
+        Lt[rr][cc] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int q = 0; q < TT; ++q) {
+        const double xq = Xs[(size_t)(s0 + q) * TS_C + cl];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a] -= Lt[rg + 16 * a][q] * xq;
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < TT * TT; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      const int gr = r0 + rr, gc = r0 + cc;
+      Lt[rr][cc] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;
+    }
+    __syncthreads();
+    const int rb = min(TT, n - r0);
+    const int gl = lane & ~15;
+#pragma unroll
+    for (int ao = 0; ao < 4; ++ao) {
+      for (int k = 0; k < 16; ++k) {
+        const int q = 16 * ao + k;
+        if (q >= rb) break;
+        double xq = rg == k ? acc[ao] / Lt[q][q] : 0.0;
+        xq = __shfl(xq, gl | k, 64);
+        if (rg == k) acc[ao] = xq;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          if (rg + 16 * a > q) acc[a] -= Lt[rg + 16 * a][q] * xq;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rl = rg + 16 * a, r = r0 + rl;
+      Xs[(size_t)r * TS_C + cl] = acc[a];
+      if (r < n && cin) B[(size_t)r * ldb + col] = acc[a];
+    }
+  }
+}
+
 __global__ void set_identity_kernel(int n, double* M, long long sM, int ldm) {
   double* P = M + blockIdx.y * sM;
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1221,6 +1295,17 @@ int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, in
                    int transpose, double* B, int ldb, long long strideB) {
   EVR_CHECK(n >= 1 && nrhs >= 0 && batch >= 1, "evr_trsm_lower: bad sizes");
   if (nrhs == 0) return 0;
+  static const bool ts16 = [] {   // EVR_TRSM16=0: the 64-column tile kernel everywhere (A/B)
+    const char* e = std::getenv("EVR_TRSM16");
+    return !(e && e[0] == '0');
+  }();
+  if (!transpose && ts16 && n <= TS_MAXN) {
+    const size_t xs = sizeof(double) * (size_t)cdiv(n, TT) * TT * TS_C;
+    trsm16_kernel<<<dim3(cdiv(nrhs, TS_C), batch), 256, xs, (hipStream_t)stream>>>(n, nrhs, L, strideL, ldl, B,
+                                                                                   strideB, ldb);
+    EVR_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid(cdiv(nrhs, TT), batch);
   if (transpose)
     trsm_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(n, nrhs, L, strideL, ldl, B, strideB, ldb);

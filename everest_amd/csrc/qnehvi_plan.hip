@@ -12,6 +12,8 @@
 // The plan copies the state / model structs; the device buffers they point to, the
 // workspace and the X / output buffers must outlive it (the Python QNEHVI object owns them).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <atomic>
 #include <cstring>
@@ -392,6 +394,13 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   const int b = p->b, n = b * p->md.d;
   for (int i = 0; i < n; ++i) EVR_CHECK(!(lb[i] > ub[i]), "evr_qnehvi_plan_minimize: lower bound above upper bound");
   hipStream_t s = (hipStream_t)stream;
+  // EVR_MIN_STATS=1: host time in the optimiser's steps vs the evaluations, to stderr
+  static const bool stats = [] {
+    const char* e = std::getenv("EVR_MIN_STATS");
+    return e && e[0] == '1';
+  }();
+  double t_step = 0.0, t_eval = 0.0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;
@@ -399,21 +408,33 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   // scipy's _minimize_lbfgsb driver loop
   for (;;) {
     if (task == LBFGSB_FG) {
+      double t0 = stats ? now() : 0.0;
       if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
+      double t1 = stats ? now() : 0.0;
       ++nfev;
       task = opt.step(f, g.data());
+      if (stats) {
+        const double t2 = now();
+        t_eval += t1 - t0;
+        t_step += t2 - t1;
+      }
     } else if (task == LBFGSB_NEW_X) {
       ++nit;
       if (nit >= maxiter || nfev > maxfun) {
         status = 1;
         break;
       }
+      double t1 = stats ? now() : 0.0;
       task = opt.step(f, g.data());
+      if (stats) t_step += now() - t1;
     } else {
       status = task == LBFGSB_ABNORMAL ? 2 : task == LBFGSB_ERROR ? 3 : 0;
       break;
     }
   }
+  if (stats)
+    std::fprintf(stderr, "EVR_MIN_STATS n=%d nit=%d nfev=%d eval_us=%.2f step_us=%.2f (per evaluation)\n", n, nit,
+                 nfev, t_eval / std::max(1, nfev) * 1e6, t_step / std::max(1, nfev) * 1e6);
   for (int i = 0; i < n; ++i) x[i] = std::min(ub[i], std::max(lb[i], opt.x()[i]));
   // re-evaluate at the clipped candidates ([upstream] gen_candidates_scipy's final no-grad call)
   if (int rc = plan_eval_host(s, p, x, &f, g.data())) return rc;

@@ -1,6 +1,8 @@
 """GPU parity of the dense float64 primitives (C-ABI through everest_amd.ops) against the
 torch-CPU float64 oracle.  Tolerances: 1e-12 relative-to-scale for exact-arithmetic
 restatements (GEMM, kernel assembly), 1e-10 for factorizations/solves."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -96,7 +98,7 @@ def test_cholesky_jitter_ladder():
     assert info.cpu().item() == 1
 
 
-@pytest.mark.parametrize("n,nrhs", [(1, 1), (50, 3), (64, 64), (200, 130), (513, 70)])
+@pytest.mark.parametrize("n,nrhs", [(1, 1), (50, 3), (64, 64), (200, 130), (280, 512), (512, 17), (513, 70)])
 @pytest.mark.parametrize("trans", [False, True])
 def test_trsm_and_inverse(n, nrhs, trans):
     from everest_amd import ops
@@ -198,3 +200,30 @@ def test_fused_cholesky_failure_and_ladder(variant, monkeypatch):
     Lr, jr = ogp.psd_safe_cholesky(A)
     assert torch.allclose(jit.cpu(), jr)
     assert torch.allclose(L.cpu(), Lr, atol=1e-7)
+
+
+def test_trsm16_bitwise_equals_tile_kernel(tmp_path):
+    """The 16-column forward substitution (n <= 512, the qNEHVI baseline solve) runs
+    trsm_kernel's operations in its order: bitwise equal to it (EVR_TRSM16=0 in a child
+    process selects the 64-column tile kernel)."""
+    import subprocess
+    import sys
+
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(7)
+    n, nrhs = 280, 96
+    A = torch.randn(3, n, n, generator=g, dtype=torch.float64)
+    L = torch.linalg.cholesky(A @ A.transpose(1, 2) + 1e-3 * torch.eye(n, dtype=torch.float64))
+    B = torch.randn(3, n, nrhs, generator=g, dtype=torch.float64)
+    torch.save({"L": L, "B": B}, tmp_path / "in.pt")
+    X = _t(B).contiguous()
+    ops.trsm(_t(L), X)
+    code = ("import sys, torch; sys.path.insert(0, %r); from everest_amd import ops; "
+            "d = torch.load(%r); X = d['B'].cuda().contiguous(); ops.trsm(d['L'].cuda(), X); "
+            "torch.save(X.cpu(), %r)") % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                          str(tmp_path / "in.pt"), str(tmp_path / "out.pt"))
+    env = dict(os.environ, EVR_TRSM16="0")
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=120)
+    X0 = torch.load(tmp_path / "out.pt")
+    assert torch.equal(X.cpu(), X0)
