@@ -1336,6 +1336,11 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
   const int Gs = 16 * NQ - ((NQ > 0 && qgl(NQ - 1) == NQall - 1) ? 16 * NQall - Gsamp : 0);
   unsigned short* pA = (unsigned short*)(zbase + Lo.pA) + wave * (CW * NQ + 1);
   const uint4* gmin = (const uint4*)kd.gbox + gbase;
+  // EVR_KD_PROF=2 build: per-wave wall-clock stamps (s_memrealtime, 100 MHz) — entry, staged,
+  // thresholds, filtered + prefixed, terms done, reduced — and the wave's pair / term counts
+  unsigned long long st_[6] = {0, 0, 0, 0, 0, 0};
+  long long np_ = 0, nt_ = 0;
+  if (EVR_KD_PROF == 2) st_[0] = wall_clock64();
 
   // ---- staging (all splits): point table, ascending lower bounds, candidate values ----
   {
@@ -1370,6 +1375,7 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
   }
   for (int e = tid; e < KD3_NZ * KD_CT * NV; e += nth) (&acc[0][0][0])[e] = 0.0;
   __syncthreads();
+  if (EVR_KD_PROF == 2) st_[1] = wall_clock64();
   // thresholds: t_j = #{rows with lower-bound value <= y_j} (hvi_thresholds' search)
   if (tid < KD_CT * 8) {
     const int c = tid >> 3, j = tid & 7;
@@ -1391,6 +1397,7 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
     ths[c][j] = v;
   }
   __syncthreads();
+  if (EVR_KD_PROF == 2) st_[2] = st_[3] = st_[4] = wall_clock64();
   const uint4* thp = reinterpret_cast<const uint4*>(&ths[0][0]);
   const int wsub = wave % W;
   const int cbase = (wave / W) * CW;
@@ -1424,7 +1431,7 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
         for (int k = 0; k < gend; ++k) mask |= (unsigned int)kd_pass4(gb[q * 16 + k], tt) << k;
         mA[q * KD_CT + cbase + cl] = (unsigned short)mask;
       }
-      if (kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
+      if (EVR_KD_PROF != 2 && kd.counters && lane == 0) atomicAdd(kd.counters + 3, (unsigned long long)nent);
     }
     wave_sync();
     const int per = (NE + 63) >> 6;
@@ -1455,13 +1462,17 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
       preE[8] = run;
       if (lane == 0) {
         pA[NE] = (unsigned short)PA;
-        if (kd.counters) {
+        if (EVR_KD_PROF != 2 && kd.counters) {
           atomicAdd(kd.counters + 0, (unsigned long long)PA);
           atomicAdd(kd.counters + 2, (unsigned long long)max(0, min(b - cand(cbase), gsz)) * Gs);
         }
       }
     }
     wave_sync();
+    if (EVR_KD_PROF == 2) {
+      st_[3] = wall_clock64();
+      np_ = PA;
+    }
     int* mb = mk[z][wave];
     int* mc = mb;
     int carryB = -1;
@@ -1508,7 +1519,8 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
       const int cntB = __popc(mB);
       int EW;
       const int pre = wave_scan_excl(cntB, &EW);
-      if (kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
+      if (EVR_KD_PROF == 2) nt_ += EW;
+      if (EVR_KD_PROF != 2 && kd.counters && lane == 0) atomicAdd(kd.counters + 1, (unsigned long long)EW);
       // ---- C: term -> pair by marks, pipelined key loads, terms, segmented sums ----
       int carryC = -1;
       auto locate = [&](int cb, int& c, unsigned long long& key) {
@@ -1580,6 +1592,7 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
       }
       wave_sync();
     }
+    if (EVR_KD_PROF == 2) st_[4] = wall_clock64();
   }
   __syncthreads();
   // ---- split partials, summed in hvi_kd2's partial order (split-major, wave-split minor) ----
@@ -1591,6 +1604,424 @@ __global__ __launch_bounds__(1024) void hvi_kd3(int b, int S, int nz, const doub
       for (int ws = 0; ws < W; ++ws) sum += acc[zz][(gi * W + ws) * CW + i][v];
     if (v == 0) sval[(size_t)s * b + gc] = sum;
     else dG[((size_t)s * M + (v - 1)) * b + gc] = 1.0 / (double)S * sum;
+  }
+  if (EVR_KD_PROF == 2 && kd.counters && lane == 0) {
+    st_[5] = wall_clock64();
+    unsigned long long* r = kd.counters + 16 + 8 * ((size_t)s * 16 + (tid >> 6));
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r[k] = st_[k];
+    r[6] = (unsigned long long)np_;
+    r[7] = (unsigned long long)nt_ | ((unsigned long long)z << 40) | ((unsigned long long)(zin && valid(cbase)) << 48);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// hvi_kdb — the restart-batch scan (b <= 32) with the work of a sample balanced over all 16
+// waves of its workgroup.  hvi_kd3 keeps hvi_kd2's per-wave ownership (a wave's candidates x
+// its round-robin chunks), and at optimised restart candidates a sample's terms concentrate in
+// a few chunks: the heaviest wave of a workgroup carried ~3x the mean wave's terms while the
+// other waves waited at the final barrier (tools/kd3_waves.py).  Here every phase is spread
+// over the workgroup in candidate-major order:
+//   A. (candidate, chunk) entries, one per thread: chunk test, then the chunk's 16 group tests
+//      -> 16-bit group masks; a block scan of their popcounts numbers the passing (candidate,
+//      group) pairs candidate-major, and each entry writes its pairs;
+//   B. pairs, one per thread (layers of KB_THREADS): the group's 16 cell tests -> 16-bit cell
+//      masks; a block scan numbers the terms and each pair writes its terms' (key index,
+//      candidate);
+//   C. terms split evenly over the 16 waves in rounds of 64: key decode, term and subgradients;
+//      a wave share spanning few candidates (the usual case: a candidate's terms are one
+//      contiguous run) sums per lane in registers and reduces once per candidate, otherwise
+//      segmented sums keyed by candidate per round — into the wave's own accumulators;
+//   then per (candidate, value) the 16 waves' partials summed in wave order.
+// Pairs and terms go through LDS in slices of KB_PCAP / KB_TCAP, so any count is handled.
+// Every order is a function of the data only: bitwise reproducible.  Not bitwise equal to
+// hvi_kd2 (different summation order; equal to rounding).
+// ---------------------------------------------------------------------------------------
+constexpr int KB_THREADS = 1024, KB_WAVES = 16, KB_B = 32, KB_PCAP = 4096, KB_TCAP = 8192;
+// candidate slots of the register accumulation (a wave share spanning more candidates takes
+// the segmented-scan rounds)
+constexpr int KB_SLOTS = 3;
+
+struct KbLds {
+  size_t pt, th, gbl, pinfo, tkey, tcand, acc, bytes;
+};
+__host__ __device__ inline KbLds kb_lds(int stride, int M, int max_groups) {
+  KbLds L;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t r = o;
+    o = (o + bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  L.pt = take((size_t)stride * M * 8);
+  L.th = take((size_t)stride * M * 8);
+  L.gbl = take((size_t)(max_groups + 15) / 16 * 16 * 16);
+  L.pinfo = take((size_t)KB_PCAP * 4);   // (candidate << 16 | group) per pair of a slice
+  L.tkey = take((size_t)KB_TCAP * 4);    // key index per term of a sub-slice
+  L.tcand = take((size_t)KB_TCAP);       // candidate per term
+  L.acc = take((size_t)KB_WAVES * KB_B * (M + 1) * 8);
+  L.bytes = o;
+  return L;
+}
+
+// block-wide exclusive scan of one int per thread (sum, or max with -1 as identity) in thread
+// order; *total = the block's sum / max.  sh: KB_WAVES ints.
+template <bool MAX>
+__device__ __forceinline__ int kb_scan_excl(int v, int* sh, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc;
+  if (MAX) {
+    inc = wave_max_incl(v);
+  } else {
+    int t;
+    inc = wave_scan_excl(v, &t) + v;
+  }
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  int pre = MAX ? -1 : 0, tot = MAX ? -1 : 0;
+#pragma unroll
+  for (int k = 0; k < KB_WAVES; ++k) {
+    const int x = sh[k];
+    if (k < w) pre = MAX ? max(pre, x) : pre + x;
+    tot = MAX ? max(tot, x) : tot + x;
+  }
+  __syncthreads();
+  int exw = __shfl_up(inc, 1, 64);
+  if (lane == 0) exw = MAX ? -1 : 0;
+  *total = tot;
+  return MAX ? max(pre, exw) : pre + exw;
+}
+
+template <int M>
+__global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double* __restrict__ G, HviKd kd,
+                                                      double* __restrict__ sval, double* __restrict__ dG) {
+  constexpr int NV = M + 1;
+  using K = CellKey<M>;
+  extern __shared__ __align__(16) unsigned char kd_dyn[];
+  __shared__ double yv[KB_B][M];
+  __shared__ __align__(16) unsigned short ths[KB_B][8];
+  __shared__ uint4 cminq[KD_MAX_NQ];
+  __shared__ int sh[KB_WAVES];
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int stride = kd.stride;
+  const KbLds Lo = kb_lds(stride, M, kd.max_groups);
+  double* pt = (double*)(kd_dyn + Lo.pt);
+  double* thv = (double*)(kd_dyn + Lo.th);
+  uint4* gbl = (uint4*)(kd_dyn + Lo.gbl);
+  unsigned int* pinfo = (unsigned int*)(kd_dyn + Lo.pinfo);
+  unsigned int* tkey = (unsigned int*)(kd_dyn + Lo.tkey);
+  unsigned char* tcand = (unsigned char*)(kd_dyn + Lo.tcand);
+  double* acc = (double*)(kd_dyn + Lo.acc);   // [wave][candidate][value]
+  const int gbase = kd.goff[s];
+  const int Gsamp = kd.goff[s + 1] - gbase;
+  const int NQall = (Gsamp + 15) >> 4;
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;
+  unsigned long long st_[7] = {0, 0, 0, 0, 0, 0, 0};
+  long long nt_ = 0;
+  if (EVR_KD_PROF == 2) st_[0] = wall_clock64();
+
+  // ---- staging: point table, ascending lower bounds, group minima (+ chunk minima), values
+  {
+    const double* src = kd.pts + (size_t)s * stride * M;
+    const double* srt = kd.sv + (size_t)s * M * stride;
+    for (int e = tid; e < stride * M; e += KB_THREADS) {
+      const double a = src[e], c = srt[e];
+      pt[e] = a;
+      thv[e] = c;
+    }
+  }
+  for (int e = tid; e < 16 * NQall; e += KB_THREADS) {
+    uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (e < Gsamp) {
+      v = gmin[e];
+      gbl[e] = v;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      v.x = pk_min_u16(v.x, (unsigned int)__shfl_xor((int)v.x, o, 64));
+      v.y = pk_min_u16(v.y, (unsigned int)__shfl_xor((int)v.y, o, 64));
+      v.z = pk_min_u16(v.z, (unsigned int)__shfl_xor((int)v.z, o, 64));
+      v.w = pk_min_u16(v.w, (unsigned int)__shfl_xor((int)v.w, o, 64));
+    }
+    if ((e & 15) == 0) cminq[e >> 4] = v;
+  }
+  for (int e = tid; e < KB_B * M; e += KB_THREADS) {
+    const int j = e / KB_B, c = e - j * KB_B;
+    yv[c][j] = c < b ? G[((size_t)s * M + j) * b + c] : -INFINITY;
+  }
+  for (int e = tid; e < KB_WAVES * KB_B * NV; e += KB_THREADS) acc[e] = 0.0;
+  __syncthreads();
+  if (EVR_KD_PROF == 2) st_[1] = wall_clock64();
+  // thresholds t_j = #{rows with lower-bound value <= y_j} (hvi_thresholds' search)
+  if (tid < KB_B * 8) {
+    const int c = tid >> 3, j = tid & 7;
+    unsigned short v = 1;
+    if (j < M) {
+      v = 0;
+      if (c < b) {
+        const double y = yv[c][j];
+        const double* tv = thv + (size_t)j * stride;
+        int lo = 0, hi = stride;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (tv[mid] <= y) lo = mid + 1;
+          else hi = mid;
+        }
+        v = (unsigned short)lo;
+      }
+    }
+    ths[c][j] = v;
+  }
+  __syncthreads();
+  const uint4* thp = reinterpret_cast<const uint4*>(&ths[0][0]);
+  if (EVR_KD_PROF == 2) st_[2] = wall_clock64();
+
+  // ---- A: entries e = c * NQall + q, one per thread ----
+  const int NE = b * NQall;   // <= KB_B * KD_MAX_NQ = KB_THREADS
+  unsigned int emk = 0;       // the entry's passing groups
+  int ec = 0, eq = 0;
+  if (tid < NE) {
+    ec = tid / NQall;
+    eq = tid - ec * NQall;
+    const uint4 tt = thp[ec];
+    if (kd_pass4(cminq[eq], tt)) {
+      const int gend = min(16, Gsamp - 16 * eq);
+      for (int k = 0; k < gend; ++k) emk |= (unsigned int)kd_pass4(gbl[eq * 16 + k], tt) << k;
+    }
+  }
+  int PT;
+  const int ep0 = kb_scan_excl<false>(__popc(emk), sh, &PT);   // the entry's first pair
+  if (kd.counters && EVR_KD_PROF != 2 && tid == 0) {
+    atomicAdd(kd.counters + 0, (unsigned long long)PT);
+    atomicAdd(kd.counters + 2, (unsigned long long)b * Gsamp);
+  }
+  if (EVR_KD_PROF == 2) st_[3] = wall_clock64();
+
+  constexpr int PPT = KB_PCAP / KB_THREADS;   // pairs per thread in a slice
+  for (int P0 = 0; P0 < PT; P0 += KB_PCAP) {
+    const int Pn = min(KB_PCAP, PT - P0);
+    // ---- the slice's pairs (candidate, group), written by their entries ----
+    {
+      unsigned int mk = emk;
+      int p = ep0;
+      while (mk) {
+        const int k = __ffs(mk) - 1;
+        mk &= mk - 1;
+        if (p >= P0 && p < P0 + Pn) pinfo[p - P0] = ((unsigned int)ec << 16) | (unsigned int)(16 * eq + k);
+        ++p;
+      }
+    }
+    __syncthreads();
+    // ---- B: the group's cell tests; pair i = u * KB_THREADS + tid (layers of one pair per
+    //      thread, so a thread writes at most 16 terms per layer) ----
+    unsigned int pmk[PPT], pin[PPT];
+    int tcnt[PPT], tpu[PPT];
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int i = u * KB_THREADS + tid;
+      tcnt[u] = 0;
+      pmk[u] = 0;
+      pin[u] = 0;
+      if (i < Pn) {
+        const unsigned int info = pinfo[i];
+        const int c = (int)(info >> 16), g = (int)(info & 0xFFFFu);
+        const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
+        const uint4 tq = thp[c];
+        const unsigned int tw[4] = {tq.x, tq.y, tq.z, tq.w};
+        unsigned int a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+          const unsigned int t2 = th16 | (th16 << 16);
+          const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+          a[0] &= kd_lt16(r1.x, t2);
+          a[1] &= kd_lt16(r1.y, t2);
+          a[2] &= kd_lt16(r1.z, t2);
+          a[3] &= kd_lt16(r1.w, t2);
+          a[4] &= kd_lt16(r2.x, t2);
+          a[5] &= kd_lt16(r2.y, t2);
+          a[6] &= kd_lt16(r2.z, t2);
+          a[7] &= kd_lt16(r2.w, t2);
+        }
+        unsigned int mB = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mB |= (((a[k] >> 15) & 1u) | ((a[k] >> 30) & 2u)) << (2 * k);
+        pmk[u] = mB;
+        pin[u] = info;
+        tcnt[u] = __popc(mB);
+      }
+    }
+    // term numbering in pair order: one block scan per populated layer
+    int TT_ = 0;
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      tpu[u] = 0;
+      if (u * KB_THREADS < Pn) {
+        int tot;
+        tpu[u] = TT_ + kb_scan_excl<false>(tcnt[u], sh, &tot);
+        TT_ += tot;
+      }
+    }
+    if (kd.counters && EVR_KD_PROF != 2 && tid == 0) atomicAdd(kd.counters + 1, (unsigned long long)TT_);
+    if (EVR_KD_PROF == 2 && P0 == 0) st_[4] = wall_clock64();
+    // ---- C: terms in sub-slices of KB_TCAP: (key index, candidate) written by their pairs,
+    //      then split evenly over the waves ----
+    for (int T0 = 0; T0 < TT_; T0 += KB_TCAP) {
+      const int Tn = min(KB_TCAP, TT_ - T0);
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        if (pmk[u] == 0 || tpu[u] >= T0 + Tn || tpu[u] + tcnt[u] <= T0) continue;
+        unsigned int mk = pmk[u];
+        int t = tpu[u];
+        const unsigned int kb = (unsigned int)(gbase + (int)(pin[u] & 0xFFFFu)) * 16u;
+        const unsigned char cc = (unsigned char)(pin[u] >> 16);
+        while (mk) {
+          const int k = __ffs(mk) - 1;
+          mk &= mk - 1;
+          if (t >= T0 && t < T0 + Tn) {
+            tkey[t - T0] = kb + (unsigned int)k;
+            tcand[t - T0] = cc;
+          }
+          ++t;
+        }
+      }
+      __syncthreads();
+      // wave's share [tb, te) of the sub-slice
+      const int tb = (int)(((long long)Tn * wave) / KB_WAVES), te = (int)(((long long)Tn * (wave + 1)) / KB_WAVES);
+      double* accw = acc + (size_t)wave * KB_B * NV;
+      auto locate = [&](int t, int& c, unsigned long long& key) {
+        const bool in = t < te;
+        const int tt = in ? t : tb;   // past the end: a valid dummy (the share's first term)
+        key = kd.gkeys[tkey[tt]];
+        c = in ? (int)tcand[tt] : -1;
+      };
+      // the term of key x candidate c and its subgradients (torch's min / clamp rules)
+      auto term_value = [&](const unsigned long long key, const int c, double (&val)[NV]) {
+        double l[M], u[M];
+        K::decode_direct(key, pt, l, u);
+        double len[M], pass[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const double y = yv[c][j];
+          const double raw = fmin(y, u[j]) - l[j];
+          len[j] = fmax(raw, 0.0);
+          const double dmin = (y < u[j]) ? 1.0 : ((y == u[j]) ? 0.5 : 0.0);
+          pass[j] = (raw >= 0.0) ? dmin : 0.0;
+        }
+        double pre_[M];
+        pre_[0] = 1.0;
+#pragma unroll
+        for (int j = 1; j < M; ++j) pre_[j] = pre_[j - 1] * len[j - 1];
+        val[0] = pre_[M - 1] * len[M - 1];
+        double suf = 1.0;
+#pragma unroll
+        for (int j = M - 1; j >= 0; --j) {
+          val[1 + j] = pass[j] * pre_[j] * suf;
+          suf *= len[j];
+        }
+      };
+      auto term_round = [&](const int c, const unsigned long long key) {
+        int rcv = -1;
+        double val[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) val[v] = 0.0;
+        if (c >= 0) {
+          term_value(key, c, val);
+          rcv = c;
+        }
+        seg_scan_wave_x<NV>(rcv >= 0 ? rcv : -3 - lane, val);
+        const int rnext = __shfl_down(rcv, 1, 64);
+        if (rcv >= 0 && (lane == 63 || rnext != rcv)) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) accw[rcv * NV + v] += val[v];
+        }
+      };
+      // the share's candidates: a contiguous range [cf, cl] (candidate-major terms)
+      const int cf = te > tb ? (int)tcand[tb] : 0;
+      const int cl = te > tb ? (int)tcand[te - 1] : -1;
+      if (te > tb && cl - cf < KB_SLOTS) {
+        // few candidates (long runs, the usual case): every lane sums its terms per candidate
+        // slot in registers across the rounds, then one butterfly per (slot, value) — instead
+        // of a segmented scan per round
+        if (EVR_KD_PROF == 2) nt_ += te - tb;
+        double as[KB_SLOTS][NV];
+#pragma unroll
+        for (int k = 0; k < KB_SLOTS; ++k)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) as[k][v] = 0.0;
+        auto term_acc = [&](const int c, const unsigned long long key) {
+          if (c < 0) return;
+          double val[NV];
+          term_value(key, c, val);
+          const int k = c - cf;
+#pragma unroll
+          for (int kk = 0; kk < KB_SLOTS; ++kk)
+            if (k == kk) {
+#pragma unroll
+              for (int v = 0; v < NV; ++v) as[kk][v] += val[v];
+            }
+        };
+        int cA, cB;
+        unsigned long long kA, kB;
+        locate(tb + lane, cA, kA);
+        locate(tb + 64 + lane, cB, kB);
+        for (int r = tb; r < te; r += 128) {
+          term_acc(cA, kA);
+          locate(r + 128 + lane, cA, kA);
+          if (r + 64 < te) term_acc(cB, kB);
+          locate(r + 192 + lane, cB, kB);
+        }
+        // per (slot, value) the wave sum by a DPP inclusive scan (VALU only, fixed order):
+        // lane 63 holds the total
+#pragma unroll
+        for (int kk = 0; kk < KB_SLOTS; ++kk) {
+          if (cf + kk > cl) break;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            double x = as[kk][v];
+            x += dpp_f64<0x111, 0xF>(x);
+            x += dpp_f64<0x112, 0xF>(x);
+            x += dpp_f64<0x114, 0xF>(x);
+            x += dpp_f64<0x118, 0xF>(x);
+            x += dpp_f64<0x142, 0xA>(x);
+            x += dpp_f64<0x143, 0xC>(x);
+            if (lane == 63) accw[(cf + kk) * NV + v] += x;
+          }
+        }
+      } else if (te > tb) {
+        if (EVR_KD_PROF == 2) nt_ += te - tb;
+        int cA, cB;
+        unsigned long long kA, kB;
+        locate(tb + lane, cA, kA);
+        locate(tb + 64 + lane, cB, kB);
+        for (int r = tb; r < te; r += 128) {
+          term_round(cA, kA);
+          locate(r + 128 + lane, cA, kA);
+          if (r + 64 < te) term_round(cB, kB);
+          locate(r + 192 + lane, cB, kB);
+        }
+      }
+      __syncthreads();   // tkey / tcand / acc rows reused
+    }
+  }
+  if (EVR_KD_PROF == 2) st_[5] = wall_clock64();
+  // ---- the waves' partials per (candidate, value), summed in wave order ----
+  for (int e = tid; e < b * NV; e += KB_THREADS) {
+    const int v = e / b, c = e - v * b;
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < KB_WAVES; ++w) sum += acc[((size_t)w * KB_B + c) * NV + v];
+    if (v == 0) sval[(size_t)s * b + c] = sum;
+    else dG[((size_t)s * M + (v - 1)) * b + c] = 1.0 / (double)S * sum;
+  }
+  if (EVR_KD_PROF == 2 && kd.counters && lane == 0) {
+    st_[6] = wall_clock64();
+    unsigned long long* r = kd.counters + 16 + 8 * ((size_t)s * 16 + wave);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) r[k] = st_[k];
+    r[7] = (unsigned long long)nt_;
   }
 }
 
@@ -1739,6 +2170,35 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
     hvi_reduce_bwd<<<cdiv(tot, 256), 256, 0, s>>>(st->S, ns, M, b, dgp, gout, dG);
     EVR_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// restart-scan kernel: 2 = hvi_kdb (balanced, default), 1 = hvi_kd3 (EVR_KDB=0 or
+// evr_hvi_set_restart_variant)
+static int g_restart_variant = 0;
+static int restart_variant() {
+  if (g_restart_variant == 0) {
+    const char* e = std::getenv("EVR_KDB");
+    g_restart_variant = (e && e[0] == '0') ? 1 : 2;
+  }
+  return g_restart_variant;
+}
+
+static bool hvi_kdb_applies(const evr_qnehvi_state* st, int b) {
+  if (restart_variant() != 2 || !st || st->log_hvi || !st->grp_off || b < 1 || b > KB_B || kd_variant() != 2 ||
+      st->m < 1 || st->m > 8)
+    return false;
+  if ((st->max_groups + 15) / 16 > KD_MAX_NQ) return false;
+  return kb_lds(st->pts_stride, st->m, st->max_groups).bytes <= 148 * 1024;
+}
+
+template <int M>
+static int hvi_kdb_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
+                          double* dG) {
+  const KbLds L = kb_lds(st->pts_stride, M, st->max_groups);
+  EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdb<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes));
+  hvi_kdb<M><<<st->S, KB_THREADS, L.bytes, s>>>(b, st->S, G, hvi_kd_of(st), sval, dG);
+  EVR_LAUNCH_CHECK();
   return 0;
 }
 
@@ -1904,18 +2364,32 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
   return 0;
 }
 
-int evr_hvi_restart_fb_applies(const evr_qnehvi_state* st, int b) { return hvi_kd3_applies(st, b) ? 1 : 0; }
+int evr_hvi_restart_fb_applies(const evr_qnehvi_state* st, int b) {
+  return (hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)) ? 1 : 0;
+}
 
 int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* sval,
                        double* dG) {
   if (int rc = hvi_check_state(st)) return rc;
-  EVR_CHECK(G && sval && dG && hvi_kd3_applies(st, b),
+  EVR_CHECK(G && sval && dG && (hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)),
             "evr_hvi_restart_fb: bad arguments or the state / batch is not a kd restart batch (b <= 32)");
   int rc = 0;
+  if (hvi_kdb_applies(st, b)) {
+#define L(MM) rc = hvi_kdb_launch<MM>((hipStream_t)stream, st, b, G, sval, dG)
+    EVR_M_SWITCH(st->m, L);
+#undef L
+    return rc;
+  }
 #define L(MM) rc = hvi_kd3_launch<MM>((hipStream_t)stream, st, b, G, sval, dG)
   EVR_M_SWITCH(st->m, L);
 #undef L
   return rc;
+}
+
+int evr_hvi_set_restart_variant(int variant) {
+  EVR_CHECK(variant == 1 || variant == 2, "evr_hvi_set_restart_variant: variant must be 1 or 2, got %d", variant);
+  g_restart_variant = variant;
+  return 0;
 }
 
 int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G, const double* gout,

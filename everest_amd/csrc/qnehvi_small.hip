@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int n, int nb, int Rr, int b, in
 
 // ---------------------------------------------------------------------------------------
 // backward: per (16 training rows i0.., output j): coefficients, dK_x tile = M_j^T gR (MFMA),
-// cross-covariance gradient partial dXp[j*ntile + tile][c][k].  gR rows come from R (rows
+// cross-covariance gradient partial dXp[c][k][(j, z, tile)].  gR rows come from R (rows
 // < n + nb, times the per-candidate coefficients), a_j dG (sample rows) or the coefficient
 // itself (mean row); the chunk of 128 rows of M (16 columns) and of the gR sources is loaded
 // with coalesced row segments, the coefficients applied while staging in LDS.
@@ -456,30 +456,35 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       double v = gx[0][cc][k];
 #pragma unroll
       for (int q = 1; q < 8; ++q) v += gx[q][cc][k];
-      if (cc < b && k < d) dXp[((((size_t)j * gridDim.z + z) * ntile + tile) * b + cc) * d + k] = v;
+      // element-major partials (dXp[c][k][p], p = (j, z, tile)): the reduction reads each
+      // element's partials contiguously
+      const size_t np = (size_t)gridDim.y * gridDim.z * ntile;
+      if (cc < b && k < d) dXp[((size_t)cc * d + k) * np + ((size_t)j * gridDim.z + z) * ntile + tile] = v;
     }
   }
 }
 
-// one wave per dX element: lane-strided partial sums, then a fixed xor-butterfly.  Host mode
-// (hout != nullptr, the plan's host graph): every block also writes its dX element (and the
-// first b blocks acq) to the pinned host buffer; after a system-scope fence each block counts
-// itself done, and the last one resets the counter and writes the evaluation's sequence
-// number into the completion word the host spins on (no separate copy-out kernel).
+// one wave per dX element (4 per workgroup): lane-strided partial sums over the element's
+// contiguous partials, then a fixed xor-butterfly.  Host mode (hout != nullptr, the plan's host
+// graph): every wave also writes its dX element (and the first b acq) to the pinned host
+// buffer; after a system-scope fence each workgroup counts itself done, and the last one
+// resets the counter and writes the evaluation's sequence number into the completion word the
+// host spins on (no separate copy-out kernel).
 //
-// With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the first b
-// blocks also form acq[c] = mean over the S samples (lane-strided, then the butterfly; NaN
-// for a candidate whose new-point Cholesky failed) and write it to acq.
-__global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
-                                                   const double* __restrict__ scale, double* __restrict__ dX,
-                                                   double* __restrict__ acq, double* hout,
-                                                   const double* seqp, unsigned int* counter,
-                                                   const double* __restrict__ sval, int S, int m,
-                                                   const int* __restrict__ flags) {
-  const int e = blockIdx.x, lane = threadIdx.x;
+// With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the waves of
+// the first b elements also form acq[c] = mean over the S samples (lane-strided, then the
+// butterfly; NaN for a candidate whose new-point Cholesky failed) and write it to acq.
+__global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
+                                                    const double* __restrict__ scale, double* __restrict__ dX,
+                                                    double* __restrict__ acq, double* hout,
+                                                    const double* seqp, unsigned int* counter,
+                                                    const double* __restrict__ sval, int S, int m,
+                                                    const int* __restrict__ flags) {
+  const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const bool ein = e < b * d;
   const int k = e % d;
   double av = 0.0;
-  if (sval && e < b) {
+  if (ein && sval && e < b) {
     double x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -499,27 +504,35 @@ __global__ __launch_bounds__(64) void qs_dx_reduce(int np, int b, int d, const d
     av = bad ? nan("") : a / (double)S;
     if (lane == 0) acq[e] = av;
   }
-  // the lane's first 8 partials loaded together, then summed in the loop's order
+  // the lane's first 8 partials (contiguous over the wave) loaded together, then summed in the
+  // loop's order
+  const double* src = dXp + (size_t)(ein ? e : 0) * np;
   double x[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int p = lane + 64 * u;
-    x[u] = p < np ? dXp[(size_t)p * b * d + e] : 0.0;
+    x[u] = (ein && p < np) ? src[p] : 0.0;
   }
   double v = 0.0;
 #pragma unroll
   for (int u = 0; u < 8; ++u)
     if (lane + 64 * u < np) v += x[u];
-  for (int p = lane + 512; p < np; p += 64) v += dXp[(size_t)p * b * d + e];
+  if (ein)
+    for (int p = lane + 512; p < np; p += 64) v += src[p];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) {
+  if (lane == 0 && ein) {
     const double r = v * (scale ? scale[k] : 1.0);
     dX[e] = r;
     if (hout) {
       hout[b + e] = r;
       if (e < b) hout[e] = sval ? av : acq[e];
       __threadfence_system();
+    }
+  }
+  if (hout) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
       const unsigned int prev = atomicAdd(counter, 1u);
       if (prev == gridDim.x - 1) {
         atomicExch(counter, 0u);
@@ -590,8 +603,8 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
                                             md->lengthscales, dXp, nt, rows_per);
   EVR_LAUNCH_CHECK();
-  qs_dx_reduce<<<b * d, 64, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter, sval,
-                                     st->S, st->m, flags);
+  qs_dx_reduce<<<cdiv(b * d, 4), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter,
+                                               sval, st->S, st->m, flags);
   EVR_LAUNCH_CHECK();
   return 0;
 }

@@ -427,6 +427,33 @@ class Inputs(_Features):
                 experiments[feat.key] = experiments[feat.key].astype("float64")
         return experiments
 
+    def check_continuous_candidates(self, candidates: pd.DataFrame) -> np.ndarray:
+        """validate_candidates of an all-continuous Inputs on arrays: the numeric-dtype and
+        bound checks (same errors, same order), returning the n x d float64 values (one
+        positional gather instead of DataFrame selections)."""
+        feats = self.get().features
+        cols = candidates.columns
+        idx = cols.get_indexer([f.key for f in feats])
+        for f, i in zip(feats, idx):
+            if i < 0:
+                raise ValueError(f"no col for input feature `{f.key}`")
+        dts = candidates.dtypes.to_numpy()
+        for f, i in zip(feats, idx):
+            if not pd.api.types.is_numeric_dtype(dts[i]):
+                raise ValueError(f"not all values of input feature `{f.key}` are numerical")
+        if all(dt == np.float64 for dt in dts):
+            vals = candidates.to_numpy(dtype=np.float64)[:, idx]
+        else:
+            vals = np.column_stack([candidates.iloc[:, i].to_numpy(dtype=np.float64) for i in idx])
+        lo = np.array([f.lower_bound for f in feats]) - 1e-6
+        hi = np.array([f.upper_bound for f in feats]) + 1e-6
+        bad = ((vals < lo) | (vals > hi)).any(axis=0)
+        for f, b in zip(feats, bad):
+            if b:
+                raise ValueError(f"not all values of input feature `{f.key}` are inside the bounds "
+                                 f"[{f.lower_bound}, {f.upper_bound}]")
+        return np.ascontiguousarray(vals)
+
     def validate_candidates(self, candidates: pd.DataFrame) -> pd.DataFrame:
         """Per-feature checks of ContinuousInput / CategoricalInput.validate_candidental, the
         continuous columns' bounds tested in one array pass (same errors, same order)."""
@@ -434,6 +461,9 @@ class Inputs(_Features):
         for feat in feats:
             if feat.key not in candidates:
                 raise ValueError(f"no col for input feature `{feat.key}`")
+        if all(isinstance(f, ContinuousInput) for f in feats):
+            vals = self.check_continuous_candidates(candidates)
+            return pd.DataFrame(vals, columns=[f.key for f in feats], index=candidates.index)
         dtypes = candidates.dtypes
         cont = [f for f in feats if isinstance(f, ContinuousInput)]
         if cont:
@@ -488,17 +518,23 @@ class Outputs(_Features):
         if predictions and experiments_adapt is None:
             raise ValueError("If predictions are used, `experiments_adapt` has to be provided.")
         adapt = experiments if experiments_adapt is None else experiments_adapt
+        col = (lambda k: experiments[f"{k}_pred"].to_numpy(dtype=np.float64)) if predictions else \
+            (lambda k: experiments[k].to_numpy(dtype=np.float64))
+        return pd.DataFrame(self.desirability_arrays(col, adapt), index=experiments.index)
+
+    def desirability_arrays(self, values, adapt) -> Dict[str, np.ndarray]:
+        """{key_des: objective(values(key))} for every output with an objective, in feature
+        order; values(key) gives the output's value array, adapt the observed experiments the
+        adaptive objectives (MovingMaximizeSigmoid) read."""
         cols = {}
         for feat in self.get().features:
             if feat.objective is None:
                 continue
-            col = f"{feat.key}_pred" if predictions else feat.key
-            x = experiments[col].to_numpy(dtype=np.float64)
             xa = None
             if isinstance(feat.objective, MovingMaximizeSigmoidObjective):
                 xa = adapt[feat.key].dropna().to_numpy(dtype=np.float64)
-            cols[f"{feat.key}_des"] = np.asarray(feat.objective(x, xa), dtype=np.float64)
-        return pd.DataFrame(cols, index=experiments.index)
+            cols[f"{feat.key}_des"] = np.asarray(feat.objective(values(feat.key), xa), dtype=np.float64)
+        return cols
 
     def preprocess_experiments_all_valid_outputs(self, experiments: pd.DataFrame,
                                                  output_feature_keys: Optional[List[str]] = None) -> pd.DataFrame:
@@ -624,7 +660,15 @@ class Domain(BaseModel):
     def validate_candidates(self, candidates: pd.DataFrame, only_inputs: bool = False, tol: float = 1e-5,
                             raise_validation_error: bool = True) -> pd.DataFrame:
         """bofire/data_models/domain/domain.py:417-459."""
-        cand = self.inputs.validate_candidates(candidates.copy())
+        if all(isinstance(f, ContinuousInput) for f in self.inputs.get().features):
+            # continuous inputs: the checks on one gathered array; the validated input frame is
+            # only formed when constraints need it
+            vals = self.inputs.check_continuous_candidates(candidates)
+            cand = None
+            if len(self.constraints):
+                cand = pd.DataFrame(vals, columns=self.inputs.get_keys(), index=candidates.index)
+        else:
+            cand = self.inputs.validate_candidates(candidates.copy())
         if len(self.constraints) and not self.constraints.is_fulfilled(cand, tol=tol).all():
             if raise_validation_error:
                 raise ConstraintNotFulfilledError(f"Constraints not fulfilled: {cand}")

@@ -239,12 +239,17 @@ class PredictiveStrategy(Strategy):
         if self.is_fitted is not True:
             raise ValueError("Model not yet fitted.")
         preds, stds = self._predict(experiments)
+        return self._predictions_frame(preds, stds, experiments.index)
+
+    def _predictions_frame(self, preds: np.ndarray, stds: np.ndarray, index) -> pd.DataFrame:
+        """[pred | sd | desirability] columns of predict() (the reference builds the
+        prediction frame, evaluates the objectives on it and concatenates): one array, one
+        frame."""
         pred_cols, sd_cols = get_column_names(self.domain.outputs)
-        predictions = pd.DataFrame(data=np.hstack((preds, stds)), columns=pred_cols + sd_cols)
-        objectives = self.domain.outputs(predictions, experiments_adapt=self.experiments, predictions=True)
-        predictions = pd.concat((predictions, objectives), axis=1)
-        predictions.index = experiments.index
-        return predictions
+        pos = {c: i for i, c in enumerate(pred_cols)}
+        des = self.domain.outputs.desirability_arrays(lambda k: preds[:, pos[f"{k}_pred"]], self.experiments)
+        data = np.hstack([preds, stds] + [v.reshape(-1, 1) for v in des.values()])
+        return pd.DataFrame(data, columns=pred_cols + sd_cols + list(des), index=index)
 
     def fit(self):
         assert self.experiments is not None and len(self.experiments) > 0, "No fitting data available"
@@ -440,8 +445,19 @@ class BotorchStrategy(PredictiveStrategy):
 
     def _postprocess_candidates(self, X: np.ndarray) -> pd.DataFrame:
         f2i, f2n = self.domain.inputs._transform_info(self.input_preprocessing_specs)
-        cols = [n for k in self.domain.inputs.get_keys() for n in f2n[k]]
+        keys = self.domain.inputs.get_keys()
+        cols = [n for k in keys for n in f2n[k]]
         df = pd.DataFrame(X, columns=cols)
+        if cols == keys:
+            # continuous inputs: the transform is the identity, so X is the candidates' frame;
+            # predictions on the transformed X directly, one frame for inputs + predictions
+            if self.is_fitted is not True:
+                raise ValueError("Model not yet fitted.")
+            Xt = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=self.model.device)
+            mean, var = self.model.posterior(Xt, observation_noise=True)
+            preds = self._predictions_frame(mean.T.cpu().numpy(), np.sqrt(var.T.cpu().numpy()), df.index)
+            return pd.DataFrame(np.hstack([np.asarray(X, dtype=np.float64), preds.to_numpy()]),
+                                columns=keys + list(preds.columns))
         df = self.domain.inputs.inverse_transform(df, self.input_preprocessing_specs)
         preds = self.predict(df)
         return pd.concat((df, preds), axis=1)

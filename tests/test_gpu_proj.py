@@ -120,14 +120,14 @@ def test_small_batch_ops_equal_plan():
     R2, P2 = ops.qnehvi_small_forward_x(st, md, Xc, b)
     assert torch.equal(R, R2) and torch.equal(P, P2)
     G, L22, flags = ops.qnehvi_small_samples(st, R, P, b)
-    # the plan's restart scan is hvi_kd3 (one launch; dG bitwise the three-launch chain's), its
-    # acq the sample mean formed inside the dX reduction (summation order differs: 1e-14)
+    # the plan's restart scan is the one-launch kernel (hvi_kdb: equal to the three-launch
+    # chain's dG to rounding), its acq the sample mean formed inside the dX reduction
     assert ops.hvi_restart_fb_applies(st, b)
     acq, dG = ops.hvi_forward_backward(st, G, b, flags)
     sval, dG3 = ops.hvi_restart_fb(st, G, b)
-    assert torch.equal(dG, dG3)
+    assert torch.allclose(dG3, dG, rtol=1e-12, atol=1e-15 * dG.abs().max().item())
     dX = ops.qnehvi_small_backward(st, md, Xc, R, L22, dG3, b)
     a_ref, g_ref = q.forward_backward(Xc)
     assert torch.equal(dX, g_ref)
-    assert torch.allclose(acq, a_ref, rtol=1e-14, atol=0) and torch.allclose(ops.mean_over_samples(sval), a_ref,
+    assert torch.allclose(acq, a_ref, rtol=1e-12, atol=0) and torch.allclose(ops.mean_over_samples(sval), a_ref,
                                                                                rtol=1e-14, atol=0)

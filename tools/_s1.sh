@@ -1,7 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/s5
+mkdir -p gpurun_out/s9
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_linalg.py tests/test_gpu_baseline_sizes.py tests/test_gpu_gp_qnehvi.py -x -q --timeout 120 --timeout-method thread > gpurun_out/s5/pytest.log 2>&1 &&
-timeout -k 10 200 python -u tools/construction_probes.py > gpurun_out/s5/probes.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-eval-pass --steps 10 > gpurun_out/s5/bench.json 2> gpurun_out/s5/bench.err
+EVR_MIN_STATS=1 timeout -k 10 200 python -u tools/ask_phases.py > gpurun_out/s9/phases_kdb.log 2>&1 &&
+EVR_KDB=0 EVR_MIN_STATS=1 timeout -k 10 200 python -u tools/ask_phases.py > gpurun_out/s9/phases_kd3.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-eval-pass --steps 10 > gpurun_out/s9/bench_kdb.json 2> gpurun_out/s9/bench.err &&
+EVR_KDB=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-eval-pass --steps 10 > gpurun_out/s9/bench_kd3.json 2>> gpurun_out/s9/bench.err
 echo rc=$?
