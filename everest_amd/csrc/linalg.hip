@@ -367,6 +367,13 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+__device__ __forceinline__ double bperm_f64(double v, int src_lane) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)x);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ int quad_bcast32(int v, int s) {
   switch (s) {   // quad_perm [s, s, s, s]
     case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false);
@@ -399,6 +406,42 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
+#ifdef EVR_LEAF_BPERM
+  // pivot column and inverse row by ds_bpermute (one LDS-crossbar round trip, no store /
+  // fence / load): lane (r, q) takes A[q + 4k][j] from lane 4(q + 4k) + (j & 3) and the
+  // inverse row entry E[j][q + 4k] from lane 4j + q — the values the LDS exchange carries
+#pragma unroll
+  for (int j = 0; j < CP; ++j) {
+    const double p = readlane_f64(a[j >> 2], 4 * j + (j & 3));
+    const double arj = quad_bcast_f64(a[j >> 2], j & 3);
+    double cj[4], er[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cj[k] = bperm_f64(a[j >> 2], 4 * q + 16 * k + (j & 3));
+      er[k] = bperm_f64(e[k], 4 * j + q);
+    }
+    if (!(p > 0.0)) {
+      bad = j;
+      break;
+    }
+    if (lane == 0) piv[j] = p;
+    double ip = __builtin_amdgcn_rcp(p);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    const double m = arj * ip;
+    const bool below = r > j;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = q + 4 * k;
+      const double dn = fma(-m, cj[k], a[k]);
+      const double en = fma(-m, er[k], e[k]);
+      a[k] = (below && c > j && c <= r) ? dn : a[k];
+      e[k] = (below && c <= j) ? en : e[k];
+    }
+  }
+  (void)colj;
+  (void)erow;
+#else
 #pragma unroll
   for (int j = 0; j < CP; ++j) {
     const double p = readlane_f64(a[j >> 2], 4 * j + (j & 3));   // A[j][j] (unnormalised pivot)
@@ -429,6 +472,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     }
     __builtin_amdgcn_wave_barrier();   // one wave: LDS ops complete in order; keep the compiler's order
   }
+#endif
   if (bad >= 0) return bad;
   lds_wave_sync();
 #pragma unroll
@@ -959,6 +1003,106 @@ __global__ __launch_bounds__(256) void tri_inv_row_kernel(int n, int i, const do
       }
 }
 
+// ---------------------------------------------------------------------------------------
+// Triangular inverse by 16-column panels, one launch (n <= NMAX): workgroup (c, b) owns
+// columns [16c, 16c + 16) of X = L^-1, which lie in block column cb = 16c / 64.  Rows above
+// block cb are zero, block cb is its slice of Dinv_cb, and every later block row i is
+//   X_i = -Dinv_i sum_{k=cb}^{i-1} L_ik X_k
+// with the solved rows X_k of its 16 columns resident in LDS.  The block rows of one column
+// panel are serial, but each step is a 64 x 16 x 64 product (16 MFMAs per wave) instead of
+// tri_inv_row_kernel's 64 x 64 x 64, and all column panels run at once: at n = 512 the
+// critical path is 36 such steps in one launch instead of 7 launches of up to 8 full-tile
+// steps.  Wave w owns rows 16w .. 16w + 15 of each block row; the A operands (L_ik, Dinv_i)
+// come straight from global memory (L2-resident, shared by the panels of a member), the next
+// step's issued before the current step's MFMAs.  Per element the accumulation sequence
+// (k ascending, then kk in steps of 4, the same lane / register positions in the MFMA tile,
+// out-of-range rows and columns loaded as zero) is tri_inv_row_kernel's: bitwise its result.
+// ---------------------------------------------------------------------------------------
+template <int NMAX>
+__global__ __launch_bounds__(256) void tri_inv_col_kernel(int n, const double* __restrict__ Lm, long long sL,
+                                                          int ldl, const double* __restrict__ Dinv, long long sD,
+                                                          double* __restrict__ Xm, long long sX, int ldx,
+                                                          const int* __restrict__ skip) {
+  constexpr int TW = 16;
+  __shared__ double Xs[NMAX][TW];    // solved rows of this panel (a half-wave reads 2 rows: conflict-free)
+  __shared__ double Ts[BNB][TW];     // sum_k L_ik X_k of the current block row (B operand of Dinv_i)
+  const int b = blockIdx.y, c0 = blockIdx.x * TW, cb = c0 / BNB, cl = c0 - cb * BNB;
+  const double* L = Lm + b * sL;
+  const double* Db = Dinv + b * sD;
+  double* X = Xm + b * sX;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, kq = lane >> 4;
+  const int nblk = (n + BNB - 1) / BNB;
+  const bool skp = skip && skip[b];
+  const int ncol = min(TW, n - c0);
+  for (int e = tid; e < cb * BNB * TW; e += 256) {   // zeros above the diagonal block
+    const int r = e / TW, c = e % TW;
+    if (c < ncol) X[(size_t)r * ldx + c0 + c] = 0.0;
+  }
+  {
+    const double* Dc = Db + (size_t)cb * BNB * BNB;
+    for (int e = tid; e < BNB * TW; e += 256) {
+      const int r = e / TW, c = e % TW, row = cb * BNB + r;
+      const bool in = row < n && c < ncol;
+      const double v = in ? Dc[(size_t)r * BNB + cl + c] : 0.0;
+      Xs[row][c] = v;
+      if (in) X[(size_t)row * ldx + c0 + c] = v;
+    }
+  }
+  if (skp) {   // a failed member: zeros below the diagonal block, as the row kernels leave it
+    for (int e = tid; e < (n - min(n, (cb + 1) * BNB)) * TW; e += 256) {
+      const int r = (cb + 1) * BNB + e / TW, c = e % TW;
+      if (c < ncol) X[(size_t)r * ldx + c0 + c] = 0.0;
+    }
+    return;
+  }
+  __syncthreads();
+  double a[16], an[16];
+  auto load_l = [&](double (&dst)[16], int i, int k) {
+    const int row = i * BNB + 16 * w + li;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int col = k * BNB + 4 * s + kq;
+      dst[s] = (row < n && col < n) ? L[(size_t)row * ldl + col] : 0.0;
+    }
+  };
+  auto load_d = [&](double (&dst)[16], int i) {
+    const double* Di = Db + (size_t)i * BNB * BNB + (size_t)(16 * w + li) * BNB;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) dst[s] = Di[4 * s + kq];
+  };
+  if (cb + 1 < nblk) load_l(a, cb + 1, cb);
+  for (int i = cb + 1; i < nblk; ++i) {
+    double4_t t = {0, 0, 0, 0};
+    for (int k = cb; k < i; ++k) {
+      if (k + 1 < i) load_l(an, i, k + 1);
+      else load_d(an, i);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) t = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], Xs[k * BNB + 4 * s + kq][li], t, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = an[s];
+    }
+    // D map: register r of lane l holds T[16w + (l >> 4) + 4r][l & 15]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Ts[16 * w + kq + 4 * r][li] = t[r];
+    __syncthreads();
+    if (i + 1 < nblk) load_l(an, i + 1, cb);
+    double4_t y = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) y = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], Ts[4 * s + kq][li], y, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i * BNB + 16 * w + kq + 4 * r;
+      const bool in = row < n && li < ncol;
+      const double v = -y[r];
+      Xs[row][li] = in ? v : 0.0;
+      if (in) X[(size_t)row * ldx + c0 + li] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a[s] = an[s];
+    __syncthreads();   // block row i in Xs, Ts free for the next block row
+  }
+}
+
 // Inverse of every 64x64 diagonal block of a given lower-triangular L (grid (blocks, batch)):
 // column-parallel forward substitution, row steps separated by barriers.
 __global__ __launch_bounds__(256) void diag_block_inverse_kernel(int n, const double* __restrict__ Lm, long long sL,
@@ -1162,6 +1306,14 @@ int tri_inv_blocked(hipStream_t s, int batch, int n, const double* L, int ldl, l
                     double* X, int ldx, long long sX, double* T, const int* skip) {
   const int nblk = (n + BNB - 1) / BNB;
   const long long sD = (long long)nblk * BNB * BNB;
+  const char* tv = std::getenv("EVR_TRIINV");   // "row": the per-block-row launches (A/B)
+  if (!chol_v1() && n <= 1024 && !(tv && !std::strcmp(tv, "row"))) {
+    dim3 g(cdiv(n, 16), batch);
+    if (n <= 512) tri_inv_col_kernel<512><<<g, 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, X, sX, ldx, skip);
+    else tri_inv_col_kernel<1024><<<g, 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, X, sX, ldx, skip);
+    EVR_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 g1(cdiv((long long)n * n, 256), batch);
   place_diag_blocks_kernel<<<g1, 256, 0, s>>>(n, Dinv, sD, X, sX, ldx);
   EVR_LAUNCH_CHECK();

@@ -227,3 +227,25 @@ def test_trsm16_bitwise_equals_tile_kernel(tmp_path):
     subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=120)
     X0 = torch.load(tmp_path / "out.pt")
     assert torch.equal(X.cpu(), X0)
+
+
+@pytest.mark.parametrize("n", [16, 64, 65, 130, 280, 512, 513, 1024])
+def test_tri_inv_col_bitwise_equals_row_kernel(n, monkeypatch):
+    """The one-launch 16-column-panel triangular inverse (n <= 1024, the GP fit's L^-1) runs
+    tri_inv_row_kernel's accumulation sequence per element: bitwise equal to the per-block-row
+    launches (EVR_TRIINV=row), including ragged n and the zero upper triangle."""
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(n + 11)
+    A = torch.randn(5, n, n + 3, generator=g, dtype=torch.float64)
+    A = _t(A @ A.transpose(1, 2) / n + 1e-2 * torch.eye(n, dtype=torch.float64))
+    monkeypatch.delenv("EVR_TRIINV", raising=False)
+    L, Li, _, info = ops.cholesky_inverse(A)
+    monkeypatch.setenv("EVR_TRIINV", "row")
+    L0, Li0, _, info0 = ops.cholesky_inverse(A)
+    assert info.cpu().eq(0).all() and info0.cpu().eq(0).all()
+    assert torch.equal(L, L0)
+    assert torch.equal(Li, Li0)
+    Lc = L.cpu()
+    eye = torch.eye(n, dtype=torch.float64).expand(5, n, n)
+    assert torch.allclose(Li.cpu() @ Lc, eye, atol=1e-8)

@@ -31,10 +31,10 @@ python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.
 python tools/pmc_traffic.py "$OUT/pmc_fetch20" "$OUT/pmc_write20" "$OUT/hbm_traffic.json" "@b20" &&
 step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
      SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES -d "$OUT/pmc_sq" -o run --output-format csv \
-     --kernel-include-regex "hvi_kd2|qs_fwd|qs_bwd|chol_step" -- python tools/loop_step.py 10 &&
+     --kernel-include-regex "hvi_kd|qs_fwd|qs_bwd|chol_step" -- python tools/loop_step.py 10 &&
 step pmc_sq20 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
      SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES -d "$OUT/pmc_sq20" -o run --output-format csv \
-     --kernel-include-regex "hvi_kd2|qs_fwd|qs_bwd" -- python tools/loop_step.py 10 20 &&
+     --kernel-include-regex "hvi_kd|qs_fwd|qs_bwd" -- python tools/loop_step.py 10 20 &&
 python tools/pmc_sq.py "$OUT/pmc_sq" "$OUT/sq_counters.json" b512 &&
 python tools/pmc_sq.py "$OUT/pmc_sq20" "$OUT/sq_counters.json" b20
 echo "done rc=$?"
