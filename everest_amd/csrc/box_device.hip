@@ -23,6 +23,7 @@
 // the HVI scan decodes them against the sample's point table (hvi.hip).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "../../include/everest_amd.h"
@@ -32,6 +33,7 @@ namespace evr {
 constexpr int BD_THREADS = 1024;
 constexpr unsigned long long BD_DEAD = ~0ull;
 constexpr int BD_LDS_BYTES = 160 * 1024 - 2048;  // dynamic LDS budget (static counters aside)
+constexpr int BD_STG = 256;                       // LDS staging of A's indices and the new keys
 
 struct BdLayout {
   // per-sample slabs (elements): lub, buf: cap u64; aidx: cap int; pts: (n+m)*m double; inv0: n+m int
@@ -87,7 +89,11 @@ __device__ void bd_bitonic(Ptr a, int P2) {
   }
 }
 
-template <int M>
+// LS: the whole LUB slab (cap keys) lives in LDS, in the final sort buffer, and the first
+// BD_STG entries of A's index list and of the new keys of a step in an LDS staging area, so a
+// Pareto point's update makes no global round trip until BD_STG is exceeded (the slab in HBM
+// cost three dependent L2 round trips per point: ~1.15 ms for 256 samples at the bench shape).
+template <int M, bool LS>
 __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, const double* __restrict__ obj,
                                                               const double* __restrict__ ref, int cap, int sortcap,
                                                               unsigned char* __restrict__ ws, BdLayout Lo,
@@ -102,9 +108,11 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
   int* inv0 = pos + n;                          // n + M: point index of rank r
   int* rank = inv0 + n + M;                     // n + M: rank of point index i
   unsigned long long* sbuf = (unsigned long long*)(((uintptr_t)(rank + n + M) + 15) & ~(uintptr_t)15);
+  unsigned long long* stg = sbuf + sortcap;     // LS: BD_STG new keys
+  int* astg = (int*)(stg + BD_STG);             // LS: BD_STG indices of A
   __shared__ int sh_nf, sh_nA, sh_nNew, sh_cnt, sh_err;
 
-  unsigned long long* lub = (unsigned long long*)(ws + Lo.off_lub) + (size_t)s * cap;
+  unsigned long long* lub = LS ? sbuf : (unsigned long long*)(ws + Lo.off_lub) + (size_t)s * cap;
   unsigned long long* buf = (unsigned long long*)(ws + Lo.off_buf) + (size_t)s * cap;
   int* aidx = (int*)(ws + Lo.off_aidx) + (size_t)s * cap;
   double* gpts = (double*)(ws + Lo.off_pts) + (size_t)s * (n + M) * M;
@@ -194,14 +202,18 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
       bool dom = pt[inv0[K::field(key, 0)] * M] > z[0];
 #pragma unroll
       for (int j = 1; j < M; ++j) dom &= pt[K::field(key, j) * M + j] > z[j];
-      if (dom) aidx[atomicAdd(&sh_nA, 1)] = u;
+      if (dom) {
+        const int k = atomicAdd(&sh_nA, 1);
+        if (LS && k < BD_STG) astg[k] = u;
+        else aidx[k] = u;
+      }
     }
     __syncthreads();
     const int nA = sh_nA;
     // (b) admissible projections u^j
     for (int t = tid; t < nA * M; t += BD_THREADS) {
       const int a = t / M, j = t - a * M;
-      const unsigned long long key = lub[aidx[a]];
+      const unsigned long long key = lub[(LS && a < BD_STG) ? astg[a] : aidx[a]];
       double zmax = -INFINITY;
 #pragma unroll
       for (int k = 0; k < M; ++k) {
@@ -211,7 +223,11 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
       }
       if (z[j] >= zmax) {
         const int slot = atomicAdd(&sh_nNew, 1);
-        if (slot < cap) buf[slot] = K::set(key, j, j == 0 ? rank[p] : p);
+        if (slot < cap) {
+          const unsigned long long nk = K::set(key, j, j == 0 ? rank[p] : p);
+          if (LS && slot < BD_STG) stg[slot] = nk;
+          else buf[slot] = nk;
+        }
       }
     }
     __syncthreads();
@@ -223,11 +239,12 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
     // (c) overwrite A's slots, append the rest, tombstone the leftovers
     const int top = nNew > nA ? nNew : nA;
     for (int i = tid; i < top; i += BD_THREADS) {
+      const bool st = LS && i < BD_STG;
       if (i < nNew) {
-        const int dst = (i < nA) ? aidx[i] : Kend + (i - nA);
-        lub[dst] = buf[i];
+        const int dst = (i < nA) ? (st ? astg[i] : aidx[i]) : Kend + (i - nA);
+        lub[dst] = st ? stg[i] : buf[i];
       } else {
-        lub[aidx[i]] = BD_DEAD;
+        lub[st ? astg[i] : aidx[i]] = BD_DEAD;
       }
     }
     if (nNew > nA) Kend += nNew - nA;
@@ -387,19 +404,31 @@ int evr_box_decompose_device(void* stream, int S, int n, int m, const double* ob
             "evr_box_decompose_device: n=%d points x m=%d exceed the device limits", n, m);
   const BdLayout Lo = bd_layout(S, n, m, cap);
   const size_t fixed = bd_lds_fixed(n, m) + 16;
-  int sortcap = 1;
-  while ((size_t)(sortcap * 2) * 8 + fixed <= (size_t)BD_LDS_BYTES && sortcap * 2 <= cap) sortcap *= 2;
-  const size_t lds = fixed + (size_t)sortcap * 8;
+  auto sort_cap = [&](size_t fx) {
+    int c = 1;
+    while ((size_t)(c * 2) * 8 + fx <= (size_t)BD_LDS_BYTES && c * 2 <= cap) c *= 2;
+    return c;
+  };
+  // the LDS slab variant when the whole capacity fits beside the staging area (EVR_BD_LDS=0: HBM slab)
+  const size_t fixed_ls = fixed + (size_t)BD_STG * (8 + 4);
+  const char* ev = std::getenv("EVR_BD_LDS");
+  const bool ls = sort_cap(fixed_ls) >= cap && !(ev && ev[0] == '0');
+  const int sortcap = ls ? cap : sort_cap(fixed);
+  const size_t lds = (ls ? fixed_ls : fixed) + (size_t)sortcap * 8;
   hipStream_t s = (hipStream_t)stream;
-#define L(MM)                                                                                           \
-  do {                                                                                                  \
-    EVR_HIP(hipFuncSetAttribute((const void*)bd_build_kernel<MM>,                                      \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                 \
-    bd_build_kernel<MM><<<S, BD_THREADS, lds, s>>>(S, n, obj, ref, cap, sortcap, (unsigned char*)work, \
-                                                   Lo, counts, status);                                 \
+#define L2(MM, LS_)                                                                                          \
+  do {                                                                                                       \
+    EVR_HIP(hipFuncSetAttribute((const void*)bd_build_kernel<MM, LS_>,                                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                      \
+    bd_build_kernel<MM, LS_><<<S, BD_THREADS, lds, s>>>(S, n, obj, ref, cap, sortcap, (unsigned char*)work, \
+                                                        Lo, counts, status);                                 \
   } while (0)
+#define L(MM)            \
+  if (ls) L2(MM, true);  \
+  else L2(MM, false)
   EVR_BD_SWITCH(m, L);
 #undef L
+#undef L2
   EVR_LAUNCH_CHECK();
   return 0;
 }

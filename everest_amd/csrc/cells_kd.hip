@@ -35,9 +35,20 @@ constexpr int KD_MAX_CELLS = 8192;          // LDS sort buffer (64 KB)
 constexpr int KD_MAX_GROUPS = KD_MAX_CELLS / 16;
 constexpr unsigned short KD_PAD = 0x7FFF;   // > every threshold (ranks < 2^15: packed signed compares)
 
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(unsigned)v, m, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), m, 64);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// Bitonic sort of P2 (a power of two) unique keys in LDS.  Stages whose partner distance j is
+// at least 64 exchange through LDS (one barrier each); the stages with j < 64 pair lanes of one
+// wave (index i = tid + 1024 t, so a wave holds 64 consecutive keys) and run in registers by
+// xor-shuffles, min / max per pair, with one barrier per merge size: 41 instead of 91 barriers
+// per sort at P2 = 8192.  Same result as the compare-and-swap network (keys are unique).
 __device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
   for (int k = 2; k <= P2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
+    int j = k >> 1;
+    for (; j >= 64; j >>= 1) {
       for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
         const int l = i ^ j;
         if (l > i) {
@@ -51,6 +62,17 @@ __device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
       }
       __syncthreads();
     }
+    for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
+      unsigned long long x = a[i];
+      const bool up = (i & k) == 0;
+      for (int jj = j; jj > 0; jj >>= 1) {
+        const unsigned long long y = shfl_xor_u64(x, jj);
+        // the lower index of a pair keeps the minimum in an ascending run, the maximum otherwise
+        x = (((i & jj) == 0) == up) ? (x < y ? x : y) : (x < y ? y : x);
+      }
+      a[i] = x;
+    }
+    __syncthreads();
   }
 }
 
@@ -117,17 +139,28 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
       }
     }
     __syncthreads();
-    for (int i = tid; i < C; i += KD_THREADS) {
+    // segment rank spans: a segment is a run of whole groups of 16 cells, so the 16 lanes of
+    // one group (uniform control flow) reduce by xor-shuffles first and one lane per group
+    // updates the segment's LDS minimum / maximum (16x fewer same-address atomics)
+    for (int i = tid; i < G * 16; i += KD_THREADS) {
       const int g = i >> 4, a = segS[g], e = segE[g];
       const int ncell = min(16 * e, C) - 16 * a;
       if (ncell <= 16) continue;
       sh_any = 1;
-      const int cell = (int)(sb[i] & 0xFFFFu);
+      const bool in = i < C;
+      const int cell = in ? (int)(sb[i] & 0xFFFFu) : 0;
 #pragma unroll
       for (int j = 0; j < M; ++j) {
-        const unsigned int r = rank_of(cell, j);
-        atomicMin(&mn[a][j], r);
-        atomicMax(&mx[a][j], r);
+        unsigned int lo = in ? rank_of(cell, j) : 0xFFFFFFFFu, hi = in ? lo : 0u;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+          lo = min(lo, (unsigned int)__shfl_xor((int)lo, o, 16));
+          hi = max(hi, (unsigned int)__shfl_xor((int)hi, o, 16));
+        }
+        if ((i & 15) == 0) {
+          atomicMin(&mn[a][j], lo);
+          atomicMax(&mx[a][j], hi);
+        }
       }
     }
     __syncthreads();

@@ -392,8 +392,10 @@ __device__ __forceinline__ double quad_bcast_f64(double v, int s) {
 // one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
 // Lane (row r, quad q) holds A[r][q + 4k].  Per pivot step the pivot comes by readlane (a
 // uniform scalar: its reciprocal starts at once and the failure test is a scalar branch),
-// the lane's own row entry A[r][j] by a DPP quad broadcast, and only the column entries of
-// the other rows (A[c][j]) and the finished inverse row go through LDS.
+// the lane's own row entry A[r][j] by a DPP quad broadcast, and the column entries of the
+// other rows (A[c][j]) and the finished inverse row by ds_bpermute (EVR_LEAF_LDS builds the
+// LDS store / fence / load exchange instead: 636 vs 532 cycles per pivot, tools/chol_prof.hip;
+// the exchanged values, hence the results, are the same).
 // Returns the first failing local pivot index or -1 (uniform over the wave).
 __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
                                               double* erow, double* piv) {
@@ -406,7 +408,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
-#ifdef EVR_LEAF_BPERM
+#ifndef EVR_LEAF_LDS
   // pivot column and inverse row by ds_bpermute (one LDS-crossbar round trip, no store /
   // fence / load): lane (r, q) takes A[q + 4k][j] from lane 4(q + 4k) + (j & 3) and the
   // inverse row entry E[j][q + 4k] from lane 4j + q — the values the LDS exchange carries

@@ -489,7 +489,10 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         if shard.k > 1:
             drv += f"-sharded{shard.k}"
         Xc = np.clip(res.x.reshape((nb,) + shp), bounds[0], bounds[1])
-        vals, _ = shard.evaluate(acqf, Xc, False)
+        # re-scored through the evaluation path the iterations used (the restart batch's fused
+        # scan forms acq in its own summation order; evr_qnehvi_plan_minimize re-scores the
+        # same way), so both drivers return bitwise the same values
+        vals, _ = shard.evaluate(acqf, Xc, True)
         return vals, Xc, {"restarts": nb, "evals": counter["n"], "nit": int(getattr(res, "nit", 0)),
                           "status": int(res.status), "driver": drv, "local_batch": shard.local_size(nb)}
 

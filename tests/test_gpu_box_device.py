@@ -75,3 +75,18 @@ def test_device_box_volume_equals_exact_hypervolume():
     P = omo.pareto_above_ref(torch.tensor(O), torch.tensor(ref)).numpy()
     hv = omo.hv_slicing(P, ref)
     assert abs((np.prod(cap - ref) - vol_nd) - hv) < 1e-10
+
+
+@pytest.mark.parametrize("m,n,S", [(5, 280, 16), (3, 60, 8), (2, 300, 4)])
+def test_device_box_lds_slab_equals_hbm_slab(m, n, S, monkeypatch):
+    """The LDS-resident LUB slab (whole capacity beside an LDS staging area of A's indices and
+    the step's new keys) gives bitwise the HBM slab's cells (EVR_BD_LDS=0)."""
+    O = _front(S, n, m, seed=7 * m + n)
+    Od = torch.tensor(np.ascontiguousarray(O.transpose(2, 1, 0)), device="cuda")
+    ref = torch.full((m,), -1.1, dtype=torch.float64, device="cuda")
+    monkeypatch.delenv("EVR_BD_LDS", raising=False)
+    c1 = ops.box_decompose_device(Od, ref)
+    monkeypatch.setenv("EVR_BD_LDS", "0")
+    c2 = ops.box_decompose_device(Od, ref)
+    assert torch.equal(c1.off, c2.off) and torch.equal(c1.keys, c2.keys)
+    assert torch.equal(c1.pts, c2.pts) and torch.equal(c1.rank0, c2.rank0)

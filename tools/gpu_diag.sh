@@ -19,9 +19,8 @@ step() {  # step <name> <timeout_s> cmd...
 if [ $# -gt 0 ]; then
   step pytest 400 python -u -m pytest "$@" -x -q --timeout 120 --timeout-method thread || exit 1
 fi
-step ask_phases 200 python tools/ask_phases.py &&
+step ask_phases 200 env EVR_MIN_STATS=1 python tools/ask_phases.py &&
 step probes 200 python tools/construction_probes.py &&
 step fit 200 python tools/bench_fit.py &&
-step chol_prof 60 ./tools/_chol_prof &&
-step chol_prof_bp 60 ./tools/_chol_prof_bp
+step chol_prof 60 ./tools/_chol_prof
 echo "done rc=$?"

@@ -37,4 +37,6 @@ step pmc_sq20 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
      --kernel-include-regex "hvi_kd|qs_fwd|qs_bwd" -- python tools/loop_step.py 10 20 &&
 python tools/pmc_sq.py "$OUT/pmc_sq" "$OUT/sq_counters.json" b512 &&
 python tools/pmc_sq.py "$OUT/pmc_sq20" "$OUT/sq_counters.json" b20
-echo "done rc=$?"
+rc=$?
+echo "done rc=$rc"
+exit $rc
