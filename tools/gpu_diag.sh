@@ -22,5 +22,7 @@ fi
 step ask_phases 200 env EVR_MIN_STATS=1 python tools/ask_phases.py &&
 step probes 200 python tools/construction_probes.py &&
 step fit 200 python tools/bench_fit.py &&
-step chol_prof 60 ./tools/_chol_prof
+step chol_prof 60 ./tools/_chol_prof &&
+step timeline 200 rocprofv3 --kernel-trace --output-format csv -d "$O/tl" -o run -- python tools/ask_timeline.py &&
+step timeline_report 60 python tools/ask_timeline.py --analyse "$O/tl"
 echo "done rc=$?"
