@@ -51,11 +51,32 @@ def _prefetch_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = Non
     nd = dim - d0 if nd is None else nd
     if nd <= 0:
         return None
+    key = (int(dim), int(seed), int(d0), int(nd))
+    fut = _PREFETCHED.pop(key, None)   # started earlier by prefetch_scramble
+    if fut is not None:
+        return fut
     if _SCRAMBLE_POOL is None:
         from concurrent.futures import ThreadPoolExecutor
 
         _SCRAMBLE_POOL = ThreadPoolExecutor(max_workers=3, thread_name_prefix="evr-sobol")
     return _SCRAMBLE_POOL.submit(ops.sobol_scramble, dim, seed, d0, nd)
+
+
+_PREFETCHED = {}
+
+
+def prefetch_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = None) -> None:
+    """Start the host scrambling of a Sobol draw as soon as its seed and dimension are known
+    (a strategy draws its seeds before building the acquisition); the acquisition's own
+    request for the same (dim, seed, range) takes the running future instead of starting
+    another.  At most 8 are kept."""
+    nd = dim - d0 if nd is None else nd
+    key = (int(dim), int(seed), int(d0), int(nd))
+    if nd <= 0 or key in _PREFETCHED:
+        return
+    while len(_PREFETCHED) >= 8:
+        _PREFETCHED.pop(next(iter(_PREFETCHED)))
+    _PREFETCHED[key] = _prefetch_scramble(dim, seed, d0, nd)
 
 
 def _submit(fn, *args):
@@ -516,13 +537,24 @@ class QNEHVI(_BoxHviAcqf):
         # baseline rows -> training rows (exact match of the transformed inputs)
         X_train_raw = np.asarray(X_train_raw, dtype=np.float64)
         X_baseline_raw = np.asarray(X_baseline_raw, dtype=np.float64)
-        first = {}
-        for i, row in enumerate(map(tuple, X_train_raw)):
-            first.setdefault(row, i)
-        try:
-            base_rows = np.array([first[tuple(r)] for r in X_baseline_raw], dtype=np.int64)
-        except KeyError as e:
-            raise ValueError("qNEHVI: every baseline point must be a training point of the models") from e
+        nbl = X_baseline_raw.shape[0]
+        def _distinct_rows(a):
+            a = np.ascontiguousarray(a)
+            if not np.isfinite(a).all() or np.any((a == 0) & np.signbit(a)):   # byte != value equality
+                return False
+            return len(np.unique(a.view(np.dtype((np.void, a.dtype.itemsize * a.shape[1]))))) == a.shape[0]
+
+        if (nbl <= X_train_raw.shape[0] and X_baseline_raw.ndim == 2 and X_baseline_raw.shape[1] > 0
+                and np.array_equal(X_baseline_raw, X_train_raw[:nbl]) and _distinct_rows(X_baseline_raw)):
+            base_rows = np.arange(nbl, dtype=np.int64)   # the usual case: the deduplicated training rows
+        else:
+            first = {}
+            for i, row in enumerate(map(tuple, X_train_raw)):
+                first.setdefault(row, i)
+            try:
+                base_rows = np.array([first[tuple(r)] for r in X_baseline_raw], dtype=np.int64)
+            except KeyError as e:
+                raise ValueError("qNEHVI: every baseline point must be a training point of the models") from e
 
         # pending points ([upstream] set_X_pending with cache_pending=True, max_iep=0) join
         # the baseline after pruning: the kernel-vector row set grows to X_k = [X_train;

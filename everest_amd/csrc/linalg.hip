@@ -408,7 +408,82 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
-#ifndef EVR_LEAF_LDS
+#if !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
+  // two pivots per exchange round: columns j, j1 = j + 1 and inverse rows j, j1 as they are
+  // before step j arrive in one round of ds_bpermute; what step j1 reads after step j (its
+  // pivot, its column entries A'[c][j1], the lane's own A'[r][j1], the inverse row E'[j1]) is
+  // formed locally with step j's own operations — m = a * ip, fma(-m, x, y) on the same
+  // operands — so every value is bitwise the one-pivot loop's, with half the exchange rounds
+#pragma unroll
+  for (int j = 0; j < CP; j += 2) {
+    const int j1 = j + 1;
+    const double p0 = readlane_f64(a[j >> 2], 4 * j + (j & 3));      // A[j][j]
+    const double a10 = readlane_f64(a[j >> 2], 4 * j1 + (j & 3));    // A[j1][j]
+    const double a11 = readlane_f64(a[j1 >> 2], 4 * j1 + (j1 & 3));  // A[j1][j1]
+    const double arj = quad_bcast_f64(a[j >> 2], j & 3);             // A[r][j]
+    double arj1 = quad_bcast_f64(a[j1 >> 2], j1 & 3);                // A[r][j1]
+    double c0[4], c1[4], e0[4], e1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c0[k] = bperm_f64(a[j >> 2], 4 * q + 16 * k + (j & 3));
+      c1[k] = bperm_f64(a[j1 >> 2], 4 * q + 16 * k + (j1 & 3));
+      e0[k] = bperm_f64(e[k], 4 * j + q);
+      e1[k] = bperm_f64(e[k], 4 * j1 + q);
+    }
+    if (!(p0 > 0.0)) {
+      bad = j;
+      break;
+    }
+    if (lane == 0) piv[j] = p0;
+    double ip = __builtin_amdgcn_rcp(p0);
+    ip = fma(ip, fma(-p0, ip, 1.0), ip);
+    ip = fma(ip, fma(-p0, ip, 1.0), ip);
+    {  // step j
+      const double m = arj * ip;
+      const bool below = r > j;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = q + 4 * k;
+        const double dn = fma(-m, c0[k], a[k]);
+        const double en = fma(-m, e0[k], e[k]);
+        a[k] = (below && c > j && c <= r) ? dn : a[k];
+        e[k] = (below && c <= j) ? en : e[k];
+      }
+    }
+    // step j's updates of the values step j1 exchanges
+    const double m10 = a10 * ip;                                      // row j1's multiplier
+    const double p1 = fma(-m10, a10, a11);                            // A'[j1][j1]
+    if (r >= j1) arj1 = fma(-(arj * ip), a10, arj1);                  // A'[r][j1]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = q + 4 * k;
+      if (c >= j1) c1[k] = fma(-(c0[k] * ip), a10, c1[k]);            // A'[c][j1]
+      if (c <= j) e1[k] = fma(-m10, e0[k], e1[k]);                    // E'[j1][c]
+    }
+    if (!(p1 > 0.0)) {
+      bad = j1;
+      break;
+    }
+    if (lane == 0) piv[j1] = p1;
+    double ip1 = __builtin_amdgcn_rcp(p1);
+    ip1 = fma(ip1, fma(-p1, ip1, 1.0), ip1);
+    ip1 = fma(ip1, fma(-p1, ip1, 1.0), ip1);
+    {  // step j1
+      const double m = arj1 * ip1;
+      const bool below = r > j1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = q + 4 * k;
+        const double dn = fma(-m, c1[k], a[k]);
+        const double en = fma(-m, e1[k], e[k]);
+        a[k] = (below && c > j1 && c <= r) ? dn : a[k];
+        e[k] = (below && c <= j1) ? en : e[k];
+      }
+    }
+  }
+  (void)colj;
+  (void)erow;
+#elif !defined(EVR_LEAF_LDS)
   // pivot column and inverse row by ds_bpermute (one LDS-crossbar round trip, no store /
   // fence / load): lane (r, q) takes A[q + 4k][j] from lane 4(q + 4k) + (j & 3) and the
   // inverse row entry E[j][q + 4k] from lane 4j + q — the values the LDS exchange carries

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -126,12 +127,31 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
-  unsigned int* counter;         // blocks-done counter of the fused copy-out (device)
+  unsigned int* counter;         // blocks-done counter of the fused copy-out, then (u64 at byte
+                                 // 8) the last sequence number the host graph served (device)
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
+  int armed;                     // a host-graph launch is queued, waiting for the next x
 };
 
 namespace evr {
 
+// Head of the host graph: the chain waits on the device until the host publishes its next
+// evaluation (the sequence number at hx[n] beyond the last one served), so the graph can be
+// launched before the host has x — evr_qnehvi_plan_minimize queues the next evaluation as
+// soon as one completes, and the launch overlaps its L-BFGS-B step.  One lane polls the pinned
+// word with system-scope loads and s_sleep backoff; a wait beyond 1 s (an abandoned plan)
+// ends on its own instead of holding the queue.
+__global__ void plan_wait_kernel(const unsigned long long* seqp, unsigned long long* wseq) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long last = __hip_atomic_load(wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = wall_clock64();
+  unsigned long long v;
+  while ((v = __hip_atomic_load(seqp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) <= last) {
+    if (wall_clock64() - t0 > 100000000ull) break;   // 1 s at the 100 MHz constant clock
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (v > last) __hip_atomic_store(wseq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // acq and dX to the host buffer, then (after every thread's system-scope fence) the
 // evaluation's sequence number into the completion word the host spins on
@@ -206,6 +226,30 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
                             md->lengthscales, nullptr, dKx, p->dX, (double*)(w + p->L.kg));
 }
 
+// Host-evaluation resources of destroyed plans, recycled by the next plan of the same batch
+// shape (every ask builds a new acquisition, hence new restart plans): the pinned buffers and
+// the completion counter are reused, and the new chain's graph updates the old executable
+// (hipGraphExecUpdate: same kernels, new arguments) instead of a fresh instantiation — 0.42 ms
+// of first-evaluation setup plus the frees per plan (tools/plan_setup_probe.py).  A failed
+// update (another kernel sequence) falls back to instantiating.  EVR_GRAPH_REUSE=0 disables.
+struct PlanHostRes {
+  int dev, b, n, backward;
+  double* hx;
+  double* hout;
+  unsigned int* counter;
+  hipGraphExec_t exec;
+  hipGraph_t graph;
+};
+static std::mutex g_hres_mu;
+static std::vector<PlanHostRes> g_hres;
+static bool graph_reuse() {
+  static const bool on = [] {
+    const char* e = std::getenv("EVR_GRAPH_REUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" {
 
 long long evr_qnehvi_plan_workspace_bytes(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
@@ -239,6 +283,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->hexec = nullptr;
   p->seq = 0;
   p->counter = nullptr;
+  p->armed = 0;
   if (int rc = gemm_backend_init()) {
     delete p;
     return rc;
@@ -286,6 +331,20 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
+  int dev = -1;
+  if (graph_reuse() && p->hexec && p->hx && p->hout && p->counter && hipGetDevice(&dev) == hipSuccess) {
+    // the plan's evaluations have completed (plan_eval_raw waits for each), so the buffers and
+    // the executable are idle; the counter is back at 0 (the last workgroup resets it)
+    std::lock_guard<std::mutex> lk(g_hres_mu);
+    if (g_hres.size() < 4) {
+      g_hres.push_back({dev, p->b, p->b * p->md.d, p->backward, p->hx, p->hout, p->counter, p->hexec, p->hgraph});
+      p->hx = nullptr;
+      p->hout = nullptr;
+      p->counter = nullptr;
+      p->hexec = nullptr;
+      p->hgraph = nullptr;
+    }
+  }
   if (p->hexec) (void)hipGraphExecDestroy(p->hexec);
   if (p->hgraph) (void)hipGraphDestroy(p->hgraph);
   if (p->hx) (void)hipHostFree(p->hx);
@@ -300,6 +359,24 @@ void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
 static int plan_host_setup(evr_qnehvi_plan* p) {
   if (p->hexec) return 0;
   const int b = p->b, n = b * p->md.d;
+  hipGraphExec_t old_exec = nullptr;
+  hipGraph_t old_graph = nullptr;
+  int dev = -1;
+  if (graph_reuse() && !p->hx && !p->hout && !p->counter && hipGetDevice(&dev) == hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_hres_mu);
+    for (size_t i = 0; i < g_hres.size(); ++i) {
+      const PlanHostRes& r = g_hres[i];
+      if (r.dev == dev && r.b == b && r.n == n && r.backward == p->backward) {
+        p->hx = r.hx;
+        p->hout = r.hout;
+        p->counter = r.counter;
+        old_exec = r.exec;
+        old_graph = r.graph;
+        g_hres.erase(g_hres.begin() + (long)i);
+        break;
+      }
+    }
+  }
   if (!p->hx)
     EVR_HIP(hipHostMalloc((void**)&p->hx, sizeof(double) * (n + 1), hipHostMallocMapped | hipHostMallocCoherent));
   if (!p->hout)
@@ -310,10 +387,8 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   double *dhx = nullptr, *dhout = nullptr;
   EVR_HIP(hipHostGetDevicePointer((void**)&dhx, p->hx, 0));
   EVR_HIP(hipHostGetDevicePointer((void**)&dhout, p->hout, 0));
-  if (!p->counter) {
-    EVR_HIP(hipMalloc((void**)&p->counter, sizeof(unsigned int)));
-    EVR_HIP(hipMemset(p->counter, 0, sizeof(unsigned int)));
-  }
+  if (!p->counter) EVR_HIP(hipMalloc((void**)&p->counter, 16));
+  EVR_HIP(hipMemset(p->counter, 0, 16));   // completion counter and the served sequence number
   hipStream_t cs = nullptr;
   EVR_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
@@ -321,12 +396,27 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
     // writes the results and the completion word itself, other chains end in plan_copy_out
     int done = 0;
+    plan_wait_kernel<<<1, 64, 0, cs>>>((const unsigned long long*)(dhx + n), (unsigned long long*)(p->counter + 2));
     rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
   }
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);
   (void)hipStreamDestroy(cs);
+  if (old_exec) {
+    hipGraphNode_t err_node = nullptr;
+    hipGraphExecUpdateResult ur = hipGraphExecUpdateError;
+    const bool ok = !rc && e == hipSuccess && g && hipGraphExecUpdate(old_exec, g, &err_node, &ur) == hipSuccess &&
+                    ur == hipGraphExecUpdateSuccess;
+    if (old_graph) (void)hipGraphDestroy(old_graph);
+    if (ok) {
+      p->hexec = old_exec;
+      p->hgraph = g;
+      return 0;
+    }
+    (void)hipGraphExecDestroy(old_exec);
+    (void)hipGetLastError();
+  }
   if (!rc && e == hipSuccess && g && hipGraphInstantiate(&p->hexec, g, nullptr, nullptr, 0) == hipSuccess) {
     p->hgraph = g;
     return 0;
@@ -345,7 +435,8 @@ static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
   const unsigned long long seq = ++p->seq;
   std::memcpy(p->hx + n, &seq, sizeof(seq));
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  EVR_HIP(hipGraphLaunch(p->hexec, s));
+  if (!p->armed) EVR_HIP(hipGraphLaunch(p->hexec, s));   // else queued already, waiting for this seq
+  p->armed = 0;
   // spin on the completion word; every 256 polls ask the stream whether it has drained (a
   // faulted or failed launch ends the wait with its error instead of spinning forever)
   volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
@@ -401,15 +492,39 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   }();
   double t_step = 0.0, t_eval = 0.0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  // EVR_PRELAUNCH=0: launch each evaluation's graph only once its x is published
+  static const bool prelaunch = [] {
+    const char* e = std::getenv("EVR_PRELAUNCH");
+    return !(e && e[0] == '0');
+  }();
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;
   int task = opt.start(x0), nit = 0, nfev = 0, status = 0;
+  // the next evaluation's graph is queued while the host works out its x (every queued launch
+  // is consumed: by the next function evaluation or by the final re-evaluation below)
+  auto arm = [&]() -> int {
+    if (!prelaunch || p->armed) return 0;
+    if (int rc = plan_host_setup(p)) return rc;
+    EVR_HIP(hipGraphLaunch(p->hexec, s));
+    p->armed = 1;
+    return 0;
+  };
+  auto drain = [&](int rc) {   // an error with a queued launch: release it with the current x
+    if (p->armed) {
+      double fd = 0.0;
+      std::vector<double> gd(n);
+      (void)plan_eval_host(s, p, opt.x(), &fd, gd.data());
+    }
+    return rc;
+  };
+  if (int rc = arm()) return rc;
   // scipy's _minimize_lbfgsb driver loop
   for (;;) {
     if (task == LBFGSB_FG) {
       double t0 = stats ? now() : 0.0;
-      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
+      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return drain(rc);
+      if (int rc = arm()) return rc;
       double t1 = stats ? now() : 0.0;
       ++nfev;
       task = opt.step(f, g.data());

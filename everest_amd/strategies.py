@@ -19,7 +19,7 @@ import torch
 
 from . import data_models as dm
 from . import ops
-from .acquisition import QEHVI, QEI, QEIJoint, QLogEHVI, QLogNEHVI, QNEHVI
+from .acquisition import QEHVI, QEI, QEIJoint, QLogEHVI, QLogNEHVI, QNEHVI, prefetch_scramble
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
 from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
 from .surrogates import BotorchSurrogates, device
@@ -607,11 +607,13 @@ class QnehviStrategy(QehviStrategy):
         """bofire/strategies/predictives/qnehvi.py:23-53."""
         assert self.experiments is not None, "No experiments available."
         X_train, X_pending = self.get_acqf_input_tensors()
-        objectives, constraints = self._objective_spec()
-        ref = self.get_adjusted_refpoint()
-        # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed
+        # RNG call order of the reference: prune sampler seed, then the acquisition sampler seed;
+        # the prune draw's host scrambling (n_baseline x m dimensions) starts right away
         prune_seed = self._draw_seed()
         sampler_seed = self._draw_seed()
+        prefetch_scramble(int(X_train.shape[0]) * int(self.model.B), prune_seed)
+        objectives, constraints = self._objective_spec()
+        ref = self.get_adjusted_refpoint()
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, None, None, S=self.num_sobol_samples,
                       sampler_seed=sampler_seed, prune_baseline=True, prune_seed=prune_seed, X_pending_raw=X_pending,
                       objective=objectives, constraints=constraints, alpha=self.alpha)

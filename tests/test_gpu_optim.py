@@ -84,3 +84,29 @@ def test_plan_eval_host_matches_device_evaluation(backward):
         else:
             a = acqf.forward(Xd)
         assert np.array_equal(out[:b], a.cpu().numpy())
+
+
+def test_recycled_host_graph_matches_device_chain():
+    """A restart plan built after another plan of the same shape was destroyed takes over its
+    pinned buffers and graph executable (hipGraphExecUpdate with the new chain's arguments):
+    its host evaluations equal the new acquisition's device-mode chain bitwise."""
+    import gc
+
+    from everest_amd.acquisition import QNEHVI
+
+    X, Y, lo, hi, hyp = make_problem(n=60, d=6, m=3, seed=4)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    x = np.random.default_rng(1).uniform(lo, hi, size=(8, 6))
+    m = 3
+    a1 = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=64, sampler_seed=3, prune_seed=5)
+    a1.plan(8, True).run_host(x)
+    a1._plans.clear()
+    del a1
+    gc.collect()
+    a2 = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=64, sampler_seed=11, prune_seed=7)
+    out = a2.plan(8, True).run_host(x).copy()
+    acq, dX = a2.forward_backward(torch.tensor(x, device="cuda"))
+    assert np.array_equal(out[:8], acq.cpu().numpy())
+    assert np.array_equal(out[8:8 + 48].reshape(8, 6), dX.cpu().numpy())
+    out2 = a2.plan(8, True).run_host(x)
+    assert np.array_equal(out2[:56], out[:56])

@@ -3,6 +3,7 @@
 // core-clock cycles per phase.  Build: hipcc --offload-arch=gfx950 -O3 -DEVR_CHOL_PROF
 //   tools/chol_prof.hip -o tools/_chol_prof
 #include <cstdio>
+#include <cstring>
 #include <vector>
 #include "../everest_amd/csrc/linalg.hip"
 
@@ -35,5 +36,18 @@ int main() {
   int h;
   hipMemcpy(&h, info, sizeof(int), hipMemcpyDeviceToHost);
   printf("{\"info\": %d}\n", h);
+  // bit-pattern digest of the factor and its inverse (compare leaf variants for equality)
+  std::vector<double> L(n * n), D(n * n);
+  hipMemcpy(L.data(), dA, sizeof(double) * n * n, hipMemcpyDeviceToHost);
+  hipMemcpy(D.data(), dD, sizeof(double) * n * n, hipMemcpyDeviceToHost);
+  unsigned long long dg = 1469598103934665603ull;
+  for (int i = 0; i < n * n; ++i) {
+    unsigned long long u, v;
+    memcpy(&u, &L[i], 8);
+    memcpy(&v, &D[i], 8);
+    dg = (dg ^ u) * 1099511628211ull;
+    dg = (dg ^ v) * 1099511628211ull;
+  }
+  printf("{\"digest\": \"%016llx\"}\n", dg);
   return 0;
 }
