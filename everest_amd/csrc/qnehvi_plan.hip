@@ -241,6 +241,15 @@ struct PlanHostRes {
   hipGraph_t graph;
 };
 static std::mutex g_hres_mu;
+// queued evaluations (plan_wait_kernel at the head of the host graph); EVR_PRELAUNCH=0 leaves
+// the wait out and launches each evaluation once its x is published
+static bool prelaunch_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("EVR_PRELAUNCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 static std::vector<PlanHostRes> g_hres;
 static bool graph_reuse() {
   static const bool on = [] {
@@ -396,7 +405,8 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
     // writes the results and the completion word itself, other chains end in plan_copy_out
     int done = 0;
-    plan_wait_kernel<<<1, 64, 0, cs>>>((const unsigned long long*)(dhx + n), (unsigned long long*)(p->counter + 2));
+    if (prelaunch_on())
+      plan_wait_kernel<<<1, 64, 0, cs>>>((const unsigned long long*)(dhx + n), (unsigned long long*)(p->counter + 2));
     rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
   }
@@ -492,11 +502,7 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   }();
   double t_step = 0.0, t_eval = 0.0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  // EVR_PRELAUNCH=0: launch each evaluation's graph only once its x is published
-  static const bool prelaunch = [] {
-    const char* e = std::getenv("EVR_PRELAUNCH");
-    return !(e && e[0] == '0');
-  }();
+  const bool prelaunch = prelaunch_on();
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;

@@ -10,6 +10,7 @@ acquisition evaluations of ``ask()`` (everest_amd/optim.py).
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import List, Optional, Sequence, Tuple
 
@@ -611,7 +612,8 @@ class QnehviStrategy(QehviStrategy):
         # the prune draw's host scrambling (n_baseline x m dimensions) starts right away
         prune_seed = self._draw_seed()
         sampler_seed = self._draw_seed()
-        prefetch_scramble(int(X_train.shape[0]) * int(self.model.B), prune_seed)
+        if os.environ.get("EVR_SCRAMBLE_PREFETCH", "1") != "0":
+            prefetch_scramble(int(X_train.shape[0]) * int(self.model.B), prune_seed)
         objectives, constraints = self._objective_spec()
         ref = self.get_adjusted_refpoint()
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, None, None, S=self.num_sobol_samples,
