@@ -241,12 +241,14 @@ struct PlanHostRes {
   hipGraph_t graph;
 };
 static std::mutex g_hres_mu;
-// queued evaluations (plan_wait_kernel at the head of the host graph); EVR_PRELAUNCH=0 leaves
-// the wait out and launches each evaluation once its x is published
+// queued evaluations (plan_wait_kernel at the head of the host graph), opt-in with
+// EVR_PRELAUNCH=1: measured within noise of launching each evaluation once its x is published
+// (≈ 110 µs per evaluation either way, profiles/r03/v), so the default graph has no waiting
+// kernel
 static bool prelaunch_on() {
   static const bool on = [] {
     const char* e = std::getenv("EVR_PRELAUNCH");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

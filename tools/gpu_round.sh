@@ -16,6 +16,7 @@ step() {  # step <name> <timeout_s> cmd...
   return $rc
 }
 step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread &&
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" &&
 step bench 600 python bench.py &&
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
      python bench.py --no-cpu-baseline --no-eval-pass &&
