@@ -527,8 +527,13 @@ class _MultiobjectiveMixin:
     def get_adjusted_refpoint(self) -> List[float]:
         assert self.experiments is not None, "No experiments available."
         if self.ref_point is None:
-            df = self._valid_experiments()
-            ref_point = infer_ref_point(self.domain, experiments=df, return_masked=False)
+            c = getattr(self, "_ref_cache", None)   # inferred once per experiments frame
+            if c is not None and c[0] is self._experiments:
+                ref_point = c[1]
+            else:
+                df = self._valid_experiments()
+                ref_point = infer_ref_point(self.domain, experiments=df, return_masked=False)
+                self._ref_cache = (self._experiments, ref_point)
         else:
             ref_point = self.ref_point
         keys = self.domain.outputs.get_keys_by_objective([MaximizeObjective, MinimizeObjective,
