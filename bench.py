@@ -36,6 +36,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -410,16 +411,38 @@ def cpu_full_ask(s, restarts, raw, S, seed=0):
     return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in out.items()}
 
 
-def _traffic(path, kernel):
-    """Per-launch HBM bytes of ``kernel`` from the committed PMC summary (FETCH_SIZE doubled
-    per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE), or None."""
+def _traffic(path, key, launched):
+    """Per-launch HBM bytes of op ``key`` from the committed PMC summary (FETCH_SIZE doubled
+    per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE), or None.  The entry counts
+    only if its PMC pass saw the kernel this run launches for the op (regex ``launched``
+    against the entry's kernel names): a figure captured on an earlier kernel is dropped."""
+    import re
+
     try:
         with open(path) as f:
             tab = json.load(f)
     except (OSError, ValueError):
         return None
-    ent = tab.get(kernel)
-    return ent if ent and "bytes_per_launch" in ent else None
+    ent = tab.get(key)
+    if not ent or "bytes_per_launch" not in ent or ent["bytes_per_launch"] <= 0:
+        return None
+    if not any(re.search(launched, k) for k in ent.get("kernels", [])):
+        return None
+    return ent
+
+
+def _launched_kernel(acqf, op, b, d):
+    """Regex of the kernel name(s) the evaluation chain launches for ``op`` at batch b."""
+    from everest_amd import ops
+
+    if op != "hvi_fwd_bwd":
+        return {"kernel_matrix": r"kmat_kernel", "samples": r"qn_samples_norms",
+                "proj_fwd": r"qs_fwd" if ops.qnehvi_small_applies(acqf.state, b, d) else r"Cijk_|qn_proj_fwd",
+                "proj_bwd": r"qs_bwd" if ops.qnehvi_small_applies(acqf.state, b, d) else r"Cijk_|qn_proj_bwd",
+                "kernel_grad": r"kcross_grad"}.get(op, re.escape(op))
+    if ops.qnehvi_small_applies(acqf.state, b, d) and ops.hvi_restart_fb_applies(acqf.state, b):
+        return r"hvi_kd3<" if os.environ.get("EVR_KDB", "1") == "0" else r"hvi_kdb<"
+    return r"hvi_kd2?<|hvi_tiled<"
 
 
 def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=None, seed: int = 1):
@@ -701,7 +724,7 @@ def main():
                 kernels_b["hvi_fwd_bwd"]["scan"] = {
                     "dense_pairs": args.b * sum_cells, "group_tests": counts["group_tests"],
                     "group_pairs": counts["group_pairs"], "terms": counts["terms"]}
-                tr = _traffic(args.traffic_json, "hvi_fwd_bwd")
+                tr = _traffic(args.traffic_json, "hvi_fwd_bwd", _launched_kernel(acqf, "hvi_fwd_bwd", args.b, args.d))
                 if tr is not None:
                     kernels_b["hvi_fwd_bwd"]["traffic"] = tr["bytes_per_launch"]
                     kernels_b["hvi_fwd_bwd"]["traffic_source"] = tr["source"]
@@ -740,7 +763,7 @@ def main():
                     "unit": r["unit"], "frac": r["frac"], "traffic": None,
                     "algorithmic_work_per_launch": r["work_per_launch"], "launch_ms": r["launch_ms"],
                     "batch": f"{b_r} restart candidates (one L-BFGS-B evaluation of this rank's chunk)"}
-            tr = _traffic(args.traffic_json, f"{dom}@b{b_r}")
+            tr = _traffic(args.traffic_json, f"{dom}@b{b_r}", _launched_kernel(acqf_ask, dom, b_r, args.d))
             if tr is not None:
                 roof["traffic"] = tr["bytes_per_launch"]
                 roof["traffic_source"] = tr["source"]

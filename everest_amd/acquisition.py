@@ -544,13 +544,18 @@ class QNEHVI(_BoxHviAcqf):
                 return False
             return len(np.unique(a.view(np.dtype((np.void, a.dtype.itemsize * a.shape[1]))))) == a.shape[0]
 
+        # a baseline point's row must be a training row of EVERY output (heterogeneous models:
+        # the rows all outputs are trained on)
+        all_rows = gp.valid_all_rows() if hasattr(gp, "valid_all_rows") else np.ones(X_train_raw.shape[0], bool)
         if (nbl <= X_train_raw.shape[0] and X_baseline_raw.ndim == 2 and X_baseline_raw.shape[1] > 0
-                and np.array_equal(X_baseline_raw, X_train_raw[:nbl]) and _distinct_rows(X_baseline_raw)):
+                and np.array_equal(X_baseline_raw, X_train_raw[:nbl]) and _distinct_rows(X_baseline_raw)
+                and all_rows[:nbl].all()):
             base_rows = np.arange(nbl, dtype=np.int64)   # the usual case: the deduplicated training rows
         else:
             first = {}
             for i, row in enumerate(map(tuple, X_train_raw)):
-                first.setdefault(row, i)
+                if all_rows[i]:
+                    first.setdefault(row, i)
             try:
                 base_rows = np.array([first[tuple(r)] for r in X_baseline_raw], dtype=np.int64)
             except KeyError as e:
@@ -669,6 +674,7 @@ class QNEHVI(_BoxHviAcqf):
                     Zb = torch.cat([Zb, Zp_], 1).contiguous()
             else:
                 Zb = z_base_full.to(dev).permute(2, 1, 0).contiguous()
+            self._Zb = Zb
             probe("baseline_sobol")
             Yb = ops.gemm(self.L_base, Zb)
             Ob = self._objective(Yb, mu_b)
@@ -761,6 +767,12 @@ class QNEHVI(_BoxHviAcqf):
         tm["total"] = _time.perf_counter() - t0
         self.timings = tm
 
+
+    def z_base_host(self) -> Optional[torch.Tensor]:
+        """The baseline base samples (S x nb x m, host), the oracle's layout; None without a
+        baseline."""
+        zb = getattr(self, "_Zb", None)
+        return None if zb is None else zb.permute(2, 1, 0).cpu().contiguous()
 
     def _objective(self, Y: torch.Tensor, mu: torch.Tensor) -> torch.Tensor:
         """m x P x S model samples (+ mean) -> m_obj x P x S objectives; infeasible samples

@@ -124,6 +124,17 @@ inline int qn_rows(const State* st) { return st->n + st->nb + qn_nh(st) + 1; }
 
 // Kernel families (same numbering as include/everest_amd.h EVR_KERNEL_*).
 enum KernelKind { RBF = 0, MATERN05 = 1, MATERN15 = 2, MATERN25 = 3 };
+// A kind code is one family for every output (0..3) or KIND_MIXED with a 2-bit family per
+// output j at bits 5 + 2 j (EVR_KERNEL_MIXED; at most KIND_MAX_MIXED outputs).
+constexpr int KIND_MIXED = 16, KIND_MAX_MIXED = 13;
+__host__ __device__ __forceinline__ int kind_of(int code, int j) {
+  return code < KIND_MIXED ? code : (code >> (5 + 2 * j)) & 3;
+}
+inline bool kind_code_ok(int code, int B) {
+  if (code >= 0 && code <= 3) return true;
+  if (!(code & KIND_MIXED) || (code & 15) || B < 1 || B > KIND_MAX_MIXED) return false;
+  return (code >> (5 + 2 * B)) == 0;
+}
 
 // k(r^2) for the stationary kernels GPyTorch exposes through BoFire
 // (bofire/kernels/mapper.py:31-69).  Matérn uses dist = sqrt(max(d2, 1e-30)).

@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
               d2 = fma(df, df, d2);
             }
           }
-          const double sgl = g[bb] * os_s[bb] * kernel_dscale(kind, d2);
+          const double sgl = g[bb] * os_s[bb] * kernel_dscale(kind_of(kind, b0 + bb), d2);
 #pragma unroll
           for (int k = 0; k < MAXD; ++k)
             if (k < d) acc[k] = fma(sgl, diff[k], acc[k]);
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void kls_grad_kernel(int kind, int n, int d, c
         sq[k] = df * df;
         d2 += sq[k];
       }
-    const double s = -w * kernel_dscale(kind, d2);
+    const double s = -w * kernel_dscale(kind_of(kind, b), d2);
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
       if (k < d) acc[k] = fma(s, sq[k] * il[k], acc[k]);
@@ -741,10 +741,24 @@ extern "C" {
 int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                       const double* scale1, const double* X2, const double* shift2, const double* scale2,
                       const double* lengthscales, const double* outputscale, const double* diag_add, double* K) {
-  EVR_CHECK(kind >= 0 && kind <= 3, "evr_kernel_matrix: bad kernel kind %d", kind);
+  EVR_CHECK(kind_code_ok(kind, B), "evr_kernel_matrix: bad kernel kind %d for %d outputs", kind, B);
   EVR_CHECK(B >= 1 && n1 >= 0 && n2 >= 0 && d >= 1 && d <= KMAXD, "evr_kernel_matrix: bad sizes B=%d n1=%d n2=%d d=%d",
             B, n1, n2, d);
   if (n1 == 0 || n2 == 0) return 0;
+  if (kind >= KIND_MIXED) {
+    // one family per output: one launch per run of consecutive outputs of the same family
+    for (int b0 = 0; b0 < B;) {
+      const int k = kind_of(kind, b0);
+      int b1 = b0 + 1;
+      while (b1 < B && kind_of(kind, b1) == k) ++b1;
+      if (int rc = evr_kernel_matrix(stream, k, b1 - b0, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2,
+                                     lengthscales + (size_t)b0 * d, outputscale ? outputscale + b0 : nullptr,
+                                     diag_add ? diag_add + b0 : nullptr, K + (size_t)b0 * n1 * n2))
+        return rc;
+      b0 = b1;
+    }
+    return 0;
+  }
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
@@ -830,7 +844,7 @@ int evr_kernel_cross_grad(void* stream, int kind, int B, int n1, int n2, int d, 
                           const double* shift1, const double* scale1, const double* X2, const double* shift2,
                           const double* scale2, const double* lengthscales, const double* outputscale,
                           const double* G, double* dX2, double* work) {
-  EVR_CHECK(kind >= 0 && kind <= 3 && B >= 1 && d >= 1 && d <= KMAXD, "evr_kernel_cross_grad: bad args");
+  EVR_CHECK(kind_code_ok(kind, B) && B >= 1 && d >= 1 && d <= KMAXD, "evr_kernel_cross_grad: bad args");
   if (n2 == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const bool own = work == nullptr;
@@ -847,7 +861,8 @@ long long evr_kernel_cross_grad_workspace_doubles(int n1, int n2, int d) {
 
 int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, const double* X,
                                 const double* lengthscales, const double* W, double* gls, double* work) {
-  EVR_CHECK(kind >= 0 && kind <= 3 && B >= 1 && n >= 1 && d >= 1 && d <= KMAXD, "evr_kernel_lengthscale_grad: bad args");
+  EVR_CHECK(kind_code_ok(kind, B) && B >= 1 && n >= 1 && d >= 1 && d <= KMAXD,
+            "evr_kernel_lengthscale_grad: bad args");
   EVR_CHECK(work != nullptr, "evr_kernel_lengthscale_grad: work (B*n*d doubles) required");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(n, B);

@@ -79,6 +79,29 @@ __device__ __forceinline__ double qg_sig(double x) {
   return x >= 0.0 ? 1.0 / (1.0 + exp(-x)) : exp(x) / (1.0 + exp(x));
 }
 
+// [upstream] botorch.utils.safe_math.log_fatmoid — the fat-tailed (Cauchy, O(1/x^2) for
+// x -> -inf) smooth Heaviside that compute_smoothed_feasibility_indicator(log=True, fat=True)
+// uses in qLogNEHVI / qLogEHVI:  fatmoid(x) = 2/3 cauchy(x - m) for x < 0,
+// 1 - 2/3 cauchy(x + m) otherwise, cauchy(x) = 1 / (1 + x^2), m = sqrt(1/3) (continuous, = 1/2
+// at 0).  Log evaluated without cancellation on both branches; qg_dlog_fatmoid is its slope.
+constexpr double QG_FATMOID_M = 0.57735026918962576;
+__device__ __forceinline__ double qg_log_fatmoid(double x) {
+  if (x < 0.0) {
+    const double u = x - QG_FATMOID_M;
+    return -0.40546510810816438 - log1p(u * u);   // log(2/3) - log(1 + u^2)
+  }
+  const double u = x + QG_FATMOID_M;
+  return log1p(-(2.0 / 3.0) / (1.0 + u * u));
+}
+__device__ __forceinline__ double qg_dlog_fatmoid(double x) {
+  if (x < 0.0) {
+    const double u = x - QG_FATMOID_M;
+    return -2.0 * u / (1.0 + u * u);
+  }
+  const double u = x + QG_FATMOID_M, w = 1.0 + u * u, c = (2.0 / 3.0) / w;
+  return 2.0 * u * c / (w * (1.0 - c));
+}
+
 // fixed-order block sum over 256 threads (4 waves): xor-butterfly in the wave, then waves 0..3
 __device__ __forceinline__ double qg_block_sum(double v, double* red4) {
 #pragma unroll
@@ -150,7 +173,7 @@ __global__ __launch_bounds__(256) void qg_gram_samples(QgDims dm, int kind, int 
             const double u = ((xa[t] - sh) * sc - (xb[t] - sh) * sc) / lsj[t];
             d2 = fma(u, u, d2);
           }
-          kq = kxx[j] * kernel_value(kind, d2);
+          kq = kxx[j] * kernel_value(kind_of(kind, j), d2);
         }
         A[i][i2] = s2 * kq - gram[p++];
       }
@@ -500,7 +523,7 @@ __global__ __launch_bounds__(64) void qg_kqq_grad(int b, int m, int d, int kind,
         const double u = (xa[t] - xb[t]) * sc / lsj[t];
         d2 = fma(u, u, d2);
       }
-      const double ks = coef * kxx[j] * kernel_dscale(kind, d2);
+      const double ks = coef * kxx[j] * kernel_dscale(kind_of(kind, j), d2);
       for (int t = 0; t < d; ++t) {
         const double sc = scale ? scale[t] : 1.0;
         out[t] += ks * (xa[t] - xb[t]) * sc * sc / (lsj[t] * lsj[t]);
@@ -634,7 +657,7 @@ static int qg_check(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, co
 //   A(T)   = sum_k fatmin(z_k(T), log(min(u_k, 1e10) - l_k)) + sum_{i in T} lf_i
 //   cell   = logdiffexp(logsumexp_{|T| odd} A(T), logsumexp_{|T| even} A(T))
 //   LSE_sc = logsumexp_cells cell,   acq_c = logmeanexp_s LSE_sc
-// lf_i = sum_t logsigmoid(-c_t(y_i) / eta_t) (log feasibility).  A workgroup owns (sample,
+// lf_i = sum_t log_fatmoid(-c_t(y_i) / eta_t) (log feasibility, fat = True).  A workgroup owns (sample,
 // CT candidates, range of cells); the cells are staged through LDS with their log lengths;
 // each thread keeps an online log-sum-exp over its cells with Q (m_obj + 1) gradient slots
 // (d / d g_ik and d / d lf_i), merged over the thread groups and splits in a fixed order.
@@ -710,7 +733,7 @@ __global__ __launch_bounds__(QL_THREADS) void qlog_scan(int b, int nsplit, int C
       double l = 0.0;
       for (int t = 0; t < o.nc; ++t) {
         const double cval = o.cs[t] * (Y[((size_t)s * o.m + o.co[t]) * bq + (size_t)c * Q + i] - o.ct[t]);
-        l += qg_logsig(-cval / o.ce[t]);
+        l += qg_log_fatmoid(-cval / o.ce[t]);   // fat = True (qLog*)
       }
       lf[i] = l;
 #pragma unroll
@@ -916,7 +939,7 @@ __global__ __launch_bounds__(QLR_THREADS) void qlog_reduce(int b, int S, int nsp
 }
 
 // thread per (sample, point): dY[s][j][p] from the weighted gradient slots through the
-// objectives and the log feasibility (d logsigmoid(x)/dx = sigmoid(-x))
+// objectives and the log feasibility (qg_dlog_fatmoid)
 template <int MM, int Q>
 __global__ void qlog_dy(int b, int S, int nsplit, QgObj o, const double* __restrict__ Y,
                         const double* __restrict__ ws, double* __restrict__ dY) {
@@ -939,7 +962,7 @@ __global__ void qlog_dy(int b, int S, int nsplit, QgObj o, const double* __restr
   for (int t = 0; t < o.nc; ++t) {
     const int jj = o.co[t];
     const double cval = o.cs[t] * (Ys[(size_t)jj * bq] - o.ct[t]);
-    dy[jj] += glf * qg_sig(cval / o.ce[t]) * (-o.cs[t] / o.ce[t]);
+    dy[jj] += glf * qg_dlog_fatmoid(-cval / o.ce[t]) * (-o.cs[t] / o.ce[t]);
   }
   for (int j = 0; j < o.m; ++j) dY[((size_t)s * o.m + j) * bq + p] = dy[j];
 }

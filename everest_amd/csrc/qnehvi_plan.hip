@@ -273,7 +273,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
                            int backward, const double* X, void* work, double* acq, double* dX, int use_graph,
                            evr_qnehvi_plan** out) {
   EVR_CHECK(st && md && out && X && work && acq && b >= 1 && (!backward || dX) && md->M && md->Xn &&
-                md->lengthscales && md->n == st->n && md->d >= 1 && md->kind >= 0 && md->kind <= 3,
+                md->lengthscales && md->n == st->n && md->d >= 1 && kind_code_ok(md->kind, st->m),
             "evr_qnehvi_plan_create: bad arguments");
   evr_qnehvi_plan* p = new (std::nothrow) evr_qnehvi_plan();
   EVR_CHECK(p, "evr_qnehvi_plan_create: out of host memory");

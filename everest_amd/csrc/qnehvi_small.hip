@@ -140,8 +140,8 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
 // half) fall on the two halves of the bank row; each lane starts its row's columns at
 // lane mod b so the K stores spread over the banks.
 // ---------------------------------------------------------------------------------------
-template <int KIND>
-__global__ __launch_bounds__(256) void qs_fwd_x(int n, int nb, int Rr, int b, int d, const double* __restrict__ M,
+template <int KIND>   // KIND < 0: the family of output j from the mixed kind code kcode
+__global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr, int b, int d, const double* __restrict__ M,
                                                 const double* __restrict__ Xn, const double* X,
                                                 const double* __restrict__ shift, const double* __restrict__ scale,
                                                 const double* __restrict__ ls, double* __restrict__ R,
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int n, int nb, int Rr, int b, in
         if (cc < b) {
           int c = cc + rot;
           if (c >= b) c -= b;
-          Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND, d2v[cc]) : 0.0;
+          Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND >= 0 ? KIND : kind_of(kcode, j), d2v[cc]) : 0.0;
         }
       }
     }
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
           diff[k] = df * il[k];
           d2 = fma(df, df, d2);
         }
-        const double sgl = gk * kernel_dscale(kind, d2);
+        const double sgl = gk * kernel_dscale(kind_of(kind, j), d2);
 #pragma unroll
         for (int k = 0; k < QS_MAXD; ++k) acc[k] = fma(sgl, diff[k], acc[k]);
       }
@@ -581,13 +581,14 @@ int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mod
   const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
   const dim3 g(nt, st->m);
 #define GO(K_)                                                                                                  \
-  qs_fwd_x<K_><<<g, 256, 0, s>>>(st->n, st->nb, Rr, b, md->d, md->M, md->Xn, X, md->shift, md->scale,           \
+  qs_fwd_x<K_><<<g, 256, 0, s>>>(md->kind, st->n, st->nb, Rr, b, md->d, md->M, md->Xn, X, md->shift, md->scale, \
                                  md->lengthscales, R, P, nt)
   switch (md->kind) {
     case RBF: GO(RBF); break;
     case MATERN05: GO(MATERN05); break;
     case MATERN15: GO(MATERN15); break;
-    default: GO(MATERN25); break;
+    case MATERN25: GO(MATERN25); break;
+    default: GO(-1); break;
   }
 #undef GO
   EVR_LAUNCH_CHECK();

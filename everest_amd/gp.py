@@ -6,9 +6,14 @@ ConstantMean, RBF/Matérn ARD kernel (no outputscale by default), Gaussian likel
 noise >= 1e-4 and hyperpriors; fit = scipy L-BFGS-B on the raw parameters
 (``fit_gpytorch_mll``, max_attempts=10), every loss/gradient evaluated on the device.
 
-``GPBatch`` holds B exact GPs that share the same normalized training inputs (the
-ModelListGP of BotorchSurrogates.compatibilize, bofire/surrogates/botorch_surrogates.py:79-128)
-so that posteriors for all outputs are one batched launch.
+``GPBatch`` holds B exact GPs over one set of normalized training rows (the ModelListGP of
+BotorchSurrogates.compatibilize, bofire/surrogates/botorch_surrogates.py:79-128) so that
+posteriors for all outputs are one batched launch.  The members may differ in kernel family
+(one per output, EVR_KERNEL_MIXED) and in training rows: with a row mask, output j's GP is
+exact over its own rows V_j only — K_j is padded to the union with identity rows / columns
+outside V_j, so chol(K_pad) is L_j interleaved with identity rows, and L^-1's rows outside V_j
+(and with them alpha's entries) are zeroed: L^-T L^-1 = K_j^-1 embedded, and every posterior,
+root and projection formula runs unchanged over the union rows.
 """
 from __future__ import annotations
 
@@ -24,6 +29,28 @@ import torch
 from . import _native, ops
 
 MIN_INFERRED_NOISE_LEVEL = 1e-4
+KIND_MIXED, KIND_MAX_MIXED = 16, 13     # include/everest_amd.h EVR_KERNEL_MIXED
+
+
+def kind_code(kinds: Sequence[int]) -> int:
+    """Kernel family code of a batch of outputs: the family itself when all agree, else
+    EVR_KERNEL_MIXED with 2 bits per output (kind_j << (5 + 2 j))."""
+    kinds = [int(k) for k in kinds]
+    if any(k < 0 or k > 3 for k in kinds):
+        raise ValueError(f"kernel kinds must be in 0..3, got {kinds}")
+    if len(set(kinds)) <= 1:
+        return kinds[0] if kinds else 0
+    if len(kinds) > KIND_MAX_MIXED:
+        raise NotImplementedError(f"mixed kernel families are supported for at most {KIND_MAX_MIXED} outputs")
+    code = KIND_MIXED
+    for j, k in enumerate(kinds):
+        code |= k << (5 + 2 * j)
+    return code
+
+
+def kinds_of(code: int, B: int) -> List[int]:
+    code = int(code)
+    return [code] * B if code < KIND_MIXED else [(code >> (5 + 2 * j)) & 3 for j in range(B)]
 
 
 def softplus_np(x):
@@ -99,12 +126,20 @@ class GPHyper:
 
 
 class GPBatch:
-    """B exact GPs on shared normalized inputs Xn (n x d, device)."""
+    """B exact GPs on shared normalized inputs Xn (n x d, device).  ``kind``: one family, a
+    per-output list, or a kind code; ``mask`` (B x n, optional): the rows each output is
+    trained on (Y's entries outside them are ignored)."""
 
-    def __init__(self, Xn: torch.Tensor, Y: torch.Tensor, hypers: Sequence[GPHyper], kind: int,
-                 lo: torch.Tensor, hi: torch.Tensor):
+    def __init__(self, Xn: torch.Tensor, Y: torch.Tensor, hypers: Sequence[GPHyper], kind,
+                 lo: torch.Tensor, hi: torch.Tensor, mask: Optional[np.ndarray] = None):
         self.Xn = Xn.contiguous()
+        B_ = len(hypers)
+        if isinstance(kind, (list, tuple, np.ndarray)):
+            if len(kind) != B_:
+                raise ValueError(f"{len(kind)} kernel kinds for {B_} outputs")
+            kind = kind_code(kind)
         self.kind = int(kind)
+        self.kinds = kinds_of(self.kind, B_)
         self.lo = lo
         self.hi = hi
         self.inv_range = 1.0 / (hi - lo)
@@ -120,16 +155,42 @@ class GPBatch:
         self.ym = t([h.y_mean for h in hypers])
         self.ys = t([h.y_std for h in hypers])
         self.kxx = torch.ones(self.B, dtype=torch.float64, device=dev)
-        # standardized targets (B x n)
+        self.mask = None
+        if mask is not None:
+            mk = np.asarray(mask, dtype=bool).reshape(self.B, self.n)
+            if not mk.any(axis=1).all():
+                raise ValueError("every output needs at least one training row")
+            if not mk.all():
+                self.mask = torch.as_tensor(mk.astype(np.float64), device=dev)
+        # standardized targets (B x n); zero (the prior mean's residual is masked) outside each
+        # output's own rows
         Yc = Y.to(device=dev, dtype=torch.float64).reshape(self.n, self.B).T.contiguous()
         self.y = ((Yc - self.ym[:, None]) / self.ys[:, None]).contiguous()
+        if self.mask is not None:
+            self.y = torch.where(self.mask > 0, self.y, torch.zeros_like(self.y)).contiguous()
         self.refresh()
+
+    def valid_all_rows(self) -> np.ndarray:
+        """Rows every output is trained on (n bools)."""
+        if self.mask is None:
+            return np.ones(self.n, dtype=bool)
+        return (self.mask.min(0).values > 0).cpu().numpy()
 
     # -- caches: L = chol(K + s2 I), Linv, alpha, M = [Linv; alpha^T] ----------------------
     def refresh(self):
         Ky = ops.kernel_matrix(self.Xn, self.Xn, self.ls, self.kind, diag_add=self.noise)
+        if self.mask is not None:
+            # K_j padded: identity rows / columns outside output j's rows
+            mk = self.mask
+            Ky.mul_(mk[:, :, None] * mk[:, None, :])
+            Ky.diagonal(dim1=-2, dim2=-1).add_(1.0 - mk)
         self.L, self.Linv, _, _ = ops.cholesky_inverse(Ky, 1e-8, 3)
-        r = (self.y - self.const[:, None]).unsqueeze(-1).contiguous()         # B x n x 1
+        if self.mask is not None:
+            self.Linv.mul_(self.mask[:, :, None])                               # K_j^-1 embedded
+        r = (self.y - self.const[:, None]).unsqueeze(-1)                        # B x n x 1
+        if self.mask is not None:
+            r = r * self.mask[:, :, None]
+        r = r.contiguous()
         v = ops.gemm(self.Linv, r)
         self.alpha = ops.gemm(self.Linv, v, transA=True)[..., 0].contiguous()  # B x n
         self.M = torch.cat([self.Linv, self.alpha.unsqueeze(1)], dim=1).contiguous()  # B x (n+1) x n

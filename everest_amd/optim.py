@@ -616,7 +616,10 @@ class _Shard:
         return self._bounds(nb)[0][self.idx]
 
     def evaluate(self, acqf, X: np.ndarray, with_grad: bool):
-        """(values (nb,), gradients shaped like X | None) of the whole chunk X on every member."""
+        """(values (nb,), gradients shaped like X | None) of the whole chunk X on every member.
+        One all-gather of [flag | value | gradient] rows into one tensor and one copy to the
+        host per evaluation; a member whose local evaluation raises still joins the gather with
+        its flag set, so every member raises together and no collective is left unmatched."""
         nb = X.shape[0]
         if self.k == 1:
             return _local_eval(acqf, X, with_grad)
@@ -624,16 +627,31 @@ class _Shard:
         per = max(sizes)
         nx = int(np.prod(X.shape[1:]))
         i0, i1 = int(starts[self.idx]), int(starts[self.idx + 1])
-        loc = np.zeros((per, 1 + nx))
+        loc = np.zeros((per, 2 + nx))
+        err: Optional[BaseException] = None
         if i1 > i0:
-            a, g = _local_eval(acqf, X[i0:i1], with_grad, check=False)
-            loc[: i1 - i0, 0] = a
-            if with_grad:
-                loc[: i1 - i0, 1:] = g.reshape(i1 - i0, nx)
+            try:
+                a, g = _local_eval(acqf, X[i0:i1], with_grad, check=False)
+                loc[: i1 - i0, 1] = a
+                if with_grad:
+                    loc[: i1 - i0, 2:] = g.reshape(i1 - i0, nx)
+            except Exception as e:   # noqa: BLE001 — re-raised after the gather, on every member
+                err = e
+                loc[0, 0] = 2.0 if _is_notpsd(e) else 1.0
         lt = torch.as_tensor(loc, device=self.dev)
-        bufs = [torch.empty_like(lt) for _ in range(self.k)]
-        self.dist.all_gather(bufs, lt, group=self.pg)
-        full = np.concatenate([b.cpu().numpy()[:sz] for b, sz in zip(bufs, sizes)])
+        out = torch.empty((self.k * per, 2 + nx), dtype=torch.float64, device=self.dev)
+        self.dist.all_gather_into_tensor(out, lt, group=self.pg)
+        allr = out.cpu().numpy().reshape(self.k, per, 2 + nx)
+        flags = allr[:, 0, 0]
+        if (flags > 0).any():
+            if err is not None:
+                raise err
+            bad = [self.ranks[i] for i in np.nonzero(flags > 0)[0]]
+            if (flags[flags > 0] == 2.0).all():
+                from .ops import NotPSDError
+                raise NotPSDError(f"acquisition not p.d. on rank(s) {bad} (sharded evaluation)")
+            raise RuntimeError(f"sharded acquisition evaluation failed on rank(s) {bad}")
+        full = np.concatenate([allr[i, :sz, 1:] for i, sz in enumerate(sizes)])
         host_values(torch.from_numpy(full[:, 0]))
         return full[:, 0], (full[:, 1:].reshape(X.shape) if with_grad else None)
 

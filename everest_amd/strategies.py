@@ -380,19 +380,26 @@ class BotorchStrategy(PredictiveStrategy):
     def _ask_mixed_sequential(self, q: int, combos, ineq, eq):
         """optimize_acqf_mixed with q > 1 (botorch.optim.optimize_mixed, sequential branch):
         returns (q x d candidates, list of the rounds' values, stats of the last round)."""
+        # The reference builds the acquisition once (its sampler / prune seeds are drawn from
+        # the global generator then) and every round's optimiser draws follow those; here the
+        # acquisition is rebuilt per round from the same seed state, and the optimiser stream
+        # continues from where the previous round (round 1: the build) left it.
         seed_state = self.gen.get_state()
+        opt_state = None
         chosen, values = [], []
         stats = None
         try:
             for _ in range(q):
-                gen_state = self.gen.get_state()
                 self.gen.set_state(seed_state)            # same acquisition seeds every round
                 self._extra_pending = np.asarray(chosen) if chosen else None
                 acqf = self._get_acqfs(1)[0]
-                self.gen.set_state(gen_state)             # the optimiser's draws continue
+                if opt_state is None:
+                    opt_state = self.gen.get_state()      # round 1: the draws after the build
+                self.gen.set_state(opt_state)             # the optimiser's draws continue
                 x, v, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts,
                                                   self.num_raw_samples, self._get_optimizer_options(), self.gen, ineq,
                                                   eq, dist=self.dist, q=1)
+                opt_state = self.gen.get_state()
                 chosen.append(np.asarray(x, dtype=np.float64).reshape(-1))
                 values.append(v)
         finally:

@@ -243,27 +243,69 @@ class BotorchSurrogates:
                 f.result()
 
     def compatibilize(self, inputs, outputs) -> GPBatch:
-        """One batched device model over the outputs in domain order (ModelListGP analogue).
-        Requires every per-output GP to share training inputs, bounds and kernel family."""
+        """One batched device model over the outputs in domain order — the ModelListGP of
+        bofire/surrogates/botorch_surrogates.py:79-128.  Outputs may be fitted on different
+        rows (each surrogate trains on the rows where its output is valid,
+        bofire/surrogates/trainable.py:44-66) and with different kernel families: the batch
+        holds the union of the training rows with a per-output row mask and a per-output
+        family (gp.GPBatch), and each output's Normalize bounds are folded into its
+        lengthscales (the stationary kernels see (x - x') / ((hi - lo) ls) only), so every
+        member is exactly its own GP."""
         by_key = {s.output_key: s for s in self.surrogates}
         order = [k for k in outputs.get_keys() if k in by_key]
         ss = [by_key[k] for k in order]
+        for k, s in zip(order, ss):
+            if not s.is_fitted:
+                raise ValueError(f"Surrogate for output feature {k} not fitted.")
+        d = ss[0].state["X"].shape[1]
+        if any(s.state["X"].shape[1] != d for s in ss):
+            raise NotImplementedError("surrogates over different input subsets are out of scope for the MI355X build")
+        X_all, rows = union_rows([s.state["X"] for s in ss])
+        n, B = X_all.shape[0], len(ss)
+        mask = np.zeros((B, n), dtype=bool)
+        Y = np.zeros((n, B))
+        for j, (s, r) in enumerate(zip(ss, rows)):
+            mask[j, r] = True
+            Y[r, j] = s.state["y"]
         s0 = ss[0].state
-        for s in ss[1:]:
+        lo, hi = np.asarray(s0["lo"], dtype=np.float64), np.asarray(s0["hi"], dtype=np.float64)
+        hypers = []
+        for s in ss:
+            h = s.hyper()
             st = s.state
-            if (st["X"].shape != s0["X"].shape or not np.array_equal(st["X"], s0["X"])
-                    or not np.array_equal(st["lo"], s0["lo"]) or not np.array_equal(st["hi"], s0["hi"])
-                    or st["kind"] != s0["kind"]):
-                raise NotImplementedError("batched device model needs all outputs fitted on the same inputs, "
-                                          "normalization and kernel family")
+            if not (np.array_equal(st["lo"], lo) and np.array_equal(st["hi"], hi)):
+                h.lengthscale = np.asarray(h.lengthscale) * ((st["hi"] - st["lo"]) / (hi - lo))
+            hypers.append(h)
         dev = device()
         t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
-        Xn = t((s0["X"] - s0["lo"]) / (s0["hi"] - s0["lo"]))
-        Y = np.stack([s.state["y"] for s in ss], axis=1)
-        gp = GPBatch(Xn, t(Y), [s.hyper() for s in ss], s0["kind"], t(s0["lo"]), t(s0["hi"]))
+        gp = GPBatch(t((X_all - lo) / (hi - lo)), t(Y), hypers, [s.state["kind"] for s in ss], t(lo), t(hi),
+                     mask=mask)
         gp.output_keys = order
-        gp.X_raw = s0["X"]
+        gp.X_raw = X_all
+        gp.rows = rows
         return gp
+
+
+def union_rows(Xs):
+    """Union of the training-row multisets of several outputs, first output's rows first in
+    their order, then each later output's rows that no earlier row of equal value (unused by
+    that output) covers.  Returns (X_union, [row indices of output j's rows])."""
+    out, index, per = [], {}, []
+    for X in Xs:
+        X = np.asarray(X, dtype=np.float64)
+        used = {}
+        ids = np.empty(X.shape[0], dtype=np.int64)
+        for i, row in enumerate(X):
+            key = row.tobytes()
+            lst = index.setdefault(key, [])
+            k = used.get(key, 0)
+            if k == len(lst):
+                lst.append(len(out))
+                out.append(row)
+            ids[i] = lst[k]
+            used[key] = k + 1
+        per.append(ids)
+    return np.asarray(out, dtype=np.float64).reshape(-1, Xs[0].shape[1]), per
 
 
 def map(data_model):

@@ -25,6 +25,10 @@ extern "C" {
 #define EVR_KERNEL_MATERN05 1
 #define EVR_KERNEL_MATERN15 2
 #define EVR_KERNEL_MATERN25 3
+/* one family per output (heterogeneous ModelListGP members, bofire/surrogates/
+ * botorch_surrogates.py:79-128): EVR_KERNEL_MIXED | kind_j << (5 + 2 j), j < 13, wherever an
+ * entry point takes `kind` together with a batch of outputs */
+#define EVR_KERNEL_MIXED 16
 
 int evr_version(void);
 const char* evr_last_error(void);

@@ -110,11 +110,15 @@ class OutputConstraints:
         return torch.nn.functional.logsigmoid(-c / eta).sum(-1).exp()
 
 
-def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
+def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor, raw: bool = False):
     """Per-output joint posterior at Xn (... x p x d, normalized).  Returns mean (... x p x m)
-    and cov (... x m x p x p), computed the GPyTorch way: R = K(X, Xtr) L^-T."""
+    and cov (... x m x p x p), computed the GPyTorch way: R = K(X, Xtr) L^-T.  ``raw``: Xn
+    holds raw inputs and each model applies its own Normalize bounds (a ModelListGP whose
+    members were fitted on different rows, bofire/surrogates/botorch_surrogates.py:79-128)."""
     means, covs = [], []
+    X_in = Xn
     for st in models:
+        Xn = st.normalize(X_in) if raw else X_in
         Ks = kernel_matrix(Xn, st.X, st.lengthscale, st.kind)
         Linv = torch.linalg.solve_triangular(st.L, torch.eye(st.L.shape[0], **TK), upper=False)
         R = Ks @ Linv.T
@@ -126,12 +130,12 @@ def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor):
 
 
 def prune_baseline(models, Xn, objective, ref, z_prune: torch.Tensor, max_frac: float = 1.0, chunk: int = 0,
-                   constraints: Optional[OutputConstraints] = None):
+                   constraints: Optional[OutputConstraints] = None, raw: bool = False):
     """prune_inferior_points_multi_objective restated.  z_prune: S' x n x m.  Returns the
     kept row indices (sorted, unique) into Xn.  ``chunk`` > 0 walks the S' draws in chunks
     (same counts; bounds the n x n dominance tensors at BASELINE sizes).  Infeasible samples
     (any output constraint > 0) are set to the reference point."""
-    mean, cov = joint_posterior(models, Xn)                    # n x m, m x n x n
+    mean, cov = joint_posterior(models, Xn, raw)               # n x m, m x n x n
     L, _ = psd_safe_cholesky(cov)                              # m x n x n
     Sp = z_prune.shape[0]
     step = chunk if chunk > 0 else Sp
@@ -158,8 +162,9 @@ class QNEHVI:
 
     def __init__(self, models: List[GPState], Xb_n: torch.Tensor, objective: Objective,
                  ref: torch.Tensor, z_base: torch.Tensor, z_new: torch.Tensor, cells=None,
-                 constraints: Optional[OutputConstraints] = None, alpha: float = 0.0):
-        """``cells`` (list of 2 x C x m per sample) may be injected to time the forward
+                 constraints: Optional[OutputConstraints] = None, alpha: float = 0.0, raw: bool = False):
+        """``raw``: Xb_n and the candidates are raw inputs, normalised per model (joint_posterior).
+        ``cells`` (list of 2 x C x m per sample) may be injected to time the forward
         pass alone (bench.py cpu_baseline); parity tests always build their own.
         ``constraints``: baseline samples infeasible under them leave the Pareto sets (set to
         ref), candidate areas are weighted by the smoothed feasibility.
@@ -172,7 +177,8 @@ class QNEHVI:
         self.z_base = z_base
         self.z_new = z_new
         self.constraints = constraints
-        mean_b, cov_b = joint_posterior(models, Xb_n)          # nb x m, m x nb x nb
+        self.raw = raw
+        mean_b, cov_b = joint_posterior(models, Xb_n, raw)     # nb x m, m x nb x nb
         self.L_base, self.base_jitter = psd_safe_cholesky(cov_b)
         Yb = mean_b.unsqueeze(0) + torch.einsum("jik,skj->sij", self.L_base, z_base)
         self.base_obj = objective(Yb)                          # S x nb x m_obj
@@ -190,7 +196,7 @@ class QNEHVI:
         b, q, _ = Xn.shape
         nb = self.Xb.shape[0]
         Xfull = torch.cat([self.Xb.expand(b, nb, self.Xb.shape[-1]), Xn], dim=-2)
-        mean, cov = joint_posterior(self.models, Xfull)         # b x (nb+q) x m, b x m x P x P
+        mean, cov = joint_posterior(self.models, Xfull, self.raw)   # b x (nb+q) x m, b x m x P x P
         bottom = cov[..., -q:, :]
         bl, br = bottom[..., :nb], bottom[..., nb:]
         bl_chol = torch.linalg.solve_triangular(self.L_base, bl.transpose(-1, -2), upper=False).transpose(-1, -2)
@@ -366,16 +372,28 @@ def log_qehvi_cells(obj: torch.Tensor, lo: torch.Tensor, hi: torch.Tensor, tau_r
     return torch.logsumexp(logdiffexp(pos, neg), dim=-1)
 
 
-def log_feasibility(constraints: Optional[OutputConstraints], Y: torch.Tensor):
-    """Sum of logsigmoid(-c / eta) over the output constraints (None without constraints).
-    [upstream] compute_smoothed_feasibility_indicator(log=True) with fat = True uses a
-    fat-tailed sigmoid here; its exact form is not restated offline, so this build uses the
-    logistic one (fat = False) — parity unpinned."""
+def log_fatmoid(x: torch.Tensor) -> torch.Tensor:
+    """[upstream] botorch.utils.safe_math.log_fatmoid (tau = 1): log of the fat-tailed smooth
+    Heaviside fatmoid(x) = 2/3 cauchy(x - m) for x < 0, 1 - 2/3 cauchy(x + m) otherwise, with
+    cauchy(x) = 1 / (1 + x^2) and m = sqrt(1/3) (the inflection point; fatmoid(0) = 1/2 on both
+    branches).  Its tail is O(1/x^2) as x -> -inf, so infeasible-region gradients decay
+    polynomially, not exponentially as the logistic sigmoid's do."""
+    m = math.sqrt(1.0 / 3.0)
+    neg = math.log(2.0 / 3.0) - torch.log1p((x - m).square())
+    pos = torch.log1p(-(2.0 / 3.0) / (1.0 + (x + m).square()))
+    return torch.where(x < 0, neg, pos)
+
+
+def log_feasibility(constraints: Optional[OutputConstraints], Y: torch.Tensor, fat: bool = True):
+    """[upstream] compute_smoothed_feasibility_indicator(log=True, fat=fat) as qLogNEHVI /
+    qLogEHVI call it (fat = True by default there): the sum over the output constraints of
+    log_fatmoid(-c / eta) (fat) or logsigmoid(-c / eta) (not fat); None without constraints."""
     if constraints is None:
         return None
     c = constraints.values(Y)
     eta = torch.as_tensor(list(constraints.eta), dtype=c.dtype)
-    return torch.nn.functional.logsigmoid(-c / eta).sum(-1)
+    x = -c / eta
+    return (log_fatmoid(x) if fat else torch.nn.functional.logsigmoid(x)).sum(-1)
 
 
 class QLogNEHVI(QNEHVI):

@@ -99,12 +99,25 @@ class FlakyAcq(OracleAcq):
         return a, g
 
 
+class RaisingAcq(HostEvalAcq):
+    """A rank-local launch failure (an exception, not NaN) on rank 1 inside the joint chunk's
+    sharded evaluation: its group peer must not be left waiting in the per-evaluation gather."""
+
+    def eval_host(self, x, backward):
+        if dist.is_initialized() and dist.get_rank() == 1:
+            raise RuntimeError("simulated native launch failure")
+        return super().eval_host(x, backward)
+
+    def forward(self, X):      # raw screening stays healthy on every rank
+        return super().forward(X)
+
+
 def _run_generic(rank, world, port, ret, acq_name, options):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from everest_amd.optim import optimize_acqf
 
-    acq = {"host": HostEvalAcq, "flaky": FlakyAcq}[acq_name]()
+    acq = {"host": HostEvalAcq, "flaky": FlakyAcq, "raising": RaisingAcq}[acq_name]()
     gen = torch.Generator().manual_seed(7)
     bounds = np.array([[0.0] * 3, [1.0] * 3])
     try:
@@ -155,6 +168,15 @@ def test_own_chunk_failure_raises_on_every_rank():
     ret = _spawn("flaky", {"batch_limit": 1, "maxiter": 50})
     assert ret[0][0] == "error" and ret[1][0] == "error"
     assert ret[0][1] == "NotPSDError" and ret[1][1] == "NotPSDError"
+
+
+def test_sharded_rank_exception_raises_on_every_member():
+    """batch_limit = num_restarts: both ranks evaluate the joint chunk, rank 1's evaluation
+    raises; the error flag travels with the gathered slice, so both raise (no hang)."""
+    ret = _spawn("raising", {"batch_limit": 4, "maxiter": 50})
+    assert ret[0][0] == "error" and ret[1][0] == "error", ret
+    assert ret[1][1] == "RuntimeError" and "simulated" in ret[1][2]
+    assert ret[0][1] == "RuntimeError" and "rank(s) [1]" in ret[0][2]
 
 
 def test_restart_layout_no_idle_ranks():

@@ -246,3 +246,48 @@ def test_logdiffexp():
     assert torch.allclose(out[:2], torch.log(torch.exp(a[:2]) - torch.exp(b[:2])))
     assert out[2] == -math.inf and out[3] == -math.inf
     assert torch.allclose(out[4], torch.log(-torch.expm1(b[4] - a[4])) + a[4])
+
+
+def test_log_fatmoid_restatement():
+    """safe_math.log_fatmoid as restated: exp of it is the two-branch Cauchy fatmoid, it is
+    continuous (1/2) at 0 with a matching slope, tends to 1 for x -> +inf, decays as
+    O(1/x^2) for x -> -inf, and the closed-form slope used by the device backward
+    (qnehvi_general.hip qg_dlog_fatmoid) equals autograd's."""
+    m = math.sqrt(1 / 3)
+    cauchy = lambda z: 1 / (1 + z * z)  # noqa: E731
+    x = torch.linspace(-50, 50, 20001, dtype=torch.float64)
+    direct = torch.where(x < 0, 2 / 3 * cauchy(x - m), 1 - 2 / 3 * cauchy(x + m))
+    lf = oq.log_fatmoid(x)
+    assert torch.allclose(lf.exp(), direct, rtol=1e-14, atol=0)
+    assert abs(float(oq.log_fatmoid(torch.tensor(0.0, dtype=torch.float64))) - math.log(0.5)) < 1e-15
+    assert abs(float(oq.log_fatmoid(torch.tensor(-1e-12, dtype=torch.float64))) - math.log(0.5)) < 1e-11
+    big = torch.tensor([-1e3, -1e4], dtype=torch.float64)
+    ratio = oq.log_fatmoid(big).exp() * big.square()
+    assert torch.allclose(ratio, torch.full_like(ratio, 2 / 3), rtol=1e-2)      # 2/3 / x^2 tail
+    assert float(oq.log_fatmoid(torch.tensor(1e6, dtype=torch.float64))) > -1e-12
+    xg = x.clone().requires_grad_(True)
+    oq.log_fatmoid(xg).sum().backward()
+
+    def dlog(v):
+        if v < 0:
+            u = v - m
+            return -2 * u / (1 + u * u)
+        u = v + m
+        w = 1 + u * u
+        c = (2 / 3) / w
+        return 2 * u * c / (w * (1 - c))
+
+    ref = torch.tensor([dlog(float(v)) for v in x], dtype=torch.float64)
+    assert torch.allclose(xg.grad, ref, rtol=1e-12, atol=1e-15)
+    assert abs(dlog(-1e-15) - dlog(0.0)) < 1e-12                  # C^1 at 0
+
+
+def test_log_feasibility_fat_default():
+    """qLog* feasibility is fat by default; fat=False is the logistic form."""
+    con = oq.OutputConstraints(out=[0], sign=[1.0], thr=[0.2], eta=[1e-3])
+    Y = torch.tensor([[[0.0], [0.2], [0.5]]], dtype=torch.float64)
+    lf = oq.log_feasibility(con, Y)
+    assert torch.allclose(lf, oq.log_fatmoid(-(Y[..., 0] - 0.2) / 1e-3))
+    ll = oq.log_feasibility(con, Y, fat=False)
+    assert torch.allclose(ll, torch.nn.functional.logsigmoid(-(Y[..., 0] - 0.2) / 1e-3))
+    assert float(lf[0, 2]) > float(ll[0, 2]) + 100          # fat tail: far less negative

@@ -1,0 +1,54 @@
+#!/bin/bash
+# One GPU-box pass made of named steps, each under its own time limit; stops at the first
+# step that faults, aborts or times out (exit status other than 0 or 1: a failing test still
+# lets later steps run).  Output under gpurun_out/<tag>/.
+# usage: bash tools/gpu_steps.sh <tag> step...
+#   pytest      the -m gpu parity suite
+#   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
+#   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
+#               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
+#   pmc512      the same over the b = 512 evaluation pass (keys without suffix)
+#   sq20        SQ wave-cycle split of the restart scan (hvi_kdb) at b = 20
+#   bench       python bench.py (the driver's default command)
+#   prof        rocprofv3 --kernel-trace --stats of the bench command
+#   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
+set -o pipefail
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # run <name> <timeout_s> cmd...
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%H:%M:%S)] $name"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%H:%M:%S)] $name rc=$rc"
+  tail -3 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for st in "$@"; do
+  case $st in
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
+    pmc20)
+      cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
+      run pmc20_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc20_f" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
+      run pmc20_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc20_w" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
+      run pmc20_parse 60 python tools/pmc_traffic.py "$OUT/pmc20_f" "$OUT/pmc20_w" "$OUT/hbm_traffic.json" @b20 ;;
+    pmc512)
+      [ -f "$OUT/hbm_traffic.json" ] || cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
+      run pmc512_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc512_f" -o run --output-format csv -- python tools/loop_step.py 10 512
+      run pmc512_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc512_w" -o run --output-format csv -- python tools/loop_step.py 10 512
+      run pmc512_parse 60 python tools/pmc_traffic.py "$OUT/pmc512_f" "$OUT/pmc512_w" "$OUT/hbm_traffic.json" ;;
+    sq20)
+      run sq20 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "hvi_kdb|qs_fwd|qs_bwd" -d "$OUT/sq20" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
+      run sq20_parse 60 python tools/pmc_sq.py "$OUT/sq20" "$OUT/sq_counters.json" ;;
+    bench) run bench 900 python bench.py ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
+    cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo done
