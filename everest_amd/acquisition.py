@@ -244,6 +244,25 @@ class _BoxHviAcqf:
     cross-covariance, the sampling step, the box-cell HVI scan and their analytic backward
     (subclasses set gp, dev, Xk, M, state, model and _plans)."""
 
+    # the attributes the reference's tests read off BoTorch's acquisition objects
+    # (tests/bofire/strategies/test_mobo.py:123-160): ref_point, constraints, eta
+    @property
+    def ref_point(self) -> torch.Tensor:
+        return self.ref
+
+    @property
+    def constraints(self) -> list:
+        """Output constraints (output, sign, threshold, eta): c = sign (y - threshold) <= 0."""
+        return list(self.spec.constraints)
+
+    @property
+    def eta(self) -> Optional[torch.Tensor]:
+        cs = self.spec.constraints
+        if not cs:
+            return None
+        e = torch.tensor([c[3] for c in cs], dtype=torch.float64)
+        return e[0] if len(set(c[3] for c in cs)) == 1 else e
+
     def _use_log_scan(self, tau_relu: float, tau_max: float):
         """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
         q = 1 affine fast path runs hvi_log.hip (the tabulated keyed kernel over compressed
@@ -341,17 +360,22 @@ class _BoxHviAcqf:
                 if v.device.type == "cuda" and id(v) not in seen:
                     seen.add(id(v))
                     out.append(v)
-            elif isinstance(v, (list, tuple)) and depth < 3:
+            elif depth >= 4 or id(v) in seen:
+                return
+            elif isinstance(v, (list, tuple)):
                 for x in v:
                     walk(x, depth + 1)
-            elif isinstance(v, dict) and depth < 3:
+            elif isinstance(v, dict):
                 for x in v.values():
                     walk(x, depth + 1)
-        for obj in (self, self.gp, getattr(self, "cells", None)):
-            if obj is not None:
-                for k, v in vars(obj).items():
+            elif type(v).__module__.startswith("everest_amd") and hasattr(v, "__dict__"):
+                # the package's own holders (Cells, KdGroups, GPBatch, ...): their tensors are
+                # what the state's cell / group pointers refer to
+                seen.add(id(v))
+                for k, x in vars(v).items():
                     if k not in ("_torch_acqs", "_plans"):
-                        walk(v)
+                        walk(x, depth + 1)
+        walk(self)
         return out
 
     def _torch_acq(self, q: int, fast: bool):
@@ -829,6 +853,7 @@ class QEHVI(_BoxHviAcqf):
         self.obj_a, self.obj_b = _fast_affine(spec, m, dev)
         self.sampler_seed = int(sampler_seed)
         Y_part = np.asarray(Y_part, dtype=np.float64).reshape(-1, mo)
+        self.Y_part = Y_part
         self.Xk = gp.Xn
         S_ = self.S
         if Y_part.shape[0] > 0:

@@ -1,5 +1,6 @@
 """Workload generators with BoFire's benchmark API (``.domain``, ``.f(df, return_complete)``):
-Detergent (bofire/benchmarks/detergent.py:15-88) and DTLZ2 (bofire/benchmarks/multi.py:37-132).
+Detergent (bofire/benchmarks/detergent.py:15-88), DTLZ2 (bofire/benchmarks/multi.py:37-132)
+and C2DTLZ2 (bofire/benchmarks/multi.py:227-272).
 Numbers restated: Detergent's coefficient table is data of the reference benchmark."""
 from __future__ import annotations
 
@@ -9,7 +10,7 @@ import numpy as np
 import pandas as pd
 
 from .data_models import (ContinuousInput, ContinuousOutput, Domain, Inputs, LinearInequalityConstraint,
-                          MinimizeObjective, Outputs)
+                          MaximizeSigmoidObjective, MinimizeObjective, Outputs)
 
 
 class Benchmark:
@@ -55,6 +56,39 @@ class DTLZ2(Benchmark):
         Y = pd.DataFrame(np.stack(fs, axis=-1), columns=keys, index=candidates.index)
         for k in keys:
             Y[f"valid_{k}"] = 1
+        return Y
+
+
+class C2DTLZ2(DTLZ2):
+    """Constrained DTLZ2 (bofire/benchmarks/multi.py:227-272): DTLZ2 plus the output ``slack``
+    with MaximizeSigmoidObjective(tp=0, steepness=1e3) — feasible where slack >= 0, i.e. an
+    output constraint with eta = 1e-3.  slack = -min(min_i [(f_i - 1)^2 + sum_{j != i}
+    (f_j^2 - r^2)], sum_i [(f_i - 1/sqrt(m))^2 - r^2]) with r = 0.2."""
+
+    def __init__(self, dim: int, num_objectives: int = 2):
+        super().__init__(dim, num_objectives)
+        self._domain = Domain(
+            inputs=self._domain.inputs,
+            outputs=Outputs(features=list(self._domain.outputs.features) + [
+                ContinuousOutput(key="slack", objective=MaximizeSigmoidObjective(w=1.0, tp=0, steepness=1.0 / 1e-3))]),
+        )
+
+    @property
+    def best_possible_hypervolume(self) -> float:
+        return 0.3996406303723544
+
+    def _f(self, candidates: pd.DataFrame) -> pd.DataFrame:
+        r = 0.2
+        Y = super()._f(candidates)
+        f = Y[[f"f_{i}" for i in range(self.num_objectives)]].values
+        m = f.shape[1]
+        sq = f ** 2 - r ** 2
+        term1 = (f - 1.0) ** 2
+        term2 = sq.sum(axis=1, keepdims=True) - sq           # sum over j != i
+        min1 = (term1 + term2).min(axis=1)
+        min2 = ((f - 1.0 / math.sqrt(m)) ** 2 - r ** 2).sum(axis=1)
+        Y["slack"] = -np.minimum(min1, min2)
+        Y["valid_slack"] = 1
         return Y
 
 

@@ -409,4 +409,56 @@ struct LseState {
   }
 };
 
+// The sampling step's per-(output, candidate) part (qn_samples_norms; fused into the restart
+// scan hvi_kdb): mu = ym + s (c + a) with a the mean row of R, and the new-point root
+// L22 = sqrt(s^2 (kxx - |C k|^2) - |L21|^2) from the per-tile partial sums of squares Pj
+// (P[tile][class][c], class 0: kernel rows, 1: baseline rows), with psd_safe_cholesky's 1x1
+// ladder (plain, then total jitter 1e-8 10^(t-1), t = 1..6); flag = 1 when every rung fails.
+// One definition so that both kernels produce bitwise the same samples.
+__device__ __forceinline__ void qn_mu_l22(const double* __restrict__ Pj, int nrt_used, int b, int c, double a,
+                                          double s, double cc, double ym, double kxx, double& mu, double& l22,
+                                          int& flag) {
+  double ssv = 0.0, ssw = 0.0;
+#pragma unroll 4
+  for (int rt = 0; rt < nrt_used; ++rt) {
+    ssv += Pj[((size_t)rt * 2 + 0) * b + c];
+    ssw += Pj[((size_t)rt * 2 + 1) * b + c];
+  }
+  mu = ym + s * (cc + a);
+  const double var = s * s * (kxx - ssv);
+  const double br = var - ssw;
+  l22 = nan("");
+  flag = 1;
+  if (!isnan(br)) {
+    for (int t = 0; t <= 6; ++t) {
+      const double jit = (t == 0) ? 0.0 : 1e-8 * pow(10.0, (double)(t - 1));
+      if (br + jit > 0.0) {
+        l22 = sqrt(br + jit);
+        flag = 0;
+        break;
+      }
+    }
+  }
+}
+
+// objective value of one sample: g = a (mu + h + L22 z) + b (h absent without sample rows)
+__device__ __forceinline__ double qn_sample_obj(double mu, double hv, bool has_h, double l22, double zv, double A,
+                                               double B) {
+  const double y = (has_h ? mu + hv : mu) + l22 * zv;
+  return fma(A, y, B);
+}
+
+// Where the restart scan takes its samples from: G (S x m x b, written by qn_samples_norms),
+// or, with R set, formed in its staging from R's rows and the partial norms (the sampling
+// launch fused away); sample s's workgroup 0 also writes L22 and the flags the backward and
+// the dX reduction read.
+struct KbSamples {
+  const double* R;        // m x Rr x b projection, nullptr: read G
+  const double* P;        // m x nrt x 2 x b partial norms
+  const double *cc, *ym, *ys, *kxx, *zq, *oa, *ob;
+  double* L22;
+  int* flags;
+  int n, nb, nh, nrt, nrt_used;
+};
+
 }  // namespace evr

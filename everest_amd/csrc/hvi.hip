@@ -1694,7 +1694,8 @@ __device__ __forceinline__ int kb_scan_excl(int v, int* sh, int* total) {
 
 template <int M>
 __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double* __restrict__ G, HviKd kd,
-                                                      double* __restrict__ sval, double* __restrict__ dG) {
+                                                      KbSamples smp, double* __restrict__ sval,
+                                                      double* __restrict__ dG) {
   constexpr int NV = M + 1;
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kd_dyn[];
@@ -1747,7 +1748,28 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
   }
   for (int e = tid; e < KB_B * M; e += KB_THREADS) {
     const int j = e / KB_B, c = e - j * KB_B;
-    yv[c][j] = c < b ? G[((size_t)s * M + j) * b + c] : -INFINITY;
+    double y = -INFINITY;
+    if (c < b) {
+      if (smp.R) {
+        // the sampling step (qn_samples_norms' arithmetic for this sample)
+        const long long Rr = (long long)smp.n + smp.nb + smp.nh + 1;
+        const double* Rj = smp.R + (size_t)j * Rr * b;
+        const double hv = smp.nh ? Rj[(size_t)(smp.n + smp.nb + s) * b + c] : 0.0;
+        const double zv = smp.zq[(size_t)s * M + j];
+        double mu, l22;
+        int flag;
+        qn_mu_l22(smp.P + (size_t)j * smp.nrt * 2 * b, smp.nrt_used, b, c, Rj[(size_t)(Rr - 1) * b + c], smp.ys[j],
+                  smp.cc[j], smp.ym[j], smp.kxx[j], mu, l22, flag);
+        if (s == 0) {
+          smp.L22[(size_t)j * b + c] = l22;
+          smp.flags[(size_t)j * b + c] = flag;
+        }
+        y = qn_sample_obj(mu, hv, smp.nh != 0, l22, zv, smp.oa[j], smp.ob[j]);
+      } else {
+        y = G[((size_t)s * M + j) * b + c];
+      }
+    }
+    yv[c][j] = y;
   }
   for (int e = tid; e < KB_WAVES * KB_B * NV; e += KB_THREADS) acc[e] = 0.0;
   __syncthreads();
@@ -2194,10 +2216,10 @@ static bool hvi_kdb_applies(const evr_qnehvi_state* st, int b) {
 
 template <int M>
 static int hvi_kdb_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
-                          double* dG) {
+                          double* dG, const KbSamples& smp) {
   const KbLds L = kb_lds(st->pts_stride, M, st->max_groups);
   EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdb<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.bytes));
-  hvi_kdb<M><<<st->S, KB_THREADS, L.bytes, s>>>(b, st->S, G, hvi_kd_of(st), sval, dG);
+  hvi_kdb<M><<<st->S, KB_THREADS, L.bytes, s>>>(b, st->S, G, hvi_kd_of(st), smp, sval, dG);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -2375,7 +2397,8 @@ int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const do
             "evr_hvi_restart_fb: bad arguments or the state / batch is not a kd restart batch (b <= 32)");
   int rc = 0;
   if (hvi_kdb_applies(st, b)) {
-#define L(MM) rc = hvi_kdb_launch<MM>((hipStream_t)stream, st, b, G, sval, dG)
+    const KbSamples smp{};
+#define L(MM) rc = hvi_kdb_launch<MM>((hipStream_t)stream, st, b, G, sval, dG, smp)
     EVR_M_SWITCH(st->m, L);
 #undef L
     return rc;
@@ -2385,6 +2408,34 @@ int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const do
 #undef L
   return rc;
 }
+
+}  // extern "C"
+
+namespace evr {
+// the restart scan with the sampling step fused into its staging (native plan, b <= 32 with
+// the kdb variant): R / P from the projection, L22 / flags written by sample 0's workgroup
+bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b) {
+  static const bool on = [] {
+    const char* e = std::getenv("EVR_FUSED_SAMPLES");
+    return !(e && e[0] == '0');
+  }();
+  return on && hvi_kdb_applies(st, b) && st->obj_a && st->obj_b && st->zq;
+}
+
+int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
+                  int nrt_used, double* L22, int* flags, double* sval, double* dG) {
+  EVR_CHECK(R && P && L22 && flags && sval && dG && hvi_kdb_fused_applies(st, b), "hvi_kdb_fused: bad arguments");
+  KbSamples smp{R, P, st->c, st->ym, st->ys, st->kxx, st->zq, st->obj_a, st->obj_b, L22, flags,
+                st->n, st->nb, qn_nh(st), nrt, nrt_used};
+  int rc = 0;
+#define L(MM) rc = hvi_kdb_launch<MM>(s, st, b, nullptr, sval, dG, smp)
+  EVR_M_SWITCH(st->m, L);
+#undef L
+  return rc;
+}
+}  // namespace evr
+
+extern "C" {
 
 int evr_hvi_set_restart_variant(int variant) {
   EVR_CHECK(variant == 1 || variant == 2, "evr_hvi_set_restart_variant: variant must be 1 or 2, got %d", variant);

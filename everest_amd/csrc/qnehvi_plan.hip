@@ -46,6 +46,9 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags);
 constexpr int QS_TILE_ROWS = 16;
+bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
+int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
+                  int nrt_used, double* L22, int* flags, double* sval, double* dG);
 
 // b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
 // EVR_SMALL=0 keeps the 64 x 64-tile path for A/B timing and the parity test
@@ -203,9 +206,18 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
                                    p->L.Wf != p->L.G ? (double*)(w + p->L.Wf) : nullptr)) {
     return rc;
   }
+  double* dG = (double*)(w + p->L.dG);
+  if (small && p->backward && p->L.fused_scan && hvi_kdb_fused_applies(st, b)) {
+    // the sampling step inside the restart scan's staging (one launch less); G is not formed
+    if (int rc = hvi_kdb_fused(s, st, b, R, P, cdiv(qn_rows(st), QS_TILE_ROWS), cdiv(st->n + st->nb, QS_TILE_ROWS),
+                               L22, flags, hw, dG))
+      return rc;
+    if (done) *done = hout ? 1 : 0;
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+                       hw, flags);
+  }
   if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : 64)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
-  double* dG = (double*)(w + p->L.dG);
   if (small && p->L.fused_scan) {
     // one launch for thresholds + scan + split reduction (hvi_kd3); the per-sample values in
     // the scan workspace become acq inside the dX reduction

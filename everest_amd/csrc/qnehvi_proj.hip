@@ -227,30 +227,9 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
     zv[q] = (q < ns) ? zq[(size_t)(s0 + q) * m + j] : 0.0;
   }
   const double* Pj = P + (size_t)j * nrt * 2 * b;
-  double ssv = 0.0, ssw = 0.0;
-#pragma unroll 4
-  for (int rt = 0; rt < nrt_used; ++rt) {
-    ssv += Pj[((size_t)rt * 2 + 0) * b + c];
-    ssw += Pj[((size_t)rt * 2 + 1) * b + c];
-  }
-  const double a = Rj[(size_t)(Rr - 1) * b + c];
-  const double s = ys[j];
-  const double mu = ym[j] + s * (cc[j] + a);
-  const double var = s * s * (kxx[j] - ssv);
-  const double br = var - ssw;
-  // psd_safe_cholesky on the 1x1 block: plain, then total jitter 1e-8*10^(t-1), t=1..6
-  double l22 = nan("");
-  int flag = 1;
-  if (!isnan(br)) {
-    for (int t = 0; t <= 6; ++t) {
-      const double jit = (t == 0) ? 0.0 : 1e-8 * pow(10.0, (double)(t - 1));
-      if (br + jit > 0.0) {
-        l22 = sqrt(br + jit);
-        flag = 0;
-        break;
-      }
-    }
-  }
+  double mu, l22;
+  int flag;
+  qn_mu_l22(Pj, nrt_used, b, c, Rj[(size_t)(Rr - 1) * b + c], ys[j], cc[j], ym[j], kxx[j], mu, l22, flag);
   if (chunk == 0) {
     L22[(size_t)j * b + c] = l22;
     flags[(size_t)j * b + c] = flag;
@@ -259,8 +238,7 @@ __global__ __launch_bounds__(64) void qn_samples_norms(int n, int nb, int S, int
 #pragma unroll
   for (int q = 0; q < SCH; ++q) {
     if (q < ns) {
-      const double y = (nh ? mu + hv[q] : mu) + l22 * zv[q];
-      G[((size_t)(s0 + q) * m + j) * b + c] = fma(A, y, B0);
+      G[((size_t)(s0 + q) * m + j) * b + c] = qn_sample_obj(mu, hv[q], nh != 0, l22, zv[q], A, B0);
     }
   }
 }

@@ -52,16 +52,25 @@ def test_config3_prune_matches_oracle(config3):
     assert np.abs(dp - probs.numpy()).max() <= 1.0 / 2048
 
 
-def test_config3_qnehvi_values_and_grads_match_oracle(config3):
-    import bench
-
+@pytest.fixture(scope="module")
+def oracle3(config3):
+    """The oracle's qNEHVI at the bench state, with its own 256 Python partitions (built once)."""
     c = config3
     acqf, m, S = c["acqf"], c["m"], c["S"]
     nb = acqf.nb
     idx = torch.as_tensor(np.sort(acqf.base_rows))
     zb = oq.base_samples(S, nb, m, 1234)
     zn = oq.base_samples(S, nb + 1, m, 1234)[:, nb:nb + 1]
-    orc = oq.QNEHVI(c["states"], c["Xn"][idx], c["objective"], c["ref"], zb, zn)   # its own 256 partitions
+    orc = oq.QNEHVI(c["states"], c["Xn"][idx], c["objective"], c["ref"], zb, zn)
+    return dict(orc=orc, idx=idx, zb=zb, zn=zn)
+
+
+def test_config3_qnehvi_values_and_grads_match_oracle(config3, oracle3):
+    import bench
+
+    c = config3
+    acqf = c["acqf"]
+    orc = oracle3["orc"]
     assert acqf.stats.total_cells == sum(cc.shape[1] for cc in orc.cells)
     assert acqf.stats.max_cells == max(cc.shape[1] for cc in orc.cells)
 
@@ -99,6 +108,35 @@ def test_config3_batch_split_equals_full_batch(config3):
     assert torch.allclose(a_full[:500], a_p, rtol=1e-7, atol=1e-7 * a_full.abs().max().item()), da
     scale = g_full.abs().max().item()
     assert torch.allclose(g_full[:500], g_p, rtol=1e-6, atol=1e-6 * scale), (g_full[:500] - g_p).abs().max().item()
+
+
+def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
+    """qLogNEHVI (MoboStrategy's default) at the BASELINE state: same GPs, prune / sampler
+    seeds, pruned baseline and partitions as the qNEHVI bench state; the b = 20 restart batch
+    (all 20 candidates) and a 16-candidate subset of a b = 512 batch against the oracle's
+    fat-smoothed log HVI and its autograd gradients."""
+    import bench
+    from everest_amd.acquisition import QLogNEHVI
+
+    c = config3
+    acqf, m, S = c["acqf"], c["m"], c["S"]
+    qa = QLogNEHVI(acqf.gp, c["X"], c["X"], -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=1234,
+                   prune_baseline=True, prune_seed=4321)
+    assert np.array_equal(np.sort(qa.base_rows), oracle3["idx"].numpy())
+    assert qa.stats.total_cells == acqf.stats.total_cells
+    olog = oq.QLogNEHVI(c["states"], c["Xn"][oracle3["idx"]], c["objective"], c["ref"], oracle3["zb"],
+                        oracle3["zn"], cells=oracle3["orc"].cells)
+    for b, sub in ((20, torch.arange(20)), (512, torch.arange(0, 512, 32))):
+        Xc = bench.candidates(b, c["d"], seed=2, device=c["dev"])
+        acq, dX = qa.forward_backward(Xc)
+        xt = Xc.cpu()[sub].clone().requires_grad_(True)
+        ref = olog.forward(xt.unsqueeze(1))
+        ref.sum().backward()
+        assert torch.isfinite(acq).all() and torch.isfinite(ref).all()
+        a = acq.cpu()[sub]
+        assert torch.allclose(a, ref.detach(), rtol=1e-9, atol=1e-9), (b, (a - ref.detach()).abs().max())
+        g = dX.cpu()[sub]
+        assert torch.allclose(g, xt.grad, rtol=1e-6, atol=1e-9 * xt.grad.abs().max()), (b, (g - xt.grad).abs().max())
 
 
 @pytest.fixture(scope="module")

@@ -102,3 +102,37 @@ def test_normalize_bounds_known_answer():
     X = pd.DataFrame({"x0": [-1.0, 2.0], "x1": [0.0, 5.0]})
     lo, hi = sur._bounds(X)
     assert np.allclose(lo, [-4.0, -4.0]) and np.allclose(hi - lo, [8.0, 9.0])
+
+
+@pytest.mark.parametrize("domain, ref_point, experiments, expected", [
+    (valid_domains[0], {"of1": 0.5, "of2": 10.0}, dfs[0], [0.5, -10.0]),
+    (valid_domains[1], {"of1": 0.5, "of3": 0.5}, dfs[1], [0.5, 0.5]),
+    (valid_domains[0], None, dfs[0], [1.0, -5.0]),
+    (valid_domains[1], None, dfs[1], [1.0, 2.0])])
+def test_mobo_get_adjusted_refpoint(domain, ref_point, experiments, expected):
+    """tests/bofire/strategies/test_mobo.py:59-75."""
+    s = strategies.map(dm.MoboStrategy(domain=domain, ref_point=ref_point))
+    s.set_experiments(experiments)   # as the reference test: no training
+    rp = s.get_adjusted_refpoint()
+    assert isinstance(rp, list) and np.allclose(rp, expected)
+
+
+def test_c2dtlz2_slack_restatement():
+    """C2DTLZ2 (bofire/benchmarks/multi.py:227-272): the slack output against a direct
+    per-row evaluation of the reference's gather formula; its objective is a sigmoid
+    constraint with eta = 1e-3."""
+    from everest_amd.benchmarks import C2DTLZ2
+
+    bm = C2DTLZ2(dim=4)
+    X = pd.DataFrame(np.random.default_rng(0).uniform(size=(16, 4)), columns=bm.domain.inputs.get_keys())
+    Y = bm.f(X)
+    f = Y[["f_0", "f_1"]].values
+    r = 0.2
+    for i, row in enumerate(f):
+        m = len(row)
+        min1 = min((row[a] - 1) ** 2 + sum(row[b] ** 2 - r ** 2 for b in range(m) if b != a) for a in range(m))
+        min2 = sum((row[a] - 1 / math.sqrt(m)) ** 2 - r ** 2 for a in range(m))
+        assert np.isclose(Y["slack"].values[i], -min(min1, min2), rtol=1e-14, atol=1e-15)
+    assert (Y["valid_slack"] == 1).all()
+    obj = bm.domain.outputs.get_by_key("slack").objective
+    assert isinstance(obj, dm.MaximizeSigmoidObjective) and obj.tp == 0 and np.isclose(1 / obj.steepness, 1e-3)

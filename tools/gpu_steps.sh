@@ -4,11 +4,13 @@
 # lets later steps run).  Output under gpurun_out/<tag>/.
 # usage: bash tools/gpu_steps.sh <tag> step...
 #   pytest      the -m gpu parity suite
+#   pytestf     the test files named in $PYTEST_FILES
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
 #   pmc512      the same over the b = 512 evaluation pass (keys without suffix)
 #   sq20        SQ wave-cycle split of the restart scan (hvi_kdb) at b = 20
+#   kdwaves     per-wave phase stamps of the restart scan (EVR_KD_PROF=2 build in _libprof/)
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
@@ -31,6 +33,7 @@ run() {  # run <name> <timeout_s> cmd...
 for st in "$@"; do
   case $st in
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    pytestf) run pytestf 900 python -u -m pytest $PYTEST_FILES -x -q --timeout 300 --timeout-method thread ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
       cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
@@ -45,6 +48,7 @@ for st in "$@"; do
     sq20)
       run sq20 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "hvi_kdb|qs_fwd|qs_bwd" -d "$OUT/sq20" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
       run sq20_parse 60 python tools/pmc_sq.py "$OUT/sq20" "$OUT/sq_counters.json" ;;
+    kdwaves) EVR_LIB_PATH=everest_amd/_libprof/libeverest_amd.so run kdwaves 300 python tools/kd3_waves.py ;;
     bench) run bench 900 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
