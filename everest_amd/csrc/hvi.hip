@@ -1968,22 +1968,25 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
         // slot in registers across the rounds, then one butterfly per (slot, value) — instead
         // of a segmented scan per round
         if (EVR_KD_PROF == 2) nt_ += te - tb;
-        double as[KB_SLOTS][NV];
+        // three named slot rows, each added to with the term masked in (a + 0.0 = a: the
+        // values are >= 0) — an indexed slot array (or a select on the slot) is lowered to
+        // scratch memory by the compiler: 112 B / lane of spills, ~58 MB written per launch
+        static_assert(KB_SLOTS == 3, "slot rows are spelled out");
+        double as0[NV], as1[NV], as2[NV];
 #pragma unroll
-        for (int k = 0; k < KB_SLOTS; ++k)
-#pragma unroll
-          for (int v = 0; v < NV; ++v) as[k][v] = 0.0;
+        for (int v = 0; v < NV; ++v) as0[v] = as1[v] = as2[v] = 0.0;
         auto term_acc = [&](const int c, const unsigned long long key) {
           if (c < 0) return;
           double val[NV];
           term_value(key, c, val);
           const int k = c - cf;
+          const double w0 = k == 0 ? 1.0 : 0.0, w1 = k == 1 ? 1.0 : 0.0, w2 = k == 2 ? 1.0 : 0.0;
 #pragma unroll
-          for (int kk = 0; kk < KB_SLOTS; ++kk)
-            if (k == kk) {
-#pragma unroll
-              for (int v = 0; v < NV; ++v) as[kk][v] += val[v];
-            }
+          for (int v = 0; v < NV; ++v) {
+            as0[v] = fma(w0, val[v], as0[v]);
+            as1[v] = fma(w1, val[v], as1[v]);
+            as2[v] = fma(w2, val[v], as2[v]);
+          }
         };
         int cA, cB;
         unsigned long long kA, kB;
@@ -1997,12 +2000,11 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
         }
         // per (slot, value) the wave sum by a DPP inclusive scan (VALU only, fixed order):
         // lane 63 holds the total
-#pragma unroll
-        for (int kk = 0; kk < KB_SLOTS; ++kk) {
-          if (cf + kk > cl) break;
+        auto slot_out = [&](const int kk, double (&a)[NV]) {
+          if (cf + kk > cl) return;
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
-            double x = as[kk][v];
+            double x = a[v];
             x += dpp_f64<0x111, 0xF>(x);
             x += dpp_f64<0x112, 0xF>(x);
             x += dpp_f64<0x114, 0xF>(x);
@@ -2011,7 +2013,10 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
             x += dpp_f64<0x143, 0xC>(x);
             if (lane == 63) accw[(cf + kk) * NV + v] += x;
           }
-        }
+        };
+        slot_out(0, as0);
+        slot_out(1, as1);
+        slot_out(2, as2);
       } else if (te > tb) {
         if (EVR_KD_PROF == 2) nt_ += te - tb;
         int cA, cB;

@@ -399,6 +399,12 @@ __global__ __launch_bounds__(256) void kmat_mfma_pers(int n1, int n2, int d, int
 // one global round trip per output: 22 us at m = 5, n = b = 512 on MI355X), 1/ls and the
 // output scales of the chunk sit in LDS.
 constexpr int KG_B = 8;
+// outputs per LDS chunk / G loads in flight per row: 8 up to 16 dims; at 32 / 64 dims the
+// fully unrolled (output x dim) body of 8 outputs did not stay in registers (1.7 / 5.2 KB of
+// scratch per lane), so those instantiations take 2 outputs per round and form the scaled
+// differences twice instead of keeping a diff[] row
+template <int MAXD>
+__host__ __device__ constexpr int kg_outputs() { return MAXD <= 16 ? KG_B : 2; }
 template <int MAXD>
 __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d, int rows_per,
                                                           const double* __restrict__ X1,
@@ -415,8 +421,9 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
   const int split = blockIdx.y;
   const int i0 = split * rows_per, i1 = min(n1, i0 + rows_per);
   __shared__ double red[4][64][MAXD];
-  __shared__ double il_s[KG_B][MAXD];
-  __shared__ double os_s[KG_B];
+  constexpr int KGO = kg_outputs<MAXD>();
+  __shared__ double il_s[KGO][MAXD];
+  __shared__ double os_s[KGO];
   double x2[MAXD];
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) {
@@ -432,8 +439,8 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) acc[k] = 0.0;
   const size_t bstride = (size_t)n1 * n2;
-  for (int b0 = 0; b0 < B; b0 += KG_B) {
-    const int nb = min(KG_B, B - b0);
+  for (int b0 = 0; b0 < B; b0 += KGO) {
+    const int nb = min(KGO, B - b0);
     __syncthreads();
     for (int t = threadIdx.x; t < nb * MAXD; t += blockDim.x) {
       const int bb = t / MAXD, k = t % MAXD;
@@ -445,9 +452,9 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
     const double* Gc = G + (size_t)b0 * bstride + c;
 #pragma unroll 2
     for (int i = i0 + ry; i < i1; i += 4) {
-      double g[KG_B];
+      double g[KGO];
 #pragma unroll
-      for (int bb = 0; bb < KG_B; ++bb) g[bb] = (bb < nb) ? Gc[bb * bstride + (size_t)i * n2] : 0.0;
+      for (int bb = 0; bb < KGO; ++bb) g[bb] = (bb < nb) ? Gc[bb * bstride + (size_t)i * n2] : 0.0;
       double x1[MAXD];
 #pragma unroll
       for (int k = 0; k < MAXD; ++k) {
@@ -460,23 +467,23 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
         x1[k] = v;
       }
 #pragma unroll
-      for (int bb = 0; bb < KG_B; ++bb) {
+      for (int bb = 0; bb < KGO; ++bb) {
         if (bb < nb) {
-          double diff[MAXD];
           double d2 = 0.0;
 #pragma unroll
           for (int k = 0; k < MAXD; ++k) {
             if (k < d) {
-              const double il = il_s[bb][k];
-              const double df = (x2[k] - x1[k]) * il;
-              diff[k] = df * il;  // (x2 - x1)/ls^2
+              const double df = (x2[k] - x1[k]) * il_s[bb][k];
               d2 = fma(df, df, d2);
             }
           }
           const double sgl = g[bb] * os_s[bb] * kernel_dscale(kind_of(kind, b0 + bb), d2);
 #pragma unroll
           for (int k = 0; k < MAXD; ++k)
-            if (k < d) acc[k] = fma(sgl, diff[k], acc[k]);
+            if (k < d) {
+              const double il = il_s[bb][k];
+              acc[k] = fma(sgl, ((x2[k] - x1[k]) * il) * il, acc[k]);   // (x2 - x1)/ls^2
+            }
         }
       }
     }

@@ -38,6 +38,7 @@ int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 bool qs_applies(const evr_qnehvi_state* st, int b, int d);
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
+unsigned int* qs_counters(const evr_qnehvi_state* st, int b, int d, double* dXp);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
 int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
@@ -130,31 +131,11 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
-  unsigned int* counter;         // blocks-done counter of the fused copy-out, then (u64 at byte
-                                 // 8) the last sequence number the host graph served (device)
+  unsigned int* counter;         // device scratch words of the host graph (zeroed at setup)
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
-  int armed;                     // a host-graph launch is queued, waiting for the next x
 };
 
 namespace evr {
-
-// Head of the host graph: the chain waits on the device until the host publishes its next
-// evaluation (the sequence number at hx[n] beyond the last one served), so the graph can be
-// launched before the host has x — evr_qnehvi_plan_minimize queues the next evaluation as
-// soon as one completes, and the launch overlaps its L-BFGS-B step.  One lane polls the pinned
-// word with system-scope loads and s_sleep backoff; a wait beyond 1 s (an abandoned plan)
-// ends on its own instead of holding the queue.
-__global__ void plan_wait_kernel(const unsigned long long* seqp, unsigned long long* wseq) {
-  if (threadIdx.x != 0) return;
-  const unsigned long long last = __hip_atomic_load(wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t0 = wall_clock64();
-  unsigned long long v;
-  while ((v = __hip_atomic_load(seqp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) <= last) {
-    if (wall_clock64() - t0 > 100000000ull) break;   // 1 s at the 100 MHz constant clock
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (v > last) __hip_atomic_store(wseq, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // acq and dX to the host buffer, then (after every thread's system-scope fence) the
 // evaluation's sequence number into the completion word the host spins on
@@ -253,17 +234,6 @@ struct PlanHostRes {
   hipGraph_t graph;
 };
 static std::mutex g_hres_mu;
-// queued evaluations (plan_wait_kernel at the head of the host graph), opt-in with
-// EVR_PRELAUNCH=1: measured within noise of launching each evaluation once its x is published
-// (≈ 110 µs per evaluation either way, profiles/r03/v), so the default graph has no waiting
-// kernel
-static bool prelaunch_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("EVR_PRELAUNCH");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 static std::vector<PlanHostRes> g_hres;
 static bool graph_reuse() {
   static const bool on = [] {
@@ -306,7 +276,6 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->hexec = nullptr;
   p->seq = 0;
   p->counter = nullptr;
-  p->armed = 0;
   if (int rc = gemm_backend_init()) {
     delete p;
     return rc;
@@ -316,7 +285,14 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   // pays for a capture and an instantiation)
   p->use_graph = use_graph ? 1 : 0;
   p->nrun = 0;
-  (void)stream;
+  if (p->backward && p->L.small) {
+    // the backward tail's blocks-done counters: zero once, every launch leaves them at zero
+    unsigned int* cnt = qs_counters(st, b, md->d, (double*)(p->work + p->L.dxp));
+    if (hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) {
+      delete p;
+      EVR_CHECK(false, "evr_qnehvi_plan_create: counter reset failed");
+    }
+  }
   *out = p;
   return 0;
 }
@@ -419,8 +395,6 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
     // writes the results and the completion word itself, other chains end in plan_copy_out
     int done = 0;
-    if (prelaunch_on())
-      plan_wait_kernel<<<1, 64, 0, cs>>>((const unsigned long long*)(dhx + n), (unsigned long long*)(p->counter + 2));
     rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
   }
@@ -459,8 +433,7 @@ static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
   const unsigned long long seq = ++p->seq;
   std::memcpy(p->hx + n, &seq, sizeof(seq));
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (!p->armed) EVR_HIP(hipGraphLaunch(p->hexec, s));   // else queued already, waiting for this seq
-  p->armed = 0;
+  EVR_HIP(hipGraphLaunch(p->hexec, s));
   // spin on the completion word; every 256 polls ask the stream whether it has drained (a
   // faulted or failed launch ends the wait with its error instead of spinning forever)
   volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
@@ -516,35 +489,15 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   }();
   double t_step = 0.0, t_eval = 0.0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  const bool prelaunch = prelaunch_on();
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;
   int task = opt.start(x0), nit = 0, nfev = 0, status = 0;
-  // the next evaluation's graph is queued while the host works out its x (every queued launch
-  // is consumed: by the next function evaluation or by the final re-evaluation below)
-  auto arm = [&]() -> int {
-    if (!prelaunch || p->armed) return 0;
-    if (int rc = plan_host_setup(p)) return rc;
-    EVR_HIP(hipGraphLaunch(p->hexec, s));
-    p->armed = 1;
-    return 0;
-  };
-  auto drain = [&](int rc) {   // an error with a queued launch: release it with the current x
-    if (p->armed) {
-      double fd = 0.0;
-      std::vector<double> gd(n);
-      (void)plan_eval_host(s, p, opt.x(), &fd, gd.data());
-    }
-    return rc;
-  };
-  if (int rc = arm()) return rc;
   // scipy's _minimize_lbfgsb driver loop
   for (;;) {
     if (task == LBFGSB_FG) {
       double t0 = stats ? now() : 0.0;
-      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return drain(rc);
-      if (int rc = arm()) return rc;
+      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
       double t1 = stats ? now() : 0.0;
       ++nfev;
       task = opt.step(f, g.data());

@@ -692,9 +692,11 @@ def optimize_acqf_mixed(acqf, bounds: np.ndarray, fixed_features_list: Sequence[
                          "(BotorchStrategy._ask_mixed_sequential)")
     stats = OptimizeStats()
     best = (None, -np.inf)
+    stats.mixed_values = []
     for ff in fixed_features_list:
         x, v, stats = optimize_acqf(acqf, bounds, num_restarts, raw_samples, options, gen, inequality_constraints,
                                     equality_constraints, dist=dist, stats=stats, fixed_features=ff)
+        stats.mixed_values.append(float(v))     # each combination's optimum, in combination order
         if best[0] is None or v > best[1]:
             best = (x, v)
     return best[0], best[1], stats

@@ -687,6 +687,7 @@ class SoboStrategy(BotorchStrategy):
     def __init__(self, data_model, dist=None, **kwargs):
         super().__init__(data_model, dist=dist)
         self.acquisition_function = data_model.acquisition_function
+        self.last_acqf = None
 
     def _get_acqfs(self, n):
         if not isinstance(self.acquisition_function, dm.qEI):
@@ -699,9 +700,12 @@ class SoboStrategy(BotorchStrategy):
         seed = int(torch.randint(0, 1000000, (1,), generator=self.gen).item())
         S = int(self.acquisition_function.n_mc_samples)
         if X_pending is None and n == 1:
-            return [QEI(self.model, X_train, a, b, S=S, seed=seed)]
-        # joint batches (q > 1) and pending points (sobo.py:72 passes X_pending)
-        return [QEIJoint(self.model, X_train, a, b, S=S, seed=seed, X_pending_raw=X_pending)]
+            acqf = QEI(self.model, X_train, a, b, S=S, seed=seed)
+        else:
+            # joint batches (q > 1) and pending points (sobo.py:72 passes X_pending)
+            acqf = QEIJoint(self.model, X_train, a, b, S=S, seed=seed, X_pending_raw=X_pending)
+        self.last_acqf = acqf
+        return [acqf]
 
 
 STRATEGY_MAP = {

@@ -40,12 +40,23 @@ def test_categorical_ask(method):
     c = s.ask(1)
     assert c["c0"].iloc[0] in ("a", "b", "c") and c["c1"].iloc[0] in ("u", "w")   # never the forbidden one
     if method == "EXHAUSTIVE":
-        # the winner is the best of the per-combination optima
-        acqf = s._get_acqfs(1)[0]
+        st = s.last_ask_stats
         X = torch.as_tensor(s._transform(c), dtype=torch.float64, device="cuda")
         Xt = X.cpu().numpy()[0]
         assert set(np.unique(Xt[2:])) <= {0.0, 1.0}                  # exact one-hot
-        assert s.last_ask_stats.raw_evals == 6 * 64
+        assert st.raw_evals == 6 * 64
+        # the winner is the best of the per-combination optima (the first on ties) ...
+        vals = st.mixed_values
+        assert len(vals) == 6 and st.best_value == max(vals)
+        k = int(np.argmax(vals))
+        assert all(v < vals[k] for v in vals[:k])
+        # ... and it carries the winning combination's one-hot columns
+        assert np.array_equal(Xt[2:], np.asarray([combos[k][j] for j in sorted(combos[k])]))
+        # re-evaluated on the ask's acquisition it gives the optimum it was selected with
+        acqf = s.last_acqf if getattr(s, "last_acqf", None) is not None else None
+        if acqf is not None:
+            v = float(acqf.forward(X).cpu()[0])
+            assert abs(v - st.best_value) <= 1e-9 * max(1.0, abs(v))
 
 
 def test_exhaustive_batch_is_sequential_greedy():

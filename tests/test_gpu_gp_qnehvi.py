@@ -32,6 +32,36 @@ def test_posterior_parity(kind, n, d, m):
             assert torch.allclose(var[j].cpu(), rv, rtol=1e-7, atol=1e-10 * ost[j].y_std ** 2)
 
 
+def test_config2_posterior_1024_sobol_points():
+    """BASELINE configs[1]: SingleTaskGP RBF, n_train = 256, d = 6,
+    X_train ~ U[0,1]^6 (default_rng(0)), y = DTLZ2(6, 5)'s first objective; hyperparameters
+    fitted once (device fit, the reference's fit_gpytorch_mll restatement) and then frozen in
+    both models; 1024 scrambled Sobol test points (seed 1).  Mean and variance against the
+    oracle posterior (north star: 1e-4 relative; asserted 1e-9 / 1e-7)."""
+    from everest_amd.gp import GPBatch, fit_single
+
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(256, 6))
+    from tests.helpers import dtlz2
+    y = dtlz2(X, 5)[:, 0]
+    dev = torch.device("cuda")
+    Xn = torch.tensor(X, device=dev)
+    prior = ogp.dim_scaled_lognormal(6)
+    h = fit_single(Xn, y, 0, prior, (-4.0, 1.0))
+    gp = GPBatch(Xn, torch.tensor(y[:, None], device=dev), [h], 0, torch.zeros(6, device=dev, dtype=torch.float64),
+                 torch.ones(6, device=dev, dtype=torch.float64))
+    st = ogp.GPState(X=torch.tensor(X), y=torch.tensor((y - h.y_mean) / h.y_std), lengthscale=torch.tensor(h.lengthscale),
+                     noise=h.noise, constant=h.constant, y_mean=h.y_mean, y_std=h.y_std, kind=ogp.RBF)
+    Xs = torch.quasirandom.SobolEngine(6, scramble=True, seed=1).draw(1024, dtype=torch.float64)
+    for obs in (False, True):
+        mean, var = gp.posterior(Xs.to(dev), observation_noise=obs)
+        rm, rv = ogp.posterior(st, Xs, observation_noise=obs)
+        assert torch.allclose(mean[0].cpu(), rm, rtol=1e-9, atol=1e-9 * h.y_std)
+        assert torch.allclose(var[0].cpu(), rv, rtol=1e-7, atol=1e-10 * h.y_std ** 2)
+        sm, sv = ogp.posterior_scipy(st, Xs, observation_noise=obs)    # independent oracle check
+        assert np.allclose(rm.numpy(), sm, rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("kind", [0, 3])
 def test_mll_value_and_grad(kind):
     from everest_amd.gp import MLLEvaluator

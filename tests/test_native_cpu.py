@@ -181,3 +181,32 @@ def test_approximate_partition_m2_is_exact_and_alpha_bounds():
     with pytest.raises(RuntimeError, match="bad arguments"):
         ops.box_decompose(obj, ref, None, 1, layout="sij", alpha=-0.1)
     assert hasattr(_native.load(), "evr_box_decompose_approx")
+
+
+def test_evaluation_chain_kernels_use_no_scratch():
+    """Register spills / dynamically indexed private arrays land in scratch memory, whose
+    traffic goes through L2 and HBM on every launch (hvi_kdb<5> wrote ~58 MB of scratch per
+    launch before round 4).  The code-object metadata of the built library must show zero
+    private-segment bytes for the restart chain, the evaluation pass, the fit and the
+    construction kernels at the configs' shapes (m <= 5 objectives, d <= 32 inputs)."""
+    import re
+    import shutil
+    import sys
+
+    if not shutil.which("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("ROCm llvm tools not installed")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import kernel_resources as kr
+
+    ks = kr.kernels(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "everest_amd", "_lib",
+                                 "libeverest_amd.so"))
+    names = dict(zip(kr.demangle(sorted(ks)), [ks[k] for k in sorted(ks)]))
+    hot = re.compile(r"evr::(qs_fwd|qs_bwd|hvi_kdb<[1-5]>|hvi_kd2<[1-5],|hvi_kd3<[1-5]>|hvi_thresholds|"
+                     r"hvi_reduce|kmat_kernel|kmat_mfma_kernel|qn_samples_norms|qn_proj|qn_gen_gr|qn_bwd_coef|"
+                     r"qn_mean_row|qn_norms_rows|kcross_grad_kernel<(8|16|32)>|kls_grad_kernel|chol_|tri_inv|"
+                     r"trsm16|pareto_f32_kernel<[1-5]>|bd_build_kernel<[1-5],|cells_kd_kernel<[1-5]>|"
+                     r"sobol|mll_|posterior_finalize|hvi_logk_kernel<[1-5], (true|false), 2|hvi_log_reduce)")
+    checked = {k: v for k, v in names.items() if hot.search(k)}
+    assert len(checked) > 40, sorted(checked)
+    spill = {k: v.get("scratch") for k, v in checked.items() if v.get("scratch")}
+    assert not spill, spill

@@ -1,0 +1,95 @@
+"""Per-kernel resources of the built gfx950 library: VGPRs, SGPRs, LDS, scratch (private
+segment) bytes per lane, read from the AMDGPU code-object metadata in the library's
+.hip_fatbin section (clang offload bundles -> llvm-readelf --notes).
+
+A kernel with private_segment_fixed_size > 0 spills registers (or keeps a dynamically
+indexed private array) in scratch memory: every lane's spill traffic goes through L2 / HBM
+(hvi_kdb<5> wrote ~58 MB of scratch per launch before round 4 — its WRITE_SIZE counter).
+tests/test_native_cpu.py asserts the evaluation chain's kernels stay at zero.
+
+usage: python tools/kernel_resources.py [lib.so] [--scratch-only]   (one JSON object per line)"""
+import json
+import os
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_objects(lib: str, arch: str = "gfx950"):
+    with tempfile.TemporaryDirectory() as td:
+        fb = os.path.join(td, "fatbin.bin")
+        subprocess.run([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", lib,
+                        os.path.join(td, "stripped.so")], check=True, capture_output=True)
+        data = open(fb, "rb").read()
+    pos = 0
+    while True:
+        j = data.find(MAGIC, pos)
+        if j < 0:
+            break
+        ne = struct.unpack_from("<Q", data, j + 24)[0]
+        p = j + 32
+        for _ in range(ne):
+            off, size, il = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            tid = data[p:p + il].decode(errors="replace")
+            p += il
+            if arch in tid:
+                yield data[j + off:j + off + size]
+        pos = j + 1
+
+
+def kernels(lib: str):
+    """{kernel symbol: {vgpr, sgpr, lds, scratch}} over every gfx950 code object."""
+    out = {}
+    for co in code_objects(lib):
+        with tempfile.NamedTemporaryFile(suffix=".o") as f:
+            f.write(co)
+            f.flush()
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f.name], check=True,
+                                   capture_output=True, text=True).stdout
+        cur = None
+        for line in notes.splitlines():
+            m = re.match(r"\s*(?:- )?\.(\w+):\s+(\S+)", line)
+            if not m:
+                continue
+            k, v = m.groups()
+            if k == "name" and not v.endswith(".kd"):
+                cur = out.setdefault(v, {})
+            elif cur is not None and k in ("vgpr_count", "sgpr_count", "group_segment_fixed_size",
+                                           "private_segment_fixed_size", "agpr_count"):
+                key = {"group_segment_fixed_size": "lds", "private_segment_fixed_size": "scratch"}.get(k, k)
+                cur[key] = int(v)
+    return out
+
+
+def demangle(names):
+    for tool in (os.path.join(LLVM, "llvm-cxxfilt"), "c++filt"):
+        try:
+            r = subprocess.run([tool], input="\n".join(names), capture_output=True, text=True)
+        except OSError:
+            continue
+        if r.returncode == 0:
+            return r.stdout.splitlines()
+    return list(names)
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    lib = args[0] if args else os.path.join(ROOT, "everest_amd", "_lib", "libeverest_amd.so")
+    ks = kernels(lib)
+    names = sorted(ks)
+    for raw, pretty in zip(names, demangle(names)):
+        r = ks[raw]
+        if "--scratch-only" in sys.argv and not r.get("scratch"):
+            continue
+        print(json.dumps({"kernel": pretty, **r}))
+
+
+if __name__ == "__main__":
+    main()
