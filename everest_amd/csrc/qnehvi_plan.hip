@@ -38,7 +38,6 @@ int samples_norms(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 bool qs_applies(const evr_qnehvi_state* st, int b, int d);
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
-unsigned int* qs_counters(const evr_qnehvi_state* st, int b, int d, double* dXp);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
 int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
@@ -131,7 +130,7 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
-  unsigned int* counter;         // device scratch words of the host graph (zeroed at setup)
+  unsigned int* counter;         // blocks-done counter of the fused copy-out (qs_dx_reduce)
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
 };
 
@@ -285,14 +284,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   // pays for a capture and an instantiation)
   p->use_graph = use_graph ? 1 : 0;
   p->nrun = 0;
-  if (p->backward && p->L.small) {
-    // the backward tail's blocks-done counters: zero once, every launch leaves them at zero
-    unsigned int* cnt = qs_counters(st, b, md->d, (double*)(p->work + p->L.dxp));
-    if (hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) {
-      delete p;
-      EVR_CHECK(false, "evr_qnehvi_plan_create: counter reset failed");
-    }
-  }
+  (void)stream;
   *out = p;
   return 0;
 }

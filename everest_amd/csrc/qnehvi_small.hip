@@ -17,9 +17,7 @@
 //            over the S samples in a fixed order), gR generated in the B fetch from R, dG and
 //            the coefficients, dK_x = M_j^T gR by MFMA, and in the epilogue the cross-
 //            covariance gradient of the tile's 16 training rows (dK_x never reaches HBM).
-//            The partials of dX are summed by the grid's own tail (blocks-done counters): the
-//            last workgroup of each output sums that output's partials, the last of those
-//            forms dX, acq and the host outputs — no separate reduction launch.
+//   qs_dx_reduce: dX = sum over the (output, tile) partials in a fixed order.
 // Every reduction order is fixed: results are bitwise reproducible.
 #include <algorithm>
 
@@ -277,24 +275,6 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
 // with coalesced row segments, the coefficients applied while staging in LDS.
 // ---------------------------------------------------------------------------------------
 constexpr int QS_RC = 128;   // rows of M per backward chunk
-
-// The backward's tail (run by its last workgroup): dX from the per-output sums, acq (the mean
-// over the samples of the fused scan's per-sample values, NaN where the new-point Cholesky
-// failed) and, in host mode, acq / dX into the plan's pinned buffer followed by the
-// evaluation's sequence number as the completion word the host spins on.
-struct QsFinal {
-  double* dXj;              // m x (b d): per-output sums of the partials
-  unsigned int* cnt;        // m + 1 blocks-done counters (each reset by its last workgroup)
-  const double* scale;      // input normalisation scale (dX in raw units)
-  double* dX;
-  double* acq;
-  double* hout;             // pinned host buffer or nullptr
-  const double* seqp;
-  const double* sval;       // S x b per-sample values (fused scan) or nullptr (acq given)
-  const int* flags;
-  int S;
-};
-constexpr int QS_CNT = 16;   // counter words reserved after the partials (m + 1 <= 16)
 __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
                                               const double* __restrict__ M, const double* __restrict__ R,
                                               const double* __restrict__ dG, const double* __restrict__ L22,
@@ -302,7 +282,7 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
                                               const double* __restrict__ oa, const double* __restrict__ Xn,
                                               const double* __restrict__ X, const double* __restrict__ shift,
                                               const double* __restrict__ scale, const double* __restrict__ ls,
-                                              double* __restrict__ dXp, int ntile, int rows_per, QsFinal fin) {
+                                              double* __restrict__ dXp, int ntile, int rows_per) {
   __shared__ double cf[3][QS_B];
   __shared__ double red[8][QS_B][2];
   // the chunk tiles and the epilogue's reduction buffers share one LDS region (~53 KB per
@@ -482,77 +462,84 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
       if (cc < b && k < d) dXp[((size_t)cc * d + k) * np + ((size_t)j * gridDim.z + z) * ntile + tile] = v;
     }
   }
-  // 4. blocks-done chain: the last workgroup of output j sums the output's partials in (z,
-  //    tile) order; the last of the outputs' last workgroups finishes the evaluation
-  __shared__ int last;
-  __syncthreads();
-  const int per_j = gridDim.z * ntile;
-  if (tid == 0) {
-    __threadfence();
-    last = atomicAdd(fin.cnt + j, 1u) == (unsigned int)(per_j - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  const size_t np = (size_t)gridDim.y * per_j;
-  const int nel = b * d;
-  for (int e = tid; e < nel; e += 256) {
-    const double* src = dXp + (size_t)e * np + (size_t)j * per_j;
-    double v = 0.0;
-#pragma unroll 8
-    for (int p = 0; p < per_j; ++p) v += src[p];
-    fin.dXj[(size_t)j * nel + e] = v;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    fin.cnt[j] = 0u;
-    __threadfence();
-    last = atomicAdd(fin.cnt + gridDim.y, 1u) == (unsigned int)(gridDim.y - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (tid == 0) fin.cnt[gridDim.y] = 0u;
-  // acq: per candidate the S samples in 8 strided groups, the groups summed in order
-  {
-    const int c = tid & (QS_B - 1), g = tid >> 5;
-    double a = 0.0;
-    if (fin.sval && c < b)
-      for (int s = g; s < fin.S; s += 8) a += fin.sval[(size_t)s * b + c];
-    red[g][c][0] = a;
-  }
-  __syncthreads();
-  if (tid < b) {
-    // acq: formed here from the fused scan's per-sample values, or (host mode) the value an
-    // earlier kernel of the chain wrote; the op-by-op path has neither (acq == nullptr)
-    if (fin.sval) {
-      double a = red[0][tid][0];
+}
+
+// one wave per dX element (4 per workgroup): lane-strided partial sums over the element's
+// contiguous partials, then a fixed xor-butterfly.  Host mode (hout != nullptr, the plan's host
+// graph): every wave also writes its dX element (and the first b acq) to the pinned host
+// buffer; after a system-scope fence each workgroup counts itself done, and the last one
+// resets the counter and writes the evaluation's sequence number into the completion word the
+// host spins on (no separate copy-out kernel).
+//
+// With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the waves of
+// the first b elements also form acq[c] = mean over the S samples (lane-strided, then the
+// butterfly; NaN for a candidate whose new-point Cholesky failed) and write it to acq.
+__global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
+                                                    const double* __restrict__ scale, double* __restrict__ dX,
+                                                    double* __restrict__ acq, double* hout,
+                                                    const double* seqp, unsigned int* counter,
+                                                    const double* __restrict__ sval, int S, int m,
+                                                    const int* __restrict__ flags) {
+  const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const bool ein = e < b * d;
+  const int k = e % d;
+  double av = 0.0;
+  if (ein && sval && e < b) {
+    double x[4];
 #pragma unroll
-      for (int g = 1; g < 8; ++g) a += red[g][tid][0];
-      bool bad = false;
-      if (fin.flags)
-        for (int jj = 0; jj < m; ++jj) bad |= fin.flags[(size_t)jj * b + tid] != 0;
-      const double av = bad ? nan("") : a / (double)fin.S;
-      if (fin.acq) fin.acq[tid] = av;
-      if (fin.hout) fin.hout[tid] = av;
-    } else if (fin.hout && fin.acq) {
-      fin.hout[tid] = fin.acq[tid];
+    for (int u = 0; u < 4; ++u) {
+      const int s = lane + 64 * u;
+      x[u] = s < S ? sval[(size_t)s * b + e] : 0.0;
+    }
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < S) a += x[u];
+    for (int s = lane + 256; s < S; s += 64) a += sval[(size_t)s * b + e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    bool bad = false;
+    if (flags)
+      for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + e] != 0;
+    av = bad ? nan("") : a / (double)S;
+    if (lane == 0) acq[e] = av;
+  }
+  // the lane's first 8 partials (contiguous over the wave) loaded together, then summed in the
+  // loop's order
+  const double* src = dXp + (size_t)(ein ? e : 0) * np;
+  double x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int p = lane + 64 * u;
+    x[u] = (ein && p < np) ? src[p] : 0.0;
+  }
+  double v = 0.0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (lane + 64 * u < np) v += x[u];
+  if (ein)
+    for (int p = lane + 512; p < np; p += 64) v += src[p];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0 && ein) {
+    const double r = v * (scale ? scale[k] : 1.0);
+    dX[e] = r;
+    if (hout) {
+      hout[b + e] = r;
+      if (e < b) hout[e] = sval ? av : acq[e];
+      __threadfence_system();
     }
   }
-  for (int e = tid; e < nel; e += 256) {
-    double v = fin.dXj[e];
-    for (int jj = 1; jj < m; ++jj) v += fin.dXj[(size_t)jj * nel + e];
-    const double r = v * (fin.scale ? fin.scale[e % d] : 1.0);
-    fin.dX[e] = r;
-    if (fin.hout) fin.hout[b + e] = r;
-  }
-  if (fin.hout) {
-    __threadfence_system();
+  if (hout) {
     __syncthreads();
-    if (tid == 0) {
-      const unsigned long long seq = *(volatile const unsigned long long*)fin.seqp;
-      __threadfence_system();
-      *(volatile unsigned long long*)(fin.hout + b + (size_t)b * d) = seq;
+    if (threadIdx.x == 0) {
+      const unsigned int prev = atomicAdd(counter, 1u);
+      if (prev == gridDim.x - 1) {
+        atomicExch(counter, 0u);
+        const unsigned long long seq = *(volatile const unsigned long long*)seqp;
+        __threadfence_system();
+        *(volatile unsigned long long*)(hout + b + (size_t)b * d) = seq;
+      }
     }
   }
 }
@@ -577,15 +564,8 @@ static int qs_rows_per(const evr_qnehvi_state* st) {
   return cdiv(nch, qs_zsplit(st)) * QS_RC;
 }
 
-// partials (m x zs x tiles per dX element), the per-output sums, then QS_CNT counter words
-static size_t qs_partials_doubles(const evr_qnehvi_state* st, int b, int d) {
-  return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
-}
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
-  return qs_partials_doubles(st, b, d) + (size_t)st->m * b * d + QS_CNT / 2;
-}
-unsigned int* qs_counters(const evr_qnehvi_state* st, int b, int d, double* dXp) {
-  return (unsigned int*)(dXp + qs_partials_doubles(st, b, d) + (size_t)st->m * b * d);
+  return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
 }
 
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
@@ -620,13 +600,12 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
-  EVR_CHECK(st->m + 1 <= QS_CNT, "qs_backward: %d outputs exceed the counter words", st->m);
-  (void)counter;   // the completion word follows the tail's system-scope fences (no count needed)
-  QsFinal fin{dXp + qs_partials_doubles(st, b, d), qs_counters(st, b, d, dXp), md->scale, dX, acq, hout, seqp,
-              sval, flags, st->S};
   qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
-                                            md->lengthscales, dXp, nt, rows_per, fin);
+                                            md->lengthscales, dXp, nt, rows_per);
+  EVR_LAUNCH_CHECK();
+  qs_dx_reduce<<<cdiv(b * d, 4), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter,
+                                               sval, st->S, st->m, flags);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -673,8 +652,6 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
                               double* dX) {
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
-  // the blocks-done counters of the tail (a plan zeroes them once; they reset themselves)
-  EVR_HIP(hipMemsetAsync(qs_counters(st, b, md->d, dXp), 0, QS_CNT * sizeof(unsigned int), (hipStream_t)stream));
   return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr,
                      nullptr, nullptr);
 }

@@ -134,10 +134,15 @@ def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
         ref.sum().backward()
         assert torch.isfinite(acq).all() and torch.isfinite(ref).all()
         a = acq.cpu()[sub]
+        r = ref.detach()
         # log values: an absolute error e in log space is a relative error e in the HVI itself,
-        # so the bar is the BASELINE-size qNEHVI one (1e-6 relative; the L22^2 cancellation
-        # near training points costs digits at n = 512, measured 2.4e-7)
-        assert torch.allclose(a, ref.detach(), rtol=0, atol=1e-6), (b, (a - ref.detach()).abs().max())
+        # so the bar is the BASELINE-size qNEHVI one: 1e-6 relative (the L22^2 cancellation
+        # near training points costs digits at n = 512); the linear test's absolute floor
+        # (1e-10) has no log-space counterpart, so improvements below e^-25 ~ 1e-11 — whose
+        # relative rounding grows as the HVI shrinks — get 1e-4 (north star: 1e-3)
+        tol = torch.where(r > -25.0, torch.full_like(r, 1e-6), torch.full_like(r, 1e-4))
+        err = (a - r).abs()
+        assert (err <= tol).all(), (b, [(float(x), float(y)) for x, y, bad in zip(a, r, err > tol) if bad])
         g = dX.cpu()[sub]
         assert torch.allclose(g, xt.grad, rtol=1e-5, atol=1e-7 * xt.grad.abs().max()), (b, (g - xt.grad).abs().max())
 
