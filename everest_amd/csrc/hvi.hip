@@ -2052,6 +2052,219 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// hvi_kdw — the restart-batch scan with one wave per (sample, candidate) and nothing shared
+// between the waves but the sample's point table (staged in LDS once per workgroup of
+// KW_WAVES candidates).  Per wave:
+//   y_j of the candidate (G, or the sampling step fused in: KbSamples);
+//   thresholds t_j = #{rows with lower-bound value <= y_j} by two wave-wide probes of the
+//     sample's ascending values (64 bucket ends, then the 64 entries of the straddling
+//     bucket) instead of a 9-step binary search;
+//   the sample's groups in chunks of 64, one per lane: group test, and for a passing group
+//     its 16 cell tests (the group's rank rows) -> cell mask; the passing cells' key indices
+//     appended to the wave's term list in (group, cell) order by a wave scan;
+//   terms in rounds of 64, term t of the candidate on lane t % 64: key decoded against the
+//     LDS point table, the term and its subgradients (hvi_kdb's arithmetic) summed per lane
+//     in t order; then one fixed xor-butterfly per value.
+// No workgroup barrier after the staging and no inter-wave order: a candidate's value and
+// gradient depend on its own term sequence only, so they are bitwise the same in any batch
+// (a restart batch sharded over ranks evaluates each candidate exactly as one rank does) and
+// bitwise reproducible.  Equal to hvi_kdb to rounding (different summation order).
+// Workgroup w runs on XCD w % 8: the candidate groups of a sample share one XCD's L2.
+// ---------------------------------------------------------------------------------------
+constexpr int KW_WAVES = 4;
+constexpr int KW_TCAP = 64 * 16 + 64;   // one 64-group chunk's terms + a partial round
+
+__host__ __device__ inline size_t kw_pt_bytes(int stride, int M) { return ((size_t)stride * M * 8 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t kw_lds_bytes(int stride, int M) {
+  return kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4;
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const double* __restrict__ G, HviKd kd,
+                                               KbSamples smp, double* __restrict__ sval, double* __restrict__ dG) {
+  constexpr int NV = M + 1;
+  using K = CellKey<M>;
+  extern __shared__ __align__(16) unsigned char kw_dyn[];
+  const int wid = blockIdx.x, xcd = wid & 7, slot = wid >> 3;
+  const int s = (slot / ncg) * 8 + xcd, cg = slot - (slot / ncg) * ncg;
+  if (s >= S) return;   // the grid covers S rounded up to 8 samples: whole workgroups leave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int stride = kd.stride;
+  double* pt = (double*)kw_dyn;
+  unsigned int* tl = (unsigned int*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
+  {
+    const double* src = kd.pts + (size_t)s * stride * M;
+    for (int e = tid; e < stride * M; e += 256) pt[e] = src[e];
+  }
+  __syncthreads();
+  const int c = cg * KW_WAVES + wave;
+  if (c >= b) return;
+
+  // ---- y_j (lane j < M), then to every lane ----
+  double yl = 0.0;
+  if (lane < M) {
+    const int j = lane;
+    if (smp.R) {
+      const long long Rr = (long long)smp.n + smp.nb + smp.nh + 1;
+      const double* Rj = smp.R + (size_t)j * Rr * b;
+      const double hv = smp.nh ? Rj[(size_t)(smp.n + smp.nb + s) * b + c] : 0.0;
+      const double zv = smp.zq[(size_t)s * M + j];
+      double mu, l22;
+      int flag;
+      qn_mu_l22(smp.P + (size_t)j * smp.nrt * 2 * b, smp.nrt_used, b, c, Rj[(size_t)(Rr - 1) * b + c], smp.ys[j],
+                smp.cc[j], smp.ym[j], smp.kxx[j], mu, l22, flag);
+      if (s == 0) {
+        smp.L22[(size_t)j * b + c] = l22;
+        smp.flags[(size_t)j * b + c] = flag;
+      }
+      yl = qn_sample_obj(mu, hv, smp.nh != 0, l22, zv, smp.oa[j], smp.ob[j]);
+    } else {
+      yl = G[((size_t)s * M + j) * b + c];
+    }
+  }
+  double y[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) y[j] = __shfl(yl, j, 64);
+
+  // ---- thresholds: two wave-wide probes per objective ----
+  unsigned int tw[4] = {0x00010001u, 0x00010001u, 0x00010001u, 0x00010001u};   // t = 1 beyond M (as kdb)
+  {
+    const double* tv = kd.sv + (size_t)s * M * stride;
+    const int B1 = (stride + 63) >> 6;
+    const int i1 = min((lane + 1) * B1, stride) - 1;
+    double v1[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) v1[j] = tv[(size_t)j * stride + i1];
+    int base[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) base[j] = min(__popcll(__ballot(v1[j] <= y[j])) * B1, stride);
+    double v2[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int i2 = base[j] + lane;
+      v2[j] = (lane < B1 && i2 < stride) ? tv[(size_t)j * stride + i2] : INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const unsigned int t = (unsigned int)(base[j] + __popcll(__ballot(lane < B1 && v2[j] <= y[j])));
+      const int sh = 16 * (j & 1);
+      tw[j >> 1] = (tw[j >> 1] & ~(0xFFFFu << sh)) | (t << sh);
+    }
+  }
+  const uint4 tt = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+
+  // ---- groups in chunks of 64 -> term list -> rounds of 64 terms ----
+  const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  auto term_add = [&](const unsigned long long key) {
+    double l[M], u[M];
+    K::decode_direct(key, pt, l, u);
+    double len[M], pass[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const double raw = fmin(y[j], u[j]) - l[j];
+      len[j] = fmax(raw, 0.0);
+      const double dmin = (y[j] < u[j]) ? 1.0 : ((y[j] == u[j]) ? 0.5 : 0.0);
+      pass[j] = (raw >= 0.0) ? dmin : 0.0;
+    }
+    double pre_[M];
+    pre_[0] = 1.0;
+#pragma unroll
+    for (int j = 1; j < M; ++j) pre_[j] = pre_[j - 1] * len[j - 1];
+    acc[0] += pre_[M - 1] * len[M - 1];
+    double suf = 1.0;
+#pragma unroll
+    for (int j = M - 1; j >= 0; --j) {
+      acc[1 + j] += pass[j] * pre_[j] * suf;
+      suf *= len[j];
+    }
+  };
+  // evaluate terms [0, nr * 64) of the list (nr full rounds) or, with part, one partial round
+  auto rounds = [&](const int nr, const int part) {
+    const int last = part > 0 ? nr : nr - 1;   // index of the final round
+    if (last < 0) return;
+    auto ld = [&](const int r) -> unsigned long long {
+      const int t = r * 64 + lane;
+      const bool in = r < nr || lane < part;
+      return in ? kd.gkeys[tl[t]] : 0ull;
+    };
+    unsigned long long kc = ld(0);
+    for (int r = 0; r <= last; ++r) {
+      const unsigned long long kn = r < last ? ld(r + 1) : 0ull;   // the next round's key in flight
+      if (r < nr || lane < part) term_add(kc);
+      kc = kn;
+    }
+  };
+  int tn = 0;   // terms in the list (wave-uniform)
+  for (int g0 = 0; g0 < Gs; g0 += 64) {
+    const int g = g0 + lane;
+    unsigned int mB = 0;
+    if (g < Gs && kd_pass4(gmin[g], tt)) {
+      const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
+      unsigned int a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = 0xFFFFFFFFu;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+        const unsigned int t2 = th16 | (th16 << 16);
+        const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+        a[0] &= kd_lt16(r1.x, t2);
+        a[1] &= kd_lt16(r1.y, t2);
+        a[2] &= kd_lt16(r1.z, t2);
+        a[3] &= kd_lt16(r1.w, t2);
+        a[4] &= kd_lt16(r2.x, t2);
+        a[5] &= kd_lt16(r2.y, t2);
+        a[6] &= kd_lt16(r2.z, t2);
+        a[7] &= kd_lt16(r2.w, t2);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mB |= (((a[k] >> 15) & 1u) | ((a[k] >> 30) & 2u)) << (2 * k);
+    }
+    int tot;
+    int p = tn + wave_scan_excl(__popc(mB), &tot);
+    {
+      const unsigned int kb = (unsigned int)(gbase + g) * 16u;
+      unsigned int mk = mB;
+      while (mk) {
+        const int k = __ffs(mk) - 1;
+        mk &= mk - 1;
+        tl[p++] = kb + (unsigned int)k;
+      }
+    }
+    tn += tot;
+    wave_sync();
+    const int nr = tn >> 6;
+    if (nr > 0) {
+      rounds(nr, 0);
+      const int rem = tn - nr * 64;
+      const unsigned int keep = lane < rem ? tl[nr * 64 + lane] : 0u;
+      wave_sync();
+      if (lane < rem) tl[lane] = keep;
+      wave_sync();
+      tn = rem;
+    }
+  }
+  rounds(0, tn);
+  // ---- per value the lanes' sums, fixed butterfly ----
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double x = acc[v];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    acc[v] = x;
+  }
+  if (lane == 0) {
+    sval[(size_t)s * b + c] = acc[0];
+#pragma unroll
+    for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = 1.0 / (double)S * acc[1 + j];
+  }
+}
+
 // scan variant: 2 = hvi_kd2 (default), 1 = hvi_kd (EVR_KD=1 or evr_hvi_set_kd_variant)
 static int g_kd_variant = 0;
 static int kd_variant() {
@@ -2205,10 +2418,33 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
 static int g_restart_variant = 0;
 static int restart_variant() {
   if (g_restart_variant == 0) {
-    const char* e = std::getenv("EVR_KDB");
-    g_restart_variant = (e && e[0] == '0') ? 1 : 2;
+    // EVR_RESTART_SCAN=kdw (default) | kdb | kd3; the older EVR_KDB=0 still selects kd3
+    const char* e = std::getenv("EVR_RESTART_SCAN");
+    const char* k = std::getenv("EVR_KDB");
+    if (e && std::string(e) == "kdb") g_restart_variant = 2;
+    else if ((e && std::string(e) == "kd3") || (k && k[0] == '0')) g_restart_variant = 1;
+    else g_restart_variant = 3;
   }
   return g_restart_variant;
+}
+
+static bool hvi_kdw_applies(const evr_qnehvi_state* st, int b) {
+  if (restart_variant() != 3 || !st || st->log_hvi || !st->grp_off || b < 1 || b > 32 || kd_variant() != 2 ||
+      st->m < 1 || st->m > 8 || st->max_groups > 0xFFFF)
+    return false;
+  return kw_lds_bytes(st->pts_stride, st->m) <= 64 * 1024;
+}
+
+template <int M>
+static int hvi_kdw_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
+                          double* dG, const KbSamples& smp) {
+  const size_t lds = kw_lds_bytes(st->pts_stride, M);
+  const int ncg = cdiv(b, KW_WAVES);
+  const int wgs = cdiv(st->S, 8) * 8 * ncg;
+  EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdw<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hvi_kdw<M><<<wgs, 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG);
+  EVR_LAUNCH_CHECK();
+  return 0;
 }
 
 static bool hvi_kdb_applies(const evr_qnehvi_state* st, int b) {
@@ -2392,15 +2628,22 @@ int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, co
 }
 
 int evr_hvi_restart_fb_applies(const evr_qnehvi_state* st, int b) {
-  return (hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)) ? 1 : 0;
+  return (hvi_kdw_applies(st, b) || hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)) ? 1 : 0;
 }
 
 int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* sval,
                        double* dG) {
   if (int rc = hvi_check_state(st)) return rc;
-  EVR_CHECK(G && sval && dG && (hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)),
+  EVR_CHECK(G && sval && dG && (hvi_kdw_applies(st, b) || hvi_kdb_applies(st, b) || hvi_kd3_applies(st, b)),
             "evr_hvi_restart_fb: bad arguments or the state / batch is not a kd restart batch (b <= 32)");
   int rc = 0;
+  if (hvi_kdw_applies(st, b)) {
+    const KbSamples smp{};
+#define L(MM) rc = hvi_kdw_launch<MM>((hipStream_t)stream, st, b, G, sval, dG, smp)
+    EVR_M_SWITCH(st->m, L);
+#undef L
+    return rc;
+  }
   if (hvi_kdb_applies(st, b)) {
     const KbSamples smp{};
 #define L(MM) rc = hvi_kdb_launch<MM>((hipStream_t)stream, st, b, G, sval, dG, smp)
@@ -2424,7 +2667,7 @@ bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b) {
     const char* e = std::getenv("EVR_FUSED_SAMPLES");
     return !(e && e[0] == '0');
   }();
-  return on && hvi_kdb_applies(st, b) && st->obj_a && st->obj_b && st->zq;
+  return on && (hvi_kdw_applies(st, b) || hvi_kdb_applies(st, b)) && st->obj_a && st->obj_b && st->zq;
 }
 
 int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
@@ -2433,6 +2676,12 @@ int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double
   KbSamples smp{R, P, st->c, st->ym, st->ys, st->kxx, st->zq, st->obj_a, st->obj_b, L22, flags,
                 st->n, st->nb, qn_nh(st), nrt, nrt_used};
   int rc = 0;
+  if (hvi_kdw_applies(st, b)) {
+#define L(MM) rc = hvi_kdw_launch<MM>(s, st, b, nullptr, sval, dG, smp)
+    EVR_M_SWITCH(st->m, L);
+#undef L
+    return rc;
+  }
 #define L(MM) rc = hvi_kdb_launch<MM>(s, st, b, nullptr, sval, dG, smp)
   EVR_M_SWITCH(st->m, L);
 #undef L
@@ -2443,7 +2692,8 @@ int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double
 extern "C" {
 
 int evr_hvi_set_restart_variant(int variant) {
-  EVR_CHECK(variant == 1 || variant == 2, "evr_hvi_set_restart_variant: variant must be 1 or 2, got %d", variant);
+  EVR_CHECK(variant >= 1 && variant <= 3, "evr_hvi_set_restart_variant: variant must be 1 (kd3), 2 (kdb) or 3 (kdw), got %d",
+            variant);
   g_restart_variant = variant;
   return 0;
 }

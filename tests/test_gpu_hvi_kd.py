@@ -167,17 +167,18 @@ def restart_variant():
 
     lib = _native.load()
     yield lambda v: _native.check(lib.evr_hvi_set_restart_variant(v), "evr_hvi_set_restart_variant")
-    lib.evr_hvi_set_restart_variant(2)
+    lib.evr_hvi_set_restart_variant(3)
 
 
 @pytest.mark.parametrize("n,d,m,S,b", [(120, 6, 5, 256, 20), (60, 4, 3, 256, 7), (40, 3, 2, 512, 1),
                                        (200, 6, 5, 512, 32), (90, 5, 4, 256, 16), (80, 4, 1, 1024, 3)])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_restart_fused_scan_equals_three_launch_chain(restart_variant, variant, n, d, m, S, b):
     """The one-launch restart scans against hvi_thresholds + hvi_kd2 + hvi_reduce_fb on the same
     samples: hvi_kd3 (variant 1, per-wave ownership as kd2) bitwise on dG; hvi_kdb (variant 2,
-    work balanced over the workgroup, its own summation order) to 1e-12; acq = mean of the
-    per-sample values to 1e-14 / 1e-12; both bitwise reproducible."""
+    work balanced over the workgroup) and hvi_kdw (variant 3, the default: one wave per
+    candidate) in their own summation orders to 1e-12; acq = mean of the per-sample values to
+    1e-14 / 1e-12; all bitwise reproducible."""
     from everest_amd import ops
 
     restart_variant(variant)
@@ -228,3 +229,41 @@ def test_restart_balanced_scan_slices(restart_variant):
     assert c[0] / S > 4096 and c[1] / S > 8192, c / S      # per-sample pairs / terms exceed the caps
     assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
     assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
+
+
+def test_restart_wave_scan_long_term_lists(restart_variant):
+    """hvi_kdw on candidates dominating most of the front (hundreds of terms per sample and
+    candidate: many 64-term rounds and list remainders) against the three-launch chain."""
+    from everest_amd import ops
+
+    restart_variant(3)
+    kd, dense, lo, hi, d = _pair(240, 6, 5, 256, seed=11, prune=False)
+    b = 32
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(b, d)), device="cuda")
+    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
+    G, L22, flags = ops.qnehvi_samples_norms(kd.state, R, P, b)
+    G = G + 3.0
+    a1, d1 = ops.hvi_forward_backward(kd.state, G, b, flags)
+    sval, d2 = ops.hvi_restart_fb(kd.state, G, b)
+    assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
+    assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
+
+
+@pytest.mark.parametrize("b", [20, 32, 7])
+def test_restart_wave_scan_is_batch_invariant(restart_variant, b):
+    """hvi_kdw: a candidate's per-sample value and gradient depend on its own terms only, so
+    they are bitwise the same in any batch — the property that makes a restart batch sharded
+    over ranks evaluate exactly as on one rank."""
+    from everest_amd import ops
+
+    restart_variant(3)
+    kd, dense, lo, hi, d = _pair(120, 6, 5, 256, seed=31)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b).uniform(size=(b, d)), device="cuda")
+    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
+    G, _, _ = ops.qnehvi_samples_norms(kd.state, R, P, b)
+    sval, dG = ops.hvi_restart_fb(kd.state, G, b)
+    h = b // 2
+    for lo_i, hi_i in ((0, h), (h, b)):
+        Gs = G[:, :, lo_i:hi_i].contiguous()
+        sv, dg = ops.hvi_restart_fb(kd.state, Gs, hi_i - lo_i)
+        assert torch.equal(sv, sval[:, lo_i:hi_i]) and torch.equal(dg, dG[:, :, lo_i:hi_i])

@@ -131,3 +131,22 @@ def test_small_batch_ops_equal_plan():
     assert torch.equal(dX, g_ref)
     assert torch.allclose(acq, a_ref, rtol=1e-12, atol=0) and torch.allclose(ops.mean_over_samples(sval), a_ref,
                                                                                rtol=1e-14, atol=0)
+
+
+def test_restart_chain_is_batch_invariant():
+    """The whole b <= 32 evaluation chain (kernel matrix, projection, fused sampling + wave scan,
+    backward, dX reduction) gives every candidate bitwise the same value and gradient whether
+    it is evaluated in the full restart batch or in a slice of it (what a rank of the sharded
+    joint restart problem evaluates, optim._Shard)."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 120, 5, 3, 256
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=29)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=2, prune_seed=3,
+               prune_samples=256)
+    Xc = lo + (hi - lo) * np.random.default_rng(6).uniform(size=(20, d))
+    a, g = q.eval_host(Xc, True)
+    for sl in (slice(0, 10), slice(10, 20), slice(3, 10)):
+        a2, g2 = q.eval_host(Xc[sl], True)
+        assert np.array_equal(a2, a[sl]) and np.array_equal(g2, g[sl])
