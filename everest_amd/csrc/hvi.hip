@@ -2060,9 +2060,10 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
 //   thresholds t_j = #{rows with lower-bound value <= y_j} by two wave-wide probes of the
 //     sample's ascending values (64 bucket ends, then the 64 entries of the straddling
 //     bucket) instead of a 9-step binary search;
-//   the sample's groups in chunks of 64, one per lane: group test, and for a passing group
-//     its 16 cell tests (the group's rank rows) -> cell mask; the passing cells' key indices
-//     appended to the wave's term list in (group, cell) order by a wave scan;
+//   the sample's groups, 64 per chunk and 8 chunks in flight: group tests; the passing groups
+//     compacted in group order; their 16 cell tests (the group's rank rows), one group per
+//     lane -> cell masks; the passing cells' key indices appended to the wave's term list in
+//     (group, cell) order by a wave scan;
 //   terms in rounds of 64, term t of the candidate on lane t % 64: key decoded against the
 //     LDS point table, the term and its subgradients (hvi_kdb's arithmetic) summed per lane
 //     in t order; then one fixed xor-butterfly per value.
@@ -2073,11 +2074,13 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
 // Workgroup w runs on XCD w % 8: the candidate groups of a sample share one XCD's L2.
 // ---------------------------------------------------------------------------------------
 constexpr int KW_WAVES = 4;
+constexpr int KW_NCH = 8;               // 64-group chunks whose group / cell tests are in flight together
 constexpr int KW_TCAP = 64 * 16 + 64;   // one 64-group chunk's terms + a partial round
 
 __host__ __device__ inline size_t kw_pt_bytes(int stride, int M) { return ((size_t)stride * M * 8 + 15) & ~(size_t)15; }
+// point table | per-wave term lists (u32 key indices) | per-wave passing-group lists (u16)
 __host__ __device__ inline size_t kw_lds_bytes(int stride, int M) {
-  return kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4;
+  return kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4 + (size_t)KW_WAVES * 64 * KW_NCH * 2;
 }
 
 template <int M>
@@ -2093,6 +2096,8 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
   const int stride = kd.stride;
   double* pt = (double*)kw_dyn;
   unsigned int* tl = (unsigned int*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
+  unsigned short* pl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4) +
+                       (size_t)wave * 64 * KW_NCH;
   {
     const double* src = kd.pts + (size_t)s * stride * M;
     for (int e = tid; e < stride * M; e += 256) pt[e] = src[e];
@@ -2154,7 +2159,11 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
   }
   const uint4 tt = make_uint4(tw[0], tw[1], tw[2], tw[3]);
 
-  // ---- groups in chunks of 64 -> term list -> rounds of 64 terms ----
+  // ---- the sample's groups in blocks of KW_NCH chunks of 64 (lane = group of a chunk):
+  //      A. every chunk's group test, all minima loads in flight together; B. the passing
+  //      groups compacted in group order; C. rounds of 64 passing groups, one per lane (rank
+  //      rows loaded together): cell masks, the passing cells' key indices appended to the
+  //      term list in (group, cell) order, full rounds of 64 terms evaluated as they fill ----
   const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
   const uint4* gmin = (const uint4*)kd.gbox + gbase;
   double acc[NV];
@@ -2199,55 +2208,80 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
       kc = kn;
     }
   };
-  int tn = 0;   // terms in the list (wave-uniform)
-  for (int g0 = 0; g0 < Gs; g0 += 64) {
-    const int g = g0 + lane;
-    unsigned int mB = 0;
-    if (g < Gs && kd_pass4(gmin[g], tt)) {
-      const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
-      unsigned int a[8];
+  // the cell mask (16 bits) of group g for this candidate: rank_j < t_j in every objective
+  auto cell_mask = [&](const int g) -> unsigned int {
+    const uint4* rp = (const uint4*)(kd.grk + (size_t)(gbase + g) * M * 16);
+    unsigned int a[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] = 0xFFFFFFFFu;
+    for (int k = 0; k < 8; ++k) a[k] = 0xFFFFFFFFu;
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-        const unsigned int t2 = th16 | (th16 << 16);
-        const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
-        a[0] &= kd_lt16(r1.x, t2);
-        a[1] &= kd_lt16(r1.y, t2);
-        a[2] &= kd_lt16(r1.z, t2);
-        a[3] &= kd_lt16(r1.w, t2);
-        a[4] &= kd_lt16(r2.x, t2);
-        a[5] &= kd_lt16(r2.y, t2);
-        a[6] &= kd_lt16(r2.z, t2);
-        a[7] &= kd_lt16(r2.w, t2);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) mB |= (((a[k] >> 15) & 1u) | ((a[k] >> 30) & 2u)) << (2 * k);
+    for (int j = 0; j < M; ++j) {
+      const unsigned int th16 = (tw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      const unsigned int t2 = th16 | (th16 << 16);
+      const uint4 r1 = rp[2 * j], r2 = rp[2 * j + 1];
+      a[0] &= kd_lt16(r1.x, t2);
+      a[1] &= kd_lt16(r1.y, t2);
+      a[2] &= kd_lt16(r1.z, t2);
+      a[3] &= kd_lt16(r1.w, t2);
+      a[4] &= kd_lt16(r2.x, t2);
+      a[5] &= kd_lt16(r2.y, t2);
+      a[6] &= kd_lt16(r2.z, t2);
+      a[7] &= kd_lt16(r2.w, t2);
     }
-    int tot;
-    int p = tn + wave_scan_excl(__popc(mB), &tot);
-    {
+    unsigned int mB = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mB |= (((a[k] >> 15) & 1u) | ((a[k] >> 30) & 2u)) << (2 * k);
+    return mB;
+  };
+  int tn = 0;   // terms in the list (wave-uniform)
+  for (int G0 = 0; G0 < Gs; G0 += 64 * KW_NCH) {
+    const int nch = min(KW_NCH, (Gs - G0 + 63) >> 6);
+    // A. group tests of up to KW_NCH chunks: one minima load per chunk and lane, all in flight
+    uint4 gm[KW_NCH];
+#pragma unroll
+    for (int k = 0; k < KW_NCH; ++k) {
+      const int g = G0 + 64 * k + lane;
+      gm[k] = (k < nch && g < Gs) ? gmin[g] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    // B. the passing groups, compacted in group order (chunk-major, lane order within a chunk)
+    int np_ = 0;
+#pragma unroll
+    for (int k = 0; k < KW_NCH; ++k) {
+      const unsigned long long bal = __ballot(kd_pass4(gm[k], tt));
+      if (bal >> lane & 1ull) pl[np_ + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)(64 * k + lane);
+      np_ += __popcll(bal);
+    }
+    wave_sync();
+    // C. pair rounds of 64, one passing group per lane (its rank rows loaded together): cell
+    //    masks -> the cells' key indices appended in (group, cell) order, term rounds as they fill
+    for (int p0 = 0; p0 < np_; p0 += 64) {
+      const int i = p0 + lane;
+      const int g = i < np_ ? G0 + (int)pl[i] : -1;
+      const unsigned int mB = g >= 0 ? cell_mask(g) : 0u;
+      int tot;
+      int p = tn + wave_scan_excl(__popc(mB), &tot);
+      if (tot == 0) continue;
       const unsigned int kb = (unsigned int)(gbase + g) * 16u;
       unsigned int mk = mB;
       while (mk) {
-        const int k = __ffs(mk) - 1;
+        const int c16 = __ffs(mk) - 1;
         mk &= mk - 1;
-        tl[p++] = kb + (unsigned int)k;
+        tl[p++] = kb + (unsigned int)c16;
+      }
+      tn += tot;
+      wave_sync();
+      const int nr = tn >> 6;
+      if (nr > 0) {
+        rounds(nr, 0);
+        const int rem = tn - nr * 64;
+        const unsigned int keep = lane < rem ? tl[nr * 64 + lane] : 0u;
+        wave_sync();
+        if (lane < rem) tl[lane] = keep;
+        wave_sync();
+        tn = rem;
       }
     }
-    tn += tot;
-    wave_sync();
-    const int nr = tn >> 6;
-    if (nr > 0) {
-      rounds(nr, 0);
-      const int rem = tn - nr * 64;
-      const unsigned int keep = lane < rem ? tl[nr * 64 + lane] : 0u;
-      wave_sync();
-      if (lane < rem) tl[lane] = keep;
-      wave_sync();
-      tn = rem;
-    }
+    wave_sync();   // pl is rewritten by the next block of chunks
   }
   rounds(0, tn);
   // ---- per value the lanes' sums, fixed butterfly ----

@@ -1,0 +1,66 @@
+"""A/B of the restart-batch scan variants at the bench state: the config-4 QnehviStrategy after
+one ask (bench.make_ask_strategy, seed 1), its optimised restart candidates (b = 20) and a
+Sobol batch; per variant (evr_hvi_set_restart_variant: 1 = hvi_kd3, 2 = hvi_kdb, 3 = hvi_kdw)
+the scan's device time (10 launches in one HIP graph between HIP events) and the native
+plan's host round trip per evaluation (plan.run_host, the restart loop's unit).
+One JSON line."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+import bench
+from everest_amd import _native, ops
+
+
+def graph_ms(f, reps=10):
+    f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            f()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    s, _ = bench.make_ask_strategy(512, 256, 1024, 20, 1, None, seed=1)
+    s.ask(1)
+    acqf = s.last_acqf
+    Xopt = np.ascontiguousarray(s.last_ask_stats.restart_X.reshape(20, -1))
+    lib = _native.load()
+    out = {}
+    for tag, X in (("opt", Xopt), ("sobol", bench.candidates(20, 6, seed=5, device=dev).cpu().numpy())):
+        Xt = torch.tensor(X, device=dev)
+        b = X.shape[0]
+        R, P = ops.qnehvi_small_forward(acqf.state, acqf.model, acqf.gp.cross(Xt), b)
+        G, L22, flags = ops.qnehvi_small_samples(acqf.state, R, P, b)
+        for v, name in ((1, "kd3"), (2, "kdb"), (3, "kdw")):
+            _native.check(lib.evr_hvi_set_restart_variant(v), "variant")
+            scan = graph_ms(lambda: ops.hvi_restart_fb(acqf.state, G, b))
+            acqf._plans = {}
+            p = acqf.plan(b, True)
+            p.run_host(X)
+            t0 = time.perf_counter()
+            for _ in range(50):
+                p.run_host(X)
+            rt = (time.perf_counter() - t0) / 50
+            out[f"{tag}_{name}"] = {"scan_us": round(scan * 1e3, 2), "eval_roundtrip_us": round(rt * 1e6, 2)}
+    _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
