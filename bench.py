@@ -441,7 +441,9 @@ def _launched_kernel(acqf, op, b, d):
                 "proj_bwd": r"qs_bwd" if ops.qnehvi_small_applies(acqf.state, b, d) else r"Cijk_|qn_proj_bwd",
                 "kernel_grad": r"kcross_grad"}.get(op, re.escape(op))
     if ops.qnehvi_small_applies(acqf.state, b, d) and ops.hvi_restart_fb_applies(acqf.state, b):
-        return r"hvi_kd3<" if os.environ.get("EVR_KDB", "1") == "0" else r"hvi_kdb<"
+        # the restart-scan variant (hvi.hip restart_variant: kdw by default, EVR_RESTART_SCAN=kdb|kd3);
+        # exactly one of them runs in the chain
+        return r"hvi_kd[3bw]<"
     return r"hvi_kd2?<|hvi_tiled<"
 
 

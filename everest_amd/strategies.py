@@ -375,7 +375,13 @@ class BotorchStrategy(PredictiveStrategy):
                                           fixed_features=combos[0] or None, q=q)
         stats.best_value = val
         self.last_ask_stats = stats
-        return self._postprocess_candidates(x.reshape(q, -1))
+        out = self._postprocess_candidates(x.reshape(q, -1))
+        self._prefetch_next_ask()
+        return out
+
+    def _prefetch_next_ask(self) -> None:
+        """Hook run at the end of ask(): strategies whose next acquisition starts with seed
+        draws of a known size may start that work early (QnehviStrategy)."""
 
     def _ask_mixed_sequential(self, q: int, combos, ineq, eq):
         """optimize_acqf_mixed with q > 1 (botorch.optim.optimize_mixed, sequential branch):
@@ -615,6 +621,25 @@ class QnehviStrategy(QehviStrategy):
     def __init__(self, data_model, dist=None, **kwargs):
         super().__init__(data_model, dist=dist)
         self.alpha = data_model.alpha
+
+    def _prefetch_next_ask(self) -> None:
+        """The next ask's first generator draws are its prune and sampler seeds (qnehvi.py
+        draws them before anything else consumes the strategy's generator), so right after an
+        ask they are known: peek at them on a copy of the generator and start the prune draw's
+        host scrambling (n_train x m Sobol dimensions) on a worker thread.  The next
+        acquisition takes the running future if its (dimension, seed) matches — a tell()
+        between the asks changes neither the generator nor, with the same rows, the size —
+        and otherwise starts its own; results are the same either way."""
+        if os.environ.get("EVR_SCRAMBLE_PREFETCH", "1") == "0" or self.model is None:
+            return
+        try:
+            X_train, _ = self.get_acqf_input_tensors()
+        except Exception:   # noqa: BLE001 — a speculative prefetch never fails an ask
+            return
+        g = torch.Generator()
+        g.set_state(self.gen.get_state())
+        prune_seed = int(torch.randint(0, 1000000, (1,), generator=g).item())
+        prefetch_scramble(int(X_train.shape[0]) * int(self.model.B), prune_seed)
 
     def _get_acqfs(self, n) -> List[QNEHVI]:
         """bofire/strategies/predictives/qnehvi.py:23-53."""

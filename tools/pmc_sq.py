@@ -1,4 +1,4 @@
-"""Summarise a rocprofv3 --pmc pass of SQ counters (tools/gpu_round.sh pmc_sq*) per kernel:
+"""Summarise a rocprofv3 --pmc pass of SQ counters (tools/gpu_steps.sh pmc_sq*) per kernel:
 average per dispatch and the wave-cycle split the MI355X guide defines (WAIT_ANY = parked on
 s_waitcnt / barrier, WAIT_INST_ANY = issue stall, ACTIVE_INST_ANY = issuing; the three add up
 to WAVE_CYCLES), plus LDS bank conflicts per LDS instruction.

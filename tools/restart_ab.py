@@ -59,6 +59,8 @@ def main():
             rt = (time.perf_counter() - t0) / 50
             out[f"{tag}_{name}"] = {"scan_us": round(scan * 1e3, 2), "eval_roundtrip_us": round(rt * 1e6, 2)}
     _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
+    out["construction"] = {k: round(v * 1e3, 3) for k, v in acqf.timings.items()}
+    out["base_jitter"] = [float(v) for v in acqf.base_jitter.cpu()]
     print(json.dumps(out))
 
 
