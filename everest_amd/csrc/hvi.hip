@@ -2447,7 +2447,7 @@ static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const
   return 0;
 }
 
-// restart-scan kernel: 2 = hvi_kdb (balanced, default), 1 = hvi_kd3 (EVR_KDB=0 or
+// restart-scan kernel: 3 = hvi_kdw (default), 2 = hvi_kdb (balanced), 1 = hvi_kd3 (EVR_KDB=0 or
 // evr_hvi_set_restart_variant)
 static int g_restart_variant = 0;
 static int restart_variant() {

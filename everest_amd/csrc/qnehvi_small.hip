@@ -469,7 +469,9 @@ __global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int 
 // graph): every wave also writes its dX element (and the first b acq) to the pinned host
 // buffer; after a system-scope fence each workgroup counts itself done, and the last one
 // resets the counter and writes the evaluation's sequence number into the completion word the
-// host spins on (no separate copy-out kernel).
+// host spins on (no separate copy-out kernel).  The sequence number (written by the host
+// before the graph launch) is read at kernel entry by every workgroup's thread 0, so its PCIe
+// round trip overlaps the sums instead of trailing the last workgroup's atomic.
 //
 // With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the waves of
 // the first b elements also form acq[c] = mean over the S samples (lane-strided, then the
@@ -483,6 +485,8 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool ein = e < b * d;
   const int k = e % d;
+  unsigned long long seq = 0;
+  if (hout && threadIdx.x == 0) seq = *(volatile const unsigned long long*)seqp;
   double av = 0.0;
   if (ein && sval && e < b) {
     double x[4];
@@ -536,7 +540,6 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
       const unsigned int prev = atomicAdd(counter, 1u);
       if (prev == gridDim.x - 1) {
         atomicExch(counter, 0u);
-        const unsigned long long seq = *(volatile const unsigned long long*)seqp;
         __threadfence_system();
         *(volatile unsigned long long*)(hout + b + (size_t)b * d) = seq;
       }

@@ -53,16 +53,22 @@ def kernels(lib: str):
             f.flush()
             notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f.name], check=True,
                                    capture_output=True, text=True).stdout
+        # one kernel's fields are one YAML list entry ("  - .agpr_count: ..." opens it); its
+        # .name sits in the middle of the alphabetical field order, so collect the entry first
         cur = None
         for line in notes.splitlines():
-            m = re.match(r"\s*(?:- )?\.(\w+):\s+(\S+)", line)
+            m = re.match(r"(\s*)(- )?\.(\w+):\s+(\S+)", line)
             if not m:
                 continue
-            k, v = m.groups()
+            ind, item, k, v = m.groups()
+            if item and len(ind) <= 4:
+                cur = {}
+            if cur is None:
+                continue
             if k == "name" and not v.endswith(".kd"):
-                cur = out.setdefault(v, {})
-            elif cur is not None and k in ("vgpr_count", "sgpr_count", "group_segment_fixed_size",
-                                           "private_segment_fixed_size", "agpr_count"):
+                out[v] = cur
+            elif k in ("vgpr_count", "sgpr_count", "group_segment_fixed_size", "private_segment_fixed_size",
+                       "agpr_count"):
                 key = {"group_segment_fixed_size": "lds", "private_segment_fixed_size": "scratch"}.get(k, k)
                 cur[key] = int(v)
     return out
