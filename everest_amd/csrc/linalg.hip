@@ -389,7 +389,82 @@ __device__ __forceinline__ double quad_bcast_f64(double v, int s) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// lane l of the lane's 16-lane DPP row, as an f64 (v_mov_b64 with DPP row_newbcast: gfx90a+
+// 64-bit DPP); l is a compile-time constant after unrolling, so the switch folds
+__device__ __forceinline__ double row_bcast_f64(double v, int l) {
+#define EVR_RB(L_) \
+  case L_: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L_, 0xf, 0xf, false);
+  switch (l) {
+    EVR_RB(0) EVR_RB(1) EVR_RB(2) EVR_RB(3) EVR_RB(4) EVR_RB(5) EVR_RB(6) EVR_RB(7)
+    EVR_RB(8) EVR_RB(9) EVR_RB(10) EVR_RB(11) EVR_RB(12) EVR_RB(13) EVR_RB(14)
+    default: return __builtin_amdgcn_update_dpp(0.0, v, 0x15F, 0xf, 0xf, false);
+  }
+#undef EVR_RB
+}
+
 // one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
+#if !defined(EVR_LEAF_PAIR) && !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
+// Row-per-lane leaf (default): lane r of every 16-lane DPP row holds row r of A (16 values)
+// and of the inverse accumulator E; the wave's four DPP rows compute the same thing.  Step j
+// needs the pivot A[j][j], the column entries A[c][j] (c > j) and the finished inverse row
+// E[j][.] — each is one register of one lane of the row, delivered by a DPP row_newbcast move
+// straight from that lane's register: no LDS, no ds_bpermute round trip, no readlane.  The
+// arithmetic is the one-pivot loop's (m = A[r][j] ip, fma(-m, A[c][j], A[r][c]),
+// fma(-m, E[j][c], E[r][c]); ip = rcp + 2 Newton steps; final A / sqrt(pivot)), so the
+// results are bitwise those of the bpermute leaves.  The pivots stay in registers.
+__device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
+                                              double* erow, double* piv) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  double a[CP], e[CP], pv[CP];
+#pragma unroll
+  for (int c = 0; c < CP; ++c) {
+    a[c] = (c <= r) ? A[c0 + r][c0 + c] : 0.0;
+    e[c] = (c == r) ? 1.0 : 0.0;
+  }
+  int bad = -1;
+#pragma unroll
+  for (int j = 0; j < CP; ++j) {
+    const double p = row_bcast_f64(a[j], j);   // A[j][j]
+    pv[j] = p;
+    if (bad < 0 && !(p > 0.0)) bad = j;
+    double ip = __builtin_amdgcn_rcp(p);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    const double m = a[j] * ip;   // A[r][j] / A[j][j]
+    const bool below = r > j;
+#pragma unroll
+    for (int c = j + 1; c < CP; ++c) {
+      const double col = row_bcast_f64(a[j], c);   // A[c][j]
+      const double dn = fma(-m, col, a[c]);
+      a[c] = (below && c <= r) ? dn : a[c];
+    }
+#pragma unroll
+    for (int c = 0; c <= j; ++c) {
+      const double er = row_bcast_f64(e[c], j);    // E[j][c] (final)
+      const double en = fma(-m, er, e[c]);
+      e[c] = below ? en : e[c];
+    }
+  }
+  (void)colj;
+  (void)erow;
+  (void)piv;
+  if (bad >= 0) return bad;
+  // group g stores columns g, g + 4, ...
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = g + 4 * k;
+    double av = 0.0, xv = 0.0, pc = pv[0], pr = pv[0];
+#pragma unroll
+    for (int t = 0; t < CP; ++t) {   // register-indexed selects (no dynamic private array)
+      if (t == c) { av = a[t]; xv = e[t]; pc = pv[t]; }
+      if (t == r) pr = pv[t];
+    }
+    A[c0 + r][c0 + c] = (c <= r) ? av / sqrt(pc) : 0.0;
+    X[c0 + r][c0 + c] = (c <= r) ? xv / sqrt(pr) : 0.0;
+  }
+  return -1;
+}
+#else
 // Lane (row r, quad q) holds A[r][q + 4k].  Per pivot step the pivot comes by readlane (a
 // uniform scalar: its reciprocal starts at once and the failure test is a scalar branch),
 // the lane's own row entry A[r][j] by a DPP quad broadcast, and the column entries of the
@@ -408,7 +483,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
-#if !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
+#if defined(EVR_LEAF_PAIR)
   // two pivots per exchange round: columns j, j1 = j + 1 and inverse rows j, j1 as they are
   // before step j arrive in one round of ds_bpermute; what step j1 reads after step j (its
   // pivot, its column entries A'[c][j1], the lane's own A'[r][j1], the inverse row E'[j1]) is
@@ -560,6 +635,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   }
   return -1;
 }
+#endif
 
 // acc += P Q over one 16x16x16 block product on the f64 matrix cores (fragment maps as in
 // gemm_f64_kernel); P = M1[pr.., pc..] (or its transpose), Q = M2[qr.., qc..] (or transpose).

@@ -14,6 +14,8 @@
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
+#   cholprof    phase cycles + result digest of the 64x64 diagonal factor, DPP leaf vs the
+#               two-pivot bpermute leaf (tools/_chol_prof_{dpp,pair}, built from tools/chol_prof.hip)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -52,6 +54,9 @@ for st in "$@"; do
     bench) run bench 900 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
+    cholprof)
+      run cholprof_dpp 60 tools/_chol_prof_dpp
+      run cholprof_pair 60 tools/_chol_prof_pair ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
