@@ -9,7 +9,8 @@
 // split-K sum, cross-gradient reduction).  Here:
 //   qs_fwd:  one workgroup per (16 rows of M_j, output j): K_x (kmat_kernel, once per
 //            output: computing it inside every row tile costs 49x the f64 exp) staged in LDS
-//            in 256-row chunks, v_mfma_f64_16x16x4 with a per-lane contiguous 128 B slice of each M row
+//            in 128-row chunks (two workgroups per CU: the m x 66 row tiles of the bench shape
+//            are resident at once), v_mfma_f64_16x16x4 with a per-lane contiguous 128 B slice of each M row
 //            (the contraction index is permuted per lane, identically in A and B), the four
 //            waves' k-quarters reduced in a fixed order; epilogue writes R and the per-tile
 //            partial sums of squares the sampling kernel reads.
@@ -30,7 +31,10 @@ namespace evr {
 
 constexpr int QS_B = 32;     // max candidates
 constexpr int QS_FR = 16;    // rows of M per forward workgroup
-constexpr int QS_KC = 256;   // K_x rows staged per chunk
+constexpr int QS_KC = 128;   // K_x rows staged per chunk (~67 KB of LDS: two workgroups per CU)
+constexpr int QS_RPP = 256 / QS_KC;        // M rows per staging pass (a thread per chunk column)
+constexpr int QS_ML = QS_FR / QS_RPP;      // M values per thread and chunk
+constexpr int QS_KL = QS_KC * QS_B / 256;  // K_x values per thread and chunk
 constexpr int QS_BI = 16;    // columns of M (training rows) per backward workgroup
 constexpr int QS_MAXD = 8;   // input dims handled in registers by the backward epilogue
 
@@ -47,8 +51,8 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
   // padded row of the staged M tile: 2 MP = 4 (mod 64 dwords) puts the 16 rows x 2
   // k-quarters of a ds_read_b64 lane half on 32 distinct bank pairs (conflict-free)
   constexpr int MP = QS_KC + 2;
-  __shared__ double Ms[QS_FR][MP];               // 16 x 256 slice of M_j (33 KB)
-  __shared__ double Ks[QS_KC][QS_B + 1];         // 256 x b slice of K_x,j (66 KB)
+  __shared__ double Ms[QS_FR][MP];               // 16 x 128 slice of M_j (16.6 KB)
+  __shared__ double Ks[QS_KC][QS_B + 1];         // 128 x b slice of K_x,j (33.8 KB)
   __shared__ double red[4][QS_FR][QS_B + 1];
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -60,18 +64,19 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
   // instruction; the chunk's K_x rows are one contiguous run of kn x b doubles), staged in
   // LDS afterwards; the next chunk's loads are issued before the current chunk's MFMAs.
   // K_x rows past the end of a partial chunk are zero (M's are too, but 0 x garbage is not 0).
-  double mv[QS_FR], kv[QS_B];
+  double mv[QS_ML], kv[QS_KL];
+  const int kk = tid % QS_KC, rh = tid / QS_KC;   // staging: chunk column kk of rows rh, rh + 2, ...
   auto load = [&](int kc) {
     const int kn = min(QS_KC, n - kc);
 #pragma unroll
-    for (int u = 0; u < QS_FR; ++u) {
-      const int r = r0 + u;
-      mv[u] = (r < Rr && tid < kn) ? Mj[(size_t)r * n + kc + tid] : 0.0;
+    for (int u = 0; u < QS_ML; ++u) {
+      const int r = r0 + QS_RPP * u + rh;
+      mv[u] = (r < Rr && kk < kn) ? Mj[(size_t)r * n + kc + kk] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < QS_B; ++u) {
+    for (int u = 0; u < QS_KL; ++u) {
       const int e = u * 256 + tid;
-      kv[u] = (u < b && e < kn * b) ? Kj[(size_t)kc * b + e] : 0.0;
+      kv[u] = (e < kn * b) ? Kj[(size_t)kc * b + e] : 0.0;
     }
   };
   load(0);
@@ -79,11 +84,11 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
   for (int kc = 0; kc < n; kc += QS_KC) {
     __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
 #pragma unroll
-    for (int u = 0; u < QS_FR; ++u) Ms[u][tid] = mv[u];
+    for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
 #pragma unroll
-    for (int u = 0; u < QS_B; ++u) {
+    for (int u = 0; u < QS_KL; ++u) {
       const int e = u * 256 + tid;
-      if (u < b) Ks[e / b][e % b] = kv[u];   // e < 256 b: every row of the chunk, columns < b
+      if (e < QS_KC * b) Ks[e / b][e % b] = kv[u];   // every row of the chunk, columns < b
     }
     __syncthreads();
     if (kc + QS_KC < n) load(kc + QS_KC);
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
 // ---------------------------------------------------------------------------------------
 // forward with the cross-covariance generated in the B fetch (the restart batch of the native
 // plan): as qs_fwd, but each chunk's K_x rows are computed by the workgroup itself —
-// thread t owns training row kc + t and forms k(x_t, x_c) for the b candidates with
+// threads t and t + 128 own training row kc + t and form k(x_t, x_c) for the b candidates with
 // kmat_kernel's arithmetic (normalised / lengthscale-divided coordinates, explicit
 // differences, fma accumulation in coordinate order, the same kernel_value), so R is bitwise
 // the kmat_kernel + qs_fwd result, without the separate launch or K_x's HBM round trip.
@@ -157,17 +162,18 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
   const int i = lane & 15, kq = lane >> 4;
   const double* Mj = M + (size_t)j * Rr * n;
   const double* lsj = ls + (size_t)j * d;
-  double mv[QS_FR];
+  double mv[QS_ML];
   double xt[QS_MAXD];
+  const int kk = tid % QS_KC, rh = tid / QS_KC;   // M staging as in qs_fwd; K rows: row kk, half rh
   auto load = [&](int kc) {
     const int kn = min(QS_KC, n - kc);
 #pragma unroll
-    for (int u = 0; u < QS_FR; ++u) {
-      const int r = r0 + u;
-      mv[u] = (r < Rr && tid < kn) ? Mj[(size_t)r * n + kc + tid] : 0.0;
+    for (int u = 0; u < QS_ML; ++u) {
+      const int r = r0 + QS_RPP * u + rh;
+      mv[u] = (r < Rr && kk < kn) ? Mj[(size_t)r * n + kc + kk] : 0.0;
     }
 #pragma unroll
-    for (int k = 0; k < QS_MAXD; ++k) xt[k] = (tid < kn && k < d) ? Xn[(size_t)(kc + tid) * d + k] : 0.0;
+    for (int k = 0; k < QS_MAXD; ++k) xt[k] = (kk < kn && k < d) ? Xn[(size_t)(kc + kk) * d + k] : 0.0;
   };
   load(0);
   // candidates, normalised and divided by the lengthscales (kmat_kernel's B operand)
@@ -188,20 +194,23 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
     const int kn = min(QS_KC, n - kc);
     __syncthreads();   // uc written / the previous chunk's MFMAs are done with Ms, Ks
 #pragma unroll
-    for (int u = 0; u < QS_FR; ++u) Ms[u][tid] = mv[u];
+    for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
     {
-      // this thread's training row kc + tid, then its b kernel values (rows past the end: 0)
+      // this thread's training row kc + kk, then its share of the row's b kernel values (the
+      // thread halves rh take alternate rotated candidates; rows past the end: 0)
       double ut[QS_MAXD];
 #pragma unroll
       for (int k = 0; k < QS_MAXD; ++k) ut[k] = xt[k] * il[k];
-      const int sw = 16 * (tid & 1);
+      const int sw = 16 * (kk & 1);
       // all b squared distances first, then the b kernel values: fully unrolled so the LDS
       // reads and the exp table loads of different candidates are in flight together (one
       // wave per SIMD here: nothing else hides their latency)
-      double d2v[QS_B];
+      constexpr int CH = QS_B / QS_RPP;
+      double d2v[CH];
 #pragma unroll
-      for (int cc = 0; cc < QS_B; ++cc) {
-        d2v[cc] = 0.0;
+      for (int ci = 0; ci < CH; ++ci) {
+        const int cc = QS_RPP * ci + rh;
+        d2v[ci] = 0.0;
         if (cc < b) {
           int c = cc + rot;
           if (c >= b) c -= b;
@@ -213,15 +222,16 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
               acc = fma(df, df, acc);
             }
           }
-          d2v[cc] = acc;
+          d2v[ci] = acc;
         }
       }
 #pragma unroll
-      for (int cc = 0; cc < QS_B; ++cc) {
+      for (int ci = 0; ci < CH; ++ci) {
+        const int cc = QS_RPP * ci + rh;
         if (cc < b) {
           int c = cc + rot;
           if (c >= b) c -= b;
-          Ks[tid][c ^ sw] = tid < kn ? kernel_value(KIND >= 0 ? KIND : kind_of(kcode, j), d2v[cc]) : 0.0;
+          Ks[kk][c ^ sw] = kk < kn ? kernel_value(KIND >= 0 ? KIND : kind_of(kcode, j), d2v[ci]) : 0.0;
         }
       }
     }
