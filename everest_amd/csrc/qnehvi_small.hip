@@ -285,7 +285,10 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
 // with coalesced row segments, the coefficients applied while staging in LDS.
 // ---------------------------------------------------------------------------------------
 constexpr int QS_RC = 128;   // rows of M per backward chunk
-__global__ __launch_bounds__(256) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
+// (256, 2): two waves per SIMD, i.e. two workgroups per CU — without the bound the compiler
+// took 244 VGPRs + 16 AGPRs (one workgroup per CU: the 480 workgroups of the bench shape ran
+// in two rounds); bounded it fits 226 registers without scratch
+__global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
                                               const double* __restrict__ M, const double* __restrict__ R,
                                               const double* __restrict__ dG, const double* __restrict__ L22,
                                               const double* __restrict__ ys, const double* __restrict__ zq,

@@ -68,10 +68,27 @@ def kernels(lib: str):
             if k == "name" and not v.endswith(".kd"):
                 out[v] = cur
             elif k in ("vgpr_count", "sgpr_count", "group_segment_fixed_size", "private_segment_fixed_size",
-                       "agpr_count"):
-                key = {"group_segment_fixed_size": "lds", "private_segment_fixed_size": "scratch"}.get(k, k)
+                       "agpr_count", "max_flat_workgroup_size"):
+                key = {"group_segment_fixed_size": "lds", "private_segment_fixed_size": "scratch",
+                       "max_flat_workgroup_size": "wg"}.get(k, k)
                 cur[key] = int(v)
     return out
+
+
+def occupancy(r: dict, lds_dyn: int = 0) -> dict:
+    """Resident workgroups per CU of a kernel at its maximum workgroup size: the unified
+    VGPR + AGPR file (512 per SIMD lane, granule 8), 160 KB of LDS per CU (plus dynamic LDS
+    the launch adds), at most 8 waves per SIMD...  {wgs_per_cu, waves_per_simd, limit}."""
+    wg = r.get("wg", 256)
+    wpw = max(1, -(-wg // 64))                 # waves per workgroup
+    regs = -(-(r.get("vgpr_count", 0) + r.get("agpr_count", 0)) // 8) * 8
+    by_regs = (512 // regs if regs else 8) * 4 // wpw
+    lds = r.get("lds", 0) + lds_dyn
+    by_lds = 160 * 1024 // lds if lds else 64
+    by_waves = 8 * 4 // wpw
+    n = min(by_regs, by_lds, by_waves)
+    lim = "regs" if n == by_regs else ("lds" if n == by_lds else "waves")
+    return {"wgs_per_cu": n, "waves_per_simd": n * wpw / 4, "limit": lim}
 
 
 def demangle(names):
@@ -94,7 +111,7 @@ def main():
         r = ks[raw]
         if "--scratch-only" in sys.argv and not r.get("scratch"):
             continue
-        print(json.dumps({"kernel": pretty, **r}))
+        print(json.dumps({"kernel": pretty, **r, **occupancy(r)}))
 
 
 if __name__ == "__main__":
