@@ -2076,15 +2076,20 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
 constexpr int KW_WAVES = 4;
 constexpr int KW_NCH = 8;               // 64-group chunks whose group / cell tests are in flight together
 constexpr int KW_TCAP = 64 * 16 + 64;   // one 64-group chunk's terms + a partial round
+constexpr int KW_MAXG = 4096;           // groups per sample: term entries (16 g + cell) fit u16
 
 __host__ __device__ inline size_t kw_pt_bytes(int stride, int M) { return ((size_t)stride * M * 8 + 15) & ~(size_t)15; }
-// point table | per-wave term lists (u32 key indices) | per-wave passing-group lists (u16)
+// point table | per-wave term lists (u16 cell index within the sample) | per-wave passing-group
+// lists (u16): ~24 KB at the bench state, so LDS admits 6 workgroups per CU
 __host__ __device__ inline size_t kw_lds_bytes(int stride, int M) {
-  return kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4 + (size_t)KW_WAVES * 64 * KW_NCH * 2;
+  return kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 2 + (size_t)KW_WAVES * 64 * KW_NCH * 2;
 }
 
+// (256, 5): 5 waves per SIMD — at b = 20 the grid (S x 5 candidate groups = 1280 workgroups at
+// S = 256) is resident in one round; unbounded the compiler took 100 VGPRs (4 per SIMD).
+// M = 8 would spill at that bound and keeps 4.
 template <int M>
-__global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const double* __restrict__ G, HviKd kd,
+__global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int ncg, const double* __restrict__ G, HviKd kd,
                                                KbSamples smp, double* __restrict__ sval, double* __restrict__ dG) {
   constexpr int NV = M + 1;
   using K = CellKey<M>;
@@ -2095,8 +2100,8 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int stride = kd.stride;
   double* pt = (double*)kw_dyn;
-  unsigned int* tl = (unsigned int*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
-  unsigned short* pl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 4) +
+  unsigned short* tl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
+  unsigned short* pl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 2) +
                        (size_t)wave * 64 * KW_NCH;
   {
     const double* src = kd.pts + (size_t)s * stride * M;
@@ -2199,7 +2204,7 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
     auto ld = [&](const int r) -> unsigned long long {
       const int t = r * 64 + lane;
       const bool in = r < nr || lane < part;
-      return in ? kd.gkeys[tl[t]] : 0ull;
+      return in ? kd.gkeys[(size_t)gbase * 16 + tl[t]] : 0ull;
     };
     unsigned long long kc = ld(0);
     for (int r = 0; r <= last; ++r) {
@@ -2261,12 +2266,12 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
       int tot;
       int p = tn + wave_scan_excl(__popc(mB), &tot);
       if (tot == 0) continue;
-      const unsigned int kb = (unsigned int)(gbase + g) * 16u;
+      const unsigned int kb = (unsigned int)g * 16u;   // within the sample (< KW_MAXG x 16)
       unsigned int mk = mB;
       while (mk) {
         const int c16 = __ffs(mk) - 1;
         mk &= mk - 1;
-        tl[p++] = kb + (unsigned int)c16;
+        tl[p++] = (unsigned short)(kb + (unsigned int)c16);
       }
       tn += tot;
       wave_sync();
@@ -2274,7 +2279,7 @@ __global__ __launch_bounds__(256) void hvi_kdw(int b, int S, int ncg, const doub
       if (nr > 0) {
         rounds(nr, 0);
         const int rem = tn - nr * 64;
-        const unsigned int keep = lane < rem ? tl[nr * 64 + lane] : 0u;
+        const unsigned short keep = lane < rem ? tl[nr * 64 + lane] : (unsigned short)0;
         wave_sync();
         if (lane < rem) tl[lane] = keep;
         wave_sync();
@@ -2464,7 +2469,7 @@ static int restart_variant() {
 
 static bool hvi_kdw_applies(const evr_qnehvi_state* st, int b) {
   if (restart_variant() != 3 || !st || st->log_hvi || !st->grp_off || b < 1 || b > 32 || kd_variant() != 2 ||
-      st->m < 1 || st->m > 8 || st->max_groups > 0xFFFF)
+      st->m < 1 || st->m > 8 || st->max_groups > KW_MAXG)
     return false;
   return kw_lds_bytes(st->pts_stride, st->m) <= 64 * 1024;
 }
