@@ -1,9 +1,11 @@
 """A/B of the restart-batch scan variants at the bench state: the config-4 QnehviStrategy after
 one ask (bench.make_ask_strategy, seed 1), its optimised restart candidates (b = 20) and a
 Sobol batch; per variant (evr_hvi_set_restart_variant: 1 = hvi_kd3, 2 = hvi_kdb, 3 = hvi_kdw)
-the scan's device time (10 launches in one HIP graph between HIP events) and the native
-plan's host round trip per evaluation (plan.run_host, the restart loop's unit).
-One JSON line."""
+the scan's device time (10 launches in one HIP graph between HIP events), the plan's device
+chain per evaluation (50 back-to-back device-mode graph launches between HIP events), its
+host round trip per evaluation (plan.run_host: launch + chain + completion poll) and the
+native L-BFGS-B's wall time per evaluation (plan.minimize from the Sobol start, 30
+iterations: round trip + the optimiser's host step).  One JSON line."""
 import json
 import os
 import sys
@@ -52,12 +54,30 @@ def main():
             scan = graph_ms(lambda: ops.hvi_restart_fb(acqf.state, G, b))
             acqf._plans = {}
             p = acqf.plan(b, True)
+            p.X.copy_(Xt)
+            for _ in range(3):
+                p.run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                p.run()
+            e1.record()
+            torch.cuda.synchronize()
+            chain = e0.elapsed_time(e1) / 50
             p.run_host(X)
             t0 = time.perf_counter()
             for _ in range(50):
                 p.run_host(X)
             rt = (time.perf_counter() - t0) / 50
-            out[f"{tag}_{name}"] = {"scan_us": round(scan * 1e3, 2), "eval_roundtrip_us": round(rt * 1e6, 2)}
+            rec = {"scan_us": round(scan * 1e3, 2), "chain_us": round(chain * 1e3, 2),
+                   "eval_roundtrip_us": round(rt * 1e6, 2)}
+            if tag == "sobol":
+                t0 = time.perf_counter()
+                _, _, info = p.minimize(X, np.zeros_like(X), np.ones_like(X), 30)
+                rec["minimize_us_per_eval"] = round((time.perf_counter() - t0) / max(1, info[1]) * 1e6, 2)
+                rec["minimize_evals"] = int(info[1])
+            out[f"{tag}_{name}"] = rec
     _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
     out["construction"] = {k: round(v * 1e3, 3) for k, v in acqf.timings.items()}
     out["base_jitter"] = [float(v) for v in acqf.base_jitter.cpu()]
