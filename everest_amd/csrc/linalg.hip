@@ -403,8 +403,10 @@ __device__ __forceinline__ double row_bcast_f64(double v, int l) {
 }
 
 // one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
-#if !defined(EVR_LEAF_PAIR) && !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
-// Row-per-lane leaf (default): lane r of every 16-lane DPP row holds row r of A (16 values)
+#if defined(EVR_LEAF_DPP)
+// Row-per-lane leaf (EVR_LEAF_DPP build, A/B only: measured slower — 40.0 k vs 32.8 k cycles for
+// the four leaves of a 64-column factor, tools/chol_prof.hip — the 64-bit DPP moves and the
+// 16-wide unrolled row updates cost more issue slots than the paired bpermute exchange saves): lane r of every 16-lane DPP row holds row r of A (16 values)
 // and of the inverse accumulator E; the wave's four DPP rows compute the same thing.  Step j
 // needs the pivot A[j][j], the column entries A[c][j] (c > j) and the finished inverse row
 // E[j][.] — each is one register of one lane of the row, delivered by a DPP row_newbcast move
@@ -483,7 +485,7 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
-#if defined(EVR_LEAF_PAIR)
+#if !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
   // two pivots per exchange round: columns j, j1 = j + 1 and inverse rows j, j1 as they are
   // before step j arrive in one round of ds_bpermute; what step j1 reads after step j (its
   // pivot, its column entries A'[c][j1], the lane's own A'[r][j1], the inverse row E'[j1]) is

@@ -15,7 +15,8 @@
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
 #   cholprof    phase cycles + result digest of the 64x64 diagonal factor, DPP leaf vs the
-#               two-pivot bpermute leaf (tools/_chol_prof_{dpp,pair}, built from tools/chol_prof.hip)
+#               two-pivot bpermute leaf (tools/_chol_prof_{dpp,pair}: hipcc --offload-arch=gfx950 -O3
+#               -DEVR_CHOL_PROF [-DEVR_LEAF_DPP] tools/chol_prof.hip -o ...)
 set -o pipefail
 TAG=${1:?tag}
 shift
