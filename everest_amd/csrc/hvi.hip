@@ -2246,7 +2246,9 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
 #pragma unroll
     for (int k = 0; k < KW_NCH; ++k) {
       const int g = G0 + 64 * k + lane;
-      gm[k] = (k < nch && g < Gs) ? gmin[g] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      // past the sample's groups: 0x7FFF ranks (cells_kd's padding), which fail the packed signed
+      // compare (0xFFFF would read as -1 and pass)
+      gm[k] = (k < nch && g < Gs) ? gmin[g] : make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
     }
     // B. the passing groups, compacted in group order (chunk-major, lane order within a chunk)
     int np_ = 0;
