@@ -5,6 +5,9 @@
 # usage: bash tools/gpu_steps.sh <tag> step...
 #   pytest      the -m gpu parity suite
 #   pytestf     the test files named in $PYTEST_FILES
+#   restartab   tools/restart_ab.py (restart-scan variants: scan / chain / round trip / optimiser per
+#               evaluation) -> <tag>/restart_ab.json
+#   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
@@ -37,6 +40,8 @@ for st in "$@"; do
   case $st in
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytestf) run pytestf 900 python -u -m pytest $PYTEST_FILES -x -q --timeout 300 --timeout-method thread ;;
+    restartab) run restartab 300 python tools/restart_ab.py && cp "$OUT/restartab.log" "$OUT/restart_ab.json" ;;
+    benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
       cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
