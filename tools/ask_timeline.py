@@ -67,7 +67,29 @@ def analyse(d, log):
     gaps.append(((b - prev_end) / 1e3, prev_name, "<ask end>", (prev_end - a) / 1e3))
     gaps.sort(reverse=True)
     idle_gt20 = sum(g[0] for g in gaps if g[0] > 20)
-    out = dict(clock=clk, wall_us=round(wall, 1), kernels=len(sel), busy_us=round(busy, 1),
+    # restart evaluations: chain span (the evaluation's first kernel -> qs_dx_reduce end) and the
+    # host turnaround (qs_dx_reduce end -> the next evaluation's first kernel), medians; the
+    # kernels of one evaluation and their mean durations
+    ends = [i for i, r in enumerate(sel) if "qs_dx_reduce" in r[2]]
+    spans, turns, per = [], [], {}
+    for k, i in enumerate(ends):
+        j = i
+        first = ends[k - 1] + 1 if k > 0 else max(0, i - 8)
+        spans.append((sel[i][1] - sel[first][0]) / 1e3)
+        for r in sel[first:i + 1]:
+            short = r[2].split("(")[0][-40:]
+            per.setdefault(short, []).append((r[1] - r[0]) / 1e3)
+        if k + 1 < len(ends):
+            turns.append((sel[i + 1][0] - sel[i][1]) / 1e3)
+    med = lambda v: round(float(sorted(v)[len(v) // 2]), 2) if v else None  # noqa: E731
+    restart = dict(evaluations=len(ends), chain_span_us_median=med(spans), turnaround_us_median=med(turns),
+                   kernels={k: [len(v), med(v)] for k, v in per.items()})
+    # construction: the kernels before the first restart-chain kernel, in order (offset, duration)
+    first_eval = ends[0] - 4 if ends else len(sel)
+    cons = [[round((r[0] - a) / 1e3, 1), round((r[1] - r[0]) / 1e3, 1), r[2].split("(")[0][-48:]]
+            for r in sel[:max(0, first_eval)]]
+    out = dict(clock=clk, wall_us=round(wall, 1), kernels=len(sel), busy_us=round(busy, 1), restart=restart,
+               construction_kernels=cons[:400],
                busy_frac=round(busy / wall, 3), idle_in_gaps_over_20us=round(idle_gt20, 1),
                phases=w["phases"],
                top_kernels=sorted(([k, v[0], round(v[1], 1)] for k, v in by.items()), key=lambda x: -x[2])[:15],

@@ -7,6 +7,8 @@
 #   pytestf     the test files named in $PYTEST_FILES
 #   restartab   tools/restart_ab.py (restart-scan variants: scan / chain / round trip / optimiser per
 #               evaluation) -> <tag>/restart_ab.json
+#   asktl       device timeline of one ask (tools/ask_timeline.py under rocprofv3 --kernel-trace)
+#               -> <tag>/ask_timeline.json
 #   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
@@ -41,6 +43,9 @@ for st in "$@"; do
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytestf) run pytestf 900 python -u -m pytest $PYTEST_FILES -x -q --timeout 300 --timeout-method thread ;;
     restartab) run restartab 300 python tools/restart_ab.py && cp "$OUT/restartab.log" "$OUT/restart_ab.json" ;;
+    asktl)
+      run asktl_trace 300 rocprofv3 --kernel-trace -d "$OUT/asktl" -o run --output-format csv -- python tools/ask_timeline.py
+      run asktl_parse 60 python tools/ask_timeline.py --analyse "$OUT/asktl" "$OUT/asktl_trace.log" && cp "$OUT/asktl_parse.log" "$OUT/ask_timeline.json" ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
