@@ -14,7 +14,7 @@
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
 #   pmc512      the same over the b = 512 evaluation pass (keys without suffix)
-#   sq20        SQ wave-cycle split of the restart scan (hvi_kdb) at b = 20
+#   sq20        SQ wave-cycle split of the restart chain kernels (hvi_kdw, qs_fwd, qs_bwd) at b = 20
 #   kdwaves     per-wave phase stamps of the restart scan (EVR_KD_PROF=2 build in _libprof/)
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
@@ -59,7 +59,7 @@ for st in "$@"; do
       run pmc512_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc512_w" -o run --output-format csv -- python tools/loop_step.py 10 512
       run pmc512_parse 60 python tools/pmc_traffic.py "$OUT/pmc512_f" "$OUT/pmc512_w" "$OUT/hbm_traffic.json" ;;
     sq20)
-      run sq20 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "hvi_kdb|qs_fwd|qs_bwd" -d "$OUT/sq20" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
+      run sq20 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "hvi_kd[bw]|qs_fwd|qs_bwd|kmat_kernel|qs_dx" -d "$OUT/sq20" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
       run sq20_parse 60 python tools/pmc_sq.py "$OUT/sq20" "$OUT/sq_counters.json" ;;
     kdwaves) EVR_LIB_PATH=everest_amd/_libprof/libeverest_amd.so run kdwaves 300 python tools/kd3_waves.py ;;
     bench) run bench 900 python bench.py ;;

@@ -25,7 +25,7 @@ OPS = [
     ("kernel_matrix", r"kmat_kernel"),
     ("proj_fwd", r"qn_proj_fwd|qn_norms_rows|qs_fwd"),
     ("samples", r"qn_samples_norms"),
-    ("hvi_fwd_bwd", r"hvi_thresholds|hvi_kd[23b]?<|hvi_tiled<|hvi_reduce_fwd|hvi_reduce_bwd|hvi_reduce_fb"),
+    ("hvi_fwd_bwd", r"hvi_thresholds|hvi_kd[23bw]?<|hvi_tiled<|hvi_reduce_fwd|hvi_reduce_bwd|hvi_reduce_fb"),
     ("proj_bwd", r"qn_bwd_coef|qn_proj_bwd|qn_splitk_sum|qn_gen_gr|qs_bwd|qs_dx_reduce"),
     ("kernel_grad", r"kcross_grad"),
 ]
