@@ -415,15 +415,29 @@ struct LseState {
 // (P[tile][class][c], class 0: kernel rows, 1: baseline rows), with psd_safe_cholesky's 1x1
 // ladder (plain, then total jitter 1e-8 10^(t-1), t = 1..6); flag = 1 when every rung fails.
 // One definition so that both kernels produce bitwise the same samples.
-__device__ __forceinline__ void qn_mu_l22(const double* __restrict__ Pj, int nrt_used, int b, int c, double a,
-                                          double s, double cc, double ym, double kxx, double& mu, double& l22,
-                                          int& flag) {
-  double ssv = 0.0, ssw = 0.0;
-#pragma unroll 4
-  for (int rt = 0; rt < nrt_used; ++rt) {
-    ssv += Pj[((size_t)rt * 2 + 0) * b + c];
-    ssw += Pj[((size_t)rt * 2 + 1) * b + c];
+// The partial-norm sums of one (output, candidate): ssv over the class-0 tile sums (rows < n),
+// ssw over class 1 (baseline rows).  Canonical order, shared by every kernel that forms them:
+// four interleaved chains s_k = sum_{i} P[4 i + k] (i ascending), then (s_0 + s_1) + (s_2 + s_3)
+// — so that one thread (qn_mu_l22) and four lanes (hvi_kdw) produce the same bits.
+__device__ __forceinline__ double qn_norm_chain(const double* __restrict__ Pj, int nrt_used, int b, int c, int cls,
+                                                int k) {
+  double a = 0.0;
+  int rt = k;
+  for (; rt + 12 < nrt_used; rt += 16) {   // four loads of the chain in flight
+    const double x0 = Pj[((size_t)rt * 2 + cls) * b + c], x1 = Pj[((size_t)(rt + 4) * 2 + cls) * b + c];
+    const double x2 = Pj[((size_t)(rt + 8) * 2 + cls) * b + c], x3 = Pj[((size_t)(rt + 12) * 2 + cls) * b + c];
+    a += x0;
+    a += x1;
+    a += x2;
+    a += x3;
   }
+  for (; rt < nrt_used; rt += 4) a += Pj[((size_t)rt * 2 + cls) * b + c];
+  return a;
+}
+
+// mu, L22 (psd_safe ladder of 6) and the failure flag from the two norm sums
+__device__ __forceinline__ void qn_mu_l22_from(double ssv, double ssw, double a, double s, double cc, double ym,
+                                               double kxx, double& mu, double& l22, int& flag) {
   mu = ym + s * (cc + a);
   const double var = s * s * (kxx - ssv);
   const double br = var - ssw;
@@ -439,6 +453,19 @@ __device__ __forceinline__ void qn_mu_l22(const double* __restrict__ Pj, int nrt
       }
     }
   }
+}
+
+__device__ __forceinline__ void qn_mu_l22(const double* __restrict__ Pj, int nrt_used, int b, int c, double a,
+                                          double s, double cc, double ym, double kxx, double& mu, double& l22,
+                                          int& flag) {
+  double ch[2][4];
+#pragma unroll
+  for (int cls = 0; cls < 2; ++cls)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ch[cls][k] = qn_norm_chain(Pj, nrt_used, b, c, cls, k);
+  const double ssv = (ch[0][0] + ch[0][1]) + (ch[0][2] + ch[0][3]);
+  const double ssw = (ch[1][0] + ch[1][1]) + (ch[1][2] + ch[1][3]);
+  qn_mu_l22_from(ssv, ssw, a, s, cc, ym, kxx, mu, l22, flag);
 }
 
 // objective value of one sample: g = a (mu + h + L22 z) + b (h absent without sample rows)

@@ -2097,40 +2097,70 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   const int wid = blockIdx.x, xcd = wid & 7, slot = wid >> 3;
   const int s = (slot / ncg) * 8 + xcd, cg = slot - (slot / ncg) * ncg;
   if (s >= S) return;   // the grid covers S rounded up to 8 samples: whole workgroups leave
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index (hence the candidate c) is wave-uniform: scalar registers, not a VGPR
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int stride = kd.stride;
   double* pt = (double*)kw_dyn;
   unsigned short* tl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
   unsigned short* pl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 2) +
                        (size_t)wave * 64 * KW_NCH;
+  const int c = cg * KW_WAVES + wave;
+  const bool cin = c < b;
+  // Every load that depends only on (sample, candidate) is issued before the staging barrier,
+  // so the dependent chain after it starts at the threshold probes: the sampling step's inputs
+  // (partial norms split over lanes: lane 8 j + 4 cls + k sums chain k of class cls of output
+  // j, qn_norm_chain's order).  (Holding the thresholds' first probe or the first block's group
+  // minima across the barrier as well spilled registers at the 5-waves bound.)
+  const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
+  const uint4* gmin = (const uint4*)kd.gbox + gbase;
+  const double* tv = kd.sv + (size_t)s * M * stride;
+  const int B1 = (stride + 63) >> 6;
+  double yl = 0.0, part = 0.0;
+  double hv = 0.0, zv = 0.0, am = 0.0;
+  if (cin && smp.R) {
+    const long long Rr = (long long)smp.n + smp.nb + smp.nh + 1;
+    if (lane < 8 * M) {
+      const int j = lane >> 3, cls = (lane >> 2) & 1, k = lane & 3;
+      part = qn_norm_chain(smp.P + (size_t)j * smp.nrt * 2 * b, smp.nrt_used, b, c, cls, k);
+    }
+    if (lane < M) {
+      const double* Rj = smp.R + (size_t)lane * Rr * b;
+      hv = smp.nh ? Rj[(size_t)(smp.n + smp.nb + s) * b + c] : 0.0;
+      zv = smp.zq[(size_t)s * M + lane];
+      am = Rj[(size_t)(Rr - 1) * b + c];
+    }
+  } else if (cin && lane < M) {
+    yl = G[((size_t)s * M + lane) * b + c];
+  }
   {
     const double* src = kd.pts + (size_t)s * stride * M;
     for (int e = tid; e < stride * M; e += 256) pt[e] = src[e];
   }
   __syncthreads();
-  const int c = cg * KW_WAVES + wave;
-  if (c >= b) return;
+  if (!cin) return;
+  // the thresholds' first probe (bucket ends) overlaps the sampling step below
+  double v1[M];
+  {
+    const int i1 = min((lane + 1) * B1, stride) - 1;
+#pragma unroll
+    for (int j = 0; j < M; ++j) v1[j] = tv[(size_t)j * stride + i1];
+  }
 
   // ---- y_j (lane j < M), then to every lane ----
-  double yl = 0.0;
-  if (lane < M) {
-    const int j = lane;
-    if (smp.R) {
-      const long long Rr = (long long)smp.n + smp.nb + smp.nh + 1;
-      const double* Rj = smp.R + (size_t)j * Rr * b;
-      const double hv = smp.nh ? Rj[(size_t)(smp.n + smp.nb + s) * b + c] : 0.0;
-      const double zv = smp.zq[(size_t)s * M + j];
+  if (smp.R) {
+    const int q = lane & ~3;   // the four chains of this lane's (output, class), fixed order
+    const double tot = (__shfl(part, q, 64) + __shfl(part, q + 1, 64)) + (__shfl(part, q + 2, 64) + __shfl(part, q + 3, 64));
+    const double ssv = __shfl(tot, 8 * (lane & 7), 64), ssw = __shfl(tot, 8 * (lane & 7) + 4, 64);
+    if (lane < M) {
+      const int j = lane;
       double mu, l22;
       int flag;
-      qn_mu_l22(smp.P + (size_t)j * smp.nrt * 2 * b, smp.nrt_used, b, c, Rj[(size_t)(Rr - 1) * b + c], smp.ys[j],
-                smp.cc[j], smp.ym[j], smp.kxx[j], mu, l22, flag);
+      qn_mu_l22_from(ssv, ssw, am, smp.ys[j], smp.cc[j], smp.ym[j], smp.kxx[j], mu, l22, flag);
       if (s == 0) {
         smp.L22[(size_t)j * b + c] = l22;
         smp.flags[(size_t)j * b + c] = flag;
       }
       yl = qn_sample_obj(mu, hv, smp.nh != 0, l22, zv, smp.oa[j], smp.ob[j]);
-    } else {
-      yl = G[((size_t)s * M + j) * b + c];
     }
   }
   double y[M];
@@ -2140,12 +2170,6 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   // ---- thresholds: two wave-wide probes per objective ----
   unsigned int tw[4] = {0x00010001u, 0x00010001u, 0x00010001u, 0x00010001u};   // t = 1 beyond M (as kdb)
   {
-    const double* tv = kd.sv + (size_t)s * M * stride;
-    const int B1 = (stride + 63) >> 6;
-    const int i1 = min((lane + 1) * B1, stride) - 1;
-    double v1[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) v1[j] = tv[(size_t)j * stride + i1];
     int base[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) base[j] = min(__popcll(__ballot(v1[j] <= y[j])) * B1, stride);
@@ -2169,8 +2193,6 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   //      groups compacted in group order; C. rounds of 64 passing groups, one per lane (rank
   //      rows loaded together): cell masks, the passing cells' key indices appended to the
   //      term list in (group, cell) order, full rounds of 64 terms evaluated as they fill ----
-  const int gbase = kd.goff[s], Gs = kd.goff[s + 1] - gbase;
-  const uint4* gmin = (const uint4*)kd.gbox + gbase;
   double acc[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.0;
@@ -2246,8 +2268,8 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
 #pragma unroll
     for (int k = 0; k < KW_NCH; ++k) {
       const int g = G0 + 64 * k + lane;
-      // past the sample's groups: 0x7FFF ranks (cells_kd's padding), which fail the packed signed
-      // compare (0xFFFF would read as -1 and pass)
+      // past the sample's groups: 0x7FFF ranks (cells_kd's padding), which fail the packed
+      // signed compare (0xFFFF would read as -1 and pass)
       gm[k] = (k < nch && g < Gs) ? gmin[g] : make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
     }
     // B. the passing groups, compacted in group order (chunk-major, lane order within a chunk)

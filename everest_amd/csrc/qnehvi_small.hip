@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
   __shared__ double Ks[QS_KC][QS_B + 1];         // 128 x b slice of K_x,j (33.8 KB)
   __shared__ double red[4][QS_FR][QS_B + 1];
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Kj = Kx + (size_t)j * n * b;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
   __shared__ double uc[QS_B][UP];
   __shared__ double red[4][QS_FR][QS_B + 1];
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
   const double* Mj = M + (size_t)j * Rr * n;
   const double* lsj = ls + (size_t)j * d;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
   auto dk = reinterpret_cast<double(*)[QS_BI][QS_B + 1]>(lds);
   auto gx = reinterpret_cast<double(*)[QS_B][QS_MAXD]>(lds + DK_SZ);
   const int tile = blockIdx.x, j = blockIdx.y, z = blockIdx.z, i0 = tile * QS_BI;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Rr = n + nb + nh + 1;
   // this split's rows of M; the mean row (Rr - 1, a rank-1 term) is added in the epilogue
   const int rbeg = z * rows_per, rend = min(Rr - 1, rbeg + rows_per);

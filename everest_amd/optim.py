@@ -374,7 +374,8 @@ class _FixedFeatures:
 def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int, options: dict,
                   gen: torch.Generator, inequality_constraints: Sequence[LinearConstraint] = (),
                   equality_constraints: Sequence[LinearConstraint] = (), dist=None,
-                  stats: Optional[OptimizeStats] = None, fixed_features: Optional[dict] = None, q: int = 1):
+                  stats: Optional[OptimizeStats] = None, fixed_features: Optional[dict] = None, q: int = 1,
+                  on_init: Optional[Callable[[], None]] = None):
     """Returns (best x, best value, stats); x is (d,) for q = 1, else the joint (q, d) batch
     ([upstream] optimize_acqf(q=...), sequential=False).  ``acqf`` exposes forward(X) and
     forward_backward(X) on device tensors of raw (transformed) inputs, X b x d (q = 1) or
@@ -392,7 +393,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         x, v, st = optimize_acqf(wrap, bounds[:, wrap.free], num_restarts, raw_samples, options, gen,
                                  _reduce_constraints(inequality_constraints, fx, wrap.free),
                                  _reduce_constraints(equality_constraints, fx, wrap.free), dist=dist, stats=stats,
-                                 q=q)
+                                 q=q, on_init=on_init)
         return wrap.full_np(x), v, st
     import time
 
@@ -437,6 +438,8 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     init = initialize_q_batch if getattr(acqf, "log_acqf", False) else initialize_q_batch_nonneg
     X0, _ = init(X_raw, Y_raw, num_restarts, gen)
     stats.init_X = X0
+    if on_init is not None:
+        on_init()    # the generator's draws of this ask are done (e.g. the next ask's prefetch)
 
     # 4. restarts, chunks of batch_limit, L-BFGS-B (box) / SLSQP (linear constraints) on host
     #    with the analytic device value+gradient

@@ -370,9 +370,11 @@ class BotorchStrategy(PredictiveStrategy):
                                                 self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
                                                 q=q)
         else:
+            # the next ask's first draws are known once the Boltzmann initialisation has drawn:
+            # its prefetch overlaps the restart loop
             x, val, stats = optimize_acqf(acqf, self._bounds(), self.num_restarts, self.num_raw_samples,
                                           self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
-                                          fixed_features=combos[0] or None, q=q)
+                                          fixed_features=combos[0] or None, q=q, on_init=self._prefetch_next_ask)
         stats.best_value = val
         self.last_ask_stats = stats
         out = self._postprocess_candidates(x.reshape(q, -1))

@@ -9,6 +9,7 @@
 #               evaluation) -> <tag>/restart_ab.json
 #   asktl       device timeline of one ask (tools/ask_timeline.py under rocprofv3 --kernel-trace)
 #               -> <tag>/ask_timeline.json
+#   planprobe   tools/plan_setup_probe.py (restart plan creation / first / warm evaluation)
 #   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
@@ -46,6 +47,7 @@ for st in "$@"; do
     asktl)
       run asktl_trace 300 rocprofv3 --kernel-trace -d "$OUT/asktl" -o run --output-format csv -- python tools/ask_timeline.py
       run asktl_parse 60 python tools/ask_timeline.py --analyse "$OUT/asktl" "$OUT/asktl_trace.log" && cp "$OUT/asktl_parse.log" "$OUT/ask_timeline.json" ;;
+    planprobe) run planprobe 300 python tools/plan_setup_probe.py ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
