@@ -47,7 +47,7 @@ def per_step(d, counter):
         with open(path) as f:
             rows += [r for r in csv.DictReader(f) if r.get("Counter_Name") == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    steps, cur, prev, names = [], None, None, defaultdict(set)
+    steps, snames, cur, prev = [], [], None, None
     for r in rows:
         op = label(r["Kernel_Name"], prev)
         if op is None:
@@ -55,11 +55,16 @@ def per_step(d, counter):
         if op == "kernel_matrix":
             cur = defaultdict(float)
             steps.append(cur)
+            snames.append(defaultdict(set))
         if cur is None:
             continue
         cur[op] += float(r["Counter_Value"]) * 1024.0   # KiB -> B
-        names[op].add(r["Kernel_Name"].split("(")[0][:80])
+        snames[-1][op].add(r["Kernel_Name"].split("(")[0][:80])
         prev = op
+    names = defaultdict(set)   # the kernels of the steps counted (not of the set-up before them)
+    for sn in snames[-LAST:]:
+        for op, ks in sn.items():
+            names[op] |= ks
     return steps[-LAST:], names
 
 
