@@ -40,6 +40,7 @@ size_t qs_norms_doubles(const evr_qnehvi_state* st, int b);
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
+int qs_done_words(int b, int d);
 int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                  double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
@@ -130,7 +131,8 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
-  unsigned int* counter;         // blocks-done counter of the fused copy-out (qs_dx_reduce)
+  unsigned int* counter;         // (kept for the recycled-resource layout; unused since round 4)
+  int nwords;                    // completion words the host graph's last kernel writes
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
 };
 
@@ -157,7 +159,8 @@ __global__ __launch_bounds__(256) void plan_copy_out(int b, int n, const double*
 
 // The chain on candidates X (device buffer, or in the host graph the pinned host buffer
 // itself).  Host mode (hout): the b <= 32 backward's dX reduction also writes [acq | dX] and
-// the completion word to hout (*done = 1); otherwise the caller appends a copy-out kernel.
+// one completion word per reduction workgroup to hout (*done = their number); otherwise
+// (*done = 0) the caller appends a copy-out kernel (one word).
 static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, double* hout = nullptr,
                       const double* seqp = nullptr, unsigned int* counter = nullptr, int* done = nullptr) {
   const evr_qnehvi_state* st = &p->st;
@@ -192,7 +195,7 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     if (int rc = hvi_kdb_fused(s, st, b, R, P, cdiv(qn_rows(st), QS_TILE_ROWS), cdiv(st->n + st->nb, QS_TILE_ROWS),
                                L22, flags, hw, dG))
       return rc;
-    if (done) *done = hout ? 1 : 0;
+    if (done) *done = hout ? qs_done_words(b, d) : 0;
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
                        hw, flags);
   }
@@ -202,13 +205,13 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     // one launch for thresholds + scan + split reduction (hvi_kd3); the per-sample values in
     // the scan workspace become acq inside the dX reduction
     if (int rc = evr_hvi_restart_fb(s, st, b, G, hw, dG)) return rc;
-    if (done) *done = hout ? 1 : 0;
+    if (done) *done = hout ? qs_done_words(b, d) : 0;
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
                        hw, flags);
   }
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (small) {
-    if (done) *done = hout ? 1 : 0;
+    if (done) *done = hout ? qs_done_words(b, d) : 0;
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
                        nullptr, nullptr);
   }
@@ -274,6 +277,7 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->hgraph = nullptr;
   p->hexec = nullptr;
   p->seq = 0;
+  p->nwords = 1;
   p->counter = nullptr;
   if (int rc = gemm_backend_init()) {
     delete p;
@@ -371,10 +375,10 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   if (!p->hx)
     EVR_HIP(hipHostMalloc((void**)&p->hx, sizeof(double) * (n + 1), hipHostMallocMapped | hipHostMallocCoherent));
   if (!p->hout)
-    EVR_HIP(hipHostMalloc((void**)&p->hout, sizeof(double) * ((size_t)b * (1 + p->md.d) + 1),
+    EVR_HIP(hipHostMalloc((void**)&p->hout, sizeof(double) * ((size_t)b * (1 + p->md.d) + 64),
                           hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(p->hx, 0, sizeof(double) * (n + 1));
-  std::memset(p->hout, 0, sizeof(double) * ((size_t)b * (1 + p->md.d) + 1));
+  std::memset(p->hout, 0, sizeof(double) * ((size_t)b * (1 + p->md.d) + 64));
   double *dhx = nullptr, *dhout = nullptr;
   EVR_HIP(hipHostGetDevicePointer((void**)&dhx, p->hx, 0));
   EVR_HIP(hipHostGetDevicePointer((void**)&dhout, p->hout, 0));
@@ -389,6 +393,7 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     int done = 0;
     rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
+    p->nwords = done > 0 ? done : 1;
   }
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);
@@ -426,15 +431,21 @@ static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
   std::memcpy(p->hx + n, &seq, sizeof(seq));
   std::atomic_thread_fence(std::memory_order_seq_cst);
   EVR_HIP(hipGraphLaunch(p->hexec, s));
-  // spin on the completion word; every 256 polls ask the stream whether it has drained (a
+  // spin on the completion words; every 256 polls ask the stream whether it has drained (a
   // faulted or failed launch ends the wait with its error instead of spinning forever)
   volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
-  for (unsigned k = 1; *done != seq; ++k) {
+  const int nw = p->nwords;
+  auto finished = [&]() {
+    for (int w = 0; w < nw; ++w)
+      if (done[w] != seq) return false;
+    return true;
+  };
+  for (unsigned k = 1; !finished(); ++k) {
     if ((k & 255) == 0) {
       const hipError_t q = hipStreamQuery(s);
       if (q == hipErrorNotReady) continue;
       EVR_HIP(q);
-      if (*done != seq) EVR_CHECK(false, "qnehvi plan: evaluation finished without its completion word");
+      if (!finished()) EVR_CHECK(false, "qnehvi plan: evaluation finished without its completion words");
     }
   }
   std::atomic_thread_fence(std::memory_order_seq_cst);

@@ -480,11 +480,11 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
 // one wave per dX element (4 per workgroup): lane-strided partial sums over the element's
 // contiguous partials, then a fixed xor-butterfly.  Host mode (hout != nullptr, the plan's host
 // graph): every wave also writes its dX element (and the first b acq) to the pinned host
-// buffer; after a system-scope fence each workgroup counts itself done, and the last one
-// resets the counter and writes the evaluation's sequence number into the completion word the
-// host spins on (no separate copy-out kernel).  The sequence number (written by the host
-// before the graph launch) is read at kernel entry by every workgroup's thread 0, so its PCIe
-// round trip overlaps the sums instead of trailing the last workgroup's atomic.
+// buffer and fences it at system scope; after a workgroup barrier thread 0 writes the
+// evaluation's sequence number into the workgroup's own completion word (hout[b + b d + w]);
+// the host waits for all of them (no inter-workgroup counter, no second fence round, no
+// separate copy-out kernel).  The sequence number (written by the host before the graph
+// launch) is read at kernel entry, so its PCIe round trip overlaps the sums.
 //
 // With sval (the fused restart scan, hvi_kd3, leaves per-sample values sval[s][c]) the waves of
 // the first b elements also form acq[c] = mean over the S samples (lane-strided, then the
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
 __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const double* __restrict__ dXp,
                                                     const double* __restrict__ scale, double* __restrict__ dX,
                                                     double* __restrict__ acq, double* hout,
-                                                    const double* seqp, unsigned int* counter,
+                                                    const double* seqp,
                                                     const double* __restrict__ sval, int S, int m,
                                                     const int* __restrict__ flags) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -549,14 +549,7 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   }
   if (hout) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned int prev = atomicAdd(counter, 1u);
-      if (prev == gridDim.x - 1) {
-        atomicExch(counter, 0u);
-        __threadfence_system();
-        *(volatile unsigned long long*)(hout + b + (size_t)b * d) = seq;
-      }
-    }
+    if (threadIdx.x == 0) *(volatile unsigned long long*)(hout + b + (size_t)b * d + blockIdx.x) = seq;
   }
 }
 
@@ -579,6 +572,9 @@ static int qs_rows_per(const evr_qnehvi_state* st) {
   const int nch = cdiv(qn_rows(st) - 1, QS_RC);
   return cdiv(nch, qs_zsplit(st)) * QS_RC;
 }
+
+// workgroups of qs_dx_reduce = completion words it writes in host mode (<= 64 at b <= 32, d <= 8)
+int qs_done_words(int b, int d) { return cdiv(b * d, 4); }
 
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
   return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
@@ -620,8 +616,9 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                                             L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
                                             md->lengthscales, dXp, nt, rows_per);
   EVR_LAUNCH_CHECK();
-  qs_dx_reduce<<<cdiv(b * d, 4), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, counter,
-                                               sval, st->S, st->m, flags);
+  (void)counter;
+  qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, sval,
+                                                   st->S, st->m, flags);
   EVR_LAUNCH_CHECK();
   return 0;
 }
