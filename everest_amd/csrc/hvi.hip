@@ -2106,6 +2106,11 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
                        (size_t)wave * 64 * KW_NCH;
   const int c = cg * KW_WAVES + wave;
   const bool cin = c < b;
+  // EVR_KD_PROF=2 build: per (sample, candidate) wall-clock stamps (s_memrealtime, 10 ns):
+  // start, after staging, after the thresholds, time in the group / cell phases, time in the
+  // term rounds, end; term and passing-group counts (tools/kdw_waves.py)
+  unsigned long long pf_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (EVR_KD_PROF == 2) pf_[0] = wall_clock64();
   // Every load that depends only on (sample, candidate) is issued before the staging barrier,
   // so the dependent chain after it starts at the threshold probes: the sampling step's inputs
   // (partial norms split over lanes: lane 8 j + 4 cls + k sums chain k of class cls of output
@@ -2138,6 +2143,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   }
   __syncthreads();
   if (!cin) return;
+  if (EVR_KD_PROF == 2) pf_[1] = wall_clock64();
   // the thresholds' first probe (bucket ends) overlaps the sampling step below
   double v1[M];
   {
@@ -2187,6 +2193,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     }
   }
   const uint4 tt = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+  if (EVR_KD_PROF == 2) pf_[2] = wall_clock64();
 
   // ---- the sample's groups in blocks of KW_NCH chunks of 64 (lane = group of a chunk):
   //      A. every chunk's group test, all minima loads in flight together; B. the passing
@@ -2261,6 +2268,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     return mB;
   };
   int tn = 0;   // terms in the list (wave-uniform)
+  unsigned long long pf_mark = EVR_KD_PROF == 2 ? wall_clock64() : 0;
   for (int G0 = 0; G0 < Gs; G0 += 64 * KW_NCH) {
     const int nch = min(KW_NCH, (Gs - G0 + 63) >> 6);
     // A. group tests of up to KW_NCH chunks: one minima load per chunk and lane, all in flight
@@ -2280,6 +2288,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
       if (bal >> lane & 1ull) pl[np_ + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)(64 * k + lane);
       np_ += __popcll(bal);
     }
+    if (EVR_KD_PROF == 2) pf_[7] += np_;
     wave_sync();
     // C. pair rounds of 64, one passing group per lane (its rank rows loaded together): cell
     //    masks -> the cells' key indices appended in (group, cell) order, term rounds as they fill
@@ -2301,7 +2310,18 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
       wave_sync();
       const int nr = tn >> 6;
       if (nr > 0) {
+        if (EVR_KD_PROF == 2) {
+          const unsigned long long t = wall_clock64();
+          pf_[3] += t - pf_mark;
+          pf_mark = t;
+          pf_[6] += 64ull * nr;
+        }
         rounds(nr, 0);
+        if (EVR_KD_PROF == 2) {
+          const unsigned long long t = wall_clock64();
+          pf_[4] += t - pf_mark;
+          pf_mark = t;
+        }
         const int rem = tn - nr * 64;
         const unsigned short keep = lane < rem ? tl[nr * 64 + lane] : (unsigned short)0;
         wave_sync();
@@ -2312,7 +2332,14 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     }
     wave_sync();   // pl is rewritten by the next block of chunks
   }
+  if (EVR_KD_PROF == 2) {
+    const unsigned long long t = wall_clock64();
+    pf_[3] += t - pf_mark;
+    pf_mark = t;
+    pf_[6] += tn;
+  }
   rounds(0, tn);
+  if (EVR_KD_PROF == 2) pf_[4] += wall_clock64() - pf_mark;
   // ---- per value the lanes' sums, fixed butterfly ----
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
@@ -2325,6 +2352,12 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     sval[(size_t)s * b + c] = acc[0];
 #pragma unroll
     for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = 1.0 / (double)S * acc[1 + j];
+  }
+  if (EVR_KD_PROF == 2 && kd.counters && lane == 0) {
+    pf_[5] = wall_clock64();
+    unsigned long long* r = kd.counters + 16 + 8 * ((size_t)s * b + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r[q] = pf_[q];
   }
 }
 

@@ -10,13 +10,15 @@
 #   asktl       device timeline of one ask (tools/ask_timeline.py under rocprofv3 --kernel-trace)
 #               -> <tag>/ask_timeline.json
 #   planprobe   tools/plan_setup_probe.py (restart plan creation / first / warm evaluation)
+#   hostprof    tools/ask_host_profile.py (cProfile of 5 warm asks)
 #   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
 #   pmc512      the same over the b = 512 evaluation pass (keys without suffix)
 #   sq20        SQ wave-cycle split of the restart chain kernels (hvi_kdw, qs_fwd, qs_bwd) at b = 20
-#   kdwaves     per-wave phase stamps of the restart scan (EVR_KD_PROF=2 build in _libprof/)
+#   kdwaves     per-wave phase stamps of hvi_kd3 / hvi_kdb (EVR_KD_PROF=2 build in _libprof/)
+#   kdwwaves    per-(sample, candidate) phase stamps of hvi_kdw (EVR_KD_PROF=2 build in _libkdprof/)
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
@@ -48,6 +50,7 @@ for st in "$@"; do
       run asktl_trace 300 rocprofv3 --kernel-trace -d "$OUT/asktl" -o run --output-format csv -- python tools/ask_timeline.py
       run asktl_parse 60 python tools/ask_timeline.py --analyse "$OUT/asktl" "$OUT/asktl_trace.log" && cp "$OUT/asktl_parse.log" "$OUT/ask_timeline.json" ;;
     planprobe) run planprobe 300 python tools/plan_setup_probe.py ;;
+    hostprof) run hostprof 300 python tools/ask_host_profile.py ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
@@ -63,6 +66,7 @@ for st in "$@"; do
     sq20)
       run sq20 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "hvi_kd[bw]|qs_fwd|qs_bwd|kmat_kernel|qs_dx" -d "$OUT/sq20" -o run --output-format csv -- python tools/loop_step.py 10 20 ask
       run sq20_parse 60 python tools/pmc_sq.py "$OUT/sq20" "$OUT/sq_counters.json" ;;
+    kdwwaves) EVR_LIB_PATH=everest_amd/_libkdprof/libeverest_amd.so run kdwwaves 300 python tools/kdw_waves.py ;;
     kdwaves) EVR_LIB_PATH=everest_amd/_libprof/libeverest_amd.so run kdwaves 300 python tools/kd3_waves.py ;;
     bench) run bench 900 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
