@@ -2138,8 +2138,23 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     yl = G[((size_t)s * M + lane) * b + c];
   }
   {
+    // the point table: a thread's loads all in flight before its LDS stores (a load -> store
+    // loop waits on every load in turn)
     const double* src = kd.pts + (size_t)s * stride * M;
-    for (int e = tid; e < stride * M; e += 256) pt[e] = src[e];
+    const int ne = stride * M;
+    for (int e0 = 0; e0 < ne; e0 += 8 * 256) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256 + tid;
+        v[u] = e < ne ? src[e] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256 + tid;
+        if (e < ne) pt[e] = v[u];
+      }
+    }
   }
   __syncthreads();
   if (!cin) return;
@@ -2230,14 +2245,20 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   auto rounds = [&](const int nr, const int part) {
     const int last = part > 0 ? nr : nr - 1;   // index of the final round
     if (last < 0) return;
+    // every round issues exactly one, unconditional key load (lanes past the list read the
+    // sample's first key; the last round reloads its own), so the wait before a round's terms
+    // counts only that round's load (vmcnt(1)) and the next round's load stays in flight —
+    // a conditional load merges at the loop head and forces vmcnt(0)
     auto ld = [&](const int r) -> unsigned long long {
       const int t = r * 64 + lane;
       const bool in = r < nr || lane < part;
-      return in ? kd.gkeys[(size_t)gbase * 16 + tl[t]] : 0ull;
+      const unsigned int ix = in ? (unsigned int)tl[t] : 0u;
+      return kd.gkeys[(size_t)gbase * 16 + ix];
     };
     unsigned long long kc = ld(0);
     for (int r = 0; r <= last; ++r) {
-      const unsigned long long kn = r < last ? ld(r + 1) : 0ull;   // the next round's key in flight
+      const unsigned long long kn = ld(min(r + 1, last));
+      __asm__ volatile("" ::: "memory");   // keep the next key's load issued before this round's terms
       if (r < nr || lane < part) term_add(kc);
       kc = kn;
     }
