@@ -282,13 +282,26 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
 // cross-covariance gradient partial dXp[c][k][(j, z, tile)].  gR rows come from R (rows
 // < n + nb, times the per-candidate coefficients), a_j dG (sample rows) or the coefficient
 // itself (mean row); the chunk of 128 rows of M (16 columns) and of the gR sources is loaded
-// with coalesced row segments, the coefficients applied while staging in LDS.
+// with coalesced row segments.  The per-candidate coefficients scale whole row classes, so
+// each class is summed apart and scaled in the epilogue, and the coefficients' own reduction
+// over the samples overlaps the chunk loop.
 // ---------------------------------------------------------------------------------------
 constexpr int QS_RC = 128;   // rows of M per backward chunk
+#ifdef EVR_QS_PROF
+// tools/qs_prof.hip: per-workgroup wall-clock stamps of qs_bwd (s_memrealtime, 10 ns)
+__device__ unsigned long long qs_prof[4096 * 8];
+#define QS_STAMP(k) do { if (threadIdx.x == 0) qs_prof[(size_t)qs_bid * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define QS_STAMP(k) do { } while (0)
+#endif
 // (256, 2): two waves per SIMD, i.e. two workgroups per CU — without the bound the compiler
 // took 244 VGPRs + 16 AGPRs (one workgroup per CU: the 480 workgroups of the bench shape ran
-// in two rounds); bounded it fits 226 registers without scratch
-__global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
+// in two rounds); bounded it fits 248 registers without scratch
+constexpr int QS_SMAX = 1024;   // samples whose z values the backward stages in LDS
+// SPLIT: baseline rows in M (nb > 0, the literal "split" root, A/B only): a third row class;
+// one workgroup per CU there (its registers would spill at two)
+template <bool SPLIT>
+__global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
                                               const double* __restrict__ M, const double* __restrict__ R,
                                               const double* __restrict__ dG, const double* __restrict__ L22,
                                               const double* __restrict__ ys, const double* __restrict__ zq,
@@ -298,6 +311,7 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
                                               double* __restrict__ dXp, int ntile, int rows_per) {
   __shared__ double cf[3][QS_B];
   __shared__ double red[8][QS_B][2];
+  __shared__ double zl[QS_SMAX];   // z_j of the samples (the coefficient rounds read them here)
   // the chunk tiles and the epilogue's reduction buffers share one LDS region (~53 KB per
   // workgroup, two resident per CU)
   constexpr int MS_SZ = QS_RC * (QS_BI + 1), BS_SZ = QS_RC * (QS_B + 1);
@@ -311,6 +325,10 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
   const int tile = blockIdx.x, j = blockIdx.y, z = blockIdx.z, i0 = tile * QS_BI;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Rr = n + nb + nh + 1;
+#ifdef EVR_QS_PROF
+  const int qs_bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+#endif
+  QS_STAMP(0);
   // this split's rows of M; the mean row (Rr - 1, a rank-1 term) is added in the epilogue
   const int rbeg = z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
   const double aj = oa[j], sj = ys[j];
@@ -344,49 +362,44 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
     }
   };
   load(rbeg);
-  // 1. gR coefficients of this output (qn_bwd_coef's algebra): dmu = sum_s a dG, dl = sum_s a dG z
-  {
-    const int c = tid & (QS_B - 1), g = tid >> 5;   // 8 sample groups
-    double dmu = 0.0, dl = 0.0;
-    if (c < b) {
-      constexpr int CU = 16;   // loads of 16 samples in flight, summed in sample order
-      for (int s0 = g; s0 < S; s0 += 8 * CU) {
-        double dv[CU], zv[CU];
+  // 1. gR coefficients of this output (qn_bwd_coef's algebra): dmu = sum_s a dG, dl = sum_s a dG z,
+  //    thread (candidate c, sample group g of 8), rounds of 16 samples summed in sample order.
+  //    They scale only whole row classes of gR, so they are applied to the class sums in the
+  //    epilogue: the rounds' loads ride along with the chunk loads below (round k is consumed
+  //    after chunk k's MFMAs) instead of standing before the first chunk.
+  const int cc_ = tid & (QS_B - 1), g_ = tid >> 5;
+  constexpr int CU = SPLIT ? 16 : 12;   // samples per thread and round: the most that stay in registers
+  double dmu = 0.0, dl = 0.0;
+  double dv[CU];
+  int s0 = g_;
+  auto coef_load = [&]() {
 #pragma unroll
-        for (int u = 0; u < CU; ++u) {
-          const int s = s0 + 8 * u;
-          dv[u] = s < S ? dG[((size_t)s * m + j) * b + c] : 0.0;
-          zv[u] = s < S ? zq[(size_t)s * m + j] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < CU; ++u) {
-          const double dy = aj * dv[u];
-          dmu += dy;
-          dl = fma(dy, zv[u], dl);
-        }
-      }
+    for (int u = 0; u < CU; ++u) {
+      const int s = s0 + 8 * u;
+      dv[u] = (cc_ < b && s < S) ? dG[((size_t)s * m + j) * b + cc_] : 0.0;
     }
-    red[g][c][0] = dmu;
-    red[g][c][1] = dl;
-    __syncthreads();
-    if (tid < QS_B) {
-      double u = red[0][tid][0], v = red[0][tid][1];
+  };
+  auto coef_acc = [&]() {
 #pragma unroll
-      for (int q = 1; q < 8; ++q) {
-        u += red[q][tid][0];
-        v += red[q][tid][1];
-      }
-      const double dbr = tid < b ? v / (2.0 * L22[(size_t)j * b + tid]) : 0.0;
-      cf[0][tid] = -2.0 * sj * sj * dbr;
-      cf[1][tid] = -2.0 * dbr;
-      cf[2][tid] = sj * u;
+    for (int u = 0; u < CU; ++u) {
+      const int s = s0 + 8 * u;
+      const double dy = aj * dv[u];
+      dmu += dy;
+      dl = fma(dy, s < S ? zl[s] : 0.0, dl);
     }
-  }
-  // 2. dK tile: D[i][c] = sum_r M[r][i0 + i] gR[r][c] over chunks of 128 rows
+    s0 += 8 * CU;
+  };
+  for (int e = tid; e < S; e += 256) zl[e] = zq[(size_t)e * m + j];   // visible after the first chunk's barrier
+  bool pend = s0 < S;
+  if (pend) coef_load();
+  QS_STAMP(1);
+  // 2. dK tile by row class: A (rows < n, scaled by cf0 in the epilogue), C (n <= r < n + nb,
+  //    cf1), B (sample rows, a_j applied while staging): D_X[i][c] = sum_r M[r][i0 + i] src[r][c]
   const int i = lane & 15, kq = lane >> 4;
-  double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  double4_t aA0 = {0, 0, 0, 0}, aA1 = {0, 0, 0, 0}, aB0 = {0, 0, 0, 0}, aB1 = {0, 0, 0, 0};
+  double4_t aC0 = {0, 0, 0, 0}, aC1 = {0, 0, 0, 0};
   for (int rc = rbeg; rc < rend; rc += QS_RC) {
-    __syncthreads();   // coefficients ready / the previous chunk's MFMAs are done with Ms, Bs
+    __syncthreads();   // the previous chunk's MFMAs are done with Ms, Bs
 #pragma unroll
     for (int u = 0; u < ML; ++u) {
       const int e = u * 256 + tid;
@@ -395,22 +408,70 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
 #pragma unroll
     for (int u = 0; u < BL; ++u) {
       const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
-      double v = bv[u];
-      if (r < n) v *= cf[0][c];
-      else if (r < n + nb) v *= cf[1][c];
-      else v *= aj;
-      Bs[rr][c] = v;
+      Bs[rr][c] = r >= n + nb ? bv[u] * aj : bv[u];
     }
     __syncthreads();
     if (rc + QS_RC < rend) load(rc + QS_RC);
+    const int lo_r = rc + wave * (QS_RC / 4), hi_r = lo_r + QS_RC / 4 - 1;
+    if (hi_r < n) {
 #pragma unroll
-    for (int t = 0; t < QS_RC / 16; ++t) {
-      const int rr = wave * (QS_RC / 4) + 4 * t + kq;
-      const double a = Ms[rr][i];
-      acc0 = mfma4(a, Bs[rr][i], acc0);
-      acc1 = mfma4(a, Bs[rr][i + 16], acc1);
+      for (int t = 0; t < QS_RC / 16; ++t) {
+        const int rr = wave * (QS_RC / 4) + 4 * t + kq;
+        const double a = Ms[rr][i];
+        aA0 = mfma4(a, Bs[rr][i], aA0);
+        aA1 = mfma4(a, Bs[rr][i + 16], aA1);
+      }
+    } else if (lo_r >= n + nb) {
+#pragma unroll
+      for (int t = 0; t < QS_RC / 16; ++t) {
+        const int rr = wave * (QS_RC / 4) + 4 * t + kq;
+        const double a = Ms[rr][i];
+        aB0 = mfma4(a, Bs[rr][i], aB0);
+        aB1 = mfma4(a, Bs[rr][i + 16], aB1);
+      }
+    } else {   // a slice across a class boundary: each class's rows through its own sums
+#pragma unroll
+      for (int t = 0; t < QS_RC / 16; ++t) {
+        const int rr = wave * (QS_RC / 4) + 4 * t + kq, r = rc + rr;
+        const double a = Ms[rr][i], b0 = Bs[rr][i], b1 = Bs[rr][i + 16];
+        const double xa = r < n ? a : 0.0, xb = r >= n + nb ? a : 0.0, xc_ = (r >= n && r < n + nb) ? a : 0.0;
+        aA0 = mfma4(xa, b0, aA0);
+        aA1 = mfma4(xa, b1, aA1);
+        aB0 = mfma4(xb, b0, aB0);
+        aB1 = mfma4(xb, b1, aB1);
+        if (SPLIT) {
+          aC0 = mfma4(xc_, b0, aC0);
+          aC1 = mfma4(xc_, b1, aC1);
+        }
+      }
+    }
+    if (pend) {   // the coefficient round issued with this chunk's loads
+      coef_acc();
+      pend = s0 < S;
+      if (pend) coef_load();
     }
   }
+  while (pend) {
+    coef_acc();
+    pend = s0 < S;
+    if (pend) coef_load();
+  }
+  red[g_][cc_][0] = dmu;
+  red[g_][cc_][1] = dl;
+  __syncthreads();
+  if (tid < QS_B) {
+    double u = red[0][tid][0], v = red[0][tid][1];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      u += red[q][tid][0];
+      v += red[q][tid][1];
+    }
+    const double dbr = tid < b ? v / (2.0 * L22[(size_t)j * b + tid]) : 0.0;
+    cf[0][tid] = -2.0 * sj * sj * dbr;
+    cf[1][tid] = -2.0 * dbr;
+    cf[2][tid] = sj * u;
+  }
+  QS_STAMP(2);
   // the epilogue's training rows and mean-row entries, loaded before the dk exchange so their
   // latency overlaps it: thread (candidate c, row group g) uses rows i0 + g and i0 + g + 8
   double xr[2][QS_MAXD], mrow[2];
@@ -425,13 +486,22 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
       mrow[h] = (in && z == 0) ? Mj[(size_t)(Rr - 1) * n + irow] : 0.0;
     }
   }
-  __syncthreads();   // all waves are done with Ms, Bs (dk aliases them)
+  __syncthreads();   // all waves are done with Ms, Bs (dk aliases them); cf is ready
+  {
+    const double f0a = cf[0][i], f0b = cf[0][16 + i], f1a = cf[1][i], f1b = cf[1][16 + i];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    dk[wave][4 * q + kq][i] = acc0[q];
-    dk[wave][4 * q + kq][16 + i] = acc1[q];
+    for (int q = 0; q < 4; ++q) {
+      double v0 = fma(f0a, aA0[q], aB0[q]), v1 = fma(f0b, aA1[q], aB1[q]);
+      if (SPLIT) {
+        v0 = fma(f1a, aC0[q], v0);
+        v1 = fma(f1b, aC1[q], v1);
+      }
+      dk[wave][4 * q + kq][i] = v0;
+      dk[wave][4 * q + kq][16 + i] = v1;
+    }
   }
   __syncthreads();
+  QS_STAMP(3);
   // 3. cross-covariance gradient of the tile's rows: thread (candidate c, row group g of 8),
   //    rows i0 + g and i0 + g + 8; dX_c += dK[i][c] dk(x_i, x_c)/dx_c (normalized units)
   {
@@ -475,6 +545,7 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
       if (cc < b && k < d) dXp[((size_t)cc * d + k) * np + ((size_t)j * gridDim.z + z) * ntile + tile] = v;
     }
   }
+  QS_STAMP(4);
 }
 
 // one wave per dX element (4 per workgroup): lane-strided partial sums over the element's
@@ -554,7 +625,9 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
 }
 
 // ---- launchers (qnehvi_plan.hip) ------------------------------------------------------
-bool qs_applies(const evr_qnehvi_state* st, int b, int d) { return b >= 1 && b <= QS_B && d <= QS_MAXD && st->m >= 1; }
+bool qs_applies(const evr_qnehvi_state* st, int b, int d) {
+  return b >= 1 && b <= QS_B && d <= QS_MAXD && st->m >= 1 && st->S <= QS_SMAX;
+}
 
 int qs_ntile_fwd(const evr_qnehvi_state* st) { return cdiv(qn_rows(st), QS_FR); }
 
@@ -612,9 +685,14 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
-  qs_bwd<<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, dG,
-                                            L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift, md->scale,
-                                            md->lengthscales, dXp, nt, rows_per);
+  EVR_CHECK(st->S <= QS_SMAX, "qs_backward: %d samples exceed the staged %d", st->S, QS_SMAX);
+#define QS_BWD(SPL)                                                                                             \
+  qs_bwd<SPL><<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, \
+                                                  dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,        \
+                                                  md->scale, md->lengthscales, dXp, nt, rows_per)
+  if (st->nb > 0) QS_BWD(true);
+  else QS_BWD(false);
+#undef QS_BWD
   EVR_LAUNCH_CHECK();
   (void)counter;
   qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, sval,
