@@ -45,7 +45,7 @@ __device__ __forceinline__ double4_t mfma4(double a, double b, double4_t c) {
 // ---------------------------------------------------------------------------------------
 // forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
+__global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
                                               const double* __restrict__ Kx, double* __restrict__ R,
                                               double* __restrict__ P, int ntile) {
   // padded row of the staged M tile: 2 MP = 4 (mod 64 dwords) puts the 16 rows x 2
@@ -62,11 +62,13 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
   double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
   // coalesced chunk loads into registers (a wave reads 512 contiguous bytes of one M row per
   // instruction; the chunk's K_x rows are one contiguous run of kn x b doubles), staged in
-  // LDS afterwards; the next chunk's loads are issued before the current chunk's MFMAs.
+  // LDS afterwards; two register buffers, so the loads of chunks k + 1 and k + 2 are in flight
+  // while chunk k is staged and multiplied (the K_x values past b x kn are never loaded).
   // K_x rows past the end of a partial chunk are zero (M's are too, but 0 x garbage is not 0).
-  double mv[QS_ML], kv[QS_KL];
+  constexpr int KLB = (QS_KC * QS_B + 255) / 256;
+  double mvA[QS_ML], kvA[KLB], mvB[QS_ML], kvB[KLB];
   const int kk = tid % QS_KC, rh = tid / QS_KC;   // staging: chunk column kk of rows rh, rh + 2, ...
-  auto load = [&](int kc) {
+  auto load = [&](double (&mv)[QS_ML], double (&kv)[KLB], int kc) {
     const int kn = min(QS_KC, n - kc);
 #pragma unroll
     for (int u = 0; u < QS_ML; ++u) {
@@ -74,24 +76,22 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
       mv[u] = (r < Rr && kk < kn) ? Mj[(size_t)r * n + kc + kk] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < QS_KL; ++u) {
+    for (int u = 0; u < KLB; ++u) {
       const int e = u * 256 + tid;
       kv[u] = (e < kn * b) ? Kj[(size_t)kc * b + e] : 0.0;
     }
   };
-  load(0);
-  constexpr int KW = QS_KC / 4;   // k per wave and chunk
-  for (int kc = 0; kc < n; kc += QS_KC) {
-    __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
+  auto stage = [&](const double (&mv)[QS_ML], const double (&kv)[KLB]) {
 #pragma unroll
     for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
 #pragma unroll
-    for (int u = 0; u < QS_KL; ++u) {
+    for (int u = 0; u < KLB; ++u) {
       const int e = u * 256 + tid;
       if (e < QS_KC * b) Ks[e / b][e % b] = kv[u];   // every row of the chunk, columns < b
     }
-    __syncthreads();
-    if (kc + QS_KC < n) load(kc + QS_KC);
+  };
+  constexpr int KW = QS_KC / 4;   // k per wave and chunk
+  auto mult = [&]() {
 #pragma unroll
     for (int t = 0; t < KW / 4; ++t) {
       const int k = wave * KW + 4 * t + kq;
@@ -100,6 +100,21 @@ __global__ __launch_bounds__(256) void qs_fwd(int n, int nb, int Rr, int b, cons
       acc0 = mfma4(a, Ks[k][i], acc0);
       acc1 = mfma4(a, Ks[k][i + 16], acc1);
     }
+  };
+  load(mvA, kvA, 0);
+  if (QS_KC < n) load(mvB, kvB, QS_KC);
+  for (int kc = 0; kc < n; kc += 2 * QS_KC) {
+    __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
+    stage(mvA, kvA);
+    __syncthreads();
+    if (kc + 2 * QS_KC < n) load(mvA, kvA, kc + 2 * QS_KC);
+    mult();
+    if (kc + QS_KC >= n) break;
+    __syncthreads();
+    stage(mvB, kvB);
+    __syncthreads();
+    if (kc + 3 * QS_KC < n) load(mvB, kvB, kc + 3 * QS_KC);
+    mult();
   }
   // D map of v_mfma_f64_16x16x4: register q of lane l holds D[4q + (l >> 4)][l & 15]
 #pragma unroll
@@ -361,6 +376,14 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
       bv[u] = src ? *src : 0.0;
     }
   };
+  // z_j of the samples, loaded first (the LDS store below then waits for these loads only:
+  // vmcnt retires in issue order, and the chunk / coefficient loads are issued after them)
+  double zr[QS_SMAX / 256];
+#pragma unroll
+  for (int u = 0; u < QS_SMAX / 256; ++u) {
+    const int e = tid + 256 * u;
+    zr[u] = e < S ? zq[(size_t)e * m + j] : 0.0;
+  }
   load(rbeg);
   // 1. gR coefficients of this output (qn_bwd_coef's algebra): dmu = sum_s a dG, dl = sum_s a dG z,
   //    thread (candidate c, sample group g of 8), rounds of 16 samples summed in sample order.
@@ -389,9 +412,13 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     }
     s0 += 8 * CU;
   };
-  for (int e = tid; e < S; e += 256) zl[e] = zq[(size_t)e * m + j];   // visible after the first chunk's barrier
   bool pend = s0 < S;
   if (pend) coef_load();
+#pragma unroll
+  for (int u = 0; u < QS_SMAX / 256; ++u) {   // visible after the first chunk's barrier
+    const int e = tid + 256 * u;
+    if (e < S) zl[e] = zr[u];
+  }
   QS_STAMP(1);
   // 2. dK tile by row class: A (rows < n, scaled by cf0 in the epilogue), C (n <= r < n + nb,
   //    cf1), B (sample rows, a_j applied while staging): D_X[i][c] = sum_r M[r][i0 + i] src[r][c]
