@@ -389,6 +389,17 @@ def cpu_full_ask(s, restarts, raw, S, seed=0):
     ref = torch.tensor(s.get_adjusted_refpoint(), dtype=torch.float64)
     out = {}
     t0 = time.perf_counter()
+    # a heartbeat on stderr every 30 s (minutes of CPU work: a silent run looks hung)
+    import threading
+
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(30.0):
+            print(f"[cpu_full_ask] {time.perf_counter() - t0:.0f} s, phases done: {sorted(out)}", file=sys.stderr,
+                  flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     zp = oq.base_samples(2048, Xn.shape[0], m, seed + 1)
     idx, _ = oq.prune_baseline(states, Xn, obj, ref, zp, chunk=32)
     out["prune_s"] = time.perf_counter() - t0
@@ -405,6 +416,7 @@ def cpu_full_ask(s, restarts, raw, S, seed=0):
     out["raw_screening_s"] = st.t_raw
     out["restarts_s"] = st.t_opt
     out["total_s"] = time.perf_counter() - t0
+    stop.set()
     out.update(n_base=nb, cells_total=int(sum(c.shape[1] for c in orc.cells)), raw_evals=st.raw_evals,
                opt_evals=st.opt_evals, optimizer_iterations=st.opt_iters, best_value=v,
                candidates_per_s=round((st.raw_evals + st.opt_evals) / out["total_s"], 3))
