@@ -131,10 +131,8 @@ struct evr_qnehvi_plan {
   hipGraph_t hgraph;
   hipGraphExec_t hexec;
   unsigned long long seq;
-  unsigned int* counter;         // device words: [0..1] the last request the wait kernel served (u64)
+  unsigned int* counter;         // (kept for the recycled-resource layout; unused since round 4)
   int nwords;                    // completion words the host graph's last kernel writes
-  bool armed;                    // a host-graph launch is queued, its wait kernel polling for x
-  hipStream_t hs;                // the stream of the host-graph launches
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
 };
 
@@ -155,27 +153,6 @@ __global__ __launch_bounds__(256) void plan_copy_out(int b, int n, const double*
     __threadfence_system();
     *(volatile unsigned long long*)(hout + b + n) = seq;
   }
-}
-
-// First kernel of the host-evaluation graph: one lane polls the pinned request word (written by
-// the host after x, behind a release fence) until it differs from the last request served,
-// records it and returns; the chain then reads x.  A graph can thus be launched before its x
-// exists (evr_qnehvi_plan_minimize queues the next evaluation's launch while the optimiser
-// computes the step), so the launch and its dispatch overlap the host's work.  After 1 s
-// without a request it returns anyway (every launch ends; the host detects the stale run by
-// its completion words and relaunches).  Loads / stores through the vector memory path only.
-__global__ __launch_bounds__(64) void plan_wait_kernel(const double* reqp, unsigned long long* served) {
-  if (threadIdx.x != 0) return;
-  const unsigned long long last = __hip_atomic_load(served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t0 = (unsigned long long)wall_clock64();
-  unsigned long long r = last;
-  for (;;) {
-    r = __hip_atomic_load((const unsigned long long*)reqp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (r != last) break;
-    if ((unsigned long long)wall_clock64() - t0 > 100000000ull) break;   // 1 s at 100 MHz
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __hip_atomic_store(served, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace evr
@@ -268,8 +245,6 @@ static bool graph_reuse() {
   return on;
 }
 
-static int plan_disarm(evr_qnehvi_plan* p);
-
 extern "C" {
 
 long long evr_qnehvi_plan_workspace_bytes(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
@@ -303,8 +278,6 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->hexec = nullptr;
   p->seq = 0;
   p->nwords = 1;
-  p->armed = false;
-  p->hs = nullptr;
   p->counter = nullptr;
   if (int rc = gemm_backend_init()) {
     delete p;
@@ -343,7 +316,6 @@ static void plan_capture(evr_qnehvi_plan* p) {
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
   EVR_CHECK(p, "evr_qnehvi_plan_run: null plan");
   hipStream_t s = (hipStream_t)stream;
-  if (int rc = plan_disarm(p)) return rc;   // the workspace is the host graph's too
   if (!p->exec && p->use_graph && p->nrun++ >= 1) plan_capture(p);
   if (p->exec) {
     EVR_HIP(hipGraphLaunch(p->exec, s));
@@ -354,7 +326,6 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
-  (void)plan_disarm(p);   // nothing of the plan may still be queued when its buffers go
   int dev = -1;
   if (graph_reuse() && p->hexec && p->hx && p->hout && p->counter && hipGetDevice(&dev) == hipSuccess) {
     // the plan's evaluations have completed (plan_eval_raw waits for each), so the buffers and
@@ -420,9 +391,7 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
     // writes the results and the completion word itself, other chains end in plan_copy_out
     int done = 0;
-    plan_wait_kernel<<<1, 64, 0, cs>>>(dhx + n, (unsigned long long*)p->counter);
-    rc = hipGetLastError() == hipSuccess ? 0 : 1;
-    if (!rc) rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
+    rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
     p->nwords = done > 0 ? done : 1;
   }
@@ -453,32 +422,17 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   EVR_CHECK(false, "qnehvi plan: host-evaluation graph capture failed (%s)", why.c_str());
 }
 
-// One evaluation at host x (b x d); [acq | dX] left in p->hout.  x, then (behind a release
-// fence) the request number go to the pinned buffer; the graph is launched unless a launch is
-// already queued (armed), whose wait kernel then picks the request up.  arm_next: queue the
-// next evaluation's launch right after this one completes (the caller must consume it with
-// another evaluation or plan_disarm).
-static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x, bool arm_next = false) {
+// One evaluation at host x (b x d); [acq | dX] left in p->hout.
+static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
   const int b = p->b, n = b * p->md.d;
   if (int rc = plan_host_setup(p)) return rc;
-  if (p->armed && p->hs != s) {   // a launch queued on another stream: consume it there first
-    p->armed = false;
-    const unsigned long long sq = ++p->seq;
-    std::atomic_thread_fence(std::memory_order_seq_cst);
-    __atomic_store_n((unsigned long long*)(p->hx + n), sq, __ATOMIC_RELEASE);
-    EVR_HIP(hipStreamSynchronize(p->hs));
-  }
   std::memcpy(p->hx, x, sizeof(double) * n);
   const unsigned long long seq = ++p->seq;
+  std::memcpy(p->hx + n, &seq, sizeof(seq));
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  __atomic_store_n((unsigned long long*)(p->hx + n), seq, __ATOMIC_RELEASE);
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  bool queued = p->armed;
-  p->armed = false;
-  if (!queued) EVR_HIP(hipGraphLaunch(p->hexec, s));
+  EVR_HIP(hipGraphLaunch(p->hexec, s));
   // spin on the completion words; every 256 polls ask the stream whether it has drained (a
-  // faulted or failed launch ends the wait with its error instead of spinning forever; a
-  // queued launch whose wait kernel gave up before the request came is relaunched once)
+  // faulted or failed launch ends the wait with its error instead of spinning forever)
   volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
   const int nw = p->nwords;
   auto finished = [&]() {
@@ -491,42 +445,20 @@ static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x, boo
       const hipError_t q = hipStreamQuery(s);
       if (q == hipErrorNotReady) continue;
       EVR_HIP(q);
-      if (finished()) break;
-      if (queued) {
-        queued = false;
-        EVR_HIP(hipGraphLaunch(p->hexec, s));
-        continue;
-      }
-      EVR_CHECK(false, "qnehvi plan: evaluation finished without its completion words");
+      if (!finished()) EVR_CHECK(false, "qnehvi plan: evaluation finished without its completion words");
     }
   }
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (arm_next) {
-    EVR_HIP(hipGraphLaunch(p->hexec, s));
-    p->armed = true;
-    p->hs = s;
-  }
   return 0;
 }
 
-// Consume a queued launch (one evaluation at the x still in the pinned buffer) so that nothing
-// of the plan runs after this returns.
-static int plan_disarm(evr_qnehvi_plan* p) {
-  if (!p || !p->armed) return 0;
-  const int n = p->b * p->md.d;
-  std::vector<double> x(p->hx, p->hx + n);
-  return plan_eval_raw(p->hs, p, x.data(), false);
-}
-
 // One evaluation of the restart batch at host x: f = -sum_r acq_r, g = -dX.
-static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g,
-                          bool arm_next = false) {
+static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g) {
   const int b = p->b, n = b * p->md.d;
-  if (int rc = plan_eval_raw(s, p, x, arm_next)) return rc;
+  if (int rc = plan_eval_raw(s, p, x)) return rc;
   double acc = 0.0;
   for (int r = 0; r < b; ++r) {
     if (std::isnan(p->hout[r])) {
-      (void)plan_disarm(p);
       ::evr::set_error("acquisition: posterior covariance block not p.d. after the jitter ladder (NotPSDError)");
       return EVR_ERR_NOTPSD;
     }
@@ -560,12 +492,6 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   }();
   double t_step = 0.0, t_eval = 0.0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  // the next evaluation's graph is launched as soon as one completes (its wait kernel holds it
-  // until the optimiser posts x); EVR_PRELAUNCH=0: launch per evaluation
-  static const bool prelaunch = [] {
-    const char* e = std::getenv("EVR_PRELAUNCH");
-    return !(e && e[0] == '0');
-  }();
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;
@@ -574,9 +500,7 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   for (;;) {
     if (task == LBFGSB_FG) {
       double t0 = stats ? now() : 0.0;
-      // every queued launch is consumed: by the next evaluation in this loop or by the final
-      // re-evaluation below
-      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data(), prelaunch)) return rc;
+      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
       double t1 = stats ? now() : 0.0;
       ++nfev;
       task = opt.step(f, g.data());
