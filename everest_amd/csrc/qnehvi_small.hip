@@ -42,6 +42,14 @@ __device__ __forceinline__ double4_t mfma4(double a, double b, double4_t c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+#ifdef EVR_QS_PROF
+// tools/qs_prof.hip: per-workgroup wall-clock stamps of qs_fwd / qs_bwd (s_memrealtime, 10 ns)
+__device__ unsigned long long qs_prof[4096 * 8];
+#define QS_STAMP(k) do { if (threadIdx.x == 0) qs_prof[(size_t)qs_bid * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define QS_STAMP(k) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------
 // forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms
 // ---------------------------------------------------------------------------------------
@@ -59,6 +67,10 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
   const int i = lane & 15, kq = lane >> 4;
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Kj = Kx + (size_t)j * n * b;
+#ifdef EVR_QS_PROF
+  const int qs_bid = 2048 + blockIdx.y * gridDim.x + blockIdx.x;   // after qs_bwd's records
+#endif
+  QS_STAMP(0);
   double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
   // coalesced chunk loads into registers (a wave reads 512 contiguous bytes of one M row per
   // instruction; the chunk's K_x rows are one contiguous run of kn x b doubles), staged in
@@ -107,6 +119,7 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
     __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
     stage(mvA, kvA);
     __syncthreads();
+    if (kc == 0) QS_STAMP(1);
     if (kc + 2 * QS_KC < n) load(mvA, kvA, kc + 2 * QS_KC);
     mult();
     if (kc + QS_KC >= n) break;
@@ -116,6 +129,7 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
     if (kc + 3 * QS_KC < n) load(mvB, kvB, kc + 3 * QS_KC);
     mult();
   }
+  QS_STAMP(2);
   // D map of v_mfma_f64_16x16x4: register q of lane l holds D[4q + (l >> 4)][l & 15]
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -145,6 +159,7 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
     }
     if (c < b) P[(((size_t)j * ntile + tile) * 2 + cls) * b + c] = s;
   }
+  QS_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -302,13 +317,7 @@ __global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr
 // over the samples overlaps the chunk loop.
 // ---------------------------------------------------------------------------------------
 constexpr int QS_RC = 128;   // rows of M per backward chunk
-#ifdef EVR_QS_PROF
-// tools/qs_prof.hip: per-workgroup wall-clock stamps of qs_bwd (s_memrealtime, 10 ns)
-__device__ unsigned long long qs_prof[4096 * 8];
-#define QS_STAMP(k) do { if (threadIdx.x == 0) qs_prof[(size_t)qs_bid * 8 + (k)] = wall_clock64(); } while (0)
-#else
-#define QS_STAMP(k) do { } while (0)
-#endif
+
 // (256, 2): two waves per SIMD, i.e. two workgroups per CU — without the bound the compiler
 // took 244 VGPRs + 16 AGPRs (one workgroup per CU: the 480 workgroups of the bench shape ran
 // in two rounds); bounded it fits 248 registers without scratch

@@ -86,6 +86,35 @@ int main() {
       pm[k] = std::max(pm[k], v);
     }
   }
+  // the forward projection at the same shape (records from 2048 on)
+  const int ntf = (Rr + 15) / 16;
+  double* Kx = dev_fill((size_t)m * n * b, 0, 1, 12);
+  double* Rf = dev_fill((size_t)m * Rr * b, 0, 0, 13);
+  double* Pf = dev_fill((size_t)m * ntf * 2 * b, 0, 0, 14);
+  for (int r = 0; r < 5; ++r) evr::qs_fwd<<<dim3(ntf, m), 256>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r) evr::qs_fwd<<<dim3(ntf, m), 256>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float msf = 0;
+  (void)hipEventElapsedTime(&msf, e0, e1);
+  (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(evr::qs_prof), st.size() * sizeof(unsigned long long));
+  unsigned long long f0 = ~0ull, f1 = 0;
+  double fp[3] = {0, 0, 0}, fm[3] = {0, 0, 0};
+  const int nwf = ntf * m;
+  for (int w = 0; w < nwf; ++w) {
+    const unsigned long long* s = &st[(size_t)(2048 + w) * 8];
+    f0 = std::min(f0, s[0]);
+    f1 = std::max(f1, s[3]);
+    for (int k = 0; k < 3; ++k) {
+      const double v = (double)(s[k + 1] - s[k]) / 100.0;
+      fp[k] += v / nwf;
+      fm[k] = std::max(fm[k], v);
+    }
+  }
+  printf("{\"qs_fwd\": {\"grid\": [%d, %d], \"launch_us\": %.2f, \"span_us\": %.2f, \"first_chunk_us\": [%.2f, %.2f], "
+         "\"other_chunks_us\": [%.2f, %.2f], \"epilogue_us\": [%.2f, %.2f]}}\n",
+         ntf, m, msf * 1e3 / reps, (double)(f1 - f0) / 100.0, fp[0], fm[0], fp[1], fm[1], fp[2], fm[2]);
   printf("{\"grid\": [%d, %d, %d], \"rows_per\": %d, \"launch_us\": %.2f, \"span_us\": %.2f, \"start_spread_us\": %.2f, "
          "\"coef_us\": [%.2f, %.2f], \"chunks_us\": [%.2f, %.2f], \"epi_loads_exchange_us\": [%.2f, %.2f], "
          "\"gradient_store_us\": [%.2f, %.2f]}\n",
