@@ -130,8 +130,6 @@ _SIGS = {
     "evr_qnehvi_small_workspace_doubles": ([POINTER(EvrQnehviState), c_int, c_int, c_int], ctypes.c_longlong),
     "evr_qnehvi_small_forward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
                                   c_void_p, c_void_p], c_int),
-    "evr_qnehvi_small_forward_x": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,
-                                    c_void_p, c_void_p], c_int),
     "evr_qnehvi_small_samples": ([c_void_p, POINTER(EvrQnehviState), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p], c_int),
     "evr_qnehvi_small_backward": ([c_void_p, POINTER(EvrQnehviState), POINTER(EvrQnehviModel), c_int, c_void_p,

@@ -41,8 +41,6 @@ size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d);
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P);
 int qs_done_words(int b, int d);
-int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                 double* R, double* P);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags);
@@ -66,7 +64,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
 
 struct PlanLayout {
   size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, bytes;
-  bool small, fused_kx, fused_scan;
+  bool small, fused_scan;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -81,12 +79,8 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     return r;
   };
   L.small = small_path(st, b, md->d);
-  {
-    const char* e = std::getenv("EVR_FUSED_KX");
-    L.fused_kx = L.small && e && std::string(e) == "1";
-  }
   L.fused_scan = L.small && backward && evr_hvi_restart_fb_applies(st, b);
-  L.Kx = take(L.fused_kx ? 0 : 8 * m * n * b);
+  L.Kx = take(8 * m * n * b);
   L.R = take(8 * m * Rr * b);
   L.P = take(8 * (L.small ? qs_norms_doubles(st, b) : m * (size_t)evr_qnehvi_norms_rows(st) * 2 * b));
   L.Wf = take(8 * (L.small ? 0 : proj_forward_ws_doubles(st, b)));
@@ -175,13 +169,10 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   int* flags = (int*)(w + p->L.flags);
   double* hw = (double*)(w + p->L.hvi);
   const bool small = p->L.small;
-  if (small && p->L.fused_kx) {
-    // K_x generated inside the projection (qs_fwd_x, EVR_FUSED_KX=1): measured slower than
-    // the separate kmat launch at b = 20 (29 vs 12.8 + 4.8 us; each of the 49 row tiles of an
-    // output recomputes the whole K_x,j at one wave per SIMD), kept for A/B
-    if (int rc = qs_forward_x(s, st, md, b, X, R, P)) return rc;
-  } else if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
-                                        md->lengthscales, nullptr, nullptr, Kx)) {
+  // (K_x generated inside the projection instead was measured slower at b = 20 twice — 29 vs
+  // 17.6 us in round 3, chain 83.9 vs 73.7 us in round 4 — and removed)
+  if (int rc = evr_kernel_matrix(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
+                                 md->lengthscales, nullptr, nullptr, Kx)) {
     return rc;
   } else if (small) {
     if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;

@@ -32,9 +32,6 @@ namespace evr {
 constexpr int QS_B = 32;     // max candidates
 constexpr int QS_FR = 16;    // rows of M per forward workgroup
 constexpr int QS_KC = 128;   // K_x rows staged per chunk (~67 KB of LDS: two workgroups per CU)
-constexpr int QS_RPP = 256 / QS_KC;        // M rows per staging pass (a thread per chunk column)
-constexpr int QS_ML = QS_FR / QS_RPP;      // M values per thread and chunk
-constexpr int QS_KL = QS_KC * QS_B / 256;  // K_x values per thread and chunk
 constexpr int QS_BI = 16;    // columns of M (training rows) per backward workgroup
 constexpr int QS_MAXD = 8;   // input dims handled in registers by the backward epilogue
 
@@ -51,17 +48,25 @@ __device__ unsigned long long qs_prof[4096 * 8];
 #endif
 
 // ---------------------------------------------------------------------------------------
-// forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms
+// forward: R_j[r0 .. r0+15][c] = sum_k M_j[r][k] Kx_j[k][c]; P[j][tile][cls][c] partial norms.
+// QS_FT = 512 threads (8 waves) per workgroup: at the bench shape the grid is m x Rr / 16 =
+// 245 workgroups, fewer than the 256 CUs, so the waves of one workgroup are all the latency
+// hiding a CU gets (4 waves: 10.4 us; each wave's chunk work halves with 8).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
-                                              const double* __restrict__ Kx, double* __restrict__ R,
-                                              double* __restrict__ P, int ntile) {
+constexpr int QS_FT = 512;
+constexpr int QS_FW = QS_FT / 64;                 // waves
+constexpr int QS_RPP = QS_FT / QS_KC;             // M rows per staging pass (a thread per chunk column)
+constexpr int QS_ML = QS_FR / QS_RPP;             // M values per thread and chunk
+constexpr int QS_KL = (QS_KC * QS_B + QS_FT - 1) / QS_FT;   // K_x values per thread and chunk
+__global__ __launch_bounds__(QS_FT, 1) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
+                                                   const double* __restrict__ Kx, double* __restrict__ R,
+                                                   double* __restrict__ P, int ntile) {
   // padded row of the staged M tile: 2 MP = 4 (mod 64 dwords) puts the 16 rows x 2
   // k-quarters of a ds_read_b64 lane half on 32 distinct bank pairs (conflict-free)
   constexpr int MP = QS_KC + 2;
   __shared__ double Ms[QS_FR][MP];               // 16 x 128 slice of M_j (16.6 KB)
   __shared__ double Ks[QS_KC][QS_B + 1];         // 128 x b slice of K_x,j (33.8 KB)
-  __shared__ double red[4][QS_FR][QS_B + 1];
+  __shared__ double red[QS_FW][QS_FR][QS_B + 1];  // the waves' k-partials (33.8 KB)
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
@@ -77,10 +82,9 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
   // LDS afterwards; two register buffers, so the loads of chunks k + 1 and k + 2 are in flight
   // while chunk k is staged and multiplied (the K_x values past b x kn are never loaded).
   // K_x rows past the end of a partial chunk are zero (M's are too, but 0 x garbage is not 0).
-  constexpr int KLB = (QS_KC * QS_B + 255) / 256;
-  double mvA[QS_ML], kvA[KLB], mvB[QS_ML], kvB[KLB];
-  const int kk = tid % QS_KC, rh = tid / QS_KC;   // staging: chunk column kk of rows rh, rh + 2, ...
-  auto load = [&](double (&mv)[QS_ML], double (&kv)[KLB], int kc) {
+  double mvA[QS_ML], kvA[QS_KL], mvB[QS_ML], kvB[QS_KL];
+  const int kk = tid % QS_KC, rh = tid / QS_KC;   // staging: chunk column kk of rows rh, rh + RPP, ...
+  auto load = [&](double (&mv)[QS_ML], double (&kv)[QS_KL], int kc) {
     const int kn = min(QS_KC, n - kc);
 #pragma unroll
     for (int u = 0; u < QS_ML; ++u) {
@@ -88,21 +92,21 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
       mv[u] = (r < Rr && kk < kn) ? Mj[(size_t)r * n + kc + kk] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < KLB; ++u) {
-      const int e = u * 256 + tid;
+    for (int u = 0; u < QS_KL; ++u) {
+      const int e = u * QS_FT + tid;
       kv[u] = (e < kn * b) ? Kj[(size_t)kc * b + e] : 0.0;
     }
   };
-  auto stage = [&](const double (&mv)[QS_ML], const double (&kv)[KLB]) {
+  auto stage = [&](const double (&mv)[QS_ML], const double (&kv)[QS_KL]) {
 #pragma unroll
     for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
 #pragma unroll
-    for (int u = 0; u < KLB; ++u) {
-      const int e = u * 256 + tid;
+    for (int u = 0; u < QS_KL; ++u) {
+      const int e = u * QS_FT + tid;
       if (e < QS_KC * b) Ks[e / b][e % b] = kv[u];   // every row of the chunk, columns < b
     }
   };
-  constexpr int KW = QS_KC / 4;   // k per wave and chunk
+  constexpr int KW = QS_KC / QS_FW;   // k per wave and chunk
   auto mult = [&]() {
 #pragma unroll
     for (int t = 0; t < KW / 4; ++t) {
@@ -138,14 +142,13 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
   }
   __syncthreads();
   {
-    const int rr = tid >> 4, cp = tid & 15;
+    const int rr = tid >> 5, c = tid & 31;   // one (row, column) per thread
+    double v = red[0][rr][c];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = cp + 16 * h;
-      const double v = ((red[0][rr][c] + red[1][rr][c]) + red[2][rr][c]) + red[3][rr][c];
-      if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
-      red[0][rr][c] = v;   // own slot only: read back by the norms below after the barrier
-    }
+    for (int w = 1; w < QS_FW; ++w) v += red[w][rr][c];
+    if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
+    __syncthreads();
+    red[0][rr][c] = v;
   }
   __syncthreads();
   if (tid < 2 * QS_B) {
@@ -160,151 +163,6 @@ __global__ __launch_bounds__(256, 2) void qs_fwd(int n, int nb, int Rr, int b, c
     if (c < b) P[(((size_t)j * ntile + tile) * 2 + cls) * b + c] = s;
   }
   QS_STAMP(3);
-}
-
-// ---------------------------------------------------------------------------------------
-// forward with the cross-covariance generated in the B fetch (the restart batch of the native
-// plan): as qs_fwd, but each chunk's K_x rows are computed by the workgroup itself —
-// threads t and t + 128 own training row kc + t and form k(x_t, x_c) for the b candidates with
-// kmat_kernel's arithmetic (normalised / lengthscale-divided coordinates, explicit
-// differences, fma accumulation in coordinate order, the same kernel_value), so R is bitwise
-// the kmat_kernel + qs_fwd result, without the separate launch or K_x's HBM round trip.
-// The candidates (b x d raw, possibly the plan's pinned host buffer) are read once per
-// workgroup.  LDS: the M tile padded as in qs_fwd; the K tile's rows of 32 doubles hold
-// column c at c ^ 16 (k & 1), so the MFMA B reads of rows k, k+1 (one ds_read_b64 lane
-// half) fall on the two halves of the bank row; each lane starts its row's columns at
-// lane mod b so the K stores spread over the banks.
-// ---------------------------------------------------------------------------------------
-template <int KIND>   // KIND < 0: the family of output j from the mixed kind code kcode
-__global__ __launch_bounds__(256) void qs_fwd_x(int kcode, int n, int nb, int Rr, int b, int d, const double* __restrict__ M,
-                                                const double* __restrict__ Xn, const double* X,
-                                                const double* __restrict__ shift, const double* __restrict__ scale,
-                                                const double* __restrict__ ls, double* __restrict__ R,
-                                                double* __restrict__ P, int ntile) {
-  constexpr int MP = QS_KC + 2;
-  constexpr int UP = QS_MAXD + 1;                // candidate rows padded: per-lane rows conflict-free
-  __shared__ double Ms[QS_FR][MP];
-  __shared__ double Ks[QS_KC][QS_B];
-  __shared__ double uc[QS_B][UP];
-  __shared__ double red[4][QS_FR][QS_B + 1];
-  const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = lane & 15, kq = lane >> 4;
-  const double* Mj = M + (size_t)j * Rr * n;
-  const double* lsj = ls + (size_t)j * d;
-  double mv[QS_ML];
-  double xt[QS_MAXD];
-  const int kk = tid % QS_KC, rh = tid / QS_KC;   // M staging as in qs_fwd; K rows: row kk, half rh
-  auto load = [&](int kc) {
-    const int kn = min(QS_KC, n - kc);
-#pragma unroll
-    for (int u = 0; u < QS_ML; ++u) {
-      const int r = r0 + QS_RPP * u + rh;
-      mv[u] = (r < Rr && kk < kn) ? Mj[(size_t)r * n + kc + kk] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < QS_MAXD; ++k) xt[k] = (kk < kn && k < d) ? Xn[(size_t)(kc + kk) * d + k] : 0.0;
-  };
-  load(0);
-  // candidates, normalised and divided by the lengthscales (kmat_kernel's B operand)
-  if (tid < b * d) {
-    const int c = tid / d, k = tid - c * d;
-    double w = X[(size_t)c * d + k];
-    if (shift) w -= shift[k];
-    if (scale) w *= scale[k];
-    uc[c][k] = w * (1.0 / lsj[k]);
-  }
-  double il[QS_MAXD];
-#pragma unroll
-  for (int k = 0; k < QS_MAXD; ++k) il[k] = k < d ? 1.0 / lsj[k] : 0.0;
-  const int rot = lane % b;
-  double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-  constexpr int KW = QS_KC / 4;
-  for (int kc = 0; kc < n; kc += QS_KC) {
-    const int kn = min(QS_KC, n - kc);
-    __syncthreads();   // uc written / the previous chunk's MFMAs are done with Ms, Ks
-#pragma unroll
-    for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
-    {
-      // this thread's training row kc + kk, then its share of the row's b kernel values (the
-      // thread halves rh take alternate rotated candidates; rows past the end: 0)
-      double ut[QS_MAXD];
-#pragma unroll
-      for (int k = 0; k < QS_MAXD; ++k) ut[k] = xt[k] * il[k];
-      const int sw = 16 * (kk & 1);
-      // all b squared distances first, then the b kernel values: fully unrolled so the LDS
-      // reads and the exp table loads of different candidates are in flight together (one
-      // wave per SIMD here: nothing else hides their latency)
-      constexpr int CH = QS_B / QS_RPP;
-      double d2v[CH];
-#pragma unroll
-      for (int ci = 0; ci < CH; ++ci) {
-        const int cc = QS_RPP * ci + rh;
-        d2v[ci] = 0.0;
-        if (cc < b) {
-          int c = cc + rot;
-          if (c >= b) c -= b;
-          double acc = 0.0;
-#pragma unroll
-          for (int k = 0; k < QS_MAXD; ++k) {
-            if (k < d) {
-              const double df = ut[k] - uc[c][k];
-              acc = fma(df, df, acc);
-            }
-          }
-          d2v[ci] = acc;
-        }
-      }
-#pragma unroll
-      for (int ci = 0; ci < CH; ++ci) {
-        const int cc = QS_RPP * ci + rh;
-        if (cc < b) {
-          int c = cc + rot;
-          if (c >= b) c -= b;
-          Ks[kk][c ^ sw] = kk < kn ? kernel_value(KIND >= 0 ? KIND : kind_of(kcode, j), d2v[ci]) : 0.0;
-        }
-      }
-    }
-    __syncthreads();
-    if (kc + QS_KC < n) load(kc + QS_KC);
-#pragma unroll
-    for (int t = 0; t < KW / 4; ++t) {
-      const int k = wave * KW + 4 * t + kq;
-      const double a = Ms[i][k];
-      const int sw = 16 * (k & 1);
-      // columns >= b of Ks are never written: they only reach D's columns >= b (not stored)
-      acc0 = mfma4(a, Ks[k][i ^ sw], acc0);
-      acc1 = mfma4(a, Ks[k][(i + 16) ^ sw], acc1);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    red[wave][4 * q + kq][i] = acc0[q];
-    red[wave][4 * q + kq][16 + i] = acc1[q];
-  }
-  __syncthreads();
-  {
-    const int rr = tid >> 4, cp = tid & 15;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = cp + 16 * h;
-      const double v = ((red[0][rr][c] + red[1][rr][c]) + red[2][rr][c]) + red[3][rr][c];
-      if (r0 + rr < Rr && c < b) R[((size_t)j * Rr + r0 + rr) * b + c] = v;
-      red[0][rr][c] = v;
-    }
-  }
-  __syncthreads();
-  if (tid < 2 * QS_B) {
-    const int cls = tid / QS_B, c = tid - cls * QS_B;
-    double s = 0.0;
-#pragma unroll
-    for (int rr = 0; rr < QS_FR; ++rr) {
-      const int r = r0 + rr;
-      const bool in = cls == 0 ? r < n : (r >= n && r < n + nb);
-      if (in) s = fma(red[0][rr][c], red[0][rr][c], s);
-    }
-    if (c < b) P[(((size_t)j * ntile + tile) * 2 + cls) * b + c] = s;
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -692,26 +550,7 @@ size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
                double* R, double* P) {
   const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
-  qs_fwd<<<dim3(nt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, md->M, Kx, R, P, nt);
-  EVR_LAUNCH_CHECK();
-  return 0;
-}
-
-int qs_forward_x(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                 double* R, double* P) {
-  const int Rr = qn_rows(st), nt = qs_ntile_fwd(st);
-  const dim3 g(nt, st->m);
-#define GO(K_)                                                                                                  \
-  qs_fwd_x<K_><<<g, 256, 0, s>>>(md->kind, st->n, st->nb, Rr, b, md->d, md->M, md->Xn, X, md->shift, md->scale, \
-                                 md->lengthscales, R, P, nt)
-  switch (md->kind) {
-    case RBF: GO(RBF); break;
-    case MATERN05: GO(MATERN05); break;
-    case MATERN15: GO(MATERN15); break;
-    case MATERN25: GO(MATERN25); break;
-    default: GO(-1); break;
-  }
-#undef GO
+  qs_fwd<<<dim3(nt, st->m), QS_FT, 0, s>>>(st->n, st->nb, Rr, b, md->M, Kx, R, P, nt);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -759,13 +598,6 @@ int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr
                              const double* Kx, double* R, double* P) {
   EVR_CHECK(st && md && Kx && R && P && qs_applies(st, b, md->d), "evr_qnehvi_small_forward: bad arguments");
   return qs_forward((hipStream_t)stream, st, md, b, Kx, R, P);
-}
-
-int evr_qnehvi_small_forward_x(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
-                               const double* X, double* R, double* P) {
-  EVR_CHECK(st && md && X && R && P && qs_applies(st, b, md->d) && md->Xn && md->M && md->lengthscales,
-            "evr_qnehvi_small_forward_x: bad arguments");
-  return qs_forward_x((hipStream_t)stream, st, md, b, X, R, P);
 }
 
 int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,

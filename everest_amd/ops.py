@@ -355,20 +355,6 @@ def qnehvi_small_forward(st: EvrQnehviState, model, Kx: torch.Tensor, b: int):
     return R, P
 
 
-def qnehvi_small_forward_x(st: EvrQnehviState, model, X: torch.Tensor, b: int):
-    """Restart-batch projection with K_x generated in the kernel from the raw candidates X
-    (qs_fwd_x, the plan's path): R, P bitwise equal to qnehvi_small_forward(kernel_matrix)."""
-    X = _dev(X, "X").contiguous()
-    dev = X.device
-    lib = _native.load()
-    Rr = st.n + st.nb + (0 if st.no_h else st.S) + 1
-    R = torch.empty(st.m, Rr, b, dtype=torch.float64, device=dev)
-    P = _workspace(lib.evr_qnehvi_small_workspace_doubles(ctypes.byref(st), b, model.d, 0), dev)
-    call("evr_qnehvi_small_forward_x", _stream(), ctypes.byref(st), ctypes.byref(model), b, X.data_ptr(),
-         R.data_ptr(), P.data_ptr())
-    return R, P
-
-
 def qnehvi_small_samples(st: EvrQnehviState, R: torch.Tensor, P: torch.Tensor, b: int):
     dev = R.device
     G = torch.empty(st.S, st.m, b, dtype=torch.float64, device=dev)

@@ -278,11 +278,6 @@ int evr_qnehvi_small_applies(const evr_qnehvi_state* st, int b, int d);
 long long evr_qnehvi_small_workspace_doubles(const evr_qnehvi_state* st, int b, int d, int which);
 int evr_qnehvi_small_forward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
                              const double* Kx, double* R, double* P);
-/* As evr_qnehvi_small_forward with the cross-covariance generated inside the projection from
- * the raw candidates X (b x d; the native plan's restart-batch path): R and P bitwise equal
- * to kernel_matrix + evr_qnehvi_small_forward. */
-int evr_qnehvi_small_forward_x(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
-                               const double* X, double* R, double* P);
 int evr_qnehvi_small_samples(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* P,
                              double* G, double* L22, int* flags);
 int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,

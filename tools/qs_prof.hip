@@ -91,9 +91,9 @@ int main() {
   double* Kx = dev_fill((size_t)m * n * b, 0, 1, 12);
   double* Rf = dev_fill((size_t)m * Rr * b, 0, 0, 13);
   double* Pf = dev_fill((size_t)m * ntf * 2 * b, 0, 0, 14);
-  for (int r = 0; r < 5; ++r) evr::qs_fwd<<<dim3(ntf, m), 256>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
+  for (int r = 0; r < 5; ++r) evr::qs_fwd<<<dim3(ntf, m), evr::QS_FT>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
   (void)hipEventRecord(e0);
-  for (int r = 0; r < reps; ++r) evr::qs_fwd<<<dim3(ntf, m), 256>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
+  for (int r = 0; r < reps; ++r) evr::qs_fwd<<<dim3(ntf, m), evr::QS_FT>>>(n, nb, Rr, b, M, Kx, Rf, Pf, ntf);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float msf = 0;

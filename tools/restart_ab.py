@@ -79,29 +79,6 @@ def main():
                 rec["minimize_evals"] = int(info[1])
             out[f"{tag}_{name}"] = rec
     _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
-    # K_x generated inside the forward projection (qs_fwd_x, EVR_FUSED_KX=1) vs kmat_kernel + qs_fwd
-    Xt = torch.tensor(Xopt, device=dev)
-    for fk in ("1", "0"):
-        os.environ["EVR_FUSED_KX"] = fk
-        acqf._plans = {}
-        p = acqf.plan(20, True)
-        p.X.copy_(Xt)
-        for _ in range(3):
-            p.run()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(50):
-            p.run()
-        e1.record()
-        torch.cuda.synchronize()
-        p.run_host(Xopt)
-        t0 = time.perf_counter()
-        for _ in range(50):
-            p.run_host(Xopt)
-        out[f"opt_kdw_fused_kx{fk}"] = {"chain_us": round(e0.elapsed_time(e1) / 50 * 1e3, 2),
-                                        "eval_roundtrip_us": round((time.perf_counter() - t0) / 50 * 1e6, 2)}
-    os.environ.pop("EVR_FUSED_KX", None)
     acqf._plans = {}
     out["construction"] = {k: round(v * 1e3, 3) for k, v in acqf.timings.items()}
     out["base_jitter"] = [float(v) for v in acqf.base_jitter.cpu()]
