@@ -228,13 +228,6 @@ struct PlanHostRes {
 };
 static std::mutex g_hres_mu;
 static std::vector<PlanHostRes> g_hres;
-static bool graph_upload() {   // EVR_GRAPH_UPLOAD=0: no hipGraphUpload after instantiate / update (A/B)
-  static const bool on = [] {
-    const char* e = std::getenv("EVR_GRAPH_UPLOAD");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 static bool graph_reuse() {
   static const bool on = [] {
     const char* e = std::getenv("EVR_GRAPH_REUSE");
@@ -405,7 +398,6 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
     if (ok) {
       p->hexec = old_exec;
       p->hgraph = g;
-      if (graph_upload()) (void)hipGraphUpload(p->hexec, nullptr);   // device-side copy of the updated executable
       return 0;
     }
     (void)hipGraphExecDestroy(old_exec);
@@ -413,7 +405,6 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   }
   if (!rc && e == hipSuccess && g && hipGraphInstantiate(&p->hexec, g, nullptr, nullptr, 0) == hipSuccess) {
     p->hgraph = g;
-    if (graph_upload()) (void)hipGraphUpload(p->hexec, nullptr);   // packets prepared once, not per launch
     return 0;
   }
   if (g) (void)hipGraphDestroy(g);
