@@ -221,9 +221,17 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
         if (gi < n1 && gj < n2) {
           double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
           if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
+#if EVR_KMAT_DIAG == 1   // profiling builds only: no kernel evaluation (the epilogue's VALU share)
+          double v = scale * d2;
+#else
           double v = scale * kernel_value_t(KIND, d2, kexp);
+#endif
           if (gi == gj) v += dadd;
+#if EVR_KMAT_DIAG == 2   // profiling builds only: no output stream (the store share)
+          if (v == -1.25) Kb[(size_t)gi * n2 + gj] = v;
+#else
           Kb[(size_t)gi * n2 + gj] = v;
+#endif
         }
       }
     return;

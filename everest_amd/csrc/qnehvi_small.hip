@@ -465,35 +465,38 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   const int k = e % d;
   unsigned long long seq = 0;
   if (hout && threadIdx.x == 0) seq = *(volatile const unsigned long long*)seqp;
-  double av = 0.0;
-  if (ein && sval && e < b) {
-    double x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int s = lane + 64 * u;
-      x[u] = s < S ? sval[(size_t)s * b + e] : 0.0;
-    }
-    double a = 0.0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (lane + 64 * u < S) a += x[u];
-    for (int s = lane + 256; s < S; s += 64) a += sval[(size_t)s * b + e];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    bool bad = false;
-    if (flags)
-      for (int j = 0; j < m; ++j) bad |= flags[(size_t)j * b + e] != 0;
-    av = bad ? nan("") : a / (double)S;
-    if (lane == 0) acq[e] = av;
-  }
-  // the lane's first 8 partials (contiguous over the wave) loaded together, then summed in the
-  // loop's order
+  // every first-round load of the kernel (the element's partials, the per-sample values and the
+  // Cholesky flags of an acquisition element) is issued before the first wait: one memory round
+  // trip instead of three dependent ones
   const double* src = dXp + (size_t)(ein ? e : 0) * np;
   double x[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int p = lane + 64 * u;
     x[u] = (ein && p < np) ? src[p] : 0.0;
+  }
+  const bool acq_e = ein && sval && e < b;
+  double sv[4];
+  int fl = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int s = lane + 64 * u;
+    sv[u] = (acq_e && s < S) ? sval[(size_t)s * b + e] : 0.0;
+  }
+  if (acq_e && flags)
+    for (int j = lane; j < m; j += 64) fl |= flags[(size_t)j * b + e];
+  double av = 0.0;
+  if (acq_e) {
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < S) a += sv[u];
+    for (int s = lane + 256; s < S; s += 64) a += sval[(size_t)s * b + e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    const bool bad = __any(fl != 0) != 0;
+    av = bad ? nan("") : a / (double)S;
+    if (lane == 0) acq[e] = av;
   }
   double v = 0.0;
 #pragma unroll
