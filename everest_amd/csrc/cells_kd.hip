@@ -25,6 +25,8 @@
 //      u16, 0x7FFF padding) and the group's minimum rank per objective.
 // Deterministic: keys are unique (cell index in the low bits), so the order never depends
 // on thread timing.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "../../include/everest_amd.h"
 
@@ -34,6 +36,19 @@ constexpr int KD_THREADS = 1024;
 constexpr int KD_MAX_CELLS = 8192;          // LDS sort buffer (64 KB)
 constexpr int KD_MAX_GROUPS = KD_MAX_CELLS / 16;
 constexpr unsigned short KD_PAD = 0x7FFF;   // > every threshold (ranks < 2^15: packed signed compares)
+
+// EVR_CKD_PROF builds (profiling only): per-sample phase clocks (s_memrealtime, 100 MHz), slot k of sample s at
+// ckd_prof[16 s + k] (0 start, 1 rank tables, 2 spans, 3 keys, 4 sorts, 5 splits, 6 end, 7 levels)
+#ifdef EVR_CKD_PROF
+__device__ unsigned long long ckd_prof[16 * 4096];
+#define CKD_T(k) if (threadIdx.x == 0 && blockIdx.x < 4096) ckd_prof[16 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();
+#define CKD_ACC(k, t0) if (threadIdx.x == 0 && blockIdx.x < 4096) ckd_prof[16 * blockIdx.x + (k)] += __builtin_amdgcn_s_memrealtime() - (t0);
+#define CKD_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define CKD_T(k)
+#define CKD_ACC(k, t0)
+#define CKD_NOW() 0ull
+#endif
 
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   const int lo = __shfl_xor((int)(unsigned)v, m, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), m, 64);
@@ -45,14 +60,20 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 // wave (index i = tid + 1024 t, so a wave holds 64 consecutive keys) and run in registers by
 // xor-shuffles, min / max per pair, with one barrier per merge size: 41 instead of 91 barriers
 // per sort at P2 = 8192.  Same result as the compare-and-swap network (keys are unique).
-__device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
+__device__ __forceinline__ unsigned int shfl_xor_key(unsigned int v, int m) {
+  return (unsigned int)__shfl_xor((int)v, m, 64);
+}
+__device__ __forceinline__ unsigned long long shfl_xor_key(unsigned long long v, int m) { return shfl_xor_u64(v, m); }
+
+template <typename KT>
+__device__ __forceinline__ void kd_bitonic(KT* a, int P2) {
   for (int k = 2; k <= P2; k <<= 1) {
     int j = k >> 1;
     for (; j >= 64; j >>= 1) {
       for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
         const int l = i ^ j;
         if (l > i) {
-          const unsigned long long x = a[i], y = a[l];
+          const KT x = a[i], y = a[l];
           const bool up = (i & k) == 0;
           if ((x > y) == up) {
             a[i] = y;
@@ -63,10 +84,10 @@ __device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
       __syncthreads();
     }
     for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
-      unsigned long long x = a[i];
+      KT x = a[i];
       const bool up = (i & k) == 0;
       for (int jj = j; jj > 0; jj >>= 1) {
-        const unsigned long long y = shfl_xor_u64(x, jj);
+        const KT y = shfl_xor_key(x, jj);
         // the lower index of a pair keeps the minimum in an ascending run, the maximum otherwise
         x = (((i & jj) == 0) == up) ? (x < y ? x : y) : (x < y ? y : x);
       }
@@ -76,7 +97,104 @@ __device__ __forceinline__ void kd_bitonic(unsigned long long* a, int P2) {
   }
 }
 
-template <int M>
+// Segmented sort of the kd levels whose unfinished segments all hold at most KD_WS_MAX cells:
+// one wave per segment (a compact list of segment start groups, dealt round-robin to the
+// waves), the segment's keys padded with ~0 to the next power of two P and bitonic-sorted in
+// registers — lane l holds elements l + 64 t, t < P / 64 — with no workgroup barrier: the
+// partner of a stage j >= 64 is a register of the same lane, of a stage j < 64 the same
+// register of lane l ^ j.  The keys of one segment share the segment field, so the order is
+// the full sort's (kd_bitonic over all P2 keys: 91 stages and 41 barriers at P2 = 8192 for
+// every level, even when the segments hold a few dozen cells).
+constexpr int KD_WS_T = 16, KD_WS_MAX = 64 * KD_WS_T;
+// branch-free compare-exchange: keep = all ones selects the minimum (u32 / u64 min, max and
+// bit selects only: no per-pair lane masks, which held the unrolled stages' SGPRs)
+__device__ __forceinline__ unsigned int kd_pick(unsigned int x, unsigned int y, unsigned int keep) {
+  const unsigned int mn = x < y ? x : y, mx = x < y ? y : x;
+  return (mn & keep) | (mx & ~keep);
+}
+__device__ __forceinline__ unsigned long long kd_pick(unsigned long long x, unsigned long long y,
+                                                      unsigned int keep) {
+  const unsigned long long mn = x < y ? x : y, mx = x < y ? y : x;
+  const unsigned long long k = (unsigned long long)(int)keep;   // sign-extend: all ones or zero
+  return (mn & k) | (mx & ~k);
+}
+template <typename KT>
+__device__ __forceinline__ void kd_cswap(KT& x, KT& y, unsigned int up) {
+  const KT a = x, b = y;
+  x = kd_pick(a, b, up);
+  y = kd_pick(a, b, ~up);
+}
+
+// one segment of n <= 64 T keys at sb[lo..], padded to P = 64 T (or 32 when T = 1); T is a
+// compile-time register count, so every stage's partner register is static
+template <typename KT, int T>
+__device__ __forceinline__ void kd_wave_sort_seg(KT* sb, int lo, int n) {
+  const int lane = threadIdx.x & 63;
+  const int P = T == 1 ? (n <= 32 ? 32 : 64) : 64 * T;
+  KT x[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int i = lane + 64 * t;
+    x[t] = i < n ? sb[lo + i] : ~(KT)0;
+  }
+  for (int k = 2, lk = 1; k <= P; k <<= 1, ++lk) {
+#pragma unroll
+    for (int lj = 4; lj >= 0; --lj) {   // in-lane stages j = 64 tj, descending
+      const int tj = 1 << lj;
+      if (tj < T && 64 * tj < k) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+          if ((t & tj) == 0) kd_cswap(x[t], x[t | tj], ((unsigned int)((lane + 64 * t) & k) >> lk) - 1u);
+      }
+    }
+    for (int j = min(k >> 1, 32), lj2 = min(lk - 1, 5); j > 0; j >>= 1, --lj2) {   // cross-lane stages
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int i = lane + 64 * t;
+        const KT y = shfl_xor_key(x[t], j);
+        // minimum where bit j of i equals bit k of i (ascending run, lower partner or descending
+        // run, upper partner): keep = ((i >> lj) ^ (i >> lk)) & 1 ? 0 : all ones
+        const unsigned int keep = (((unsigned int)(i >> lj2) ^ (unsigned int)(i >> lk)) & 1u) - 1u;
+        x[t] = kd_pick(x[t], y, keep);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int i = lane + 64 * t;
+    if (i < n) sb[lo + i] = x[t];
+  }
+}
+
+template <typename KT>
+__device__ void kd_wave_sort(KT* sb, const int* segl, int nseg, const int* segE, int C) {
+  const int wave = threadIdx.x >> 6;
+  for (int q = wave; q < nseg; q += KD_THREADS / 64) {
+    const int a = segl[q], lo = 16 * a, n = min(16 * segE[a], C) - lo;
+    // three register counts (P = 32 / 64, 256, 1024): a fourth and fifth instantiation pushed
+    // the kernel past its SGPR budget (spills)
+    if (n <= 64) kd_wave_sort_seg<KT, 1>(sb, lo, n);
+    else if (n <= 256) kd_wave_sort_seg<KT, 4>(sb, lo, n);
+    else kd_wave_sort_seg<KT, KD_WS_T>(sb, lo, n);
+  }
+}
+
+// Sort-key layouts (segment start group a | order value v | cell), compared as integers: u64
+// (a << 40 | v << 16 | cell) in general; u32 (a << 23 | v << 13 | cell) when every field fits —
+// cells < 8192, groups < 512, rank values < 1023 — half the LDS and shuffle traffic per sort
+// stage and the same order (every field is order-preserving in both layouts).
+template <typename KT>
+struct KdKey;
+template <>
+struct KdKey<unsigned long long> {
+  static constexpr int CB = 16, AS = 40;
+};
+template <>
+struct KdKey<unsigned int> {
+  static constexpr int CB = 13, AS = 23;
+};
+
+template <int M, typename KT>
 __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const int* __restrict__ off,
                                                              const int* __restrict__ goff,
                                                              const unsigned long long* __restrict__ keys,
@@ -85,22 +203,30 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
                                                              unsigned long long* __restrict__ okeys,
                                                              unsigned short* __restrict__ ork,
                                                              unsigned short* __restrict__ ogb,
-                                                             double* __restrict__ osv) {
+                                                             double* __restrict__ osv, int ws_max) {
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kd_dyn[];
   __shared__ int segS[KD_MAX_GROUPS], segE[KD_MAX_GROUPS];
   __shared__ unsigned int mn[KD_MAX_GROUPS][M], mx[KD_MAX_GROUPS][M];
-  __shared__ int sh_any;
+  __shared__ int segl[KD_MAX_GROUPS];
+  __shared__ int sh_any, sh_maxlen, sh_nseg;
   const int s = blockIdx.x, tid = threadIdx.x;
   const int c0 = off[s], C = off[s + 1] - c0;
   const int g0 = goff[s], G = goff[s + 1] - g0;
-  unsigned long long* sb = (unsigned long long*)kd_dyn;               // P2 sort keys
+  constexpr int CB = KdKey<KT>::CB, AS = KdKey<KT>::AS;
+  constexpr KT CMASK = ((KT)1 << CB) - 1;
+  KT* sb = (KT*)kd_dyn;                                                // P2 sort keys
   int P2 = 16;
   while (P2 < C) P2 <<= 1;
-  double* pt = (double*)(sb + P2);                                     // stride x M
+  double* pt = (double*)(kd_dyn + (size_t)P2 * 8);                     // stride x M
   unsigned short* rk = (unsigned short*)(pt + (size_t)stride * M);     // M x stride
   const double* gp = pts + (size_t)s * stride * M;
   const int* gr0 = rank0 + (size_t)s * stride;
+  CKD_T(0);
+#ifdef EVR_CKD_PROF
+  if (tid == 0 && s < 4096)
+    for (int k = 2; k < 8; ++k) ckd_prof[16 * s + k] = 0;
+#endif
   for (int e = tid; e < stride * M; e += KD_THREADS) pt[e] = gp[e];
   __syncthreads();
   // 1. rank tables and ascending lower-bound values per objective
@@ -124,11 +250,18 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
     segS[g] = 0;
     segE[g] = G;
   }
-  for (int i = tid; i < P2; i += KD_THREADS) sb[i] = (i < C) ? (unsigned long long)i : ~0ull;
+  for (int i = tid; i < P2; i += KD_THREADS) sb[i] = (i < C) ? (KT)i : ~(KT)0;
   __syncthreads();
+  CKD_T(1);
   // 2. kd levels
   for (int level = 0; level < 32; ++level) {
-    if (tid == 0) sh_any = 0;
+    unsigned long long ck = CKD_NOW();
+    (void)ck;
+    if (tid == 0) {
+      sh_any = 0;
+      sh_maxlen = 0;
+      sh_nseg = 0;
+    }
     for (int g = tid; g < G; g += KD_THREADS) {
       if (segS[g] == g) {
 #pragma unroll
@@ -147,8 +280,12 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
       const int ncell = min(16 * e, C) - 16 * a;
       if (ncell <= 16) continue;
       sh_any = 1;
+      if (g == a && (i & 15) == 0) {   // one lane per unfinished segment
+        atomicMax(&sh_maxlen, ncell);
+        segl[atomicAdd(&sh_nseg, 1)] = a;
+      }
       const bool in = i < C;
-      const int cell = in ? (int)(sb[i] & 0xFFFFu) : 0;
+      const int cell = in ? (int)(sb[i] & CMASK) : 0;
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         unsigned int lo = in ? rank_of(cell, j) : 0xFFFFFFFFu, hi = in ? lo : 0u;
@@ -164,12 +301,14 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
       }
     }
     __syncthreads();
+    CKD_ACC(2, ck);
     if (!sh_any) break;
+    ck = CKD_NOW();
     for (int i = tid; i < C; i += KD_THREADS) {
       const int g = i >> 4, a = segS[g], e = segE[g];
       const int ncell = min(16 * e, C) - 16 * a;
-      const int cell = (int)(sb[i] & 0xFFFFu);
-      unsigned long long v;
+      const int cell = (int)(sb[i] & CMASK);
+      KT v;
       if (ncell > 16) {
         int jb = 0;
         unsigned int best = mx[a][0] - mn[a][0];
@@ -183,40 +322,54 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
         }
         v = rank_of(cell, jb);
       } else {
-        v = (unsigned long long)i;  // finished segment: keep its order
+        v = (KT)(i - 16 * a);  // finished segment: keep its order
       }
-      sb[i] = ((unsigned long long)a << 40) | (v << 16) | (unsigned long long)cell;
+      sb[i] = ((KT)a << AS) | (v << CB) | (KT)cell;
     }
     __syncthreads();
-    kd_bitonic(sb, P2);
+    CKD_ACC(3, ck);
+    ck = CKD_NOW();
+    // the levels whose segments fit a wave sort them apart; the first levels sort the whole
+    // buffer (ws_max = 0, EVR_KD_WS=0: always the full sort — A/B, same order)
+    if (sh_maxlen <= ws_max) {
+      kd_wave_sort(sb, segl, sh_nseg, segE, C);
+      __syncthreads();
+    } else {
+      kd_bitonic(sb, P2);
+    }
+    CKD_ACC(4, ck);
+    ck = CKD_NOW();
+#ifdef EVR_CKD_PROF
+    if (tid == 0 && s < 4096) ckd_prof[16 * s + 7] += 1;
+#endif
     // split: [a, e) -> [a, a + h), [a + h, e), h = ceil(ncell / 32) groups
-    int na[KD_MAX_GROUPS / KD_THREADS + 1], ne[KD_MAX_GROUPS / KD_THREADS + 1];
-    int t = 0;
-    for (int g = tid; g < G; g += KD_THREADS, ++t) {
-      const int a = segS[g], e = segE[g];
+    static_assert(KD_MAX_GROUPS <= KD_THREADS, "one group per thread in the split");
+    int na = 0, ne = 0;
+    if (tid < G) {
+      const int g = tid, a = segS[g], e = segE[g];
       const int ncell = min(16 * e, C) - 16 * a;
-      na[t] = a;
-      ne[t] = e;
+      na = a;
+      ne = e;
       if (ncell > 16) {
         const int h = (ncell + 31) / 32;
-        if (g < a + h) ne[t] = a + h;
-        else na[t] = a + h;
+        if (g < a + h) ne = a + h;
+        else na = a + h;
       }
     }
     __syncthreads();
-    t = 0;
-    for (int g = tid; g < G; g += KD_THREADS, ++t) {
-      segS[g] = na[t];
-      segE[g] = ne[t];
+    if (tid < G) {
+      segS[tid] = na;
+      segE[tid] = ne;
     }
     __syncthreads();
+    CKD_ACC(5, ck);
   }
   // 3. outputs: keys, rank coordinates and group minimum corners
   for (int i = tid; i < G * 16; i += KD_THREADS) {
     const int g = i >> 4, w = i & 15;
     const size_t gg = (size_t)(g0 + g);
     if (i < C) {
-      const int cell = (int)(sb[i] & 0xFFFFu);
+      const int cell = (int)(sb[i] & CMASK);
       const unsigned long long key = keys[c0 + cell];
       okeys[gg * 16 + w] = K::set(key, 0, gr0[K::field(key, 0)]);   // field 0: rank -> point index
 #pragma unroll
@@ -238,6 +391,7 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
     }
     ogb[(size_t)(g0 + g) * 8 + j] = v;
   }
+  CKD_T(6);
 }
 
 }  // namespace evr
@@ -245,6 +399,15 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
 using namespace evr;
 
 extern "C" {
+
+#ifdef EVR_CKD_PROF
+// profiling builds only: copy the per-sample phase clocks (16 per sample) to the host
+int evr_ckd_prof_read(unsigned long long* host, int nsamples) {
+  EVR_HIP(hipDeviceSynchronize());
+  EVR_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(ckd_prof), sizeof(unsigned long long) * 16 * (size_t)nsamples));
+  return 0;
+}
+#endif
 
 int evr_cells_kd_limits(int stride, int m, int max_cells, long long* lds_bytes) {
   EVR_CHECK(stride > 0 && m >= 1 && m <= 8, "evr_cells_kd_limits: bad arguments");
@@ -265,12 +428,23 @@ int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int*
   EVR_CHECK(evr_cells_kd_limits(stride, m, max_cells, &lds) == 0,
             "evr_cells_kd_order_device: %d cells / %d point rows exceed the kd kernel limits", max_cells, stride);
   hipStream_t s = (hipStream_t)stream;
-#define L(MM)                                                                                            \
-  do {                                                                                                   \
-    EVR_HIP(hipFuncSetAttribute((const void*)cells_kd_kernel<MM>,                                       \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                  \
-    cells_kd_kernel<MM><<<S, KD_THREADS, lds, s>>>(stride, off, goff, keys, pts, rank0, okeys, ork, ogb, \
-                                                   osv);                                                 \
+  // u32 sort keys when every field fits (KdKey); EVR_KD_KEY64=1 keeps the u64 layout (A/B: same order)
+  const char* ek = std::getenv("EVR_KD_KEY64");   // read per call (a test switches it)
+  const bool key64 = ek && ek[0] == '1';
+  const bool k32 = !key64 && max_cells < 8192 && stride < 1023;
+  const char* ew = std::getenv("EVR_KD_WS");   // read per call (a test switches it)
+  const int ws_max = (ew && ew[0] == '0') ? 0 : KD_WS_MAX;
+#define LK(MM, KT_)                                                                                        \
+  do {                                                                                                     \
+    EVR_HIP(hipFuncSetAttribute((const void*)cells_kd_kernel<MM, KT_>,                                    \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                    \
+    cells_kd_kernel<MM, KT_><<<S, KD_THREADS, lds, s>>>(stride, off, goff, keys, pts, rank0, okeys, ork, ogb, \
+                                                        osv, ws_max);                                              \
+  } while (0)
+#define L(MM)                             \
+  do {                                    \
+    if (k32) LK(MM, unsigned int);        \
+    else LK(MM, unsigned long long);      \
   } while (0)
   switch (m) {
     case 1: L(1); break;
@@ -283,6 +457,7 @@ int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int*
     case 8: L(8); break;
   }
 #undef L
+#undef LK
   EVR_LAUNCH_CHECK();
   return 0;
 }

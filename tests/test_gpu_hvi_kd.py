@@ -160,6 +160,24 @@ def test_kd_index_invariants():
     assert np.array_equal(np.sort(lo_rank, axis=0), np.sort(lo_x[:C], axis=0))
 
 
+@pytest.mark.parametrize("n,m,S", [(200, 5, 128), (60, 3, 32), (150, 4, 64), (512, 5, 32)])
+def test_kd_sort_variants_bitwise_equal(monkeypatch, n, m, S):
+    """The kd ordering's sort variants produce one ordering bitwise — u32 sort keys (the default
+    when every field fits) or u64 keys, per-segment wave sorts for the deep levels (default) or
+    the whole-buffer sort at every level: kd keys, rank coordinates, group minima and sorted
+    lower bounds."""
+    outs = []
+    for key64, ws in (("1", "0"), ("0", "0"), ("1", "1"), ("0", "1")):
+        monkeypatch.setenv("EVR_KD_KEY64", key64)
+        monkeypatch.setenv("EVR_KD_WS", ws)
+        kd, _, _, _, _ = _pair(n, 6, m, S, seed=n + m)
+        g = kd.cells.kd
+        outs.append([t.cpu() for t in (g.keys, g.rank, g.box, g.sorted_lo)])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 @pytest.fixture
 def restart_variant():
     """Select the one-launch restart scan (evr_hvi_set_restart_variant) and restore the default."""
