@@ -301,7 +301,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
   if (P2 <= sortcap) {
     for (int i = tid; i < P2; i += BD_THREADS) sbuf[i] = (i < C) ? buf[i] : BD_DEAD;
     __syncthreads();
-    bd_bitonic(sbuf, P2);
+    wg_bitonic<unsigned long long, BD_THREADS>(sbuf, P2);   // in-wave stages by shuffles (41 barriers, not 91)
     for (int i = tid; i < C; i += BD_THREADS) buf[i] = sbuf[i];
   } else {
     for (int i = C + tid; i < P2; i += BD_THREADS) buf[i] = BD_DEAD;  // P2 <= cap (cap is a power of 2)

@@ -50,52 +50,7 @@ __device__ unsigned long long ckd_prof[16 * 4096];
 #define CKD_NOW() 0ull
 #endif
 
-__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
-  const int lo = __shfl_xor((int)(unsigned)v, m, 64), hi = __shfl_xor((int)(unsigned)(v >> 32), m, 64);
-  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-
-// Bitonic sort of P2 (a power of two) unique keys in LDS.  Stages whose partner distance j is
-// at least 64 exchange through LDS (one barrier each); the stages with j < 64 pair lanes of one
-// wave (index i = tid + 1024 t, so a wave holds 64 consecutive keys) and run in registers by
-// xor-shuffles, min / max per pair, with one barrier per merge size: 41 instead of 91 barriers
-// per sort at P2 = 8192.  Same result as the compare-and-swap network (keys are unique).
-__device__ __forceinline__ unsigned int shfl_xor_key(unsigned int v, int m) {
-  return (unsigned int)__shfl_xor((int)v, m, 64);
-}
-__device__ __forceinline__ unsigned long long shfl_xor_key(unsigned long long v, int m) { return shfl_xor_u64(v, m); }
-
-template <typename KT>
-__device__ __forceinline__ void kd_bitonic(KT* a, int P2) {
-  for (int k = 2; k <= P2; k <<= 1) {
-    int j = k >> 1;
-    for (; j >= 64; j >>= 1) {
-      for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
-        const int l = i ^ j;
-        if (l > i) {
-          const KT x = a[i], y = a[l];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            a[i] = y;
-            a[l] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-    for (int i = threadIdx.x; i < P2; i += KD_THREADS) {
-      KT x = a[i];
-      const bool up = (i & k) == 0;
-      for (int jj = j; jj > 0; jj >>= 1) {
-        const KT y = shfl_xor_key(x, jj);
-        // the lower index of a pair keeps the minimum in an ascending run, the maximum otherwise
-        x = (((i & jj) == 0) == up) ? (x < y ? x : y) : (x < y ? y : x);
-      }
-      a[i] = x;
-    }
-    __syncthreads();
-  }
-}
+// the workgroup bitonic sort and the key shuffles: common.hpp (wg_bitonic, shared with box_device.hip)
 
 // Segmented sort of the kd levels whose unfinished segments all hold at most KD_WS_MAX cells:
 // one wave per segment (a compact list of segment start groups, dealt round-robin to the
@@ -103,7 +58,7 @@ __device__ __forceinline__ void kd_bitonic(KT* a, int P2) {
 // registers — lane l holds elements l + 64 t, t < P / 64 — with no workgroup barrier: the
 // partner of a stage j >= 64 is a register of the same lane, of a stage j < 64 the same
 // register of lane l ^ j.  The keys of one segment share the segment field, so the order is
-// the full sort's (kd_bitonic over all P2 keys: 91 stages and 41 barriers at P2 = 8192 for
+// the full sort's (wg_bitonic over all P2 keys: 91 stages and 41 barriers at P2 = 8192 for
 // every level, even when the segments hold a few dozen cells).
 constexpr int KD_WS_T = 16, KD_WS_MAX = 64 * KD_WS_T;
 // branch-free compare-exchange: keep = all ones selects the minimum (u32 / u64 min, max and
@@ -241,6 +196,8 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
     rk[j * stride + p] = (unsigned short)r;
     osv[((size_t)s * M + j) * stride + r] = v;
   }
+  // (an LDS cache of every cell's M ranks instead of this key -> rank0 -> rank-table chain
+  // measured the same: 129 vs 130 us of span passes per sample, profiles/r04/w)
   auto rank_of = [&](int cell, int j) -> unsigned int {
     const unsigned long long key = keys[c0 + cell];
     const int p = (j == 0) ? gr0[K::field(key, 0)] : K::field(key, j);
@@ -335,7 +292,7 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
       kd_wave_sort(sb, segl, sh_nseg, segE, C);
       __syncthreads();
     } else {
-      kd_bitonic(sb, P2);
+      wg_bitonic<KT, KD_THREADS>(sb, P2);
     }
     CKD_ACC(4, ck);
     ck = CKD_NOW();
