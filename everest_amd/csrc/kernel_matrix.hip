@@ -270,6 +270,137 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   }
 }
 
+// Symmetric train matrix K(X, X) (the GP fit's case: both operands the same rows with the same
+// normalisation): one workgroup per lower tile (I >= J) computes it exactly as
+// kmat_mfma_kernel does (same staging, MFMA order and epilogue — u_i . u_j and u_j . u_i are
+// the same products in the same k order, |u_i|^2 + |u_j|^2 commutes) and writes it twice: the
+// tile in place and, for I > J, its transpose through LDS as 512-byte row segments.  Half the
+// MFMA and epilogue work (the kernel is compute-heavy at d = 32: 17.7 us without the kernel
+// evaluation vs 24.5 us, profiles/r04/u), the same output stream.
+template <int DP, int KIND>
+__global__ __launch_bounds__(256) void kmat_mfma_sym(int n, int d, int B, const double* __restrict__ X,
+                                                     const double* __restrict__ sh, const double* __restrict__ sc,
+                                                     const double* __restrict__ ls, const double* __restrict__ os,
+                                                     const double* __restrict__ dg, double* __restrict__ K) {
+  constexpr int OPS = 2 * DP * (KT + 2), OUT = KT * (KT + 1);
+  __shared__ double smem[OPS > OUT ? OPS : OUT];
+  double (*As)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem);
+  double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
+  __shared__ double na[KT], nb2[KT];
+  __shared__ int eqr[KT];
+  __shared__ double kexp[64];
+  const int nt = (n + KT - 1) / KT, tpb = nt * (nt + 1) / 2;
+  const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int b = t / tpb, tl = t - b * tpb;
+  int I = (int)((sqrt(8.0 * tl + 1.0) - 1.0) * 0.5);   // lower tiles row-major: row I holds I + 1 tiles
+  while ((I + 1) * (I + 2) / 2 <= tl) ++I;
+  while (I * (I + 1) / 2 > tl) --I;
+  const int J = tl - I * (I + 1) / 2;
+  const int i0 = I * KT, j0 = J * KT;
+  const double* lsb = ls + (size_t)b * d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NE = (KT * DP + 255) / 256;
+  double v[NE], w[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 256 * q;
+    const int r = e / DP, k = e - r * DP;
+    v[q] = 0.0;
+    w[q] = 0.0;
+    if (e < KT * DP && k < d) {
+      if (i0 + r < n) v[q] = X[(size_t)(i0 + r) * d + k];
+      if (j0 + r < n) w[q] = X[(size_t)(j0 + r) * d + k];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 256 * q;
+    const int r = e / DP, k = e - r * DP;
+    if (e < KT * DP) {
+      double a = 0.0, c = 0.0;
+      if (k < d) {
+        const double il = 1.0 / lsb[k];
+        if (i0 + r < n) {
+          a = v[q];
+          if (sh) a -= sh[k];
+          if (sc) a *= sc[k];
+          a *= il;
+        }
+        if (j0 + r < n) {
+          c = w[q];
+          if (sh) c -= sh[k];
+          if (sc) c *= sc[k];
+          c *= il;
+        }
+      }
+      As[k][r] = a;
+      Bs[k][r] = c;
+    }
+  }
+  kexp_stage(kexp, tid, 256);
+  __syncthreads();
+  if (tid < 2 * KT) {
+    const int r = tid & (KT - 1);
+    double sq = 0.0;
+    if (tid < KT) {
+      int eq = 1;
+      for (int k = 0; k < DP; ++k) {
+        sq = fma(As[k][r], As[k][r], sq);
+        eq &= As[k][r] == Bs[k][r];
+      }
+      na[r] = sq;
+      eqr[r] = eq;
+    } else {
+      for (int k = 0; k < DP; ++k) sq = fma(Bs[k][r], Bs[k][r], sq);
+      nb2[r] = sq;
+    }
+  }
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int i = lane & 15, kq = lane >> 4;
+  kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int kk = 0; kk < DP; kk += 4) {
+    const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
+    const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+  }
+  __syncthreads();   // na / nb2 / eqr; every wave's As / Bs reads are done
+  const double scale = os ? os[b] : 1.0;
+  const double dadd = dg ? dg[b] : 0.0;
+  double* Kb = K + (size_t)b * n * n;
+  const int col = lane & 15, rq = lane >> 4;
+  double vals[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+      const int gi = i0 + li, gj = j0 + lj;
+      double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+      if (gi == gj && eqr[li]) d2 = 0.0;
+      double val = scale * kernel_value_t(KIND, d2, kexp);
+      if (gi == gj) val += dadd;
+      vals[4 * q + r] = val;
+      if (gi < n && gj < n) Kb[(size_t)gi * n + gj] = val;
+    }
+  if (I == J) return;
+  double (*T)[KT + 1] = reinterpret_cast<double (*)[KT + 1]>(smem);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[4 * q + r];
+  __syncthreads();
+  const int gc = i0 + lane;   // column of the transposed tile
+#pragma unroll 4
+  for (int rr = wave; rr < KT; rr += 4) {
+    const int gr = j0 + rr;
+    if (gr < n && gc < n) Kb[(size_t)gr * n + gc] = T[lane][rr];
+  }
+}
+
 // Persistent form of kmat_mfma_kernel for large outputs (DP = 16 / 32 / 64): a workgroup
 // walks tiles t = blockIdx.x, + gridDim.x, ...  The next tile's operand rows (and its
 // lengthscales) are loaded into registers right after the current tile's MFMAs, before the
@@ -777,6 +908,28 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
+    // the symmetric train matrix: lower tiles only (kmat_mfma_sym); EVR_KMAT_SYM=0 disables it
+    // (A/B and the bitwise test; read per call)
+    const char* esym = getenv("EVR_KMAT_SYM");
+    if (X1 == X2 && n1 == n2 && shift1 == shift2 && scale1 == scale2 && d <= 64 && d != 48 &&
+        !(esym && esym[0] == '0')) {
+      const int nt = cdiv(n1, KT);
+      const long long tiles = (long long)nt * (nt + 1) / 2 * B;
+#define KS(DP_, K_) kmat_mfma_sym<DP_, K_><<<(unsigned)tiles, 256, 0, s>>>(n1, d, B, X1, shift1, scale1, lengthscales, \
+                                                                          outputscale, diag_add, K)
+#define KSD(DP_)                                \
+  if (kind == RBF) KS(DP_, RBF);                \
+  else if (kind == MATERN05) KS(DP_, MATERN05); \
+  else if (kind == MATERN15) KS(DP_, MATERN15); \
+  else KS(DP_, MATERN25)
+      if (d <= 16) { KSD(16); }
+      else if (d <= 32) { KSD(32); }
+      else { KSD(64); }
+#undef KSD
+#undef KS
+      EVR_LAUNCH_CHECK();
+      return 0;
+    }
     // EVR_KMAT_PERS=<n>: the persistent pipelined form with n workgroups per CU (opt-in:
     // measured slower at config 5, 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — fewer
     // resident waves hide less latency than the load / store overlap gains)

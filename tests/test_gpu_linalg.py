@@ -155,6 +155,32 @@ def test_kernel_matrix_wide_mfma(d, kind):
         assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
 
 
+@pytest.mark.parametrize("n,d,kind,norm", [(300, 16, 0, True), (300, 32, 3, False), (130, 64, 2, True),
+                                           (2048, 32, 3, False), (65, 40, 1, True)])
+def test_kernel_matrix_symmetric_tiles_bitwise(monkeypatch, n, d, kind, norm):
+    """K(X, X) through the lower-tile kernel (kmat_mfma_sym: each tile computed once, written
+    in place and transposed) equals the all-tiles kernel bitwise (EVR_KMAT_SYM=0), and is
+    exactly symmetric."""
+    from everest_amd import ops
+
+    rng = np.random.default_rng(n + d)
+    B = 2
+    X = torch.tensor(rng.uniform(0, 2, size=(n, d)), device="cuda")
+    ls = torch.tensor(rng.uniform(0.5, 2.0, size=(B, d)), device="cuda")
+    noise = torch.tensor([1e-3, 2e-2], device="cuda", dtype=torch.float64)
+    kw = {}
+    if norm:
+        sh = torch.zeros(d, dtype=torch.float64, device="cuda")
+        sc = torch.full((d,), 0.5, dtype=torch.float64, device="cuda")
+        kw = dict(shift1=sh, scale1=sc, shift2=sh, scale2=sc)   # the same tensors: the symmetric path
+    monkeypatch.setenv("EVR_KMAT_SYM", "1")
+    Ks = ops.kernel_matrix(X, X, ls, kind, diag_add=noise, **kw).cpu()
+    monkeypatch.setenv("EVR_KMAT_SYM", "0")
+    Kf = ops.kernel_matrix(X, X, ls, kind, diag_add=noise, **kw).cpu()
+    assert torch.equal(Ks, Kf)
+    assert torch.equal(Ks, Ks.transpose(1, 2))
+
+
 @pytest.mark.parametrize("variant", ["la", "rl"])
 @pytest.mark.parametrize("n", [64, 65, 130, 513, 1024])
 def test_fused_cholesky_inverse_matches_torch_and_v1(n, variant, monkeypatch):

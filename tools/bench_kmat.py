@@ -27,21 +27,23 @@ out = {"variant": os.environ.get("EVR_KMAT", "rows"), "rpt": os.environ.get("EVR
        "exp": os.environ.get("EVR_KMAT_EXP", "fast")}
 cases = (("cfg3_cross_b512", 5, 512, 512, 6, 0), ("cfg3_cross_b20", 5, 512, 20, 6, 0),
          ("fit_train_n512", 1, 512, 512, 6, 0), ("cfg2_cross", 1, 256, 1024, 6, 0),
-         ("cfg5_n2048_d32", 1, 2048, 2048, 32, 3), ("n2048_d6", 1, 2048, 2048, 6, 0),
+         ("cfg5_n2048_d32", 1, 2048, 2048, 32, 3), ("cfg5_train_sym", 1, 2048, 2048, 32, 3),
+         ("n2048_d6", 1, 2048, 2048, 6, 0),
          ("cfg3_cross_b4096", 5, 512, 4096, 6, 0))
 only = os.environ.get("KMAT_CASES")
 for (name, B, n1, n2, d, kind) in cases:
     if only and name not in only.split(","):
         continue
     X1 = torch.rand(n1, d, dtype=torch.float64, device="cuda")
-    X2 = torch.rand(n2, d, dtype=torch.float64, device="cuda")
-    sh = torch.zeros(d, dtype=torch.float64, device="cuda")
-    sc = torch.ones(d, dtype=torch.float64, device="cuda")
+    sym = name.endswith("_sym")   # the fit's train matrix K(X, X): one tensor, no normalisation (kmat_mfma_sym)
+    X2 = X1 if sym else torch.rand(n2, d, dtype=torch.float64, device="cuda")
+    sh = None if sym else torch.zeros(d, dtype=torch.float64, device="cuda")
+    sc = None if sym else torch.ones(d, dtype=torch.float64, device="cuda")
     ls = torch.rand(B, d, dtype=torch.float64, device="cuda") + 0.3
     K = torch.empty(B, n1, n2, dtype=torch.float64, device="cuda")
     Kref = ops.kernel_matrix(X1, X2, ls, kind, shift2=sh, scale2=sc)
-    f = lambda: call("evr_kernel_matrix", _stream(), kind, B, n1, n2, d, X1.data_ptr(), 0, 0, X2.data_ptr(),
-                     sh.data_ptr(), sc.data_ptr(), ls.data_ptr(), 0, 0, K.data_ptr())
+    f = lambda: call("evr_kernel_matrix", _stream(), kind, B, n1, n2, d, X1.data_ptr(), 0, 0, X2.data_ptr(),  # noqa: E731
+                     _p(sh), _p(sc), ls.data_ptr(), 0, 0, K.data_ptr())
     t = ev(f)
     # exactness vs a torch fp64 restatement (explicit differences)
     u1 = X1[None] / ls[:, None, :]

@@ -7,6 +7,7 @@
 #   pytestf     the test files named in $PYTEST_FILES
 #   restartab   tools/restart_ab.py (restart-scan variants: scan / chain / round trip / optimiser per
 #               evaluation) -> <tag>/restart_ab.json
+#   kmat        tools/bench_kmat.py (kernel assembly: config 5 cross / symmetric train, fill ceiling)
 #   asktl       device timeline of one ask (tools/ask_timeline.py under rocprofv3 --kernel-trace)
 #               -> <tag>/ask_timeline.json
 #   planprobe   tools/plan_setup_probe.py (restart plan creation / first / warm evaluation)
@@ -52,6 +53,7 @@ for st in "$@"; do
     planprobe) run planprobe 300 python tools/plan_setup_probe.py ;;
     hostprof) run hostprof 300 python tools/ask_host_profile.py ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
+    kmat) KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6,fit_train_n512 run kmat 300 python tools/bench_kmat.py && cp "$OUT/kmat.log" "$OUT/kmat.json" ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
       cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
