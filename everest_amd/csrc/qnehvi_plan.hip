@@ -284,16 +284,34 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   return 0;
 }
 
+// One non-blocking capture stream per device for the plans' graph captures (created once:
+// a stream creation / destruction per plan cost host time at every ask's first restart
+// evaluation); the returned lock serialises captures across threads.
+static std::mutex g_cap_mu;
+static hipStream_t capture_stream(std::unique_lock<std::mutex>* lk) {
+  static hipStream_t streams[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  *lk = std::unique_lock<std::mutex>(g_cap_mu);
+  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
+    streams[dev] = nullptr;
+    lk->unlock();
+  }
+  return streams[dev];
+}
+
 // Capture the device-mode chain into p->exec (private stream: the caller's stream, torch's,
 // never enters capture mode).  On failure the plan keeps running the chain eagerly.
 static void plan_capture(evr_qnehvi_plan* p) {
   p->use_graph = 0;
-  hipStream_t cs = nullptr;
-  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return;
+  std::unique_lock<std::mutex> cap_lk;
+  hipStream_t cs = capture_stream(&cap_lk);
+  if (!cs) return;
   int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
   if (!rc) rc = plan_chain(cs, p, p->X);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);
+  cap_lk.unlock();
   if (!rc && e == hipSuccess && g && hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0) == hipSuccess) {
     p->graph = g;
   } else {
@@ -301,7 +319,6 @@ static void plan_capture(evr_qnehvi_plan* p) {
     p->exec = nullptr;
     (void)hipGetLastError();
   }
-  (void)hipStreamDestroy(cs);
 }
 
 int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
@@ -318,7 +335,7 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
   int dev = -1;
-  if (graph_reuse() && p->hexec && p->hx && p->hout && p->counter && hipGetDevice(&dev) == hipSuccess) {
+  if (graph_reuse() && p->hexec && p->hx && p->hout && hipGetDevice(&dev) == hipSuccess) {
     // the plan's evaluations have completed (plan_eval_raw waits for each), so the buffers and
     // the executable are idle; the counter is back at 0 (the last workgroup resets it)
     std::lock_guard<std::mutex> lk(g_hres_mu);
@@ -348,7 +365,7 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   hipGraphExec_t old_exec = nullptr;
   hipGraph_t old_graph = nullptr;
   int dev = -1;
-  if (graph_reuse() && !p->hx && !p->hout && !p->counter && hipGetDevice(&dev) == hipSuccess) {
+  if (graph_reuse() && !p->hx && !p->hout && hipGetDevice(&dev) == hipSuccess) {
     std::lock_guard<std::mutex> lk(g_hres_mu);
     for (size_t i = 0; i < g_hres.size(); ++i) {
       const PlanHostRes& r = g_hres[i];
@@ -373,10 +390,12 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   double *dhx = nullptr, *dhout = nullptr;
   EVR_HIP(hipHostGetDevicePointer((void**)&dhx, p->hx, 0));
   EVR_HIP(hipHostGetDevicePointer((void**)&dhout, p->hout, 0));
-  if (!p->counter) EVR_HIP(hipMalloc((void**)&p->counter, 16));
-  EVR_HIP(hipMemset(p->counter, 0, 16));   // completion counter and the served sequence number
-  hipStream_t cs = nullptr;
-  EVR_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  // (no completion counter since round 4: its hipMalloc and the synchronous hipMemset — which
+  // waited for the device to drain — were the setup's largest host stalls, with the stream
+  // creation / destruction now replaced by one capture stream per device)
+  std::unique_lock<std::mutex> cap_lk;
+  hipStream_t cs = capture_stream(&cap_lk);
+  EVR_CHECK(cs, "qnehvi plan: no capture stream");
   int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
   if (!rc) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
@@ -388,7 +407,7 @@ static int plan_host_setup(evr_qnehvi_plan* p) {
   }
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);
-  (void)hipStreamDestroy(cs);
+  cap_lk.unlock();
   if (old_exec) {
     hipGraphNode_t err_node = nullptr;
     hipGraphExecUpdateResult ur = hipGraphExecUpdateError;
