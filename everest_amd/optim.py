@@ -148,6 +148,40 @@ def draw_sobol_samples(bounds: np.ndarray, n: int, seed: int, q: int = 1) -> np.
     return X[:, 0] if q == 1 else X
 
 
+_RAW_POOL = None
+_RAW_PREFETCHED: dict = {}
+
+
+def _raw_key(bounds: np.ndarray, n: int, seed: int, q: int):
+    return int(seed), int(n), int(q), np.asarray(bounds, dtype=np.float64).tobytes()
+
+
+def prefetch_raw_samples(bounds: np.ndarray, n: int, gen: torch.Generator, q: int = 1) -> None:
+    """Start optimize_acqf's raw Sobol draw on a worker thread as soon as its seed is known:
+    the seed is the generator's next draw once the acquisition has drawn its own seeds, so a
+    strategy can peek at it (on a copy of the generator) before the acquisition's construction
+    and have the draw ready when raw screening starts.  optimize_acqf takes the future if
+    (seed, n, q, bounds) match and draws itself otherwise; the values are the same either way.
+    EVR_RAW_PREFETCH=0 disables."""
+    global _RAW_POOL
+    if os.environ.get("EVR_RAW_PREFETCH", "1") == "0":
+        return
+    g = torch.Generator()
+    g.set_state(gen.get_state())
+    seed = int(torch.randint(10_000_000, (1,), generator=g).item())
+    b = np.array(bounds, dtype=np.float64)
+    key = _raw_key(b, n, seed, q)
+    if key in _RAW_PREFETCHED:
+        return
+    while len(_RAW_PREFETCHED) >= 4:
+        _RAW_PREFETCHED.pop(next(iter(_RAW_PREFETCHED)))
+    if _RAW_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _RAW_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="evr-raw")
+    _RAW_PREFETCHED[key] = _RAW_POOL.submit(draw_sobol_samples, b, int(n), seed, int(q))
+
+
 def _as_Ab(d: int, bounds: np.ndarray, ineq: Sequence[LinearConstraint]):
     """Polytope A x <= b from bounds and BoTorch-form inequality constraints."""
     rows, rhs = [], []
@@ -415,7 +449,8 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
         if q > 1:
             X_raw = X_raw.reshape(raw_samples, q, d)
     else:
-        X_raw = draw_sobol_samples(bounds, raw_samples, seed, q)
+        fut = _RAW_PREFETCHED.pop(_raw_key(bounds, raw_samples, seed, q), None)
+        X_raw = fut.result() if fut is not None else draw_sobol_samples(bounds, raw_samples, seed, q)
     shp = (q, d) if q > 1 else (d,)          # one candidate (q-batch) of the acquisition
     # 2. evaluate (sharded over ranks, all-gather of the per-shard values)
     Xr = torch.as_tensor(X_raw, dtype=torch.float64, device=dev)

@@ -22,7 +22,8 @@ from . import data_models as dm
 from . import ops
 from .acquisition import QEHVI, QEI, QEIJoint, QLogEHVI, QLogNEHVI, QNEHVI, prefetch_scramble
 from .data_models.domain import CloseToTargetObjective, MaximizeObjective, MinimizeObjective
-from .optim import OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed
+from .optim import (OptimizeStats, hit_and_run, host_values, optimize_acqf, optimize_acqf_mixed,
+                    prefetch_raw_samples)
 from .surrogates import BotorchSurrogates, device
 
 
@@ -653,6 +654,13 @@ class QnehviStrategy(QehviStrategy):
         sampler_seed = self._draw_seed()
         if os.environ.get("EVR_SCRAMBLE_PREFETCH", "1") != "0":
             prefetch_scramble(int(X_train.shape[0]) * int(self.model.B), prune_seed)
+        # optimize_acqf's raw-sample seed is the generator's next draw: its Sobol draw runs on a
+        # worker thread while the acquisition is built (plain box bounds only; otherwise the
+        # optimiser draws as usual)
+        if (not get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
+                and not get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
+                and len(self.get_categorical_combinations()) <= 1):
+            prefetch_raw_samples(self._bounds(), self.num_raw_samples, self.gen, q=n)
         objectives, constraints = self._objective_spec()
         ref = self.get_adjusted_refpoint()
         acqf = QNEHVI(self.model, self.model.X_raw, X_train, ref, None, None, S=self.num_sobol_samples,

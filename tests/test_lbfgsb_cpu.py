@@ -105,3 +105,22 @@ def test_nonfinite_trial_points_are_rejected(which):
     assert all(np.all(np.isfinite(x)) for x in seen)
     assert np.all(np.isfinite(r.x)) and np.isfinite(r.fun)
     assert np.all(r.x <= 2.5) and np.all(r.x > 2.0)
+
+
+def test_raw_sample_prefetch_equals_direct_draw():
+    """optim.prefetch_raw_samples peeks at the generator's next seed and draws the raw Sobol
+    samples on a worker thread; the future optimize_acqf takes holds exactly the direct draw,
+    and the real generator is not advanced by the peek."""
+    import numpy as np
+    import torch
+
+    from everest_amd import optim
+
+    g = torch.Generator().manual_seed(11)
+    state = g.get_state()
+    bounds = np.array([[0.0, -1.0, 2.0], [1.0, 1.0, 5.0]])
+    optim.prefetch_raw_samples(bounds, 256, g, q=2)
+    assert torch.equal(g.get_state(), state)
+    seed = int(torch.randint(10_000_000, (1,), generator=g).item())
+    fut = optim._RAW_PREFETCHED.pop(optim._raw_key(bounds, 256, seed, 2))
+    assert np.array_equal(fut.result(), optim.draw_sobol_samples(bounds, 256, seed, 2))
