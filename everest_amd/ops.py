@@ -743,16 +743,6 @@ def kd_supported(cells: Cells) -> bool:
     return _native.load().evr_cells_kd_limits(cells.stride, cells.m, cells.max_cells, None) == 0
 
 
-def _to_device_async(a: np.ndarray, dev) -> torch.Tensor:
-    """Host array -> device tensor through torch's cached pinned staging, without blocking the
-    host (a pageable .to(dev) waits for its copy: two such waits sat between the box kernels).
-    The pinned block is not reused before the copy's stream has passed it (torch records it)."""
-    t = torch.from_numpy(np.ascontiguousarray(a))
-    if dev is None or torch.device(dev).type != "cuda":
-        return t.to(dev)
-    return t.pin_memory().to(dev, non_blocking=True)
-
-
 def cells_kd_order(cells: Cells) -> KdGroups:
     """kd order + rank index of compressed cells (one workgroup per sample); attaches and
     returns the KdGroups (the HVI scan then runs the sparse three-level filter)."""
@@ -764,7 +754,7 @@ def cells_kd_order(cells: Cells) -> KdGroups:
     goff_h = np.zeros(S + 1, dtype=np.int64)
     np.cumsum(ng, out=goff_h[1:])
     G = int(goff_h[-1])
-    goff = _to_device_async(goff_h.astype(np.int32), dev)
+    goff = torch.as_tensor(goff_h.astype(np.int32)).to(dev)
     keys = torch.empty(max(G, 1) * 16, dtype=torch.int64, device=dev)
     rank = torch.empty(max(G, 1) * m * 16, dtype=torch.int16, device=dev)       # uint16 bit patterns
     box = torch.empty(max(G, 1) * 8, dtype=torch.int16, device=dev)
@@ -811,7 +801,7 @@ def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, m
     off_h = np.zeros(S + 1, dtype=np.int64)
     np.cumsum(counts, out=off_h[1:])
     total = int(off_h[-1])
-    off = _to_device_async(off_h.astype(np.int32), dev)
+    off = torch.as_tensor(off_h.astype(np.int32)).to(dev)
     stride = n + m
     keys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)      # uint64 bit patterns
     pts = torch.empty(S, stride, m, dtype=torch.float64, device=dev)
