@@ -109,6 +109,8 @@ _SIGS = {
                                   c_void_p], c_int),
     "evr_box_pack_keys_device": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                   c_void_p, c_void_p], c_int),
+    "evr_box_kd_pipeline": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 8
+                            + [c_int] + [c_void_p] * 6, c_int),
     "evr_cells_from_keys": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int] + [c_void_p] * 5, c_int),
     "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
     "evr_hvi_restart_fb_applies": ([POINTER(EvrQnehviState), c_int], c_int),

@@ -131,8 +131,12 @@ def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None
     if approx and box_device:
         raise ValueError("the device box decomposition is exact only (alpha = 0)")
     if not approx and (box_device if box_device is not None else ops.box_device_supported(P, m)):
+        kd_built = False
         try:
-            cells = ops.box_decompose_device(O, ref)
+            if kd_scan is False or os.environ.get("EVR_BOX_PIPELINE", "1") == "0":
+                cells = ops.box_decompose_device(O, ref)
+            else:   # box, pack and kd order in one native call (EVR_BOX_PIPELINE=0: the op sequence)
+                cells, kd_built = ops.box_decompose_kd_device(O, ref, want_kd=True)
         except ops.BoxCapacityError as e:
             if box_device:      # explicitly requested: surface the limit
                 raise
@@ -140,7 +144,9 @@ def _decompose(O: torch.Tensor, ref: torch.Tensor, box_device=None, kd_scan=None
             cells = None
         if cells is not None:
             path = "device"
-            if kd_scan if kd_scan is not None else ops.kd_supported(cells):
+            if kd_built:
+                path = "device+kd"
+            elif kd_scan if kd_scan is not None else ops.kd_supported(cells):
                 ops.cells_kd_order(cells)
                 path = "device+kd"
             elif kd_scan is None:

@@ -463,4 +463,75 @@ int evr_box_pack_keys_device(void* stream, int S, int n, int m, int cap, const v
   return 0;
 }
 
+
+// The device box decomposition, its packing and the kd ordering in one host call (the box
+// worker thread of acquisition._decompose_async): bd_build, the per-sample counts to pinned
+// host memory (the one synchronisation), the cell / group offsets formed on the host and sent
+// back from the same pinned staging, then the pack and kd launches — no Python, hence no GIL
+// hand-over, between the kernels (the Python sequence left ≈ 0.25 ms between bd_build and the
+// pack launch, profiles/r04/z).  Outputs are sized by the caller for the capacity: keys S cap,
+// okeys 16 (S cap / 16 + S), ork 16 m (S cap / 16 + S), ogb 8 (S cap / 16 + S).  want_kd: 0
+// no kd, 1 kd when evr_cells_kd_limits accepts the counts.  info[0] = 1 when a sample overflowed
+// cap (nothing packed: rerun with a larger cap), info[1] = 1 when the kd order was built,
+// info[2] = the largest per-sample cell count; counts_host[s] = cells of sample s.
+int evr_box_kd_pipeline(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
+                        void* work, int* counts_dev, int* status_dev, int* off_dev, int* goff_dev,
+                        unsigned long long* keys, double* pts, int* rank0, int want_kd, unsigned long long* okeys,
+                        unsigned short* ork, unsigned short* ogb, double* osv, int* counts_host, int* info) {
+  EVR_CHECK(S >= 1 && counts_dev && status_dev && off_dev && goff_dev && keys && pts && rank0 && counts_host &&
+                info && (!want_kd || (okeys && ork && ogb && osv)),
+            "evr_box_kd_pipeline: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (int rc = evr_box_decompose_device(stream, S, n, m, obj, ref, cap, work, counts_dev, status_dev)) return rc;
+  // pinned staging per thread: [counts S | status S] in, [off S+1 | goff S+1] out; the out
+  // half is free again at the next call's synchronisation (same stream order)
+  thread_local int* stage = nullptr;
+  thread_local size_t stage_n = 0;
+  const size_t need = (size_t)4 * S + 2;
+  if (stage_n < need) {
+    if (stage) (void)hipHostFree(stage);
+    stage = nullptr;
+    stage_n = 0;
+    EVR_HIP(hipHostMalloc((void**)&stage, sizeof(int) * need, hipHostMallocDefault));
+    stage_n = need;
+  }
+  int* hc = stage;
+  int* hs = stage + S;
+  int* hoff = stage + 2 * S;
+  int* hgoff = hoff + S + 1;
+  EVR_HIP(hipMemcpyAsync(hc, counts_dev, sizeof(int) * S, hipMemcpyDeviceToHost, s));
+  EVR_HIP(hipMemcpyAsync(hs, status_dev, sizeof(int) * S, hipMemcpyDeviceToHost, s));
+  EVR_HIP(hipStreamSynchronize(s));
+  info[0] = info[1] = info[2] = 0;
+  int maxc = 0;
+  for (int i = 0; i < S; ++i) {
+    counts_host[i] = hc[i];
+    if (hs[i]) info[0] = 1;
+    maxc = std::max(maxc, hc[i]);
+  }
+  info[2] = maxc;
+  if (info[0]) return 0;
+  long long c = 0, g = 0;
+  for (int i = 0; i < S; ++i) {
+    hoff[i] = (int)c;
+    hgoff[i] = (int)g;
+    c += hc[i];
+    g += (hc[i] + 15) / 16;
+  }
+  hoff[S] = (int)c;
+  hgoff[S] = (int)g;
+  EVR_CHECK(c <= (long long)S * cap && c < 0x7FFFFFFFLL, "evr_box_kd_pipeline: %lld cells exceed the capacity", c);
+  EVR_HIP(hipMemcpyAsync(off_dev, hoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  EVR_HIP(hipMemcpyAsync(goff_dev, hgoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  if (int rc = evr_box_pack_keys_device(stream, S, n, m, cap, work, off_dev, maxc, keys, pts, rank0)) return rc;
+  const int stride = n + m;
+  if (want_kd && evr_cells_kd_limits(stride, m, maxc, nullptr) == 0) {
+    if (int rc = evr_cells_kd_order_device(stream, S, m, stride, off_dev, goff_dev, maxc, keys, pts, rank0, okeys,
+                                           ork, ogb, osv))
+      return rc;
+    info[1] = 1;
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -811,6 +811,57 @@ def box_decompose_device(O: torch.Tensor, ref: torch.Tensor, cap: int = 16384, m
     return Cells(off, counts, m, keys=keys, pts=pts, rank0=rank0, stride=stride)
 
 
+def box_decompose_kd_device(O: torch.Tensor, ref: torch.Tensor, want_kd: bool = True, cap: int = 16384,
+                            max_cap: int = 1 << 20, max_workspace_bytes: int = 8 << 30):
+    """box_decompose_device + cells_kd_order in one native call (evr_box_kd_pipeline): the
+    count read-back, the offsets and the pack / kd launches happen in C++ with the GIL released,
+    so no Python runs between the kernels.  Outputs are allocated for the capacity and returned
+    as views of the used prefix.  Returns (cells, kd_built); cells.kd is attached when built."""
+    O, ref = _dev(O, "O"), _dev(ref, "ref")
+    m, n, S = O.shape
+    dev = O.device
+    stride = n + m
+    lib = _native.load()
+    counts_h = np.zeros(S, dtype=np.int32)
+    info = np.zeros(3, dtype=np.int32)
+    while True:
+        nbytes = lib.evr_box_device_workspace_bytes(S, n, m, cap)
+        if nbytes > max_workspace_bytes:
+            raise BoxCapacityError(f"box decomposition: {cap} LUB slots x {S} samples need {nbytes} B of workspace")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        cs = torch.empty(2, S, dtype=torch.int32, device=dev)
+        offs = torch.empty(2, S + 1, dtype=torch.int32, device=dev)
+        keys = torch.empty(S * cap, dtype=torch.int64, device=dev)           # uint64 bit patterns
+        pts = torch.empty(S, stride, m, dtype=torch.float64, device=dev)
+        rank0 = torch.empty(S, stride, dtype=torch.int32, device=dev)
+        G = S * cap // 16 + S
+        if want_kd:
+            okeys = torch.empty(G * 16, dtype=torch.int64, device=dev)
+            ork = torch.empty(G * m * 16, dtype=torch.int16, device=dev)    # uint16 bit patterns
+            ogb = torch.empty(G * 8, dtype=torch.int16, device=dev)
+            osv = torch.empty(S, m, stride, dtype=torch.float64, device=dev)
+        else:
+            okeys = ork = ogb = osv = None
+        call("evr_box_kd_pipeline", _stream(), S, n, m, O.data_ptr(), ref.data_ptr(), cap, ws.data_ptr(),
+             cs[0].data_ptr(), cs[1].data_ptr(), offs[0].data_ptr(), offs[1].data_ptr(), keys.data_ptr(),
+             pts.data_ptr(), rank0.data_ptr(), int(bool(want_kd)), _p(okeys), _p(ork), _p(ogb), _p(osv),
+             counts_h.ctypes.data, info.ctypes.data)
+        if not info[0]:
+            break
+        if cap >= max_cap:
+            raise BoxCapacityError(f"box decomposition: more than {max_cap} local upper bounds in one sample")
+        cap *= 4
+    counts = counts_h.astype(np.int64)
+    total = int(counts.sum())
+    cells = Cells(offs[0], counts, m, keys=keys[:max(total, 1)], pts=pts, rank0=rank0, stride=stride)
+    if info[1]:
+        ng = (counts + 15) // 16
+        Gu = int(ng.sum())
+        cells.kd = KdGroups(offs[1], okeys[:max(Gu, 1) * 16], ork[:max(Gu, 1) * m * 16], ogb[:max(Gu, 1) * 8], osv,
+                            int(ng.max()) if S else 0)
+    return cells, bool(info[1])
+
+
 _SOBOL_DIRECTIONS = {}
 
 

@@ -474,6 +474,17 @@ int evr_cells_from_keys(void* stream, int S, int m, int stride, const int* off, 
  * stride fit the kernel (LDS sort buffer), else 3 (the tiled scan is used then).
  * Replaces nothing in the reference: an MI355X-side index over the [upstream]
  * FastNondominatedPartitioning cells (bofire/strategies/predictives/qnehvi.py:50). */
+/* evr_box_decompose_device + evr_box_pack_keys_device + evr_cells_kd_order_device in one host
+ * call with one synchronisation (the per-sample counts): outputs sized by the caller for the
+ * capacity (keys S*cap; okeys 16*G, ork 16*m*G, ogb 8*G with G = S*cap/16 + S; off / goff S+1);
+ * info[0] = 1: a sample overflowed cap (rerun with a larger cap), info[1] = 1: kd order built,
+ * info[2] = largest per-sample count; counts_host[s] = cells of sample s.  Replaces the
+ * reference's host-side partition + cell list (bofire/strategies/predictives/qnehvi.py:39-52
+ * -> [upstream] FastNondominatedPartitioning) for the sparse scan in one step. */
+int evr_box_kd_pipeline(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
+                        void* work, int* counts_dev, int* status_dev, int* off_dev, int* goff_dev,
+                        unsigned long long* keys, double* pts, int* rank0, int want_kd, unsigned long long* okeys,
+                        unsigned short* ork, unsigned short* ogb, double* osv, int* counts_host, int* info);
 int evr_cells_kd_limits(int stride, int m, int max_cells, long long* lds_bytes);
 int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int* off, const int* goff,
                               int max_cells, const unsigned long long* keys, const double* pts,

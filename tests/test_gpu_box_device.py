@@ -90,3 +90,23 @@ def test_device_box_lds_slab_equals_hbm_slab(m, n, S, monkeypatch):
     c2 = ops.box_decompose_device(Od, ref)
     assert torch.equal(c1.off, c2.off) and torch.equal(c1.keys, c2.keys)
     assert torch.equal(c1.pts, c2.pts) and torch.equal(c1.rank0, c2.rank0)
+
+
+@pytest.mark.parametrize("m,n,S,cap", [(5, 120, 32, 16384), (3, 60, 16, 4), (2, 40, 8, 16384), (6, 40, 4, 64)])
+def test_box_kd_pipeline_equals_op_sequence(m, n, S, cap):
+    """evr_box_kd_pipeline (box, pack and kd order in one native call, capacity-sized outputs,
+    the overflow rerun included at cap = 4 / 64) equals box_decompose_device + cells_kd_order
+    bitwise: offsets, counts, keys, point tables, kd keys, rank coordinates, group minima,
+    sorted lower bounds."""
+    O = _front(S, n, m, seed=7 * m + n)
+    Od = torch.tensor(np.ascontiguousarray(O.transpose(2, 1, 0)), device="cuda")
+    ref = torch.tensor(-1.1 * np.ones(m), device="cuda")
+    c1 = ops.box_decompose_device(Od, ref, cap=cap)
+    k1 = ops.cells_kd_order(c1)
+    c2, built = ops.box_decompose_kd_device(Od, ref, want_kd=True, cap=cap)
+    assert built and c2.kd is not None
+    assert np.array_equal(c1.counts, c2.counts)
+    for a, b in ((c1.off, c2.off), (c1.keys, c2.keys), (c1.pts, c2.pts), (c1.rank0, c2.rank0),
+                 (k1.goff, c2.kd.goff), (k1.keys, c2.kd.keys), (k1.rank, c2.kd.rank), (k1.box, c2.kd.box),
+                 (k1.sorted_lo, c2.kd.sorted_lo)):
+        assert torch.equal(a.cpu(), b.cpu())
