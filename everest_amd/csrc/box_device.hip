@@ -97,7 +97,8 @@ template <int M, bool LS>
 __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, const double* __restrict__ obj,
                                                               const double* __restrict__ ref, int cap, int sortcap,
                                                               unsigned char* __restrict__ ws, BdLayout Lo,
-                                                              int* __restrict__ counts, int* __restrict__ status) {
+                                                              int* __restrict__ counts, int* __restrict__ status,
+                                                              int* hmap) {
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
@@ -270,6 +271,10 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
     if (tid == 0) {
       status[s] = 1;
       counts[s] = 0;
+      if (hmap) {   // the host's mapped copy (evr_box_kd_pipeline): visible at the kernel's end
+        hmap[s] = 0;
+        hmap[S + s] = 1;
+      }
     }
     return;
   }
@@ -315,6 +320,10 @@ __global__ __launch_bounds__(BD_THREADS) void bd_build_kernel(int S, int n, cons
     counts[s] = C;
     status[s] = 0;
     ((int*)(ws + Lo.off_nf))[s] = nf;
+    if (hmap) {
+      hmap[s] = C;
+      hmap[S + s] = 0;
+    }
   }
 }
 
@@ -395,8 +404,17 @@ long long evr_box_device_workspace_bytes(int S, int n, int m, int cap) {
   return (long long)bd_layout(S, n, m, cap).bytes;
 }
 
+static int box_decompose_launch(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
+                                void* work, int* counts, int* status, int* hmap);
+
 int evr_box_decompose_device(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
                              void* work, int* counts, int* status) {
+  return box_decompose_launch(stream, S, n, m, obj, ref, cap, work, counts, status, nullptr);
+}
+
+// hmap: optional device pointer of mapped host memory receiving [counts S | status S]
+static int box_decompose_launch(void* stream, int S, int n, int m, const double* obj, const double* ref, int cap,
+                                void* work, int* counts, int* status, int* hmap) {
   EVR_CHECK(S >= 1 && n >= 1 && m >= 1 && m <= 8 && obj && ref && work && counts && status,
             "evr_box_decompose_device: bad arguments");
   EVR_CHECK(cap >= 2 && (cap & (cap - 1)) == 0, "evr_box_decompose_device: cap must be a power of two");
@@ -421,7 +439,7 @@ int evr_box_decompose_device(void* stream, int S, int n, int m, const double* ob
     EVR_HIP(hipFuncSetAttribute((const void*)bd_build_kernel<MM, LS_>,                                      \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                      \
     bd_build_kernel<MM, LS_><<<S, BD_THREADS, lds, s>>>(S, n, obj, ref, cap, sortcap, (unsigned char*)work, \
-                                                        Lo, counts, status);                                 \
+                                                        Lo, counts, status, hmap);                           \
   } while (0)
 #define L(MM)            \
   if (ls) L2(MM, true);  \
@@ -482,25 +500,31 @@ int evr_box_kd_pipeline(void* stream, int S, int n, int m, const double* obj, co
                 info && (!want_kd || (okeys && ork && ogb && osv)),
             "evr_box_kd_pipeline: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  if (int rc = evr_box_decompose_device(stream, S, n, m, obj, ref, cap, work, counts_dev, status_dev)) return rc;
-  // pinned staging per thread: [counts S | status S] in, [off S+1 | goff S+1] out; the out
-  // half is free again at the next call's synchronisation (same stream order)
+  // staging per thread in mapped, coherent host memory: bd_build writes [counts S | status S]
+  // there itself (no read-back copy); [off S+1 | goff S+1] are read from it by the pack and kd
+  // kernels and copied to the device arrays after them
   thread_local int* stage = nullptr;
+  thread_local int* stage_d = nullptr;
   thread_local size_t stage_n = 0;
   const size_t need = (size_t)4 * S + 2;
   if (stage_n < need) {
     if (stage) (void)hipHostFree(stage);
-    stage = nullptr;
+    stage = stage_d = nullptr;
     stage_n = 0;
-    EVR_HIP(hipHostMalloc((void**)&stage, sizeof(int) * need, hipHostMallocDefault));
+    EVR_HIP(hipHostMalloc((void**)&stage, sizeof(int) * need, hipHostMallocMapped | hipHostMallocCoherent));
+    EVR_HIP(hipHostGetDevicePointer((void**)&stage_d, stage, 0));
     stage_n = need;
   }
+  // the previous call's kernels and copies read the staging on their own stream: an event
+  // recorded after them is waited on before the staging is reused
+  thread_local hipEvent_t copied = nullptr;
+  if (!copied) EVR_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+  else EVR_HIP(hipEventSynchronize(copied));
   int* hc = stage;
   int* hs = stage + S;
   int* hoff = stage + 2 * S;
   int* hgoff = hoff + S + 1;
-  EVR_HIP(hipMemcpyAsync(hc, counts_dev, sizeof(int) * S, hipMemcpyDeviceToHost, s));
-  EVR_HIP(hipMemcpyAsync(hs, status_dev, sizeof(int) * S, hipMemcpyDeviceToHost, s));
+  if (int rc = box_decompose_launch(stream, S, n, m, obj, ref, cap, work, counts_dev, status_dev, stage_d)) return rc;
   EVR_HIP(hipStreamSynchronize(s));
   info[0] = info[1] = info[2] = 0;
   int maxc = 0;
@@ -521,16 +545,22 @@ int evr_box_kd_pipeline(void* stream, int S, int n, int m, const double* obj, co
   hoff[S] = (int)c;
   hgoff[S] = (int)g;
   EVR_CHECK(c <= (long long)S * cap && c < 0x7FFFFFFFLL, "evr_box_kd_pipeline: %lld cells exceed the capacity", c);
-  EVR_HIP(hipMemcpyAsync(off_dev, hoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
-  EVR_HIP(hipMemcpyAsync(goff_dev, hgoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
-  if (int rc = evr_box_pack_keys_device(stream, S, n, m, cap, work, off_dev, maxc, keys, pts, rank0)) return rc;
+  // the pack and kd kernels read the offsets straight from the mapped staging (a few reads
+  // per workgroup); the device copies the acquisition keeps follow them on the stream (blit
+  // copies ahead of the kernels queued behind the other stream's work: ≈ 0.13 ms, r04ze)
+  const int* moff = stage_d + 2 * S;
+  const int* mgoff = moff + S + 1;
+  if (int rc = evr_box_pack_keys_device(stream, S, n, m, cap, work, moff, maxc, keys, pts, rank0)) return rc;
   const int stride = n + m;
   if (want_kd && evr_cells_kd_limits(stride, m, maxc, nullptr) == 0) {
-    if (int rc = evr_cells_kd_order_device(stream, S, m, stride, off_dev, goff_dev, maxc, keys, pts, rank0, okeys,
-                                           ork, ogb, osv))
+    if (int rc = evr_cells_kd_order_device(stream, S, m, stride, moff, mgoff, maxc, keys, pts, rank0, okeys, ork,
+                                           ogb, osv))
       return rc;
     info[1] = 1;
   }
+  EVR_HIP(hipMemcpyAsync(off_dev, hoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  EVR_HIP(hipMemcpyAsync(goff_dev, hgoff, sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  EVR_HIP(hipEventRecord(copied, s));
   return 0;
 }
 
