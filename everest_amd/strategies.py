@@ -472,7 +472,8 @@ class BotorchStrategy(PredictiveStrategy):
                 raise ValueError("Model not yet fitted.")
             Xt = torch.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=self.model.device)
             mean, var = self.model.posterior(Xt, observation_noise=True)
-            preds = self._predictions_frame(mean.T.cpu().numpy(), np.sqrt(var.T.cpu().numpy()), df.index)
+            mv = torch.stack((mean, var)).cpu().numpy()      # one device -> host copy for both
+            preds = self._predictions_frame(mv[0].T, np.sqrt(mv[1].T), df.index)
             return pd.DataFrame(np.hstack([np.asarray(X, dtype=np.float64), preds.to_numpy()]),
                                 columns=keys + list(preds.columns))
         df = self.domain.inputs.inverse_transform(df, self.input_preprocessing_specs)
