@@ -506,20 +506,31 @@ int evr_box_kd_pipeline(void* stream, int S, int n, int m, const double* obj, co
   thread_local int* stage = nullptr;
   thread_local int* stage_d = nullptr;
   thread_local size_t stage_n = 0;
+  thread_local int stage_dev = -1;
+  // the previous call's kernels and copies read the staging on their own stream: an event
+  // recorded after them is waited on before the staging is reused, reallocated or freed
+  thread_local hipEvent_t copied = nullptr;
+  if (copied) EVR_HIP(hipEventSynchronize(copied));
+  int dev = 0;
+  EVR_HIP(hipGetDevice(&dev));
   const size_t need = (size_t)4 * S + 2;
-  if (stage_n < need) {
+  if (stage_n < need || stage_dev != dev) {
+    // the staging, its device pointer and the event belong to the device current when they
+    // were made (one worker thread serves every device)
+    if (copied) {
+      (void)hipEventDestroy(copied);
+      copied = nullptr;
+    }
     if (stage) (void)hipHostFree(stage);
     stage = stage_d = nullptr;
     stage_n = 0;
+    stage_dev = -1;
     EVR_HIP(hipHostMalloc((void**)&stage, sizeof(int) * need, hipHostMallocMapped | hipHostMallocCoherent));
     EVR_HIP(hipHostGetDevicePointer((void**)&stage_d, stage, 0));
     stage_n = need;
+    stage_dev = dev;
   }
-  // the previous call's kernels and copies read the staging on their own stream: an event
-  // recorded after them is waited on before the staging is reused
-  thread_local hipEvent_t copied = nullptr;
   if (!copied) EVR_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
-  else EVR_HIP(hipEventSynchronize(copied));
   int* hc = stage;
   int* hs = stage + S;
   int* hoff = stage + 2 * S;

@@ -2549,6 +2549,9 @@ static bool hvi_kdw_applies(const evr_qnehvi_state* st, int b) {
   if (restart_variant() != 3 || !st || st->log_hvi || !st->grp_off || b < 1 || b > 32 || kd_variant() != 2 ||
       st->m < 1 || st->m > 8 || st->max_groups > KW_MAXG)
     return false;
+  // the threshold probe reads 64 bucket ends, then the 64 entries of the straddling bucket:
+  // exact for strides up to 64 x 64 rows only
+  if (st->pts_stride > 64 * 64) return false;
   return kw_lds_bytes(st->pts_stride, st->m) <= 64 * 1024;
 }
 

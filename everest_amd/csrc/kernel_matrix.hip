@@ -9,6 +9,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "gemm_core.hpp"
 #include "../../include/everest_amd.h"
 
 namespace evr {
@@ -860,11 +861,133 @@ __global__ __launch_bounds__(1024) void posterior_finalize_kernel(int B, int n, 
   }
 }
 
-int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA, const double* B,
-            int ldb, long long sB, double* C, int ldc, long long sC, int batch);
-int rb_gemv_rows(hipStream_t s, int N, int K, const double* X, long long sX, const double* a, long long sa,
-                 double* y, long long sy, int batch);
-int gemm_backend_init();
+// ---------------------------------------------------------------------------------------
+// Posterior projection (gemm_core.hpp engine): per output j, V = L^-1 K_* (n x nt) is never
+// stored — each 32-row tile writes the partial sums of squares of its rows per test point,
+// and the tiles of the last row block (the only ones whose k range is the whole of [0, n))
+// also form the mean row alpha^T K_* from the staged K_* tiles.  L^-1 is lower triangular:
+// row tile [m0, m0 + 32) contracts over k < m0 + 32 only (half the flops of the dense
+// product; the skipped entries are exact zeros).  Longer row tiles are dispatched first.
+// ---------------------------------------------------------------------------------------
+using PostCfg = DgCfg<32, 32, 16, false>;
+constexpr int POST_NT = PostCfg::BM;
+
+// alpha^T B over the staged k-steps: the step's 16 alpha entries ride in the B image's first
+// padding column (thread t < 16 loads alpha[k0 + t] with the operand fetch and stages it);
+// thread (column c = tid % BN, row group g = tid / BN) accumulates rows g, g + 8 of every step
+struct PostMeanHook {
+  static constexpr int NG = 256 / PostCfg::BN, RPG = PostCfg::BK / NG;
+  const double* alpha;   // nullptr: not the last row block
+  int n;
+  double av;
+  double acc;
+  __device__ __forceinline__ void prefetch(int k0) {
+    if (!alpha) return;
+    const int k = k0 + (int)threadIdx.x;
+    if (threadIdx.x < PostCfg::BK) av = k < n ? alpha[k] : 0.0;
+  }
+  __device__ __forceinline__ void stage(double* Bs) {
+    if (alpha && threadIdx.x < PostCfg::BK) Bs[threadIdx.x * PostCfg::BST + PostCfg::BN] = av;
+  }
+  __device__ __forceinline__ void step(const double* Bs, int, int) {
+    if (!alpha) return;
+    const int g = threadIdx.x / PostCfg::BN, c = threadIdx.x % PostCfg::BN;
+#pragma unroll
+    for (int t = 0; t < RPG; ++t) {
+      const int r = g + NG * t;
+      acc = fma(Bs[r * PostCfg::BST + PostCfg::BN], Bs[r * PostCfg::BST + c], acc);
+    }
+  }
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const double* __restrict__ Mm,
+                                                           const double* __restrict__ Kx, double* __restrict__ Pn,
+                                                           double* __restrict__ mrow) {
+  using C = PostCfg;
+  __shared__ double lds[C::LDS_DOUBLES];
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  // dispatch order = descending k range (the longest row blocks start first), then output,
+  // then column tile; consecutive workgroups go round-robin over the XCDs, so every XCD gets
+  // the same mix of long and short tiles (an XCD-contiguous tile order would hand whole
+  // ranges of long tiles to some XCDs and short ones to others)
+  const int f = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int bx = f % gx, j = (f / gx) % gz, by = gy - 1 - f / (gx * gz);
+  const int m0 = by * C::BM, n0 = bx * C::BN;
+  const double* A = Mm + (size_t)j * (n + 1) * n;
+  const double* B = Kx + (size_t)j * n * nt;
+  const int kend = min(n, m0 + C::BM);
+  PostMeanHook hook{by == gy - 1 ? A + (size_t)n * n : nullptr, n, 0.0, 0.0};
+  dg_double4 acc[C::FM][C::FN];
+  dg_mainloop<C>(
+      lds, 0, kend,
+      [&](int r, int k) -> dg_double2 {
+        const bool ok = m0 + r < n;
+        return dg_pair<VEC>(A + (size_t)(m0 + r) * n + k, ok && k < kend, ok && k + 1 < kend);
+      },
+      [&](int k, int c) -> dg_double2 {
+        const bool ok = k < kend;
+        return dg_pair<VEC>(B + (size_t)k * nt + n0 + c, ok && n0 + c < nt, ok && n0 + c + 1 < nt);
+      },
+      acc, hook);
+  // the mainloop ended on a barrier: its LDS is free.  Column sums of squares over the
+  // tile's rows (fixed order: the 16 rows of a wave by xor-shuffles, then the two waves)
+  constexpr int BN = C::BN, NG = PostMeanHook::NG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, i = lane & 15, q = lane >> 4;
+  double* red = lds;              // [2][BN]
+  double* redm = lds + 2 * BN;    // [NG][BN]
+#pragma unroll
+  for (int bb = 0; bb < C::FN; ++bb) {
+    double sq = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double val = acc[0][bb][r];
+      if (m0 + wr * C::WM + q + 4 * r < n) sq = fma(val, val, sq);
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    if (q == 0) red[wr * BN + wc * C::WN + bb * 16 + i] = sq;
+  }
+  if (hook.alpha) redm[tid] = hook.acc;
+  __syncthreads();
+  if (tid < BN && n0 + tid < nt) {
+    Pn[((size_t)j * gy + by) * nt + n0 + tid] = red[tid] + red[BN + tid];
+    if (hook.alpha) {
+      double a = 0.0;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) a += redm[g * BN + tid];
+      mrow[(size_t)j * nt + n0 + tid] = a;
+    }
+  }
+}
+
+// mean / variance from the row-tile partials (fixed order) and the mean row
+__global__ __launch_bounds__(256) void post_finalize_kernel(int B, int n, int nt, int nrt, const double* __restrict__ Pn,
+                                                            const double* __restrict__ mrow,
+                                                            const double* __restrict__ cc,
+                                                            const double* __restrict__ ym,
+                                                            const double* __restrict__ ys,
+                                                            const double* __restrict__ kxx,
+                                                            const double* __restrict__ noise,
+                                                            double* __restrict__ mean, double* __restrict__ var) {
+  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= nt) return;
+  const double* P = Pn + (size_t)b * nrt * nt + c;
+  double s0 = 0.0, s1 = 0.0;
+  int rt = 0;
+  for (; rt + 1 < nrt; rt += 2) {
+    s0 += P[(size_t)rt * nt];
+    s1 += P[(size_t)(rt + 1) * nt];
+  }
+  if (rt < nrt) s0 += P[(size_t)rt * nt];
+  const double ss = s0 + s1;
+  const double s = ys[b];
+  mean[(size_t)b * nt + c] = ym[b] + s * (cc[b] + mrow[(size_t)b * nt + c]);
+  double v = kxx[b] - ss;
+  if (noise) v += noise[b];
+  var[(size_t)b * nt + c] = s * s * v;
+}
 
 }  // namespace evr
 
@@ -1074,7 +1197,8 @@ int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* 
 }
 
 long long evr_gp_posterior_workspace_doubles(int B, int n, int nt) {
-  return (B > 0 && n > 0 && nt > 0) ? (long long)B * nt * (2LL * n + 1) : 0;
+  // K_* (B x n x nt), the row-tile partials (B x ceil(n / 32) x nt) and the mean row (B x nt)
+  return (B > 0 && n > 0 && nt > 0) ? (long long)B * nt * ((long long)n + cdiv(n, POST_NT) + 1) : 0;
 }
 
 int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const double* Xn, const double* X,
@@ -1084,16 +1208,23 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
   EVR_CHECK(B >= 1 && n >= 1 && nt >= 0 && d >= 1 && Xn && M && work, "evr_gp_posterior: bad arguments");
   if (nt == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const int nrt = cdiv(n, POST_NT);
   double* Kx = work;                                   // B x n x nt
-  double* R = work + (size_t)B * n * nt;               // B x (n+1) x nt
+  double* Pn = Kx + (size_t)B * n * nt;                // B x nrt x nt
+  double* mrow = Pn + (size_t)B * nrt * nt;            // B x nt
   if (int rc = evr_kernel_matrix(stream, kind, B, n, nt, d, Xn, nullptr, nullptr, X, shift, scale, lengthscales,
                                  nullptr, nullptr, Kx))
     return rc;
-  if (int rc = gemm_backend_init()) return rc;
-  if (int rc = rb_gemm(s, false, n + 1, nt, n, M, n, (long long)(n + 1) * n, Kx, nt, (long long)n * nt, R, nt,
-                       (long long)(n + 1) * nt, B))
-    return rc;
-  return evr_gp_posterior_finalize(stream, B, n, nt, R, c, ym, ys, kxx, noise_add, mean, var);
+  const dim3 grid(cdiv(nt, PostCfg::BN), nrt, B);
+  if (n % 2 == 0 && nt % 2 == 0 && (uintptr_t)M % 16 == 0 && (uintptr_t)Kx % 16 == 0)
+    post_proj_kernel<true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+  else
+    post_proj_kernel<false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+  EVR_LAUNCH_CHECK();
+  post_finalize_kernel<<<dim3(cdiv(nt, 256), B), 256, 0, s>>>(B, n, nt, nrt, Pn, mrow, c, ym, ys, kxx, noise_add,
+                                                              mean, var);
+  EVR_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // extern "C"

@@ -1309,6 +1309,12 @@ __global__ void place_diag_blocks_kernel(int n, const double* __restrict__ Dinv,
   X[b * sX + (size_t)i * ldx + j] = v;
 }
 
+// the gemm_core.hpp engine (gemm.hip)
+size_t dg_gemm_ws_doubles(bool tA, int M, int N, int K, int batch);
+int dg_gemm(hipStream_t s, bool tA, int M, int N, int K, double alpha, const double* A, int lda, long long sA,
+            const double* B, int ldb, long long sB, double beta, double* Cm, int ldc, long long sC, int batch,
+            double* W);
+
 }  // namespace evr
 
 namespace {
@@ -1343,10 +1349,36 @@ static int stream_scratch(int slot, hipStream_t s, size_t bytes, void** out) {
 static int ladder_scratch(hipStream_t s, size_t bytes, void** out) { return stream_scratch(0, s, bytes, out); }
 static int gemm_scratch(hipStream_t s, size_t bytes, void** out) { return stream_scratch(1, s, bytes, out); }
 
+// split-K partials: the stream's reusable scratch (stream order protects it), or a
+// stream-ordered allocation while the stream is being captured into a graph (*pooled false:
+// the caller frees it after the reduction)
+static int splitk_scratch(hipStream_t s, size_t bytes, double** W, bool* pooled) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  EVR_HIP(hipStreamIsCapturing(s, &cap));
+  if (cap == hipStreamCaptureStatusNone) {
+    *pooled = true;
+    return gemm_scratch(s, bytes, (void**)W);
+  }
+  *pooled = false;
+  EVR_HIP(hipMallocAsync((void**)W, bytes, s));
+  return 0;
+}
+
 int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alpha, const double* A, int lda,
                 long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
                 int batch, int lower_only = 0, const int* skip = nullptr, bool allow_split = false) {
   if (M == 0 || N == 0) return 0;
+  if (!tB && !lower_only && !skip) {
+    // the gemm_core.hpp engine (gemm.hip): every non-triangular product with B untransposed
+    double* W = nullptr;
+    bool pooled = true;
+    const size_t wn = allow_split ? dg_gemm_ws_doubles(tA, M, N, K, batch) : 0;
+    if (wn)
+      if (int rc = splitk_scratch(s, sizeof(double) * wn, &W, &pooled)) return rc;
+    if (int rc = dg_gemm(s, tA, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, W)) return rc;
+    if (!pooled) EVR_HIP(hipFreeAsync(W, s));
+    return 0;
+  }
   const int tiles = cdiv(N, GT) * cdiv(M, GT) * batch;
   // Split K when the tile grid cannot fill the 256 CUs and each slice keeps >= 8 k-steps
   // (only for non-aliased outputs: the Cholesky panel update runs in place).
@@ -1359,19 +1391,8 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
   if (ksplit > 1) ksplit = cdiv(K, kchunk);
   double* W = nullptr;
   bool pooled = false;
-  if (ksplit > 1) {
-    // split-K partials: the stream's reusable scratch (stream order protects it), or a
-    // stream-ordered allocation while the stream is being captured into a graph
-    const size_t wbytes = sizeof(double) * (size_t)ksplit * batch * M * N;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    EVR_HIP(hipStreamIsCapturing(s, &cap));
-    if (cap == hipStreamCaptureStatusNone) {
-      if (int rc = gemm_scratch(s, wbytes, (void**)&W)) return rc;
-      pooled = true;
-    } else {
-      EVR_HIP(hipMallocAsync((void**)&W, wbytes, s));
-    }
-  }
+  if (ksplit > 1)
+    if (int rc = splitk_scratch(s, sizeof(double) * (size_t)ksplit * batch * M * N, &W, &pooled)) return rc;
   dim3 grid(cdiv(N, GT), cdiv(M, GT), batch * ksplit);
 #define G_(TA_, TB_)                                                                                       \
   gemm_f64_kernel<TA_, TB_><<<grid, 256, 0, s>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, \

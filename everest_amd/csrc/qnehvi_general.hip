@@ -39,9 +39,10 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
                        const double* scale1, const double* X2, const double* shift2, const double* scale2,
                        const double* lengthscales, const double* outputscale, const double* G, double* dX2,
                        double* work);
-int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA, const double* B,
-            int ldb, long long sB, double* C, int ldc, long long sC, int batch);
-int gemm_backend_init();
+int dg_gemm(hipStream_t s, bool tA, int M, int N, int K, double alpha, const double* A, int lda, long long sA,
+            const double* B, int ldb, long long sB, double beta, double* Cm, int ldc, long long sC, int batch,
+            double* W);
+size_t dg_gemm_ws_doubles(bool tA, int M, int N, int K, int batch);
 long long hvi_raw_workspace(const evr_qnehvi_state* st, int b, bool backward);
 int hvi_raw(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, bool backward, double* work,
             double* dG, int* nsplit);
@@ -596,7 +597,7 @@ static int qg_params(const evr_qn_general* g, int m_model, QgObj* o) {
 }
 
 struct QgLayout {
-  size_t Kx, R, P, Wf, Y, Lq, flags, Gv, Wv, hvi, dGv, dY, cf, dKqq, cm, gR, dKx, kg, total;
+  size_t Kx, R, P, Wf, Y, Lq, flags, Gv, Wv, hvi, dGv, dY, cf, dKqq, cm, gR, dKx, Wb, kg, total;
 };
 
 static QgLayout qg_layout(const evr_qnehvi_state* stm, const evr_qnehvi_state* sth, int q, int d, int b,
@@ -628,6 +629,7 @@ static QgLayout qg_layout(const evr_qnehvi_state* stm, const evr_qnehvi_state* s
     L.cm = take(m * bq);
     L.gR = take(m * Rr * bq);
     L.dKx = take(m * n * bq);
+    L.Wb = take(dg_gemm_ws_doubles(true, (int)n, (int)bq, (int)Rr, (int)m));   // split-K partials of M^T gR
     L.kg = take(kcross_grad_ws_doubles((int)n, (int)bq, d));
   }
   L.total = o;
@@ -1001,7 +1003,7 @@ static QlPlan ql_plan(const evr_qnehvi_state* sth, int b) {
   }
 
 struct QlLayout {
-  size_t Kx, R, P, Wf, Y, Lq, flags, LW, dY, cf, dKqq, cm, gR, dKx, kg, total;
+  size_t Kx, R, P, Wf, Y, Lq, flags, LW, dY, cf, dKqq, cm, gR, dKx, Wb, kg, total;
   QlPlan plan;
   int MM;
 };
@@ -1035,6 +1037,7 @@ static QlLayout ql_layout(const evr_qnehvi_state* stm, const evr_qnehvi_state* s
     L.cm = take(m * bq);
     L.gR = take(m * Rr * bq);
     L.dKx = take(m * n * bq);
+    L.Wb = take(dg_gemm_ws_doubles(true, (int)n, (int)bq, (int)Rr, (int)m));   // split-K partials of M^T gR
     L.kg = take(kcross_grad_ws_doubles((int)n, (int)bq, d));
   }
   L.total = o;
@@ -1061,7 +1064,6 @@ int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_sta
   if (b == 0) return 0;
   QgObj o;
   if (int rc = qg_params(g, stm->m, &o)) return rc;
-  if (int rc = gemm_backend_init()) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int q = g->q, m = stm->m, n = stm->n, d = md->d, S = stm->S, nsub = (1 << q) - 1;
   const int bq = b * q, bv = b * nsub;
@@ -1112,8 +1114,8 @@ int evr_qng_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_sta
   EVR_LAUNCH_CHECK()
   QG_SWITCH(q, GO);
 #undef GO
-  if (int rc = rb_gemm(s, true, n, bq, Rr, md->M, n, (long long)Rr * n, gR, bq, (long long)Rr * bq, dKx, bq,
-                       (long long)n * bq, m))
+  if (int rc = dg_gemm(s, true, n, bq, Rr, 1.0, md->M, n, (long long)Rr * n, gR, bq, (long long)Rr * bq, 0.0, dKx, bq,
+                       (long long)n * bq, m, w + L.Wb))
     return rc;
   if (int rc = kcross_grad_launch(s, md->kind, m, n, bq, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                   md->lengthscales, nullptr, dKx, dX, w + L.kg))
@@ -1173,7 +1175,6 @@ int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_st
   if (b == 0) return 0;
   QgObj o;
   if (int rc = qg_params(g, stm->m, &o)) return rc;
-  if (int rc = gemm_backend_init()) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int q = g->q, m = stm->m, n = stm->n, d = md->d, S = stm->S;
   const int bq = b * q;
@@ -1240,8 +1241,8 @@ int evr_qlog_eval(void* stream, const evr_qnehvi_state* stm, const evr_qnehvi_st
   EVR_LAUNCH_CHECK()
   QG_SWITCH(q, GO);
 #undef GO
-  if (int rc = rb_gemm(s, true, n, bq, Rr, md->M, n, (long long)Rr * n, gR, bq, (long long)Rr * bq, dKx, bq,
-                       (long long)n * bq, m))
+  if (int rc = dg_gemm(s, true, n, bq, Rr, 1.0, md->M, n, (long long)Rr * n, gR, bq, (long long)Rr * bq, 0.0, dKx, bq,
+                       (long long)n * bq, m, w + L.Wb))
     return rc;
   if (int rc = kcross_grad_launch(s, md->kind, m, n, bq, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                   md->lengthscales, nullptr, dKx, dX, w + L.kg))

@@ -45,6 +45,7 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags);
 constexpr int QS_TILE_ROWS = 16;
+constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
 int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
                   int nrt_used, double* L22, int* flags, double* sval, double* dG);
@@ -56,7 +57,6 @@ static bool small_path(const evr_qnehvi_state* st, int b, int d) {
   return !(e && std::string(e) == "0") && qs_applies(st, b, d);
 }
 size_t kcross_grad_ws_doubles(int n1, int n2, int d);
-int gemm_backend_init();
 int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                        const double* scale1, const double* X2, const double* shift2, const double* scale2,
                        const double* lengthscales, const double* outputscale, const double* G, double* dX2,
@@ -190,7 +190,7 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
                        hw, flags);
   }
-  if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : 64)) return rc;
+  if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : QN_NORM_TILE)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
   if (small && p->L.fused_scan) {
     // one launch for thresholds + scan + split reduction (hvi_kd3); the per-sample values in
@@ -270,10 +270,6 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   p->seq = 0;
   p->nwords = 1;
   p->counter = nullptr;
-  if (int rc = gemm_backend_init()) {
-    delete p;
-    return rc;
-  }
   // the device-mode graph is captured on the second run (a plan evaluated once — the raw
   // screening chunks — or only host-driven — the restarts, which use the host graph — never
   // pays for a capture and an instantiation)

@@ -1,10 +1,13 @@
-// qNEHVI projection GEMMs with fused prologue / epilogue (gfx950 f64 MFMA).
+// qNEHVI projection GEMMs with fused prologue / epilogue (gfx950 f64 MFMA, the
+// gemm_core.hpp tile engine), the candidate-batch path (b > 32: raw screening, evaluation
+// passes, joint batches; b <= 32 is qnehvi_small.hip).
 //
-// Forward:  R_j = M_j K_x  (M_j = [L^-1; G; H^T; alpha^T], Rr x n; K_x: n x b), as in
-// acquisition.py.  The epilogue also emits, per 64-row tile and candidate, the partial sums
-// of squares of the L^-1 k rows (rows < n) and of the L21 rows (n <= row < n + nb), so the
-// sampling step reads (rows-tiles x 2) partials and the S + 1 sample / mean rows instead of
-// the whole 21 MB R (the old samples kernel re-read all of R with 40 workgroups).
+// Forward:  R_j = M_j K_x  (M_j = [C_j; H_j^T; alpha_j^T] or [L^-1; G; H^T; alpha^T], Rr x n;
+// K_x: n x b), as in acquisition.py.  All Rr rows, the mean row included, in one launch of
+// 32 x 64 tiles.  The epilogue also emits, per 32-row tile and candidate, the partial sums of
+// squares of the L^-1 k rows (rows < n) and of the L21 rows (n <= row < n + nb), so the
+// sampling step reads (row tiles x 2) partials and the S + 1 sample / mean rows instead of
+// the whole R.
 //
 // Backward: dK_x,j = M_j^T gR_j with gR_j never materialised.  gR_j is, per candidate c,
 //   rows < n:            2 R[i][c] dssv(c)      (var = s^2 (kxx - |L^-1 k|^2))
@@ -12,191 +15,133 @@
 //   sample rows s:       a_j dG[s][j][c]
 //   mean row:            s_j dmu(c),  dmu = sum_s a_j dG, dl = sum_s a_j dG zq[s][j],
 //                        dbr = dl / (2 L22), dssv = -s^2 dbr, dssw = -dbr.
-// A small kernel reduces dmu, dl over the samples into per-candidate coefficients; the GEMM
-// fetch then generates gR from R, dG and those coefficients — one pass over R and dG, no
-// 21 MB gR write + re-read (the unfused qn_samples_bwd_kernel + gemm^T).  Both GEMMs split K
-// (fixed-order reduction) when their tile grid cannot fill the 256 CUs (small candidate
-// batches: the L-BFGS restarts).
-//
-// Tile: 64 x 64 outputs per 256-thread workgroup, 4 waves x (2 x 2) v_mfma_f64_16x16x4f64,
-// K step 16 staged through LDS, global loads of step t+1 issued before the MFMAs of step t.
+// A small kernel reduces dmu, dl over the samples into per-candidate coefficients; the GEMM's
+// B fetch then generates gR from R, dG and those coefficients — one pass over R and dG.
+// Both GEMMs split K (fixed-order reduction) when their tile grid cannot fill the chip.
 #include <algorithm>
 #include <cstdlib>
 
-#include <rocblas/rocblas.h>
-
 #include "common.hpp"
+#include "gemm_core.hpp"
 #include "../../include/everest_amd.h"
 
-using double4_t = __attribute__((ext_vector_type(4))) double;
-
-#ifndef EVR_PK
-#define EVR_PK 16
-#endif
 namespace evr {
 
-constexpr int PT = 64, PK = EVR_PK, PPAD = 16;
-constexpr int PU = PT * PK / 256;   // staged elements of A and of B per thread and k-step
+using ProjF = DgCfg<32, 64, 16, false>;   // R = M K_x          (A = M: k-contiguous rows)
+using ProjB = DgCfg<32, 32, 16, true>;    // dK_x = M^T gR      (A = M^T: m-contiguous)
+constexpr int QN_NT = ProjF::BM;          // rows per partial-norm tile
 
-// 64 x 64 f64 MFMA tile over k in [kbeg, kend): fa(row, k) / fb(k, col) fetch one element
-// (tile-local row / col); the fetch of step t+1 is issued before the MFMAs of step t.
-// TA: A element (row, k) is contiguous along row (coalesce the A fetch along rows).
-template <bool TA, class FA, class FB>
-__device__ __forceinline__ void proj_tile(int kbeg, int kend, FA fa, FB fb, double4_t (&acc)[4]) {
-  __shared__ double As[PK][PT + PPAD];
-  __shared__ double Bs[PK][PT + PPAD];
+int dg_ksplit(long long tiles, int K, int bk, int* kchunk);
+
+// partial sums of squares of a BM x BN tile of R by row class (cls 0: rows < n, 1: rows in
+// [n, n + nb)), reduced over the tile's rows in a fixed order -> Pout[cls][c] (b columns)
+template <class C>
+__device__ __forceinline__ void proj_tile_norms(const dg_double4 (&acc)[C::FM][C::FN], double* lds, int m0, int n0,
+                                                int n, int nb, int b, double* __restrict__ Pout) {
+  static_assert(C::FM == 1, "one 16-row block per wave");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  int am[PU], ak[PU], bn[PU], bk[PU];
+  const int wr = wave >> 1, wc = wave & 1, i = lane & 15, q = lane >> 4;
+  double sq[C::FN][2];
 #pragma unroll
-  for (int u = 0; u < PU; ++u) {
-    const int e = u * 256 + tid;
-    if (TA) { am[u] = e % PT; ak[u] = e / PT; } else { ak[u] = e % PK; am[u] = e / PK; }
-    bn[u] = e % PT;
-    bk[u] = e / PT;
-  }
-  double ra[PU], rb[PU];
-  auto fetch = [&](int k0) {
+  for (int bb = 0; bb < C::FN; ++bb) {
+    sq[bb][0] = sq[bb][1] = 0.0;
 #pragma unroll
-    for (int u = 0; u < PU; ++u) {
-      const int k = k0 + ak[u], kb = k0 + bk[u];
-      ra[u] = (k < kend) ? fa(am[u], k) : 0.0;
-      rb[u] = (kb < kend) ? fb(kb, bn[u]) : 0.0;
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * C::WM + q + 4 * r;
+      const double v = acc[0][bb][r];
+      if (row < n) sq[bb][0] = fma(v, v, sq[bb][0]);
+      else if (row < n + nb) sq[bb][1] = fma(v, v, sq[bb][1]);
     }
-  };
-  if (kbeg < kend) fetch(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += PK) {
-#pragma unroll
-    for (int u = 0; u < PU; ++u) {
-      As[ak[u]][am[u]] = ra[u];
-      Bs[bk[u]][bn[u]] = rb[u];
-    }
-    __syncthreads();
-    if (k0 + PK < kend) fetch(k0 + PK);
-    const int i = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int kk = 0; kk < PK; kk += 4) {
-      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
-      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
-      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-}
-
-// visit the tile's outputs: f(local_row, local_col, value) — D map of v_mfma_f64_16x16x4:
-// register r of lane l holds D[(l >> 4) + 4 r][l & 15]
-template <class F>
-__device__ __forceinline__ void proj_for_each(const double4_t (&acc)[4], F f) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const int col = lane & 15, rq = lane >> 4;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) f(wm + (q >> 1) * 16 + rq + 4 * r, wn + (q & 1) * 16 + col, acc[q][r]);
-}
-
-// partial sums of squares of a 64 x 64 tile of R, by row class (cls 0: rows < n, 1: rows in
-// [n, n + nb)), reduced over the tile's rows in a fixed order -> P[j][rt][cls][c]
-__device__ __forceinline__ void proj_norms(const double (&sq)[2][2], int n0, int b, double* __restrict__ Pout) {
-  __shared__ double red[4][32][2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = lane & 15, rq = lane >> 4;
-  double v4[2][2];
-#pragma unroll
-  for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
     for (int cls = 0; cls < 2; ++cls) {
-      double v = sq[ni][cls];
+      double v = sq[bb][cls];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      v4[ni][cls] = v;
+      sq[bb][cls] = v;
     }
-  if (rq == 0) {
+  }
+  // the mainloop ended on a barrier: its LDS is free
+  double (*red)[C::BN][2] = reinterpret_cast<double (*)[C::BN][2]>(lds);
+  if (q == 0) {
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      red[wave][ni * 16 + col][0] = v4[ni][0];
-      red[wave][ni * 16 + col][1] = v4[ni][1];
+    for (int bb = 0; bb < C::FN; ++bb) {
+      red[wr][wc * C::WN + bb * 16 + i][0] = sq[bb][0];
+      red[wr][wc * C::WN + bb * 16 + i][1] = sq[bb][1];
     }
   }
   __syncthreads();
-  if (tid < 128) {
-    const int cls = tid >> 6, t = tid & 63;
-    const int h = t >> 5, cw = t & 31;   // waves h (rows 0-31) and h + 2 (rows 32-63) share columns
-    const double v = red[h][cw][cls] + red[h + 2][cw][cls];
-    if (n0 + t < b) Pout[(size_t)cls * b + n0 + t] = v;
+  if (tid < 2 * C::BN) {
+    const int cls = tid / C::BN, c = tid - cls * C::BN;
+    const double v = red[0][c][cls] + red[1][c][cls];
+    if (n0 + c < b) Pout[(size_t)cls * b + n0 + c] = v;
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // forward: R_j = M_j K_x,j (+ partial norms), optional split-K into W
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void qn_proj_fwd(int n, int nb, int Rr, int b, int m, const double* __restrict__ Mm,
-                                                   const double* __restrict__ Kx, double* __restrict__ R,
-                                                   double* __restrict__ P, int nrt, int ksplit, int kchunk,
-                                                   double* __restrict__ W) {
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void qn_proj_fwd(int n, int nb, int Rr, int b, int m, const double* __restrict__ Mm,
+                                                      const double* __restrict__ Kx, double* __restrict__ R,
+                                                      double* __restrict__ P, int nrt, int ksplit, int kchunk,
+                                                      double* __restrict__ W) {
+  using C = ProjF;
+  __shared__ double lds[C::LDS_DOUBLES];
   const int gx = gridDim.x, gy = gridDim.y;
   const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   const int bx = t % gx, by = (t / gx) % gy, bz = t / (gx * gy);
   const int j = bz / ksplit, kz = bz - j * ksplit;
-  const int m0 = by * PT, n0 = bx * PT;
+  const int m0 = by * C::BM, n0 = bx * C::BN;
   const double* A = Mm + (size_t)j * Rr * n;
   const double* B = Kx + (size_t)j * n * b;
-  double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
   const int kbeg = kz * kchunk, kend = min(n, kbeg + kchunk);
-  proj_tile<false>(
-      kbeg, kend, [&](int r, int k) { return (m0 + r < Rr) ? A[(size_t)(m0 + r) * n + k] : 0.0; },
-      [&](int k, int c) { return (n0 + c < b) ? B[(size_t)k * b + n0 + c] : 0.0; }, acc);
+  dg_double4 acc[C::FM][C::FN];
+  dg_mainloop<C>(
+      lds, kbeg, kend,
+      [&](int r, int k) -> dg_double2 {
+        const bool ok = m0 + r < Rr;
+        return dg_pair<VEC>(A + (size_t)(m0 + r) * n + k, ok && k < kend, ok && k + 1 < kend);
+      },
+      [&](int k, int c) -> dg_double2 {
+        const bool ok = k < kend;
+        return dg_pair<VEC>(B + (size_t)k * b + n0 + c, ok && n0 + c < b, ok && n0 + c + 1 < b);
+      },
+      acc);
   if (ksplit > 1) {
     double* Wz = W + ((size_t)kz * m + j) * Rr * b;
-    proj_for_each(acc, [&](int r, int c, double v) {
-      if (m0 + r < Rr && n0 + c < b) Wz[(size_t)(m0 + r) * b + n0 + c] = v;
+    dg_for_each<C>(acc, [&](int r, int c, double val) {
+      if (m0 + r < Rr && n0 + c < b) Wz[(size_t)(m0 + r) * b + n0 + c] = val;
     });
     return;
   }
   double* Rj = R + (size_t)j * Rr * b;
-  double sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-  proj_for_each(acc, [&](int r, int c, double v) {
-    const int row = m0 + r;
-    if (row < Rr && n0 + c < b) Rj[(size_t)row * b + n0 + c] = v;
-    const int ni = (c & 31) >> 4;
-    if (row < n) sq[ni][0] += v * v;
-    else if (row < n + nb) sq[ni][1] += v * v;
+  dg_for_each<C>(acc, [&](int r, int c, double val) {
+    if (m0 + r < Rr && n0 + c < b) Rj[(size_t)(m0 + r) * b + n0 + c] = val;
   });
-  proj_norms(sq, n0, b, P + ((size_t)j * nrt + by) * 2 * b);
+  proj_tile_norms<C>(acc, lds, m0, n0, n, nb, b, P + ((size_t)j * nrt + by) * 2 * b);
 }
 
-// split-K reduction of the forward: R = sum_kz W[kz] (fixed order) + the partial norms
+// split-K reduction of the forward: R = sum_kz W[kz] (fixed order), then the partial norms of
+// each 32-row tile (thread per candidate column, rows in order)
 __global__ __launch_bounds__(256) void qn_proj_fwd_reduce(int n, int nb, int Rr, int b, int m, int ksplit,
                                                           const double* __restrict__ W, double* __restrict__ R,
                                                           double* __restrict__ P, int nrt) {
-  const int j = blockIdx.z;
-  const int m0 = blockIdx.y * PT, n0 = blockIdx.x * PT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // reuse the MFMA D layout so proj_norms' reduction order applies unchanged
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const int col = lane & 15, rq = lane >> 4;
-  double sq[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  const int j = blockIdx.z, rt = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= b) return;
+  double s0 = 0.0, s1 = 0.0;
   double* Rj = R + (size_t)j * Rr * b;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm + (q >> 1) * 16 + rq + 4 * r, c = n0 + wn + (q & 1) * 16 + col;
-      double v = 0.0;
-      if (row < Rr && c < b) {
-#pragma unroll 4
-        for (int kz = 0; kz < ksplit; ++kz) v += W[(((size_t)kz * m + j) * Rr + row) * b + c];
-        Rj[(size_t)row * b + c] = v;
-      }
-      if (row < n) sq[q & 1][0] += v * v;
-      else if (row < n + nb) sq[q & 1][1] += v * v;
-    }
-  proj_norms(sq, n0, b, P + ((size_t)j * nrt + blockIdx.y) * 2 * b);
+  for (int rr = 0; rr < QN_NT; ++rr) {
+    const int row = rt * QN_NT + rr;
+    if (row >= Rr) break;
+    double v = 0.0;
+    for (int kz = 0; kz < ksplit; ++kz) v += W[(((size_t)kz * m + j) * Rr + row) * b + c];
+    Rj[(size_t)row * b + c] = v;
+    if (row < n) s0 = fma(v, v, s0);
+    else if (row < n + nb) s1 = fma(v, v, s1);
+  }
+  P[(((size_t)j * nrt + rt) * 2 + 0) * b + c] = s0;
+  P[(((size_t)j * nrt + rt) * 2 + 1) * b + c] = s1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -302,45 +247,79 @@ __global__ __launch_bounds__(BC_C * BC_G) void qn_bwd_coef(int S, int m, int b, 
 }
 
 // ---------------------------------------------------------------------------------------
-// backward: dKx_j = M_j^T gR_j with gR generated in the fetch, optional split-K into W
+// backward: dKx_j = M_j^T gR_j, gR never formed.  Its row classes scale whole columns
+// (rows < n by 2 dssv(c), rows [n, n + nb) by 2 dssw(c), sample rows by a_j, the mean row is
+// s_j dmu(c) itself), and a column scale commutes with the sum over rows: each class's rows
+// are one plain GEMM segment over R / dG (the tile engine's main loop, no per-element work
+// in the fetch), scaled in the epilogue, where the mean row's rank-1 term is added.
+// Optional split-K into W (the classes intersected with the slice's k range).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void qn_proj_bwd(int n, int nb, int S, int nh, int m, int b,
-                                                   const double* __restrict__ Mm, const double* __restrict__ R,
-                                                   const double* __restrict__ dG, const double* __restrict__ oa,
-                                                   const double* __restrict__ coef, double* __restrict__ dK,
-                                                   int ksplit, int kchunk, double* __restrict__ W) {
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void qn_proj_bwd(int n, int nb, int nh, int m, int b, const double* __restrict__ Mm,
+                                                      const double* __restrict__ R, const double* __restrict__ dG,
+                                                      const double* __restrict__ oa, const double* __restrict__ coef,
+                                                      double* __restrict__ dK, int ksplit, int kchunk,
+                                                      double* __restrict__ W) {
+  using C = ProjB;
+  __shared__ double lds[C::LDS_DOUBLES];
   const int gx = gridDim.x, gy = gridDim.y;
   const int t = xcd_swizzle(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   const int bx = t % gx, by = (t / gx) % gy, bz = t / (gx * gy);
   const int j = bz / ksplit, kz = bz - j * ksplit;
-  const int m0 = by * PT, n0 = bx * PT;
+  const int m0 = by * C::BM, n0 = bx * C::BN;
   const int Rr = n + nb + nh + 1;
   const double* A = Mm + (size_t)j * Rr * n;   // A(row, k) = M_j[k][row]
   const double* Rj = R + (size_t)j * Rr * b;
+  const double* dGj = dG + (size_t)j * b;
   const double* cj = coef + (size_t)j * 3 * b;
   const double aj = oa[j];
-  __shared__ double cf[3][PT];
-  if (threadIdx.x < 3 * PT) {
-    const int q = threadIdx.x / PT, c = threadIdx.x - q * PT;
-    cf[q][c] = (n0 + c < b) ? cj[(size_t)q * b + n0 + c] : 0.0;
-  }
-  __syncthreads();
-  double4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
   const int kbeg = kz * kchunk, kend = min(Rr, kbeg + kchunk);
-  proj_tile<true>(
-      kbeg, kend, [&](int r, int k) { return (m0 + r < n) ? A[(size_t)k * n + m0 + r] : 0.0; },
-      [&](int k, int c) {
-        if (n0 + c >= b) return 0.0;
-        if (k < n) return Rj[(size_t)k * b + n0 + c] * cf[0][c];
-        if (k < n + nb) return Rj[(size_t)k * b + n0 + c] * cf[1][c];
-        if (k < n + nb + nh) return aj * dG[((size_t)(k - n - nb) * m + j) * b + n0 + c];
-        return cf[2][c];
-      },
-      acc);
+  auto fa = [&](int k, int c) -> dg_double2 {
+    return dg_pair<VEC>(A + (size_t)k * n + m0 + c, m0 + c < n, m0 + c + 1 < n);
+  };
+  // class segments of this slice: [lo, hi) of rows < n, [n, n + nb), the sample rows
+  dg_double4 a0[C::FM][C::FN], a1[C::FM][C::FN], a2[C::FM][C::FN];
+  {
+    const int lo = kbeg, hi = min(kend, n);
+    dg_mainloop<C>(lds, lo, hi, fa, [&](int k, int c) -> dg_double2 {
+      return dg_pair<VEC>(Rj + (size_t)k * b + n0 + c, k < hi && n0 + c < b, k < hi && n0 + c + 1 < b);
+    }, a0);
+  }
+  {
+    const int lo = max(kbeg, n), hi = min(kend, n + nb);
+    dg_mainloop<C>(lds, lo, hi, fa, [&](int k, int c) -> dg_double2 {
+      return dg_pair<VEC>(Rj + (size_t)k * b + n0 + c, k < hi && n0 + c < b, k < hi && n0 + c + 1 < b);
+    }, a1);
+  }
+  {
+    const int lo = max(kbeg, n + nb), hi = min(kend, n + nb + nh);
+    dg_mainloop<C>(lds, lo, hi, fa, [&](int k, int c) -> dg_double2 {
+      return dg_pair<VEC>(dGj + (size_t)(k - n - nb) * m * b + n0 + c, k < hi && n0 + c < b, k < hi && n0 + c + 1 < b);
+    }, a2);
+  }
+  const bool mean_in = Rr - 1 >= kbeg && Rr - 1 < kend;
+  const double* Mmean = A + (size_t)(Rr - 1) * n;
   double* out = (ksplit > 1) ? W + ((size_t)kz * m + j) * n * b : dK + (size_t)j * n * b;
-  proj_for_each(acc, [&](int r, int c, double v) {
-    if (m0 + r < n && n0 + c < b) out[(size_t)(m0 + r) * b + n0 + c] = v;
-  });
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * C::WM, wn = (wave & 1) * C::WN, i = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int x = 0; x < C::FM; ++x)
+#pragma unroll
+    for (int y = 0; y < C::FN; ++y) {
+      const int col = n0 + wn + y * 16 + i;
+      const bool cok = col < b;
+      const double k0c = cok ? cj[col] : 0.0, k1c = cok ? cj[(size_t)b + col] : 0.0;
+      const double k2c = cok ? cj[(size_t)2 * b + col] : 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + x * 16 + q + 4 * r;
+        if (row < n && cok) {
+          double v = fma(k0c, a0[x][y][r], fma(k1c, a1[x][y][r], aj * a2[x][y][r]));
+          if (mean_in) v = fma(Mmean[row], k2c, v);
+          out[(size_t)row * b + col] = v;
+        }
+      }
+    }
 }
 
 __global__ __launch_bounds__(256) void qn_splitk_sum(long long per, int ksplit, const double* __restrict__ W,
@@ -353,150 +332,13 @@ __global__ __launch_bounds__(256) void qn_splitk_sum(long long per, int ksplit, 
   out[e] = v;
 }
 
-// split K when the tile grid cannot fill the chip (aim at >= 512 workgroups, i.e. two per
-// CU); each slice keeps >= 8 k-steps.  More slices than that only add partial-sum traffic.
-static int proj_ksplit(int tiles, int K, int* kchunk) {
-  int ks = 1;
-  if (tiles < 512) ks = std::max(1, std::min(std::min(cdiv(512, tiles), K / (8 * PK)), 32));
-  *kchunk = ks > 1 ? cdiv(cdiv(K, ks), PK) * PK : std::max(K, 1);
-  return ks > 1 ? cdiv(K, *kchunk) : 1;
-}
-
-// ---------------------------------------------------------------------------------------
-// Library-GEMM variant (rocBLAS dgemm for the plain contractions, hand-written fused
-// epilogue / prologue kernels around them).  rocBLAS' f64 MFMA kernels reach ~48 TF/s at
-// this shape vs ~26 TF/s for the 64x64 tile above; EVR_GEMM=mfma selects the fully fused
-// kernels instead.
-// ---------------------------------------------------------------------------------------
-// partial norms of R rows [0, n + nb) per 64-row tile: block = 64 candidates x 4 row groups
-__global__ __launch_bounds__(256) void qn_norms_rows(int n, int nb, int Rr, int b, int nrt,
-                                                     const double* __restrict__ R, double* __restrict__ P) {
-  const int j = blockIdx.z, rt = blockIdx.y;
-  const int cx = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
-  __shared__ double red[4][64][2];
-  double s0 = 0.0, s1 = 0.0;
-  if (c < b) {
-    const double* Rj = R + (size_t)j * Rr * b;
-#pragma unroll 4
-    for (int r = 0; r < 16; ++r) {
-      const int row = rt * 64 + rg * 16 + r;
-      if (row < n + nb) {
-        const double v = Rj[(size_t)row * b + c];
-        if (row < n) s0 = fma(v, v, s0);
-        else s1 = fma(v, v, s1);
-      }
-    }
-  }
-  red[rg][cx][0] = s0;
-  red[rg][cx][1] = s1;
-  __syncthreads();
-  if (rg < 2 && c < b) {
-    const double v = ((red[0][cx][rg] + red[1][cx][rg]) + red[2][cx][rg]) + red[3][cx][rg];
-    P[(((size_t)j * nrt + rt) * 2 + rg) * b + c] = v;
-  }
-}
-
-// gR_j (Rr x b) from R, dG and the per-candidate coefficients (see the header).  Grid =
-// (m * Rr rows, candidate tiles): no 64-bit division per element (the flat-index form spent
-// 8.5 us on 31 MB at m = 5, Rr = 769, b = 512 on MI355X)
-__global__ __launch_bounds__(256) void qn_gen_gr(int n, int nb, int nh, int m, int b, const double* __restrict__ R,
-                                                 const double* __restrict__ dG, const double* __restrict__ oa,
-                                                 const double* __restrict__ coef, double* __restrict__ gR) {
-  const int Rr = n + nb + nh + 1;
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= b) return;
-  const int rj = blockIdx.x;
-  const int j = rj / Rr, row = rj - j * Rr;
-  const size_t e = (size_t)rj * b + c;
-  const double* cj = coef + (size_t)j * 3 * b;
-  double v;
-  if (row < n) v = R[e] * cj[c];
-  else if (row < n + nb) v = R[e] * cj[(size_t)b + c];
-  else if (row < n + nb + nh) v = oa[j] * dG[((size_t)(row - n - nb) * m + j) * b + c];
-  else v = cj[(size_t)2 * b + c];
-  gR[e] = v;
-}
-
-static bool use_rocblas() {
-  static const bool v = [] {
-    const char* e = std::getenv("EVR_GEMM");
-    return !(e && std::string(e) == "mfma");
-  }();
-  return v;
-}
-
-static rocblas_handle rb_handle() {
-  thread_local rocblas_handle h = nullptr;
-  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
-  // bitwise-reproducible results: no atomics-based split-K in the Tensile kernels
-  if (h) (void)rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);
-  return h;
-}
-
-// row-major C = op(A) op(B) batched (alpha 1, beta 0) through rocBLAS' column-major dgemm
-int rb_gemm(hipStream_t s, bool tA, int M, int N, int K, const double* A, int lda, long long sA,
-                   const double* B, int ldb, long long sB, double* C, int ldc, long long sC, int batch) {
-  rocblas_handle h = rb_handle();
-  EVR_CHECK(h, "rocBLAS handle creation failed");
-  EVR_CHECK(rocblas_set_stream(h, s) == rocblas_status_success, "rocblas_set_stream failed");
-  const double one = 1.0, zero = 0.0;
-  const rocblas_status st = rocblas_dgemm_strided_batched(h, rocblas_operation_none,
-                                                           tA ? rocblas_operation_transpose : rocblas_operation_none,
-                                                           N, M, K, &one, B, ldb, sB, A, lda, sA, &zero, C, ldc, sC,
-                                                           batch);
-  EVR_CHECK(st == rocblas_status_success, "rocblas_dgemm_strided_batched failed (%d)", (int)st);
-  return 0;
-}
-
-// mean row of R (the operator's last row, alpha^T K_x): 16 candidates x 64 row groups per
-// block, so a b = 512, m = 5 pass spreads over 160 workgroups (64-candidate blocks used only
-// 40 CUs: 9.1 us for 10.5 MB on MI355X).  Each wave reads 4 rows x 128 B (one cache line per
-// row); fixed-order sums: 8 strided rows per thread, then 8 groups of 8, then 8 partials
-// (see proj_forward for why it is not a GEMM row)
-constexpr int MR_C = 16, MR_G = 64;
-__global__ __launch_bounds__(MR_C * MR_G) void qn_mean_row(int n, int Rr, int b, const double* __restrict__ Mm,
-                                                          const double* __restrict__ Kx, double* __restrict__ R) {
-  __shared__ double red[MR_G][MR_C];
-  const int j = blockIdx.y, cx = threadIdx.x % MR_C, rg = threadIdx.x / MR_C;
-  const int c = blockIdx.x * MR_C + cx;
-  const double* a = Mm + ((size_t)j * Rr + (Rr - 1)) * n;
-  const double* K = Kx + (size_t)j * n * b;
-  double acc = 0.0;
-  if (c < b) {
-#pragma unroll 8
-    for (int i = rg; i < n; i += MR_G) acc = fma(a[i], K[(size_t)i * b + c], acc);
-  }
-  red[rg][cx] = acc;
-  __syncthreads();
-  if (rg < 8) {
-    double v = red[rg * 8][cx];
-#pragma unroll
-    for (int g = 1; g < 8; ++g) v += red[rg * 8 + g][cx];
-    acc = v;
-  }
-  __syncthreads();
-  if (rg < 8) red[rg][cx] = acc;
-  __syncthreads();
-  if (rg == 0 && c < b) {
-    double v = red[0][cx];
-#pragma unroll
-    for (int g = 1; g < 8; ++g) v += red[g][cx];
-    R[((size_t)j * Rr + (Rr - 1)) * b + c] = v;
-  }
-}
-
-int gemm_backend_init() {
-  if (use_rocblas()) EVR_CHECK(rb_handle(), "rocBLAS handle creation failed");
-  return 0;
-}
+static bool proj_vec(const evr_qnehvi_state* st, int b) { return st->n % 2 == 0 && b % 2 == 0; }
 
 // ---- internal launchers (workspace supplied by the caller; qnehvi_plan.hip) ----------
 size_t proj_forward_ws_doubles(const evr_qnehvi_state* st, int b) {
   const int Rr = qn_rows(st);
-  if (use_rocblas()) return 0;
   int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(Rr, PT) * st->m, st->n, &kchunk);
+  const int ks = dg_ksplit((long long)cdiv(b, ProjF::BN) * cdiv(Rr, ProjF::BM) * st->m, st->n, ProjF::BK, &kchunk);
   return ks > 1 ? (size_t)ks * st->m * Rr * b : 0;
 }
 
@@ -504,45 +346,28 @@ int proj_forward(hipStream_t s, const evr_qnehvi_state* st, int b, const double*
                  double* norms, double* W) {
   if (b == 0) return 0;
   const int Rr = qn_rows(st);
-  const int nrt = cdiv(Rr, PT);
-  if (use_rocblas()) {
-    // The mean row alpha^T k is the operator's last row; kept in the GEMM it adds a 13th
-    // 64-row tile at Rr = 769 and unbalances the tile grid over the 256 CUs (MI355X,
-    // 5 x {769, 768} x 512 x 512: 54 vs 40 us).  GEMM over the first Rr - 1 rows, the mean
-    // row by qn_mean_row over the same K_x (rocBLAS' batched gemv took ~20 us there).
-    if (int rc = rb_gemm(s, false, Rr - 1, b, st->n, Mm, st->n, (long long)Rr * st->n, Kx, b, (long long)st->n * b, R,
-                         b, (long long)Rr * b, st->m))
-      return rc;
-    qn_mean_row<<<dim3(cdiv(b, MR_C), st->m), MR_C * MR_G, 0, s>>>(st->n, Rr, b, Mm, Kx, R);
-    EVR_LAUNCH_CHECK();
-    qn_norms_rows<<<dim3(cdiv(b, 64), cdiv(st->n + st->nb, 64), st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, nrt, R,
-                                                                                     norms);
-    EVR_LAUNCH_CHECK();
-    return 0;
-  }
+  const int nrt = cdiv(Rr, QN_NT);
   int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * nrt * st->m, st->n, &kchunk);
+  const int ks = dg_ksplit((long long)cdiv(b, ProjF::BN) * nrt * st->m, st->n, ProjF::BK, &kchunk);
   EVR_CHECK(ks == 1 || W, "proj_forward: split-K workspace missing");
-  dim3 grid(cdiv(b, PT), nrt, st->m * ks);
-  qn_proj_fwd<<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
+  dim3 grid(cdiv(b, ProjF::BN), nrt, st->m * ks);
+  if (proj_vec(st, b))
+    qn_proj_fwd<true><<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
+  else
+    qn_proj_fwd<false><<<grid, 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, Mm, Kx, R, norms, nrt, ks, kchunk, W);
   EVR_LAUNCH_CHECK();
   if (ks > 1) {
-    qn_proj_fwd_reduce<<<dim3(cdiv(b, PT), nrt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, ks, W, R, norms,
-                                                                       nrt);
+    qn_proj_fwd_reduce<<<dim3(cdiv(b, 256), nrt, st->m), 256, 0, s>>>(st->n, st->nb, Rr, b, st->m, ks, W, R, norms,
+                                                                        nrt);
     EVR_LAUNCH_CHECK();
   }
   return 0;
 }
 
-// backward: the generated-gR MFMA kernel wins at small candidate batches (the L-BFGS
-// restarts), gR materialisation + rocBLAS from b = 64 on (measured on MI355X)
-static bool bwd_rocblas(int b) { return use_rocblas() && b >= 64; }
-
 size_t proj_backward_ws_doubles(const evr_qnehvi_state* st, int b) {
   const int Rr = qn_rows(st);
-  if (bwd_rocblas(b)) return (size_t)st->m * 3 * b + (size_t)st->m * Rr * b;   // coefficients + gR
   int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
+  const int ks = dg_ksplit((long long)cdiv(b, ProjB::BN) * cdiv(st->n, ProjB::BM) * st->m, Rr, ProjB::BK, &kchunk);
   return (size_t)st->m * 3 * b + (ks > 1 ? (size_t)ks * st->m * st->n * b : 0);
 }
 
@@ -553,18 +378,16 @@ int proj_backward(hipStream_t s, const evr_qnehvi_state* st, int b, const double
   double* coef = ws;
   qn_bwd_coef<<<dim3(cdiv(b, BC_C), st->m), BC_C * BC_G, 0, s>>>(st->S, st->m, b, dG, L22, st->ys, st->zq, st->obj_a, coef);
   EVR_LAUNCH_CHECK();
-  if (bwd_rocblas(b)) {
-    double* gR = ws + (size_t)st->m * 3 * b;
-    qn_gen_gr<<<dim3(st->m * Rr, cdiv(b, 256)), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, R, dG, st->obj_a, coef, gR);
-    EVR_LAUNCH_CHECK();
-    return rb_gemm(s, true, st->n, b, Rr, Mm, st->n, (long long)Rr * st->n, gR, b, (long long)Rr * b, dKx, b,
-                   (long long)st->n * b, st->m);
-  }
   int kchunk = 0;
-  const int ks = proj_ksplit(cdiv(b, PT) * cdiv(st->n, PT) * st->m, Rr, &kchunk);
+  const int ks = dg_ksplit((long long)cdiv(b, ProjB::BN) * cdiv(st->n, ProjB::BM) * st->m, Rr, ProjB::BK, &kchunk);
   double* W = ws + (size_t)st->m * 3 * b;
-  dim3 grid(cdiv(b, PT), cdiv(st->n, PT), st->m * ks);
-  qn_proj_bwd<<<grid, 256, 0, s>>>(st->n, st->nb, st->S, qn_nh(st), st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks, kchunk, W);
+  dim3 grid(cdiv(b, ProjB::BN), cdiv(st->n, ProjB::BM), st->m * ks);
+  if (proj_vec(st, b))
+    qn_proj_bwd<true><<<grid, 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks,
+                                           kchunk, W);
+  else
+    qn_proj_bwd<false><<<grid, 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->m, b, Mm, R, dG, st->obj_a, coef, dKx, ks,
+                                            kchunk, W);
   EVR_LAUNCH_CHECK();
   if (ks > 1) {
     const long long per = (long long)st->m * st->n * b;
@@ -595,7 +418,7 @@ extern "C" {
 
 int evr_qnehvi_norms_rows(const evr_qnehvi_state* st) {
   if (!st) return 0;
-  return cdiv((long long)qn_rows(st), PT);
+  return cdiv((long long)qn_rows(st), QN_NT);
 }
 
 long long evr_qnehvi_project_workspace_doubles(const evr_qnehvi_state* st, int b) {
@@ -618,7 +441,7 @@ int evr_qnehvi_project(void* stream, const evr_qnehvi_state* st, int b, const do
 int evr_qnehvi_samples_norms(void* stream, const evr_qnehvi_state* st, int b, const double* R, const double* norms,
                              double* G, double* L22, int* flags) {
   EVR_CHECK(st && R && norms && G && L22 && flags && b >= 0, "evr_qnehvi_samples_norms: bad arguments");
-  return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags, PT);
+  return samples_norms((hipStream_t)stream, st, b, R, norms, G, L22, flags, QN_NT);
 }
 
 long long evr_qnehvi_project_backward_workspace_doubles(const evr_qnehvi_state* st, int b) {

@@ -824,24 +824,34 @@ def box_decompose_kd_device(O: torch.Tensor, ref: torch.Tensor, want_kd: bool = 
     lib = _native.load()
     counts_h = np.zeros(S, dtype=np.int32)
     info = np.zeros(3, dtype=np.int32)
+    cap0 = cap
     while True:
         nbytes = lib.evr_box_device_workspace_bytes(S, n, m, cap)
-        if nbytes > max_workspace_bytes:
-            raise BoxCapacityError(f"box decomposition: {cap} LUB slots x {S} samples need {nbytes} B of workspace")
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        cs = torch.empty(2, S, dtype=torch.int32, device=dev)
-        offs = torch.empty(2, S + 1, dtype=torch.int32, device=dev)
-        keys = torch.empty(S * cap, dtype=torch.int64, device=dev)           # uint64 bit patterns
-        pts = torch.empty(S, stride, m, dtype=torch.float64, device=dev)
-        rank0 = torch.empty(S, stride, dtype=torch.int32, device=dev)
         G = S * cap // 16 + S
+        # the capacity-sized outputs count against the budget too (they live as long as the
+        # acquisition when not trimmed below)
+        out_bytes = 8 * S * cap + 8 * S * stride * m + 4 * S * stride + 16 * S + 8
         if want_kd:
-            okeys = torch.empty(G * 16, dtype=torch.int64, device=dev)
-            ork = torch.empty(G * m * 16, dtype=torch.int16, device=dev)    # uint16 bit patterns
-            ogb = torch.empty(G * 8, dtype=torch.int16, device=dev)
-            osv = torch.empty(S, m, stride, dtype=torch.float64, device=dev)
-        else:
-            okeys = ork = ogb = osv = None
+            out_bytes += G * 16 * 8 + G * m * 16 * 2 + G * 8 * 2 + 8 * S * m * stride
+        if nbytes + out_bytes > max_workspace_bytes:
+            raise BoxCapacityError(f"box decomposition: {cap} LUB slots x {S} samples need {nbytes + out_bytes} B "
+                                   "of workspace and outputs")
+        try:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            cs = torch.empty(2, S, dtype=torch.int32, device=dev)
+            offs = torch.empty(2, S + 1, dtype=torch.int32, device=dev)
+            keys = torch.empty(S * cap, dtype=torch.int64, device=dev)           # uint64 bit patterns
+            pts = torch.empty(S, stride, m, dtype=torch.float64, device=dev)
+            rank0 = torch.empty(S, stride, dtype=torch.int32, device=dev)
+            if want_kd:
+                okeys = torch.empty(G * 16, dtype=torch.int64, device=dev)
+                ork = torch.empty(G * m * 16, dtype=torch.int16, device=dev)    # uint16 bit patterns
+                ogb = torch.empty(G * 8, dtype=torch.int16, device=dev)
+                osv = torch.empty(S, m, stride, dtype=torch.float64, device=dev)
+            else:
+                okeys = ork = ogb = osv = None
+        except torch.OutOfMemoryError as e:
+            raise BoxCapacityError(f"box decomposition: out of device memory at {cap} LUB slots x {S} samples") from e
         call("evr_box_kd_pipeline", _stream(), S, n, m, O.data_ptr(), ref.data_ptr(), cap, ws.data_ptr(),
              cs[0].data_ptr(), cs[1].data_ptr(), offs[0].data_ptr(), offs[1].data_ptr(), keys.data_ptr(),
              pts.data_ptr(), rank0.data_ptr(), int(bool(want_kd)), _p(okeys), _p(ork), _p(ogb), _p(osv),
@@ -853,12 +863,17 @@ def box_decompose_kd_device(O: torch.Tensor, ref: torch.Tensor, want_kd: bool = 
         cap *= 4
     counts = counts_h.astype(np.int64)
     total = int(counts.sum())
-    cells = Cells(offs[0], counts, m, keys=keys[:max(total, 1)], pts=pts, rank0=rank0, stride=stride)
+    del ws
+    # a capacity rerun leaves outputs sized for 4x the slots or more: keep copies of the used
+    # prefixes instead of views that pin the whole allocation (the first-try capacity keeps
+    # views: no copy on the ask's critical path)
+    trim = (lambda t: t.clone()) if cap > cap0 else (lambda t: t)
+    cells = Cells(offs[0], counts, m, keys=trim(keys[:max(total, 1)]), pts=pts, rank0=rank0, stride=stride)
     if info[1]:
         ng = (counts + 15) // 16
         Gu = int(ng.sum())
-        cells.kd = KdGroups(offs[1], okeys[:max(Gu, 1) * 16], ork[:max(Gu, 1) * m * 16], ogb[:max(Gu, 1) * 8], osv,
-                            int(ng.max()) if S else 0)
+        cells.kd = KdGroups(offs[1], trim(okeys[:max(Gu, 1) * 16]), trim(ork[:max(Gu, 1) * m * 16]),
+                            trim(ogb[:max(Gu, 1) * 8]), osv, int(ng.max()) if S else 0)
     return cells, bool(info[1])
 
 

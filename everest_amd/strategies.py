@@ -365,7 +365,13 @@ class BotorchStrategy(PredictiveStrategy):
             stats.best_value = val
             self.last_ask_stats = stats
             return self._postprocess_candidates(x.reshape(q, -1))
-        acqf = self._get_acqfs(q)[0]
+        # only this call site runs optimize_acqf's raw screening: the acquisition builder may
+        # start that draw early (calc_acquisition and the mixed paths never use it)
+        self._prefetch_raw = len(combos) <= 1
+        try:
+            acqf = self._get_acqfs(q)[0]
+        finally:
+            self._prefetch_raw = False
         if len(combos) > 1:     # EXHAUSTIVE categorical method: optimize_acqf_mixed
             x, val, stats = optimize_acqf_mixed(acqf, self._bounds(), combos, self.num_restarts, self.num_raw_samples,
                                                 self._get_optimizer_options(), self.gen, ineq, eq, dist=self.dist,
@@ -658,7 +664,8 @@ class QnehviStrategy(QehviStrategy):
         # optimize_acqf's raw-sample seed is the generator's next draw: its Sobol draw runs on a
         # worker thread while the acquisition is built (plain box bounds only; otherwise the
         # optimiser draws as usual)
-        if (not get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
+        if (getattr(self, "_prefetch_raw", False)
+                and not get_linear_constraints(self.domain, dm.LinearInequalityConstraint)
                 and not get_linear_constraints(self.domain, dm.LinearEqualityConstraint)
                 and len(self.get_categorical_combinations()) <= 1):
             prefetch_raw_samples(self._bounds(), self.num_raw_samples, self.gen, q=n)

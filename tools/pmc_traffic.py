@@ -4,10 +4,9 @@ bench.py's ``roofline.traffic``.
 
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports half the bytes of a wide coalesced
 read on gfx950 — doubled here; WRITE_SIZE is exact for 16 B/lane stores.  rocprofv3 reports
-both in KiB.  Dispatches are labelled with the bench op that launches them (rocBLAS GEMMs
-by position: the one after kmat_kernel is the forward projection, the one after qn_gen_gr
-the backward); a step starts at each kmat_kernel dispatch; the per-launch figure of an op
-is its summed bytes per step, averaged over the last PMC_LAST steps.
+both in KiB.  Dispatches are labelled with the bench op that launches them; a step starts at
+each kmat_kernel dispatch; the per-launch figure of an op is its summed bytes per step,
+averaged over the last PMC_LAST steps.
 
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> [out.json] [suffix]
 (suffix, e.g. "@b20" for a tools/loop_step.py N 20 pass: keys become op@b20 and are merged into
@@ -23,18 +22,16 @@ from collections import defaultdict
 
 OPS = [
     ("kernel_matrix", r"kmat_kernel"),
-    ("proj_fwd", r"qn_proj_fwd|qn_norms_rows|qs_fwd"),
+    ("proj_fwd", r"qn_proj_fwd|qs_fwd"),
     ("samples", r"qn_samples_norms"),
     ("hvi_fwd_bwd", r"hvi_thresholds|hvi_kd[23bw]?<|hvi_tiled<|hvi_reduce_fwd|hvi_reduce_bwd|hvi_reduce_fb"),
-    ("proj_bwd", r"qn_bwd_coef|qn_proj_bwd|qn_splitk_sum|qn_gen_gr|qs_bwd|qs_dx_reduce"),
+    ("proj_bwd", r"qn_bwd_coef|qn_proj_bwd|qn_splitk_sum|qs_bwd|qs_dx_reduce"),
     ("kernel_grad", r"kcross_grad"),
 ]
 LAST = int(os.environ.get("PMC_LAST", "10"))   # tools/loop_step.py: the last N steps
 
 
 def label(name, prev):
-    if name.startswith("Cijk") or "Cijk_" in name:
-        return "proj_bwd" if prev == "proj_bwd" else "proj_fwd"
     for op, pat in OPS:
         if re.search(pat, name):
             return op
