@@ -253,6 +253,56 @@ def gp_posterior_ms(device, gp=None, n_test=1024, reps=20):
     return _event_ms(lambda: gp.posterior(Xs), reps=reps)
 
 
+def config1_loop(seed=7):
+    """BASELINE configs[0] (README.md:82-104): the Detergent benchmark, QnehviStrategy at the
+    data model's defaults (512 MC samples, 1024 raw samples, 8 restarts, batch_limit 8, two
+    linear inequality constraints: hit-and-run raw samples, SLSQP restarts on the device
+    gradient), 2 random initial experiments then 4 x (tell -> ask(1) -> f).  Wall time of
+    every tell and ask (synchronised); the first tell / ask include the process's first use
+    of those code paths."""
+    import everest_amd.data_models as dm
+    from everest_amd import strategies
+    from everest_amd.benchmarks import Detergent
+
+    bm = Detergent()
+    rnd = strategies.map(dm.RandomStrategy(domain=bm.domain, seed=19))
+    exps = bm.f(rnd.ask(2), return_complete=True)
+    s = strategies.map(dm.QnehviStrategy(domain=bm.domain, seed=seed))
+    tells, asks = [], []
+    for it in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.tell(exps)
+        torch.cuda.synchronize()
+        tells.append(time.perf_counter() - t0)
+        if it == 4:
+            break
+        t0 = time.perf_counter()
+        c = s.ask(candidate_count=1)
+        torch.cuda.synchronize()
+        asks.append(time.perf_counter() - t0)
+        exps = bm.f(c[bm.domain.inputs.get_keys()], return_complete=True)
+    r = lambda v: [round(x, 4) for x in v]  # noqa: E731
+    return {"workload": "BASELINE configs[0]: Detergent, QnehviStrategy defaults (S=512, raw 1024, 8 restarts, "
+                        "SLSQP under 2 linear constraints), 2 initial + 4 ask/tell rounds",
+            "ask_s": r(asks), "tell_s": r(tells), "ask_s_median": round(float(np.median(asks)), 4),
+            "tell_s_median": round(float(np.median(tells)), 4), "experiments": s.num_experiments,
+            "driver": s.last_ask_stats.chunks[0]["driver"] if s.last_ask_stats.chunks else None}
+
+
+def build_provenance():
+    """everest_amd/_lib/build_info.json (written by the Makefile next to the libraries): the
+    commit the shipped .so files were built from and their SHA-256."""
+    try:
+        with open(os.path.join(ROOT, "everest_amd", "_lib", "build_info.json")) as f:
+            info = json.load(f)
+        return {"commit": info.get("commit"), "dirty": info.get("dirty"), "built_utc": info.get("built_utc"),
+                "compiler": info.get("compiler"),
+                "sha256": {k: v.get("sha256", "")[:16] for k, v in info.get("libs", {}).items()}}
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(acqf, hypers, X, Y, Xc_cpu, chunk=8, budget_s=12.0):
     """Reference-structure CPU restatement (oracle/, torch-CPU fp64, BoTorch computation
     shape: joint posterior over [X_base; x] per forward, per-sample cell scan, autograd
@@ -589,6 +639,7 @@ def main():
     ap.add_argument("--cpu-full-ask", default=None, metavar="JSON",
                     help="also run one FULL reference-structure ask on the host (minutes) and write it to JSON")
     ap.add_argument("--no-eval-pass", action="store_true", help="skip the b-candidate evaluation-pass figures")
+    ap.add_argument("--no-config1", action="store_true", help="skip the configs[0] Detergent ask/tell loop timing")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -824,6 +875,7 @@ def main():
             torch.set_num_threads(threads)
         gp_ask = s.model
         t_post = gp_posterior_ms(device, gp=gp_ask)
+        cfg1 = None if args.no_config1 else config1_loop()
         out = {
             "metric": "QnehviStrategy.ask() candidates/sec + GP posterior ms, n=512 d=6 m=5",
             "value": round(value, 1),
@@ -864,6 +916,8 @@ def main():
             "gp_posterior": {"ms": round(t_post, 4), "shape": f"n_train={args.n} d={args.d} m={args.m} (the ask's "
                              "fitted model), 1024 test points, mean+var, HIP events",
                              "config2_ms": round(gp_posterior_ms(device), 4)},
+            "config1": cfg1,
+            "build": build_provenance(),
         }
         print(json.dumps(out))
     if dist is not None:
