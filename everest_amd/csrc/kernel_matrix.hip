@@ -17,14 +17,38 @@ namespace evr {
 constexpr int KT = 64;
 constexpr int KMAXD = 64;
 
+// Host-driven evaluations queued one ahead (qnehvi_plan.hip): the first kernel of the queued
+// chain waits here until the host posts the next request — the request word (pinned host
+// memory, written after the candidates) differs from the sequence number the previous chain
+// processed (device memory).  Thread 0 polls with relaxed loads of the fine-grained host
+// word (uncached: every poll reads host memory); the workgroup barrier after the poll orders
+// the candidates' loads — the same uncached host memory, written before the request word —
+// after it.  No system-scope fence: its L2 writeback / invalidate cost the chain 25 us per
+// evaluation (its operator M is L2-resident across evaluations).  A 2 s failsafe ends the
+// wait (the host's own wait then times out with an error).
+__device__ __forceinline__ void kmat_wait_request(const unsigned long long* poll, const unsigned long long* plast) {
+  if (threadIdx.x == 0) {
+    const unsigned long long last = *plast;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(const_cast<unsigned long long*>(poll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+           last) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > 200000000ull) break;   // s_memrealtime: 100 MHz
+    }
+  }
+  __syncthreads();
+}
+
 template <int RA, int KIND>
 __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int d, const double* __restrict__ X1,
                                                    const double* __restrict__ sh1, const double* __restrict__ sc1,
                                                    const double* __restrict__ X2, const double* __restrict__ sh2,
                                                    const double* __restrict__ sc2, const double* __restrict__ ls,
                                                    const double* __restrict__ os, const double* __restrict__ dg,
-                                                   double* __restrict__ K) {
+                                                   double* __restrict__ K, const unsigned long long* poll,
+                                                   const unsigned long long* plast) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if (poll) kmat_wait_request(poll, plast);
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * (16 * RA), j0 = blockIdx.x * KT;
   const int ld = d + 1;
@@ -42,6 +66,8 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
     xw[t] = 0.0;
     if (e < KT * d) {
       if (r < 16 * RA && i0 + r < n1) xv[t] = X1[(size_t)(i0 + r) * d + (e - r * d)];
+      // (a queued chain's candidates live in fine-grained host memory, which the GPU does not
+      // cache: these loads read what the host posted before the request word)
       if (j0 + r < n2) xw[t] = X2[(size_t)(j0 + r) * d + (e - r * d)];
     }
   }
@@ -1003,6 +1029,10 @@ int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const doubl
   EVR_LAUNCH_CHECK();
   return 0;
 }
+int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
+                         const double* scale1, const double* X2, const double* shift2, const double* scale2,
+                         const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
+                         const unsigned long long* poll, const unsigned long long* plast);
 }  // namespace evr
 
 extern "C" {
@@ -1010,6 +1040,21 @@ extern "C" {
 int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                       const double* scale1, const double* X2, const double* shift2, const double* scale2,
                       const double* lengthscales, const double* outputscale, const double* diag_add, double* K) {
+  return kernel_matrix_launch(stream, kind, B, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, lengthscales,
+                              outputscale, diag_add, K, nullptr, nullptr);
+}
+
+}  // extern "C"
+
+namespace evr {
+// evr_kernel_matrix with the request wait of the queued host-driven chains (poll / plast, see
+// kmat_wait_request): the VALU kernel (d < 16, one output family) only
+int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
+                         const double* scale1, const double* X2, const double* shift2, const double* scale2,
+                         const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
+                         const unsigned long long* poll, const unsigned long long* plast) {
+  EVR_CHECK(!poll || (plast && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
+            "kernel_matrix_launch: the request wait needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(kind_code_ok(kind, B), "evr_kernel_matrix: bad kernel kind %d for %d outputs", kind, B);
   EVR_CHECK(B >= 1 && n1 >= 0 && n2 >= 0 && d >= 1 && d <= KMAXD, "evr_kernel_matrix: bad sizes B=%d n1=%d n2=%d d=%d",
             B, n1, n2, d);
@@ -1116,7 +1161,8 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   dim3 g(cdiv(n2, KT), cdiv(n1, 16 * ra), B);
 #define KTK(RA_, K_)                                                                              \
   kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
-                                                             scale2, lengthscales, outputscale, diag_add, K)
+                                                             scale2, lengthscales, outputscale, diag_add, K, poll,   \
+                                                             plast)
 #define KT_(RA_)                         \
   if (kind == RBF) KTK(RA_, RBF);           \
   else if (kind == MATERN05) KTK(RA_, MATERN05); \
@@ -1130,6 +1176,9 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
   EVR_LAUNCH_CHECK();
   return 0;
 }
+}  // namespace evr
+
+extern "C" {
 
 int evr_kernel_cross_grad(void* stream, int kind, int B, int n1, int n2, int d, const double* X1,
                           const double* shift1, const double* scale1, const double* X2, const double* shift2,

@@ -16,6 +16,7 @@
 #include <new>
 
 #include "common.hpp"
+#include "gemm_core.hpp"
 #include "../../include/everest_amd.h"
 
 namespace evr {
@@ -26,9 +27,54 @@ int gemm_plain(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alph
                long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
                int batch);
 size_t mll_terms_part_doubles(int B);
+size_t dg_gemm_ws_doubles(bool tA, int M, int N, int K, int batch);
+int dg_gemm(hipStream_t s, bool tA, int M, int N, int K, double alpha, const double* A, int lda, long long sA,
+            const double* B, int ldb, long long sB, double beta, double* Cm, int ldc, long long sC, int batch,
+            double* W);
 int mll_terms_chunks();
 int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const double* Linv, const double* r,
                        const double* alpha, double* part);
+
+// W = alpha alpha^T - K^-1 = alpha alpha^T - L^-T L^-1 in one launch of the gemm_core.hpp
+// engine (A = L^-T: L^-1 read m-contiguous).  L^-1 is lower triangular, so W[i][j] sums over
+// k >= max(i, j) only: tile (by, bx) contracts over k >= 32 max(by, bx) — a third of the dense
+// product's flops, the skipped terms exact zeros.  Tiles are dispatched in shells of equal
+// max(by, bx), longest k range first, outputs interleaved; the rank-1 alpha alpha^T term is
+// the epilogue (the former separate alpha alpha^T GEMM launch).
+using MllW = DgCfg<32, 32, 16, true>;
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 4) void mll_w_kernel(int n, int B, const double* __restrict__ Linv,
+                                                       const double* __restrict__ alpha, double* __restrict__ W) {
+  using C = MllW;
+  __shared__ double lds[C::LDS_DOUBLES];
+  const int f = blockIdx.x, j = f % B, t = f / B;
+  int sh = (int)sqrt((double)t);
+  while (sh * sh > t) --sh;
+  while ((sh + 1) * (sh + 1) <= t) ++sh;
+  const int pp = t - sh * sh;
+  const int by = pp <= sh ? sh : pp - sh - 1, bx = pp <= sh ? pp : sh;
+  const int m0 = by * C::BM, n0 = bx * C::BN;
+  const size_t nn = (size_t)n * n;
+  const double* Lj = Linv + j * nn;
+  const int kbeg = max(m0, n0);
+  dg_double4 acc[C::FM][C::FN];
+  dg_mainloop<C>(
+      lds, kbeg, n,
+      [&](int k, int c) -> dg_double2 {
+        return dg_pair<VEC>(Lj + (size_t)k * n + m0 + c, k < n && m0 + c < n, k < n && m0 + c + 1 < n);
+      },
+      [&](int k, int c) -> dg_double2 {
+        return dg_pair<VEC>(Lj + (size_t)k * n + n0 + c, k < n && n0 + c < n, k < n && n0 + c + 1 < n);
+      },
+      acc);
+  const double* aj = alpha + (size_t)j * n;
+  double* Wj = W + j * nn;
+  dg_for_each<C>(acc, [&](int r, int c, double v) {
+    const int row = m0 + r, col = n0 + c;
+    if (row < n && col < n) Wj[(size_t)row * n + col] = aj[row] * aj[col] - v;
+  });
+}
 
 // hx: [ls (B x d) | noise (B) | constant (B) | sequence number]
 __global__ void mll_copy_in(int B, int d, const double* hx, double* ls, double* noise, double* cst) {
@@ -75,7 +121,7 @@ using namespace evr;
 struct evr_mll_plan {
   int kind, B, n, d;
   const double* Xn;
-  double *Y, *ls, *noise, *cst, *K, *L, *Linv, *Dinv, *T, *r, *v, *alpha, *gls, *gw, *part, *jit0;
+  double *Y, *ls, *noise, *cst, *K, *L, *Linv, *Dinv, *T, *r, *v, *alpha, *gls, *gw, *part, *jit0, *mvw;
   int* info;
   double *hx, *hout;
   hipGraph_t graph;
@@ -95,11 +141,16 @@ static int mll_chain(hipStream_t s, evr_mll_plan* p, const double* dhx, double* 
   mll_resid<<<cdiv(B * n, 256), 256, 0, s>>>(B, n, p->Y, p->cst, p->r);
   EVR_LAUNCH_CHECK();
   double* W = p->K;   // K was consumed by the factorisation
-  if (int rc = gemm_plain(s, false, false, n, 1, n, 1.0, p->Linv, n, nn, p->r, 1, n, 0.0, p->v, 1, n, B)) return rc;
-  if (int rc = gemm_plain(s, true, false, n, 1, n, 1.0, p->Linv, n, nn, p->v, 1, n, 0.0, p->alpha, 1, n, B))
-    return rc;
-  if (int rc = gemm_plain(s, false, true, n, n, 1, 1.0, p->alpha, 1, n, p->alpha, 1, n, 0.0, W, n, nn, B)) return rc;
-  if (int rc = gemm_plain(s, true, false, n, n, n, -1.0, p->Linv, n, nn, p->Linv, n, nn, 1.0, W, n, nn, B)) return rc;
+  // v = L^-1 r, alpha = L^-T v: matrix-vector products, split over k (the plan's workspace
+  // holds the partials; a fixed-order reduction) so that they spread over ~300 workgroups
+  if (int rc = dg_gemm(s, false, n, 1, n, 1.0, p->Linv, n, nn, p->r, 1, n, 0.0, p->v, 1, n, B, p->mvw)) return rc;
+  if (int rc = dg_gemm(s, true, n, 1, n, 1.0, p->Linv, n, nn, p->v, 1, n, 0.0, p->alpha, 1, n, B, p->mvw)) return rc;
+  {
+    const int T = cdiv(n, MllW::BM);
+    if (n % 2 == 0) mll_w_kernel<true><<<T * T * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
+    else mll_w_kernel<false><<<T * T * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
+    EVR_LAUNCH_CHECK();
+  }
   if (int rc = evr_kernel_lengthscale_grad(s, p->kind, B, n, d, p->Xn, p->ls, W, p->gls, p->gw)) return rc;
   if (int rc = mll_terms_partials(s, B, n, p->L, p->Linv, p->r, p->alpha, p->part)) return rc;
   mll_copy_out<<<1, 256, 0, s>>>(B, d, mll_terms_chunks(), p->part, p->gls, p->info, dhx, dhout);
@@ -112,7 +163,7 @@ static void mll_free(evr_mll_plan* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   double* bufs[] = {p->Y, p->ls, p->noise, p->cst, p->K, p->L, p->Linv, p->Dinv, p->T, p->r, p->v, p->alpha,
-                    p->gls, p->gw, p->part, p->jit0};
+                    p->gls, p->gw, p->part, p->jit0, p->mvw};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
@@ -144,7 +195,8 @@ int evr_mll_plan_create(void* stream, int kind, int B, int n, int d, const doubl
               {&p->Linv, B * nn},       {&p->Dinv, chol_inverse_dinv_doubles(B, n)},
               {&p->T, (size_t)B * 64 * n}, {&p->r, (size_t)B * n}, {&p->v, (size_t)B * n},
               {&p->alpha, (size_t)B * n}, {&p->gls, (size_t)B * d}, {&p->gw, (size_t)B * n * d},
-              {&p->part, mll_terms_part_doubles(B)}, {&p->jit0, (size_t)B}};
+              {&p->part, mll_terms_part_doubles(B)}, {&p->jit0, (size_t)B},
+              {&p->mvw, std::max(dg_gemm_ws_doubles(false, n, 1, n, B), dg_gemm_ws_doubles(true, n, 1, n, B))}};
   for (auto& q : need) {
     if (hipMalloc((void**)q.ptr, sizeof(double) * std::max<size_t>(q.count, 1)) != hipSuccess) {
       mll_free(p);

@@ -459,7 +459,8 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
                                                     double* __restrict__ acq, double* hout,
                                                     const double* seqp,
                                                     const double* __restrict__ sval, int S, int m,
-                                                    const int* __restrict__ flags) {
+                                                    const int* __restrict__ flags,
+                                                    unsigned long long* __restrict__ plast) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool ein = e < b * d;
   const int k = e % d;
@@ -518,6 +519,9 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   if (hout) {
     __syncthreads();
     if (threadIdx.x == 0) *(volatile unsigned long long*)(hout + b + (size_t)b * d + blockIdx.x) = seq;
+    // the request this chain served: a chain queued behind it waits for a newer one
+    // (kmat_wait_request); read by the next kernel of the stream only
+    if (plast && blockIdx.x == 0 && threadIdx.x == 0) *plast = seq;
   }
 }
 
@@ -560,7 +564,8 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
 
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
-                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags) {
+                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags,
+                unsigned long long* plast) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
   EVR_CHECK(st->S <= QS_SMAX, "qs_backward: %d samples exceed the staged %d", st->S, QS_SMAX);
@@ -574,7 +579,7 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
   EVR_LAUNCH_CHECK();
   (void)counter;
   qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, sval,
-                                                   st->S, st->m, flags);
+                                                   st->S, st->m, flags, plast);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -615,7 +620,7 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
   return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr);
+                     nullptr, nullptr, nullptr);
 }
 
 }  // extern "C"
