@@ -12,8 +12,10 @@
 // reported through info; the caller reruns that evaluation through the jitter ladder.
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "common.hpp"
 #include "gemm_core.hpp"
@@ -272,5 +274,125 @@ int evr_mll_plan_eval(void* stream, evr_mll_plan* p, const double* params, doubl
 }
 
 void evr_mll_plan_destroy(evr_mll_plan* p) { mll_free(p); }
+
+int evr_lbfgsb_advance(void* run, double f, const double* g, double* x, int* task, int* nit, int* nfev, int* status,
+                       int maxiter, int maxfun) {
+  EVR_CHECK(run && g && x && task && nit && nfev && status, "evr_lbfgsb_advance: bad arguments");
+  evr_lbfgsb* h = (evr_lbfgsb*)run;
+  ++*nfev;
+  int t = evr_lbfgsb_step(h, f, g, x);
+  while (t == EVR_LBFGSB_NEW_X) {
+    ++*nit;
+    if (*nit >= maxiter || *nfev > maxfun) {
+      *status = 1;
+      *task = 0;
+      return 0;
+    }
+    t = evr_lbfgsb_step(h, f, g, x);
+  }
+  if (t == EVR_LBFGSB_FG) {
+    *task = EVR_LBFGSB_FG;
+    return 0;
+  }
+  *status = t == EVR_LBFGSB_ABNORMAL ? 2 : (t == EVR_LBFGSB_ERROR ? 3 : 0);
+  *task = 0;
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+// gpytorch LogNormalPrior / GammaPrior / NormalPrior log densities and their derivatives
+// (gp.prior_logpdf_np / prior_dlogpdf_np)
+double prior_logpdf(int fam, double a, double b, double x) {
+  if (fam == 1) {
+    const double lx = std::log(x), z = (lx - a) / b;
+    return -lx - std::log(b) - 0.5 * std::log(2.0 * M_PI) - 0.5 * (z * z);
+  }
+  if (fam == 2) return a * std::log(b) - std::lgamma(a) + (a - 1.0) * std::log(x) - b * x;
+  const double z = (x - a) / b;
+  return -0.5 * std::log(2.0 * M_PI * b * b) - 0.5 * (z * z);
+}
+double prior_dlogpdf(int fam, double a, double b, double x) {
+  if (fam == 1) return (-1.0 - (std::log(x) - a) / (b * b)) / x;
+  if (fam == 2) return (a - 1.0) / x - b;
+  return -(x - a) / (b * b);
+}
+double softplus(double v) {   // numpy logaddexp(0, v)
+  if (v == 0.0) return M_LN2;
+  return v > 0.0 ? v + std::log1p(std::exp(-v)) : std::log1p(std::exp(v));
+}
+}  // namespace
+
+extern "C" {
+
+int evr_mll_fit_rounds(void* stream, evr_mll_plan* p, void** runs, int* task, double* x, double* f, double* g,
+                       int* nit, int* nfev, int* status, int maxiter, int maxfun, const double* prior, double* params,
+                       int* pending) {
+  EVR_CHECK(p && runs && task && x && f && g && nit && nfev && status && prior && params && pending,
+            "evr_mll_fit_rounds: bad arguments");
+  const int B = p->B, d = p->d, n = p->n, nx = d + 2;
+  const int lf = (int)prior[0], nzf = (int)prior[3];
+  std::vector<double> out((size_t)B * (5 + d + 1)), gb(nx);
+  *pending = 0;
+  for (;;) {
+    bool any = false;
+    for (int b = 0; b < B; ++b) {
+      if (task[b] != EVR_LBFGSB_FG) continue;
+      any = true;
+      const double* xb = x + (size_t)b * nx;
+      for (int j = 0; j < d; ++j) params[(size_t)b * d + j] = softplus(xb[2 + j]);
+      params[(size_t)B * d + b] = xb[0];
+      params[(size_t)B * d + B + b] = xb[1];
+    }
+    if (!any) return 0;
+    if (int rc = evr_mll_plan_eval(stream, p, params, out.data())) return rc;
+    const double* terms = out.data();
+    const double* gls = terms + (size_t)5 * B;
+    const double* info = gls + (size_t)B * d;
+    for (int b = 0; b < B; ++b) {
+      if (task[b] != EVR_LBFGSB_FG) continue;
+      bool ok = info[b] == 0.0;
+      for (int q = 0; q < 5; ++q) ok = ok && std::isfinite(terms[(size_t)b * 5 + q]);
+      if (!ok) {
+        *pending = 1;   // this round goes through the jitter ladder (the caller)
+        return 0;
+      }
+    }
+    for (int b = 0; b < B; ++b) {
+      if (task[b] != EVR_LBFGSB_FG) continue;
+      double* xb = x + (size_t)b * nx;
+      const double* t = terms + (size_t)b * 5;
+      const double logdet = t[0], quad = t[1], trKinv = t[2], sum_a = t[3], sum_a2 = t[4];
+      double ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * std::log(2.0 * M_PI);
+      double d_noise = 0.5 * (sum_a2 - trKinv);
+      const double d_const = sum_a;
+      const double noise = xb[0];
+      if (lf) {
+        double s = 0.0;
+        for (int j = 0; j < d; ++j) s += prior_logpdf(lf, prior[1], prior[2], params[(size_t)b * d + j]);
+        ll += s;
+      }
+      if (nzf) {
+        ll += prior_logpdf(nzf, prior[4], prior[5], noise);
+        d_noise += prior_dlogpdf(nzf, prior[4], prior[5], noise);
+      }
+      gb[0] = d_noise / n;
+      gb[1] = d_const / n;
+      for (int j = 0; j < d; ++j) {
+        const double lsj = params[(size_t)b * d + j];
+        double dl = 0.5 * gls[(size_t)b * d + j];
+        if (lf) dl += prior_dlogpdf(lf, prior[1], prior[2], lsj);
+        gb[2 + j] = dl * (1.0 / (1.0 + std::exp(-xb[2 + j]))) / n;
+      }
+      // minimise -MLL / n
+      f[b] = -(ll / n);
+      for (int j = 0; j < nx; ++j) g[(size_t)b * nx + j] = -gb[j];
+      if (int rc = evr_lbfgsb_advance(runs[b], f[b], g + (size_t)b * nx, xb, task + b, nit + b, nfev + b, status + b,
+                                      maxiter, maxfun))
+        return rc;
+    }
+  }
+}
 
 }  // extern "C"

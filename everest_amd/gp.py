@@ -344,22 +344,40 @@ class MLLBatch:
         terms = ops.mll_terms(L, Linv, r[..., 0].contiguous(), alpha[..., 0].contiguous())
         return torch.cat([terms.reshape(-1), gls.reshape(-1), info.to(torch.float64)]).cpu().numpy()
 
-    def _eval_plan(self, idx, ls, noise, const):
-        """All members through the native MLL plan (evr_mll_plan_eval: one graph launch);
-        members outside idx keep their last parameters.  None when an active member's
-        attempt-0 factor fails (the caller takes the ladder path)."""
-        Bt, d = self.Y.shape[0], self.d
+    def plan_handle(self):
+        """The native MLL plan (evr_mll_plan_create), built on first use."""
         if self._plan is None:
+            Bt, d = self.Y.shape[0], self.d
             h = ctypes.c_void_p()
             ops.call("evr_mll_plan_create", ops._stream(), int(self.kind), Bt, self.n, d, self.Xn.data_ptr(),
                      self.Y.data_ptr(), ctypes.byref(h))
             self._plan = h
             self._lib = _native.load()
+            self._params = None
+            self._pout = np.empty(Bt * (5 + d + 1))
+        return self._plan
+
+    def prior_spec(self) -> np.ndarray:
+        """[ls family, a, b, noise family, a, b] for evr_mll_fit_rounds (family 0 none,
+        1 LogNormal, 2 Gamma, 3 Normal)."""
+        fam = {"lognormal": 1, "gamma": 2, "normal": 3}
+        out = np.zeros(6)
+        for k, p in enumerate((self.ls_prior, self.noise_prior)):
+            if p is not None:
+                out[3 * k:3 * k + 3] = (fam[p[0]], p[1], p[2])
+        return out
+
+    def _eval_plan(self, idx, ls, noise, const):
+        """All members through the native MLL plan (evr_mll_plan_eval: one graph launch);
+        members outside idx keep their last parameters.  None when an active member's
+        attempt-0 factor fails (the caller takes the ladder path)."""
+        Bt, d = self.Y.shape[0], self.d
+        self.plan_handle()
+        if self._params is None:
             self._params = np.empty((Bt, d + 2))
             self._params[:, :d] = ls[0]
             self._params[:, d] = noise[0]
             self._params[:, d + 1] = const[0]
-            self._pout = np.empty(Bt * (5 + d + 1))
         P = self._params
         for k, b in enumerate(idx):
             P[b, :d], P[b, d], P[b, d + 1] = ls[k], noise[k], const[k]
@@ -415,6 +433,76 @@ class MLLBatch:
         return out
 
 
+def _fit_rounds_native(ev: "MLLBatch", B: int, d: int, x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int,
+                       maxfun: int, restart_x) -> List[np.ndarray]:
+    """fit_batch's lock-step loop in native code (evr_mll_fit_rounds: per round one MLL plan
+    evaluation, the -MLL / n value and gradient with the priors, and every member's L-BFGS-B
+    steps, with no Python between rounds).  A round in which a member's attempt-0 factor
+    fails comes back here: it is evaluated through MLLBatch (the jitter ladder), members that
+    stay not p.d. restart from a prior sample, and the others advance (evr_lbfgsb_advance).
+    Same algorithm and state machine as the generator loop (lbfgsb_steps)."""
+    from .optim import _EPS, LBFGSB_FG
+
+    lib = _native.load()
+    nx = d + 2
+    lo = np.ascontiguousarray(lb, dtype=np.float64)
+    hi = np.ascontiguousarray(ub, dtype=np.float64)
+    runs = (ctypes.c_void_p * B)()
+    task = np.zeros(B, dtype=np.int32)
+    nit = np.zeros(B, dtype=np.int32)
+    nfev = np.zeros(B, dtype=np.int32)
+    status = np.zeros(B, dtype=np.int32)
+    X = np.zeros((B, nx))
+    F = np.zeros(B)
+    G = np.zeros((B, nx))
+    params = np.zeros(B * nx)
+    prior = ev.prior_spec()
+    plan = ev.plan_handle()
+    i32 = lambda a, k=0: a.ctypes.data + 4 * k  # noqa: E731
+
+    def start(b, xb0):
+        if runs[b]:
+            lib.evr_lbfgsb_destroy(runs[b])
+            runs[b] = None
+        h = ctypes.c_void_p()
+        _native.check(lib.evr_lbfgsb_create(nx, 10, lo.ctypes.data, hi.ctypes.data, 2.220446049250313e-09 / _EPS,
+                                            1e-5, 20, ctypes.byref(h)), "evr_lbfgsb_create")
+        runs[b] = h.value
+        x0c = np.ascontiguousarray(xb0, dtype=np.float64)
+        task[b] = lib.evr_lbfgsb_start(runs[b], x0c.ctypes.data, X[b].ctypes.data)
+        nit[b] = nfev[b] = status[b] = 0
+
+    try:
+        for b in range(B):
+            start(b, x0)
+        pending = ctypes.c_int(0)
+        while True:
+            _native.check(lib.evr_mll_fit_rounds(ops._stream(), plan, ctypes.addressof(runs), task.ctypes.data,
+                                                 X.ctypes.data,
+                                                 F.ctypes.data, G.ctypes.data, nit.ctypes.data, nfev.ctypes.data,
+                                                 status.ctypes.data, int(maxiter), int(maxfun), prior.ctypes.data,
+                                                 params.ctypes.data, ctypes.byref(pending)), "evr_mll_fit_rounds")
+            if not pending.value:
+                break
+            idx = [b for b in range(B) if task[b] == LBFGSB_FG]
+            vals = ev(idx, [X[b].copy() for b in idx])
+            for b, v in zip(idx, vals):
+                if v is None:
+                    start(b, restart_x(b))
+                    continue
+                f, g = v
+                F[b] = -f
+                G[b] = -np.asarray(g, dtype=np.float64)
+                _native.check(lib.evr_lbfgsb_advance(runs[b], float(F[b]), G[b].ctypes.data, X[b].ctypes.data,
+                                                     i32(task, b), i32(nit, b), i32(nfev, b), i32(status, b),
+                                                     int(maxiter), int(maxfun)), "evr_lbfgsb_advance")
+        return [X[b].copy() for b in range(B)]
+    finally:
+        for b in range(B):
+            if runs[b]:
+                lib.evr_lbfgsb_destroy(runs[b])
+
+
 def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_prior=(-4.0, 1.0),
               max_attempts: int = 10, seed: int = 0, options: Optional[dict] = None,
               standardize: bool = True) -> List[GPHyper]:
@@ -449,6 +537,20 @@ def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_pr
     rngs = [np.random.default_rng(seed) for _ in range(B)]
     attempts = [0] * B
 
+    def restart_x(b):   # NotPSDError: sample_all_priors, then retry (max_attempts)
+        attempts[b] += 1
+        if attempts[b] >= max_attempts:
+            raise RuntimeError(f"GP fit of output {b} failed after {max_attempts} attempts (NotPSDError)")
+        ls = prior_sample_np(lsp, rngs[b], d) if lsp else np.full(d, math.log(2.0))
+        nz = max(float(prior_sample_np(nzp, rngs[b], 1)[0]) if nzp else 1e-3, MIN_INFERRED_NOISE_LEVEL)
+        return np.concatenate([[nz, 0.0], np.log(np.expm1(ls))])
+
+    if ev.use_plan and os.environ.get("EVR_FIT_NATIVE", "1") != "0":
+        xs = _fit_rounds_native(ev, B, d, np.concatenate([[noise0, 0.0], np.zeros(d)]), lb, ub, maxiter, maxfun,
+                                restart_x)
+        return [GPHyper(lengthscale=softplus_np(xs[b][2:]), noise=float(xs[b][0]), constant=float(xs[b][1]),
+                        y_mean=stats[b][0], y_std=stats[b][1]) for b in range(B)]
+
     def start(x0):
         gen = lbfgsb_steps(x0, lb, ub, maxiter, maxfun)
         return gen, next(gen)
@@ -462,12 +564,7 @@ def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_pr
             gen, _ = runs[b]
             if v is None:        # NotPSDError: sample_all_priors, then retry (max_attempts)
                 gen.close()
-                attempts[b] += 1
-                if attempts[b] >= max_attempts:
-                    raise RuntimeError(f"GP fit of output {b} failed after {max_attempts} attempts (NotPSDError)")
-                ls = prior_sample_np(lsp, rngs[b], d) if lsp else np.full(d, math.log(2.0))
-                nz = max(float(prior_sample_np(nzp, rngs[b], 1)[0]) if nzp else 1e-3, MIN_INFERRED_NOISE_LEVEL)
-                runs[b] = start(np.concatenate([[nz, 0.0], np.log(np.expm1(ls))]))
+                runs[b] = start(restart_x(b))
                 continue
             f, g = v
             try:

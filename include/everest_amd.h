@@ -87,6 +87,28 @@ int evr_mll_plan_create(void* stream, int kind, int B, int n, int d, const doubl
 int evr_mll_plan_eval(void* stream, evr_mll_plan* plan, const double* params, double* out);
 void evr_mll_plan_destroy(evr_mll_plan* plan);
 
+/* The lock-step fit of the plan's B members in native code (gp.fit_batch: one L-BFGS-B per
+ * output over -MLL / n with the gpytorch priors, [upstream] fit_gpytorch_mll ->
+ * scipy L-BFGS-B, bofire/surrogates/single_task_gp.py:70-71).  Member b: runs[b] an
+ * evr_lbfgsb of dimension d + 2 over x = [noise, constant, raw lengthscales (softplus)],
+ * task[b] its current task (EVR_LBFGSB_FG: x[b] is to be evaluated; 0: finished), f / g the
+ * last evaluation it was given, nit / nfev / status as scipy's driver loop counts them
+ * (status 0 converged, 1 iteration / evaluation limit, 2 abnormal line search, 3 error).
+ * params (B x (d + 2), the plan's layout) carries the members' last evaluated parameters
+ * across calls.  prior: ls (fam, a, b), noise (fam, a, b) with fam 0 none, 1 LogNormal,
+ * 2 Gamma, 3 Normal.  Runs rounds (one plan evaluation of every member with task FG, then
+ * each one's L-BFGS-B steps) until every member has finished (*pending = 0), or a round in
+ * which an evaluated member's attempt-0 factor failed or its terms are not finite: then
+ * nothing of that round is consumed and *pending = 1 (the caller evaluates that round
+ * through the jitter ladder and hands the results to evr_lbfgsb_advance). */
+int evr_mll_fit_rounds(void* stream, evr_mll_plan* plan, void** runs, int* task, double* x, double* f, double* g,
+                       int* nit, int* nfev, int* status, int maxiter, int maxfun, const double* prior, double* params,
+                       int* pending);
+/* One member's L-BFGS-B after its evaluation at x (f, g): scipy's driver loop up to the next
+ * evaluation request or the end (the state machine evr_mll_fit_rounds applies). */
+int evr_lbfgsb_advance(void* run, double f, const double* g, double* x, int* task, int* nit, int* nfev,
+                       int* status, int maxiter, int maxfun);
+
 /* ---- dense float64 linear algebra --------------------------------------------------- */
 int evr_gemm_f64(void* stream, int transA, int transB, int M, int N, int K, double alpha,
                  const double* A, int lda, long long strideA, const double* B, int ldb,

@@ -95,3 +95,31 @@ def test_mll_plan_matches_op_chain(kind, monkeypatch):
     if got[0] is not None:
         a, b = got[0][0], want[0][0]
         assert (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-6 * max(1.0, abs(b))
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_native_fit_rounds_match_python_loop(dup, monkeypatch):
+    """gp.fit_batch's lock-step loop in native code (evr_mll_fit_rounds: the plan evaluation,
+    -MLL / n with the priors and the L-BFGS-B steps per round without Python) against the
+    Python generator loop over the same plan: the same optimisation problem and algorithm, so
+    the same optimum (the prior terms' summation order is the only difference).  With
+    duplicated inputs the plain factor of some iterates fails and those rounds take the
+    jitter-ladder path (the native driver hands them back)."""
+    from everest_amd.gp import fit_batch
+
+    rng = np.random.default_rng(21)
+    n, d, m = 90, 4, 3
+    X = rng.uniform(size=(n, d))
+    if dup:
+        X[60:75] = X[:15]
+    Y = dtlz2(X, m) + (0.0 if dup else 0.01) * rng.normal(size=(n, m))
+    Xn = torch.tensor(X, device="cuda")
+    prior = (math.sqrt(2) + 0.5 * math.log(d), math.sqrt(3))
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("EVR_FIT_NATIVE", mode)
+        out[mode] = fit_batch(Xn, Y, 0, prior, (-4.0, 1.0))
+    for a, b in zip(out["1"], out["0"]):
+        assert np.allclose(a.lengthscale, b.lengthscale, rtol=1e-4), (a.lengthscale, b.lengthscale)
+        assert abs(a.noise - b.noise) <= 1e-4 * b.noise + 1e-10
+        assert abs(a.constant - b.constant) <= 1e-4 * max(1.0, abs(b.constant))
