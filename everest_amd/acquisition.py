@@ -271,7 +271,7 @@ class _BoxHviAcqf:
 
     def _use_log_scan(self, tau_relu: float, tau_max: float):
         """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
-        q = 1 affine fast path runs hvi_log.hip (the tabulated keyed kernel over compressed
+        q = 1 affine fast path runs hvi_log.hip (the kd-bounded tabulated kernel over compressed
         cells, the dense kernel over explicit ones), every other case
         (output constraints, CloseToTarget / selected outputs, q > 1, qLogEHVI pending points)
         the general log scan (evr_qlog_eval), both over the explicit cell bounds (compressed
@@ -283,9 +283,9 @@ class _BoxHviAcqf:
         def logify(src):
             st = _native.EvrQnehviState.from_buffer_copy(src)
             st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
-            # compressed cells stay: the q = 1 scan tabulates log fatplus over the point table
-            # (hvi_logk_kernel); the general log scan reads the explicit rows
-            st.grp_off = st.grp_keys = st.grp_rank = st.grp_box = st.sorted_lo = None
+            # compressed cells and their kd groups stay: the q = 1 scan tabulates log fatplus
+            # over the point table and skips the kd groups whose bound is below 2^-60 of the
+            # sample's sum (hvi_logkd_kernel); the general log scan reads the explicit rows
             st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
             return st
         self._log_cells = (lo, hi)

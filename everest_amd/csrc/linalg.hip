@@ -466,6 +466,86 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   }
   return -1;
 }
+#elif !defined(EVR_LEAF_QUAD)
+// Symmetric leaf (default): lane (r, q), r = lane & 15, q = lane >> 4, holds row r of BOTH
+// triangles of the 16x16 block at columns q + 4k, and of the inverse accumulator E.  Keeping
+// the upper triangle lets every exchange of a pivot step stay in VALU cross-lane moves:
+//   the pivot row A[j][c] (= the pivot column by symmetry) and the finished inverse row
+//   E[j][c] sit in lane j of the lane's own 16-lane DPP row (row_newbcast:j, 64-bit DPP);
+//   the lane's own entry A[r][j] sits in DPP row j & 3 at the same r: broadcast to all four
+//   rows by v_permlane32_swap + v_permlane16_swap (two VALU ops per dword);
+//   the pivot by readlane.
+// No LDS round trips (the quad leaf's 16 ds_bpermute per pivot, EVR_LEAF_QUAD build).  Rows
+// r <= j take m = 0 and are left as they are, so no per-entry masks: the eliminated column j
+// of rows below keeps a rounding residue that only ever updates itself (its L entries are
+// read from the upper triangle instead: row j of the upper triangle is final after step
+// j - 1 and equals the unnormalised column j, L[c][j] d_j^1/2 = A[j][c]); E[j][c] is zero for
+// c > j and one at c = j.  The results differ from the quad leaf by rounding only (the
+// upper-triangle operands are other roundings of the same values).
+__device__ __forceinline__ double xrow_bcast_f64(double v, int R) {   // DPP row R -> all rows
+  const long long x = __double_as_longlong(v);
+  unsigned d[2] = {(unsigned)x, (unsigned)(x >> 32)};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto t = __builtin_amdgcn_permlane32_swap(d[h], d[h], false, false);   // [0 1 0 1] | [2 3 2 3]
+    const unsigned u = (R >> 1) ? t[1] : t[0];
+    const auto w = __builtin_amdgcn_permlane16_swap(u, u, false, false);          // [0 0 2 2] | [1 1 3 3]
+    d[h] = (R & 1) ? w[1] : w[0];
+  }
+  return __longlong_as_double(((long long)d[1] << 32) | d[0]);
+}
+
+__device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
+                                              double* erow, double* piv) {
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  double a[4], e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = q + 4 * k;
+    a[k] = (c <= r) ? A[c0 + r][c0 + c] : A[c0 + c][c0 + r];
+    e[k] = (c == r) ? 1.0 : 0.0;
+  }
+  int bad = -1;
+#pragma unroll
+  for (int j = 0; j < CP; ++j) {
+    const double p = readlane_f64(a[j >> 2], j + 16 * (j & 3));   // A[j][j]
+    const double arj = xrow_bcast_f64(a[j >> 2], j & 3);           // A[r][j]
+    double aj[4], ej[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      aj[k] = row_bcast_f64(a[k], j);                              // A[j][q + 4k]
+      ej[k] = row_bcast_f64(e[k], j);                              // E[j][q + 4k]
+    }
+    if (!(p > 0.0)) {
+      bad = j;
+      break;
+    }
+    if (lane == 0) piv[j] = p;
+    double ip = __builtin_amdgcn_rcp(p);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    ip = fma(ip, fma(-p, ip, 1.0), ip);
+    const double m = (r > j) ? arj * ip : 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = fma(-m, aj[k], a[k]);
+      e[k] = fma(-m, ej[k], e[k]);
+    }
+  }
+  (void)colj;
+  (void)erow;
+  if (bad >= 0) return bad;
+  lds_wave_sync();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = q + 4 * k;
+    if (c >= r) {   // upper entry (r, c): L[c][r] = A[r][c] / d_r^1/2 (c = r: the diagonal)
+      A[c0 + c][c0 + r] = a[k] / sqrt(piv[r]);
+      if (c > r) A[c0 + r][c0 + c] = 0.0;
+    }
+    X[c0 + r][c0 + c] = (c <= r) ? e[k] / sqrt(piv[r]) : 0.0;
+  }
+  return -1;
+}
 #else
 // Lane (row r, quad q) holds A[r][q + 4k].  Per pivot step the pivot comes by readlane (a
 // uniform scalar: its reciprocal starts at once and the failure test is a scalar branch),
@@ -847,9 +927,67 @@ __device__ __forceinline__ void put_quadrant(double (*T)[BNB + 1], int wr, int w
       for (int r = 0; r < 4; ++r) T[wr + bi * 16 + rq + 4 * r][wc + bj * 16 + col] = acc[bi][bj][r];
 }
 
+// quadrant of the 64x64 product P Q (both row-major LDS tiles)
+__device__ __forceinline__ void mm64_nn(const double (*P)[BNB + 1], const double (*Q)[BNB + 1], int wr, int wc,
+                                        double4_t (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+  for (int kk = 0; kk < BNB; kk += 4) {
+    const double a0 = P[wr + i][kk + kq], a1 = P[wr + 16 + i][kk + kq];
+    const double b0 = Q[kk + kq][wc + i], b1 = Q[kk + kq][wc + 16 + i];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+}
+
+// Inverse tile of the fused sweep (chol_step_kernel, blockIdx beyond the trailing tiles):
+// X = L^-1 is formed right-looking on the identity alongside the factorisation.  With
+// B_ij = delta_ij I - sum_{s<i} L_is X_sj, the block row X_k = Dinv_k B_k is complete once
+// step k - 1 has run, so step k applies B_ij -= L_ik (Dinv_k B_kj) to every i > k, j <= k
+// (B_kk = I: the product is L_ik Dinv_k, the tile's first write).  L_ik = A_ik Dinv_k^T is
+// recomputed from the un-normalised panel like the trailing tiles do; B lives in X and
+// chol_final_kernel turns it into X_kj = Dinv_k B_kj.  The step's critical path is the next
+// diagonal block's factor, which these tiles run beside.
+__device__ __forceinline__ void chol_inv_tile(int n, int k, int i, int j, const double* L, int ldl, const double* Dk,
+                                              double* X, int ldx, double (*TI)[BNB + 1], double (*TJ)[BNB + 1],
+                                              double (*TD)[BNB + 1]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
+  const int r0 = i * BNB, c0 = j * BNB, p0 = k * BNB;
+  load_tile64(TI, L, ldl, n, r0, p0);                 // A_ik
+  if (j < k) load_tile64(TJ, X, ldx, n, p0, c0);      // B_kj
+  load_dinv64(TD, Dk);
+  __syncthreads();
+  double4_t pi[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  double4_t xk[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  mm64_nt(TI, TD, wr, wc, pi);                        // L_ik
+  if (j < k) mm64_nn(TD, TJ, wr, wc, xk);             // X_kj = Dinv_k B_kj
+  __syncthreads();
+  put_quadrant(TI, wr, wc, pi);
+  if (j < k) put_quadrant(TJ, wr, wc, xk);
+  __syncthreads();
+  double4_t u[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+  mm64_nn(TI, j < k ? TJ : TD, wr, wc, u);
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
+        if (row < n && cc < n) {
+          double* o = X + (size_t)row * ldx + cc;
+          *o = (j < k) ? *o + (-1.0) * u[bi][bj][r] : -u[bi][bj][r];
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void chol_step_kernel(int n, int k, double* __restrict__ Lm, long long sL, int ldl,
                                                         double* __restrict__ Dinv, long long sD,
-                                                        int* __restrict__ info) {
+                                                        int* __restrict__ info, int ntrail, double* __restrict__ Xm,
+                                                        long long sX, int ldx) {
   const int b = blockIdx.y;
   if (info[b]) return;
   double* L = Lm + b * sL;
@@ -860,6 +998,12 @@ __global__ __launch_bounds__(256) void chol_step_kernel(int n, int k, double* __
   __shared__ int fail;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
+  if ((int)blockIdx.x >= ntrail) {   // inverse tile (i > k, j <= k) of the fused sweep
+    const int t = blockIdx.x - ntrail;
+    chol_inv_tile(n, k, k + 1 + t / (k + 1), t % (k + 1), L, ldl, Dinv + b * sD + (size_t)k * BNB * BNB,
+                  Xm + b * sX, ldx, TI, TJ, TD);
+    return;
+  }
   int I = 0, J = 0;   // trailing tile (lower, row-major enumeration)
   {
     const int t = blockIdx.x;
@@ -933,23 +1077,61 @@ __global__ __launch_bounds__(256) void chol_step_kernel(int n, int k, double* __
   store_diag64(TI, TJ, nb, L, ldl, r0, Dinv + b * sD + (size_t)(k + 1) * BNB * BNB);
 }
 
-// off-diagonal tiles (I > K): L_IK = A_IK Dinv_K^T in place
+// off-diagonal tiles (I > K): L_IK = A_IK Dinv_K^T in place; with X (the fused inverse),
+// workgroups beyond the panel tiles finish X: tile (k, j) = Dinv_k B_kj below the diagonal
+// block, Dinv_k on it, zero above (a failed member: Dinv_k on the diagonal, zeros elsewhere)
 __global__ __launch_bounds__(256) void chol_panel_kernel(int n, double* __restrict__ Lm, long long sL, int ldl,
                                                          const double* __restrict__ Dinv, long long sD,
-                                                         const int* __restrict__ info) {
+                                                         const int* __restrict__ info, int npanel,
+                                                         double* __restrict__ Xm, long long sX, int ldx) {
   const int b = blockIdx.y;
-  if (info[b]) return;
-  double* L = Lm + b * sL;
   __shared__ double TA[BNB][BNB + 1];
   __shared__ double TD[BNB][BNB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
+  if ((int)blockIdx.x >= npanel) {
+    const int nblk = (n + BNB - 1) / BNB, t = blockIdx.x - npanel, K = t / nblk, J = t % nblk;
+    double* X = Xm + b * sX;
+    const double* Dk = Dinv + b * sD + (size_t)K * BNB * BNB;
+    if (J > K || (J < K && info[b])) {
+      for (int e = tid; e < BNB * BNB; e += 256) {
+        const int row = K * BNB + (e >> 6), cc = J * BNB + (e & 63);
+        if (row < n && cc < n) X[(size_t)row * ldx + cc] = 0.0;
+      }
+      return;
+    }
+    if (J == K) {
+      for (int e = tid; e < BNB * BNB; e += 256) {
+        const int row = K * BNB + (e >> 6), cc = K * BNB + (e & 63);
+        if (row < n && cc < n) X[(size_t)row * ldx + cc] = Dk[e];
+      }
+      return;
+    }
+    load_tile64(TA, X, ldx, n, K * BNB, J * BNB);   // B_KJ
+    load_dinv64(TD, Dk);
+    __syncthreads();
+    double4_t p[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
+    mm64_nn(TD, TA, wr, wc, p);
+    __syncthreads();   // every wave has read TA before the stores overwrite its source rows
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = K * BNB + wr + bi * 16 + rq + 4 * r, cc = J * BNB + wc + bj * 16 + col;
+          if (row < n && cc < n) X[(size_t)row * ldx + cc] = p[bi][bj][r];
+        }
+    return;
+  }
+  if (info[b]) return;
+  double* L = Lm + b * sL;
   int I = 1, K = 0;
   {
     const int t = blockIdx.x;   // strictly lower tiles, row-major: row I has I tiles
     while (I * (I + 1) / 2 <= t) ++I;
     K = t - I * (I - 1) / 2;
   }
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
   load_tile64(TA, L, ldl, n, I * BNB, K * BNB);
   load_dinv64(TD, Dinv + b * sD + (size_t)K * BNB * BNB);
   __syncthreads();
@@ -1432,7 +1614,15 @@ static size_t chol_dinv_doubles(int batch, int n) {
   return (size_t)batch * nblk * BNB * BNB + ((size_t)batch * nblk + 1) / 2;
 }
 
-int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long sL, double* Dinv, int* info) {
+// the fused right-looking variant forms X = L^-1 in the same launches (n <= 1024;
+// EVR_TRIINV=sep: the separate triangular inverse after the factorisation, A/B)
+static bool chol_inv_fused(int n) {
+  const char* tv = std::getenv("EVR_TRIINV");   // read per call: tests switch it
+  return chol_variant() == 1 && n <= 1024 && !(tv && tv[0]);
+}
+
+int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long sL, double* Dinv, int* info,
+                 double* X = nullptr, int ldx = 0, long long sX = 0) {
   const int nblk = (n + BNB - 1) / BNB;
   const long long sD = (long long)nblk * BNB * BNB;
   if (chol_variant() == 0) {
@@ -1450,11 +1640,14 @@ int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long 
     for (int k = -1; k < nblk - 1; ++k) {
       const int T = nblk - 1 - k;   // trailing tile rows (block 0 alone for k = -1)
       const int tiles = k < 0 ? 1 : T * (T + 1) / 2;
-      chol_step_kernel<<<dim3(tiles, batch), 256, 0, s>>>(n, k, L, sL, ldl, Dinv, sD, info);
+      const int itiles = (X && k >= 0) ? (nblk - 1 - k) * (k + 1) : 0;
+      chol_step_kernel<<<dim3(tiles + itiles, batch), 256, 0, s>>>(n, k, L, sL, ldl, Dinv, sD, info, tiles, X, sX,
+                                                                   ldx);
       EVR_LAUNCH_CHECK();
     }
-    if (nblk > 1) {
-      chol_panel_kernel<<<dim3(nblk * (nblk - 1) / 2, batch), 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, info);
+    const int npanel = nblk * (nblk - 1) / 2, nx = X ? nblk * nblk : 0;
+    if (npanel + nx > 0) {
+      chol_panel_kernel<<<dim3(npanel + nx, batch), 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, info, npanel, X, sX, ldx);
       EVR_LAUNCH_CHECK();
     }
     return 0;
@@ -1538,13 +1731,14 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
   std::vector<double> jit(batch, 0.0);
   std::vector<int> info(batch, 0);
   int rc = 0;
+  const bool fused = Linv && chol_inv_fused(n);
   for (int t = 0; t <= max_tries; ++t) {
     EVR_HIP(hipMemcpyAsync(jit_d, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
     EVR_HIP(hipMemsetAsync(info_d, 0, sizeof(int) * batch, s));
     dim3 g1(cdiv((long long)n * n, 256), batch);
     chol_init_kernel<<<g1, 256, 0, s>>>(n, A, sA, lda, L, sL, ldl, jit_d);
     EVR_LAUNCH_CHECK();
-    if ((rc = chol_blocked(s, batch, n, L, ldl, sL, Dinv, info_d))) break;
+    if ((rc = chol_blocked(s, batch, n, L, ldl, sL, Dinv, info_d, fused ? Linv : nullptr, ldi, sI))) break;
     EVR_HIP(hipMemcpyAsync(info.data(), info_d, sizeof(int) * batch, hipMemcpyDeviceToHost, s));
     EVR_HIP(hipStreamSynchronize(s));
     bool anyfail = false;
@@ -1555,7 +1749,7 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
       }
     if (!anyfail || t == max_tries) break;
   }
-  if (!rc && Linv) rc = tri_inv_blocked(s, batch, n, L, ldl, sL, Dinv, Linv, ldi, sI, T, info_d);
+  if (!rc && Linv && !fused) rc = tri_inv_blocked(s, batch, n, L, ldl, sL, Dinv, Linv, ldi, sI, T, info_d);
   if (!rc) {
     if (jitter_used) EVR_HIP(hipMemcpyAsync(jitter_used, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
     if (info_out) EVR_HIP(hipMemcpyAsync(info_out, info_d, sizeof(int) * batch, hipMemcpyDeviceToDevice, s));
@@ -1575,8 +1769,10 @@ int chol_inverse_attempt(hipStream_t s, int batch, int n, const double* A, doubl
   dim3 g1(cdiv((long long)n * n, 256), batch);
   chol_init_kernel<<<g1, 256, 0, s>>>(n, A, (long long)n * n, n, L, (long long)n * n, n, jit_d);
   EVR_LAUNCH_CHECK();
-  if (int rc = chol_blocked(s, batch, n, L, n, (long long)n * n, Dinv, info_d)) return rc;
-  return tri_inv_blocked(s, batch, n, L, n, (long long)n * n, Dinv, Linv, n, (long long)n * n, T, info_d);
+  const long long nn = (long long)n * n;
+  if (chol_inv_fused(n)) return chol_blocked(s, batch, n, L, n, nn, Dinv, info_d, Linv, n, nn);
+  if (int rc = chol_blocked(s, batch, n, L, n, nn, Dinv, info_d)) return rc;
+  return tri_inv_blocked(s, batch, n, L, n, nn, Dinv, Linv, n, nn, T, info_d);
 }
 
 size_t chol_inverse_dinv_doubles(int batch, int n) { return chol_dinv_doubles(batch, n); }

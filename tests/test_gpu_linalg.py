@@ -265,7 +265,7 @@ def test_tri_inv_col_bitwise_equals_row_kernel(n, monkeypatch):
     g = torch.Generator().manual_seed(n + 11)
     A = torch.randn(5, n, n + 3, generator=g, dtype=torch.float64)
     A = _t(A @ A.transpose(1, 2) / n + 1e-2 * torch.eye(n, dtype=torch.float64))
-    monkeypatch.delenv("EVR_TRIINV", raising=False)
+    monkeypatch.setenv("EVR_TRIINV", "col")
     L, Li, _, info = ops.cholesky_inverse(A)
     monkeypatch.setenv("EVR_TRIINV", "row")
     L0, Li0, _, info0 = ops.cholesky_inverse(A)
@@ -275,3 +275,27 @@ def test_tri_inv_col_bitwise_equals_row_kernel(n, monkeypatch):
     Lc = L.cpu()
     eye = torch.eye(n, dtype=torch.float64).expand(5, n, n)
     assert torch.allclose(Li.cpu() @ Lc, eye, atol=1e-8)
+
+
+@pytest.mark.parametrize("n", [16, 64, 65, 130, 280, 512, 513, 1024])
+def test_fused_inverse_matches_separate(n, monkeypatch):
+    """The inverse formed right-looking inside the Cholesky launches (B_ij -= L_ik Dinv_k B_kj
+    beside each step's trailing tiles, X_kj = Dinv_k B_kj at the end): the factor is bitwise
+    the separate path's, the inverse agrees to rounding (another summation order) and has
+    the zero upper triangle; ragged n included."""
+    from everest_amd import ops
+
+    g = torch.Generator().manual_seed(n + 29)
+    A = torch.randn(5, n, n + 3, generator=g, dtype=torch.float64)
+    A = _t(A @ A.transpose(1, 2) / n + 1e-2 * torch.eye(n, dtype=torch.float64))
+    monkeypatch.delenv("EVR_TRIINV", raising=False)
+    L, Li, _, info = ops.cholesky_inverse(A)
+    monkeypatch.setenv("EVR_TRIINV", "col")
+    L0, Li0, _, info0 = ops.cholesky_inverse(A)
+    assert info.cpu().eq(0).all() and info0.cpu().eq(0).all()
+    assert torch.equal(L, L0)
+    err = float((Li - Li0).abs().max() / Li0.abs().max())
+    assert err <= 1e-12, err
+    assert torch.equal(torch.triu(Li, 1), torch.zeros_like(Li))
+    eye = torch.eye(n, dtype=torch.float64).expand(5, n, n)
+    assert torch.allclose(Li.cpu() @ L.cpu(), eye, atol=1e-8)

@@ -232,23 +232,34 @@ def test_mobo_default_constrained_ask_joint_batch():
 
 @pytest.mark.parametrize("m,prune", [(2, False), (3, True), (5, True)])
 def test_qlog_keyed_scan_matches_dense(m, prune, monkeypatch):
-    """The tabulated scan over compressed cells (hvi_logk_kernel: log fatplus once per
-    (candidate, objective, point), lam once per cell) against the dense kernel over the same
-    cells expanded to explicit rows (EVR_LOG=dense): equal up to the summation order of the
-    online log-sum-exp; forward-only and fused forward + backward plans agree bitwise."""
+    """The kd-bounded tabulated scan (hvi_logkd_kernel: groups whose bound is below 2^-60 of
+    the sample's sum skipped), the unbounded one over every compressed cell (EVR_LOG=keyed:
+    hvi_logk_kernel) and the dense kernel over the same cells expanded to explicit rows
+    (EVR_LOG=dense): equal up to the summation order of the online log-sum-exp (the skipped
+    mass is < 2^-60 relative); forward-only and fused forward + backward plans agree bitwise."""
     X, lo, hi, orc, dq = _matched(48, 4, m, 32, seed=3 + m, prune=prune)
-    assert dq.cells.keys is not None and dq.state.cell_keys
+    assert dq.cells.keys is not None and dq.state.cell_keys and dq.state.grp_off
     rng = np.random.default_rng(m)
+
+    def run(mode):
+        if mode:
+            monkeypatch.setenv("EVR_LOG", mode)
+        else:
+            monkeypatch.delenv("EVR_LOG", raising=False)
+        dq._plans = {}
+        a, g = dq.forward_backward(Xc)
+        f = dq.forward(Xc)
+        monkeypatch.delenv("EVR_LOG", raising=False)
+        dq._plans = {}
+        return a, g, f
+
     for b in (1, 5, 20, 67):
         Xc = torch.tensor(lo + (hi - lo) * rng.uniform(size=(b, 4)), device="cuda")
-        dq._plans = {}
-        a_k, g_k = dq.forward_backward(Xc)
-        f_k = dq.forward(Xc)
-        monkeypatch.setenv("EVR_LOG", "dense")
-        dq._plans = {}
-        a_d, g_d = dq.forward_backward(Xc)
-        monkeypatch.delenv("EVR_LOG")
-        dq._plans = {}
-        assert torch.allclose(a_k, a_d, rtol=1e-12, atol=1e-12), (a_k - a_d).abs().max()
-        assert torch.allclose(g_k, g_d, rtol=1e-10, atol=1e-12 * g_d.abs().max()), (g_k - g_d).abs().max()
+        a_b, g_b, f_b = run(None)
+        a_k, g_k, f_k = run("keyed")
+        a_d, g_d, _ = run("dense")
+        for a, g in ((a_b, g_b), (a_k, g_k)):
+            assert torch.allclose(a, a_d, rtol=1e-12, atol=1e-12), (a - a_d).abs().max()
+            assert torch.allclose(g, g_d, rtol=1e-10, atol=1e-12 * g_d.abs().max()), (g - g_d).abs().max()
         assert torch.equal(f_k, a_k)
+        assert torch.equal(f_b, a_b)

@@ -1,7 +1,7 @@
 // Phase profile of the 64x64 diagonal-block factor (factor_diag64) with the EVR_CHOL_PROF
 // cycle counters of linalg.hip: one workgroup per launch, many launches; prints average
 // core-clock cycles per phase.  Build: hipcc --offload-arch=gfx950 -O3 -DEVR_CHOL_PROF
-//   tools/chol_prof.hip -o tools/_chol_prof
+//   tools/chol_prof.hip everest_amd/csrc/gemm.hip -o tools/_chol_prof
 #include <cstdio>
 #include <cstring>
 #include <vector>

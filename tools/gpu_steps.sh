@@ -20,12 +20,13 @@
 #   sq20        SQ wave-cycle split of the restart chain kernels (hvi_kdw, qs_fwd, qs_bwd) at b = 20
 #   kdwaves     per-wave phase stamps of hvi_kd3 / hvi_kdb (EVR_KD_PROF=2 build in _libprof/)
 #   kdwwaves    per-(sample, candidate) phase stamps of hvi_kdw (EVR_KD_PROF=2 build in _libkdprof/)
+#   qlogab      tools/qlog_ab.py (qLogNEHVI scan: kd-bounded vs unbounded keyed) -> <tag>/qlog_ab.json
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
-#   cholprof    phase cycles + result digest of the 64x64 diagonal factor, DPP leaf vs the
-#               two-pivot bpermute leaf (tools/_chol_prof_{dpp,pair}: hipcc --offload-arch=gfx950 -O3
-#               -DEVR_CHOL_PROF [-DEVR_LEAF_DPP] tools/chol_prof.hip -o ...)
+#   cholprof    phase cycles + result digest of the 64x64 diagonal factor, the symmetric
+#               permlane/DPP leaf vs the two-pivot bpermute quad leaf (tools/_chol_prof_{sym,pair}:
+#               hipcc --offload-arch=gfx950 -O3 -DEVR_CHOL_PROF [-DEVR_LEAF_QUAD] tools/chol_prof.hip everest_amd/csrc/gemm.hip -o ...)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -50,6 +51,7 @@ for st in "$@"; do
     asktl)
       run asktl_trace 300 rocprofv3 --kernel-trace -d "$OUT/asktl" -o run --output-format csv -- python tools/ask_timeline.py
       run asktl_parse 60 python tools/ask_timeline.py --analyse "$OUT/asktl" "$OUT/asktl_trace.log" && cp "$OUT/asktl_parse.log" "$OUT/ask_timeline.json" ;;
+    qlogab) run qlogab 300 python tools/qlog_ab.py && cp "$OUT/qlogab.log" "$OUT/qlog_ab.json" ;;
     planprobe) run planprobe 300 python tools/plan_setup_probe.py ;;
     hostprof) run hostprof 300 python tools/ask_host_profile.py ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
@@ -74,7 +76,7 @@ for st in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
     cholprof)
-      run cholprof_dpp 60 tools/_chol_prof_dpp
+      run cholprof_sym 60 tools/_chol_prof_sym
       run cholprof_pair 60 tools/_chol_prof_pair ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

@@ -1,0 +1,47 @@
+"""A/B of the qLogNEHVI scan at the bench state (DTLZ2 n = 512, d = 6, m = 5, S = 256): the
+kd-bounded tabulated kernel (default) against the unbounded keyed scan (EVR_LOG=keyed),
+forward + backward at b = 512 and b = 20, plus the largest |difference| of values and
+gradients between the two.  Prints one JSON object.
+
+usage: python tools/qlog_ab.py"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import bench
+    from everest_amd.acquisition import QLogNEHVI
+
+    dev = torch.device("cuda", 0)
+    X, Y, gp, hypers, acqf, _, _ = bench.build_state(512, 6, 5, 256, dev)
+    del acqf
+    qa = QLogNEHVI(gp, X, X, -1.1 * np.ones(5), -np.ones(5), np.zeros(5), S=256, sampler_seed=1234,
+                   prune_baseline=True, prune_seed=4321)
+    out = {"cells_total": qa.stats.total_cells, "box_decomposition": qa.box_path,
+           "kd": bool(qa.state.grp_off)}
+    res = {}
+    for mode in ("bounded", "keyed"):
+        if mode == "keyed":
+            os.environ["EVR_LOG"] = "keyed"
+        qa._plans = {}
+        for b in (512, 20):
+            Xc = bench.candidates(b, 6, seed=3, device=dev)
+            a, g = qa.forward_backward(Xc)
+            res[(mode, b)] = (a.clone(), g.clone())
+            out[f"{mode}_b{b}_ms"] = round(bench._event_ms(lambda: qa.forward_backward(Xc), reps=10), 4)
+        os.environ.pop("EVR_LOG", None)
+    for b in (512, 20):
+        (a0, g0), (a1, g1) = res[("bounded", b)], res[("keyed", b)]
+        out[f"b{b}_max_abs_dacq"] = float((a0 - a1).abs().max())
+        out[f"b{b}_max_rel_dgrad"] = float(((g0 - g1).abs().amax(1) / g1.abs().amax(1).clamp_min(1e-300)).max())
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
