@@ -810,16 +810,17 @@ def main():
 
         qa = QLogNEHVI(gp, X, X, -1.1 * np.ones(args.m), -np.ones(args.m), np.zeros(args.m), S=args.S,
                        sampler_seed=1234, prune_baseline=True, prune_seed=4321)
-        qlog = {"note": "qLogNEHVI forward + backward (fat-smoothed log scan; kd groups whose bound is below "
-                        "2^-60 of the sample's sum skipped), same GPs and seeds as eval_pass; device time between "
-                        "HIP events incl. any host syncs; *_unbounded_ms: EVR_LOG=keyed (every cell, A/B)",
+        qlog = {"note": "qLogNEHVI forward + backward (tabulated fat-smoothed log scan over every compressed "
+                        "cell), same GPs and seeds as eval_pass; device time between HIP events incl. any host "
+                        "syncs; *_kd_ms: EVR_LOG=kd (kd groups whose bound is below 2^-60 of the sample's sum "
+                        "skipped, A/B)",
                 "cells_total": qa.stats.total_cells, "box_decomposition": qa.box_path}
         for bb, XX in ((args.b, Xc), (b_r, Xr)):
             qlog[f"b{bb}_ms"] = round(_event_ms(lambda: qa.forward_backward(XX), reps=10), 4)
-        os.environ["EVR_LOG"] = "keyed"
+        os.environ["EVR_LOG"] = "kd"
         qa._plans = {}
         try:
-            qlog[f"b{args.b}_unbounded_ms"] = round(_event_ms(lambda: qa.forward_backward(Xc), reps=5), 4)
+            qlog[f"b{args.b}_kd_ms"] = round(_event_ms(lambda: qa.forward_backward(Xc), reps=5), 4)
         finally:
             del os.environ["EVR_LOG"]
             qa._plans = {}

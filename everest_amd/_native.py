@@ -141,6 +141,7 @@ _SIGS = {
     "evr_mll_plan_destroy": ([c_void_p], None),
     "evr_mll_fit_rounds": ([c_void_p, c_void_p, c_void_p] + [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p,
                                                                              c_void_p], c_int),
+    "evr_mll_assemble": ([c_int, c_int, c_int] + [c_void_p] * 6, c_int),
     "evr_lbfgsb_advance": ([c_void_p, c_double] + [c_void_p] * 6 + [c_int, c_int], c_int),
     "evr_qnehvi_plan_eval_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "evr_qnehvi_plan_destroy": ([c_void_p], None),

@@ -393,7 +393,7 @@ __global__ __launch_bounds__(HLK_THREADS) void hvi_logk_kernel(int b, int nsplit
 // B_g < A - 60 ln 2 - log(16 G): the skipped mass is below 2^-60 of the sample's sum.  The
 // threshold depends on (sample, candidate) alone — not on the split, the batch or thread
 // timing — and the surviving groups are compacted in kd order by a ballot prefix scan, so the
-// result is deterministic.  EVR_LOG=keyed keeps the unbounded keyed scan (A/B, parity).
+// result is deterministic.  Opt-in (EVR_LOG=kd, see hl_kd): measured slower at the bench state.
 constexpr double HLKD_SKIP_LOG = 41.58883083359671856;   // 60 ln 2
 constexpr int HLKD_MAXG = 512;                           // cells_kd.hip KD_MAX_CELLS / 16
 constexpr unsigned short HLKD_PAD = 0x7FFF;
@@ -653,10 +653,13 @@ static bool hl_keyed(const evr_qnehvi_state* st, bool bwd) {
          hlk_lds_bytes(st->pts_stride, st->m, bwd ? hlk_ct_bwd() : HLK_CT_FWD, bwd) <= 150 * 1024;
 }
 
-// the kd-bounded scan: compressed cells with kd groups (EVR_LOG=keyed: the unbounded keyed scan)
+// the kd-bounded scan, opt-in (EVR_LOG=kd): compressed cells with kd groups.  Measured slower
+// than the unbounded keyed scan at the bench state (10.3 vs 9.4 ms at b = 512, profiles/r05/m:
+// with tau_relu = 1e-6 a cell above y in one objective still lies within 2^-60 of the maximum,
+// so few groups fall below the bound)
 static bool hl_kd(const evr_qnehvi_state* st, bool bwd) {
   const char* e = std::getenv("EVR_LOG");   // read per plan (tests switch it)
-  if (e && !std::strcmp(e, "keyed")) return false;
+  if (!e || std::strcmp(e, "kd")) return false;
   return st->grp_off && st->grp_keys && st->grp_rank && st->grp_box && st->sorted_lo && st->max_groups >= 0 &&
          st->max_groups <= HLKD_MAXG &&
          hlkd_lds_bytes(st->pts_stride, st->m, bwd ? hlk_ct_bwd() : HLK_CT_FWD, bwd, st->max_groups) <=

@@ -141,6 +141,7 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
 // applies the kernel, outputscale and diagonal add, and streams the tile out: the f64 VALU
 // distance loop of kmat_kernel (2 flop per coordinate per entry) was the bound at d = 32.
 using kd4_t = __attribute__((ext_vector_type(4))) double;
+using kd2_t = __attribute__((ext_vector_type(2))) double;
 
 template <int DP, int KIND, int EPI>
 __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
@@ -286,6 +287,26 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
 #pragma unroll
     for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[4 * q + r];
   __syncthreads();
+  if (EPI == 3) {
+    // 16 bytes per lane: a store instruction writes two 512-byte row segments (lanes 0-31 row
+    // rr, lanes 32-63 row rr + 1; the plain fill of the config-5 output runs at 4.8 TB/s this
+    // way vs 4.3 TB/s with 8 bytes per lane, tools/micro/fill_probe.hip)
+    const int c2 = 2 * (lane & 31), gj2 = j0 + c2;
+#pragma unroll 4
+    for (int rr = 2 * wave + (lane >> 5); rr < KT; rr += 8) {
+      const int gi = i0 + rr;
+      if (gi >= n1) continue;
+      double* o = Kb + (size_t)gi * n2 + gj2;
+      const double v0 = T[rr][c2], v1 = T[rr][c2 + 1];
+      if (gj2 + 1 < n2 && (((uintptr_t)o) & 15) == 0) {
+        *reinterpret_cast<kd2_t*>(o) = kd2_t{v0, v1};
+      } else {
+        if (gj2 < n2) o[0] = v0;
+        if (gj2 + 1 < n2) o[1] = v1;
+      }
+    }
+    return;
+  }
   const int gj = j0 + lane;
 #pragma unroll 4
   for (int rr = wave; rr < KT; rr += 4) {
@@ -1123,10 +1144,10 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
       EVR_LAUNCH_CHECK();
       return 0;
     }
-    static const int epi = [] {   // EVR_KMAT_EPI: 0 direct D-layout stores, 1 LDS rows, 2 + non-temporal
-      const char* e = getenv("EVR_KMAT_EPI");
+    static const int epi = [] {   // EVR_KMAT_EPI: 0 direct D-layout stores, 1 LDS rows, 2 + non-temporal,
+      const char* e = getenv("EVR_KMAT_EPI");   // 3 LDS rows with 16-byte stores
       const int v = e ? atoi(e) : 0;
-      return (v >= 0 && v <= 2) ? v : 0;
+      return (v >= 0 && v <= 3) ? v : 0;
     }();
 #define KMK(DP_, K_)                                                                                          \
   if (epi == 0)                                                                                               \
@@ -1135,8 +1156,11 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
   else if (epi == 1)                                                                                          \
     kmat_mfma_kernel<DP_, K_, 1><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
                                                       lengthscales, outputscale, diag_add, K);                 \
-  else                                                                                                        \
+  else if (epi == 2)                                                                                          \
     kmat_mfma_kernel<DP_, K_, 2><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                      lengthscales, outputscale, diag_add, K);                 \
+  else                                                                                                        \
+    kmat_mfma_kernel<DP_, K_, 3><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
                                                       lengthscales, outputscale, diag_add, K)
 #define KM(DP_)                         \
   if (kind == RBF) KMK(DP_, RBF);           \

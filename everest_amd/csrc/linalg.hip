@@ -466,8 +466,9 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   }
   return -1;
 }
-#elif !defined(EVR_LEAF_QUAD)
-// Symmetric leaf (default): lane (r, q), r = lane & 15, q = lane >> 4, holds row r of BOTH
+#elif defined(EVR_LEAF_SYM)
+// Symmetric leaf (EVR_LEAF_SYM build; measured slower than the paired quad leaf — 34.9 k vs
+// 32.8 k cycles for the four leaves of a 64-column factor, tools/chol_prof.hip, profiles/r05/m): lane (r, q), r = lane & 15, q = lane >> 4, holds row r of BOTH
 // triangles of the 16x16 block at columns q + 4k, and of the inverse accumulator E.  Keeping
 // the upper triangle lets every exchange of a pivot step stay in VALU cross-lane moves:
 //   the pivot row A[j][c] (= the pivot column by symmetry) and the finished inverse row

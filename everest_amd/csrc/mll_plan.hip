@@ -322,9 +322,52 @@ double softplus(double v) {   // numpy logaddexp(0, v)
   if (v == 0.0) return M_LN2;
   return v > 0.0 ? v + std::log1p(std::exp(-v)) : std::log1p(std::exp(v));
 }
+
+
+// -MLL / n's pieces for one member: ll / n and its gradient in x = [noise, constant, raw
+// lengthscales] (ExactMarginalLogLikelihood with the hyperparameter priors, divided by n as
+// fit_gpytorch_mll's closure does) from the plan's terms (logdet, r.alpha, tr K^-1, sum alpha,
+// sum alpha^2) and lengthscale-gradient pieces gls; ls = softplus(raw).  Shared by the native
+// round driver and gp.MLLBatch (evr_mll_assemble), so both drivers see the same bits.
+void mll_assemble_one(int n, int d, const double* prior, const double* xb, const double* t, const double* gls,
+                      double* llo, double* gout) {
+  const int lf = (int)prior[0], nzf = (int)prior[3];
+  const double logdet = t[0], quad = t[1], trKinv = t[2], sum_a = t[3], sum_a2 = t[4];
+  double ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * std::log(2.0 * M_PI);
+  double d_noise = 0.5 * (sum_a2 - trKinv);
+  const double d_const = sum_a;
+  const double noise = xb[0];
+  if (lf) {
+    double s = 0.0;
+    for (int j = 0; j < d; ++j) s += prior_logpdf(lf, prior[1], prior[2], softplus(xb[2 + j]));
+    ll += s;
+  }
+  if (nzf) {
+    ll += prior_logpdf(nzf, prior[4], prior[5], noise);
+    d_noise += prior_dlogpdf(nzf, prior[4], prior[5], noise);
+  }
+  gout[0] = d_noise / n;
+  gout[1] = d_const / n;
+  for (int j = 0; j < d; ++j) {
+    const double lsj = softplus(xb[2 + j]);
+    double dl = 0.5 * gls[j];
+    if (lf) dl += prior_dlogpdf(lf, prior[1], prior[2], lsj);
+    gout[2 + j] = dl * (1.0 / (1.0 + std::exp(-xb[2 + j]))) / n;
+  }
+  *llo = ll / n;
+}
 }  // namespace
 
 extern "C" {
+
+int evr_mll_assemble(int B, int n, int d, const double* prior, const double* x, const double* terms,
+                     const double* gls, double* ll, double* g) {
+  EVR_CHECK(B >= 0 && n >= 1 && d >= 1 && prior && x && terms && gls && ll && g, "evr_mll_assemble: bad arguments");
+  for (int b = 0; b < B; ++b)
+    mll_assemble_one(n, d, prior, x + (size_t)b * (d + 2), terms + (size_t)b * 5, gls + (size_t)b * d, ll + b,
+                     g + (size_t)b * (d + 2));
+  return 0;
+}
 
 int evr_mll_fit_rounds(void* stream, evr_mll_plan* p, void** runs, int* task, double* x, double* f, double* g,
                        int* nit, int* nfev, int* status, int maxiter, int maxfun, const double* prior, double* params,
@@ -332,7 +375,6 @@ int evr_mll_fit_rounds(void* stream, evr_mll_plan* p, void** runs, int* task, do
   EVR_CHECK(p && runs && task && x && f && g && nit && nfev && status && prior && params && pending,
             "evr_mll_fit_rounds: bad arguments");
   const int B = p->B, d = p->d, n = p->n, nx = d + 2;
-  const int lf = (int)prior[0], nzf = (int)prior[3];
   std::vector<double> out((size_t)B * (5 + d + 1)), gb(nx);
   *pending = 0;
   for (;;) {
@@ -362,31 +404,10 @@ int evr_mll_fit_rounds(void* stream, evr_mll_plan* p, void** runs, int* task, do
     for (int b = 0; b < B; ++b) {
       if (task[b] != EVR_LBFGSB_FG) continue;
       double* xb = x + (size_t)b * nx;
-      const double* t = terms + (size_t)b * 5;
-      const double logdet = t[0], quad = t[1], trKinv = t[2], sum_a = t[3], sum_a2 = t[4];
-      double ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * std::log(2.0 * M_PI);
-      double d_noise = 0.5 * (sum_a2 - trKinv);
-      const double d_const = sum_a;
-      const double noise = xb[0];
-      if (lf) {
-        double s = 0.0;
-        for (int j = 0; j < d; ++j) s += prior_logpdf(lf, prior[1], prior[2], params[(size_t)b * d + j]);
-        ll += s;
-      }
-      if (nzf) {
-        ll += prior_logpdf(nzf, prior[4], prior[5], noise);
-        d_noise += prior_dlogpdf(nzf, prior[4], prior[5], noise);
-      }
-      gb[0] = d_noise / n;
-      gb[1] = d_const / n;
-      for (int j = 0; j < d; ++j) {
-        const double lsj = params[(size_t)b * d + j];
-        double dl = 0.5 * gls[(size_t)b * d + j];
-        if (lf) dl += prior_dlogpdf(lf, prior[1], prior[2], lsj);
-        gb[2 + j] = dl * (1.0 / (1.0 + std::exp(-xb[2 + j]))) / n;
-      }
+      double llb;
+      mll_assemble_one(n, d, prior, xb, terms + (size_t)b * 5, gls + (size_t)b * d, &llb, gb.data());
       // minimise -MLL / n
-      f[b] = -(ll / n);
+      f[b] = -llb;
       for (int j = 0; j < nx; ++j) g[(size_t)b * nx + j] = -gb[j];
       if (int rc = evr_lbfgsb_advance(runs[b], f[b], g + (size_t)b * nx, xb, task + b, nit + b, nfev + b, status + b,
                                       maxiter, maxfun))

@@ -22,6 +22,9 @@
 // Every reduction order is fixed: results are bitwise reproducible.
 #include <algorithm>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "common.hpp"
 #include "../../include/everest_amd.h"
 
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
                                                     const double* seqp,
                                                     const double* __restrict__ sval, int S, int m,
                                                     const int* __restrict__ flags,
-                                                    unsigned long long* __restrict__ plast) {
+                                                    unsigned long long* __restrict__ plast, int light) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool ein = e < b * d;
   const int k = e % d;
@@ -511,14 +514,31 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
     const double r = v * (scale ? scale[k] : 1.0);
     dX[e] = r;
     if (hout) {
-      hout[b + e] = r;
-      if (e < b) hout[e] = sval ? av : acq[e];
-      __threadfence_system();
+      const double a = (e < b) ? (sval ? av : acq[e]) : 0.0;
+      if (light) {
+        // system-coherent write-through stores (sc0 sc1) and a wait for their completion
+        // instead of the system-scope fence, whose L2 writeback + invalidate walks the whole
+        // cache (and leaves the next evaluation's operands to be refetched)
+        __hip_atomic_store((unsigned long long*)(hout + b + e), (unsigned long long)__double_as_longlong(r),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (e < b)
+          __hip_atomic_store((unsigned long long*)(hout + e), (unsigned long long)__double_as_longlong(a),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        hout[b + e] = r;
+        if (e < b) hout[e] = a;
+        __threadfence_system();
+      }
     }
   }
   if (hout) {
     __syncthreads();
-    if (threadIdx.x == 0) *(volatile unsigned long long*)(hout + b + (size_t)b * d + blockIdx.x) = seq;
+    if (threadIdx.x == 0) {
+      unsigned long long* w = (unsigned long long*)(hout + b + (size_t)b * d + blockIdx.x);
+      if (light) __hip_atomic_store(w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else *(volatile unsigned long long*)w = seq;
+    }
     // the request this chain served: a chain queued behind it waits for a newer one
     // (kmat_wait_request); read by the next kernel of the stream only
     if (plast && blockIdx.x == 0 && threadIdx.x == 0) *plast = seq;
@@ -578,8 +598,11 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
 #undef QS_BWD
   EVR_LAUNCH_CHECK();
   (void)counter;
+  // EVR_HOSTFENCE=light: write-through stores instead of the system fence (read per call)
+  const char* hf = std::getenv("EVR_HOSTFENCE");
+  const int light = (hf && !std::strcmp(hf, "light")) ? 1 : 0;
   qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, sval,
-                                                   st->S, st->m, flags, plast);
+                                                   st->S, st->m, flags, plast, light);
   EVR_LAUNCH_CHECK();
   return 0;
 }

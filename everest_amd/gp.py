@@ -57,6 +57,15 @@ def softplus_np(x):
     return np.logaddexp(0.0, x)
 
 
+def _softplus_libm(v: float) -> float:
+    """numpy.logaddexp(0, v) with the C library's scalar exp / log1p (CPython's math module):
+    the arithmetic of the native fit driver's softplus (mll_plan.hip)."""
+    v = float(v)
+    if v == 0.0:
+        return 0.6931471805599453
+    return v + math.log1p(math.exp(-v)) if v > 0.0 else math.log1p(math.exp(v))
+
+
 def sigmoid_np(x):
     return 1.0 / (1.0 + np.exp(-x))
 
@@ -402,35 +411,30 @@ class MLLBatch:
 
     def __call__(self, idx: Sequence[int], xs: Sequence[np.ndarray]):
         n, d = self.n, self.d
-        xs = np.stack([np.asarray(x, dtype=np.float64) for x in xs])
+        xs = np.ascontiguousarray(np.stack([np.asarray(x, dtype=np.float64) for x in xs]))
         noise, const, raw = xs[:, 0], xs[:, 1], xs[:, 2:]
-        ls = softplus_np(raw)
+        # softplus with libm's scalar exp / log1p: the native round driver's arithmetic
+        ls = np.array([[_softplus_libm(v) for v in row] for row in raw]).reshape(raw.shape)
         host = self._eval_plan(idx, ls, noise, const) if self.use_plan else None
         if host is None:
             host = self._eval_ops(idx, ls, noise, const)
         B = len(idx)
-        terms_h = host[:5 * B].reshape(B, 5)
-        gls_h = host[5 * B:5 * B + B * d].reshape(B, d)
+        terms_h = np.ascontiguousarray(host[:5 * B].reshape(B, 5))
+        gls_h = np.ascontiguousarray(host[5 * B:5 * B + B * d].reshape(B, d))
         info_h = host[5 * B + B * d:]
-        out = []
-        for k in range(B):
-            if info_h[k] != 0 or not np.all(np.isfinite(terms_h[k])):
-                out.append(None)
-                continue
-            logdet, quad, trKinv, sum_a, sum_a2 = terms_h[k]
-            ll = -0.5 * quad - 0.5 * logdet - 0.5 * n * math.log(2 * math.pi)
-            d_noise = 0.5 * (sum_a2 - trKinv)
-            d_const = sum_a
-            d_ls = 0.5 * gls_h[k]
-            if self.ls_prior is not None:
-                ll += float(np.sum(prior_logpdf_np(self.ls_prior, ls[k])))
-                d_ls = d_ls + prior_dlogpdf_np(self.ls_prior, ls[k])
-            if self.noise_prior is not None:
-                ll += float(prior_logpdf_np(self.noise_prior, noise[k]))
-                d_noise += float(prior_dlogpdf_np(self.noise_prior, noise[k]))
-            g = np.concatenate([[d_noise, d_const], d_ls * sigmoid_np(raw[k])]) / n
-            out.append((ll / n, g))
-        return out
+        # ll / n and its gradient with the priors: evr_mll_assemble, the code the native driver
+        # (evr_mll_fit_rounds) runs, so both drivers take bitwise the same L-BFGS-B steps
+        ll = np.empty(B)
+        g = np.empty((B, d + 2))
+        lib = _native.load()
+        _native.check(lib.evr_mll_assemble(B, n, d, self.prior_spec().ctypes.data, xs.ctypes.data, terms_h.ctypes.data,
+                                           gls_h.ctypes.data, ll.ctypes.data, g.ctypes.data), "evr_mll_assemble")
+        return [None if info_h[k] != 0 or not np.all(np.isfinite(terms_h[k])) else (float(ll[k]), g[k].copy())
+                for k in range(B)]
+
+
+# the last fit_batch's per-output L-BFGS-B evaluation / iteration counts (tools/fit_probe.py)
+LAST_FIT_STATS: dict = {}
 
 
 def _fit_rounds_native(ev: "MLLBatch", B: int, d: int, x0: np.ndarray, lb: np.ndarray, ub: np.ndarray, maxiter: int,
@@ -496,6 +500,10 @@ def _fit_rounds_native(ev: "MLLBatch", B: int, d: int, x0: np.ndarray, lb: np.nd
                 _native.check(lib.evr_lbfgsb_advance(runs[b], float(F[b]), G[b].ctypes.data, X[b].ctypes.data,
                                                      i32(task, b), i32(nit, b), i32(nfev, b), i32(status, b),
                                                      int(maxiter), int(maxfun)), "evr_lbfgsb_advance")
+        # per-member evaluation / iteration counts (tools/fit_probe.py): max nfev is the number
+        # of lock-step rounds since the last restart
+        ev.native_stats = {"nfev": nfev.tolist(), "nit": nit.tolist(), "status": status.tolist()}
+        LAST_FIT_STATS.update(driver="native", nfev=nfev.tolist(), nit=nit.tolist())
         return [X[b].copy() for b in range(B)]
     finally:
         for b in range(B):
@@ -556,7 +564,7 @@ def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_pr
         return gen, next(gen)
 
     runs = {b: start(np.concatenate([[noise0, 0.0], np.zeros(d)])) for b in range(B)}
-    result = {}
+    result, counts = {}, {}
     while runs:
         idx = sorted(runs)
         vals = ev(idx, [runs[b][1] for b in idx])
@@ -571,6 +579,8 @@ def fit_batch(Xn: torch.Tensor, Y_raw: np.ndarray, kind: int, ls_prior, noise_pr
                 runs[b] = (gen, gen.send((-f, -g)))
             except StopIteration as stop:
                 result[b] = stop.value.x
+                counts[b] = (stop.value.nfev, stop.value.nit)
                 del runs[b]
+    LAST_FIT_STATS.update(driver="python", nfev=[counts[b][0] for b in range(B)], nit=[counts[b][1] for b in range(B)])
     return [GPHyper(lengthscale=softplus_np(result[b][2:]), noise=float(result[b][0]), constant=float(result[b][1]),
                     y_mean=stats[b][0], y_std=stats[b][1]) for b in range(B)]

@@ -104,6 +104,13 @@ void evr_mll_plan_destroy(evr_mll_plan* plan);
 int evr_mll_fit_rounds(void* stream, evr_mll_plan* plan, void** runs, int* task, double* x, double* f, double* g,
                        int* nit, int* nfev, int* status, int maxiter, int maxfun, const double* prior, double* params,
                        int* pending);
+/* Host-only.  ll / n and its gradient in x = [noise, constant, raw lengthscales] per member
+ * (B x (d + 2)), the ExactMarginalLogLikelihood with the hyperparameter priors (prior as in
+ * evr_mll_fit_rounds) divided by n, from the plan's terms (B x 5) and lengthscale-gradient
+ * pieces gls (B x d): the closure of fit_gpytorch_mll (bofire/surrogates/single_task_gp.py:70-71)
+ * after the device work; evr_mll_fit_rounds applies the same code. */
+int evr_mll_assemble(int B, int n, int d, const double* prior, const double* x, const double* terms,
+                     const double* gls, double* ll, double* g);
 /* One member's L-BFGS-B after its evaluation at x (f, g): scipy's driver loop up to the next
  * evaluation request or the end (the state machine evr_mll_fit_rounds applies). */
 int evr_lbfgsb_advance(void* run, double f, const double* g, double* x, int* task, int* nit, int* nfev,

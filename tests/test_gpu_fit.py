@@ -101,11 +101,15 @@ def test_mll_plan_matches_op_chain(kind, monkeypatch):
 def test_native_fit_rounds_match_python_loop(dup, monkeypatch):
     """gp.fit_batch's lock-step loop in native code (evr_mll_fit_rounds: the plan evaluation,
     -MLL / n with the priors and the L-BFGS-B steps per round without Python) against the
-    Python generator loop over the same plan: the same optimisation problem and algorithm, so
-    the same optimum (the prior terms' summation order is the only difference).  With
-    duplicated inputs the plain factor of some iterates fails and those rounds take the
-    jitter-ladder path (the native driver hands them back)."""
-    from everest_amd.gp import fit_batch
+    Python generator loop over the same plan.  Both assemble -MLL / n through
+    evr_mll_assemble with libm's softplus, and the native step is the generator's state
+    machine (bitwise on the host, test_native_cpu.py), so the fits are bitwise equal — the
+    optimiser's path is sensitive enough to ulp-level differences (other exp / log
+    implementations changed the iteration count of an output from 89 to 332 at the bench
+    shape) that only a bitwise check says the drivers are the same.  With duplicated inputs
+    the plain factor of some iterates fails and those rounds take the jitter-ladder path (the
+    native driver hands them back)."""
+    from everest_amd.gp import LAST_FIT_STATS, fit_batch
 
     rng = np.random.default_rng(21)
     n, d, m = 90, 4, 3
@@ -115,11 +119,13 @@ def test_native_fit_rounds_match_python_loop(dup, monkeypatch):
     Y = dtlz2(X, m) + (0.0 if dup else 0.01) * rng.normal(size=(n, m))
     Xn = torch.tensor(X, device="cuda")
     prior = (math.sqrt(2) + 0.5 * math.log(d), math.sqrt(3))
-    out = {}
+    out, counts = {}, {}
     for mode in ("1", "0"):
         monkeypatch.setenv("EVR_FIT_NATIVE", mode)
         out[mode] = fit_batch(Xn, Y, 0, prior, (-4.0, 1.0))
+        counts[mode] = (LAST_FIT_STATS.get("driver"), LAST_FIT_STATS.get("nfev"))
+    assert counts["1"][0] == "native" and counts["0"][0] == "python"
+    assert counts["1"][1] == counts["0"][1], counts
     for a, b in zip(out["1"], out["0"]):
-        assert np.allclose(a.lengthscale, b.lengthscale, rtol=1e-4), (a.lengthscale, b.lengthscale)
-        assert abs(a.noise - b.noise) <= 1e-4 * b.noise + 1e-10
-        assert abs(a.constant - b.constant) <= 1e-4 * max(1.0, abs(b.constant))
+        assert np.array_equal(a.lengthscale, b.lengthscale), (a.lengthscale, b.lengthscale)
+        assert a.noise == b.noise and a.constant == b.constant

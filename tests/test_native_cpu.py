@@ -210,3 +210,62 @@ def test_evaluation_chain_kernels_use_no_scratch():
     assert len(checked) > 40, sorted(checked)
     spill = {k: v.get("scratch") for k, v in checked.items() if v.get("scratch")}
     assert not spill, spill
+
+
+def test_lbfgsb_advance_matches_generator_state_machine():
+    """evr_lbfgsb_advance (the per-member step of the native GP-fit driver, evr_mll_fit_rounds)
+    applies optim.lbfgsb_steps' state machine — evaluation counting, NEW_X iterations, the
+    maxiter / maxfun stops, the final status — to the same native L-BFGS-B: on a host
+    objective (5-d Rosenbrock, and a bounded quadratic that hits maxiter) both drivers visit
+    the same iterates bitwise and stop with the same counts."""
+    from everest_amd import _native
+    from everest_amd.optim import LBFGSB_FG, _EPS, lbfgsb_steps
+
+    lib = _native.load()
+
+    def rosen(x):
+        f, g = 0.0, np.zeros_like(x)
+        for i in range(len(x) - 1):
+            f += 100 * (x[i + 1] - x[i] ** 2) ** 2 + (1 - x[i]) ** 2
+            g[i] += -400 * x[i] * (x[i + 1] - x[i] ** 2) - 2 * (1 - x[i])
+            g[i + 1] += 200 * (x[i + 1] - x[i] ** 2)
+        return f, g
+
+    def quad(x):
+        w = np.arange(1.0, len(x) + 1.0)
+        return float(np.sum(w * (x - 0.3) ** 2)), 2 * w * (x - 0.3)
+
+    cases = ((rosen, np.array([-1.2, 1.0, 0.5, -0.3, 0.8]), np.full(5, -np.inf), np.full(5, np.inf), 15000),
+             (quad, np.full(4, 2.0), np.full(4, 0.5), np.full(4, 3.0), 2))
+    for fun, x0, lb, ub, maxiter in cases:
+        n = len(x0)
+        gen = lbfgsb_steps(x0, lb, ub, maxiter=maxiter)
+        xs_gen, x = [], next(gen)
+        try:
+            while True:
+                xs_gen.append(x.copy())
+                x = gen.send(fun(x))
+        except StopIteration as stop:
+            res = stop.value
+        h = ctypes.c_void_p()
+        lo, hi = np.ascontiguousarray(lb), np.ascontiguousarray(ub)
+        _native.check(lib.evr_lbfgsb_create(n, 10, lo.ctypes.data, hi.ctypes.data, 2.220446049250313e-09 / _EPS,
+                                            1e-5, 20, ctypes.byref(h)), "evr_lbfgsb_create")
+        try:
+            X = np.zeros(n)
+            task, nit, nfev, st = (np.zeros(1, dtype=np.int32) for _ in range(4))
+            task[0] = lib.evr_lbfgsb_start(h, np.ascontiguousarray(x0).ctypes.data, X.ctypes.data)
+            xs_adv = []
+            while task[0] == LBFGSB_FG:
+                xs_adv.append(X.copy())
+                f, g = fun(X.copy())
+                g = np.ascontiguousarray(g, dtype=np.float64)
+                _native.check(lib.evr_lbfgsb_advance(h, ctypes.c_double(f), g.ctypes.data, X.ctypes.data,
+                                                     task.ctypes.data, nit.ctypes.data, nfev.ctypes.data,
+                                                     st.ctypes.data, maxiter, 15000), "evr_lbfgsb_advance")
+        finally:
+            lib.evr_lbfgsb_destroy(h)
+        assert len(xs_adv) == len(xs_gen)
+        assert all(np.array_equal(a, b) for a, b in zip(xs_adv, xs_gen))
+        assert (int(nit[0]), int(nfev[0]), int(st[0])) == (res.nit, res.nfev, res.status)
+        assert np.array_equal(X, res.x)

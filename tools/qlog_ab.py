@@ -1,5 +1,5 @@
 """A/B of the qLogNEHVI scan at the bench state (DTLZ2 n = 512, d = 6, m = 5, S = 256): the
-kd-bounded tabulated kernel (default) against the unbounded keyed scan (EVR_LOG=keyed),
+kd-bounded tabulated kernel (EVR_LOG=kd) against the unbounded keyed scan (default),
 forward + backward at b = 512 and b = 20, plus the largest |difference| of values and
 gradients between the two.  Prints one JSON object.
 
@@ -27,8 +27,8 @@ def main():
            "kd": bool(qa.state.grp_off)}
     res = {}
     for mode in ("bounded", "keyed"):
-        if mode == "keyed":
-            os.environ["EVR_LOG"] = "keyed"
+        if mode == "bounded":
+            os.environ["EVR_LOG"] = "kd"
         qa._plans = {}
         for b in (512, 20):
             Xc = bench.candidates(b, 6, seed=3, device=dev)
