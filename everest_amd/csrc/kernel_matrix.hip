@@ -46,9 +46,15 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
                                                    const double* __restrict__ sc2, const double* __restrict__ ls,
                                                    const double* __restrict__ os, const double* __restrict__ dg,
                                                    double* __restrict__ K, const unsigned long long* poll,
-                                                   const unsigned long long* plast) {
+                                                   const unsigned long long* plast,
+                                                   const unsigned long long* seq_src, unsigned long long* seq_dst) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (poll) kmat_wait_request(poll, plast);
+  // host-driven chains: the evaluation's sequence number (pinned host memory, posted with the
+  // candidates) copied to device memory, so the chain's last kernel reads it from L2 instead of
+  // across PCIe (this kernel's candidate loads pay that latency anyway)
+  if (seq_dst && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    *seq_dst = __hip_atomic_load(const_cast<unsigned long long*>(seq_src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * (16 * RA), j0 = blockIdx.x * KT;
   const int ld = d + 1;
@@ -1053,7 +1059,8 @@ int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const doubl
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast);
+                         const unsigned long long* poll, const unsigned long long* plast,
+                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr);
 }  // namespace evr
 
 extern "C" {
@@ -1073,9 +1080,12 @@ namespace evr {
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast) {
+                         const unsigned long long* poll, const unsigned long long* plast,
+                         const unsigned long long* seq_src, unsigned long long* seq_dst) {
   EVR_CHECK(!poll || (plast && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
             "kernel_matrix_launch: the request wait needs the VALU kernel (d < 16, one family)");
+  EVR_CHECK(!seq_dst || (seq_src && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
+            "kernel_matrix_launch: the sequence copy needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(kind_code_ok(kind, B), "evr_kernel_matrix: bad kernel kind %d for %d outputs", kind, B);
   EVR_CHECK(B >= 1 && n1 >= 0 && n2 >= 0 && d >= 1 && d <= KMAXD, "evr_kernel_matrix: bad sizes B=%d n1=%d n2=%d d=%d",
             B, n1, n2, d);
@@ -1186,7 +1196,7 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
 #define KTK(RA_, K_)                                                                              \
   kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
                                                              scale2, lengthscales, outputscale, diag_add, K, poll,   \
-                                                             plast)
+                                                             plast, seq_src, seq_dst)
 #define KT_(RA_)                         \
   if (kind == RBF) KTK(RA_, RBF);           \
   else if (kind == MATERN05) KTK(RA_, MATERN05); \

@@ -322,10 +322,12 @@ __global__ void set_identity_kernel(int n, double* M, long long sM, int ldm) {
 // ---------------------------------------------------------------------------------------
 constexpr int BNB = 64;
 
+// (also clears the member's info word: no separate memset node per attempt)
 __global__ void chol_init_kernel(int n, const double* __restrict__ A, long long sA, int lda, double* __restrict__ L,
-                                 long long sL, int ldl, const double* __restrict__ jit) {
+                                 long long sL, int ldl, const double* __restrict__ jit, int* __restrict__ info) {
   const int b = blockIdx.y;
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) info[b] = 0;
   if (e >= (long long)n * n) return;
   const int i = (int)(e / n), j = (int)(e % n);
   double v = (j <= i) ? A[b * sA + (size_t)i * lda + j] : 0.0;
@@ -1735,9 +1737,8 @@ int chol_ladder(hipStream_t s, int batch, int n, const double* A, int lda, long 
   const bool fused = Linv && chol_inv_fused(n);
   for (int t = 0; t <= max_tries; ++t) {
     EVR_HIP(hipMemcpyAsync(jit_d, jit.data(), sizeof(double) * batch, hipMemcpyHostToDevice, s));
-    EVR_HIP(hipMemsetAsync(info_d, 0, sizeof(int) * batch, s));
     dim3 g1(cdiv((long long)n * n, 256), batch);
-    chol_init_kernel<<<g1, 256, 0, s>>>(n, A, sA, lda, L, sL, ldl, jit_d);
+    chol_init_kernel<<<g1, 256, 0, s>>>(n, A, sA, lda, L, sL, ldl, jit_d, info_d);
     EVR_LAUNCH_CHECK();
     if ((rc = chol_blocked(s, batch, n, L, ldl, sL, Dinv, info_d, fused ? Linv : nullptr, ldi, sI))) break;
     EVR_HIP(hipMemcpyAsync(info.data(), info_d, sizeof(int) * batch, hipMemcpyDeviceToHost, s));
@@ -1766,9 +1767,8 @@ namespace evr {
 // triangular inverse, and the GEMM without the split-K workspace allocation.
 int chol_inverse_attempt(hipStream_t s, int batch, int n, const double* A, double* L, double* Linv, double* Dinv,
                          double* T, const double* jit_d, int* info_d) {
-  EVR_HIP(hipMemsetAsync(info_d, 0, sizeof(int) * batch, s));
   dim3 g1(cdiv((long long)n * n, 256), batch);
-  chol_init_kernel<<<g1, 256, 0, s>>>(n, A, (long long)n * n, n, L, (long long)n * n, n, jit_d);
+  chol_init_kernel<<<g1, 256, 0, s>>>(n, A, (long long)n * n, n, L, (long long)n * n, n, jit_d, info_d);
   EVR_LAUNCH_CHECK();
   const long long nn = (long long)n * n;
   if (chol_inv_fused(n)) return chol_blocked(s, batch, n, L, n, nn, Dinv, info_d, Linv, n, nn);

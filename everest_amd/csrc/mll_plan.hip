@@ -78,20 +78,18 @@ __global__ __launch_bounds__(256, 4) void mll_w_kernel(int n, int B, const doubl
   });
 }
 
-// hx: [ls (B x d) | noise (B) | constant (B) | sequence number]
-__global__ void mll_copy_in(int B, int d, const double* hx, double* ls, double* noise, double* cst) {
+// hx: [ls (B x d) | noise (B) | constant (B) | sequence number]; also the residuals
+// r = Y - constant (one launch: the constant comes straight from the host buffer, one read
+// per wave since a wave's rows share a member when n >= 64)
+__global__ void mll_copy_in(int B, int n, int d, const double* hx, const double* __restrict__ Y, double* ls,
+                            double* noise, double* cst, double* __restrict__ r) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B * d) ls[i] = hx[i];
   if (i < B) {
     noise[i] = hx[B * d + i];
     cst[i] = hx[B * d + B + i];
   }
-}
-
-__global__ void mll_resid(int B, int n, const double* __restrict__ Y, const double* __restrict__ cst,
-                          double* __restrict__ r) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < B * n) r[i] = Y[i] - cst[i / n];
+  if (i < B * n) r[i] = Y[i] - hx[B * d + B + i / n];
 }
 
 // hout: [terms (B x 5: logdet, r.alpha, tr K^-1, sum alpha, sum alpha^2) | gls (B x d) |
@@ -134,14 +132,13 @@ struct evr_mll_plan {
 static int mll_chain(hipStream_t s, evr_mll_plan* p, const double* dhx, double* dhout) {
   const int B = p->B, n = p->n, d = p->d;
   const long long nn = (long long)n * n;
-  mll_copy_in<<<cdiv(B * d + B, 256), 256, 0, s>>>(B, d, dhx, p->ls, p->noise, p->cst);
+  mll_copy_in<<<cdiv(std::max(B * d + B, B * n), 256), 256, 0, s>>>(B, n, d, dhx, p->Y, p->ls, p->noise, p->cst,
+                                                                       p->r);
   EVR_LAUNCH_CHECK();
   if (int rc = evr_kernel_matrix(s, p->kind, B, n, n, d, p->Xn, nullptr, nullptr, p->Xn, nullptr, nullptr, p->ls,
                                  nullptr, p->noise, p->K))
     return rc;
   if (int rc = chol_inverse_attempt(s, B, n, p->K, p->L, p->Linv, p->Dinv, p->T, p->jit0, p->info)) return rc;
-  mll_resid<<<cdiv(B * n, 256), 256, 0, s>>>(B, n, p->Y, p->cst, p->r);
-  EVR_LAUNCH_CHECK();
   double* W = p->K;   // K was consumed by the factorisation
   // v = L^-1 r, alpha = L^-T v: matrix-vector products, split over k (the plan's workspace
   // holds the partials; a fixed-order reduction) so that they spread over ~300 workgroups

@@ -48,7 +48,8 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast);
+                         const unsigned long long* poll, const unsigned long long* plast,
+                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr);
 constexpr int QS_TILE_ROWS = 16;
 constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
@@ -68,7 +69,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
                        double* work);
 
 struct PlanLayout {
-  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqw, bytes;
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqw, seqd, bytes;
   bool small, fused_scan;
 };
 
@@ -104,6 +105,7 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
     }
   }
   L.seqw = take(8);   // the last request a host-driven chain served (queued evaluations)
+  L.seqd = take(8);   // the host-driven chain's sequence number, copied to device memory by kmat
   L.bytes = o;
   return L;
 }
@@ -185,9 +187,13 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   // (K_x generated inside the projection instead was measured slower at b = 20 twice — 29 vs
   // 17.6 us in round 3, chain 83.9 vs 73.7 us in round 4 — and removed)
   unsigned long long* plast = queued ? (unsigned long long*)(w + p->L.seqw) : nullptr;
+  // host mode through the b <= 32 kernels: qs_dx_reduce reads the sequence number from the
+  // device copy kmat makes (an L2 read instead of a PCIe read at the end of the chain)
+  unsigned long long* seqd = (hout && seqp && small) ? (unsigned long long*)(w + p->L.seqd) : nullptr;
   if (int rc = kernel_matrix_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                     md->lengthscales, nullptr, nullptr, Kx,
-                                    queued ? (const unsigned long long*)seqp : nullptr, plast)) {
+                                    queued ? (const unsigned long long*)seqp : nullptr, plast,
+                                    seqd ? (const unsigned long long*)seqp : nullptr, seqd)) {
     return rc;
   } else if (small) {
     if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;
@@ -202,7 +208,7 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
                                L22, flags, hw, dG))
       return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
                        hw, flags, plast);
   }
   if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : QN_NORM_TILE)) return rc;
@@ -212,13 +218,13 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     // the scan workspace become acq inside the dX reduction
     if (int rc = evr_hvi_restart_fb(s, st, b, G, hw, dG)) return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
                        hw, flags, plast);
   }
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (small) {
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqp, counter,
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
                        nullptr, nullptr, plast);
   }
   double* dKx = (double*)(w + p->L.dKx);

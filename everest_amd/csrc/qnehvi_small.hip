@@ -468,27 +468,36 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   const bool ein = e < b * d;
   const int k = e % d;
   unsigned long long seq = 0;
-  if (hout && threadIdx.x == 0) seq = *(volatile const unsigned long long*)seqp;
   // every first-round load of the kernel (the element's partials, the per-sample values and the
   // Cholesky flags of an acquisition element) is issued before the first wait: one memory round
-  // trip instead of three dependent ones
+  // trip instead of three dependent ones.  The sequence number (pinned host memory: a PCIe read)
+  // is issued after them — the memory counter retires in order, so a wait for the partials
+  // would otherwise wait for the PCIe read too
+  // (unconditional loads at clamped indices, selected afterwards: a guarded load let the
+  // compiler fold the first partial's add into the guard's branch with a wait right after it,
+  // one extra memory round trip per load group)
   const double* src = dXp + (size_t)(ein ? e : 0) * np;
+  const double sck = scale ? scale[k] : 1.0;   // issued with the first loads, used at the end
   double x[8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int p = lane + 64 * u;
-    x[u] = (ein && p < np) ? src[p] : 0.0;
-  }
+  for (int u = 0; u < 8; ++u) x[u] = src[min(lane + 64 * u, np - 1)];
   const bool acq_e = ein && sval && e < b;
-  double sv[4];
+  double sv[4] = {0.0, 0.0, 0.0, 0.0};
   int fl = 0;
+  if (sval) {
+    const int ec = min(e, b - 1);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int s = lane + 64 * u;
-    sv[u] = (acq_e && s < S) ? sval[(size_t)s * b + e] : 0.0;
+    for (int u = 0; u < 4; ++u) sv[u] = sval[(size_t)min(lane + 64 * u, S - 1) * b + ec];
   }
-  if (acq_e && flags)
-    for (int j = lane; j < m; j += 64) fl |= flags[(size_t)j * b + e];
+  if (flags) {   // m <= 8 outputs: one flag per lane
+    const int fv = flags[(size_t)min(lane, m - 1) * b + min(e, b - 1)];
+    fl = (acq_e && lane < m) ? fv : 0;
+  }
+  // a relaxed system-scope atomic load, not a volatile one: the backend follows a volatile
+  // load with a wait for every outstanding load
+  if (hout && threadIdx.x == 0)
+    seq = __hip_atomic_load(const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(seqp)),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   double av = 0.0;
   if (acq_e) {
     double a = 0.0;
@@ -505,13 +514,13 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   double v = 0.0;
 #pragma unroll
   for (int u = 0; u < 8; ++u)
-    if (lane + 64 * u < np) v += x[u];
+    if (ein && lane + 64 * u < np) v += x[u];
   if (ein)
     for (int p = lane + 512; p < np; p += 64) v += src[p];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if (lane == 0 && ein) {
-    const double r = v * (scale ? scale[k] : 1.0);
+    const double r = v * sck;
     dX[e] = r;
     if (hout) {
       const double a = (e < b) ? (sval ? av : acq[e]) : 0.0;
