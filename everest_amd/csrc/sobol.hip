@@ -17,9 +17,12 @@
 //     the inverse-normal transform with torch's calc_erfinv (rational seed + 2 Newton steps).
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <functional>
 #include <new>
 #include <cstdint>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -171,6 +174,59 @@ int evr_sobol_scramble(int dim, unsigned long long seed, long long* V, long long
 }  // extern "C"
 
 namespace evr {
+// A persistent pool of scrambling workers: run(k, f) hands f(0..k-1) to k workers, wait()
+// returns when all are done.  One job at a time (a mutex serialises concurrent draws from the
+// acquisition's scrambling threads).
+class SobolPool {
+ public:
+  void run(int k, std::function<void(int)> f) {
+    job_mu_.lock();
+    std::unique_lock<std::mutex> lk(mu_);
+    while ((int)th_.size() < k) th_.emplace_back([this, i = (int)th_.size()] { loop(i); });
+    f_ = std::move(f);
+    k_ = k;
+    left_ = k;
+    ++gen_;
+    cv_.notify_all();
+  }
+  void wait() {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      done_cv_.wait(lk, [this] { return left_ == 0; });
+    }
+    job_mu_.unlock();
+  }
+
+ private:
+  void loop(int i) {
+    unsigned long long seen = 0;
+    for (;;) {
+      std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (i >= k_) continue;
+        f = &f_;
+      }
+      (*f)(i);
+      std::unique_lock<std::mutex> lk(mu_);
+      if (--left_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_, job_mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+  std::function<void(int)> f_;
+  int k_ = 0, left_ = 0;
+  unsigned long long gen_ = 0;
+};
+
+static SobolPool& sobol_pool() {
+  static SobolPool* p = new SobolPool();   // never destroyed: the workers live for the process
+  return *p;
+}
+
 // Dimensions [d0, d0 + nd) of a dim-dimensional engine from the raw words wp of its seed's
 // stream: shift bits (dim x 30), then the scrambling-matrix bits (dim x 30 x 30).  With
 // `done`, the words are still being generated: each worker waits until its range is in.
@@ -205,27 +261,42 @@ static void scramble_apply(const uint32_t* wp, int dim, int d0, int nd, long lon
       }
     }
   };
-  const int nth = nd >= 256 ? 8 : 1;
+  // worker threads: the job's host-thread share (EVR_HOST_THREADS / OMP_NUM_THREADS, default
+  // 16 — the GPU box's share), at least 128 dimensions each (the baseline draw of the bench
+  // ask, ~1.4 k dimensions, waited ~0.54 ms on 8 threads with the device idle)
+  static const int nmax = [] {
+    const char* e = std::getenv("EVR_HOST_THREADS");
+    if (!e) e = std::getenv("OMP_NUM_THREADS");
+    const int v = e ? std::atoi(e) : 16;
+    return std::max(1, std::min(v > 0 ? v : 16, 32));
+  }();
+  const int nth = std::max(1, std::min(nmax, nd / 128));
   if (nth == 1) {
     if (producer) producer();
     work(d0, d0 + nd);
     return;
   }
-  std::vector<std::thread> th;
   const int per = (nd + nth - 1) / nth;
-  for (int i = 0; i < nth; ++i) {
+  auto part = [&](int i) {
     const int a = d0 + i * per, b = std::min(d0 + nd, a + per);
-    if (a < b)
-      th.emplace_back([&, a, b] {
-        if (done) {
-          const size_t need = nshift + (size_t)b * per_dim;
-          while (done->load(std::memory_order_acquire) < need) std::this_thread::yield();
-        }
-        work(a, b);
-      });
+    if (a >= b) return;
+    if (done) {
+      const size_t need = nshift + (size_t)b * per_dim;
+      while (done->load(std::memory_order_acquire) < need) std::this_thread::yield();
+    }
+    work(a, b);
+  };
+  // the parts on the persistent pool (spawning 16 threads per draw cost ~0.2 ms); the calling
+  // thread generates the words meanwhile, or takes part 0 itself
+  if (producer) {
+    sobol_pool().run(nth, part);
+    producer();
+    sobol_pool().wait();
+  } else {
+    sobol_pool().run(nth - 1, [&](int i) { part(i + 1); });
+    part(0);
+    sobol_pool().wait();
   }
-  if (producer) producer();
-  for (auto& t : th) t.join();
 }
 }  // namespace evr
 

@@ -249,11 +249,16 @@ def test_restart_balanced_scan_slices(restart_variant):
     assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
 
 
-def test_restart_wave_scan_long_term_lists(restart_variant):
+@pytest.mark.parametrize("split", ["2", "1"])
+def test_restart_wave_scan_long_term_lists(restart_variant, split, monkeypatch):
     """hvi_kdw on candidates dominating most of the front (hundreds of terms per sample and
-    candidate: many 64-term rounds and list remainders) against the three-launch chain."""
+    candidate: many 64-term rounds and list remainders) against the three-launch chain, with
+    two waves per (sample, candidate) (default, each walking every other 64-group chunk) and
+    with one (EVR_KDW_SPLIT=1); both batch-invariant bitwise (a candidate's result depends on
+    its own cells only: the first 9 candidates alone equal their values in the batch of 32)."""
     from everest_amd import ops
 
+    monkeypatch.setenv("EVR_KDW_SPLIT", split)
     restart_variant(3)
     kd, dense, lo, hi, d = _pair(240, 6, 5, 256, seed=11, prune=False)
     b = 32
@@ -265,6 +270,10 @@ def test_restart_wave_scan_long_term_lists(restart_variant):
     sval, d2 = ops.hvi_restart_fb(kd.state, G, b)
     assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
     assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
+    G9 = G.reshape(kd.S, -1, b)[:, :, :9].contiguous()
+    sval9, d9 = ops.hvi_restart_fb(kd.state, G9, 9)
+    assert torch.equal(sval9, sval.reshape(kd.S, b)[:, :9])
+    assert torch.equal(d9, d2.reshape(kd.S, -1, b)[:, :, :9])
 
 
 @pytest.mark.parametrize("b", [20, 32, 7])
