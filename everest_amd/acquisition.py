@@ -623,8 +623,11 @@ class QNEHVI(_BoxHviAcqf):
         # possible pruning outcome (draws of one seed are prefixes of one stream): start it now,
         # scramble the needed dimension ranges once the pruned baseline size is known
         max_dim = (len(base_rows) + npend + 1) * m
-        def _stream_job(after=fut_prune):
-            if after is not None:      # after the prune draw, which is needed first
+        def _stream_job(after=fut_prune if _host_threads() < 4 else None):
+            # beside the prune draw's scrambling when the host has the threads for both (the
+            # stream is one sequential mt19937 run; generated after the prune draw it held the
+            # baseline draw — and the device — ~0.5 ms at the bench shape, profiles/r05/r)
+            if after is not None:
                 after.result()
             return ops.SobolStream(int(sampler_seed), max_dim)
 

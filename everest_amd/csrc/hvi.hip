@@ -2053,10 +2053,9 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
 }
 
 // ---------------------------------------------------------------------------------------
-// hvi_kdw — the restart-batch scan with SPL waves per (sample, candidate) (SPL = 2: each wave
-// walks every other 64-group chunk of the sample; the halves' sums meet after one workgroup
-// barrier) and nothing else shared between the waves but the sample's point table (staged in
-// LDS once per workgroup of KW_WAVES / SPL candidates).  Per wave:
+// hvi_kdw — the restart-batch scan with one wave per (sample, candidate) and nothing shared
+// between the waves but the sample's point table (staged in LDS once per workgroup of
+// KW_WAVES candidates).  Per wave:
 //   y_j of the candidate (G, or the sampling step fused in: KbSamples);
 //   thresholds t_j = #{rows with lower-bound value <= y_j} by two wave-wide probes of the
 //     sample's ascending values (64 bucket ends, then the 64 entries of the straddling
@@ -2068,8 +2067,8 @@ __global__ __launch_bounds__(KB_THREADS) void hvi_kdb(int b, int S, const double
 //   terms in rounds of 64, term t of the candidate on lane t % 64: key decoded against the
 //     LDS point table, the term and its subgradients (hvi_kdb's arithmetic) summed per lane
 //     in t order; then one fixed xor-butterfly per value.
-// No inter-wave order beyond the halves' fixed sum: a candidate's value and gradient depend on
-// its own term sequence only, so they are bitwise the same in any batch
+// No workgroup barrier after the staging and no inter-wave order: a candidate's value and
+// gradient depend on its own term sequence only, so they are bitwise the same in any batch
 // (a restart batch sharded over ranks evaluates each candidate exactly as one rank does) and
 // bitwise reproducible.  Equal to hvi_kdb to rounding (different summation order).
 // Workgroup w runs on XCD w % 8: the candidate groups of a sample share one XCD's L2.
@@ -2089,17 +2088,10 @@ __host__ __device__ inline size_t kw_lds_bytes(int stride, int M) {
 // (256, 5): 5 waves per SIMD — at b = 20 the grid (S x 5 candidate groups = 1280 workgroups at
 // S = 256) is resident in one round; unbounded the compiler took 100 VGPRs (4 per SIMD).
 // M = 8 would spill at that bound and keeps 4.
-// SPL = 2 (default): two waves per (sample, candidate), each walking every other 64-group chunk
-// of the sample and its own term list; the halves' butterflied sums are added in a fixed order
-// (half 0 + half 1), so a candidate's result still depends on its own cells only (batch- and
-// rank-invariant).  The heaviest pairs set the span (28.9 us vs a 19.5 us mean per wave at
-// SPL = 1, r04): splitting every pair's chunks halves them.  EVR_KDW_SPLIT=1: one wave per pair.
-template <int M, int SPL>
+template <int M>
 __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int ncg, const double* __restrict__ G, HviKd kd,
                                                KbSamples smp, double* __restrict__ sval, double* __restrict__ dG) {
   constexpr int NV = M + 1;
-  constexpr int CPW = KW_WAVES / SPL;   // candidates per workgroup
-  __shared__ double kw_half[KW_WAVES][NV];
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kw_dyn[];
   const int wid = blockIdx.x, xcd = wid & 7, slot = wid >> 3;
@@ -2112,7 +2104,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   unsigned short* tl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M)) + (size_t)wave * KW_TCAP;
   unsigned short* pl = (unsigned short*)(kw_dyn + kw_pt_bytes(stride, M) + (size_t)KW_WAVES * KW_TCAP * 2) +
                        (size_t)wave * 64 * KW_NCH;
-  const int c = cg * CPW + wave / SPL, half = wave % SPL;
+  const int c = cg * KW_WAVES + wave;
   const bool cin = c < b;
   // EVR_KD_PROF=2 build: per (sample, candidate) wall-clock stamps (s_memrealtime, 10 ns):
   // start, after staging, after the thresholds, time in the group / cell phases, time in the
@@ -2165,9 +2157,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     }
   }
   __syncthreads();
-  if (SPL == 1 && !cin) return;
-  double acc[NV];   // this wave's sums (butterflied at the end; SPL = 2: combined after the barrier)
-  if (cin) {
+  if (!cin) return;
   if (EVR_KD_PROF == 2) pf_[1] = wall_clock64();
   // the thresholds' first probe (bucket ends) overlaps the sampling step below
   double v1[M];
@@ -2187,7 +2177,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
       double mu, l22;
       int flag;
       qn_mu_l22_from(ssv, ssw, am, smp.ys[j], smp.cc[j], smp.ym[j], smp.kxx[j], mu, l22, flag);
-      if (s == 0 && half == 0) {
+      if (s == 0) {
         smp.L22[(size_t)j * b + c] = l22;
         smp.flags[(size_t)j * b + c] = flag;
       }
@@ -2225,6 +2215,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   //      groups compacted in group order; C. rounds of 64 passing groups, one per lane (rank
   //      rows loaded together): cell masks, the passing cells' key indices appended to the
   //      term list in (group, cell) order, full rounds of 64 terms evaluated as they fill ----
+  double acc[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.0;
   auto term_add = [&](const unsigned long long key) {
@@ -2299,16 +2290,13 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
   };
   int tn = 0;   // terms in the list (wave-uniform)
   unsigned long long pf_mark = EVR_KD_PROF == 2 ? wall_clock64() : 0;
-  // this wave's 64-group chunks: q = half, half + SPL, ... (every chunk when SPL = 1), taken
-  // KW_NCH at a time; pl entries are 64 k + lane within the block, group 64 (q0 + SPL k) + lane
-  const int nchunks = (Gs + 63) >> 6;
-  for (int q0 = half; q0 < nchunks; q0 += SPL * KW_NCH) {
-    const int nch = min(KW_NCH, (nchunks - q0 + SPL - 1) / SPL);
+  for (int G0 = 0; G0 < Gs; G0 += 64 * KW_NCH) {
+    const int nch = min(KW_NCH, (Gs - G0 + 63) >> 6);
     // A. group tests of up to KW_NCH chunks: one minima load per chunk and lane, all in flight
     uint4 gm[KW_NCH];
 #pragma unroll
     for (int k = 0; k < KW_NCH; ++k) {
-      const int g = 64 * (q0 + SPL * k) + lane;
+      const int g = G0 + 64 * k + lane;
       // past the sample's groups: 0x7FFF ranks (cells_kd's padding), which fail the packed
       // signed compare (0xFFFF would read as -1 and pass)
       gm[k] = (k < nch && g < Gs) ? gmin[g] : make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
@@ -2327,8 +2315,7 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     //    masks -> the cells' key indices appended in (group, cell) order, term rounds as they fill
     for (int p0 = 0; p0 < np_; p0 += 64) {
       const int i = p0 + lane;
-      const int pv = i < np_ ? (int)pl[i] : 0;
-      const int g = i < np_ ? 64 * (q0 + SPL * (pv >> 6)) + (pv & 63) : -1;
+      const int g = i < np_ ? G0 + (int)pl[i] : -1;
       const unsigned int mB = g >= 0 ? cell_mask(g) : 0u;
       int tot;
       int p = tn + wave_scan_excl(__popc(mB), &tot);
@@ -2382,30 +2369,16 @@ __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
     acc[v] = x;
   }
-  if (SPL > 1 && half > 0 && lane == 0) {
+  if (lane == 0) {
+    sval[(size_t)s * b + c] = acc[0];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) kw_half[wave][v] = acc[v];
+    for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = 1.0 / (double)S * acc[1 + j];
   }
-  if (EVR_KD_PROF == 2 && kd.counters && lane == 0 && half == 0) {
+  if (EVR_KD_PROF == 2 && kd.counters && lane == 0) {
     pf_[5] = wall_clock64();
     unsigned long long* r = kd.counters + 16 + 8 * ((size_t)s * b + c);
 #pragma unroll
     for (int q = 0; q < 8; ++q) r[q] = pf_[q];
-  }
-  }   // cin
-  if (SPL > 1) {
-    __syncthreads();   // every wave reaches it (no early return at SPL > 1)
-    if (cin && half == 0) {
-#pragma unroll
-      for (int q = 1; q < SPL; ++q)
-#pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v] += kw_half[wave + q][v];
-    }
-  }
-  if (cin && half == 0 && lane == 0) {
-    sval[(size_t)s * b + c] = acc[0];
-#pragma unroll
-    for (int j = 0; j < M; ++j) dG[((size_t)s * M + j) * b + c] = 1.0 / (double)S * acc[1 + j];
   }
 }
 
@@ -2586,17 +2559,10 @@ template <int M>
 static int hvi_kdw_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
                           double* dG, const KbSamples& smp) {
   const size_t lds = kw_lds_bytes(st->pts_stride, M);
-  const char* e = std::getenv("EVR_KDW_SPLIT");   // read per call (plans capture it)
-  const int spl = (e && e[0] == '1') ? 1 : 2;
-  const int ncg = cdiv(b, KW_WAVES / spl);
+  const int ncg = cdiv(b, KW_WAVES);
   const int wgs = cdiv(st->S, 8) * 8 * ncg;
-  if (spl == 1) {
-    EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdw<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hvi_kdw<M, 1><<<wgs, 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG);
-  } else {
-    EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdw<M, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hvi_kdw<M, 2><<<wgs, 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG);
-  }
+  EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdw<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hvi_kdw<M><<<wgs, 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG);
   EVR_LAUNCH_CHECK();
   return 0;
 }

@@ -919,10 +919,19 @@ def sobol_scramble(dim: int, seed: int, d0: int = 0, nd: Optional[int] = None):
         raise ValueError("sobol_scramble: dims out of range")
     if dim > SOBOL_MAXDIM:
         return None
-    V = _sobol_directions(dim)[d0:d0 + nd].clone()
-    shift = torch.empty(nd, dtype=torch.long)
+    V, shift = _pinned_scramble_out(dim, d0, nd)
     call("evr_sobol_scramble_range", dim, int(seed), d0, nd, V.data_ptr(), shift.data_ptr())
     return V, shift
+
+
+def _pinned_scramble_out(dim: int, d0: int, nd: int):
+    """(direction numbers of dims [d0, d0+nd), shift buffer) in pinned host memory when a GPU
+    is present, so that sobol_normal's uploads are asynchronous (a pageable .to(device) blocks
+    the host until the stream has drained)."""
+    pin = torch.cuda.is_available()
+    V = torch.empty(nd, 30, dtype=torch.long, pin_memory=pin)
+    V.copy_(_sobol_directions(dim)[d0:d0 + nd])
+    return V, torch.empty(nd, dtype=torch.long, pin_memory=pin)
 
 
 class SobolStream:
@@ -944,8 +953,7 @@ class SobolStream:
         nd = dim - d0 if nd is None else nd
         if dim > SOBOL_MAXDIM or dim > self.max_dim or nd < 1:
             return None
-        V = _sobol_directions(dim)[d0:d0 + nd].clone()
-        shift = torch.empty(nd, dtype=torch.long)
+        V, shift = _pinned_scramble_out(dim, d0, nd)
         call("evr_sobol_scramble_stream", self._h, dim, d0, nd, V.data_ptr(), shift.data_ptr())
         return V, shift
 
@@ -978,8 +986,8 @@ def sobol_normal(n: int, dim: int, seed: int, device, d0: int = 0, nd: Optional[
     if nd == 0:
         return out
     V, shift = scrambled if scrambled is not None else sobol_scramble(dim, seed, d0, nd)
-    Vd = V.to(device, non_blocking=False)
-    sd = shift.to(device)
+    Vd = V.to(device, non_blocking=V.is_pinned())
+    sd = shift.to(device, non_blocking=shift.is_pinned())
     call("evr_sobol_normal", _stream(), n, nd, 0, Vd.data_ptr(), sd.data_ptr(), layout, m, out.data_ptr())
     return out
 

@@ -249,16 +249,13 @@ def test_restart_balanced_scan_slices(restart_variant):
     assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
 
 
-@pytest.mark.parametrize("split", ["2", "1"])
-def test_restart_wave_scan_long_term_lists(restart_variant, split, monkeypatch):
+def test_restart_wave_scan_long_term_lists(restart_variant):
     """hvi_kdw on candidates dominating most of the front (hundreds of terms per sample and
-    candidate: many 64-term rounds and list remainders) against the three-launch chain, with
-    two waves per (sample, candidate) (default, each walking every other 64-group chunk) and
-    with one (EVR_KDW_SPLIT=1); both batch-invariant bitwise (a candidate's result depends on
-    its own cells only: the first 9 candidates alone equal their values in the batch of 32)."""
+    candidate: many 64-term rounds and list remainders) against the three-launch chain, and
+    batch-invariant bitwise (a candidate's result depends on its own cells only: the first 9
+    candidates alone equal their values in the batch of 32)."""
     from everest_amd import ops
 
-    monkeypatch.setenv("EVR_KDW_SPLIT", split)
     restart_variant(3)
     kd, dense, lo, hi, d = _pair(240, 6, 5, 256, seed=11, prune=False)
     b = 32

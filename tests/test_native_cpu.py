@@ -201,7 +201,7 @@ def test_evaluation_chain_kernels_use_no_scratch():
     ks = kr.kernels(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "everest_amd", "_lib",
                                  "libeverest_amd.so"))
     names = dict(zip(kr.demangle(sorted(ks)), [ks[k] for k in sorted(ks)]))
-    hot = re.compile(r"evr::(qs_fwd|qs_bwd|qs_dx_reduce|hvi_kdb<[1-5]>|hvi_kdw<[1-5], 2>|hvi_kd2<[1-5],|hvi_kd3<[1-5]>|hvi_thresholds|"
+    hot = re.compile(r"evr::(qs_fwd|qs_bwd|qs_dx_reduce|hvi_kdb<[1-5]>|hvi_kdw<[1-5]>|hvi_kd2<[1-5],|hvi_kd3<[1-5]>|hvi_thresholds|"
                      r"hvi_reduce|kmat_kernel|kmat_mfma_kernel|kmat_mfma_sym|qn_samples_norms|qn_proj|qn_gen_gr|qn_bwd_coef|"
                      r"qn_mean_row|qn_norms_rows|kcross_grad_kernel<(8|16|32)>|kls_grad_kernel|chol_|tri_inv|"
                      r"trsm16|pareto_f32_kernel<[1-5]>|bd_build_kernel<[1-5],|cells_kd_kernel<[1-5],|"
