@@ -773,19 +773,22 @@ __global__ __launch_bounds__(256) void kls_grad_kernel(int kind, int n, int d, c
     for (int k = 0; k < MAXD; ++k)
       if (k < d) acc[k] = fma(s, sq[k] * il[k], acc[k]);
   }
-  for (int k = 0; k < d; ++k) {
-    double v = 0.0;
+  // all d sums at once: a fixed xor butterfly per wave, then the four waves' partials in wave
+  // order (one barrier; the former per-dimension LDS tree took 9 barriers per dimension)
+  const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int kk = 0; kk < MAXD; ++kk)
-      if (kk == k) v = acc[kk];
-    red[tid] = v;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
+  for (int k = 0; k < MAXD; ++k) {
+    if (k < d) {
+      double v = acc[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) red[wave * MAXD + k] = v;
     }
-    if (tid == 0) part[((size_t)b * n + i) * d + k] = red[0];
-    __syncthreads();
+  }
+  __syncthreads();
+  if (tid < d) {
+    const double v = ((red[tid] + red[MAXD + tid]) + red[2 * MAXD + tid]) + red[3 * MAXD + tid];
+    part[((size_t)b * n + i) * d + tid] = v;
   }
 }
 

@@ -39,27 +39,28 @@ int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const doubl
 
 // W = alpha alpha^T - K^-1 = alpha alpha^T - L^-T L^-1 in one launch of the gemm_core.hpp
 // engine (A = L^-T: L^-1 read m-contiguous).  L^-1 is lower triangular, so W[i][j] sums over
-// k >= max(i, j) only: tile (by, bx) contracts over k >= 32 max(by, bx) — a third of the dense
-// product's flops, the skipped terms exact zeros.  Tiles are dispatched in shells of equal
-// max(by, bx), longest k range first, outputs interleaved; the rank-1 alpha alpha^T term is
-// the epilogue (the former separate alpha alpha^T GEMM launch).
+// k >= max(i, j) only: tile (by, bx) contracts over k >= 32 max(by, bx), the skipped terms
+// exact zeros.  W is symmetric: only the lower tiles (by >= bx) are formed — ascending by,
+// i.e. longest k range first, outputs interleaved — and each off-diagonal tile is also written
+// transposed, through LDS as 256-byte row segments (W exactly symmetric; half the MFMA work of
+// forming every tile).  The rank-1 alpha alpha^T term is the epilogue.
 using MllW = DgCfg<32, 32, 16, true>;
 
 template <bool VEC>
 __global__ __launch_bounds__(256, 4) void mll_w_kernel(int n, int B, const double* __restrict__ Linv,
                                                        const double* __restrict__ alpha, double* __restrict__ W) {
   using C = MllW;
-  __shared__ double lds[C::LDS_DOUBLES];
+  static_assert(C::BM == C::BN, "square tiles");
+  __shared__ double lds[C::LDS_DOUBLES > C::BM * (C::BN + 1) ? C::LDS_DOUBLES : C::BM * (C::BN + 1)];
   const int f = blockIdx.x, j = f % B, t = f / B;
-  int sh = (int)sqrt((double)t);
-  while (sh * sh > t) --sh;
-  while ((sh + 1) * (sh + 1) <= t) ++sh;
-  const int pp = t - sh * sh;
-  const int by = pp <= sh ? sh : pp - sh - 1, bx = pp <= sh ? pp : sh;
+  int by = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);   // lower tiles, row-major: row by holds by + 1
+  while ((by + 1) * (by + 2) / 2 <= t) ++by;
+  while (by * (by + 1) / 2 > t) --by;
+  const int bx = t - by * (by + 1) / 2;
   const int m0 = by * C::BM, n0 = bx * C::BN;
   const size_t nn = (size_t)n * n;
   const double* Lj = Linv + j * nn;
-  const int kbeg = max(m0, n0);
+  const int kbeg = m0;   // max(m0, n0): bx <= by
   dg_double4 acc[C::FM][C::FN];
   dg_mainloop<C>(
       lds, kbeg, n,
@@ -72,10 +73,28 @@ __global__ __launch_bounds__(256, 4) void mll_w_kernel(int n, int B, const doubl
       acc);
   const double* aj = alpha + (size_t)j * n;
   double* Wj = W + j * nn;
+  if (by == bx) {
+    dg_for_each<C>(acc, [&](int r, int c, double v) {
+      const int row = m0 + r, col = n0 + c;
+      if (row < n && col < n) Wj[(size_t)row * n + col] = aj[row] * aj[col] - v;
+    });
+    return;
+  }
+  __syncthreads();   // every wave's main-loop LDS reads are done
+  double(*T)[C::BN + 1] = reinterpret_cast<double(*)[C::BN + 1]>(lds);
   dg_for_each<C>(acc, [&](int r, int c, double v) {
     const int row = m0 + r, col = n0 + c;
-    if (row < n && col < n) Wj[(size_t)row * n + col] = aj[row] * aj[col] - v;
+    const double w = (row < n && col < n) ? aj[row] * aj[col] - v : 0.0;
+    T[r][c] = w;
+    if (row < n && col < n) Wj[(size_t)row * n + col] = w;
   });
+  __syncthreads();
+  // the transposed tile: row n0 + c of W holds T[.][c]; a thread per (row, 8-byte column)
+  for (int e = threadIdx.x; e < C::BM * C::BN; e += 256) {
+    const int c = e / C::BM, r = e - c * C::BM;
+    const int row = n0 + c, col = m0 + r;
+    if (row < n && col < n) Wj[(size_t)row * n + col] = T[r][c];
+  }
 }
 
 // hx: [ls (B x d) | noise (B) | constant (B) | sequence number]; also the residuals
@@ -145,9 +164,9 @@ static int mll_chain(hipStream_t s, evr_mll_plan* p, const double* dhx, double* 
   if (int rc = dg_gemm(s, false, n, 1, n, 1.0, p->Linv, n, nn, p->r, 1, n, 0.0, p->v, 1, n, B, p->mvw)) return rc;
   if (int rc = dg_gemm(s, true, n, 1, n, 1.0, p->Linv, n, nn, p->v, 1, n, 0.0, p->alpha, 1, n, B, p->mvw)) return rc;
   {
-    const int T = cdiv(n, MllW::BM);
-    if (n % 2 == 0) mll_w_kernel<true><<<T * T * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
-    else mll_w_kernel<false><<<T * T * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
+    const int T = cdiv(n, MllW::BM), lower = T * (T + 1) / 2;
+    if (n % 2 == 0) mll_w_kernel<true><<<lower * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
+    else mll_w_kernel<false><<<lower * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);
     EVR_LAUNCH_CHECK();
   }
   if (int rc = evr_kernel_lengthscale_grad(s, p->kind, B, n, d, p->Xn, p->ls, W, p->gls, p->gw)) return rc;

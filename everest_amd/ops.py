@@ -928,7 +928,7 @@ def _pinned_scramble_out(dim: int, d0: int, nd: int):
     """(direction numbers of dims [d0, d0+nd), shift buffer) in pinned host memory when a GPU
     is present, so that sobol_normal's uploads are asynchronous (a pageable .to(device) blocks
     the host until the stream has drained)."""
-    pin = torch.cuda.is_available()
+    pin = os.environ.get("EVR_SOBOL_PINNED", "1") != "0" and torch.cuda.is_available()
     V = torch.empty(nd, 30, dtype=torch.long, pin_memory=pin)
     V.copy_(_sobol_directions(dim)[d0:d0 + nd])
     return V, torch.empty(nd, dtype=torch.long, pin_memory=pin)
