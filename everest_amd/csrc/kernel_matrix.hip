@@ -703,11 +703,14 @@ __global__ void kcross_grad_reduce(int nsplit, int n2, int d, const double* __re
   dX2[e] = v * (sc2 ? sc2[k] : 1.0);
 }
 
-// row split of kcross_grad: fill >= 512 blocks, >= 16 rows per block
+// row split of kcross_grad: up to 2048 blocks, >= 8 rows per block (two per row group).  At
+// the b = 512 evaluation pass (n1 = 512, 8 column tiles) that is 512 blocks: two waves per
+// SIMD instead of one (the 16-row floor left 256 blocks, one wave per SIMD and nothing to
+// hide the G loads behind: 18.8 us for a 10.5 MB read)
 static int kcross_nsplit(int n1, int n2) {
   const int ct = cdiv(n2, 64);
-  int ns = cdiv(512, ct);
-  ns = std::max(1, std::min(ns, cdiv(n1, 16)));
+  int ns = cdiv(2048, ct);
+  ns = std::max(1, std::min(ns, cdiv(n1, 8)));
   return ns;
 }
 

