@@ -73,7 +73,7 @@ def main():
     fs, names = per_step(fdir, "FETCH_SIZE")
     ws, _ = per_step(wdir, "WRITE_SIZE")
     res = {}
-    if suffix and os.path.exists(out):
+    if os.path.exists(out):   # merge: keys of other passes (other suffixes) are kept
         with open(out) as fi:
             res = json.load(fi)
     for op, _ in OPS:
