@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "qs_tail.hpp"
 
 #ifndef EVR_KD_EXP
 #define EVR_KD_EXP 0   // experiment switches of the instrumented builds (0 = production)
@@ -2088,13 +2089,22 @@ __host__ __device__ inline size_t kw_lds_bytes(int stride, int M) {
 // (256, 5): 5 waves per SIMD — at b = 20 the grid (S x 5 candidate groups = 1280 workgroups at
 // S = 256) is resident in one round; unbounded the compiler took 100 VGPRs (4 per SIMD).
 // M = 8 would spill at that bound and keeps 4.
+// qtl.M != null: workgroups from nkdw on run the restart backward's training-row class
+// (qs_tail.hpp) — dispatched last, into the slots the light (sample, candidate) waves free.
 template <int M>
 __global__ __launch_bounds__(256, M <= 7 ? 5 : 4) void hvi_kdw(int b, int S, int ncg, const double* __restrict__ G, HviKd kd,
-                                               KbSamples smp, double* __restrict__ sval, double* __restrict__ dG) {
+                                               KbSamples smp, double* __restrict__ sval, double* __restrict__ dG,
+                                               QsTail qtl, int nkdw, int ntail_first) {
   constexpr int NV = M + 1;
   using K = CellKey<M>;
   extern __shared__ __align__(16) unsigned char kw_dyn[];
-  const int wid = blockIdx.x, xcd = wid & 7, slot = wid >> 3;
+  // ntail_first > 0: the tail's workgroups come first instead (a multiple of 8: the scan's
+  // workgroup -> XCD map is unchanged)
+  if (qtl.M && ((int)blockIdx.x >= nkdw + ntail_first || (int)blockIdx.x < ntail_first)) {
+    qs_tail_tile(qtl, ntail_first ? blockIdx.x : blockIdx.x - nkdw, (double*)kw_dyn);
+    return;
+  }
+  const int wid = blockIdx.x - ntail_first, xcd = wid & 7, slot = wid >> 3;
   const int s = (slot / ncg) * 8 + xcd, cg = slot - (slot / ncg) * ncg;
   if (s >= S) return;   // the grid covers S rounded up to 8 samples: whole workgroups leave
   // the wave index (hence the candidate c) is wave-uniform: scalar registers, not a VGPR
@@ -2557,12 +2567,24 @@ static bool hvi_kdw_applies(const evr_qnehvi_state* st, int b) {
 
 template <int M>
 static int hvi_kdw_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, double* sval,
-                          double* dG, const KbSamples& smp) {
-  const size_t lds = kw_lds_bytes(st->pts_stride, M);
+                          double* dG, const KbSamples& smp, const QsTail* tail = nullptr) {
+  size_t lds = kw_lds_bytes(st->pts_stride, M);
   const int ncg = cdiv(b, KW_WAVES);
   const int wgs = cdiv(st->S, 8) * 8 * ncg;
+  QsTail tl{};
+  int twgs = 0;
+  if (tail) {
+    tl = *tail;
+    twgs = st->m * tl.za * tl.nt;
+    lds = std::max(lds, (size_t)QT_LDS_DOUBLES * 8);
+  }
   EVR_HIP(hipFuncSetAttribute((const void*)hvi_kdw<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hvi_kdw<M><<<wgs, 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG);
+  // EVR_QS_TAIL_FIRST=1: the tail's workgroups dispatched before the scan's (A/B)
+  const char* tfe = std::getenv("EVR_QS_TAIL_FIRST");
+  const bool tfirst = tfe && tfe[0] == '1';
+  const int nfirst = (tfirst && twgs) ? cdiv(twgs, 8) * 8 : 0;
+  hvi_kdw<M><<<wgs + (nfirst ? nfirst : twgs), 256, lds, s>>>(b, st->S, ncg, G, hvi_kd_of(st), smp, sval, dG, tl, wgs,
+                                                               nfirst);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -2790,16 +2812,21 @@ bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b) {
   return on && (hvi_kdw_applies(st, b) || hvi_kdb_applies(st, b)) && st->obj_a && st->obj_b && st->zq;
 }
 
+// tail (optional): the restart backward's training-row class, run in hvi_kdw's tail; *tail_ran
+// says whether it was (hvi_kdb has no tail: the caller launches it itself)
 int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
-                  int nrt_used, double* L22, int* flags, double* sval, double* dG) {
+                  int nrt_used, double* L22, int* flags, double* sval, double* dG, const QsTail* tail,
+                  bool* tail_ran) {
+  if (tail_ran) *tail_ran = false;
   EVR_CHECK(R && P && L22 && flags && sval && dG && hvi_kdb_fused_applies(st, b), "hvi_kdb_fused: bad arguments");
   KbSamples smp{R, P, st->c, st->ym, st->ys, st->kxx, st->zq, st->obj_a, st->obj_b, L22, flags,
                 st->n, st->nb, qn_nh(st), nrt, nrt_used};
   int rc = 0;
   if (hvi_kdw_applies(st, b)) {
-#define L(MM) rc = hvi_kdw_launch<MM>(s, st, b, nullptr, sval, dG, smp)
+#define L(MM) rc = hvi_kdw_launch<MM>(s, st, b, nullptr, sval, dG, smp, tail)
     EVR_M_SWITCH(st->m, L);
 #undef L
+    if (tail_ran) *tail_ran = tail != nullptr && rc == 0;
     return rc;
   }
 #define L(MM) rc = hvi_kdb_launch<MM>(s, st, b, nullptr, sval, dG, smp)

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "qs_tail.hpp"
 #include "lbfgsb.hpp"
 #include "../../include/everest_amd.h"
 
@@ -44,7 +45,9 @@ int qs_done_words(int b, int d);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags,
-                unsigned long long* plast);
+                unsigned long long* plast, bool tail_done);
+bool qs_tail_make(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X, const double* R,
+                  double* dXp, QsTail* t);
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
@@ -54,7 +57,8 @@ constexpr int QS_TILE_ROWS = 16;
 constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
 int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
-                  int nrt_used, double* L22, int* flags, double* sval, double* dG);
+                  int nrt_used, double* L22, int* flags, double* sval, double* dG, const QsTail* tail,
+                  bool* tail_ran);
 
 // b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
 // EVR_SMALL=0 keeps the 64 x 64-tile path for A/B timing and the parity test
@@ -203,13 +207,18 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   }
   double* dG = (double*)(w + p->L.dG);
   if (small && p->backward && p->L.fused_scan && hvi_kdb_fused_applies(st, b)) {
-    // the sampling step inside the restart scan's staging (one launch less); G is not formed
+    // the sampling step inside the restart scan's staging (one launch less); G is not formed.
+    // The backward's training-row class rides in the scan's tail (qs_tail.hpp)
+    double* dxp = (double*)(w + p->L.dxp);
+    QsTail tl;
+    const bool tail = qs_tail_make(st, md, b, X, R, dxp, &tl);
+    bool tail_ran = false;
     if (int rc = hvi_kdb_fused(s, st, b, R, P, cdiv(qn_rows(st), QS_TILE_ROWS), cdiv(st->n + st->nb, QS_TILE_ROWS),
-                               L22, flags, hw, dG))
+                               L22, flags, hw, dG, tail ? &tl : nullptr, &tail_ran))
       return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       hw, flags, plast);
+    return qs_backward(s, st, md, b, X, R, L22, dG, dxp, p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
+                       hw, flags, plast, tail_ran);
   }
   if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : QN_NORM_TILE)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
@@ -219,13 +228,13 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     if (int rc = evr_hvi_restart_fb(s, st, b, G, hw, dG)) return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       hw, flags, plast);
+                       hw, flags, plast, false);
   }
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (small) {
     if (done) *done = hout ? qs_done_words(b, d) : 0;
     return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       nullptr, nullptr, plast);
+                       nullptr, nullptr, plast, false);
   }
   double* dKx = (double*)(w + p->L.dKx);
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;

@@ -26,6 +26,7 @@
 #include <cstring>
 
 #include "common.hpp"
+#include "qs_tail.hpp"
 #include "../../include/everest_amd.h"
 
 using double4_t = __attribute__((ext_vector_type(4))) double;
@@ -185,7 +186,10 @@ constexpr int QS_RC = 128;   // rows of M per backward chunk
 constexpr int QS_SMAX = 1024;   // samples whose z values the backward stages in LDS
 // SPLIT: baseline rows in M (nb > 0, the literal "split" root, A/B only): a third row class;
 // one workgroup per CU there (its registers would spill at two)
-template <bool SPLIT>
+// TAIL: the training-row class is done elsewhere (qs_tail.hpp, in the scan's tail): the splits
+// cover the sample rows only, and the class coefficient cf0 goes to cfo[j][c] for the dX
+// reduction (written by the (tile 0, split 0) workgroup of each output)
+template <bool SPLIT, bool TAIL>
 __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
                                               const double* __restrict__ M, const double* __restrict__ R,
                                               const double* __restrict__ dG, const double* __restrict__ L22,
@@ -193,7 +197,8 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
                                               const double* __restrict__ oa, const double* __restrict__ Xn,
                                               const double* __restrict__ X, const double* __restrict__ shift,
                                               const double* __restrict__ scale, const double* __restrict__ ls,
-                                              double* __restrict__ dXp, int ntile, int rows_per) {
+                                              double* __restrict__ dXp, int ntile, int rows_per, int np_all,
+                                              double* __restrict__ cfo, int zsb, QsTail qtl) {
   __shared__ double cf[3][QS_B];
   __shared__ double red[8][QS_B][2];
   __shared__ double zl[QS_SMAX];   // z_j of the samples (the coefficient rounds read them here)
@@ -207,6 +212,10 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
   auto Bs = reinterpret_cast<double(*)[QS_B + 1]>(lds + MS_SZ);
   auto dk = reinterpret_cast<double(*)[QS_BI][QS_B + 1]>(lds);
   auto gx = reinterpret_cast<double(*)[QS_B][QS_MAXD]>(lds + DK_SZ);
+  if (TAIL && (int)blockIdx.z >= zsb) {   // the training-row class (EVR_QS_TAIL=bwd): its own workgroups
+    qs_tail_tile(qtl, ((int)blockIdx.y * qtl.za + ((int)blockIdx.z - zsb)) * qtl.nt + blockIdx.x, lds);
+    return;
+  }
   const int tile = blockIdx.x, j = blockIdx.y, z = blockIdx.z, i0 = tile * QS_BI;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Rr = n + nb + nh + 1;
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
 #endif
   QS_STAMP(0);
   // this split's rows of M; the mean row (Rr - 1, a rank-1 term) is added in the epilogue
-  const int rbeg = z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
+  const int rbeg = (TAIL ? n + nb : 0) + z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
   const double aj = oa[j], sj = ys[j];
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Rj = R + (size_t)j * Rr * b;
@@ -282,7 +291,11 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     }
     s0 += 8 * CU;
   };
-  bool pend = s0 < S;
+  // TAIL with the sample rows in M (nh = S, one split over all of them): the coefficients are
+  // summed from the staged chunks in LDS (Bs holds a_j dG of the chunk's samples) in the same
+  // per-thread sample order — no separate dG loads or their dependent rounds
+  const bool coef_lds = TAIL && nh == S && zsb == 1;
+  bool pend = !coef_lds && s0 < S;
   if (pend) coef_load();
 #pragma unroll
   for (int u = 0; u < QS_SMAX / 256; ++u) {   // visible after the first chunk's barrier
@@ -342,6 +355,17 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
         }
       }
     }
+    if (coef_lds) {
+#pragma unroll
+      for (int v = 0; v < QS_RC / 8; ++v) {
+        const int rr = g_ + 8 * v, sidx = rc + rr - n - nb;
+        if (sidx < S) {
+          const double dy = Bs[rr][cc_];
+          dmu += dy;
+          dl = fma(dy, zl[sidx], dl);
+        }
+      }
+    }
     if (pend) {   // the coefficient round issued with this chunk's loads
       coef_acc();
       pend = s0 < S;
@@ -367,6 +391,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     cf[0][tid] = -2.0 * sj * sj * dbr;
     cf[1][tid] = -2.0 * dbr;
     cf[2][tid] = sj * u;
+    if (TAIL && tile == 0 && z == 0 && tid < b) cfo[(size_t)j * b + tid] = -2.0 * sj * sj * dbr;
   }
   QS_STAMP(2);
   // the epilogue's training rows and mean-row entries, loaded before the dk exchange so their
@@ -388,7 +413,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     const double f0a = cf[0][i], f0b = cf[0][16 + i], f1a = cf[1][i], f1b = cf[1][16 + i];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      double v0 = fma(f0a, aA0[q], aB0[q]), v1 = fma(f0b, aA1[q], aB1[q]);
+      double v0 = TAIL ? aB0[q] : fma(f0a, aA0[q], aB0[q]), v1 = TAIL ? aB1[q] : fma(f0b, aA1[q], aB1[q]);
       if (SPLIT) {
         v0 = fma(f1a, aC0[q], v0);
         v1 = fma(f1b, aC1[q], v1);
@@ -438,8 +463,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
       for (int q = 1; q < 8; ++q) v += gx[q][cc][k];
       // element-major partials (dXp[c][k][p], p = (j, z, tile)): the reduction reads each
       // element's partials contiguously
-      const size_t np = (size_t)gridDim.y * gridDim.z * ntile;
-      if (cc < b && k < d) dXp[((size_t)cc * d + k) * np + ((size_t)j * gridDim.z + z) * ntile + tile] = v;
+      if (cc < b && k < d) dXp[((size_t)cc * d + k) * np_all + ((size_t)j * zsb + z) * ntile + tile] = v;
     }
   }
   QS_STAMP(4);
@@ -463,7 +487,8 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
                                                     const double* seqp,
                                                     const double* __restrict__ sval, int S, int m,
                                                     const int* __restrict__ flags,
-                                                    unsigned long long* __restrict__ plast, int light) {
+                                                    unsigned long long* __restrict__ plast, int light,
+                                                    int npB, int ntA, const double* __restrict__ cfo) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool ein = e < b * d;
   const int k = e % d;
@@ -478,9 +503,18 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   // one extra memory round trip per load group)
   const double* src = dXp + (size_t)(ein ? e : 0) * np;
   const double sck = scale ? scale[k] : 1.0;   // issued with the first loads, used at the end
-  double x[8];
+  // partials p >= npB (the training-row class from the scan's tail, qs_tail.hpp) carry their
+  // output's coefficient cf0[j][c], j = (p - npB) / ntA; the others weigh 1 (fma(1, x, v) is
+  // v + x exactly)
+  const int ce = ein ? e / d : 0;
+  auto wsrc = [&](int p) { return cfo + (size_t)min(max(p - npB, 0) / max(ntA, 1), m - 1) * b + ce; };
+  constexpr int NU = 10;
+  double x[NU], wv[NU];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) x[u] = src[min(lane + 64 * u, np - 1)];
+  for (int u = 0; u < NU; ++u) {
+    x[u] = src[min(lane + 64 * u, np - 1)];
+    wv[u] = cfo ? *wsrc(lane + 64 * u) : 1.0;
+  }
   const bool acq_e = ein && sval && e < b;
   double sv[4] = {0.0, 0.0, 0.0, 0.0};
   int fl = 0;
@@ -513,10 +547,10 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
   }
   double v = 0.0;
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (ein && lane + 64 * u < np) v += x[u];
+  for (int u = 0; u < NU; ++u)
+    if (ein && lane + 64 * u < np) v = fma(lane + 64 * u >= npB ? wv[u] : 1.0, x[u], v);
   if (ein)
-    for (int p = lane + 512; p < np; p += 64) v += src[p];
+    for (int p = lane + 64 * NU; p < np; p += 64) v = fma(cfo && p >= npB ? *wsrc(p) : 1.0, src[p], v);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if (lane == 0 && ein) {
@@ -563,24 +597,57 @@ int qs_ntile_fwd(const evr_qnehvi_state* st) { return cdiv(qn_rows(st), QS_FR); 
 
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b) { return (size_t)st->m * qs_ntile_fwd(st) * 2 * b; }
 
-// backward row splits over the Rr - 1 non-mean rows: as many as keep every workgroup resident
-// at once (two per CU), in whole 128-row chunks
+// The training-row class apart from the sample rows (qs_tail.hpp), fused root only (nb = 0).
+// EVR_QS_TAIL (read per call: plans read it once, at capture): "bwd" (default) — its
+// workgroups ride in the backward's launch beside the sample-row workgroups (those hold one
+// workgroup on 160 of the 256 CUs); "kdw" — in the restart scan's tail (measured: the scan
+// holds every workgroup slot, so the tail stretches it by ~4 us); "0" — inside qs_bwd's
+// workgroups as before
+static int qs_tail_mode(const evr_qnehvi_state* st) {
+  const char* e = std::getenv("EVR_QS_TAIL");
+  if (st->nb != 0 || (e && e[0] == '0')) return 0;
+  return (e && !std::strcmp(e, "kdw")) ? 2 : 1;
+}
+bool qs_tail_on(const evr_qnehvi_state* st) { return qs_tail_mode(st) != 0; }
+// training rows per tail workgroup's split: 256 (64 per wave, two load batches); EVR_QS_TAIL_ROWS
+// (a multiple of 16) for A/B
+static int qs_tail_rows() {
+  const char* e = std::getenv("EVR_QS_TAIL_ROWS");
+  const int v = e ? std::atoi(e) : 0;
+  return (v >= 16 && v % 16 == 0) ? v : 256;
+}
+static int qs_tail_za(const evr_qnehvi_state* st) { return cdiv(st->n, qs_tail_rows()); }
+
+// rows the backward's splits cover: every non-mean row, or (tail) the sample rows only
+static int qs_bwd_rows(const evr_qnehvi_state* st) {
+  return qs_tail_on(st) ? qn_rows(st) - 1 - st->n - st->nb : qn_rows(st) - 1;
+}
+
+// backward row splits over those rows: as many as keep every workgroup resident at once (two
+// per CU), in whole 128-row chunks
 static int qs_zsplit(const evr_qnehvi_state* st) {
-  const int tiles = cdiv(st->n, QS_BI) * st->m, nch = cdiv(qn_rows(st) - 1, QS_RC);
+  if (qs_tail_on(st)) return 1;   // one split over the sample rows: the coefficients come from its chunks
+  const int tiles = cdiv(st->n, QS_BI) * st->m, nch = std::max(1, cdiv(qs_bwd_rows(st), QS_RC));
   const int zs = std::max(1, std::min(nch, 512 / std::max(1, tiles)));
   return cdiv(nch, cdiv(nch, zs));
 }
 
 static int qs_rows_per(const evr_qnehvi_state* st) {
-  const int nch = cdiv(qn_rows(st) - 1, QS_RC);
+  const int nch = std::max(1, cdiv(qs_bwd_rows(st), QS_RC));
   return cdiv(nch, qs_zsplit(st)) * QS_RC;
 }
 
 // workgroups of qs_dx_reduce = completion words it writes in host mode (<= 64 at b <= 32, d <= 8)
 int qs_done_words(int b, int d) { return cdiv(b * d, 4); }
 
+// dX partials per element: the backward's (output, split, tile) and, with the tail, the tail's
+static size_t qs_np_bwd(const evr_qnehvi_state* st) { return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI); }
+static size_t qs_np_all(const evr_qnehvi_state* st) {
+  return qs_np_bwd(st) + (qs_tail_on(st) ? (size_t)st->m * qs_tail_za(st) * cdiv(st->n, QS_BI) : 0);
+}
+
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
-  return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI) * b * d;
+  return qs_np_all(st) * b * d + (qs_tail_on(st) ? (size_t)st->m * b : 0);   // + cf0 (m x b)
 }
 
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
@@ -591,27 +658,66 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
   return 0;
 }
 
+__global__ __launch_bounds__(256) void qs_bwd_tail(QsTail t) {
+  __shared__ double lds[QT_LDS_DOUBLES];
+  qs_tail_tile(t, blockIdx.x, lds);
+}
+
+static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                         const double* R, double* dXp, QsTail* t);
+
+// the tail's arguments when it is to run in the restart scan (EVR_QS_TAIL=kdw)
+bool qs_tail_make(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X, const double* R,
+                  double* dXp, QsTail* t) {
+  if (qs_tail_mode(st) != 2) return false;
+  qs_tail_fill(st, md, b, X, R, dXp, t);
+  return true;
+}
+
+static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
+                         const double* R, double* dXp, QsTail* t) {
+  const int nt = cdiv(st->n, QS_BI);
+  *t = QsTail{md->M, R, md->Xn, X, md->shift, md->scale, md->lengthscales, dXp, st->n, qn_rows(st), b, md->d,
+              md->kind, nt, qs_tail_za(st), qs_tail_rows(), (int)qs_np_bwd(st), (int)qs_np_all(st),
+              st->m * qs_tail_za(st) * nt};
+}
+
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
                 double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags,
-                unsigned long long* plast) {
+                unsigned long long* plast, bool tail_done) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
+  const int mode = qs_tail_mode(st);
+  const bool tail = mode != 0;
+  const int npB = (int)qs_np_bwd(st), np = (int)qs_np_all(st);
+  double* cfo = tail ? dXp + (size_t)np * b * d : nullptr;
   EVR_CHECK(st->S <= QS_SMAX, "qs_backward: %d samples exceed the staged %d", st->S, QS_SMAX);
-#define QS_BWD(SPL)                                                                                             \
-  qs_bwd<SPL><<<dim3(nt, st->m, zs), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R, \
-                                                  dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,        \
-                                                  md->scale, md->lengthscales, dXp, nt, rows_per)
-  if (st->nb > 0) QS_BWD(true);
-  else QS_BWD(false);
+  QsTail t{};
+  if (tail) qs_tail_fill(st, md, b, X, R, dXp, &t);
+  if (mode == 2 && !tail_done) {   // the op path (and scans without a tail): its own launch first
+    qs_bwd_tail<<<t.nwg, 256, 0, s>>>(t);
+    EVR_LAUNCH_CHECK();
+  }
+  // mode 1: the tail's workgroups are the launch's z >= 1 slices
+  const int gz = mode == 1 ? zs + t.za : zs;
+#define QS_BWD(SPL, TL)                                                                                         \
+  qs_bwd<SPL, TL><<<dim3(nt, st->m, gz), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, \
+                                                      R, dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,   \
+                                                      md->scale, md->lengthscales, dXp, nt, rows_per, np, cfo,       \
+                                                      mode == 1 ? zs : gz, t)
+  if (st->nb > 0) QS_BWD(true, false);
+  else if (tail) QS_BWD(false, true);
+  else QS_BWD(false, false);
 #undef QS_BWD
   EVR_LAUNCH_CHECK();
   (void)counter;
   // EVR_HOSTFENCE=light: write-through stores instead of the system fence (read per call)
   const char* hf = std::getenv("EVR_HOSTFENCE");
   const int light = (hf && !std::strcmp(hf, "light")) ? 1 : 0;
-  qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(st->m * zs * nt, b, d, dXp, md->scale, dX, acq, hout, seqp, sval,
-                                                   st->S, st->m, flags, plast, light);
+  qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(np, b, d, dXp, md->scale, dX, acq, hout, seqp, sval, st->S, st->m,
+                                                   flags, plast, light, tail ? npB : np,
+                                                   tail ? qs_tail_za(st) * nt : 1, cfo);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -652,7 +758,7 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
   return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, false);
 }
 
 }  // extern "C"

@@ -80,7 +80,7 @@ for st in "$@"; do
     bench) run bench 900 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
-    qsprof) run qsprof 60 tools/_qs_prof ;;
+    qsprof) run qsprof 60 tools/_qs_prof && run qsprof_tail 60 tools/_qs_prof tail ;;
     cholprof)
       run cholprof_sym 60 tools/_chol_prof_sym
       run cholprof_pair 60 tools/_chol_prof_pair ;;

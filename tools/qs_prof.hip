@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <vector>
 #include <algorithm>
+#include <string>
 #include "../everest_amd/csrc/qnehvi_small.hip"
 
 namespace evr {
@@ -31,14 +32,19 @@ static double* dev_fill(size_t n, double lo, double hi, unsigned seed) {
   return d;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // "tail": the backward over the sample rows only (TAIL build of qs_bwd), and the tail kernel
+  // (qs_tail.hpp, standalone launch) timed on its own
+  const bool tail = argc > 1 && std::string(argv[1]) == "tail";
   const int n = 512, nb = 0, S = 256, nh = S, m = 5, b = 20, d = 6, kind = 0;
   const int Rr = n + nb + nh + 1, nt = (n + 15) / 16;
-  const int tiles = nt * m, nch = (Rr - 1 + 127) / 128;
+  const int tiles = nt * m, nch = ((tail ? nh : Rr - 1) + 127) / 128;
   int zs = std::max(1, std::min(nch, 512 / std::max(1, tiles)));
   zs = (nch + (nch + zs - 1) / zs - 1) / ((nch + zs - 1) / zs);
+  if (tail) zs = 1;   // qnehvi_small.hip qs_zsplit: one split over the sample rows
   const int rows_per = ((nch + zs - 1) / zs) * 128;
-  const int np = m * zs * nt;
+  const int za = (n + 255) / 256;
+  const int npB = m * zs * nt, np = npB + (tail ? m * za * nt : 0);
   double* M = dev_fill((size_t)m * Rr * n, -1, 1, 1);
   double* R = dev_fill((size_t)m * Rr * b, -1, 1, 2);
   double* dG = dev_fill((size_t)S * m * b, -1e-3, 1e-3, 3);
@@ -49,24 +55,32 @@ int main() {
   double* Xn = dev_fill((size_t)n * d, 0, 1, 8);
   double* X = dev_fill((size_t)b * d, 0, 1, 9);
   double* ls = dev_fill((size_t)m * d, 0.3, 1.3, 10);
-  double* dXp = dev_fill((size_t)b * d * np, 0, 0, 11);
+  double* dXp = dev_fill((size_t)b * d * np + m * b, 0, 0, 11);
+  double* cfo = dXp + (size_t)b * d * np;
   if (!M || !R || !dG || !L22 || !ys || !zq || !oa || !Xn || !X || !ls || !dXp) {
     printf("{\"error\": \"alloc\"}\n");
     return 1;
   }
   const dim3 grid(nt, m, zs);
+#define QSB(G_, T_)                                                                                                 \
+  do {                                                                                                           \
+    if (tail)                                                                                                    \
+      evr::qs_bwd<false, true><<<G_, T_>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, \
+                                           nullptr, ls, dXp, nt, rows_per, np, cfo, zs, evr::QsTail{});          \
+    else                                                                                                         \
+      evr::qs_bwd<false, false><<<G_, T_>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, \
+                                            nullptr, ls, dXp, nt, rows_per, np, cfo, zs, evr::QsTail{});         \
+  } while (0)
   const int nwg = nt * m * zs;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   for (int r = 0; r < 5; ++r)
-    evr::qs_bwd<false><<<grid, 256>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, nullptr, ls,
-                                dXp, nt, rows_per);
+    QSB(grid, 256);
   (void)hipEventRecord(e0);
   const int reps = 20;
   for (int r = 0; r < reps; ++r)
-    evr::qs_bwd<false><<<grid, 256>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, nullptr, ls,
-                                dXp, nt, rows_per);
+    QSB(grid, 256);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float ms = 0;
@@ -111,6 +125,31 @@ int main() {
       fp[k] += v / nwf;
       fm[k] = std::max(fm[k], v);
     }
+  }
+  float mst = 0;
+  if (tail) {
+    evr::QsTail tl{M, Rf, Xn, X, nullptr, nullptr, ls, dXp, n, Rr, b, d, kind, nt, za, 256, npB, np, m * za * nt};
+    for (int r = 0; r < 5; ++r) evr::qs_bwd_tail<<<m * za * nt, 256>>>(tl);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < reps; ++r) evr::qs_bwd_tail<<<m * za * nt, 256>>>(tl);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&mst, e0, e1);
+    printf("{\"qs_bwd_tail\": {\"grid\": %d, \"launch_us\": %.2f}}\n", m * za * nt, mst * 1e3 / reps);
+    // the default mode: the tail's workgroups as the backward launch's z >= 1 slices
+    const dim3 gc(nt, m, zs + za);
+    auto comb = [&]() {
+      evr::qs_bwd<false, true><<<gc, 256>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr,
+                                            nullptr, ls, dXp, nt, rows_per, np, cfo, zs, tl);
+    };
+    for (int r = 0; r < 5; ++r) comb();
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < reps; ++r) comb();
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float msc = 0;
+    (void)hipEventElapsedTime(&msc, e0, e1);
+    printf("{\"qs_bwd_with_tail\": {\"grid\": [%d, %d, %d], \"launch_us\": %.2f}}\n", nt, m, zs + za, msc * 1e3 / reps);
   }
   printf("{\"qs_fwd\": {\"grid\": [%d, %d], \"launch_us\": %.2f, \"span_us\": %.2f, \"first_chunk_us\": [%.2f, %.2f], "
          "\"other_chunks_us\": [%.2f, %.2f], \"epilogue_us\": [%.2f, %.2f]}}\n",

@@ -5,7 +5,9 @@ the scan's device time (10 launches in one HIP graph between HIP events), the pl
 chain per evaluation (50 back-to-back device-mode graph launches between HIP events), its
 host round trip per evaluation (plan.run_host: launch + chain + completion poll) and the
 native L-BFGS-B's wall time per evaluation (plan.minimize from the Sobol start, 30
-iterations: round trip + the optimiser's host step).  One JSON line."""
+iterations: round trip + the optimiser's host step); kdw_tailscan / kdw_notail: EVR_QS_TAIL=kdw / 0
+(the backward's training-row class in the scan's tail / inside qs_bwd's workgroups instead of
+workgroups of its own in the backward's launch).  One JSON line."""
 import json
 import os
 import sys
@@ -49,7 +51,15 @@ def main():
         b = X.shape[0]
         R, P = ops.qnehvi_small_forward(acqf.state, acqf.model, acqf.gp.cross(Xt), b)
         G, L22, flags = ops.qnehvi_small_samples(acqf.state, R, P, b)
-        for v, name in ((1, "kd3"), (2, "kdb"), (3, "kdw")):
+        for v, name, tl, tr, tf in ((1, "kd3", "bwd", "256", "0"), (2, "kdb", "bwd", "256", "0"),
+                                    (3, "kdw", "bwd", "256", "0"), (3, "kdw_tailscan", "kdw", "256", "0"),
+                                    (3, "kdw_notail", "0", "256", "0")):
+            # EVR_QS_TAIL: the backward's training-row class in workgroups of its own inside the
+            # backward's launch (bwd), in the scan's tail (kdw) or in qs_bwd's workgroups (0);
+            # EVR_QS_TAIL_ROWS: training rows per tail workgroup; EVR_QS_TAIL_FIRST (kdw mode)
+            os.environ["EVR_QS_TAIL"] = tl
+            os.environ["EVR_QS_TAIL_ROWS"] = tr
+            os.environ["EVR_QS_TAIL_FIRST"] = tf
             _native.check(lib.evr_hvi_set_restart_variant(v), "variant")
             scan = graph_ms(lambda: ops.hvi_restart_fb(acqf.state, G, b))
             acqf._plans = {}
@@ -79,6 +89,9 @@ def main():
                 rec["minimize_evals"] = int(info[1])
             out[f"{tag}_{name}"] = rec
     _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
+    os.environ.pop("EVR_QS_TAIL", None)
+    os.environ.pop("EVR_QS_TAIL_ROWS", None)
+    os.environ.pop("EVR_QS_TAIL_FIRST", None)
     acqf._plans = {}
     out["construction"] = {k: round(v * 1e3, 3) for k, v in acqf.timings.items()}
     out["base_jitter"] = [float(v) for v in acqf.base_jitter.cpu()]
