@@ -47,7 +47,8 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
                                                    const double* __restrict__ os, const double* __restrict__ dg,
                                                    double* __restrict__ K, const unsigned long long* poll,
                                                    const unsigned long long* plast,
-                                                   const unsigned long long* seq_src, unsigned long long* seq_dst) {
+                                                   const unsigned long long* seq_src, unsigned long long* seq_dst,
+                                                   double* __restrict__ x_dst) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if (poll) kmat_wait_request(poll, plast);
   // host-driven chains: the evaluation's sequence number (pinned host memory, posted with the
@@ -75,6 +76,15 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
       // (a queued chain's candidates live in fine-grained host memory, which the GPU does not
       // cache: these loads read what the host posted before the request word)
       if (j0 + r < n2) xw[t] = X2[(size_t)(j0 + r) * d + (e - r * d)];
+    }
+  }
+  // host-driven chains: the candidates (n2 <= KT: one column tile) copied to device memory by
+  // the first workgroup, so that the chain's later kernels read them from L2, not across PCIe
+  if (x_dst && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int e = tid + 256 * t;
+      if (e < KT * d && e / d < n2) x_dst[e] = xw[t];
     }
   }
 #pragma unroll
@@ -1066,7 +1076,8 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
                          const unsigned long long* poll, const unsigned long long* plast,
-                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr);
+                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
+                         double* x_dst = nullptr);
 }  // namespace evr
 
 extern "C" {
@@ -1087,11 +1098,13 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
                          const unsigned long long* poll, const unsigned long long* plast,
-                         const unsigned long long* seq_src, unsigned long long* seq_dst) {
+                         const unsigned long long* seq_src, unsigned long long* seq_dst, double* x_dst) {
   EVR_CHECK(!poll || (plast && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
             "kernel_matrix_launch: the request wait needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(!seq_dst || (seq_src && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
             "kernel_matrix_launch: the sequence copy needs the VALU kernel (d < 16, one family)");
+  EVR_CHECK(!x_dst || (d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0 && n2 <= KT),
+            "kernel_matrix_launch: the candidate copy needs the VALU kernel (d < 16, one family, n2 <= %d)", KT);
   EVR_CHECK(kind_code_ok(kind, B), "evr_kernel_matrix: bad kernel kind %d for %d outputs", kind, B);
   EVR_CHECK(B >= 1 && n1 >= 0 && n2 >= 0 && d >= 1 && d <= KMAXD, "evr_kernel_matrix: bad sizes B=%d n1=%d n2=%d d=%d",
             B, n1, n2, d);
@@ -1202,7 +1215,7 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
 #define KTK(RA_, K_)                                                                              \
   kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
                                                              scale2, lengthscales, outputscale, diag_add, K, poll,   \
-                                                             plast, seq_src, seq_dst)
+                                                             plast, seq_src, seq_dst, x_dst)
 #define KT_(RA_)                         \
   if (kind == RBF) KTK(RA_, RBF);           \
   else if (kind == MATERN05) KTK(RA_, MATERN05); \

@@ -52,7 +52,8 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
                          const unsigned long long* poll, const unsigned long long* plast,
-                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr);
+                         const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
+                         double* x_dst = nullptr);
 constexpr int QS_TILE_ROWS = 16;
 constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
@@ -73,7 +74,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
                        double* work);
 
 struct PlanLayout {
-  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqw, seqd, bytes;
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqw, seqd, xd, bytes;
   bool small, fused_scan;
 };
 
@@ -110,6 +111,7 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
   }
   L.seqw = take(8);   // the last request a host-driven chain served (queued evaluations)
   L.seqd = take(8);   // the host-driven chain's sequence number, copied to device memory by kmat
+  L.xd = take(8 * (size_t)b * md->d);   // the host-driven chain's candidates, copied likewise
   L.bytes = o;
   return L;
 }
@@ -194,10 +196,12 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   // host mode through the b <= 32 kernels: qs_dx_reduce reads the sequence number from the
   // device copy kmat makes (an L2 read instead of a PCIe read at the end of the chain)
   unsigned long long* seqd = (hout && seqp && small) ? (unsigned long long*)(w + p->L.seqd) : nullptr;
+  // and the candidates: the later kernels of the chain read the device copy
+  double* xd = seqd ? (double*)(w + p->L.xd) : nullptr;
   if (int rc = kernel_matrix_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                     md->lengthscales, nullptr, nullptr, Kx,
                                     queued ? (const unsigned long long*)seqp : nullptr, plast,
-                                    seqd ? (const unsigned long long*)seqp : nullptr, seqd)) {
+                                    seqd ? (const unsigned long long*)seqp : nullptr, seqd, xd)) {
     return rc;
   } else if (small) {
     if (int rc = qs_forward(s, st, md, b, Kx, R, P)) return rc;
@@ -206,6 +210,7 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
     return rc;
   }
   double* dG = (double*)(w + p->L.dG);
+  if (xd) X = xd;
   if (small && p->backward && p->L.fused_scan && hvi_kdb_fused_applies(st, b)) {
     // the sampling step inside the restart scan's staging (one launch less); G is not formed.
     // The backward's training-row class rides in the scan's tail (qs_tail.hpp)
