@@ -602,14 +602,18 @@ __global__ __launch_bounds__(256) void kmat_mfma_pers(int n1, int n2, int d, int
 // one global round trip per output: 22 us at m = 5, n = b = 512 on MI355X), 1/ls and the
 // output scales of the chunk sit in LDS.
 constexpr int KG_B = 8;
-// outputs per LDS chunk / G loads in flight per row: 8 up to 16 dims; at 32 / 64 dims the
+// outputs per LDS chunk / G loads in flight per row: 4 up to 8 dims (the compiler keeps the
+// chunk's 1/ls table in registers across the row loop: 8 outputs x 8 dims did not fit two
+// waves per SIMD), 8 up to 16 dims; at 32 / 64 dims the
 // fully unrolled (output x dim) body of 8 outputs did not stay in registers (1.7 / 5.2 KB of
 // scratch per lane), so those instantiations take 2 outputs per round and form the scaled
 // differences twice instead of keeping a diff[] row
 template <int MAXD>
-__host__ __device__ constexpr int kg_outputs() { return MAXD <= 16 ? KG_B : 2; }
+__host__ __device__ constexpr int kg_outputs() { return MAXD <= 8 ? 4 : MAXD <= 16 ? KG_B : 2; }
+// (256, 2) at MAXD = 8: unbounded, the unrolled (output x dim) body took 292 VGPRs + 36 AGPRs —
+// one wave per SIMD, so the b = 512 pass's 2048 waves ran in two rounds (20.6 us)
 template <int MAXD>
-__global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d, int rows_per,
+__global__ __launch_bounds__(256, MAXD <= 8 ? 2 : 1) void kcross_grad_kernel(int kind, int B, int n1, int n2, int d, int rows_per,
                                                           const double* __restrict__ X1,
                                                           const double* __restrict__ sh1,
                                                           const double* __restrict__ sc1,
@@ -653,7 +657,7 @@ __global__ __launch_bounds__(256) void kcross_grad_kernel(int kind, int B, int n
     __syncthreads();
     if (c >= n2) continue;
     const double* Gc = G + (size_t)b0 * bstride + c;
-#pragma unroll 2
+#pragma unroll 1
     for (int i = i0 + ry; i < i1; i += 4) {
       double g[KGO];
 #pragma unroll

@@ -13,6 +13,7 @@
 #   planprobe   tools/plan_setup_probe.py (restart plan creation / first / warm evaluation)
 #   hostprof    tools/ask_host_profile.py (cProfile of 5 warm asks)
 #   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
+#   benche      python bench.py --no-cpu-baseline --no-config1 (ask line + evaluation pass + qLog)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
@@ -60,6 +61,7 @@ for st in "$@"; do
     planprobe) run planprobe 300 python tools/plan_setup_probe.py ;;
     hostprof) run hostprof 300 python tools/ask_host_profile.py ;;
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
+    benche) run benche 600 python bench.py --no-cpu-baseline --no-config1 ;;
     kmat) KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6,fit_train_n512 run kmat 300 python tools/bench_kmat.py && cp "$OUT/kmat.log" "$OUT/kmat.json" ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
