@@ -195,7 +195,10 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   unsigned long long* plast = queued ? (unsigned long long*)(w + p->L.seqw) : nullptr;
   // host mode through the b <= 32 kernels: qs_dx_reduce reads the sequence number from the
   // device copy kmat makes (an L2 read instead of a PCIe read at the end of the chain)
-  unsigned long long* seqd = (hout && seqp && small) ? (unsigned long long*)(w + p->L.seqd) : nullptr;
+  // (the copies ride in kmat_kernel, the VALU assembly: d < 16 and one kernel family)
+  unsigned long long* seqd = (hout && seqp && small && d < 16 && md->kind < KIND_MIXED)
+                                 ? (unsigned long long*)(w + p->L.seqd)
+                                 : nullptr;
   // and the candidates: the later kernels of the chain read the device copy
   double* xd = seqd ? (double*)(w + p->L.xd) : nullptr;
   if (int rc = kernel_matrix_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
