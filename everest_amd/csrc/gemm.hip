@@ -70,7 +70,15 @@ __global__ __launch_bounds__(256) void dg_splitk_reduce(int M, int N, int batch,
   if (e >= mn) return;
   const int bz = blockIdx.y;
   double acc = 0.0;
-  for (int kz = 0; kz < ksplit; ++kz) acc += W[((size_t)kz * batch + bz) * mn + e];
+  // 8 unconditional loads (clamped slice indices) in flight per round, summed in slice order
+  for (int k0 = 0; k0 < ksplit; k0 += 8) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = W[((size_t)min(k0 + u, ksplit - 1) * batch + bz) * mn + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u < ksplit) acc += t[u];
+  }
   const int row = (int)(e / N), cc = (int)(e - (long long)row * N);
   double* p = Cm + bz * sC + (size_t)row * ldc + cc;
   *p = beta == 0.0 ? alpha * acc : alpha * acc + beta * *p;

@@ -711,10 +711,19 @@ __global__ void kcross_grad_reduce(int nsplit, int n2, int d, const double* __re
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)n2 * d) return;
   const int k = (int)(e % d);
+  const double sck = sc2 ? sc2[k] : 1.0;
   double v = 0.0;
-#pragma unroll 8
-  for (int sp = 0; sp < nsplit; ++sp) v += part[(size_t)sp * n2 * d + e];   // loads issued ahead
-  dX2[e] = v * (sc2 ? sc2[k] : 1.0);
+  // 32 unconditional loads (clamped indices) in flight per round, summed in split order
+  // afterwards: one memory round trip per 32 splits (the guarded unroll-8 loop waited per 8)
+  for (int s0 = 0; s0 < nsplit; s0 += 32) {
+    double t[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) t[u] = part[(size_t)min(s0 + u, nsplit - 1) * n2 * d + e];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (s0 + u < nsplit) v += t[u];
+  }
+  dX2[e] = v * sck;
 }
 
 // row split of kcross_grad: up to 2048 blocks, >= 8 rows per block (two per row group).  At
