@@ -761,10 +761,75 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
 }
 
 // part[b][i][k] = sum_j W[b][i][j] * dK_b[i][j]/dls_k, dK/dls_k = -dscale * diff_k^2 / ls_k^3
-// (diff in normalized units).  One block per (row i, output b); rows summed afterwards in a
-// fixed order by colsum_kernel so that the MLL gradient is bitwise reproducible.
+// (diff in normalized units).  One wave per (row i, output b), four rows per block: lane l sums
+// j = l, l + 64, ... (its W loads and the row's inputs all issued before the arithmetic), then
+// one fixed xor butterfly per dimension — no LDS, no barrier.  (The former block per row, 256
+// threads over j, gave 2560 blocks at n = 512, B = 5: two residency rounds, 20.4 us.)  Rows are
+// summed afterwards in a fixed order by colsum_kernel, so the MLL gradient is bitwise
+// reproducible.
+constexpr int KLS_ROWS = 4;
 template <int MAXD>
 __global__ __launch_bounds__(256) void kls_grad_kernel(int kind, int n, int d, const double* __restrict__ X,
+                                                       const double* __restrict__ ls,
+                                                       const double* __restrict__ W, double* __restrict__ part) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * KLS_ROWS + (threadIdx.x >> 6);
+  if (i >= n) return;   // whole waves (no barrier below)
+  const double* lsb = ls + (size_t)b * d;
+  const double* Wr = W + ((size_t)b * n + i) * n;
+  const int kb = kind_of(kind, b);
+  double xi[MAXD], il[MAXD];
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) {
+    xi[k] = k < d ? X[(size_t)i * d + k] : 0.0;
+    il[k] = k < d ? 1.0 / lsb[k] : 0.0;
+  }
+  double acc[MAXD];
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) acc[k] = 0.0;
+  // UJ columns per lane and round, their W entries (coalesced rows) in flight together; one
+  // above 8 dims (the unrolled body would not stay in registers).  (Preloading the columns'
+  // inputs as well: 147 VGPRs, 16.8 vs 15.5 us.)
+  constexpr int UJ = MAXD <= 8 ? 4 : 1;
+  for (int j0 = 0; j0 < n; j0 += 64 * UJ) {
+    double w[UJ];
+#pragma unroll
+    for (int u = 0; u < UJ; ++u) w[u] = Wr[min(j0 + lane + 64 * u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < UJ; ++u) {
+      const int j = j0 + lane + 64 * u;
+      if (j >= n) break;
+      double sq[MAXD];
+      double d2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k)
+        if (k < d) {
+          const double df = (xi[k] - X[(size_t)j * d + k]) * il[k];
+          sq[k] = df * df;
+          d2 += sq[k];
+        }
+      const double s = -w[u] * kernel_dscale(kb, d2);
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k)
+        if (k < d) acc[k] = fma(s, sq[k] * il[k], acc[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) {
+    if (k < d) {
+      double v = acc[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) part[((size_t)b * n + i) * d + k] = v;
+    }
+  }
+}
+
+// Above 16 dims: one block per (row i, output b), 256 threads over j (the wave-per-row form's
+// per-lane (dimension x column) arrays do not stay in registers there).
+template <int MAXD>
+__global__ __launch_bounds__(256) void kls_grad_block_kernel(int kind, int n, int d, const double* __restrict__ X,
                                                        const double* __restrict__ ls,
                                                        const double* __restrict__ W, double* __restrict__ part) {
   const int b = blockIdx.y;
@@ -1271,12 +1336,14 @@ int evr_kernel_lengthscale_grad(void* stream, int kind, int B, int n, int d, con
             "evr_kernel_lengthscale_grad: bad args");
   EVR_CHECK(work != nullptr, "evr_kernel_lengthscale_grad: work (B*n*d doubles) required");
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(n, B);
+  dim3 grid(cdiv(n, KLS_ROWS), B), gridb(n, B);
 #define LAUNCH(MD) kls_grad_kernel<MD><<<grid, 256, 0, s>>>(kind, n, d, X, lengthscales, W, work)
+#define LAUNCHB(MD) kls_grad_block_kernel<MD><<<gridb, 256, 0, s>>>(kind, n, d, X, lengthscales, W, work)
   if (d <= 8) LAUNCH(8);
   else if (d <= 16) LAUNCH(16);
-  else if (d <= 32) LAUNCH(32);
-  else LAUNCH(64);
+  else if (d <= 32) LAUNCHB(32);
+  else LAUNCHB(64);
+#undef LAUNCHB
 #undef LAUNCH
   EVR_LAUNCH_CHECK();
   colsum_kernel<<<B * d, 256, 0, s>>>(B, n, d, work, gls);

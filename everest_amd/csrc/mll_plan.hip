@@ -97,6 +97,50 @@ __global__ __launch_bounds__(256, 4) void mll_w_kernel(int n, int B, const doubl
   }
 }
 
+// v = L^-1 r (TRANS false) and alpha = L^-T v (TRANS true) for the B members: one workgroup
+// per 16 outputs of a member, L^-1's triangle only (k <= i, resp. k >= i).  Thread (output o,
+// k-group g) sums k = g, g + 16, ... (non-transposed: the 16 lanes of a k-group row read 128
+// contiguous bytes of row i; transposed: of row k), the 16 partials summed in g order: no
+// split-K workspace and no second (reduction) launch — the split-K GEMM pair took 14 us per
+// product at n = 512, almost all of it launch and reduction latency.
+template <bool TRANS>
+__global__ __launch_bounds__(256) void mll_matvec(int n, const double* __restrict__ L, const double* __restrict__ x,
+                                                  double* __restrict__ out) {
+  __shared__ double red[16][17];
+  const int j = blockIdx.y, i0 = blockIdx.x * 16, t = threadIdx.x;
+  const int o = TRANS ? (t & 15) : (t >> 4), g = TRANS ? (t >> 4) : (t & 15);
+  const int i = i0 + o;
+  const double* Lj = L + (size_t)j * n * n;
+  const double* xj = x + (size_t)j * n;
+  double s = 0.0;
+  if (i < n) {
+    const int kb = TRANS ? i0 : 0, ke = TRANS ? n : min(n, i0 + 16);
+    // rounds of 8 loads in flight (k = kb + g + 16 u), the triangle's other entries skipped
+    for (int k0 = kb; k0 < ke; k0 += 128) {
+      double a[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = min(k0 + g + 16 * u, n - 1);
+        a[u] = TRANS ? Lj[(size_t)k * n + i] : Lj[(size_t)i * n + k];
+        xv[u] = xj[k];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + g + 16 * u;
+        if (k < ke && (TRANS ? k >= i : k <= i)) s = fma(a[u], xv[u], s);
+      }
+    }
+  }
+  red[o][g] = s;
+  __syncthreads();
+  if (t < 16 && i0 + t < n) {
+    double v = red[t][0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v += red[t][q];
+    out[(size_t)j * n + i0 + t] = v;
+  }
+}
+
 // hx: [ls (B x d) | noise (B) | constant (B) | sequence number]; also the residuals
 // r = Y - constant (one launch: the constant comes straight from the host buffer, one read
 // per wave since a wave's rows share a member when n >= 64)
@@ -119,7 +163,15 @@ __global__ void mll_copy_out(int B, int d, int nch, const double* __restrict__ p
   if (t < B * 5) {
     const int b = t / 5, q = t - b * 5;
     double s = 0.0;
-    for (int ch = 0; ch < nch; ++ch) s += part[((size_t)b * nch + ch) * 5 + q];
+    // the chunk partials' loads in flight together (clamped indices), summed in chunk order
+    for (int c0 = 0; c0 < nch; c0 += 32) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = part[((size_t)b * nch + min(c0 + u, nch - 1)) * 5 + q];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (c0 + u < nch) s += v[u];
+    }
     hout[t] = q == 0 ? 2.0 * s : s;
   }
   for (int i = t; i < B * d; i += blockDim.x) hout[B * 5 + i] = gls[i];
@@ -150,7 +202,6 @@ struct evr_mll_plan {
 
 static int mll_chain(hipStream_t s, evr_mll_plan* p, const double* dhx, double* dhout) {
   const int B = p->B, n = p->n, d = p->d;
-  const long long nn = (long long)n * n;
   mll_copy_in<<<cdiv(std::max(B * d + B, B * n), 256), 256, 0, s>>>(B, n, d, dhx, p->Y, p->ls, p->noise, p->cst,
                                                                        p->r);
   EVR_LAUNCH_CHECK();
@@ -159,10 +210,11 @@ static int mll_chain(hipStream_t s, evr_mll_plan* p, const double* dhx, double* 
     return rc;
   if (int rc = chol_inverse_attempt(s, B, n, p->K, p->L, p->Linv, p->Dinv, p->T, p->jit0, p->info)) return rc;
   double* W = p->K;   // K was consumed by the factorisation
-  // v = L^-1 r, alpha = L^-T v: matrix-vector products, split over k (the plan's workspace
-  // holds the partials; a fixed-order reduction) so that they spread over ~300 workgroups
-  if (int rc = dg_gemm(s, false, n, 1, n, 1.0, p->Linv, n, nn, p->r, 1, n, 0.0, p->v, 1, n, B, p->mvw)) return rc;
-  if (int rc = dg_gemm(s, true, n, 1, n, 1.0, p->Linv, n, nn, p->v, 1, n, 0.0, p->alpha, 1, n, B, p->mvw)) return rc;
+  // v = L^-1 r, alpha = L^-T v: one-launch triangular matrix-vector products (mll_matvec)
+  mll_matvec<false><<<dim3(cdiv(n, 16), B), 256, 0, s>>>(n, p->Linv, p->r, p->v);
+  EVR_LAUNCH_CHECK();
+  mll_matvec<true><<<dim3(cdiv(n, 16), B), 256, 0, s>>>(n, p->Linv, p->v, p->alpha);
+  EVR_LAUNCH_CHECK();
   {
     const int T = cdiv(n, MllW::BM), lower = T * (T + 1) / 2;
     if (n % 2 == 0) mll_w_kernel<true><<<lower * B, 256, 0, s>>>(n, B, p->Linv, p->alpha, W);

@@ -26,6 +26,7 @@
 #               per lane, cached / non-temporal; hipcc -O3 tools/micro/fill_probe.hip -o tools/_fill_probe)
 #   bench       python bench.py (the driver's default command)
 #   prof        rocprofv3 --kernel-trace --stats of the bench command
+#   fitprof     the same over tools/fit_probe.py (tell(): the MLL plan's kernels per round)
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
 #   qsprof      per-workgroup phase stamps of qs_bwd at the bench shape (tools/_qs_prof: hipcc
 #               --offload-arch=gfx950 -O3 -std=c++17 -DEVR_QS_PROF tools/qs_prof.hip -o tools/_qs_prof)
@@ -80,6 +81,7 @@ for st in "$@"; do
     kdwwaves) EVR_LIB_PATH=everest_amd/_libkdprof/libeverest_amd.so run kdwwaves 300 python tools/kdw_waves.py ;;
     kdwaves) EVR_LIB_PATH=everest_amd/_libprof/libeverest_amd.so run kdwaves 300 python tools/kd3_waves.py ;;
     bench) run bench 900 python bench.py ;;
+    fitprof) run fitprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/fitprof" -o run --output-format csv -- python tools/fit_probe.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
     qsprof) run qsprof 60 tools/_qs_prof && run qsprof_tail 60 tools/_qs_prof tail ;;
