@@ -147,3 +147,32 @@ def test_restart_chain_is_batch_invariant():
     for sl in (slice(0, 10), slice(10, 20), slice(3, 10)):
         a2, g2 = q.eval_host(Xc[sl], True)
         assert np.array_equal(a2, a[sl]) and np.array_equal(g2, g[sl])
+
+
+def test_restart_backward_tail_placements(monkeypatch):
+    """The restart backward's training-row class (qs_tail.hpp) in workgroups of its own inside
+    the backward launch (EVR_QS_TAIL=bwd, default) and in the restart scan's tail (kdw) run
+    the same device function on the same inputs: bitwise equal, device chain and host-driven
+    evaluation alike; inside qs_bwd's own workgroups (0) the class is scaled before the
+    cross-covariance step instead of after it: equal to rounding."""
+    from everest_amd.acquisition import QNEHVI
+
+    n, d, m, S = 90, 5, 4, 48
+    X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=35)
+    gp = device_gp(X, Y, lo, hi, hyp)
+    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=5, prune_baseline=True,
+               prune_seed=6, prune_samples=256)
+    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(20, d)), device="cuda")
+    out = {}
+    for mode in ("bwd", "kdw", "0"):
+        monkeypatch.setenv("EVR_QS_TAIL", mode)
+        q._plans = {}
+        a, g = q.forward_backward(Xc)
+        ah, gh = q.eval_host(Xc.cpu().numpy(), True)
+        assert np.array_equal(ah, a.cpu().numpy()) and np.array_equal(gh, g.cpu().numpy())
+        out[mode] = (a.clone(), g.clone())
+    q._plans = {}
+    assert torch.equal(out["bwd"][0], out["kdw"][0]) and torch.equal(out["bwd"][1], out["kdw"][1])
+    assert torch.equal(out["bwd"][0], out["0"][0])     # the forward is untouched
+    g0, g1 = out["0"][1], out["bwd"][1]
+    assert torch.allclose(g1, g0, rtol=1e-10, atol=1e-13 * g0.abs().max())
