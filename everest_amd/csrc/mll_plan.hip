@@ -29,10 +29,6 @@ int gemm_plain(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alph
                long long sA, const double* B, int ldb, long long sB, double beta, double* C, int ldc, long long sC,
                int batch);
 size_t mll_terms_part_doubles(int B);
-size_t dg_gemm_ws_doubles(bool tA, int M, int N, int K, int batch);
-int dg_gemm(hipStream_t s, bool tA, int M, int N, int K, double alpha, const double* A, int lda, long long sA,
-            const double* B, int ldb, long long sB, double beta, double* Cm, int ldc, long long sC, int batch,
-            double* W);
 int mll_terms_chunks();
 int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const double* Linv, const double* r,
                        const double* alpha, double* part);
@@ -192,7 +188,7 @@ using namespace evr;
 struct evr_mll_plan {
   int kind, B, n, d;
   const double* Xn;
-  double *Y, *ls, *noise, *cst, *K, *L, *Linv, *Dinv, *T, *r, *v, *alpha, *gls, *gw, *part, *jit0, *mvw;
+  double *Y, *ls, *noise, *cst, *K, *L, *Linv, *Dinv, *T, *r, *v, *alpha, *gls, *gw, *part, *jit0;
   int* info;
   double *hx, *hout;
   hipGraph_t graph;
@@ -233,7 +229,7 @@ static void mll_free(evr_mll_plan* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   double* bufs[] = {p->Y, p->ls, p->noise, p->cst, p->K, p->L, p->Linv, p->Dinv, p->T, p->r, p->v, p->alpha,
-                    p->gls, p->gw, p->part, p->jit0, p->mvw};
+                    p->gls, p->gw, p->part, p->jit0};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
@@ -265,8 +261,7 @@ int evr_mll_plan_create(void* stream, int kind, int B, int n, int d, const doubl
               {&p->Linv, B * nn},       {&p->Dinv, chol_inverse_dinv_doubles(B, n)},
               {&p->T, (size_t)B * 64 * n}, {&p->r, (size_t)B * n}, {&p->v, (size_t)B * n},
               {&p->alpha, (size_t)B * n}, {&p->gls, (size_t)B * d}, {&p->gw, (size_t)B * n * d},
-              {&p->part, mll_terms_part_doubles(B)}, {&p->jit0, (size_t)B},
-              {&p->mvw, std::max(dg_gemm_ws_doubles(false, n, 1, n, B), dg_gemm_ws_doubles(true, n, 1, n, B))}};
+              {&p->part, mll_terms_part_doubles(B)}, {&p->jit0, (size_t)B}};
   for (auto& q : need) {
     if (hipMalloc((void**)q.ptr, sizeof(double) * std::max<size_t>(q.count, 1)) != hipSuccess) {
       mll_free(p);
