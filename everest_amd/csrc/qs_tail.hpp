@@ -1,8 +1,10 @@
 // The training-row class of the restart-batch backward projection (qnehvi_small.hip qs_bwd),
-// computed where it has slack: it needs only the forward's R, so it runs in the tail of the
-// restart scan (hvi.hip hvi_kdw: extra workgroups after the scan's, dispatched into the slots
-// the light (sample, candidate) waves free) or, on the op path, as its own launch before the
-// backward.  For 16 training rows i of output j and a split of the rows r < n of M_j:
+// apart from the sample rows: it needs only the forward's R.  By default its workgroups are
+// the backward launch's z >= 1 slices, beside the sample-row workgroups (which hold one
+// workgroup on 160 of the 256 CUs at the bench shape); EVR_QS_TAIL=kdw runs them in the tail
+// of the restart scan (hvi.hip hvi_kdw: extra workgroups after the scan's — measured slower,
+// the scan holds every slot), and the op path with that setting launches them on their own
+// (qs_bwd_tail).  For 16 training rows i of output j and a split of the rows r < n of M_j:
 //   D[i][c]  = sum_r M_j[r][i] R_j[r][c]                       (f64 MFMA, per-wave k-quarters)
 //   Q[c][k]  = sum_i D[i][c] dk(x_i, x_c)/dx_c[k]               (the cross-covariance gradient)
 // The gR coefficient of this class (cf0[c], a reduction of the scan's dG over the samples) is a
