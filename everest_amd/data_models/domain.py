@@ -658,9 +658,13 @@ class Domain(BaseModel):
         return experiments
 
     def validate_candidates(self, candidates: pd.DataFrame, only_inputs: bool = False, tol: float = 1e-5,
-                            raise_validation_error: bool = True) -> pd.DataFrame:
-        """bofire/data_models/domain/domain.py:417-459."""
-        if all(isinstance(f, ContinuousInput) for f in self.inputs.get().features):
+                            raise_validation_error: bool = True, inputs_validated: bool = False) -> pd.DataFrame:
+        """bofire/data_models/domain/domain.py:417-459.  inputs_validated: the caller has just
+        validated this very frame's inputs (PredictiveStrategy.ask after Strategy.ask); without
+        constraints the input checks are not repeated (the output columns still are)."""
+        if inputs_validated and not len(self.constraints):
+            pass
+        elif all(isinstance(f, ContinuousInput) for f in self.inputs.get().features):
             # continuous inputs: the checks on one gathered array; the validated input frame is
             # only formed when constraints need it
             vals = self.inputs.check_continuous_candidates(candidates)

@@ -223,7 +223,10 @@ class PredictiveStrategy(Strategy):
             raise_validation_error: bool = True) -> pd.DataFrame:
         candidates = super().ask(candidate_count=candidate_count, add_pending=add_pending,
                                  raise_validation_error=raise_validation_error)
-        self.domain.validate_candidates(candidates=candidates, raise_validation_error=raise_validation_error)
+        # Strategy.ask validated this frame's inputs (and constraints) a moment ago: only the
+        # prediction columns are new to check
+        self.domain.validate_candidates(candidates=candidates, raise_validation_error=raise_validation_error,
+                                        inputs_validated=True)
         return candidates
 
     def tell(self, experiments: pd.DataFrame, replace: bool = False, retrain: bool = True):
