@@ -268,7 +268,7 @@ def config1_loop(seed=7):
     rnd = strategies.map(dm.RandomStrategy(domain=bm.domain, seed=19))
     exps = bm.f(rnd.ask(2), return_complete=True)
     s = strategies.map(dm.QnehviStrategy(domain=bm.domain, seed=seed))
-    tells, asks = [], []
+    tells, asks, phases = [], [], []
     for it in range(5):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -281,12 +281,21 @@ def config1_loop(seed=7):
         c = s.ask(candidate_count=1)
         torch.cuda.synchronize()
         asks.append(time.perf_counter() - t0)
+        st = s.last_ask_stats
+        construction = float(getattr(s.last_acqf, "timings", {}).get("total", 0.0))
+        phases.append({"construction": construction, "raw_draw": st.t_raw_draw,
+                       "raw_screening": st.t_raw - st.t_raw_draw, "restarts": st.t_opt,
+                       "other": asks[-1] - construction - st.t_raw - st.t_opt,
+                       "restart_evals": int(st.opt_evals), "driver": st.chunks[0]["driver"] if st.chunks else None})
         exps = bm.f(c[bm.domain.inputs.get_keys()], return_complete=True)
     r = lambda v: [round(x, 4) for x in v]  # noqa: E731
     return {"workload": "BASELINE configs[0]: Detergent, QnehviStrategy defaults (S=512, raw 1024, 8 restarts, "
                         "SLSQP under 2 linear constraints), 2 initial + 4 ask/tell rounds",
             "ask_s": r(asks), "tell_s": r(tells), "ask_s_median": round(float(np.median(asks)), 4),
             "tell_s_median": round(float(np.median(tells)), 4), "experiments": s.num_experiments,
+            "phases_median_s": {k: round(float(np.median([p[k] for p in phases])), 4)
+                                for k in ("construction", "raw_draw", "raw_screening", "restarts", "other")},
+            "restart_evals": [p["restart_evals"] for p in phases],
             "driver": s.last_ask_stats.chunks[0]["driver"] if s.last_ask_stats.chunks else None}
 
 
@@ -509,13 +518,16 @@ def _launched_kernel(acqf, op, b, d):
     return r"hvi_kd2?<|hvi_tiled<"
 
 
-def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=None, seed: int = 1):
+def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=None, seed: int = 1,
+                      batch_limit: int = 0):
     """QnehviStrategy of config 4 (DTLZ2(6, 5), n_train = n, S MC samples, ``raw`` Sobol raw
     samples, ``restarts`` L-BFGS-B restarts) through the BoFire-compatible API, fitted once
     (tell).  batch_limit = restarts at every N (the data model's default,
     bofire/data_models/strategies/predictives/botorch.py:101-108): one joint problem whose
     evaluations the ranks shard; raw screening is sharded over the ranks with an all-gather of
-    the values.  Returns (strategy, tell_s)."""
+    the values.  ``batch_limit`` > 0 overrides it (1: every restart its own
+    problem, the independent-restart layout BoFire forces under NChooseK / product
+    constraints, bofire/strategies/predictives/botorch.py:114-126).  Returns (strategy, tell_s)."""
     import pandas as pd
 
     import everest_amd.data_models as dm
@@ -526,7 +538,7 @@ def make_ask_strategy(n: int, S: int, raw: int, restarts: int, world: int, dist=
     Xd = pd.DataFrame(np.random.default_rng(0).uniform(size=(n, 6)), columns=bm.domain.inputs.get_keys())
     s = strategies.map(dm.QnehviStrategy(domain=bm.domain, ref_point=bm.ref_point, seed=seed, num_sobol_samples=S,
                                          num_raw_samples=raw, num_restarts=restarts,
-                                         batch_limit=restarts), dist=dist)
+                                         batch_limit=batch_limit or restarts), dist=dist)
     exps = bm.f(Xd, return_complete=True)
     times = []
     for _ in range(2):      # cold (first GPU work of the process: module loads, plan captures), then warm

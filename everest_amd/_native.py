@@ -150,6 +150,8 @@ _SIGS = {
     "evr_lbfgsb_step": ([c_void_p, c_double, c_void_p, c_void_p], c_int),
     "evr_lbfgsb_stats": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], None),
     "evr_lbfgsb_destroy": ([c_void_p], None),
+    "evr_hit_and_run": ([c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_longlong, ctypes.c_ulonglong,
+                         c_longlong, c_longlong, c_void_p], c_int),
     "evr_qnehvi_plan_minimize": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double,
                                   c_double, c_int, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "evr_qng_workspace_doubles": ([POINTER(EvrQnehviState), POINTER(EvrQnehviState), POINTER(EvrQnGeneral),

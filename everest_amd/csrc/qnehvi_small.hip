@@ -62,15 +62,20 @@ constexpr int QS_FW = QS_FT / 64;                 // waves
 constexpr int QS_RPP = QS_FT / QS_KC;             // M rows per staging pass (a thread per chunk column)
 constexpr int QS_ML = QS_FR / QS_RPP;             // M values per thread and chunk
 constexpr int QS_KL = (QS_KC * QS_B + QS_FT - 1) / QS_FT;   // K_x values per thread and chunk
-__global__ __launch_bounds__(QS_FT, 1) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
+// Two workgroups per CU (50 KB of LDS; four waves per SIMD: <= 128 VGPRs): the split root's m x 66 row tiles
+// (330 workgroups) are resident in one round like the fused root's m x 49.
+__global__ __launch_bounds__(QS_FT, 4) void qs_fwd(int n, int nb, int Rr, int b, const double* __restrict__ M,
                                                    const double* __restrict__ Kx, double* __restrict__ R,
                                                    double* __restrict__ P, int ntile) {
   // padded row of the staged M tile: 2 MP = 4 (mod 64 dwords) puts the 16 rows x 2
   // k-quarters of a ds_read_b64 lane half on 32 distinct bank pairs (conflict-free)
   constexpr int MP = QS_KC + 2;
-  __shared__ double Ms[QS_FR][MP];               // 16 x 128 slice of M_j (16.6 KB)
-  __shared__ double Ks[QS_KC][QS_B + 1];         // 128 x b slice of K_x,j (33.8 KB)
-  __shared__ double red[QS_FW][QS_FR][QS_B + 1];  // the waves' k-partials (33.8 KB)
+  constexpr int MS_SZ = QS_FR * MP, KS_SZ = QS_KC * (QS_B + 1), RED_SZ = QS_FW * QS_FR * (QS_B + 1);
+  static_assert(RED_SZ <= MS_SZ + KS_SZ, "the k-partials alias the chunk tiles");
+  __shared__ double lds[MS_SZ + KS_SZ];
+  auto Ms = reinterpret_cast<double(*)[MP]>(lds);                      // 16 x 128 slice of M_j (16.6 KB)
+  auto Ks = reinterpret_cast<double(*)[QS_B + 1]>(lds + MS_SZ);        // 128 x b slice of K_x,j (33.8 KB)
+  auto red = reinterpret_cast<double(*)[QS_FR][QS_B + 1]>(lds);       // the waves' k-partials (after the loop)
   const int tile = blockIdx.x, j = blockIdx.y, r0 = tile * QS_FR;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
@@ -104,10 +109,19 @@ __global__ __launch_bounds__(QS_FT, 1) void qs_fwd(int n, int nb, int Rr, int b,
   auto stage = [&](const double (&mv)[QS_ML], const double (&kv)[QS_KL]) {
 #pragma unroll
     for (int u = 0; u < QS_ML; ++u) Ms[QS_RPP * u + rh][kk] = mv[u];
+    // element e = u QS_FT + tid of the chunk's row-major run -> (e / b, e % b), stepped per u
+    // (no per-element division: it kept 2 QS_KL index registers alive)
+    int kr = tid / b, kc_ = tid - kr * b;
+    const int dq = QS_FT / b, dr = QS_FT - dq * b;
 #pragma unroll
     for (int u = 0; u < QS_KL; ++u) {
-      const int e = u * QS_FT + tid;
-      if (e < QS_KC * b) Ks[e / b][e % b] = kv[u];   // every row of the chunk, columns < b
+      if (u * QS_FT + tid < QS_KC * b) Ks[kr][kc_] = kv[u];   // every row of the chunk, columns < b
+      kr += dq;
+      kc_ += dr;
+      if (kc_ >= b) {
+        kc_ -= b;
+        ++kr;
+      }
     }
   };
   constexpr int KW = QS_KC / QS_FW;   // k per wave and chunk
@@ -138,6 +152,7 @@ __global__ __launch_bounds__(QS_FT, 1) void qs_fwd(int n, int nb, int Rr, int b,
     mult();
   }
   QS_STAMP(2);
+  __syncthreads();   // every wave is done with Ms, Ks (red aliases them)
   // D map of v_mfma_f64_16x16x4: register q of lane l holds D[4q + (l >> 4)][l & 15]
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -391,7 +406,9 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     cf[0][tid] = -2.0 * sj * sj * dbr;
     cf[1][tid] = -2.0 * dbr;
     cf[2][tid] = sj * u;
-    if (TAIL && tile == 0 && z == 0 && tid < b) cfo[(size_t)j * b + tid] = -2.0 * sj * sj * dbr;
+    // the tail's class coefficient: -2 dbr with the split root (its L^-1 rows carry s^2 in the
+    // tail's weights), -2 s^2 dbr with the fused one
+    if (TAIL && tile == 0 && z == 0 && tid < b) cfo[(size_t)j * b + tid] = nb > 0 ? -2.0 * dbr : -2.0 * sj * sj * dbr;
   }
   QS_STAMP(2);
   // the epilogue's training rows and mean-row entries, loaded before the dk exchange so their
@@ -597,26 +614,23 @@ int qs_ntile_fwd(const evr_qnehvi_state* st) { return cdiv(qn_rows(st), QS_FR); 
 
 size_t qs_norms_doubles(const evr_qnehvi_state* st, int b) { return (size_t)st->m * qs_ntile_fwd(st) * 2 * b; }
 
-// The training-row class apart from the sample rows (qs_tail.hpp), fused root only (nb = 0).
-// EVR_QS_TAIL (read per call: plans read it once, at capture): "bwd" (default) — its
-// workgroups ride in the backward's launch beside the sample-row workgroups (those hold one
-// workgroup on 160 of the 256 CUs); "kdw" — in the restart scan's tail (measured: the scan
-// holds every workgroup slot, so the tail stretches it by ~4 us); "0" — inside qs_bwd's
-// workgroups as before
-static int qs_tail_mode(const evr_qnehvi_state* st) {
-  const char* e = std::getenv("EVR_QS_TAIL");
-  if (st->nb != 0 || (e && e[0] == '0')) return 0;
-  return (e && !std::strcmp(e, "kdw")) ? 2 : 1;
-}
+// The training-row classes apart from the sample rows (qs_tail.hpp): the fused root's C rows, or
+// the split root's L^-1 and G rows (nb > 0) weighted into one class.  Their workgroups ride in
+// the backward's launch beside the sample-row workgroups (those hold one workgroup on 160 of the
+// 256 CUs at the bench shape).  Measured and removed (round 5): the tail in the restart scan's
+// launch (the scan holds every workgroup slot, so the tail stretched it by ~4 us) and inside
+// qs_bwd's own workgroups.  A function of the state only, so a plan's layout (qs_dxp_doubles)
+// and its launches always agree.
+static int qs_tail_mode(const evr_qnehvi_state* st) { return st->n > 0 ? 1 : 0; }
 bool qs_tail_on(const evr_qnehvi_state* st) { return qs_tail_mode(st) != 0; }
-// training rows per tail workgroup's split: 256 (64 per wave, two load batches); EVR_QS_TAIL_ROWS
-// (a multiple of 16) for A/B
-static int qs_tail_rows() {
-  const char* e = std::getenv("EVR_QS_TAIL_ROWS");
-  const int v = e ? std::atoi(e) : 0;
-  return (v >= 16 && v % 16 == 0) ? v : 256;
+// training rows per tail workgroup's split: 256 (64 per wave, two load batches), or half the
+// class (rounded to 16) when that is longer, so the class is two splits and the launch's
+// m (2 + 1) 32 workgroups stay resident in one round at two per CU
+static int qs_tail_rows(const evr_qnehvi_state* st) {
+  const int half = ((st->n + st->nb + 1) / 2 + 15) & ~15;
+  return half > 256 ? half : 256;
 }
-static int qs_tail_za(const evr_qnehvi_state* st) { return cdiv(st->n, qs_tail_rows()); }
+static int qs_tail_za(const evr_qnehvi_state* st) { return cdiv(st->n + st->nb, qs_tail_rows(st)); }
 
 // rows the backward's splits cover: every non-mean row, or (tail) the sample rows only
 static int qs_bwd_rows(const evr_qnehvi_state* st) {
@@ -677,8 +691,8 @@ bool qs_tail_make(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b,
 static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                          const double* R, double* dXp, QsTail* t) {
   const int nt = cdiv(st->n, QS_BI);
-  *t = QsTail{md->M, R, md->Xn, X, md->shift, md->scale, md->lengthscales, dXp, st->n, qn_rows(st), b, md->d,
-              md->kind, nt, qs_tail_za(st), qs_tail_rows(), (int)qs_np_bwd(st), (int)qs_np_all(st),
+  *t = QsTail{md->M, R, md->Xn, X, md->shift, md->scale, md->lengthscales, dXp, st->ys, st->n, st->nb, qn_rows(st),
+              b, md->d, md->kind, nt, qs_tail_za(st), qs_tail_rows(st), (int)qs_np_bwd(st), (int)qs_np_all(st),
               st->m * qs_tail_za(st) * nt};
 }
 
@@ -706,8 +720,8 @@ int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_mode
                                                       R, dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,   \
                                                       md->scale, md->lengthscales, dXp, nt, rows_per, np, cfo,       \
                                                       mode == 1 ? zs : gz, t)
-  if (st->nb > 0) QS_BWD(true, false);
-  else if (tail) QS_BWD(false, true);
+  if (tail) QS_BWD(false, true);
+  else if (st->nb > 0) QS_BWD(true, false);
   else QS_BWD(false, false);
 #undef QS_BWD
   EVR_LAUNCH_CHECK();

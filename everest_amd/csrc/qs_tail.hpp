@@ -4,8 +4,12 @@
 // workgroup on 160 of the 256 CUs at the bench shape); EVR_QS_TAIL=kdw runs them in the tail
 // of the restart scan (hvi.hip hvi_kdw: extra workgroups after the scan's — measured slower,
 // the scan holds every slot), and the op path with that setting launches them on their own
-// (qs_bwd_tail).  For 16 training rows i of output j and a split of the rows r < n of M_j:
-//   D[i][c]  = sum_r M_j[r][i] R_j[r][c]                       (f64 MFMA, per-wave k-quarters)
+// (qs_bwd_tail).  For 16 training rows i of output j and a split of the rows r < n + nb of M_j
+// (nb = 0: the fused root C; nb > 0: the split root's L^-1 and G blocks):
+//   D[i][c]  = sum_r w_r M_j[r][i] R_j[r][c]                   (f64 MFMA, per-wave k-quarters)
+// with w_r = s_j^2 on the L^-1 rows of the split root and 1 elsewhere: the two blocks' gR
+// coefficients are -2 s_j^2 dbr and -2 dbr (L22^2 = s^2 (kxx - |L^-1 k|^2) - |G k|^2), so one
+// class coefficient cf0 = -2 dbr (split) or -2 s^2 dbr (fused) covers both.
 //   Q[c][k]  = sum_i D[i][c] dk(x_i, x_c)/dx_c[k]               (the cross-covariance gradient)
 // The gR coefficient of this class (cf0[c], a reduction of the scan's dG over the samples) is a
 // per-candidate scalar, so it is applied to Q in the dX reduction (qs_dx_reduce) instead of to
@@ -24,7 +28,8 @@ struct QsTail {
   const double* scale;  // d or null
   const double* ls;     // m x d lengthscales
   double* part;         // dX partials, element-major: part[(c d + k) np + p]
-  int n, Rr, b, d, kind, nt, za, rows_per, poff, np;
+  const double* ys;     // m output scales s_j (split root: rows < n of R are weighted by s_j^2)
+  int n, nb, Rr, b, d, kind, nt, za, rows_per, poff, np;
   int nwg;              // workgroups (m za nt); a launch may carry padding ones past it
 };
 
@@ -62,7 +67,8 @@ __device__ __forceinline__ void qs_tail_tile(const QsTail& t, int wg, double* ld
     lv = t.ls[(size_t)j * d + tid % d];
   }
   // this wave's rows of the split: a quarter, whole k-steps
-  const int zb = z * t.rows_per, ze = min(n, zb + t.rows_per);
+  const int zb = z * t.rows_per, ze = min(n + t.nb, zb + t.rows_per);
+  const double w0 = t.nb > 0 ? t.ys[j] * t.ys[j] : 1.0;
   const int rw = (((t.rows_per + 3) / 4) + 3) & ~3;
   const int r0 = zb + wave * rw, r1 = min(ze, r0 + rw);
   const bool colok = i0 + i < n;
@@ -73,9 +79,10 @@ __device__ __forceinline__ void qs_tail_tile(const QsTail& t, int wg, double* ld
     for (int u = 0; u < QT_KB; ++u) {
       const int r = rb + 4 * u + kq;
       const bool rin = r < r1;
+      const double w = r < n ? w0 : 1.0;
       av[u] = (rin && colok) ? Mj[(size_t)r * n + i0 + i] : 0.0;
-      b0[u] = (rin && i < b) ? Rj[(size_t)r * b + i] : 0.0;
-      b1[u] = (rin && 16 + i < b) ? Rj[(size_t)r * b + 16 + i] : 0.0;
+      b0[u] = (rin && i < b) ? Rj[(size_t)r * b + i] * w : 0.0;
+      b1[u] = (rin && 16 + i < b) ? Rj[(size_t)r * b + 16 + i] * w : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < QT_KB; ++u) {

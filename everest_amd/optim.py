@@ -45,7 +45,8 @@ class OptimizeStats:
     raw_evals: int = 0
     opt_evals: int = 0
     opt_iters: int = 0
-    t_raw: float = 0.0
+    t_raw: float = 0.0          # raw candidates: draw + screening
+    t_raw_draw: float = 0.0     # of which the draw (Sobol, or hit-and-run under linear constraints)
     t_opt: float = 0.0
     chunks: List[dict] = field(default_factory=list)
     restart_X: Optional[np.ndarray] = None    # the optimised restart candidates of this rank's last chunk
@@ -229,26 +230,24 @@ def hit_and_run(bounds: np.ndarray, ineq: Sequence[LinearConstraint], eq: Sequen
         N = np.eye(d)
     if N.shape[1] == 0:      # the equalities fix every dimension: the polytope is one point
         return np.repeat(x[None, :], n, axis=0)
-    rng = np.random.default_rng(seed)
-    out = np.empty((n, d))
-    total = n_burnin + n * n_thinning
-    k = 0
-    for it in range(total):
-        r = N @ rng.standard_normal(N.shape[1])
-        nr = np.linalg.norm(r)
-        if nr == 0.0:
-            continue
-        r /= nr
-        Ar = A @ r
-        slack = b - A @ x
-        with np.errstate(divide="ignore"):
-            t = slack / Ar
-        tmax = np.min(t[Ar > 1e-14]) if np.any(Ar > 1e-14) else 0.0
-        tmin = np.max(t[Ar < -1e-14]) if np.any(Ar < -1e-14) else 0.0
-        x = x + rng.uniform(tmin, tmax) * r
-        if it >= n_burnin and (it - n_burnin) % n_thinning == n_thinning - 1:
-            out[k] = x
-            k += 1
+    return hit_and_run_chain(A, b, N, x, n, seed, n_burnin, n_thinning)
+
+
+def hit_and_run_chain(A: np.ndarray, b: np.ndarray, N: np.ndarray, x0: np.ndarray, n: int, seed: int,
+                      n_burnin: int, n_thinning: int) -> np.ndarray:
+    """The chain of ``hit_and_run`` from the interior point x0 in x0 + span(N): the native
+    sampler (csrc/polytope.cpp, evr_hit_and_run; counter-based SplitMix64 variates)."""
+    from ._native import check, load
+
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    N = np.ascontiguousarray(N, dtype=np.float64)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    d, k = N.shape
+    out = np.empty((int(n), d))
+    p = lambda a: a.ctypes.data   # noqa: E731
+    check(load().evr_hit_and_run(d, A.shape[0], p(A), p(b), k, p(N), p(x0), int(n), int(seed) & (2 ** 64 - 1),
+                                 int(n_burnin), int(n_thinning), p(out)), "evr_hit_and_run")
     return out
 
 
@@ -451,6 +450,7 @@ def optimize_acqf(acqf, bounds: np.ndarray, num_restarts: int, raw_samples: int,
     else:
         fut = _RAW_PREFETCHED.pop(_raw_key(bounds, raw_samples, seed, q), None)
         X_raw = fut.result() if fut is not None else draw_sobol_samples(bounds, raw_samples, seed, q)
+    stats.t_raw_draw += time.perf_counter() - t0
     shp = (q, d) if q > 1 else (d,)          # one candidate (q-batch) of the acquisition
     # 2. evaluate (sharded over ranks, all-gather of the per-shard values)
     Xr = torch.as_tensor(X_raw, dtype=torch.float64, device=dev)

@@ -344,6 +344,19 @@ int evr_lbfgsb_step(evr_lbfgsb* h, double f, const double* g, double* x);
 void evr_lbfgsb_stats(const evr_lbfgsb* h, int* nit, int* nfev, double* f, double* pgnorm);
 void evr_lbfgsb_destroy(evr_lbfgsb* h);
 
+/* Hit-and-run sampler over {x : A x <= b} (rows x d, row-major), moving in x0 + span(N)
+ * (N: d x k, row-major; k = d and N = I without equality constraints).  x0 must be
+ * interior.  n_burnin + n * n_thinning steps from x0; every n_thinning-th step after the
+ * burn-in is written to out (n x d).  Step i draws its variates 2k + 1 from a counter-based
+ * SplitMix64 stream at counters i (2k + 1) + j: k Box-Muller normals (cos branch) for the
+ * direction, one uniform for the point on the chord.  Host-only.
+ * Replaces [upstream] HitAndRunPolytopeSampler / sample_q_batches_from_polytope, called by
+ * optimize_acqf under linear constraints (bofire/strategies/predictives/botorch.py:384-405)
+ * and by RandomStrategy (bofire/strategies/random.py:300-326). */
+int evr_hit_and_run(int d, int rows, const double* A, const double* b, int k, const double* N,
+                    const double* x0, long long n, unsigned long long seed, long long n_burnin,
+                    long long n_thinning, double* out);
+
 /* One joint restart problem driven natively on a backward plan: minimise
  * -sum_r acq(x_r) over the b restarts of `plan` in the box [lb, ub] (b*d host arrays each)
  * from x0 (b*d host), with scipy's wrapper rules (stop after maxiter iterations or more

@@ -269,3 +269,98 @@ def test_lbfgsb_advance_matches_generator_state_machine():
         assert all(np.array_equal(a, b) for a, b in zip(xs_adv, xs_gen))
         assert (int(nit[0]), int(nfev[0]), int(st[0])) == (res.nit, res.nfev, res.status)
         assert np.array_equal(X, res.x)
+
+
+def _hit_and_run_restated(A, b, N, x0, n, seed, n_burnin, n_thinning):
+    """Plain-Python restatement of csrc/polytope.cpp's chain (the counter-based SplitMix64
+    variates, Box-Muller cos branch, index-order sums): the native sampler must equal it step
+    for step."""
+    import math
+
+    M64 = (1 << 64) - 1
+
+    def uni(c):
+        z = (seed + (c + 1) * 0x9E3779B97F4A7C15) & M64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        z ^= z >> 31
+        return (z >> 11) * 2.0 ** -53
+
+    d, k = N.shape
+    x = [float(v) for v in x0]
+    out, per = [], 2 * k + 1
+    for it in range(n_burnin + n * n_thinning):
+        c0 = it * per
+        z = [math.sqrt(-2.0 * math.log(1.0 - uni(c0 + 2 * j))) * math.cos(6.283185307179586 * uni(c0 + 2 * j + 1))
+             for j in range(k)]
+        r, nr2 = [], 0.0
+        for i in range(d):
+            s = 0.0
+            for j in range(k):
+                s += float(N[i, j]) * z[j]
+            r.append(s)
+            nr2 += s * s
+        nr = math.sqrt(nr2)
+        if nr > 0.0:
+            r = [v / nr for v in r]
+            tmax = tmin = None
+            for q in range(A.shape[0]):
+                ar = ax = 0.0
+                for i in range(d):
+                    ar += float(A[q, i]) * r[i]
+                    ax += float(A[q, i]) * x[i]
+                if ar > 1e-14 or ar < -1e-14:
+                    t = (float(b[q]) - ax) / ar
+                    if ar > 1e-14:
+                        tmax = t if tmax is None or t < tmax else tmax
+                    else:
+                        tmin = t if tmin is None or t > tmin else tmin
+            u = uni(c0 + 2 * k)
+            lo_, hi_ = (tmin if tmin is not None else 0.0), (tmax if tmax is not None else 0.0)
+            step = lo_ + (hi_ - lo_) * u
+            x = [xi + step * ri for xi, ri in zip(x, r)]
+        if it >= n_burnin and (it - n_burnin) % n_thinning == n_thinning - 1:
+            out.append(list(x))
+    return np.array(out)
+
+
+def test_hit_and_run_native_chain_equals_restatement():
+    """evr_hit_and_run (the raw-candidate sampler of optimize_acqf under linear constraints,
+    [upstream] HitAndRunPolytopeSampler, bofire/strategies/predictives/botorch.py:384-405)
+    equals the plain-Python restatement bitwise: a Detergent-like 5-d box with two linear
+    inequalities, and the same with one equality (null-space directions)."""
+    from everest_amd.optim import _as_Ab, hit_and_run_chain
+
+    d = 5
+    bounds = np.array([[0.0] * d, [1.0, 0.8, 0.6, 1.0, 0.5]])
+    ineq = [([0, 1, 2], [-1.0, -1.0, -1.0], -1.2), ([2, 3, 4], [1.0, 1.0, 1.0], 0.2)]
+    A, b = _as_Ab(d, bounds, ineq)
+    x0 = np.array([0.2, 0.2, 0.2, 0.3, 0.1])
+    assert (A @ x0 < b).all()
+    for N, seed in ((np.eye(d), 12345), (np.linalg.svd(np.ones((1, d)))[2][1:].T, 2 ** 63 + 7)):
+        got = hit_and_run_chain(A, b, N, x0, 40, seed, 50, 3)
+        want = _hit_and_run_restated(A, b, N, x0, 40, seed, 50, 3)
+        assert got.shape == (40, d)
+        assert np.array_equal(got, want), np.abs(got - want).max()
+
+
+def test_hit_and_run_samples_feasible_and_uniform():
+    """Properties of the native sampler at the optimizer's defaults (burn-in 10000, thinning
+    32): every sample inside the polytope; on the triangle {x, y >= 0, x + y <= 1} the sample
+    mean is the centroid (1/3, 1/3) and each of the four congruent sub-triangles holds a
+    quarter of the samples; with an equality constraint every sample lies on it."""
+    from everest_amd.optim import hit_and_run
+
+    bounds = np.array([[0.0, 0.0], [1.0, 1.0]])
+    X = hit_and_run(bounds, [([0, 1], [-1.0, -1.0], -1.0)], [], 4000, seed=3)
+    assert X.shape == (4000, 2)
+    assert (X >= -1e-12).all() and (X.sum(1) <= 1.0 + 1e-12).all()
+    assert np.abs(X.mean(0) - 1.0 / 3.0).max() < 0.02
+    mid = (X[:, 0] >= 0.5).mean(), (X[:, 1] >= 0.5).mean(), (X.sum(1) <= 0.5).mean()
+    assert all(abs(f - 0.25) < 0.03 for f in mid), mid
+    bounds3 = np.array([[0.0] * 3, [1.0] * 3])
+    Y = hit_and_run(bounds3, [], [([0, 1, 2], [1.0, 1.0, 1.0], 1.0)], 500, seed=9, n_burnin=200, n_thinning=4)
+    assert np.abs(Y.sum(1) - 1.0).max() < 1e-10 and (Y >= -1e-12).all()
+    # seeded: the same seed gives the same samples, another seed others
+    assert np.array_equal(Y, hit_and_run(bounds3, [], [([0, 1, 2], [1.0, 1.0, 1.0], 1.0)], 500, seed=9,
+                                         n_burnin=200, n_thinning=4))

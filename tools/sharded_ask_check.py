@@ -5,7 +5,7 @@ The parent never touches HIP: it starts one 1-rank child, then ``--ranks`` child
 share the box's GPU(s) round-robin and exchange over gloo (the RCCL path is the same code
 with "nccl"; bench.py EVR_DIST_BACKEND).  Every child builds the config-4 QnehviStrategy
 (bench.make_ask_strategy: DTLZ2(6, 5), n = 512, S = 256, 1024 raw, 20 restarts,
-batch_limit 20, seed 1) and runs ``--asks`` asks; rank 0 writes per ask the candidate x, the
+batch_limit 20 or ``--batch-limit``, seed 1) and runs ``--asks`` asks; rank 0 writes per ask the candidate x, the
 best acquisition value, the global optimiser evaluation count, the restart driver label and
 the ask time.  The parent compares the two runs and writes ``DIR/sharded_ask.json``.
 
@@ -37,7 +37,8 @@ def child(args):
         import torch.distributed as dist
 
         dist.init_process_group("gloo")
-    s, tells = bench.make_ask_strategy(args.n, args.S, args.raw, args.restarts, world, dist, seed=1)
+    s, tells = bench.make_ask_strategy(args.n, args.S, args.raw, args.restarts, world, dist, seed=1,
+                                       batch_limit=args.batch_limit)
     out = []
     for _ in range(args.asks):
         torch.cuda.synchronize()
@@ -87,6 +88,7 @@ def main():
     ap.add_argument("--S", type=int, default=256)
     ap.add_argument("--raw", type=int, default=1024)
     ap.add_argument("--restarts", type=int, default=20)
+    ap.add_argument("--batch-limit", type=int, default=0, help="0: = restarts (one joint problem)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sharded"))
     args = ap.parse_args()
     if args.child:
@@ -109,7 +111,7 @@ def main():
                      "drivers": [p["drivers"], q["drivers"]], "ask_s": [p["ask_s"], q["ask_s"]]})
     res = {"ranks": args.ranks, "backend": "gloo (ranks share the box's GPU; RCCL on a multi-GPU node)",
            "config": f"DTLZ2(6,5) n={args.n} S={args.S} raw={args.raw} restarts={args.restarts} batch_limit="
-                     f"{args.restarts} seed=1", "asks": rows,
+                     f"{args.batch_limit or args.restarts} seed=1", "asks": rows,
            "all_bitwise_equal": all(r["x_bitwise_equal"] and r["best_value_bitwise_equal"] for r in rows)}
     with open(os.path.join(args.out, "sharded_ask.json"), "w") as f:
         json.dump(res, f, indent=1)
