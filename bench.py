@@ -512,9 +512,8 @@ def _launched_kernel(acqf, op, b, d):
                 "proj_bwd": r"qs_bwd" if ops.qnehvi_small_applies(acqf.state, b, d) else r"Cijk_|qn_proj_bwd",
                 "kernel_grad": r"kcross_grad"}.get(op, re.escape(op))
     if ops.qnehvi_small_applies(acqf.state, b, d) and ops.hvi_restart_fb_applies(acqf.state, b):
-        # the restart-scan variant (hvi.hip restart_variant: kdw by default, EVR_RESTART_SCAN=kdb|kd3);
-        # exactly one of them runs in the chain
-        return r"hvi_kd[3bw]<"
+        # the one-launch restart scan (hvi.hip hvi_kdw)
+        return r"hvi_kdw<"
     return r"hvi_kd2?<|hvi_tiled<"
 
 
@@ -824,18 +823,10 @@ def main():
                        sampler_seed=1234, prune_baseline=True, prune_seed=4321)
         qlog = {"note": "qLogNEHVI forward + backward (tabulated fat-smoothed log scan over every compressed "
                         "cell), same GPs and seeds as eval_pass; device time between HIP events incl. any host "
-                        "syncs; *_kd_ms: EVR_LOG=kd (kd groups whose bound is below 2^-60 of the sample's sum "
-                        "skipped, A/B)",
+                        "syncs",
                 "cells_total": qa.stats.total_cells, "box_decomposition": qa.box_path}
         for bb, XX in ((args.b, Xc), (b_r, Xr)):
             qlog[f"b{bb}_ms"] = round(_event_ms(lambda: qa.forward_backward(XX), reps=10), 4)
-        os.environ["EVR_LOG"] = "kd"
-        qa._plans = {}
-        try:
-            qlog[f"b{args.b}_kd_ms"] = round(_event_ms(lambda: qa.forward_backward(Xc), reps=5), 4)
-        finally:
-            del os.environ["EVR_LOG"]
-            qa._plans = {}
         del qa
 
     if rank == 0:

@@ -115,8 +115,6 @@ _SIGS = {
     "evr_hvi_forward_backward": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 6, c_int),
     "evr_hvi_restart_fb_applies": ([POINTER(EvrQnehviState), c_int], c_int),
     "evr_hvi_restart_fb": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 3, c_int),
-    "evr_hvi_set_restart_variant": ([c_int], c_int),
-    "evr_hvi_set_kd_variant": ([c_int], c_int),
     "evr_qnehvi_norms_rows": ([POINTER(EvrQnehviState)], c_int),
     "evr_qnehvi_project": ([c_void_p, POINTER(EvrQnehviState), c_int] + [c_void_p] * 5, c_int),
     "evr_qnehvi_project_workspace_doubles": ([POINTER(EvrQnehviState), c_int], c_longlong),

@@ -287,7 +287,7 @@ __global__ __launch_bounds__(KD_THREADS) void cells_kd_kernel(int stride, const 
     CKD_ACC(3, ck);
     ck = CKD_NOW();
     // the levels whose segments fit a wave sort them apart; the first levels sort the whole
-    // buffer (ws_max = 0, EVR_KD_WS=0: always the full sort — A/B, same order)
+    // buffer
     if (sh_maxlen <= ws_max) {
       kd_wave_sort(sb, segl, sh_nseg, segE, C);
       __syncthreads();
@@ -385,12 +385,9 @@ int evr_cells_kd_order_device(void* stream, int S, int m, int stride, const int*
   EVR_CHECK(evr_cells_kd_limits(stride, m, max_cells, &lds) == 0,
             "evr_cells_kd_order_device: %d cells / %d point rows exceed the kd kernel limits", max_cells, stride);
   hipStream_t s = (hipStream_t)stream;
-  // u32 sort keys when every field fits (KdKey); EVR_KD_KEY64=1 keeps the u64 layout (A/B: same order)
-  const char* ek = std::getenv("EVR_KD_KEY64");   // read per call (a test switches it)
-  const bool key64 = ek && ek[0] == '1';
-  const bool k32 = !key64 && max_cells < 8192 && stride < 1023;
-  const char* ew = std::getenv("EVR_KD_WS");   // read per call (a test switches it)
-  const int ws_max = (ew && ew[0] == '0') ? 0 : KD_WS_MAX;
+  // u32 sort keys when every field fits (KdKey), the u64 layout otherwise (the same order)
+  const bool k32 = max_cells < 8192 && stride < 1023;
+  const int ws_max = KD_WS_MAX;
 #define LK(MM, KT_)                                                                                        \
   do {                                                                                                     \
     EVR_HIP(hipFuncSetAttribute((const void*)cells_kd_kernel<MM, KT_>,                                    \

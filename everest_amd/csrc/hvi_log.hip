@@ -380,298 +380,33 @@ __global__ __launch_bounds__(HLK_THREADS) void hvi_logk_kernel(int b, int nsplit
   hlk_merge_out<M, BWD, CT, HLK_THREADS>(st, nc, tab, out, s, nsplit, split, b, c0);
 }
 
-// ---- kd-bounded keyed scan ---------------------------------------------------------------
-// The fat tails keep every cell's term positive, but most are negligible: a cell whose lower
-// corner lies above y_j in two or more objectives carries log terms of ~-35 each (tau_relu =
-// 1e-6) against ~-10 for the cells that bound y.  The kd-ordered groups of 16 cells
-// (cells_kd.hip: keys in kd order, per-cell rank coordinates, the group's minimum rank per
-// objective) bound every cell of a group at once: fatmin(a, b) <= min(a, b) <= a and the
-// tabulated psi (objective 0: its whole fatmin term) is non-increasing in the lower bound l,
-// so a_k <= B_g = sum_j tab[c][j][min rank_j of group g] for every cell k of g.  Per (sample,
-// candidate) the workgroup takes the group of largest bound, evaluates its 16 cells exactly
-// (A = their maximum, a lower bound on the sample's log-sum-exp) and skips every group with
-// B_g < A - 60 ln 2 - log(16 G): the skipped mass is below 2^-60 of the sample's sum.  The
-// threshold depends on (sample, candidate) alone — not on the split, the batch or thread
-// timing — and the surviving groups are compacted in kd order by a ballot prefix scan, so the
-// result is deterministic.  Opt-in (EVR_LOG=kd, see hl_kd): measured slower at the bench state.
-constexpr double HLKD_SKIP_LOG = 41.58883083359671856;   // 60 ln 2
-constexpr int HLKD_MAXG = 512;                           // cells_kd.hip KD_MAX_CELLS / 16
-constexpr unsigned short HLKD_PAD = 0x7FFF;
-
-__host__ __device__ inline size_t hlkd_bnd_off(int stride, int M, int CT, bool bwd) {
-  return hlk_lds_bytes(stride, M, CT, bwd);
-}
-__host__ __device__ inline size_t hlkd_lds_bytes(int stride, int M, int CT, bool bwd, int max_groups) {
-  return hlkd_bnd_off(stride, M, CT, bwd) + (size_t)max_groups * CT * 8 + (size_t)max_groups * 4 +
-         (16 + 2 * CT) * 8;
-}
-
-// lam_j = log(min(u_j, 1e10) - l_j) of a kd-ordered key (field 0: point index), j >= 1
-template <int M>
-__device__ __forceinline__ void hlkd_lam(unsigned long long key, const double* pt, double* lam,
-                                         const FastLogTabs& T) {
-  using K = CellKey<M>;
-  int P[M];
-#pragma unroll
-  for (int j = 0; j < M; ++j) P[j] = K::field(key, j);
-#pragma unroll
-  for (int j = 1; j < M; ++j) {
-    double bl = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < j; ++i) bl = fmax(bl, pt[P[i] * M + j]);
-    lam[j] = log_tab(fmin(-bl, HL_UMAX) - (-pt[P[j] * M + j]), T);
-  }
-}
-
-// a_k (and da_k / dy) of one cell for one candidate from the rank-indexed table tc [M][stride]
-template <int M, bool BWD>
-__device__ __forceinline__ double hlkd_term(const double* tc, int stride, const int* R, const double* lam,
-                                            double tm, double itm, double* da, const FastLogTabs& T) {
-  double a = 0.0;
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const size_t ti = (size_t)j * stride + R[j];
-    double v, dv = 0.0;
-    if (BWD) {
-      const double2 pd = *reinterpret_cast<const double2*>(tc + 2 * ti);
-      v = pd.x;
-      dv = pd.y;
-    } else {
-      v = tc[ti];
-    }
-    if (j == 0) {
-      a = v;
-      da[0] = dv;
-    } else {
-      double dfm;
-      a += fatmin_fast(v, lam[j], tm, itm, &dfm, T);
-      da[j] = dfm * dv;
-    }
-  }
-  return a;
-}
-
-template <int M, bool BWD, int CT, int NT>
-__global__ __launch_bounds__(NT) void hvi_logkd_kernel(int b, int nsplit, int stride, const double* __restrict__ G,
-                                                       const int* __restrict__ goff,
-                                                       const unsigned long long* __restrict__ gkeys,
-                                                       const unsigned short* __restrict__ grank,
-                                                       const unsigned short* __restrict__ gbox,
-                                                       const double* __restrict__ pts,
-                                                       const double* __restrict__ slo, double tr, double tm,
-                                                       double* __restrict__ out) {
-  constexpr int NW = NT / 64;
-  extern __shared__ __align__(16) unsigned char hl_dyn[];
-  double* pt = (double*)hl_dyn;
-  FastLogTabs& T = *reinterpret_cast<FastLogTabs*>(hl_dyn + hlk_flt_off(stride, M));
-  double* tab = (double*)(hl_dyn + hlk_tab_off(stride, M));
-  const int s = blockIdx.y, split = blockIdx.z, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g0 = goff[s], Gs = goff[s + 1] - g0;
-  double* bnd = (double*)(hl_dyn + hlkd_bnd_off(stride, M, CT, BWD));   // [g][c]
-  int* list = (int*)(bnd + (size_t)Gs * CT);                            // surviving groups | bits << 16
-  double* scr = (double*)(((uintptr_t)(list + Gs) + 15) & ~(uintptr_t)15);
-  int* wtot = (int*)scr;                                                // NW ints (<= 16)
-  double* thr = scr + 8;                                                // CT thresholds
-  int* best = (int*)(thr + CT);                                         // CT group indices
-  T.fill(tid, NT);
-  __syncthreads();
-  const int c0 = blockIdx.x * CT;
-  const int nc = min(CT, b - c0);
-  const double* gp = pts + (size_t)s * stride * M;
-  for (int e = tid; e < stride * M; e += NT) pt[e] = gp[e];
-  const double itm = 1.0 / tm;
-  // table [c][j][r] over the ascending lower bounds l = sorted_lo[s][j][r] (the values the
-  // unbounded keyed table takes, in rank order): objective 0 its whole fatmin term
-  for (int e = tid; e < CT * M * stride; e += NT) {
-    const int c = e / (M * stride), r = e - c * (M * stride), j = r / stride, p = r - j * stride;
-    const int gc = min(c0 + c, b - 1);
-    const double lo = slo[((size_t)s * M + j) * stride + p];
-    const double z = G[((size_t)s * M + j) * b + gc] - lo;
-    double dpsi = 0.0;
-    double v = log_fatplus(z, tr, BWD ? &dpsi : nullptr);
-    if (j == 0) {
-      double dfm;
-      v = fatmin_fast(v, log(HL_UMAX - lo), tm, itm, &dfm, T);
-      dpsi *= dfm;
-    }
-    if (BWD) {
-      tab[2 * (size_t)e] = v;
-      tab[2 * (size_t)e + 1] = dpsi;
-    } else {
-      tab[e] = v;
-    }
-  }
-  __syncthreads();
-  auto tv = [&](int c, int j, int r) -> double { return tab[(BWD ? 2 : 1) * (((size_t)c * M + j) * stride + r)]; };
-  // 1. group bounds and the group of largest bound per candidate (smallest index on ties)
-  double bm[CT];
-  int bg[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    bm[c] = -INFINITY;
-    bg[c] = 0x7FFFFFFF;
-  }
-  for (int g = tid; g < Gs; g += NT) {
-    const uint4 bx = *reinterpret_cast<const uint4*>(gbox + (size_t)(g0 + g) * 8);
-    const unsigned int bw[4] = {bx.x, bx.y, bx.z, bx.w};
-    int r[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) r[j] = (int)((bw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      double v = 0.0;
-#pragma unroll
-      for (int j = 0; j < M; ++j) v += tv(c, j, r[j]);
-      bnd[(size_t)g * CT + c] = v;
-      if (v > bm[c]) {
-        bm[c] = v;
-        bg[c] = g;
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double om = __shfl_xor(bm[c], o);
-      const int og = __shfl_xor(bg[c], o);
-      if (om > bm[c] || (om == bm[c] && og < bg[c])) {
-        bm[c] = om;
-        bg[c] = og;
-      }
-    }
-  }
-  // per-wave winners, NW x CT (value, index)
-  __shared__ double s_wv[16][CT];
-  __shared__ int s_wg[16][CT];
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      s_wv[w][c] = bm[c];
-      s_wg[w][c] = bg[c];
-    }
-  }
-  __syncthreads();
-  if (tid < CT) {
-    double v = s_wv[0][tid];
-    int g = s_wg[0][tid];
-    for (int q = 1; q < NW; ++q) {
-      if (s_wv[q][tid] > v || (s_wv[q][tid] == v && s_wg[q][tid] < g)) {
-        v = s_wv[q][tid];
-        g = s_wg[q][tid];
-      }
-    }
-    best[tid] = (g < Gs) ? g : -1;
-  }
-  __syncthreads();
-  // 2. exact terms of the best group's 16 cells per candidate -> threshold (wave 0)
-  if (w == 0) {
-    const int c = lane >> 4, i = lane & 15;
-    double a = -INFINITY;
-    const int g = (c < nc) ? best[c] : -1;
-    if (g >= 0) {
-      int R[M];
-#pragma unroll
-      for (int j = 0; j < M; ++j) R[j] = grank[((size_t)(g0 + g) * M + j) * 16 + i];
-      if (R[0] != HLKD_PAD) {
-        double lam[M], da[M];
-        hlkd_lam<M>(gkeys[(size_t)(g0 + g) * 16 + i], pt, lam, T);
-        a = hlkd_term<M, BWD>(tab + (size_t)c * M * stride * (BWD ? 2 : 1), stride, R, lam, tm, itm, da, T);
-      }
-    }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) a = fmax(a, __shfl_xor(a, o, 16));
-    if (i == 0 && c < CT)
-      thr[c] = (a > -INFINITY) ? a - HLKD_SKIP_LOG - log(16.0 * (double)Gs) : -INFINITY;
-  }
-  __syncthreads();
-  // 3. surviving groups (bit c: B_g >= threshold_c; a NaN bound survives), compacted in kd
-  // order by a ballot prefix scan
-  int L = 0;
-  for (int base = 0; base < Gs; base += NT) {
-    const int g = base + tid;
-    int bits = 0;
-    if (g < Gs) {
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-        if (c < nc && !(bnd[(size_t)g * CT + c] < thr[c])) bits |= 1 << c;
-    }
-    const unsigned long long mask = __ballot(bits != 0);
-    const int pos = __popcll(mask & ((1ull << lane) - 1ull));
-    if (lane == 0) wtot[w] = __popcll(mask);
-    __syncthreads();
-    int offw = L, tot = 0;
-    for (int q = 0; q < NW; ++q) {
-      if (q < w) offw += wtot[q];
-      tot += wtot[q];
-    }
-    if (bits) list[offw + pos] = g | (bits << 16);
-    L += tot;
-    __syncthreads();
-  }
-  // 4. the surviving cells of this split's share of the list
-  LseState<M, BWD> st[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) st[c].init();
-  const int per = (L + nsplit - 1) / nsplit;
-  const int lb = min(L, split * per), le = min(L, lb + per);
-  for (int k = lb * 16 + tid; k < le * 16; k += NT) {
-    const int e = list[k >> 4], g = e & 0xFFFF, bits = e >> 16, i = k & 15;
-    int R[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) R[j] = grank[((size_t)(g0 + g) * M + j) * 16 + i];
-    if (R[0] == HLKD_PAD) continue;
-    double lam[M];
-    hlkd_lam<M>(gkeys[(size_t)(g0 + g) * 16 + i], pt, lam, T);
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      if ((bits >> c) & 1) {
-        double da[M];
-        const double a =
-            hlkd_term<M, BWD>(tab + (size_t)c * M * stride * (BWD ? 2 : 1), stride, R, lam, tm, itm, da, T);
-        lse_add_tab(st[c], a, da, T);
-      }
-    }
-  }
-  hlk_merge_out<M, BWD, CT, NT>(st, nc, tab, out, s, nsplit, split, b, c0);
-}
+// (A kd-bounded variant that skipped kd groups bounded below 2^-60 of the sample's sum was
+// measured slower at the bench state — 10.3 vs 9.4 ms at b = 512, profiles/r05/m: with
+// tau_relu = 1e-6 few groups fall below the bound — and removed in round 6.)
 
 struct HlPlan {
   int CT, nsplit, CB;
-  bool keyed, kd;
+  bool keyed;
 };
 
-static int hlk_ct_bwd() {   // 2 (default) or EVR_LOGK=4 (CT = 4 / 1024 threads: 128-VGPR cap, measured slower)
-  const char* e = std::getenv("EVR_LOGK");   // read per plan (tests switch it)
-  return (e && e[0] == '4') ? 4 : 2;
-}
+// candidates per workgroup of the keyed backward (CT = 4 with 1024 threads measured slower:
+// 11.7 vs 9.7 ms, the 128-VGPR cap spills)
+constexpr int HLK_CT_BWD = 2;
 
 static bool hl_keyed(const evr_qnehvi_state* st, bool bwd) {
-  const char* e = std::getenv("EVR_LOG");   // read per plan (tests switch it)
+  // EVR_LOG=dense: the dense kernel over the explicit rows even when keys exist (the parity
+  // test's reference; read per plan)
+  const char* e = std::getenv("EVR_LOG");
   const bool dense = e && !std::strcmp(e, "dense");
   return !dense && st->cell_keys && st->cell_pts && st->cell_rank0 && st->pts_stride > 0 &&
-         hlk_lds_bytes(st->pts_stride, st->m, bwd ? hlk_ct_bwd() : HLK_CT_FWD, bwd) <= 150 * 1024;
-}
-
-// the kd-bounded scan, opt-in (EVR_LOG=kd): compressed cells with kd groups.  Measured slower
-// than the unbounded keyed scan at the bench state (10.3 vs 9.4 ms at b = 512, profiles/r05/m:
-// with tau_relu = 1e-6 a cell above y in one objective still lies within 2^-60 of the maximum,
-// so few groups fall below the bound)
-static bool hl_kd(const evr_qnehvi_state* st, bool bwd) {
-  const char* e = std::getenv("EVR_LOG");   // read per plan (tests switch it)
-  if (!e || std::strcmp(e, "kd")) return false;
-  return st->grp_off && st->grp_keys && st->grp_rank && st->grp_box && st->sorted_lo && st->max_groups >= 0 &&
-         st->max_groups <= HLKD_MAXG &&
-         hlkd_lds_bytes(st->pts_stride, st->m, bwd ? hlk_ct_bwd() : HLK_CT_FWD, bwd, st->max_groups) <=
-             150 * 1024;
+         hlk_lds_bytes(st->pts_stride, st->m, bwd ? HLK_CT_BWD : HLK_CT_FWD, bwd) <= 150 * 1024;
 }
 
 static HlPlan hl_plan(const evr_qnehvi_state* st, int b, bool bwd) {
   HlPlan p;
   p.keyed = hl_keyed(st, bwd);
-  p.kd = p.keyed && hl_kd(st, bwd);
   if (p.keyed)
-    p.CT = bwd ? hlk_ct_bwd() : HLK_CT_FWD;
+    p.CT = bwd ? HLK_CT_BWD : HLK_CT_FWD;
   else
     p.CT = b >= 48 ? 64 : (b > 16 ? 32 : 16);
   const int ctiles = cdiv(b, p.CT);
@@ -680,10 +415,6 @@ static HlPlan hl_plan(const evr_qnehvi_state* st, int b, bool bwd) {
   p.nsplit = std::min(want, cdiv(maxc, HL_CHUNK));
   p.CB = cdiv(cdiv(maxc, p.nsplit), HL_CHUNK) * HL_CHUNK;
   p.nsplit = cdiv(maxc, p.CB);
-  if (p.kd) {   // splits share the surviving-group list: at least 8 groups per split
-    p.nsplit = std::max(1, std::min(want, st->max_groups / 8));
-    p.CB = 0;
-  }
   return p;
 }
 
@@ -697,25 +428,7 @@ static int hvi_log_launch_m(hipStream_t s, const evr_qnehvi_state* st, int b, co
                             const double* gout, double* work, double* acq, double* dG) {
   const HlPlan p = hl_plan(st, b, BWD);
   dim3 grid(cdiv(b, p.CT), st->S, p.nsplit);
-  if (p.kd) {
-    const size_t lds = hlkd_lds_bytes(st->pts_stride, M, p.CT, BWD, st->max_groups);
-#define HLKD_GO(CT_, NT_)                                                                                      \
-  do {                                                                                                         \
-    EVR_HIP(hipFuncSetAttribute((const void*)hvi_logkd_kernel<M, BWD, CT_, NT_>,                               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                        \
-    hvi_logkd_kernel<M, BWD, CT_, NT_><<<grid, NT_, lds, s>>>(b, p.nsplit, st->pts_stride, G, st->grp_off,      \
-                                                              st->grp_keys, st->grp_rank, st->grp_box,         \
-                                                              st->cell_pts, st->sorted_lo, st->tau_relu,       \
-                                                              st->tau_max, work);                              \
-  } while (0)
-    if (!BWD)
-      HLKD_GO(HLK_CT_FWD, 1024);
-    else if (p.CT == 2)
-      HLKD_GO(2, 512);
-    else
-      HLKD_GO(4, 1024);
-#undef HLKD_GO
-  } else if (p.keyed) {
+  if (p.keyed) {
     const size_t lds = hlk_lds_bytes(st->pts_stride, M, p.CT, BWD);
 #define HLK_GO(CT_, NT_)                                                                                     \
   do {                                                                                                       \
@@ -727,10 +440,8 @@ static int hvi_log_launch_m(hipStream_t s, const evr_qnehvi_state* st, int b, co
   } while (0)
     if (!BWD)
       HLK_GO(HLK_CT_FWD, 1024);
-    else if (p.CT == 2)
-      HLK_GO(2, 512);
     else
-      HLK_GO(4, 1024);
+      HLK_GO(HLK_CT_BWD, 512);
 #undef HLK_GO
   } else {
     EVR_CHECK(st->cell_lo && st->cell_hi, "hvi (log): the dense log-space scan needs explicit cells");

@@ -17,40 +17,16 @@ namespace evr {
 constexpr int KT = 64;
 constexpr int KMAXD = 64;
 
-// Host-driven evaluations queued one ahead (qnehvi_plan.hip): the first kernel of the queued
-// chain waits here until the host posts the next request — the request word (pinned host
-// memory, written after the candidates) differs from the sequence number the previous chain
-// processed (device memory).  Thread 0 polls with relaxed loads of the fine-grained host
-// word (uncached: every poll reads host memory); the workgroup barrier after the poll orders
-// the candidates' loads — the same uncached host memory, written before the request word —
-// after it.  No system-scope fence: its L2 writeback / invalidate cost the chain 25 us per
-// evaluation (its operator M is L2-resident across evaluations).  A 2 s failsafe ends the
-// wait (the host's own wait then times out with an error).
-__device__ __forceinline__ void kmat_wait_request(const unsigned long long* poll, const unsigned long long* plast) {
-  if (threadIdx.x == 0) {
-    const unsigned long long last = *plast;
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(const_cast<unsigned long long*>(poll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
-           last) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 200000000ull) break;   // s_memrealtime: 100 MHz
-    }
-  }
-  __syncthreads();
-}
-
 template <int RA, int KIND>
 __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int d, const double* __restrict__ X1,
                                                    const double* __restrict__ sh1, const double* __restrict__ sc1,
                                                    const double* __restrict__ X2, const double* __restrict__ sh2,
                                                    const double* __restrict__ sc2, const double* __restrict__ ls,
                                                    const double* __restrict__ os, const double* __restrict__ dg,
-                                                   double* __restrict__ K, const unsigned long long* poll,
-                                                   const unsigned long long* plast,
+                                                   double* __restrict__ K,
                                                    const unsigned long long* seq_src, unsigned long long* seq_dst,
                                                    double* __restrict__ x_dst) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  if (poll) kmat_wait_request(poll, plast);
   // host-driven chains: the evaluation's sequence number (pinned host memory, posted with the
   // candidates) copied to device memory, so the chain's last kernel reads it from L2 instead of
   // across PCIe (this kernel's candidate loads pay that latency anyway)
@@ -73,8 +49,6 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
     xw[t] = 0.0;
     if (e < KT * d) {
       if (r < 16 * RA && i0 + r < n1) xv[t] = X1[(size_t)(i0 + r) * d + (e - r * d)];
-      // (a queued chain's candidates live in fine-grained host memory, which the GPU does not
-      // cache: these loads read what the host posted before the request word)
       if (j0 + r < n2) xw[t] = X2[(size_t)(j0 + r) * d + (e - r * d)];
     }
   }
@@ -159,16 +133,16 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
 using kd4_t = __attribute__((ext_vector_type(4))) double;
 using kd2_t = __attribute__((ext_vector_type(2))) double;
 
-template <int DP, int KIND, int EPI>
+template <int DP, int KIND>
 __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
                                                         const double* __restrict__ X1, const double* __restrict__ sh1,
                                                         const double* __restrict__ sc1, const double* __restrict__ X2,
                                                         const double* __restrict__ sh2, const double* __restrict__ sc2,
                                                         const double* __restrict__ ls, const double* __restrict__ os,
                                                         const double* __restrict__ dg, double* __restrict__ K) {
-  // operand tiles As / Bs; EPI 1 / 2 reuse the same storage for the output tile
-  constexpr int OPS = 2 * DP * (KT + 2), OUT = EPI ? KT * (KT + 1) : 0;
-  __shared__ double smem[OPS > OUT ? OPS : OUT];
+  // operand tiles As / Bs
+  constexpr int OPS = 2 * DP * (KT + 2);
+  __shared__ double smem[OPS];
   double (*As)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem);
   double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
   __shared__ double na[KT], nb2[KT];
@@ -255,83 +229,30 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n1 * n2;
   const int col = lane & 15, rq = lane >> 4;
-  if (EPI == 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-        const int gi = i0 + li, gj = j0 + lj;
-        if (gi < n1 && gj < n2) {
-          double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-          if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
-#if EVR_KMAT_DIAG == 1   // profiling builds only: no kernel evaluation (the epilogue's VALU share)
-          double v = scale * d2;
-#else
-          double v = scale * kernel_value_t(KIND, d2, kexp);
-#endif
-          if (gi == gj) v += dadd;
-#if EVR_KMAT_DIAG == 2   // profiling builds only: no output stream (the store share)
-          if (v == -1.25) Kb[(size_t)gi * n2 + gj] = v;
-#else
-          Kb[(size_t)gi * n2 + gj] = v;
-#endif
-        }
-      }
-    return;
-  }
-  // EPI 1 / 2: the tile's values go through LDS (aliasing the operand tiles, whose MFMA reads
-  // are done) so that every store instruction writes one contiguous 512-byte row segment
-  // (EPI 2: non-temporal stores — the output is not re-read by this kernel)
-  double vals[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
       const int gi = i0 + li, gj = j0 + lj;
-      double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-      if (gi == gj && eqr[li]) d2 = 0.0;
-      double v = scale * kernel_value_t(KIND, d2, kexp);
-      if (gi == gj) v += dadd;
-      vals[4 * q + r] = v;
-    }
-  __syncthreads();   // every wave is done with As / Bs
-  double (*T)[KT + 1] = reinterpret_cast<double (*)[KT + 1]>(smem);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[4 * q + r];
-  __syncthreads();
-  if (EPI == 3) {
-    // 16 bytes per lane: a store instruction writes two 512-byte row segments (lanes 0-31 row
-    // rr, lanes 32-63 row rr + 1; the plain fill of the config-5 output runs at 4.8 TB/s this
-    // way vs 4.3 TB/s with 8 bytes per lane, tools/micro/fill_probe.hip)
-    const int c2 = 2 * (lane & 31), gj2 = j0 + c2;
-#pragma unroll 4
-    for (int rr = 2 * wave + (lane >> 5); rr < KT; rr += 8) {
-      const int gi = i0 + rr;
-      if (gi >= n1) continue;
-      double* o = Kb + (size_t)gi * n2 + gj2;
-      const double v0 = T[rr][c2], v1 = T[rr][c2 + 1];
-      if (gj2 + 1 < n2 && (((uintptr_t)o) & 15) == 0) {
-        *reinterpret_cast<kd2_t*>(o) = kd2_t{v0, v1};
-      } else {
-        if (gj2 < n2) o[0] = v0;
-        if (gj2 + 1 < n2) o[1] = v1;
+      if (gi < n1 && gj < n2) {
+        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
+        if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
+#if EVR_KMAT_DIAG == 1   // profiling builds only: no kernel evaluation (the epilogue's VALU share)
+        double v = scale * d2;
+#else
+        double v = scale * kernel_value_t(KIND, d2, kexp);
+#endif
+        if (gi == gj) v += dadd;
+#if EVR_KMAT_DIAG == 2   // profiling builds only: no output stream (the store share)
+        if (v == -1.25) Kb[(size_t)gi * n2 + gj] = v;
+#else
+        Kb[(size_t)gi * n2 + gj] = v;
+#endif
       }
     }
-    return;
-  }
-  const int gj = j0 + lane;
-#pragma unroll 4
-  for (int rr = wave; rr < KT; rr += 4) {
-    const int gi = i0 + rr;
-    if (gi < n1 && gj < n2) {
-      if (EPI == 2) __builtin_nontemporal_store(T[rr][lane], Kb + (size_t)gi * n2 + gj);
-      else Kb[(size_t)gi * n2 + gj] = T[rr][lane];
-    }
-  }
+  // (LDS-staged row-segment epilogues, with and without non-temporal or 16-byte stores, were
+  // measured slower at config 5 and removed in round 6: profiles/r05/p/kmat_epi*.json)
 }
 
 // Symmetric train matrix K(X, X) (the GP fit's case: both operands the same rows with the same
@@ -465,139 +386,6 @@ __global__ __launch_bounds__(256) void kmat_mfma_sym(int n, int d, int B, const 
   }
 }
 
-// Persistent form of kmat_mfma_kernel for large outputs (DP = 16 / 32 / 64): a workgroup
-// walks tiles t = blockIdx.x, + gridDim.x, ...  The next tile's operand rows (and its
-// lengthscales) are loaded into registers right after the current tile's MFMAs, before the
-// current epilogue's stores, so the stores of tile t drain while tile t + 1's loads are in
-// flight (vmcnt retires in issue order: loads issued after the stores would wait for them).
-// One-shot launches leave every workgroup in the same phase — all staging, then all
-// storing — and the output stream never overlaps the operand fetch.  Values bitwise equal
-// kmat_mfma_kernel's (same staging arithmetic, MFMA order and epilogue).
-template <int DP, int KIND>
-__global__ __launch_bounds__(256) void kmat_mfma_pers(int n1, int n2, int d, int B, const double* __restrict__ X1,
-                                                      const double* __restrict__ sh1, const double* __restrict__ sc1,
-                                                      const double* __restrict__ X2, const double* __restrict__ sh2,
-                                                      const double* __restrict__ sc2, const double* __restrict__ ls,
-                                                      const double* __restrict__ os, const double* __restrict__ dg,
-                                                      double* __restrict__ K) {
-  static_assert(256 % DP == 0, "one coordinate per thread");
-  constexpr int NE = KT * DP / 256;   // operand elements per thread and operand
-  __shared__ double As[DP][KT + 2], Bs[DP][KT + 2];
-  __shared__ double na[KT], nb2[KT];
-  __shared__ int eqr[KT];
-  __shared__ double kexp[64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int gx = (n2 + KT - 1) / KT, gy = (n1 + KT - 1) / KT, T = gx * gy * B;
-  const int k = tid % DP, r0 = tid / DP;   // this thread's coordinate; rows r0 + (256 / DP) t
-  constexpr int RS = 256 / DP;
-  // batch-independent normalisation of coordinate k
-  const bool kin = k < d;
-  const double s1 = (kin && sh1) ? sh1[k] : 0.0, c1 = (kin && sc1) ? sc1[k] : 1.0;
-  const double s2 = (kin && sh2) ? sh2[k] : 0.0, c2 = (kin && sc2) ? sc2[k] : 1.0;
-  kexp_stage(kexp, tid, 256);
-  double v[NE], w[NE], lk = 1.0;
-  auto fetch = [&](int t) {
-    const int b = t / (gx * gy), rem = t - b * gx * gy, i0 = (rem / gx) * KT, j0 = (rem % gx) * KT;
-    lk = kin ? ls[(size_t)b * d + k] : 1.0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int r = r0 + RS * e;
-      v[e] = (kin && i0 + r < n1) ? X1[(size_t)(i0 + r) * d + k] : 0.0;
-      w[e] = (kin && j0 + r < n2) ? X2[(size_t)(j0 + r) * d + k] : 0.0;
-    }
-  };
-  int t = blockIdx.x;
-  if (t < T) fetch(t);
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const int i = lane & 15, kq = lane >> 4, col = lane & 15, rq = lane >> 4;
-  for (; t < T; t += gridDim.x) {
-    const int b = t / (gx * gy), rem = t - b * gx * gy, i0 = (rem / gx) * KT, j0 = (rem % gx) * KT;
-    {
-      const double il = 1.0 / lk;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int r = r0 + RS * e;
-        double a = 0.0, c = 0.0;
-        if (kin) {
-          if (i0 + r < n1) {
-            a = v[e];
-            if (sh1) a -= s1;
-            if (sc1) a *= c1;
-            a *= il;
-          }
-          if (j0 + r < n2) {
-            c = w[e];
-            if (sh2) c -= s2;
-            if (sc2) c *= c2;
-            c *= il;
-          }
-        }
-        As[k][r] = a;
-        Bs[k][r] = c;
-      }
-    }
-    __syncthreads();
-    if (tid < 2 * KT) {
-      const int rr = tid & (KT - 1);
-      double sq = 0.0;
-      if (tid < KT) {
-        int eq = 1;
-        for (int kk = 0; kk < DP; ++kk) {
-          sq = fma(As[kk][rr], As[kk][rr], sq);
-          eq &= As[kk][rr] == Bs[kk][rr];
-        }
-        na[rr] = sq;
-        eqr[rr] = eq;
-      } else {
-        for (int kk = 0; kk < DP; ++kk) sq = fma(Bs[kk][rr], Bs[kk][rr], sq);
-        nb2[rr] = sq;
-      }
-    }
-    kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-    for (int kk = 0; kk < DP; kk += 4) {
-      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
-      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
-      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
-    }
-    if (t + (int)gridDim.x < T) fetch(t + gridDim.x);   // next tile's loads ahead of this tile's stores
-    __syncthreads();   // na / nb2 / eqr; every wave's As / Bs reads are done
-    const double scale = os ? os[b] : 1.0;
-    const double dadd = dg ? dg[b] : 0.0;
-    double* Kb = K + (size_t)b * n1 * n2;
-    double vals[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-        const int gi = i0 + li, gj = j0 + lj;
-        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-        if (gi == gj && eqr[li]) d2 = 0.0;
-        double val = scale * kernel_value_t(KIND, d2, kexp);
-        if (gi == gj) val += dadd;
-        vals[4 * q + r] = val;
-      }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-        const int gi = i0 + li, gj = j0 + lj;
-        if (gi < n1 && gj < n2) Kb[(size_t)gi * n2 + gj] = vals[4 * q + r];
-      }
-    __syncthreads();   // na / nb2 / eqr are rewritten by the next tile
-  }
-}
-
-// dX2[c][k] = sum_b sum_i G[b][i][c] * dk_b(x1_i, x2_c)/dx2_ck.
-// Block = 64 candidates (lanes; G rows read coalesced, candidates fastest) x 4 row groups
-// (waves; all lanes of a wave share the training row -> broadcast loads); the rows are
-// split over gridDim.y blocks, the per-split partials part[split][c][k] summed in a fixed
-// order by kcross_grad_reduce (bitwise reproducible).  Rows outer, outputs inner: the G
 // loads of up to KG_B outputs of one row are issued together (the b-outer loop serialised
 // one global round trip per output: 22 us at m = 5, n = b = 512 on MI355X), 1/ls and the
 // output scales of the chunk sit in LDS.
@@ -1153,7 +941,6 @@ int mll_terms_partials(hipStream_t s, int B, int n, const double* L, const doubl
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast,
                          const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
                          double* x_dst = nullptr);
 }  // namespace evr
@@ -1164,21 +951,18 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
                       const double* scale1, const double* X2, const double* shift2, const double* scale2,
                       const double* lengthscales, const double* outputscale, const double* diag_add, double* K) {
   return kernel_matrix_launch(stream, kind, B, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, lengthscales,
-                              outputscale, diag_add, K, nullptr, nullptr);
+                              outputscale, diag_add, K);
 }
 
 }  // extern "C"
 
 namespace evr {
-// evr_kernel_matrix with the request wait of the queued host-driven chains (poll / plast, see
-// kmat_wait_request): the VALU kernel (d < 16, one output family) only
+// evr_kernel_matrix with the host-driven chain's copies (the evaluation's sequence number and
+// the candidates to device memory): the VALU kernel (d < 16, one output family) only
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast,
                          const unsigned long long* seq_src, unsigned long long* seq_dst, double* x_dst) {
-  EVR_CHECK(!poll || (plast && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
-            "kernel_matrix_launch: the request wait needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(!seq_dst || (seq_src && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
             "kernel_matrix_launch: the sequence copy needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(!x_dst || (d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0 && n2 <= KT),
@@ -1204,11 +988,8 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
   dim3 grid(cdiv(n2, KT), cdiv(n1, KT), B);
   if (d >= 16) {   // matrix-core distance expansion (see kmat_mfma_kernel)
     hipStream_t s = (hipStream_t)stream;
-    // the symmetric train matrix: lower tiles only (kmat_mfma_sym); EVR_KMAT_SYM=0 disables it
-    // (A/B and the bitwise test; read per call)
-    const char* esym = getenv("EVR_KMAT_SYM");
-    if (X1 == X2 && n1 == n2 && shift1 == shift2 && scale1 == scale2 && d <= 64 && d != 48 &&
-        !(esym && esym[0] == '0')) {
+    // the symmetric train matrix (the same operand pointer): lower tiles only (kmat_mfma_sym)
+    if (X1 == X2 && n1 == n2 && shift1 == shift2 && scale1 == scale2 && d <= 64 && d != 48) {
       const int nt = cdiv(n1, KT);
       const long long tiles = (long long)nt * (nt + 1) / 2 * B;
 #define KS(DP_, K_) kmat_mfma_sym<DP_, K_><<<(unsigned)tiles, 256, 0, s>>>(n1, d, B, X1, shift1, scale1, lengthscales, \
@@ -1226,49 +1007,11 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
       EVR_LAUNCH_CHECK();
       return 0;
     }
-    // EVR_KMAT_PERS=<n>: the persistent pipelined form with n workgroups per CU (opt-in:
-    // measured slower at config 5, 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — fewer
-    // resident waves hide less latency than the load / store overlap gains)
-    static const int pers = [] {
-      const char* e = getenv("EVR_KMAT_PERS");
-      return e ? atoi(e) : 0;
-    }();
-    const long long tiles = (long long)grid.x * grid.y * grid.z;
-    if (pers > 0 && d != 48 && d <= 64 && tiles >= 4LL * 256) {
-      const int nwg = (int)std::min<long long>(tiles, 256LL * pers);
-#define KP(DP_, K_) kmat_mfma_pers<DP_, K_><<<nwg, 256, 0, s>>>(n1, n2, d, B, X1, shift1, scale1, X2, shift2, scale2, \
-                                                               lengthscales, outputscale, diag_add, K)
-#define KPD(DP_)                                    \
-  if (kind == RBF) KP(DP_, RBF);                    \
-  else if (kind == MATERN05) KP(DP_, MATERN05);     \
-  else if (kind == MATERN15) KP(DP_, MATERN15);     \
-  else KP(DP_, MATERN25)
-      if (d <= 16) { KPD(16); }
-      else if (d <= 32) { KPD(32); }
-      else { KPD(64); }
-#undef KPD
-#undef KP
-      EVR_LAUNCH_CHECK();
-      return 0;
-    }
-    static const int epi = [] {   // EVR_KMAT_EPI: 0 direct D-layout stores, 1 LDS rows, 2 + non-temporal,
-      const char* e = getenv("EVR_KMAT_EPI");   // 3 LDS rows with 16-byte stores
-      const int v = e ? atoi(e) : 0;
-      return (v >= 0 && v <= 3) ? v : 0;
-    }();
-#define KMK(DP_, K_)                                                                                          \
-  if (epi == 0)                                                                                               \
-    kmat_mfma_kernel<DP_, K_, 0><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                      lengthscales, outputscale, diag_add, K);                 \
-  else if (epi == 1)                                                                                          \
-    kmat_mfma_kernel<DP_, K_, 1><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                      lengthscales, outputscale, diag_add, K);                 \
-  else if (epi == 2)                                                                                          \
-    kmat_mfma_kernel<DP_, K_, 2><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                      lengthscales, outputscale, diag_add, K);                 \
-  else                                                                                                        \
-    kmat_mfma_kernel<DP_, K_, 3><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                      lengthscales, outputscale, diag_add, K)
+    // (a persistent pipelined form, n workgroups per CU walking the tiles, measured slower at
+    // config 5 — 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — and removed in round 6)
+#define KMK(DP_, K_)                                                                                      \
+  kmat_mfma_kernel<DP_, K_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                 lengthscales, outputscale, diag_add, K)
 #define KM(DP_)                         \
   if (kind == RBF) KMK(DP_, RBF);           \
   else if (kind == MATERN05) KMK(DP_, MATERN05); \
@@ -1283,25 +1026,19 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
     EVR_LAUNCH_CHECK();
     return 0;
   }
-  static const int ra = [] {
-    const char* e = getenv("EVR_KMAT_RA");
-    const int v = e ? atoi(e) : 2;
-    return (v == 1 || v == 4) ? v : 2;
-  }();
+  constexpr int ra = 2;   // 32 rows per workgroup (16 and 64 measured slower)
   const size_t lds = (size_t)(KT + 16 * ra) * (d + 1) * sizeof(double);
   dim3 g(cdiv(n2, KT), cdiv(n1, 16 * ra), B);
 #define KTK(RA_, K_)                                                                              \
   kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
-                                                             scale2, lengthscales, outputscale, diag_add, K, poll,   \
-                                                             plast, seq_src, seq_dst, x_dst)
+                                                             scale2, lengthscales, outputscale, diag_add, K,         \
+                                                             seq_src, seq_dst, x_dst)
 #define KT_(RA_)                         \
   if (kind == RBF) KTK(RA_, RBF);           \
   else if (kind == MATERN05) KTK(RA_, MATERN05); \
   else if (kind == MATERN15) KTK(RA_, MATERN15); \
   else KTK(RA_, MATERN25)
-  if (ra == 1) { KT_(1); }
-  else if (ra == 2) { KT_(2); }
-  else { KT_(4); }
+  KT_(2);
 #undef KTK
 #undef KT_
   EVR_LAUNCH_CHECK();

@@ -1152,121 +1152,6 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(int n, double* __restri
 }
 
 // ---------------------------------------------------------------------------------------
-// Look-ahead steps (default): the panel of every step is normalised once, not per consumer.
-//   chol_la_kernel(k): one workgroup per trailing lower tile (I, J) of step k (k = -1: the
-//     first block column only, nothing to update).  Every tile applies C_IJ -= L_Ik L_Jk^T
-//     with the FINAL panel L_.k (one MFMA GEMM).  Workgroup 0 owns the next diagonal tile:
-//     after its update it factors L_k+1,k+1 and inv(L_k+1,k+1), publishes them and raises
-//     flags[b][k+1]; the tiles of the next block column (J = 0) wait for that flag after
-//     their own update and normalise themselves, L_I,k+1 = C Dinv^T, so that the next
-//     launch reads a finished panel.  Deadlock-free: workgroup 0 of a batch member is
-//     dispatched before every workgroup that waits on it, and a failing factor (info set)
-//     raises the flag too.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void chol_la_kernel(int n, int k, double* __restrict__ Lm, long long sL, int ldl,
-                                                      double* __restrict__ Dinv, long long sD, int* __restrict__ info,
-                                                      int* __restrict__ flags, int nblk) {
-  const int b = blockIdx.y;
-  if (__hip_atomic_load(&info[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  double* L = Lm + b * sL;
-  __shared__ double TI[BNB][BNB + 1];
-  __shared__ double TJ[BNB][BNB + 1];
-  __shared__ double TD[BNB][BNB + 1];
-  __shared__ double colj[CP], erow[CP], piv[CP];
-  __shared__ int fail;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, col = lane & 15, rq = lane >> 4;
-  int I = 0, J = 0;
-  if (k < 0) {
-    I = blockIdx.x;   // first block column
-  } else {
-    const int t = blockIdx.x;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    J = t - I * (I + 1) / 2;
-  }
-  const int r0 = (k + 1 + I) * BNB, c0 = (k + 1 + J) * BNB;
-  double4_t acc[2][2];
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
-        acc[bi][bj][r] = (row < n && cc < n) ? L[(size_t)row * ldl + cc] : 0.0;
-      }
-  if (k >= 0) {
-    const int p0 = k * BNB;
-    load_tile64(TI, L, ldl, n, r0, p0);
-    if (I != J) load_tile64(TJ, L, ldl, n, c0, p0);
-    __syncthreads();
-    double4_t u[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
-    mm64_nt(TI, I != J ? TJ : TI, wr, wc, u);
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[bi][bj][r] = acc[bi][bj][r] + (-1.0) * u[bi][bj][r];
-  }
-  int* flag = flags + (size_t)b * nblk + (k + 1);
-  if (I == 0 && J == 0) {   // the next diagonal block: factor and publish
-    const int nb = min(BNB, n - r0);
-    __syncthreads();   // TI / TJ free
-    put_quadrant(TI, wr, wc, acc);
-    __syncthreads();
-    for (int e = tid; e < BNB * BNB; e += 256) {
-      const int i = e >> 6, c = e & 63;
-      TI[i][c] = (i < nb && c < nb) ? (c <= i ? TI[i][c] : 0.0) : (i == c ? 1.0 : 0.0);
-      TJ[i][c] = 0.0;
-    }
-    const int f = factor_diag64(TI, TJ, colj, erow, piv, &fail);
-    if (f >= 0 && f < nb) {
-      if (tid == 0) __hip_atomic_store(&info[b], r0 + f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      store_diag64(TI, TJ, nb, L, ldl, r0, Dinv + b * sD + (size_t)(k + 1) * BNB * BNB);
-    }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (J != 0) {   // plain trailing tile
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
-          if (row < n && cc < n && (I != J || cc <= row)) L[(size_t)row * ldl + cc] = acc[bi][bj][r];
-        }
-    return;
-  }
-  // next block column: wait for the diagonal block, then L_I,k+1 = C inv(L_k+1,k+1)^T
-  __syncthreads();   // TI free
-  put_quadrant(TI, wr, wc, acc);
-  if (tid == 0)
-    while (!__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) __builtin_amdgcn_s_sleep(2);
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (__hip_atomic_load(&info[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  load_dinv64(TD, Dinv + b * sD + (size_t)(k + 1) * BNB * BNB);
-  __syncthreads();
-  double4_t p[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
-  mm64_nt(TI, TD, wr, wc, p);
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + wr + bi * 16 + rq + 4 * r, cc = c0 + wc + bj * 16 + col;
-        if (row < n && cc < n) L[(size_t)row * ldl + cc] = p[bi][bj][r];
-      }
-}
-
-// ---------------------------------------------------------------------------------------
 // Triangular inverse by block rows, one launch per row i (instead of two GEMMs):
 //   X_ij = -Dinv_i sum_{k=j}^{i-1} L_ik X_kj   for every j < i (one workgroup each),
 // X_ii = Dinv_i and zeros above the diagonal placed beforehand (place_diag_blocks_kernel).
@@ -1599,15 +1484,12 @@ int launch_gemm(hipStream_t s, bool tA, bool tB, int M, int N, int K, double alp
 
 // One blocked factorisation attempt of every batch member (jitter already in L's diagonal).
 // Default: the fused right-looking steps that recompute the panel per consumer (nblk + 1
-// launches); EVR_CHOL=la the look-ahead steps (nblk launches, chol_la_kernel; measured slower:
-// 1.43 vs 1.29 ms at n = 2048, profiles/r03/b); EVR_CHOL=v1 the diag / panel GEMM / trailing
-// GEMM sequence (3 launches per block).  A/B timing and the parity tests.
-static int chol_variant() {   // 0 look-ahead, 1 fused right-looking, 2 v1 (read per call: tests switch it)
+// launches); EVR_CHOL=v1 the diag / panel GEMM / trailing GEMM sequence (3 launches per block,
+// the parity tests' reference).  (A look-ahead form, nblk launches, measured slower — 1.43 vs
+// 1.29 ms at n = 2048, profiles/r03/b — and was removed in round 6.)
+static int chol_variant() {   // 1 fused right-looking, 2 v1 (read per call: tests switch it)
   const char* e = std::getenv("EVR_CHOL");
-  if (!e) return 1;
-  if (!std::strcmp(e, "v1")) return 2;
-  if (!std::strcmp(e, "la")) return 0;
-  return 1;
+  return (e && !std::strcmp(e, "v1")) ? 2 : 1;
 }
 static bool chol_v1() { return chol_variant() == 2; }
 
@@ -1617,28 +1499,19 @@ static size_t chol_dinv_doubles(int batch, int n) {
   return (size_t)batch * nblk * BNB * BNB + ((size_t)batch * nblk + 1) / 2;
 }
 
-// the fused right-looking variant forms X = L^-1 in the same launches (n <= 1024;
-// EVR_TRIINV=sep: the separate triangular inverse after the factorisation, A/B)
-static bool chol_inv_fused(int n) {
-  const char* tv = std::getenv("EVR_TRIINV");   // read per call: tests switch it
-  return chol_variant() == 1 && n <= 1024 && !(tv && tv[0]);
+// EVR_TRIINV (read per call; the parity tests' references): unset — the fused right-looking
+// variant forms X = L^-1 in the same launches (n <= 1024); "col" — the separate one-launch
+// column-panel inverse after the factorisation; "row" — the per-block-row launches
+static int triinv_mode() {
+  const char* tv = std::getenv("EVR_TRIINV");
+  return !(tv && tv[0]) ? 0 : (!std::strcmp(tv, "row") ? 2 : 1);
 }
+static bool chol_inv_fused(int n) { return chol_variant() == 1 && n <= 1024 && triinv_mode() == 0; }
 
 int chol_blocked(hipStream_t s, int batch, int n, double* L, int ldl, long long sL, double* Dinv, int* info,
                  double* X = nullptr, int ldx = 0, long long sX = 0) {
   const int nblk = (n + BNB - 1) / BNB;
   const long long sD = (long long)nblk * BNB * BNB;
-  if (chol_variant() == 0) {
-    int* flags = reinterpret_cast<int*>(Dinv + (size_t)batch * nblk * BNB * BNB);
-    EVR_HIP(hipMemsetAsync(flags, 0, sizeof(int) * batch * nblk, s));
-    for (int k = -1; k < nblk - 1; ++k) {
-      const int T = nblk - 1 - k;
-      const int tiles = k < 0 ? nblk : T * (T + 1) / 2;
-      chol_la_kernel<<<dim3(tiles, batch), 256, 0, s>>>(n, k, L, sL, ldl, Dinv, sD, info, flags, nblk);
-      EVR_LAUNCH_CHECK();
-    }
-    return 0;
-  }
   if (!chol_v1()) {
     for (int k = -1; k < nblk - 1; ++k) {
       const int T = nblk - 1 - k;   // trailing tile rows (block 0 alone for k = -1)
@@ -1678,8 +1551,7 @@ int tri_inv_blocked(hipStream_t s, int batch, int n, const double* L, int ldl, l
                     double* X, int ldx, long long sX, double* T, const int* skip) {
   const int nblk = (n + BNB - 1) / BNB;
   const long long sD = (long long)nblk * BNB * BNB;
-  const char* tv = std::getenv("EVR_TRIINV");   // "row": the per-block-row launches (A/B)
-  if (!chol_v1() && n <= 1024 && !(tv && !std::strcmp(tv, "row"))) {
+  if (!chol_v1() && n <= 1024 && triinv_mode() != 2) {
     dim3 g(cdiv(n, 16), batch);
     if (n <= 512) tri_inv_col_kernel<512><<<g, 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, X, sX, ldx, skip);
     else tri_inv_col_kernel<1024><<<g, 256, 0, s>>>(n, L, sL, ldl, Dinv, sD, X, sX, ldx, skip);
@@ -1820,11 +1692,7 @@ int evr_trsm_lower(void* stream, int batch, int n, int nrhs, const double* L, in
                    int transpose, double* B, int ldb, long long strideB) {
   EVR_CHECK(n >= 1 && nrhs >= 0 && batch >= 1, "evr_trsm_lower: bad sizes");
   if (nrhs == 0) return 0;
-  static const bool ts16 = [] {   // EVR_TRSM16=0: the 64-column tile kernel everywhere (A/B)
-    const char* e = std::getenv("EVR_TRSM16");
-    return !(e && e[0] == '0');
-  }();
-  if (!transpose && ts16 && n <= TS_MAXN) {
+  if (!transpose && n <= TS_MAXN) {
     const size_t xs = sizeof(double) * (size_t)cdiv(n, TT) * TT * TS_C;
     trsm16_kernel<<<dim3(cdiv(nrhs, TS_C), batch), 256, xs, (hipStream_t)stream>>>(n, nrhs, L, strideL, ldl, B,
                                                                                    strideB, ldb);

@@ -476,12 +476,9 @@ int evr_pareto_mask(void* stream, int S, int n, int m, const double* O, const do
   hipStream_t s = (hipStream_t)stream;
   constexpr size_t kLds = 96 * 1024;
   const size_t per = (size_t)n * m * sizeof(double);
-  // f32 pre-filter variant (EVR_PARETO=f64 keeps the f64-only scan): f64 + f32 copies of
-  // SB samples per block, SB chosen so that two blocks fit a CU's LDS
-  static const int f32_filter = [] {
-    const char* e = std::getenv("EVR_PARETO");
-    return (e && std::string(e) == "f64") ? 0 : 1;
-  }();
+  // f32 pre-filter variant: f64 + f32 copies of SB samples per block, SB chosen so that two
+  // blocks fit a CU's LDS (the f64-only scan when they do not)
+  constexpr int f32_filter = 1;
   const int npad = (n + 7) & ~7;
   const size_t per2 = (size_t)n * m * sizeof(double) + (size_t)npad * m * sizeof(float);
   constexpr size_t kLds2 = 78 * 1024;

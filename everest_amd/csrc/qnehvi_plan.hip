@@ -44,22 +44,17 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
 int qs_done_words(int b, int d);
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
-                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags,
-                unsigned long long* plast, bool tail_done);
-bool qs_tail_make(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X, const double* R,
-                  double* dXp, QsTail* t);
+                double* hout, const double* seqp, const double* sval, const int* flags);
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* poll, const unsigned long long* plast,
                          const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
                          double* x_dst = nullptr);
 constexpr int QS_TILE_ROWS = 16;
 constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
 int hvi_kdb_fused(hipStream_t s, const evr_qnehvi_state* st, int b, const double* R, const double* P, int nrt,
-                  int nrt_used, double* L22, int* flags, double* sval, double* dG, const QsTail* tail,
-                  bool* tail_ran);
+                  int nrt_used, double* L22, int* flags, double* sval, double* dG);
 
 // b <= 32 restart batches take the M-streaming small-batch kernels (qnehvi_small.hip);
 // EVR_SMALL=0 keeps the 64 x 64-tile path for A/B timing and the parity test
@@ -74,7 +69,7 @@ int kcross_grad_launch(hipStream_t s, int kind, int B, int n1, int n2, int d, co
                        double* work);
 
 struct PlanLayout {
-  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqw, seqd, xd, bytes;
+  size_t Kx, R, P, Wf, G, L22, flags, hvi, dG, bws, dKx, kg, dxp, seqd, xd, bytes;
   bool small, fused_scan;
 };
 
@@ -109,7 +104,6 @@ static PlanLayout plan_layout(const evr_qnehvi_state* st, const evr_qnehvi_model
       L.kg = take(8 * kcross_grad_ws_doubles(st->n, b, md->d));
     }
   }
-  L.seqw = take(8);   // the last request a host-driven chain served (queued evaluations)
   L.seqd = take(8);   // the host-driven chain's sequence number, copied to device memory by kmat
   L.xd = take(8 * (size_t)b * md->d);   // the host-driven chain's candidates, copied likewise
   L.bytes = o;
@@ -142,12 +136,6 @@ struct evr_qnehvi_plan {
   unsigned int* counter;         // (kept for the recycled-resource layout; unused since round 4)
   int nwords;                    // completion words the host graph's last kernel writes
   int use_graph, nrun;           // device-mode graph wanted / runs so far (captured on the 2nd)
-  // queued evaluations (restart batches): the host graph's first kernel waits for the request
-  // word, so the next evaluation's graph is launched while the current one runs (its launch
-  // and dispatch latency overlap the GPU work) and starts as soon as the host posts x
-  int queue_ok;                  // the host graph carries the request wait
-  int pend;                      // a queued graph waits for the next request
-  hipStream_t qstream;           // the stream it waits on
 };
 
 namespace evr {
@@ -176,8 +164,7 @@ __global__ __launch_bounds__(256) void plan_copy_out(int b, int n, const double*
 // one completion word per reduction workgroup to hout (*done = their number); otherwise
 // (*done = 0) the caller appends a copy-out kernel (one word).
 static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, double* hout = nullptr,
-                      const double* seqp = nullptr, unsigned int* counter = nullptr, int* done = nullptr,
-                      bool queued = false) {
+                      const double* seqp = nullptr, int* done = nullptr) {
   const evr_qnehvi_state* st = &p->st;
   const evr_qnehvi_model* md = &p->md;
   const int b = p->b, m = st->m, n = st->n, d = md->d;
@@ -192,7 +179,6 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   const bool small = p->L.small;
   // (K_x generated inside the projection instead was measured slower at b = 20 twice — 29 vs
   // 17.6 us in round 3, chain 83.9 vs 73.7 us in round 4 — and removed)
-  unsigned long long* plast = queued ? (unsigned long long*)(w + p->L.seqw) : nullptr;
   // host mode through the b <= 32 kernels: qs_dx_reduce reads the sequence number from the
   // device copy kmat makes (an L2 read instead of a PCIe read at the end of the chain)
   // (the copies ride in kmat_kernel, the VALU assembly: d < 16 and one kernel family)
@@ -203,7 +189,6 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   double* xd = seqd ? (double*)(w + p->L.xd) : nullptr;
   if (int rc = kernel_matrix_launch(s, md->kind, m, n, b, d, md->Xn, nullptr, nullptr, X, md->shift, md->scale,
                                     md->lengthscales, nullptr, nullptr, Kx,
-                                    queued ? (const unsigned long long*)seqp : nullptr, plast,
                                     seqd ? (const unsigned long long*)seqp : nullptr, seqd, xd)) {
     return rc;
   } else if (small) {
@@ -215,34 +200,29 @@ static int plan_chain(hipStream_t s, const evr_qnehvi_plan* p, const double* X, 
   double* dG = (double*)(w + p->L.dG);
   if (xd) X = xd;
   if (small && p->backward && p->L.fused_scan && hvi_kdb_fused_applies(st, b)) {
-    // the sampling step inside the restart scan's staging (one launch less); G is not formed.
-    // The backward's training-row class rides in the scan's tail (qs_tail.hpp)
-    double* dxp = (double*)(w + p->L.dxp);
-    QsTail tl;
-    const bool tail = qs_tail_make(st, md, b, X, R, dxp, &tl);
-    bool tail_ran = false;
+    // the sampling step inside the restart scan's staging (one launch less); G is not formed
     if (int rc = hvi_kdb_fused(s, st, b, R, P, cdiv(qn_rows(st), QS_TILE_ROWS), cdiv(st->n + st->nb, QS_TILE_ROWS),
-                               L22, flags, hw, dG, tail ? &tl : nullptr, &tail_ran))
+                               L22, flags, hw, dG))
       return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, dxp, p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       hw, flags, plast, tail_ran);
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout,
+                       seqd ? (const double*)seqd : seqp, hw, flags);
   }
   if (int rc = samples_norms(s, st, b, R, P, G, L22, flags, small ? QS_TILE_ROWS : QN_NORM_TILE)) return rc;
   if (!p->backward) return evr_hvi_forward(s, st, b, G, flags, hw, p->acq);
   if (small && p->L.fused_scan) {
-    // one launch for thresholds + scan + split reduction (hvi_kd3); the per-sample values in
-    // the scan workspace become acq inside the dX reduction
+    // the restart scan in one launch (hvi_kdw); the per-sample values in the scan workspace
+    // become acq inside the dX reduction
     if (int rc = evr_hvi_restart_fb(s, st, b, G, hw, dG)) return rc;
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       hw, flags, plast, false);
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout,
+                       seqd ? (const double*)seqd : seqp, hw, flags);
   }
   if (int rc = evr_hvi_forward_backward(s, st, b, G, flags, nullptr, hw, p->acq, dG)) return rc;
   if (small) {
     if (done) *done = hout ? qs_done_words(b, d) : 0;
-    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout, seqd ? (const double*)seqd : seqp, counter,
-                       nullptr, nullptr, plast, false);
+    return qs_backward(s, st, md, b, X, R, L22, dG, (double*)(w + p->L.dxp), p->dX, p->acq, hout,
+                       seqd ? (const double*)seqd : seqp, nullptr, nullptr);
   }
   double* dKx = (double*)(w + p->L.dKx);
   if (int rc = proj_backward(s, st, b, md->M, R, L22, dG, dKx, (double*)(w + p->L.bws))) return rc;
@@ -313,9 +293,6 @@ int evr_qnehvi_plan_create(void* stream, const evr_qnehvi_state* st, const evr_q
   // pays for a capture and an instantiation)
   p->use_graph = use_graph ? 1 : 0;
   p->nrun = 0;
-  p->queue_ok = 0;
-  p->pend = 0;
-  p->qstream = nullptr;
   (void)stream;
   *out = p;
   return 0;
@@ -369,11 +346,9 @@ int evr_qnehvi_plan_run(void* stream, evr_qnehvi_plan* p) {
   return plan_chain(s, p, p->X);
 }
 
-static int plan_release(hipStream_t s, evr_qnehvi_plan* p);
 
 void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (!p) return;
-  if (p->pend) (void)plan_release(p->qstream, p);   // normally released by evr_qnehvi_plan_minimize
   int dev = -1;
   if (graph_reuse() && p->hexec && p->hx && p->hout && hipGetDevice(&dev) == hipSuccess) {
     // the plan's evaluations have completed (plan_eval_raw waits for each), so the buffers and
@@ -396,16 +371,6 @@ void evr_qnehvi_plan_destroy(evr_qnehvi_plan* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   delete p;
-}
-
-// queued evaluations: opt-in (EVR_QUEUE=1, read when a plan builds its host graph).  Measured
-// on the config-4 ask (tools/queue_probe.py, profiles/r05/j): 85 vs 81 us per evaluation
-// round trip queued vs not — the host's graph launch costs little (the round trip is the
-// ~73 us device chain + ~8 us), and the queued chain's PCIe poll of the request word adds
-// its own latency back
-static bool queue_enabled() {
-  const char* e = std::getenv("EVR_QUEUE");
-  return e && e[0] == '1';
 }
 
 // The host-evaluation buffers and graph, built on first use.
@@ -446,19 +411,14 @@ static int plan_host_setup(hipStream_t s, evr_qnehvi_plan* p) {
   std::unique_lock<std::mutex> cap_lk;
   hipStream_t cs = capture_stream(&cap_lk);
   EVR_CHECK(cs, "qnehvi plan: no capture stream");
-  // queued evaluations: the restart batch's chain (b <= 32 kernels with backward) ends in the
-  // dX reduction, which records the request it served in the plan's device word
-  const bool queued = queue_enabled() && p->L.small && p->backward;
-  if (queued) EVR_HIP(hipMemsetAsync(p->work + p->L.seqw, 0, 8, s));
   int rc = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess ? 0 : 1;
   if (!rc) {
     // the kernels read x straight from the pinned buffer; the restart batch's dX reduction
     // writes the results and the completion word itself, other chains end in plan_copy_out
     int done = 0;
-    rc = plan_chain(cs, p, dhx, dhout, dhx + n, p->counter, &done, queued);
+    rc = plan_chain(cs, p, dhx, dhout, dhx + n, &done);
     if (!rc && !done) plan_copy_out<<<1, 256, 0, cs>>>(b, n, p->acq, p->backward ? p->dX : nullptr, dhx, dhout);
     p->nwords = done > 0 ? done : 1;
-    p->queue_ok = queued && done > 0;
   }
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cs, &g);
@@ -487,31 +447,21 @@ static int plan_host_setup(hipStream_t s, evr_qnehvi_plan* p) {
   EVR_CHECK(false, "qnehvi plan: host-evaluation graph capture failed (%s)", why.c_str());
 }
 
-// One evaluation at host x (b x d); [acq | dX] left in p->hout.  queue_next: also launch the
-// next evaluation's graph now (its first kernel waits for the next request), so that its
-// launch and dispatch run while this evaluation computes; a graph queued by the previous call
-// serves this one without a launch.  The caller ends a queued sequence with queue_next false
-// (or plan_release).
-static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x, bool queue_next = false) {
+// One evaluation at host x (b x d); [acq | dX] left in p->hout.  (Queuing the next evaluation's
+// graph behind a request-word wait was measured in rounds 3-5 and removed in round 6: the
+// extra kernel boundary and the PCIe poll cost more than the hidden launch, profiles/r05/j.)
+static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x) {
   const int b = p->b, n = b * p->md.d;
   if (int rc = plan_host_setup(s, p)) return rc;
-  queue_next = queue_next && p->queue_ok;
   std::memcpy(p->hx, x, sizeof(double) * n);
   const unsigned long long seq = ++p->seq;
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  // the request word last: a queued chain reads x only after it sees the new number
   __atomic_store_n((unsigned long long*)(p->hx + n), seq, __ATOMIC_RELEASE);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (!p->pend) EVR_HIP(hipGraphLaunch(p->hexec, s));
-  p->pend = 0;
-  if (queue_next) {
-    EVR_HIP(hipGraphLaunch(p->hexec, s));
-    p->pend = 1;
-    p->qstream = s;
-  }
+  EVR_HIP(hipGraphLaunch(p->hexec, s));
   // spin on the completion words; every 256 polls ask the stream whether it has drained (a
-  // faulted or failed launch ends the wait with its error instead of spinning forever; with a
-  // queued graph the stream never drains, so a 30 s limit backs the wait up)
+  // faulted or failed launch ends the wait with its error instead of spinning forever; a 30 s
+  // limit backs the wait up)
   volatile const unsigned long long* done = (volatile const unsigned long long*)(p->hout + b + n);
   const int nw = p->nwords;
   auto finished = [&]() {
@@ -536,22 +486,13 @@ static int plan_eval_raw(hipStream_t s, evr_qnehvi_plan* p, const double* x, boo
   return 0;
 }
 
-// Release a queued graph: it serves one more request at the current x (results discarded).
-static int plan_release(hipStream_t s, evr_qnehvi_plan* p) {
-  if (!p->pend) return 0;
-  std::vector<double> x(p->hx, p->hx + (size_t)p->b * p->md.d);
-  return plan_eval_raw(s, p, x.data(), false);
-}
-
 // One evaluation of the restart batch at host x: f = -sum_r acq_r, g = -dX.
-static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g,
-                          bool queue_next = false) {
+static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, double* f, double* g) {
   const int b = p->b, n = b * p->md.d;
-  if (int rc = plan_eval_raw(s, p, x, queue_next)) return rc;
+  if (int rc = plan_eval_raw(s, p, x)) return rc;
   double acc = 0.0;
   for (int r = 0; r < b; ++r) {
     if (std::isnan(p->hout[r])) {
-      if (int rc = plan_release(s, p)) return rc;
       ::evr::set_error("acquisition: posterior covariance block not p.d. after the jitter ladder (NotPSDError)");
       return EVR_ERR_NOTPSD;
     }
@@ -564,7 +505,7 @@ static int plan_eval_host(hipStream_t s, evr_qnehvi_plan* p, const double* x, do
 
 int evr_qnehvi_plan_eval_host(void* stream, evr_qnehvi_plan* p, const double* x, double* out) {
   EVR_CHECK(p && x && out, "evr_qnehvi_plan_eval_host: bad arguments");
-  if (int rc = plan_eval_raw((hipStream_t)stream, p, x, false)) return rc;
+  if (int rc = plan_eval_raw((hipStream_t)stream, p, x)) return rc;
   std::memcpy(out, p->hout, sizeof(double) * (size_t)p->b * (p->backward ? 1 + p->md.d : 1));
   return 0;
 }
@@ -578,13 +519,6 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   const int b = p->b, n = b * p->md.d;
   for (int i = 0; i < n; ++i) EVR_CHECK(!(lb[i] > ub[i]), "evr_qnehvi_plan_minimize: lower bound above upper bound");
   hipStream_t s = (hipStream_t)stream;
-  // EVR_MIN_STATS=1: host time in the optimiser's steps vs the evaluations, to stderr
-  static const bool stats = [] {
-    const char* e = std::getenv("EVR_MIN_STATS");
-    return e && e[0] == '1';
-  }();
-  double t_step = 0.0, t_eval = 0.0;
-  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   Lbfgsb opt(n, mcor, lb, ub, factr, pgtol, maxls);
   std::vector<double> g(n);
   double f = 0.0;
@@ -592,39 +526,24 @@ int evr_qnehvi_plan_minimize(void* stream, evr_qnehvi_plan* p, const double* x0,
   // scipy's _minimize_lbfgsb driver loop
   for (;;) {
     if (task == LBFGSB_FG) {
-      double t0 = stats ? now() : 0.0;
-      // the next evaluation's graph is queued behind this one (released by the final
-      // re-evaluation below, or on the error paths)
-      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data(), true)) return rc;
-      double t1 = stats ? now() : 0.0;
+      if (int rc = plan_eval_host(s, p, opt.x(), &f, g.data())) return rc;
       ++nfev;
       task = opt.step(f, g.data());
-      if (stats) {
-        const double t2 = now();
-        t_eval += t1 - t0;
-        t_step += t2 - t1;
-      }
     } else if (task == LBFGSB_NEW_X) {
       ++nit;
       if (nit >= maxiter || nfev > maxfun) {
         status = 1;
         break;
       }
-      double t1 = stats ? now() : 0.0;
       task = opt.step(f, g.data());
-      if (stats) t_step += now() - t1;
     } else {
       status = task == LBFGSB_ABNORMAL ? 2 : task == LBFGSB_ERROR ? 3 : 0;
       break;
     }
   }
-  if (stats)
-    std::fprintf(stderr, "EVR_MIN_STATS n=%d nit=%d nfev=%d eval_us=%.2f step_us=%.2f (per evaluation)\n", n, nit,
-                 nfev, t_eval / std::max(1, nfev) * 1e6, t_step / std::max(1, nfev) * 1e6);
   for (int i = 0; i < n; ++i) x[i] = std::min(ub[i], std::max(lb[i], opt.x()[i]));
-  // re-evaluate at the clipped candidates ([upstream] gen_candidates_scipy's final no-grad
-  // call); served by the queued graph, none queued after it
-  if (int rc = plan_eval_host(s, p, x, &f, g.data(), false)) return rc;
+  // re-evaluate at the clipped candidates ([upstream] gen_candidates_scipy's final no-grad call)
+  if (int rc = plan_eval_host(s, p, x, &f, g.data())) return rc;
   std::memcpy(acq, p->hout, sizeof(double) * b);
   info[0] = nit;
   info[1] = nfev;

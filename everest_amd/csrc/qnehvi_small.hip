@@ -199,13 +199,11 @@ constexpr int QS_RC = 128;   // rows of M per backward chunk
 // took 244 VGPRs + 16 AGPRs (one workgroup per CU: the 480 workgroups of the bench shape ran
 // in two rounds); bounded it fits 248 registers without scratch
 constexpr int QS_SMAX = 1024;   // samples whose z values the backward stages in LDS
-// SPLIT: baseline rows in M (nb > 0, the literal "split" root, A/B only): a third row class;
-// one workgroup per CU there (its registers would spill at two)
-// TAIL: the training-row class is done elsewhere (qs_tail.hpp, in the scan's tail): the splits
-// cover the sample rows only, and the class coefficient cf0 goes to cfo[j][c] for the dX
-// reduction (written by the (tile 0, split 0) workgroup of each output)
-template <bool SPLIT, bool TAIL>
-__global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
+// The training-row classes (rows < n + nb) are the launch's z >= zsb workgroups (qs_tail.hpp):
+// the sample-row workgroups (z < zsb) cover the S sample rows only, and the classes'
+// coefficient goes to cfo[j][c] for the dX reduction (written by the (tile 0, split 0)
+// workgroup of each output)
+__global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, int m, int b, int d, int kind,
                                               const double* __restrict__ M, const double* __restrict__ R,
                                               const double* __restrict__ dG, const double* __restrict__ L22,
                                               const double* __restrict__ ys, const double* __restrict__ zq,
@@ -214,7 +212,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
                                               const double* __restrict__ scale, const double* __restrict__ ls,
                                               double* __restrict__ dXp, int ntile, int rows_per, int np_all,
                                               double* __restrict__ cfo, int zsb, QsTail qtl) {
-  __shared__ double cf[3][QS_B];
+  __shared__ double cf[3][QS_B];   // [2]: the mean row's coefficient (0, 1 unused)
   __shared__ double red[8][QS_B][2];
   __shared__ double zl[QS_SMAX];   // z_j of the samples (the coefficient rounds read them here)
   // the chunk tiles and the epilogue's reduction buffers share one LDS region (~53 KB per
@@ -227,7 +225,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
   auto Bs = reinterpret_cast<double(*)[QS_B + 1]>(lds + MS_SZ);
   auto dk = reinterpret_cast<double(*)[QS_BI][QS_B + 1]>(lds);
   auto gx = reinterpret_cast<double(*)[QS_B][QS_MAXD]>(lds + DK_SZ);
-  if (TAIL && (int)blockIdx.z >= zsb) {   // the training-row class (EVR_QS_TAIL=bwd): its own workgroups
+  if ((int)blockIdx.z >= zsb) {   // the training-row classes: their own workgroups
     qs_tail_tile(qtl, ((int)blockIdx.y * qtl.za + ((int)blockIdx.z - zsb)) * qtl.nt + blockIdx.x, lds);
     return;
   }
@@ -239,7 +237,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
 #endif
   QS_STAMP(0);
   // this split's rows of M; the mean row (Rr - 1, a rank-1 term) is added in the epilogue
-  const int rbeg = (TAIL ? n + nb : 0) + z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
+  const int rbeg = n + nb + z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
   const double aj = oa[j], sj = ys[j];
   const double* Mj = M + (size_t)j * Rr * n;
   const double* Rj = R + (size_t)j * Rr * b;
@@ -264,10 +262,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
 #pragma unroll
     for (int u = 0; u < BL; ++u) {
       const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
-      const double* src = nullptr;
-      if (c < b && r < rend)
-        src = r < n + nb ? Rj + (size_t)r * b + c : dG + ((size_t)(r - n - nb) * m + j) * b + c;
-      bv[u] = src ? *src : 0.0;
+      bv[u] = (c < b && r < rend) ? dG[((size_t)(r - n - nb) * m + j) * b + c] : 0.0;
     }
   };
   // z_j of the samples, loaded first (the LDS store below then waits for these loads only:
@@ -285,7 +280,7 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
   //    epilogue: the rounds' loads ride along with the chunk loads below (round k is consumed
   //    after chunk k's MFMAs) instead of standing before the first chunk.
   const int cc_ = tid & (QS_B - 1), g_ = tid >> 5;
-  constexpr int CU = SPLIT ? 16 : 12;   // samples per thread and round: the most that stay in registers
+  constexpr int CU = 12;   // samples per thread and round: the most that stay in registers
   double dmu = 0.0, dl = 0.0;
   double dv[CU];
   int s0 = g_;
@@ -306,10 +301,10 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     }
     s0 += 8 * CU;
   };
-  // TAIL with the sample rows in M (nh = S, one split over all of them): the coefficients are
-  // summed from the staged chunks in LDS (Bs holds a_j dG of the chunk's samples) in the same
+  // with the sample rows in M (nh = S, one split over all of them) the coefficients are summed
+  // from the staged chunks in LDS (Bs holds a_j dG of the chunk's samples) in the same
   // per-thread sample order — no separate dG loads or their dependent rounds
-  const bool coef_lds = TAIL && nh == S && zsb == 1;
+  const bool coef_lds = nh == S && zsb == 1;
   bool pend = !coef_lds && s0 < S;
   if (pend) coef_load();
 #pragma unroll
@@ -318,11 +313,9 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     if (e < S) zl[e] = zr[u];
   }
   QS_STAMP(1);
-  // 2. dK tile by row class: A (rows < n, scaled by cf0 in the epilogue), C (n <= r < n + nb,
-  //    cf1), B (sample rows, a_j applied while staging): D_X[i][c] = sum_r M[r][i0 + i] src[r][c]
+  // 2. dK tile over the sample rows (a_j applied while staging): D[i][c] = sum_r M[r][i0 + i] a_j dG[r][c]
   const int i = lane & 15, kq = lane >> 4;
-  double4_t aA0 = {0, 0, 0, 0}, aA1 = {0, 0, 0, 0}, aB0 = {0, 0, 0, 0}, aB1 = {0, 0, 0, 0};
-  double4_t aC0 = {0, 0, 0, 0}, aC1 = {0, 0, 0, 0};
+  double4_t aB0 = {0, 0, 0, 0}, aB1 = {0, 0, 0, 0};
   for (int rc = rbeg; rc < rend; rc += QS_RC) {
     __syncthreads();   // the previous chunk's MFMAs are done with Ms, Bs
 #pragma unroll
@@ -332,43 +325,17 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
     }
 #pragma unroll
     for (int u = 0; u < BL; ++u) {
-      const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B, r = rc + rr;
-      Bs[rr][c] = r >= n + nb ? bv[u] * aj : bv[u];
+      const int e = u * 256 + tid, rr = e / QS_B, c = e % QS_B;
+      Bs[rr][c] = bv[u] * aj;
     }
     __syncthreads();
     if (rc + QS_RC < rend) load(rc + QS_RC);
-    const int lo_r = rc + wave * (QS_RC / 4), hi_r = lo_r + QS_RC / 4 - 1;
-    if (hi_r < n) {
 #pragma unroll
-      for (int t = 0; t < QS_RC / 16; ++t) {
-        const int rr = wave * (QS_RC / 4) + 4 * t + kq;
-        const double a = Ms[rr][i];
-        aA0 = mfma4(a, Bs[rr][i], aA0);
-        aA1 = mfma4(a, Bs[rr][i + 16], aA1);
-      }
-    } else if (lo_r >= n + nb) {
-#pragma unroll
-      for (int t = 0; t < QS_RC / 16; ++t) {
-        const int rr = wave * (QS_RC / 4) + 4 * t + kq;
-        const double a = Ms[rr][i];
-        aB0 = mfma4(a, Bs[rr][i], aB0);
-        aB1 = mfma4(a, Bs[rr][i + 16], aB1);
-      }
-    } else {   // a slice across a class boundary: each class's rows through its own sums
-#pragma unroll
-      for (int t = 0; t < QS_RC / 16; ++t) {
-        const int rr = wave * (QS_RC / 4) + 4 * t + kq, r = rc + rr;
-        const double a = Ms[rr][i], b0 = Bs[rr][i], b1 = Bs[rr][i + 16];
-        const double xa = r < n ? a : 0.0, xb = r >= n + nb ? a : 0.0, xc_ = (r >= n && r < n + nb) ? a : 0.0;
-        aA0 = mfma4(xa, b0, aA0);
-        aA1 = mfma4(xa, b1, aA1);
-        aB0 = mfma4(xb, b0, aB0);
-        aB1 = mfma4(xb, b1, aB1);
-        if (SPLIT) {
-          aC0 = mfma4(xc_, b0, aC0);
-          aC1 = mfma4(xc_, b1, aC1);
-        }
-      }
+    for (int t = 0; t < QS_RC / 16; ++t) {
+      const int rr = wave * (QS_RC / 4) + 4 * t + kq;
+      const double a = Ms[rr][i];
+      aB0 = mfma4(a, Bs[rr][i], aB0);
+      aB1 = mfma4(a, Bs[rr][i + 16], aB1);
     }
     if (coef_lds) {
 #pragma unroll
@@ -403,12 +370,10 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
       v += red[q][tid][1];
     }
     const double dbr = tid < b ? v / (2.0 * L22[(size_t)j * b + tid]) : 0.0;
-    cf[0][tid] = -2.0 * sj * sj * dbr;
-    cf[1][tid] = -2.0 * dbr;
     cf[2][tid] = sj * u;
-    // the tail's class coefficient: -2 dbr with the split root (its L^-1 rows carry s^2 in the
-    // tail's weights), -2 s^2 dbr with the fused one
-    if (TAIL && tile == 0 && z == 0 && tid < b) cfo[(size_t)j * b + tid] = nb > 0 ? -2.0 * dbr : -2.0 * sj * sj * dbr;
+    // the training-row classes' coefficient: -2 dbr with the split root (its L^-1 rows carry
+    // s^2 in the tail's weights), -2 s^2 dbr with the fused one
+    if (tile == 0 && z == 0 && tid < b) cfo[(size_t)j * b + tid] = nb > 0 ? -2.0 * dbr : -2.0 * sj * sj * dbr;
   }
   QS_STAMP(2);
   // the epilogue's training rows and mean-row entries, loaded before the dk exchange so their
@@ -427,16 +392,10 @@ __global__ __launch_bounds__(256, SPLIT ? 1 : 2) void qs_bwd(int n, int nb, int 
   }
   __syncthreads();   // all waves are done with Ms, Bs (dk aliases them); cf is ready
   {
-    const double f0a = cf[0][i], f0b = cf[0][16 + i], f1a = cf[1][i], f1b = cf[1][16 + i];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      double v0 = TAIL ? aB0[q] : fma(f0a, aA0[q], aB0[q]), v1 = TAIL ? aB1[q] : fma(f0b, aA1[q], aB1[q]);
-      if (SPLIT) {
-        v0 = fma(f1a, aC0[q], v0);
-        v1 = fma(f1b, aC1[q], v1);
-      }
-      dk[wave][4 * q + kq][i] = v0;
-      dk[wave][4 * q + kq][16 + i] = v1;
+      dk[wave][4 * q + kq][i] = aB0[q];
+      dk[wave][4 * q + kq][16 + i] = aB1[q];
     }
   }
   __syncthreads();
@@ -504,7 +463,6 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
                                                     const double* seqp,
                                                     const double* __restrict__ sval, int S, int m,
                                                     const int* __restrict__ flags,
-                                                    unsigned long long* __restrict__ plast, int light,
                                                     int npB, int ntA, const double* __restrict__ cfo) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool ein = e < b * d;
@@ -575,33 +533,17 @@ __global__ __launch_bounds__(256) void qs_dx_reduce(int np, int b, int d, const 
     dX[e] = r;
     if (hout) {
       const double a = (e < b) ? (sval ? av : acq[e]) : 0.0;
-      if (light) {
-        // system-coherent write-through stores (sc0 sc1) and a wait for their completion
-        // instead of the system-scope fence, whose L2 writeback + invalidate walks the whole
-        // cache (and leaves the next evaluation's operands to be refetched)
-        __hip_atomic_store((unsigned long long*)(hout + b + e), (unsigned long long)__double_as_longlong(r),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (e < b)
-          __hip_atomic_store((unsigned long long*)(hout + e), (unsigned long long)__double_as_longlong(a),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        hout[b + e] = r;
-        if (e < b) hout[e] = a;
-        __threadfence_system();
-      }
+      hout[b + e] = r;
+      if (e < b) hout[e] = a;
+      __threadfence_system();
     }
   }
   if (hout) {
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long* w = (unsigned long long*)(hout + b + (size_t)b * d + blockIdx.x);
-      if (light) __hip_atomic_store(w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      else *(volatile unsigned long long*)w = seq;
+      *(volatile unsigned long long*)w = seq;
     }
-    // the request this chain served: a chain queued behind it waits for a newer one
-    // (kmat_wait_request); read by the next kernel of the stream only
-    if (plast && blockIdx.x == 0 && threadIdx.x == 0) *plast = seq;
   }
 }
 
@@ -621,8 +563,6 @@ size_t qs_norms_doubles(const evr_qnehvi_state* st, int b) { return (size_t)st->
 // launch (the scan holds every workgroup slot, so the tail stretched it by ~4 us) and inside
 // qs_bwd's own workgroups.  A function of the state only, so a plan's layout (qs_dxp_doubles)
 // and its launches always agree.
-static int qs_tail_mode(const evr_qnehvi_state* st) { return st->n > 0 ? 1 : 0; }
-bool qs_tail_on(const evr_qnehvi_state* st) { return qs_tail_mode(st) != 0; }
 // training rows per tail workgroup's split: 256 (64 per wave, two load batches), or half the
 // class (rounded to 16) when that is longer, so the class is two splits and the launch's
 // m (2 + 1) 32 workgroups stay resident in one round at two per CU
@@ -632,36 +572,21 @@ static int qs_tail_rows(const evr_qnehvi_state* st) {
 }
 static int qs_tail_za(const evr_qnehvi_state* st) { return cdiv(st->n + st->nb, qs_tail_rows(st)); }
 
-// rows the backward's splits cover: every non-mean row, or (tail) the sample rows only
-static int qs_bwd_rows(const evr_qnehvi_state* st) {
-  return qs_tail_on(st) ? qn_rows(st) - 1 - st->n - st->nb : qn_rows(st) - 1;
-}
-
-// backward row splits over those rows: as many as keep every workgroup resident at once (two
-// per CU), in whole 128-row chunks
-static int qs_zsplit(const evr_qnehvi_state* st) {
-  if (qs_tail_on(st)) return 1;   // one split over the sample rows: the coefficients come from its chunks
-  const int tiles = cdiv(st->n, QS_BI) * st->m, nch = std::max(1, cdiv(qs_bwd_rows(st), QS_RC));
-  const int zs = std::max(1, std::min(nch, 512 / std::max(1, tiles)));
-  return cdiv(nch, cdiv(nch, zs));
-}
-
-static int qs_rows_per(const evr_qnehvi_state* st) {
-  const int nch = std::max(1, cdiv(qs_bwd_rows(st), QS_RC));
-  return cdiv(nch, qs_zsplit(st)) * QS_RC;
-}
+// one backward split over the S sample rows (the coefficients come from its chunks)
+static int qs_zsplit(const evr_qnehvi_state*) { return 1; }
+static int qs_rows_per(const evr_qnehvi_state* st) { return cdiv(std::max(1, qn_rows(st) - 1 - st->n - st->nb), QS_RC) * QS_RC; }
 
 // workgroups of qs_dx_reduce = completion words it writes in host mode (<= 64 at b <= 32, d <= 8)
 int qs_done_words(int b, int d) { return cdiv(b * d, 4); }
 
-// dX partials per element: the backward's (output, split, tile) and, with the tail, the tail's
+// dX partials per element: the sample rows' (output, tile) and the training-row classes' (output, split, tile)
 static size_t qs_np_bwd(const evr_qnehvi_state* st) { return (size_t)st->m * qs_zsplit(st) * cdiv(st->n, QS_BI); }
 static size_t qs_np_all(const evr_qnehvi_state* st) {
-  return qs_np_bwd(st) + (qs_tail_on(st) ? (size_t)st->m * qs_tail_za(st) * cdiv(st->n, QS_BI) : 0);
+  return qs_np_bwd(st) + (size_t)st->m * qs_tail_za(st) * cdiv(st->n, QS_BI);
 }
 
 size_t qs_dxp_doubles(const evr_qnehvi_state* st, int b, int d) {
-  return qs_np_all(st) * b * d + (qs_tail_on(st) ? (size_t)st->m * b : 0);   // + cf0 (m x b)
+  return qs_np_all(st) * b * d + (size_t)st->m * b;   // + the classes' coefficients (m x b)
 }
 
 int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* Kx,
@@ -670,22 +595,6 @@ int qs_forward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model
   qs_fwd<<<dim3(nt, st->m), QS_FT, 0, s>>>(st->n, st->nb, Rr, b, md->M, Kx, R, P, nt);
   EVR_LAUNCH_CHECK();
   return 0;
-}
-
-__global__ __launch_bounds__(256) void qs_bwd_tail(QsTail t) {
-  __shared__ double lds[QT_LDS_DOUBLES];
-  qs_tail_tile(t, blockIdx.x, lds);
-}
-
-static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
-                         const double* R, double* dXp, QsTail* t);
-
-// the tail's arguments when it is to run in the restart scan (EVR_QS_TAIL=kdw)
-bool qs_tail_make(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X, const double* R,
-                  double* dXp, QsTail* t) {
-  if (qs_tail_mode(st) != 2) return false;
-  qs_tail_fill(st, md, b, X, R, dXp, t);
-  return true;
 }
 
 static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
@@ -698,40 +607,21 @@ static void qs_tail_fill(const evr_qnehvi_state* st, const evr_qnehvi_model* md,
 
 int qs_backward(hipStream_t s, const evr_qnehvi_state* st, const evr_qnehvi_model* md, int b, const double* X,
                 const double* R, const double* L22, const double* dG, double* dXp, double* dX, double* acq,
-                double* hout, const double* seqp, unsigned int* counter, const double* sval, const int* flags,
-                unsigned long long* plast, bool tail_done) {
+                double* hout, const double* seqp, const double* sval, const int* flags) {
   const int nt = cdiv(st->n, QS_BI), d = md->d, zs = qs_zsplit(st);
   const int rows_per = qs_rows_per(st);
-  const int mode = qs_tail_mode(st);
-  const bool tail = mode != 0;
   const int npB = (int)qs_np_bwd(st), np = (int)qs_np_all(st);
-  double* cfo = tail ? dXp + (size_t)np * b * d : nullptr;
-  EVR_CHECK(st->S <= QS_SMAX, "qs_backward: %d samples exceed the staged %d", st->S, QS_SMAX);
+  double* cfo = dXp + (size_t)np * b * d;
+  EVR_CHECK(st->S <= QS_SMAX && st->n > 0, "qs_backward: %d samples exceed the staged %d", st->S, QS_SMAX);
   QsTail t{};
-  if (tail) qs_tail_fill(st, md, b, X, R, dXp, &t);
-  if (mode == 2 && !tail_done) {   // the op path (and scans without a tail): its own launch first
-    qs_bwd_tail<<<t.nwg, 256, 0, s>>>(t);
-    EVR_LAUNCH_CHECK();
-  }
-  // mode 1: the tail's workgroups are the launch's z >= 1 slices
-  const int gz = mode == 1 ? zs + t.za : zs;
-#define QS_BWD(SPL, TL)                                                                                         \
-  qs_bwd<SPL, TL><<<dim3(nt, st->m, gz), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, \
-                                                      R, dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,   \
-                                                      md->scale, md->lengthscales, dXp, nt, rows_per, np, cfo,       \
-                                                      mode == 1 ? zs : gz, t)
-  if (tail) QS_BWD(false, true);
-  else if (st->nb > 0) QS_BWD(true, false);
-  else QS_BWD(false, false);
-#undef QS_BWD
+  qs_tail_fill(st, md, b, X, R, dXp, &t);
+  // the training-row classes' workgroups are the launch's z >= zs slices
+  qs_bwd<<<dim3(nt, st->m, zs + t.za), 256, 0, s>>>(st->n, st->nb, qn_nh(st), st->S, st->m, b, d, md->kind, md->M, R,
+                                                     dG, L22, st->ys, st->zq, st->obj_a, md->Xn, X, md->shift,
+                                                     md->scale, md->lengthscales, dXp, nt, rows_per, np, cfo, zs, t);
   EVR_LAUNCH_CHECK();
-  (void)counter;
-  // EVR_HOSTFENCE=light: write-through stores instead of the system fence (read per call)
-  const char* hf = std::getenv("EVR_HOSTFENCE");
-  const int light = (hf && !std::strcmp(hf, "light")) ? 1 : 0;
   qs_dx_reduce<<<qs_done_words(b, d), 256, 0, s>>>(np, b, d, dXp, md->scale, dX, acq, hout, seqp, sval, st->S, st->m,
-                                                   flags, plast, light, tail ? npB : np,
-                                                   tail ? qs_tail_za(st) * nt : 1, cfo);
+                                                   flags, npB, qs_tail_za(st) * nt, cfo);
   EVR_LAUNCH_CHECK();
   return 0;
 }
@@ -772,7 +662,7 @@ int evr_qnehvi_small_backward(void* stream, const evr_qnehvi_state* st, const ev
   EVR_CHECK(st && md && X && R && L22 && dG && dXp && dX && qs_applies(st, b, md->d),
             "evr_qnehvi_small_backward: bad arguments");
   return qs_backward((hipStream_t)stream, st, md, b, X, R, L22, dG, dXp, dX, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, false);
+                     nullptr);
 }
 
 }  // extern "C"

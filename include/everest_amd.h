@@ -236,23 +236,14 @@ int evr_hvi_backward(void* stream, const evr_qnehvi_state* st, int b, const doub
 int evr_hvi_forward_backward(void* stream, const evr_qnehvi_state* st, int b, const double* G,
                              const int* flags, const double* gout, double* work, double* acq,
                              double* dG);
-/* Sparse-scan kernel for kd-grouped cells: 2 = hvi_kd2 (default: chunk pre-filter, mark-based
- * owner lookups), 1 = hvi_kd (the earlier kernel; also selected by EVR_KD=1).  Both give
- * bitwise identical results; the switch exists for A/B timing and the parity test.  Plans
- * keep the kernel they were captured with.  Process-global, not thread-safe. */
-int evr_hvi_set_kd_variant(int variant);
-/* Restart-batch scan (kd cells, b <= 32) in one launch: thresholds, the sparse scan and the
- * reduction of evr_hvi_forward_backward (gout = NULL).  sval (S x b) holds the per-sample HVI values, acq = their mean
+/* Restart-batch scan (kd cells, b <= 32) in one launch (hvi_kdw: one wave per sample and
+ * candidate): what evr_hvi_forward_backward (gout = NULL) computes, in the wave's own
+ * summation order.  sval (S x b) holds the per-sample HVI values, acq = their mean
  * (evr_mean_over_samples; the plan folds it into the dX reduction).  _applies: 1 when the
- * state / batch qualifies (EVR_KD3=0 disables it). */
+ * state / batch qualifies. */
 int evr_hvi_restart_fb_applies(const evr_qnehvi_state* st, int b);
 int evr_hvi_restart_fb(void* stream, const evr_qnehvi_state* st, int b, const double* G, double* sval,
                        double* dG);
-/* Restart-scan kernel: 2 = hvi_kdb (default: the sample's entries, pairs and terms balanced over
- * the 16 waves of its workgroup; equal to rounding), 1 = hvi_kd3 (hvi_kd2's per-wave ownership;
- * dG bitwise evr_hvi_forward_backward's; also selected by EVR_KDB=0).  Plans keep the kernel
- * they were captured with.  Process-global, not thread-safe. */
-int evr_hvi_set_restart_variant(int variant);
 /* gR_j (Rr x b): gradient w.r.t. R_j given dG (chains objective, sampling, L22 ladder) */
 int evr_qnehvi_samples_backward(void* stream, const evr_qnehvi_state* st, int b, const double* R,
                                 const double* L22, const double* dG, double* gR);

@@ -74,37 +74,43 @@ def test_config3_qnehvi_values_and_grads_match_oracle(config3, oracle3):
     assert acqf.stats.total_cells == sum(cc.shape[1] for cc in orc.cells)
     assert acqf.stats.max_cells == max(cc.shape[1] for cc in orc.cells)
 
-    Xc = bench.candidates(512, c["d"], seed=2, device=c["dev"])
-    acq, dX = acqf.forward_backward(Xc)            # b = 512 through the native plan
-    sub = torch.arange(0, 512, 32)                 # 16 candidates checked against the oracle
-    xt = Xc.cpu()[sub].clone().requires_grad_(True)
-    ref = orc.forward(xt.unsqueeze(1))
-    ref.sum().backward()
-    a = acq.cpu()[sub]
-    assert (ref.detach() > 0).sum() >= 4           # the subset exercises non-zero improvements
-    assert torch.allclose(a, ref.detach(), rtol=1e-6, atol=1e-10), (a, ref)
-    g = dX.cpu()[sub]
-    scale = xt.grad.abs().max()
-    assert torch.allclose(g, xt.grad, rtol=1e-5, atol=1e-7 * scale), (g - xt.grad).abs().max()
+    # a 16-candidate subset of b = 512 (the MFMA-engine path) and the whole b = 20 restart batch
+    # (the restart-batch kernels), both Sobol seed 2; the b = 20 batch holds the candidates
+    # whose new-point variance cancels furthest (L22^2 / (s^2 kxx) down to 1e-11): there the
+    # oracle itself is up to 9e-6 from the 60-digit truth (tests/test_hp_truth_oracle.py), so
+    # values are held to 2e-5 and gradients to 1e-4 of each candidate's scale
+    for b, sub, vtol, gtol in ((512, torch.arange(0, 512, 32), 1e-6, 1e-5), (20, torch.arange(20), 2e-5, 1e-4)):
+        Xc = bench.candidates(b, c["d"], seed=2, device=c["dev"])
+        acq, dX = acqf.forward_backward(Xc)
+        xt = Xc.cpu()[sub].clone().requires_grad_(True)
+        ref = orc.forward(xt.unsqueeze(1))
+        ref.sum().backward()
+        a = acq.cpu()[sub]
+        assert (ref.detach() > 0).sum() >= 4       # the set exercises non-zero improvements
+        rel = ((a - ref.detach()).abs() / ref.detach().abs().clamp_min(1e-300))[ref.detach() > 1e-12]
+        print(f"qnehvi b={b}: max relative value difference {float(rel.max()):.3e}")
+        assert torch.allclose(a, ref.detach(), rtol=vtol, atol=1e-12), (a, ref)
+        g = dX.cpu()[sub]
+        row = (g - xt.grad).abs().amax(1) / xt.grad.abs().amax(1).clamp_min(1e-300)
+        print(f"qnehvi b={b}: max row-relative gradient difference {float(row[ref.detach() > 1e-12].max()):.3e}")
+        assert (row[ref.detach() > 1e-12] <= gtol).all(), row
 
 
 def test_config3_batch_split_equals_full_batch(config3):
     """The 512-candidate plan against 20-candidate plans (the L-BFGS restart size) on the
     same candidates: equal up to the summation-order rounding of the different GEMM /
-    split-K reductions the two batch sizes select (f64: ~1e-15 relative on R).  That rounding
-    is amplified by the cancellation in L22^2 = s^2 (kxx - |R|^2) next to training points:
-    where 1 - |R|^2 / kxx falls to ~1e-11 the computed L22^2 (R's absolute rounding ~1e-9 at
-    the bench state's ~1e4 operator entries) is noise, and either path may land below zero
-    and take the psd_safe floor (tools/diag_split.py: exact L22 1e-6, one path 1e-6, the
-    other 1e-4) — the reference's own Cholesky of the joint covariance rounds the same way.
-    Those candidates (one path's L22 an order of magnitude off the other's in some output)
-    are held to the north-star bar, 1e-3 of the batch's largest value; every other
-    candidate to 1e-7 (measured 1.6e-11 absolute on values up to ~1e-2)."""
+    split-K reductions the two batch sizes select.  With the split operator (round 6) that
+    rounding stays below the L22^2 cancellation at this state (the fused root's C k carried
+    ~1e-10 absolute rounding against L22^2 / (s^2 kxx) ~ 1e-7 .. 1e-11, and round 5 had to
+    excuse up to 50 of these 500 candidates): every candidate is held to 1e-7 (values) / 1e-6
+    (gradients) and at most 2 may have L22 an order of magnitude apart between the paths
+    (measured 0, max |diff| 1.4e-11)."""
     import bench
     from everest_amd import ops
 
     c = config3
     acqf = c["acqf"]
+    assert acqf.root == "split"
     Xc = bench.candidates(512, c["d"], seed=3, device=c["dev"])
     a_full, g_full = acqf.forward_backward(Xc)
     parts = [acqf.forward_backward(Xc[i:i + 20]) for i in range(0, 500, 20)]
@@ -119,21 +125,17 @@ def test_config3_batch_split_equals_full_batch(config3):
         RB, PB = ops.qnehvi_small_forward(st, acqf.model, Kx[:, :, i:i + 20].contiguous(), 20)
         LB.append(ops.qnehvi_small_samples(st, RB, PB, 20)[1])
     LB = torch.cat(LB, 1)
-    # one path at the psd floor and the other not: their L22 differ by orders of magnitude
-    # (the rounding noise of an unclamped L22 is ~10 % at the bench state's smallest variances)
     la, lb = LA[:, :500].abs(), LB.abs()
     ill = (torch.maximum(la, lb) > 10.0 * torch.minimum(la, lb)).any(0)
-    well = ~ill
     amax = a_full.abs().max().item()
     da = (a_full[:500] - a_p).abs()
-    print(f"batch split: {int(ill.sum())} cancellation-bound candidates; max |diff| well-conditioned "
-          f"{float(da[well].max()):.3e}, all {float(da.max()):.3e}")
-    assert torch.allclose(a_full[:500][well], a_p[well], rtol=1e-7, atol=1e-7 * amax), float(da[well].max())
-    assert float(da.max()) <= 1e-3 * amax, float(da.max())
-    assert int(ill.sum()) <= 50, int(ill.sum())   # a handful next to training points, not a drift
     scale = g_full.abs().max().item()
     dg = (g_full[:500] - g_p).abs()
-    assert torch.allclose(g_full[:500][well], g_p[well], rtol=1e-6, atol=1e-6 * scale), float(dg[well].max())
+    print(f"batch split: {int(ill.sum())} cancellation-bound candidates; max |diff| {float(da.max()):.3e} (values), "
+          f"{float(dg.max()):.3e} (gradients)")
+    assert int(ill.sum()) <= 2, int(ill.sum())
+    assert torch.allclose(a_full[:500], a_p, rtol=1e-7, atol=1e-7 * amax), float(da.max())
+    assert torch.allclose(g_full[:500], g_p, rtol=1e-6, atol=1e-6 * scale), float(dg.max())
 
 
 def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
@@ -163,53 +165,24 @@ def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
         a = acq.cpu()[sub]
         r = ref.detach()
         # log values: an absolute error e in log space is a relative error e in the HVI itself.
-        # North-star bar (1e-3 relative on qNEHVI values) for EVERY candidate, whatever its
-        # HVI; candidates with HVI > 1e-6 (log HVI > -14, where the ~1e-13 absolute rounding of
-        # the L22^2 = var - |L21|^2 cancellation is below 1e-6 relative) are held to 1e-6
+        # Every candidate, whatever its HVI, is held to 2e-5 (the oracle's own distance to the
+        # 60-digit truth is up to 9e-6 at this kind of state, tests/test_hp_truth_oracle.py;
+        # measured device-oracle 1.2e-6; north star 1e-3).  With the fused root (round 5)
+        # candidates whose new-point variance had cancelled to < 1e-6 of the prior differed by
+        # up to 5.6e-4 and were excused from the tight class; the split operator (round 6)
+        # leaves nothing to excuse.
         err = (a - r).abs()
         worst = int(err.argmax())
         print(f"qlog b={b}: max |d log| {float(err.max()):.3e} at log HVI {float(r[worst]):.2f}; "
               f"min log HVI {float(r.min()):.2f}")
-        assert (err <= 1e-3).all(), (b, [(float(x), float(y)) for x, y, bad in zip(a, r, err > 1e-3) if bad])
-        # the 1e-6 class also leaves out candidates whose new-point variance given the
-        # baseline's samples (L22^2 = s^2 (kxx - |R|^2), R = C k through the fused root) has
-        # cancelled to below 1e-6 of the prior in some output: R's entries carry ~1e-12 absolute
-        # rounding (C's entries are ~1e4-1e5 at this state), so the computed L22^2 carries
-        # ~2e-12 of s^2 kxx — over 1e-6 of itself there, and device and oracle round it
-        # differently (tools/qlog_diag.py: the qNEHVI values of such a candidate differ by the
-        # same 5.6e-4 as its log values).  Which candidates these are moves with the fitted state
-        Xs = Xc[sub.to(Xc.device)].contiguous()
-        R, P = ops.qnehvi_small_forward(qa.state, qa.model, qa.gp.cross(Xs), Xs.shape[0])
-        L22 = ops.qnehvi_small_samples(qa.state, R, P, Xs.shape[0])[1]
-        rel = (L22 ** 2 / (qa.gp.ys[:, None] ** 2 * qa.gp.kxx[:, None])).min(0).values.cpu()
-        well = (r > -14.0) & (rel > 1e-6)
-        print(f"qlog b={b}: {int(((r > -14.0) & (rel <= 1e-6)).sum())} candidates with log HVI > -14 at the "
-              f"cancelled-variance floor (held to 1e-3 only)")
-        assert (err[well] <= 1e-6).all(), (b, [(float(x), float(y)) for x, y, e in zip(a[well], r[well], err[well])
-                                               if e > 1e-6])
-        # gradients: the backward contracts the fused root C = Lv^T L^-1 (entries ~1e4-1e5 at
-        # this state) against gR, so each dK entry is an O(1) sum of O(1e5) terms and carries
-        # ~1e-11 absolute rounding whatever the summation order; through d log HVI / dx =
-        # (d HVI / dx) / HVI and the 1 / L22 of the new-point root that reaches a few 1e-5 of a
-        # candidate's gradient scale (measured 1.2e-5 on the b = 512 path; the oracle's own
-        # Cholesky-solve path rounds differently).  Held to 1e-4 of each candidate's gradient
-        # scale where the new-point variance has not cancelled (rel > 1e-6, as above), 1e-3 where
-        # it has cancelled to 1e-8 .. 1e-6 of the prior but the HVI is not negligible (log HVI
-        # > -14); below that the rounding of L22^2 reaches the gradient through 1 / L22 (a
-        # candidate at rel = 7e-9 in one output differs by a few 1e-2 of its gradient scale at
-        # one fitted state), and so does the fat-smoothed tail of a zero-HVI candidate: only
-        # finite there
+        assert (err <= 2e-5).all(), (b, [(float(x), float(y)) for x, y, bad in zip(a, r, err > 2e-5) if bad])
+        # gradients, every candidate (the fat-smoothed tail of a zero-HVI candidate included):
+        # row-relative <= 1e-3 (measured 8.4e-5 at b = 20, 9.8e-7 at b = 512)
         g = dX.cpu()[sub]
         gr = xt.grad
         row_err = (g - gr).abs().amax(1) / gr.abs().amax(1).clamp_min(1e-300)
-        tight = rel > 1e-6
-        mid = ~tight & (rel > 1e-8) & (r > -14.0)
-        for name, sel, bar in (("tight", tight, 1e-4), ("mid", mid, 1e-3)):
-            if int(sel.sum()):
-                print(f"qlog b={b}: {name}: {int(sel.sum())} candidates, max row-relative gradient error "
-                      f"{float(row_err[sel].max()):.3e}")
-                assert (row_err[sel] <= bar).all(), (b, name, row_err)
         print(f"qlog b={b}: max row-relative gradient error, all candidates {float(row_err.max()):.3e}")
+        assert (row_err <= 1e-3).all(), (b, row_err)
         assert torch.isfinite(g).all()
 
 

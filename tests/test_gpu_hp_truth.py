@@ -11,10 +11,12 @@ Candidates: the b = 20 Sobol batch of seed 2, every 32nd of the b = 512 batch of
 at its own batch size (the restart-batch kernels) and all inside one b = 512 batch (the MFMA
 engine path); 16 candidates 1e-2 .. 1e-6 from training points (near16, below).
 
-Bars (the north star's 1e-3 on qNEHVI values), printed with their maxima:
-* values: relative error <= 1e-3 wherever the truth's HVI > 1e-9 (absolute 1e-12 below);
-  qLogNEHVI |d log| <= 1e-3 for every candidate;
-* gradients: row-relative error <= 1e-3 wherever HVI > 1e-9.
+Bars (ten times inside the north star's 1e-3), printed with their maxima:
+* values: relative error <= 1e-4 wherever the truth's HVI > 1e-9 (absolute 1e-12 below);
+  qLogNEHVI |d log| <= 1e-4 there and <= 1e-3 for every candidate;
+* gradients: row-relative error <= 1e-4 wherever HVI > 1e-9.
+Measured (round 6, split root): values 2.2e-6, gradients 1.5e-5; the fused root missed by
+5.6e-4 / 2.6e-2 on the same candidates (tools/hp_eval.py, profiles/r06/c/hp_eval.json).
 """
 import json
 import math
@@ -61,14 +63,14 @@ def _check(name, a, ga, T, GT, log):
     if log:
         verr = np.abs(a - T)
         big = T > math.log(1e-9)
-        vbad = verr > 1e-3
+        vbad = np.where(big, verr > 1e-4, verr > 1e-3)
     else:
         verr = np.abs(a - T) / np.maximum(np.abs(T), 1e-300)
         verr[(a == 0) & (T == 0)] = 0.0
         big = T > 1e-9
-        vbad = np.where(big, verr > 1e-3, np.abs(a - T) > 1e-12)
+        vbad = np.where(big, verr > 1e-4, np.abs(a - T) > 1e-12)
     gerr = np.abs(ga - GT).max(1) / np.maximum(np.abs(GT).max(1), 1e-300)
-    gbad = big & (gerr > 1e-3)
+    gbad = big & (gerr > 1e-4)
     vmax = float(verr[big].max()) if big.any() else 0.0
     gmax = float(gerr[big].max()) if big.any() else 0.0
     print(f"{name}: max value error {vmax:.3e}, max row-relative gradient error {gmax:.3e} "
@@ -98,3 +100,34 @@ def test_qnehvi_and_qlog_match_high_precision_truth(hp, which):
         a, g = acq.forward_backward(Xb)
         _check(f"{which} b=512 {key}", a.cpu()[:len(xs)], g.cpu()[:len(xs)], T[key], T[key + "_grad"],
                key == "qlog")
+
+
+def test_near_training_points_match_truth_to_f64_resolution(hp):
+    """near16: candidates 1e-2 .. 1e-6 from training points (12 of them next to baseline rows).
+    There the exact L22^2 / (s^2 kxx) is 1e-13 .. 1e-19 — below f64's resolution of Sigma_xx
+    (~1e-16 absolute) — so no f64 evaluation of the reference's formula resolves L22 (the
+    oracle, BoTorch's computation shape, is off by up to 5e-7 absolute / O(1) relative there,
+    tests/test_hp_truth_oracle.py).  Held: qNEHVI values within 2e-6 absolute (1.5e-3 of the
+    state's largest HVI, 1.3e-3), exact where the truth is 0; qLogNEHVI |d log| <= 1e-3 where
+    the truth's HVI > 8e-7 (log > -14) and L22 is resolvable in f64 (exact L22^2 / (s^2 kxx)
+    >= 1e-14 in every output; below that the log of a ~1e-6 HVI moves by up to 2e-3 with the
+    rounding of L22^2); both batch paths.  Maxima printed."""
+    import bench
+
+    st, tr, dev = hp["st"], hp["tr"]["near16"], hp["dev"]
+    xs = np.asarray(st["sets"]["near16"])
+    big = bench.candidates(512, hp["d"], seed=5, device="cpu").numpy()
+    big[:len(xs)] = xs
+    for path, Xc in (("b=16", xs), ("b=512", big)):
+        a, _ = hp["acqf"].forward_backward(torch.tensor(Xc, device=dev))
+        la, _ = hp["qa"].forward_backward(torch.tensor(Xc, device=dev))
+        a, la = a.cpu().numpy()[:len(xs)], la.cpu().numpy()[:len(xs)]
+        t, lt = np.asarray(tr["qnehvi"]), np.asarray(tr["qlog"])
+        err = np.abs(a - t)
+        lerr = np.abs(la - lt)
+        sel = (lt > -14.0) & (np.asarray(tr["rel"]).min(0) >= 1e-14)
+        print(f"near16 {path}: max |d qNEHVI| {err.max():.3e}; |d log| where log HVI > -14: "
+              f"{np.array2string(lerr[lt > -14.0], precision=2)}; held to 1e-3: {int(sel.sum())} candidates")
+        assert (err <= 2e-6).all(), (path, err)
+        assert (a[t == 0] == 0).all(), (path, a[t == 0])
+        assert (lerr[sel] <= 1e-3).all(), (path, lerr)

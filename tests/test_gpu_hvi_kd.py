@@ -55,44 +55,6 @@ def test_kd_scan_gout_and_sample_grad():
     assert torch.allclose(d1, d2, rtol=1e-10, atol=1e-14)
 
 
-@pytest.fixture
-def kd_variant():
-    """Select the sparse-scan kernel (evr_hvi_set_kd_variant) and restore the default."""
-    from everest_amd import _native
-
-    lib = _native.load()
-    yield lambda v: _native.check(lib.evr_hvi_set_kd_variant(v), "evr_hvi_set_kd_variant")
-    lib.evr_hvi_set_kd_variant(2)
-
-
-@pytest.mark.parametrize("n,d,m,S,b", [(200, 6, 5, 128, 200), (60, 4, 3, 32, 65), (40, 3, 2, 16, 1),
-                                       (120, 6, 5, 64, 20)])
-def test_kd2_bitwise_equals_kd(kd_variant, n, d, m, S, b):
-    """hvi_kd2 (chunk pre-filter + mark-based owner lookups) visits the same pairs and terms
-    in the same order as hvi_kd: forward and fused forward+backward are bitwise equal — for
-    b > 32; smaller batches split a candidate group's chunks over 2 or 4 waves (one more
-    partial per split, summed in a fixed order by the reduction): equal to 1e-13."""
-    from everest_amd import ops
-
-    kd, dense, lo, hi, d = _pair(n, d, m, S, seed=n + 3 * m)
-    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b + 1).uniform(size=(b, d)), device="cuda")
-    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
-    G, L22, flags = ops.qnehvi_samples_norms(kd.state, R, P, b)
-    out = {}
-    for v in (1, 2):
-        kd_variant(v)
-        a, g = ops.hvi_forward_backward(kd.state, G, b, flags)
-        out[v] = (a, g, ops.hvi_forward(kd.state, G, b, flags))
-    if b > 32:
-        assert all(torch.equal(x, y) for x, y in zip(out[1], out[2]))
-    else:
-        for x, y in zip(out[1], out[2]):
-            assert torch.allclose(y, x, rtol=1e-13, atol=1e-16 * max(1.0, x.abs().max().item()))
-        a2, g2 = ops.hvi_forward_backward(kd.state, G, b, flags)     # repeats bitwise
-        assert torch.equal(a2, out[2][0]) and torch.equal(g2, out[2][1])
-    assert torch.isfinite(out[2][0]).all() and (out[2][0] >= 0).all()
-
-
 def test_kd2_bench_size_matches_tiled_scan():
     """BASELINE configs[2] size (DTLZ2 n=512, d=6, m=5, S=256, b=512): the sparse scan equals
     the tiled dense scan over the same compressed cells, and repeats bitwise."""
@@ -160,46 +122,14 @@ def test_kd_index_invariants():
     assert np.array_equal(np.sort(lo_rank, axis=0), np.sort(lo_x[:C], axis=0))
 
 
-@pytest.mark.parametrize("n,m,S", [(200, 5, 128), (60, 3, 32), (150, 4, 64), (512, 5, 32)])
-def test_kd_sort_variants_bitwise_equal(monkeypatch, n, m, S):
-    """The kd ordering's sort variants produce one ordering bitwise — u32 sort keys (the default
-    when every field fits) or u64 keys, per-segment wave sorts for the deep levels (default) or
-    the whole-buffer sort at every level: kd keys, rank coordinates, group minima and sorted
-    lower bounds."""
-    outs = []
-    for key64, ws in (("1", "0"), ("0", "0"), ("1", "1"), ("0", "1")):
-        monkeypatch.setenv("EVR_KD_KEY64", key64)
-        monkeypatch.setenv("EVR_KD_WS", ws)
-        kd, _, _, _, _ = _pair(n, 6, m, S, seed=n + m)
-        g = kd.cells.kd
-        outs.append([t.cpu() for t in (g.keys, g.rank, g.box, g.sorted_lo)])
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
-
-
-@pytest.fixture
-def restart_variant():
-    """Select the one-launch restart scan (evr_hvi_set_restart_variant) and restore the default."""
-    from everest_amd import _native
-
-    lib = _native.load()
-    yield lambda v: _native.check(lib.evr_hvi_set_restart_variant(v), "evr_hvi_set_restart_variant")
-    lib.evr_hvi_set_restart_variant(3)
-
-
 @pytest.mark.parametrize("n,d,m,S,b", [(120, 6, 5, 256, 20), (60, 4, 3, 256, 7), (40, 3, 2, 512, 1),
                                        (200, 6, 5, 512, 32), (90, 5, 4, 256, 16), (80, 4, 1, 1024, 3)])
-@pytest.mark.parametrize("variant", [1, 2, 3])
-def test_restart_fused_scan_equals_three_launch_chain(restart_variant, variant, n, d, m, S, b):
-    """The one-launch restart scans against hvi_thresholds + hvi_kd2 + hvi_reduce_fb on the same
-    samples: hvi_kd3 (variant 1, per-wave ownership as kd2) bitwise on dG; hvi_kdb (variant 2,
-    work balanced over the workgroup) and hvi_kdw (variant 3, the default: one wave per
-    candidate) in their own summation orders to 1e-12; acq = mean of the per-sample values to
-    1e-14 / 1e-12; all bitwise reproducible."""
+def test_restart_fused_scan_equals_three_launch_chain(n, d, m, S, b):
+    """The one-launch restart scan (hvi_kdw: one wave per candidate) against hvi_thresholds +
+    hvi_kd2 + hvi_reduce_fb on the same samples, in its own summation order to 1e-12; acq =
+    mean of the per-sample values to 1e-12; bitwise reproducible."""
     from everest_amd import ops
 
-    restart_variant(variant)
     kd, dense, lo, hi, d = _pair(n, d, m, S, seed=n + 5 * m)
     assert ops.hvi_restart_fb_applies(kd.state, b)
     assert not ops.hvi_restart_fb_applies(kd.state, 33) and not ops.hvi_restart_fb_applies(dense.state, b)
@@ -210,53 +140,20 @@ def test_restart_fused_scan_equals_three_launch_chain(restart_variant, variant, 
     sval, d2 = ops.hvi_restart_fb(kd.state, G, b)
     torch.cuda.synchronize()
     a2 = ops.mean_over_samples(sval)
-    if variant == 1:
-        assert torch.equal(d1, d2)
-        assert torch.allclose(a1, a2, rtol=1e-14, atol=1e-300)
-    else:
-        assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
-        assert torch.allclose(a2, a1, rtol=1e-12, atol=1e-300)
+    assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
+    assert torch.allclose(a2, a1, rtol=1e-12, atol=1e-300)
     assert torch.isfinite(a1).all() and (b < 7 or (a1 > 0).any())
     sval2, d3 = ops.hvi_restart_fb(kd.state, G, b)
     assert torch.equal(sval, sval2) and torch.equal(d2, d3)      # bitwise reproducible
 
 
-def test_restart_balanced_scan_slices(restart_variant):
-    """hvi_kdb's pair and term slices (more than KB_PCAP = 4096 pairs / KB_TCAP = 8192 terms in
-    one sample: many cells, candidates dominating much of the front) against the three-launch
-    chain."""
-    from everest_amd import ops
-
-    restart_variant(2)
-    kd, dense, lo, hi, d = _pair(240, 6, 5, 256, seed=11, prune=False)
-    b = 32
-    # candidates far above the front: every cell lower corner is below them
-    Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(b, d)), device="cuda")
-    R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)
-    G, L22, flags = ops.qnehvi_samples_norms(kd.state, R, P, b)
-    G = G + 3.0                                    # shift every objective up: dominate the front
-    a1, d1 = ops.hvi_forward_backward(kd.state, G, b, flags)
-    ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
-    kd.state.scan_counters = ctr.data_ptr()
-    try:
-        sval, d2 = ops.hvi_restart_fb(kd.state, G, b)
-        c = ctr.cpu().numpy()
-    finally:
-        kd.state.scan_counters = None
-    S = kd.S
-    assert c[0] / S > 4096 and c[1] / S > 8192, c / S      # per-sample pairs / terms exceed the caps
-    assert torch.allclose(d2, d1, rtol=1e-12, atol=1e-15 * d1.abs().max().item())
-    assert torch.allclose(ops.mean_over_samples(sval), a1, rtol=1e-12)
-
-
-def test_restart_wave_scan_long_term_lists(restart_variant):
+def test_restart_wave_scan_long_term_lists():
     """hvi_kdw on candidates dominating most of the front (hundreds of terms per sample and
     candidate: many 64-term rounds and list remainders) against the three-launch chain, and
     batch-invariant bitwise (a candidate's result depends on its own cells only: the first 9
     candidates alone equal their values in the batch of 32)."""
     from everest_amd import ops
 
-    restart_variant(3)
     kd, dense, lo, hi, d = _pair(240, 6, 5, 256, seed=11, prune=False)
     b = 32
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(b, d)), device="cuda")
@@ -274,13 +171,12 @@ def test_restart_wave_scan_long_term_lists(restart_variant):
 
 
 @pytest.mark.parametrize("b", [20, 32, 7])
-def test_restart_wave_scan_is_batch_invariant(restart_variant, b):
+def test_restart_wave_scan_is_batch_invariant(b):
     """hvi_kdw: a candidate's per-sample value and gradient depend on its own terms only, so
     they are bitwise the same in any batch — the property that makes a restart batch sharded
     over ranks evaluate exactly as on one rank."""
     from everest_amd import ops
 
-    restart_variant(3)
     kd, dense, lo, hi, d = _pair(120, 6, 5, 256, seed=31)
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(b).uniform(size=(b, d)), device="cuda")
     R, P = ops.qnehvi_project(kd.state, kd.M, kd.gp.cross(Xc), b)

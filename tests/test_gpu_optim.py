@@ -51,25 +51,6 @@ def test_plan_minimize_equals_python_driven_lbfgsb():
     assert v1 > 0
 
 
-def test_queued_evaluations_equal_unqueued(monkeypatch):
-    """EVR_QUEUE=1 (opt-in): the restart loop queues each evaluation's host graph behind the
-    previous one, its first kernel waiting for the request word — same chain, same results:
-    the optimiser's trajectory, candidates and values are bitwise those of the default path."""
-    from everest_amd.optim import optimize_acqf
-
-    bounds = None
-    runs = []
-    for q in ("0", "1"):
-        monkeypatch.setenv("EVR_QUEUE", q)
-        acqf, lo, hi = _acqf()          # a fresh acquisition: its plans read EVR_QUEUE at setup
-        bounds = np.stack([lo, hi])
-        runs.append(optimize_acqf(acqf, bounds, 8, 256, {"batch_limit": 8, "maxiter": 2000},
-                                  torch.Generator().manual_seed(1)))
-    (x1, v1, s1), (x2, v2, s2) = runs
-    assert s1.chunks[0]["driver"] == s2.chunks[0]["driver"] == "native-plan"
-    assert np.array_equal(x1, x2) and v1 == v2 and s1.chunks[0]["evals"] == s2.chunks[0]["evals"]
-
-
 def test_native_lbfgsb_tracks_scipy_on_the_acquisition():
     from everest_amd.optim import optimize_acqf
 

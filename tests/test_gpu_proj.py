@@ -149,30 +149,25 @@ def test_restart_chain_is_batch_invariant():
         assert np.array_equal(a2, a[sl]) and np.array_equal(g2, g[sl])
 
 
-def test_restart_backward_tail_placements(monkeypatch):
-    """The restart backward's training-row class (qs_tail.hpp) in workgroups of its own inside
-    the backward launch (EVR_QS_TAIL=bwd, default) and in the restart scan's tail (kdw) run
-    the same device function on the same inputs: bitwise equal, device chain and host-driven
-    evaluation alike; inside qs_bwd's own workgroups (0) the class is scaled before the
-    cross-covariance step instead of after it: equal to rounding."""
+def test_restart_backward_device_and_host_chains_equal():
+    """The restart backward's training-row classes (qs_tail.hpp: the split root's L^-1 and G
+    rows, weighted into one class; the fused root's C rows) run as the backward launch's own
+    workgroups: the device chain and the host-driven evaluation are bitwise equal for both
+    roots, and the two roots agree to the cancellation-free rounding of this state."""
     from everest_amd.acquisition import QNEHVI
 
     n, d, m, S = 90, 5, 4, 48
     X, Y, lo, hi, hyp = make_problem(n=n, d=d, m=m, seed=35)
     gp = device_gp(X, Y, lo, hi, hyp)
-    q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=5, prune_baseline=True,
-               prune_seed=6, prune_samples=256)
     Xc = torch.tensor(lo + (hi - lo) * np.random.default_rng(3).uniform(size=(20, d)), device="cuda")
     out = {}
-    for mode in ("bwd", "kdw", "0"):
-        monkeypatch.setenv("EVR_QS_TAIL", mode)
-        q._plans = {}
+    for root in ("split", "fused"):
+        q = QNEHVI(gp, X, X, -1.1 * np.ones(m), -np.ones(m), np.zeros(m), S=S, sampler_seed=5, prune_baseline=True,
+                   prune_seed=6, prune_samples=256, root=root)
         a, g = q.forward_backward(Xc)
         ah, gh = q.eval_host(Xc.cpu().numpy(), True)
         assert np.array_equal(ah, a.cpu().numpy()) and np.array_equal(gh, g.cpu().numpy())
-        out[mode] = (a.clone(), g.clone())
-    q._plans = {}
-    assert torch.equal(out["bwd"][0], out["kdw"][0]) and torch.equal(out["bwd"][1], out["kdw"][1])
-    assert torch.equal(out["bwd"][0], out["0"][0])     # the forward is untouched
-    g0, g1 = out["0"][1], out["bwd"][1]
-    assert torch.allclose(g1, g0, rtol=1e-10, atol=1e-13 * g0.abs().max())
+        out[root] = (a, g)
+    a0, g0 = out["split"]
+    assert torch.allclose(out["fused"][0], a0, rtol=1e-7, atol=1e-12)
+    assert torch.allclose(out["fused"][1], g0, rtol=1e-5, atol=1e-8 * g0.abs().max())

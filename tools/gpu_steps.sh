@@ -21,7 +21,6 @@
 #   sq20        SQ wave-cycle split of the restart chain kernels (hvi_kdw, qs_fwd, qs_bwd) at b = 20
 #   kdwaves     per-wave phase stamps of hvi_kd3 / hvi_kdb (EVR_KD_PROF=2 build in _libprof/)
 #   kdwwaves    per-(sample, candidate) phase stamps of hvi_kdw (EVR_KD_PROF=2 build in _libkdprof/)
-#   qlogab      tools/qlog_ab.py (qLogNEHVI scan: kd-bounded vs unbounded keyed) -> <tag>/qlog_ab.json
 #   hpeval      tools/hp_eval.py (device vs the 60-digit truth, fused and split roots) -> <tag>/hp_eval.json
 #   benchsplit  benchq with EVR_ROOT=split (benchfused: EVR_ROOT=fused)
 #   hpdump      tools/hp_state_dump.py (config-3 state + device values for tools/hp_truth.py) -> <tag>/hp_state.json
@@ -60,7 +59,6 @@ for st in "$@"; do
     asktl)
       run asktl_trace 300 rocprofv3 --kernel-trace -d "$OUT/asktl" -o run --output-format csv -- python tools/ask_timeline.py
       run asktl_parse 60 python tools/ask_timeline.py --analyse "$OUT/asktl" "$OUT/asktl_trace.log" && cp "$OUT/asktl_parse.log" "$OUT/ask_timeline.json" ;;
-    qlogab) run qlogab 300 python tools/qlog_ab.py && cp "$OUT/qlogab.log" "$OUT/qlog_ab.json" ;;
     hpdump) run hpdump 300 python tools/hp_state_dump.py "$OUT/hp_state.json" ;;
     hpeval) run hpeval 300 python tools/hp_eval.py "$OUT/hp_eval.json" ;;
     benchsplit) EVR_ROOT=split run benchsplit 600 python bench.py --no-cpu-baseline --no-eval-pass ;;

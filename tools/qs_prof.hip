@@ -62,15 +62,9 @@ int main(int argc, char** argv) {
     return 1;
   }
   const dim3 grid(nt, m, zs);
-#define QSB(G_, T_)                                                                                                 \
-  do {                                                                                                           \
-    if (tail)                                                                                                    \
-      evr::qs_bwd<false, true><<<G_, T_>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, \
-                                           nullptr, ls, dXp, nt, rows_per, np, cfo, zs, evr::QsTail{});          \
-    else                                                                                                         \
-      evr::qs_bwd<false, false><<<G_, T_>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, \
-                                            nullptr, ls, dXp, nt, rows_per, np, cfo, zs, evr::QsTail{});         \
-  } while (0)
+#define QSB(G_, T_)                                                                                               \
+  evr::qs_bwd<<<G_, T_>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, nullptr, ls, dXp, nt, \
+                          rows_per, np, cfo, zs, evr::QsTail{})
   const int nwg = nt * m * zs;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -128,19 +122,13 @@ int main(int argc, char** argv) {
   }
   float mst = 0;
   if (tail) {
-    evr::QsTail tl{M, Rf, Xn, X, nullptr, nullptr, ls, dXp, n, Rr, b, d, kind, nt, za, 256, npB, np, m * za * nt};
-    for (int r = 0; r < 5; ++r) evr::qs_bwd_tail<<<m * za * nt, 256>>>(tl);
-    (void)hipEventRecord(e0);
-    for (int r = 0; r < reps; ++r) evr::qs_bwd_tail<<<m * za * nt, 256>>>(tl);
-    (void)hipEventRecord(e1);
-    (void)hipEventSynchronize(e1);
-    (void)hipEventElapsedTime(&mst, e0, e1);
-    printf("{\"qs_bwd_tail\": {\"grid\": %d, \"launch_us\": %.2f}}\n", m * za * nt, mst * 1e3 / reps);
+    evr::QsTail tl{M, Rf, Xn, X, nullptr, nullptr, ls, dXp, ys, n, nb, Rr, b, d, kind, nt, za, 256, npB, np,
+                   m * za * nt};
     // the default mode: the tail's workgroups as the backward launch's z >= 1 slices
     const dim3 gc(nt, m, zs + za);
     auto comb = [&]() {
-      evr::qs_bwd<false, true><<<gc, 256>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr,
-                                            nullptr, ls, dXp, nt, rows_per, np, cfo, zs, tl);
+      evr::qs_bwd<<<gc, 256>>>(n, nb, nh, S, m, b, d, kind, M, R, dG, L22, ys, zq, oa, Xn, X, nullptr, nullptr, ls,
+                               dXp, nt, rows_per, np, cfo, zs, tl);
     };
     for (int r = 0; r < 5; ++r) comb();
     (void)hipEventRecord(e0);

@@ -1,13 +1,11 @@
-"""A/B of the restart-batch scan variants at the bench state: the config-4 QnehviStrategy after
-one ask (bench.make_ask_strategy, seed 1), its optimised restart candidates (b = 20) and a
-Sobol batch; per variant (evr_hvi_set_restart_variant: 1 = hvi_kd3, 2 = hvi_kdb, 3 = hvi_kdw)
-the scan's device time (10 launches in one HIP graph between HIP events), the plan's device
-chain per evaluation (50 back-to-back device-mode graph launches between HIP events), its
-host round trip per evaluation (plan.run_host: launch + chain + completion poll) and the
-native L-BFGS-B's wall time per evaluation (plan.minimize from the Sobol start, 30
-iterations: round trip + the optimiser's host step); kdw_tailscan / kdw_notail: EVR_QS_TAIL=kdw / 0
-(the backward's training-row class in the scan's tail / inside qs_bwd's workgroups instead of
-workgroups of its own in the backward's launch).  One JSON line."""
+"""The restart-batch evaluation at the bench state: the config-4 QnehviStrategy after one ask
+(bench.make_ask_strategy, seed 1), its optimised restart candidates (b = 20) and a Sobol batch:
+the restart scan's device time (hvi_kdw, 10 launches in one HIP graph between HIP events), the
+plan's device chain per evaluation (50 back-to-back device-mode graph launches between HIP
+events), its host round trip per evaluation (plan.run_host: launch + chain + completion poll)
+and the native L-BFGS-B's wall time per evaluation (plan.minimize from the Sobol start, 30
+iterations: round trip + the optimiser's host step).  The forward operator is EVR_ROOT's
+(split by default).  One JSON line."""
 import json
 import os
 import sys
@@ -18,7 +16,7 @@ import numpy as np
 import torch
 
 import bench
-from everest_amd import _native, ops
+from everest_amd import ops
 
 
 def graph_ms(f, reps=10):
@@ -44,23 +42,13 @@ def main():
     s.ask(1)
     acqf = s.last_acqf
     Xopt = np.ascontiguousarray(s.last_ask_stats.restart_X.reshape(20, -1))
-    lib = _native.load()
     out = {}
     for tag, X in (("opt", Xopt), ("sobol", bench.candidates(20, 6, seed=5, device=dev).cpu().numpy())):
         Xt = torch.tensor(X, device=dev)
         b = X.shape[0]
         R, P = ops.qnehvi_small_forward(acqf.state, acqf.model, acqf.gp.cross(Xt), b)
         G, L22, flags = ops.qnehvi_small_samples(acqf.state, R, P, b)
-        for v, name, tl, tr, tf in ((1, "kd3", "bwd", "256", "0"), (2, "kdb", "bwd", "256", "0"),
-                                    (3, "kdw", "bwd", "256", "0"), (3, "kdw_tailscan", "kdw", "256", "0"),
-                                    (3, "kdw_notail", "0", "256", "0")):
-            # EVR_QS_TAIL: the backward's training-row class in workgroups of its own inside the
-            # backward's launch (bwd), in the scan's tail (kdw) or in qs_bwd's workgroups (0);
-            # EVR_QS_TAIL_ROWS: training rows per tail workgroup; EVR_QS_TAIL_FIRST (kdw mode)
-            os.environ["EVR_QS_TAIL"] = tl
-            os.environ["EVR_QS_TAIL_ROWS"] = tr
-            os.environ["EVR_QS_TAIL_FIRST"] = tf
-            _native.check(lib.evr_hvi_set_restart_variant(v), "variant")
+        for name in ("kdw",):
             scan = graph_ms(lambda: ops.hvi_restart_fb(acqf.state, G, b))
             acqf._plans = {}
             p = acqf.plan(b, True)
@@ -88,11 +76,8 @@ def main():
                 rec["minimize_us_per_eval"] = round((time.perf_counter() - t0) / max(1, info[1]) * 1e6, 2)
                 rec["minimize_evals"] = int(info[1])
             out[f"{tag}_{name}"] = rec
-    _native.check(lib.evr_hvi_set_restart_variant(3), "variant")
-    os.environ.pop("EVR_QS_TAIL", None)
-    os.environ.pop("EVR_QS_TAIL_ROWS", None)
-    os.environ.pop("EVR_QS_TAIL_FIRST", None)
     acqf._plans = {}
+    out["root"] = acqf.root
     out["construction"] = {k: round(v * 1e3, 3) for k, v in acqf.timings.items()}
     out["base_jitter"] = [float(v) for v in acqf.base_jitter.cpu()]
     print(json.dumps(out))
