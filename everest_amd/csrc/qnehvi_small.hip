@@ -135,20 +135,23 @@ __global__ __launch_bounds__(QS_FT, 4) void qs_fwd(int n, int nb, int Rr, int b,
       acc1 = mfma4(a, Ks[k][i + 16], acc1);
     }
   };
+  // split root (nb > 0): rows r < n are L^-1's, lower triangular — the tile's rows reach
+  // column r0 + 15 at most, so the chunks past it are exact zeros and are skipped
+  const int kend = (nb > 0 && r0 < n) ? min(n, r0 + QS_FR) : n;
   load(mvA, kvA, 0);
-  if (QS_KC < n) load(mvB, kvB, QS_KC);
-  for (int kc = 0; kc < n; kc += 2 * QS_KC) {
+  if (QS_KC < kend) load(mvB, kvB, QS_KC);
+  for (int kc = 0; kc < kend; kc += 2 * QS_KC) {
     __syncthreads();   // the previous chunk's MFMAs are done with Ms, Ks
     stage(mvA, kvA);
     __syncthreads();
     if (kc == 0) QS_STAMP(1);
-    if (kc + 2 * QS_KC < n) load(mvA, kvA, kc + 2 * QS_KC);
+    if (kc + 2 * QS_KC < kend) load(mvA, kvA, kc + 2 * QS_KC);
     mult();
-    if (kc + QS_KC >= n) break;
+    if (kc + QS_KC >= kend) break;
     __syncthreads();
     stage(mvB, kvB);
     __syncthreads();
-    if (kc + 3 * QS_KC < n) load(mvB, kvB, kc + 3 * QS_KC);
+    if (kc + 3 * QS_KC < kend) load(mvB, kvB, kc + 3 * QS_KC);
     mult();
   }
   QS_STAMP(2);

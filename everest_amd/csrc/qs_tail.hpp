@@ -36,7 +36,10 @@ struct QsTail {
 constexpr int QT_BI = 16;     // training rows per tail workgroup
 constexpr int QT_MAXD = 8;    // input dims
 constexpr int QT_B = 32;      // candidates
-constexpr int QT_KB = 8;      // MFMA k-steps (4 rows each) per load batch
+#ifndef EVR_QT_KB
+#define EVR_QT_KB 8
+#endif
+constexpr int QT_KB = EVR_QT_KB;   // MFMA k-steps (4 rows each) per load batch (compile-time A/B knob)
 // LDS (doubles): the waves' D tiles, then (aliased) the row groups' gradient partials; after
 // them the candidates (normalised, b x d) and the inverse lengthscales (d)
 constexpr int QT_RED = (4 * QT_BI * (QT_B + 1) > 8 * QT_B * QT_MAXD) ? 4 * QT_BI * (QT_B + 1) : 8 * QT_B * QT_MAXD;
@@ -66,10 +69,13 @@ __device__ __forceinline__ void qs_tail_tile(const QsTail& t, int wg, double* ld
     xv = t.X[tid];
     lv = t.ls[(size_t)j * d + tid % d];
   }
-  // this wave's rows of the split: a quarter, whole k-steps
-  const int zb = z * t.rows_per, ze = min(n + t.nb, zb + t.rows_per);
+  // this wave's rows of the split: a quarter, whole k-steps.  Split root: the L^-1 block is
+  // lower triangular, so its rows r < i0 are exact zeros in this tile's columns — the split's
+  // rows start at i0 there and the waves share what remains
+  const int zb0 = z * t.rows_per, ze = min(n + t.nb, zb0 + t.rows_per);
+  const int zb = t.nb > 0 ? min(ze, max(zb0, i0)) : zb0;
   const double w0 = t.nb > 0 ? t.ys[j] * t.ys[j] : 1.0;
-  const int rw = (((t.rows_per + 3) / 4) + 3) & ~3;
+  const int rw = (((ze - zb + 3) / 4) + 3) & ~3;
   const int r0 = zb + wave * rw, r1 = min(ze, r0 + rw);
   const bool colok = i0 + i < n;
   qt_double4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
