@@ -271,8 +271,9 @@ class _BoxHviAcqf:
 
     def _use_log_scan(self, tau_relu: float, tau_max: float):
         """Switch the scan to the log-space fat-smoothed HVI (qLogNEHVI / qLogEHVI): the
-        q = 1 affine fast path runs hvi_log.hip (the kd-bounded tabulated kernel over compressed
-        cells, the dense kernel over explicit ones), every other case
+        q = 1 affine fast path runs hvi_log.hip (hvi_logk_kernel, log fatplus tabulated over the
+        point table, over every compressed cell; the dense kernel over explicit ones, or with
+        EVR_LOG=dense), every other case
         (output constraints, CloseToTarget / selected outputs, q > 1, qLogEHVI pending points)
         the general log scan (evr_qlog_eval), both over the explicit cell bounds (compressed
         cells are expanded once, on the device)."""
@@ -283,9 +284,9 @@ class _BoxHviAcqf:
         def logify(src):
             st = _native.EvrQnehviState.from_buffer_copy(src)
             st.cell_lo, st.cell_hi = lo.data_ptr(), hi.data_ptr()
-            # compressed cells and their kd groups stay: the q = 1 scan tabulates log fatplus
-            # over the point table and skips the kd groups whose bound is below 2^-60 of the
-            # sample's sum (hvi_logkd_kernel); the general log scan reads the explicit rows
+            # compressed cells stay: the q = 1 scan tabulates log fatplus over the point table
+            # and visits every compressed cell (hvi_logk_kernel; the fat-smoothed terms have no
+            # sparsity to skip); the general log scan reads the explicit rows
             st.log_hvi, st.tau_relu, st.tau_max = 1, float(tau_relu), float(tau_max)
             return st
         self._log_cells = (lo, hi)

@@ -149,6 +149,34 @@ __device__ __forceinline__ double kernel_value(int kind, double d2) {
   const double s = 2.23606797749979 * d;
   return (1.0 + s + (5.0 / 3.0) * d2) * exp_k(-s);
 }
+// sqrt of a normal x > 0 (the Matérn distance after the 1e-30 clamp): v_rsq_f64, one
+// Goldschmidt step and one Newton correction — 8 VALU ops against the ~20 of the libm-style
+// f64 sqrt (denormal scaling, two corrections, class tests); within ~1 ulp of sqrt.
+__device__ __forceinline__ double sqrt_pos(double x) {
+#pragma clang fp contract(off)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  return fma(fma(-g, g, x), h, g);
+}
+// kernel_value_t with sqrt_pos (the MFMA kernel-matrix epilogues).  Every product and sum is
+// spelled out (contraction off, explicit fma): the cross and the symmetric kernels inline it
+// into different code, and the backend's free fusion of (1 + s) + (5/3) d2 differed between
+// them by an ulp — K(X, X) must be bitwise the same through either.
+__device__ __forceinline__ double kernel_value_r(int kind, double d2, const double* __restrict__ T) {
+#pragma clang fp contract(off)
+  if (kind == RBF) return exp_k_t(-0.5 * d2, T);
+  const double d = sqrt_pos(fmax(d2, 1e-30));
+  if (kind == MATERN05) return exp_k_t(-d, T);
+  if (kind == MATERN15) {
+    const double s = 1.7320508075688772 * d;
+    return (1.0 + s) * exp_k_t(-s, T);
+  }
+  const double s = 2.23606797749979 * d;
+  return fma(5.0 / 3.0, d2, 1.0 + s) * exp_k_t(-s, T);
+}
 // kernel_value with the exp table in LDS (bitwise equal)
 __device__ __forceinline__ double kernel_value_t(int kind, double d2, const double* __restrict__ T) {
   if (kind == RBF) return exp_k_t(-0.5 * d2, T);

@@ -7,6 +7,7 @@
 // doubles of a row.  Distances are formed from explicit differences (no x^2+x'^2-2xx'
 // cancellation).  HBM-bound for small d: 8 bytes written per entry.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "gemm_core.hpp"
@@ -133,6 +134,196 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
 using kd4_t = __attribute__((ext_vector_type(4))) double;
 using kd2_t = __attribute__((ext_vector_type(2))) double;
 
+// The tile's kernel values (wave quadrant rows wm.., cols wn..; acc[q] in the MFMA D layout:
+// register r of lane l is entry (wm + (q >> 1) 16 + (l >> 4) + 4 r, wn + (q & 1) 16 + (l & 15))).
+// d2 = |u1|^2 + |u2|^2 - 2 u1.u2 clamped at 0, exactly 0 on a diagonal entry pairing bitwise-
+// identical points (dtile: i0 == j0, the only tiles holding diagonal entries).
+template <int KIND>
+__device__ __forceinline__ void kmat_epilogue(const kd4_t (&acc)[4], const double* na, const double* nb2,
+                                              const int* eqr, const double* kexp, int wm, int wn, bool dtile,
+                                              double scale, double dadd, double (&vals)[4][4]) {
+#pragma clang fp contract(off)   // explicit fma only: the same rounding in both kernels
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+  const double nbv[2] = {nb2[wn + col], nb2[wn + 16 + col]};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double d2 = fmax(fma(-2.0, acc[q][r], na[wm + (q >> 1) * 16 + rq + 4 * r] + nbv[q & 1]), 0.0);
+      vals[q][r] = scale * kernel_value_r(KIND, d2, kexp);
+    }
+  // the diagonal entries, apart (a per-entry test in the loop above became a branch around
+  // each entry's LDS read): identical points take d2 = 0, every diagonal entry gets dadd
+  if (dtile) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+        if (li == lj) vals[q][r] = (eqr[li] ? scale * kernel_value_r(KIND, 0.0, kexp) : vals[q][r]) + dadd;
+      }
+  }
+}
+
+// kmat_epilogue + kmat_store fused per accumulator register group: the four values of
+// acc[q] are stored as soon as they are formed, so the tile's stores stream out under the
+// kernel evaluation of the next group instead of leaving in one burst after all 16 values
+// (the one-shot grid runs every workgroup in the same phase: the burst was the chip's store
+// phase).  Values bitwise those of kmat_epilogue; vals keeps them (the symmetric kernel's
+// transposed write).
+template <int KIND>
+__device__ __forceinline__ void kmat_epilogue_stream(const kd4_t (&acc)[4], const double* na, const double* nb2,
+                                                     const int* eqr, const double* kexp, int wm, int wn, bool dtile,
+                                                     double scale, double dadd, double* Kb, int n1, int n2, int i0,
+                                                     int j0, double (&vals)[4][4]) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+  const double nbv[2] = {nb2[wn + col], nb2[wn + 16 + col]};
+  bool interior = i0 + KT <= n1 && j0 + KT <= n2;
+  const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
+  double* p0 = Kb + (size_t)min(gi0, n1 - 1) * n2 + min(gj0, n2 - 1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double d2 = fmax(fma(-2.0, acc[q][r], na[wm + (q >> 1) * 16 + rq + 4 * r] + nbv[q & 1]), 0.0);
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 1)   // profiling builds only: no kernel evaluation
+      vals[q][r] = scale * d2;
+#else
+      vals[q][r] = scale * kernel_value_r(KIND, d2, kexp);
+#endif
+    }
+    if (dtile) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
+        if (li == lj) vals[q][r] = (eqr[li] ? scale * kernel_value_r(KIND, 0.0, kexp) : vals[q][r]) + dadd;
+      }
+    }
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 2)   // profiling builds only: no output stream
+    if (vals[q][0] == -1.25) interior = false;
+    if (vals[q][1] != -1.25) continue;
+#endif
+    if (interior) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p0[(size_t)((q >> 1) * 16 + 4 * r) * n2 + (q & 1) * 16] = vals[q][r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = gi0 + (q >> 1) * 16 + 4 * r, gj = gj0 + (q & 1) * 16;
+        if (gi < n1 && gj < n2) Kb[(size_t)gi * n2 + gj] = vals[q][r];
+      }
+    }
+  }
+}
+
+// the tile's values to K (n1 x n2, row-major): interior tiles without per-entry guards
+__device__ __forceinline__ void kmat_store(double* Kb, int n1, int n2, int i0, int j0, int wm, int wn,
+                                           const double (&vals)[4][4]) {
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+  const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
+  if (i0 + KT <= n1 && j0 + KT <= n2) {
+    double* p = Kb + (size_t)gi0 * n2 + gj0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[(size_t)((q >> 1) * 16 + 4 * r) * n2 + (q & 1) * 16] = vals[q][r];
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = gi0 + (q >> 1) * 16 + 4 * r, gj = gj0 + (q & 1) * 16;
+      if (gi < n1 && gj < n2) Kb[(size_t)gi * n2 + gj] = vals[q][r];
+    }
+}
+
+// Operand staging of the MFMA kernels: rows i0.. of X1 and j0.. of X2 (zero beyond n1 / n2),
+// the d columns normalised ((x - shift) scale) and divided by the lengthscales, transposed
+// into As[k][r] / Bs[k][r] (zero for k >= d).  Every load is issued before the first wait.
+// DP | 256 (16, 32, 64): thread tid owns column k = tid % DP of rows tid / DP + (256 / DP) t,
+// one reciprocal of its lengthscale and branch-free clamped loads; DP = 48 the generic map.
+template <int DP>
+__device__ __forceinline__ void kmat_stage(double (*As)[KT + 2], double (*Bs)[KT + 2], const double* X1,
+                                           const double* sh1, const double* sc1, const double* X2,
+                                           const double* sh2, const double* sc2, const double* lsb, int n1,
+                                           int n2, int d, int i0, int j0) {
+  const int tid = threadIdx.x;
+  if constexpr (256 % DP == 0) {
+    constexpr int RS = 256 / DP, NE = KT / RS;
+    const int k = tid % DP, rr = tid / DP;
+    const bool kin = k < d;
+    const int kc = kin ? k : 0;
+    const double il = 1.0 / lsb[kc];
+    const double s1 = sh1 ? sh1[kc] : 0.0, c1 = sc1 ? sc1[kc] : 1.0;
+    const double s2 = sh2 ? sh2[kc] : 0.0, c2 = sc2 ? sc2[kc] : 1.0;
+    double v[NE], w[NE];
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int r = rr + RS * t;
+      v[t] = X1[(size_t)min(i0 + r, n1 - 1) * d + kc];
+      w[t] = X2[(size_t)min(j0 + r, n2 - 1) * d + kc];
+    }
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int r = rr + RS * t;
+      // (v - 0) and v * 1 are exact: the same values as the optional shift / scale steps
+      As[k][r] = (kin && i0 + r < n1) ? (v[t] - s1) * c1 * il : 0.0;
+      Bs[k][r] = (kin && j0 + r < n2) ? (w[t] - s2) * c2 * il : 0.0;
+    }
+  } else {
+    constexpr int NE = (KT * DP + 255) / 256;
+    double v[NE], w[NE];
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int e = tid + 256 * t;
+      const int r = e / DP, k = e - r * DP;
+      v[t] = 0.0;
+      w[t] = 0.0;
+      if (e < KT * DP && k < d) {
+        if (i0 + r < n1) v[t] = X1[(size_t)(i0 + r) * d + k];
+        if (j0 + r < n2) w[t] = X2[(size_t)(j0 + r) * d + k];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int e = tid + 256 * t;
+      const int r = e / DP, k = e - r * DP;
+      if (e < KT * DP) {
+        double a = 0.0, c = 0.0;
+        if (k < d) {
+          const double il = 1.0 / lsb[k];
+          if (i0 + r < n1) a = (v[t] - (sh1 ? sh1[k] : 0.0)) * (sc1 ? sc1[k] : 1.0) * il;
+          if (j0 + r < n2) c = (w[t] - (sh2 ? sh2[k] : 0.0)) * (sc2 ? sc2[k] : 1.0) * il;
+        }
+        As[k][r] = a;
+        Bs[k][r] = c;
+      }
+    }
+  }
+}
+
+// squared row norms of the staged operands (one wave each, k in order) and, on a diagonal
+// tile, which rows of the two operands are bitwise identical (a third wave)
+template <int DP>
+__device__ __forceinline__ void kmat_norms(const double (*As)[KT + 2], const double (*Bs)[KT + 2], double* na,
+                                           double* nb2, int* eqr, bool dtile) {
+  const int wave = threadIdx.x >> 6, r = threadIdx.x & 63;
+  if (wave < 2) {
+    const double (*S)[KT + 2] = wave == 0 ? As : Bs;
+    double sq = 0.0;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) sq = fma(S[k][r], S[k][r], sq);
+    (wave == 0 ? na : nb2)[r] = sq;
+  } else if (wave == 2 && dtile) {
+    int eq = 1;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) eq &= As[k][r] == Bs[k][r];
+    eqr[r] = eq;
+  }
+}
+
 template <int DP, int KIND>
 __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2, int d,
                                                         const double* __restrict__ X1, const double* __restrict__ sh1,
@@ -154,64 +345,10 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const int i0 = by * KT, j0 = bx * KT;
   const double* lsb = ls + (size_t)b * d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // staging: every load of the tile is issued before the first wait (NE independent
-  // loads per operand per thread), then the normalised values go to LDS
-  constexpr int NE = (KT * DP + 255) / 256;
-  double v[NE], w[NE];
-#pragma unroll
-  for (int t = 0; t < NE; ++t) {
-    const int e = tid + 256 * t;
-    const int r = e / DP, k = e - r * DP;
-    v[t] = 0.0;
-    w[t] = 0.0;
-    if (e < KT * DP && k < d) {
-      if (i0 + r < n1) v[t] = X1[(size_t)(i0 + r) * d + k];
-      if (j0 + r < n2) w[t] = X2[(size_t)(j0 + r) * d + k];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < NE; ++t) {
-    const int e = tid + 256 * t;
-    const int r = e / DP, k = e - r * DP;
-    if (e < KT * DP) {
-      double a = 0.0, c = 0.0;
-      if (k < d) {
-        const double il = 1.0 / lsb[k];
-        if (i0 + r < n1) {
-          a = v[t];
-          if (sh1) a -= sh1[k];
-          if (sc1) a *= sc1[k];
-          a *= il;
-        }
-        if (j0 + r < n2) {
-          c = w[t];
-          if (sh2) c -= sh2[k];
-          if (sc2) c *= sc2[k];
-          c *= il;
-        }
-      }
-      As[k][r] = a;
-      Bs[k][r] = c;
-    }
-  }
+  kmat_stage<DP>(As, Bs, X1, sh1, sc1, X2, sh2, sc2, lsb, n1, n2, d, i0, j0);
   kexp_stage(kexp, tid, 256);
   __syncthreads();
-  if (tid < 2 * KT) {
-    const int r = tid & (KT - 1);
-    double sq = 0.0;
-    if (tid < KT) {
-      int eq = 1;
-      for (int k = 0; k < DP; ++k) {
-        sq = fma(As[k][r], As[k][r], sq);
-        eq &= As[k][r] == Bs[k][r];
-      }
-      na[r] = sq;
-      eqr[r] = eq;
-    } else {
-      for (int k = 0; k < DP; ++k) sq = fma(Bs[k][r], Bs[k][r], sq);
-      nb2[r] = sq;
-    }
-  }
+  kmat_norms<DP>(As, Bs, na, nb2, eqr, i0 == j0);
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int i = lane & 15, kq = lane >> 4;
   kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -228,31 +365,151 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const double scale = os ? os[b] : 1.0;
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n1 * n2;
-  const int col = lane & 15, rq = lane >> 4;
+  // every value is formed first and the stores follow: a per-entry bounds branch around the
+  // kernel evaluation serialised the 16 entries' dependent chains (SQ: ~90 VALU + 39 SALU per
+  // entry, round 5); out-of-range entries compute on the zero padding and are not stored
+  double vals[4][4];
+  kmat_epilogue_stream<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0 == j0, scale, dadd, Kb, n1, n2, i0, j0, vals);
+  // (LDS-staged row-segment epilogues, with and without non-temporal or 16-byte stores, were
+  // measured slower at config 5 and removed in round 6: profiles/r05/p/kmat_epi*.json)
+}
+
+// Persistent form of kmat_mfma_kernel (DP | 256): a grid of a few workgroups per CU walks the
+// tiles, each XCD a contiguous run of them (operand panels shared in its L2).  The next tile's
+// operand loads are issued before this tile's epilogue and stores: gfx9's vmcnt retires loads
+// and stores in issue order, so loads issued after the stores would wait for them, while loads
+// issued before let the stores drain under the next tile's staging, MFMA and kernel
+// evaluation.  (The one-shot grid runs every phase chip-wide in lock step — operand loads,
+// then VALU, then a 33.5 MB store burst at config 5 — nothing overlapped.)  Values bitwise
+// those of kmat_mfma_kernel.
+// the tile's values to K through a buffer descriptor: entries outside n1 x n2 take an offset
+// past the descriptor's range, which the hardware drops — every store is issued on every path
+// (no exec-mask branch around a store: the persistent kernel's memory-counter waits assume
+// the 16 stores are always behind the next tile's loads).  n1 n2 8 < 2^31.
+__device__ __forceinline__ void kmat_store_buf(__amdgpu_buffer_rsrc_t rsrc, int n1, int n2, int i0, int j0, int wm,
+                                               int wn, const double (&vals)[4][4]) {
+  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
+  const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-      const int gi = i0 + li, gj = j0 + lj;
-      if (gi < n1 && gj < n2) {
-        double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-        if (gi == gj && eqr[li]) d2 = 0.0;   // identical points: exact zero distance (i0 == j0 here)
-#if EVR_KMAT_DIAG == 1   // profiling builds only: no kernel evaluation (the epilogue's VALU share)
-        double v = scale * d2;
-#else
-        double v = scale * kernel_value_t(KIND, d2, kexp);
-#endif
-        if (gi == gj) v += dadd;
-#if EVR_KMAT_DIAG == 2   // profiling builds only: no output stream (the store share)
-        if (v == -1.25) Kb[(size_t)gi * n2 + gj] = v;
-#else
-        Kb[(size_t)gi * n2 + gj] = v;
-#endif
-      }
+      const int gi = gi0 + (q >> 1) * 16 + 4 * r, gj = gj0 + (q & 1) * 16;
+      const int off = (gi < n1 && gj < n2) ? (gi * n2 + gj) * 8 : 0x7ffffff8;
+      const unsigned long long u = __double_as_longlong(vals[q][r]);
+      const __attribute__((ext_vector_type(2))) unsigned int v2 = {(unsigned)u, (unsigned)(u >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(v2, rsrc, off, 0, 0);
     }
-  // (LDS-staged row-segment epilogues, with and without non-temporal or 16-byte stores, were
-  // measured slower at config 5 and removed in round 6: profiles/r05/p/kmat_epi*.json)
+}
+
+template <int DP>
+struct KmatOps {
+  static constexpr int RS = 256 / DP, NE = KT / RS;
+  double v[NE], w[NE];
+  __device__ __forceinline__ void load(const double* X1, const double* X2, int n1, int n2, int d, int i0, int j0) {
+    const int k = threadIdx.x % DP, rr = threadIdx.x / DP, kc = k < d ? k : 0;
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int r = rr + RS * t;
+      v[t] = X1[(size_t)min(i0 + r, n1 - 1) * d + kc];
+      w[t] = X2[(size_t)min(j0 + r, n2 - 1) * d + kc];
+    }
+  }
+  // the thread's column constants (one output's lengthscale, the optional shift / scale)
+  double il = 0.0, s1 = 0.0, c1 = 1.0, s2 = 0.0, c2 = 1.0;
+  __device__ __forceinline__ void consts(const double* sh1, const double* sc1, const double* sh2, const double* sc2,
+                                         const double* lsb, int d) {
+    const int k = threadIdx.x % DP, kc = k < d ? k : 0;
+    il = 1.0 / lsb[kc];
+    s1 = sh1 ? sh1[kc] : 0.0;
+    c1 = sc1 ? sc1[kc] : 1.0;
+    s2 = sh2 ? sh2[kc] : 0.0;
+    c2 = sc2 ? sc2[kc] : 1.0;
+  }
+  __device__ __forceinline__ void put(double (*As)[KT + 2], double (*Bs)[KT + 2], int n1, int n2, int d, int i0,
+                                      int j0) const {
+    const int k = threadIdx.x % DP, rr = threadIdx.x / DP;
+    const bool kin = k < d;
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int r = rr + RS * t;
+      As[k][r] = (kin && i0 + r < n1) ? (v[t] - s1) * c1 * il : 0.0;
+      Bs[k][r] = (kin && j0 + r < n2) ? (w[t] - s2) * c2 * il : 0.0;
+    }
+  }
+};
+
+template <int DP, int KIND>
+__global__ __launch_bounds__(256, 2) void kmat_mfma_pers(int n1, int n2, int d, const double* __restrict__ X1,
+                                                      const double* __restrict__ sh1, const double* __restrict__ sc1,
+                                                      const double* __restrict__ X2, const double* __restrict__ sh2,
+                                                      const double* __restrict__ sc2, const double* __restrict__ ls,
+                                                      const double* __restrict__ os, const double* __restrict__ dg,
+                                                      double* __restrict__ K) {
+  static_assert(256 % DP == 0, "persistent kernel-matrix staging needs DP | 256");
+  constexpr int OPS = 2 * DP * (KT + 2);
+  __shared__ double smem[OPS];
+  double (*As)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem);
+  double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
+  __shared__ double na[KT], nb2[KT];
+  __shared__ int eqr[KT];
+  __shared__ double kexp[64];
+  const int gx = (n2 + KT - 1) / KT, gy = (n1 + KT - 1) / KT, ntiles = gx * gy;   // one output
+  // gridDim.x is a multiple of 8: workgroup w runs on XCD w % 8 and takes every (nwg / 8)-th
+  // tile of that XCD's contiguous run
+  const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3;
+  const int t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
+  int t = (int)((long long)ntiles * xcd / 8) + (int)(blockIdx.x >> 3);
+  if (t >= t_hi) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int i = lane & 15, kq = lane >> 4;
+  kexp_stage(kexp, tid, 256);
+  auto decode = [&](int tt, int& i0, int& j0) {
+    i0 = (tt / gx) * KT;
+    j0 = (tt - (tt / gx) * gx) * KT;
+  };
+  KmatOps<DP> R;
+  R.consts(sh1, sc1, sh2, sc2, ls, d);
+  int i0, j0;
+  decode(t, i0, j0);
+  R.load(X1, X2, n1, n2, d, i0, j0);
+  const double scale = os ? os[0] : 1.0, dadd = dg ? dg[0] : 0.0;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(K, 0, n1 * n2 * 8, 0x00020000);
+  // one tile: stage the prefetched operands, issue the next tile's loads, norms, MFMA,
+  // kernel values, stores.  Called once before the loop and then in it, so every entry to
+  // the loop body has the same memory-counter state (loads of the tile, then the previous
+  // tile's stores outstanding) and the staging waits for those loads only.
+  auto step = [&](int i0c, int j0c, int tn) {
+    __syncthreads();   // the previous tile's MFMA / epilogue reads of As, Bs, na, nb2, eqr are done
+    R.put(As, Bs, n1, n2, d, i0c, j0c);
+    __syncthreads();
+    if (tn < t_hi) {   // uniform: the next tile's loads go out ahead of this tile's stores
+      int i0n, j0n;
+      decode(tn, i0n, j0n);
+      R.load(X1, X2, n1, n2, d, i0n, j0n);
+    }
+    kmat_norms<DP>(As, Bs, na, nb2, eqr, i0c == j0c);
+    kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int kk = 0; kk < DP; kk += 4) {
+      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
+      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
+      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
+    }
+    __syncthreads();   // na / nb2 / eqr
+    double vals[4][4];
+    kmat_epilogue<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0c == j0c, scale, dadd, vals);
+    kmat_store_buf(rsrc, n1, n2, i0c, j0c, wm, wn, vals);
+  };
+  step(i0, j0, t + nslot);
+  for (t += nslot; t < t_hi; t += nslot) {
+    decode(t, i0, j0);
+    step(i0, j0, t + nslot);
+  }
 }
 
 // Symmetric train matrix K(X, X) (the GP fit's case: both operands the same rows with the same
@@ -284,62 +541,10 @@ __global__ __launch_bounds__(256) void kmat_mfma_sym(int n, int d, int B, const 
   const int i0 = I * KT, j0 = J * KT;
   const double* lsb = ls + (size_t)b * d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NE = (KT * DP + 255) / 256;
-  double v[NE], w[NE];
-#pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int e = tid + 256 * q;
-    const int r = e / DP, k = e - r * DP;
-    v[q] = 0.0;
-    w[q] = 0.0;
-    if (e < KT * DP && k < d) {
-      if (i0 + r < n) v[q] = X[(size_t)(i0 + r) * d + k];
-      if (j0 + r < n) w[q] = X[(size_t)(j0 + r) * d + k];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int e = tid + 256 * q;
-    const int r = e / DP, k = e - r * DP;
-    if (e < KT * DP) {
-      double a = 0.0, c = 0.0;
-      if (k < d) {
-        const double il = 1.0 / lsb[k];
-        if (i0 + r < n) {
-          a = v[q];
-          if (sh) a -= sh[k];
-          if (sc) a *= sc[k];
-          a *= il;
-        }
-        if (j0 + r < n) {
-          c = w[q];
-          if (sh) c -= sh[k];
-          if (sc) c *= sc[k];
-          c *= il;
-        }
-      }
-      As[k][r] = a;
-      Bs[k][r] = c;
-    }
-  }
+  kmat_stage<DP>(As, Bs, X, sh, sc, X, sh, sc, lsb, n, n, d, i0, j0);
   kexp_stage(kexp, tid, 256);
   __syncthreads();
-  if (tid < 2 * KT) {
-    const int r = tid & (KT - 1);
-    double sq = 0.0;
-    if (tid < KT) {
-      int eq = 1;
-      for (int k = 0; k < DP; ++k) {
-        sq = fma(As[k][r], As[k][r], sq);
-        eq &= As[k][r] == Bs[k][r];
-      }
-      na[r] = sq;
-      eqr[r] = eq;
-    } else {
-      for (int k = 0; k < DP; ++k) sq = fma(Bs[k][r], Bs[k][r], sq);
-      nb2[r] = sq;
-    }
-  }
+  kmat_norms<DP>(As, Bs, na, nb2, eqr, I == J);
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int i = lane & 15, kq = lane >> 4;
   kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -357,26 +562,14 @@ __global__ __launch_bounds__(256) void kmat_mfma_sym(int n, int d, int B, const 
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n * n;
   const int col = lane & 15, rq = lane >> 4;
-  double vals[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-      const int gi = i0 + li, gj = j0 + lj;
-      double d2 = fmax(na[li] + nb2[lj] - 2.0 * acc[q][r], 0.0);
-      if (gi == gj && eqr[li]) d2 = 0.0;
-      double val = scale * kernel_value_t(KIND, d2, kexp);
-      if (gi == gj) val += dadd;
-      vals[4 * q + r] = val;
-      if (gi < n && gj < n) Kb[(size_t)gi * n + gj] = val;
-    }
+  double vals[4][4];
+  kmat_epilogue_stream<KIND>(acc, na, nb2, eqr, kexp, wm, wn, I == J, scale, dadd, Kb, n, n, i0, j0, vals);
   if (I == J) return;
   double (*T)[KT + 1] = reinterpret_cast<double (*)[KT + 1]>(smem);
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[4 * q + r];
+    for (int r = 0; r < 4; ++r) T[wm + (q >> 1) * 16 + rq + 4 * r][wn + (q & 1) * 16 + col] = vals[q][r];
   __syncthreads();
   const int gc = i0 + lane;   // column of the transposed tile
 #pragma unroll 4
@@ -957,6 +1150,11 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
 }  // extern "C"
 
 namespace evr {
+// workgroups per CU of the persistent kernel-matrix form (0: one-shot grid); A/B switch
+static int kmat_pers_wpc() {
+  const char* e = std::getenv("EVR_KMAT_WPC");
+  return e ? std::atoi(e) : 0;
+}
 // evr_kernel_matrix with the host-driven chain's copies (the evaluation's sequence number and
 // the candidates to device memory): the VALU kernel (d < 16, one output family) only
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
@@ -1009,6 +1207,25 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
     }
     // (a persistent pipelined form, n workgroups per CU walking the tiles, measured slower at
     // config 5 — 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — and removed in round 6)
+    const long long ntiles = (long long)grid.x * grid.y * B;
+    const int wpc = kmat_pers_wpc();
+    if (wpc > 0 && B == 1 && d != 48 && ntiles >= 256LL * wpc && (long long)n1 * n2 * 8 < (1LL << 31) - 8) {
+      const unsigned nwg = 256u * wpc;
+#define KPK(DP_, K_) kmat_mfma_pers<DP_, K_><<<nwg, 256, 0, s>>>(n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
+                                                                  lengthscales, outputscale, diag_add, K)
+#define KP(DP_)                                  \
+  if (kind == RBF) KPK(DP_, RBF);                \
+  else if (kind == MATERN05) KPK(DP_, MATERN05); \
+  else if (kind == MATERN15) KPK(DP_, MATERN15); \
+  else KPK(DP_, MATERN25)
+      if (d <= 16) { KP(16); }
+      else if (d <= 32) { KP(32); }
+      else { KP(64); }
+#undef KP
+#undef KPK
+      EVR_LAUNCH_CHECK();
+      return 0;
+    }
 #define KMK(DP_, K_)                                                                                      \
   kmat_mfma_kernel<DP_, K_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
                                                  lengthscales, outputscale, diag_add, K)

@@ -155,6 +155,39 @@ def test_kernel_matrix_wide_mfma(d, kind):
         assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
 
 
+@pytest.mark.parametrize("n1,n2,d,kind", [(2048, 2048, 32, 3), (1100, 1900, 16, 0), (1500, 1600, 64, 1),
+                                          (2048, 2048, 32, 2)])
+def test_kernel_matrix_persistent_equals_one_shot(n1, n2, d, kind, monkeypatch):
+    """The persistent kernel-matrix form (one output, >= 512 tiles: config 5's cross matrix;
+    next tile's operand loads ahead of the stores, buffer stores with out-of-range entries
+    dropped by the descriptor) against the one-shot grid (EVR_KMAT_WPC=0): bitwise equal, ragged
+    edges included; the diagonal of an X-with-itself call (diag_add) exactly k(0) + noise."""
+    from everest_amd import ops
+
+    rng = np.random.default_rng(n1 + d)
+    X1 = torch.tensor(rng.uniform(0, 2, size=(n1, d)), device="cuda")
+    X2 = torch.tensor(rng.uniform(0, 2, size=(n2, d)), device="cuda")
+    X2[: min(n1, n2) // 3] = X1[: min(n1, n2) // 3]          # identical rows on the diagonal tiles
+    ls = torch.tensor(rng.uniform(0.5, 2.0, size=(1, d)), device="cuda")
+    noise = torch.tensor([1e-3], device="cuda", dtype=torch.float64)
+    sh = torch.zeros(d, dtype=torch.float64, device="cuda")
+    sc = torch.full((d,), 0.5, dtype=torch.float64, device="cuda")
+    out = {}
+    for wpc in ("2", "0"):   # persistent (opt-in), one-shot (default)
+        monkeypatch.setenv("EVR_KMAT_WPC", wpc)
+        buf = torch.full((n1 * n2 + 4096,), -7.0, dtype=torch.float64, device="cuda")   # sentinel tail
+        ops.call("evr_kernel_matrix", ops._stream(), kind, 1, n1, n2, d, X1.data_ptr(), sh.data_ptr(), sc.data_ptr(),
+                 X2.data_ptr(), sh.data_ptr(), sc.data_ptr(), ls.data_ptr(), 0, noise.data_ptr(), buf.data_ptr())
+        buf = buf.cpu()
+        assert (buf[n1 * n2:] == -7.0).all(), wpc       # nothing written past the matrix
+        out[wpc] = buf[: n1 * n2].view(1, n1, n2)
+    assert torch.equal(out["2"], out["0"])
+    k0 = {0: 1.0, 1: float(np.exp(-1e-15)), 2: None, 3: None}[kind]
+    diag = torch.diagonal(out["2"][0])[: min(n1, n2) // 3]
+    if k0 is not None:
+        assert torch.allclose(diag, torch.full_like(diag, k0 + 1e-3), rtol=0, atol=2.0 ** -49)
+
+
 @pytest.mark.parametrize("n,d,kind,norm", [(300, 16, 0, True), (300, 32, 3, False), (130, 64, 2, True),
                                            (2048, 32, 3, False), (65, 40, 1, True)])
 def test_kernel_matrix_symmetric_tiles_bitwise(n, d, kind, norm):

@@ -14,6 +14,11 @@
 #   hostprof    tools/ask_host_profile.py (cProfile of 5 warm asks)
 #   benchq      python bench.py --no-cpu-baseline --no-eval-pass (the ask line only)
 #   benche      python bench.py --no-cpu-baseline --no-config1 (ask line + evaluation pass + qLog)
+#   kmatab      bench_kmat.py with the shipped library and everest_amd/_lib_ab, twice interleaved
+#   kmatprof    bench_kmat.py with EVR_KMAT_PROF builds in everest_amd/_libkm{1,2,3} (1: no kernel evaluation,
+#               2: no stores, 3: neither) beside the shipped library
+#   kmatsq      two SQ counter passes over bench_kmat.py's MFMA kernel-matrix launches (KMAT_CASES)
+#   kmatwpc     bench_kmat.py at EVR_KMAT_WPC = 0 (one-shot grid) / 1 / 2 / 4 (persistent, workgroups per CU)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
 #               ask's optimised restart candidates) -> <tag>/hbm_traffic.json (keys op@b20)
@@ -69,6 +74,23 @@ for st in "$@"; do
     benchq) run benchq 600 python bench.py --no-cpu-baseline --no-eval-pass ;;
     benche) run benche 600 python bench.py --no-cpu-baseline --no-config1 ;;
     kmat) KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6,fit_train_n512 run kmat 300 python tools/bench_kmat.py && cp "$OUT/kmat.log" "$OUT/kmat.json" ;;
+    kmatab)
+      for i in 1 2; do
+        KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6 run kmat_new_$i 300 python tools/bench_kmat.py
+        EVR_LIB_PATH=everest_amd/_lib_ab/libeverest_amd.so KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6 run kmat_ab_$i 300 python tools/bench_kmat.py
+      done ;;
+    kmatprof)
+      for k in 0 1 2 3; do
+        lib=everest_amd/_lib/libeverest_amd.so; [ $k -gt 0 ] && lib=everest_amd/_libkm$k/libeverest_amd.so
+        EVR_LIB_PATH=$lib KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym run kmat_prof$k 300 python tools/bench_kmat.py
+      done ;;
+    kmatsq)
+      run kmatsq_a 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_a" -o run --output-format csv -- python tools/bench_kmat.py
+      run kmatsq_b 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_b" -o run --output-format csv -- python tools/bench_kmat.py ;;
+    kmatwpc)
+      for w in 0 1 2 4; do
+        EVR_KMAT_WPC=$w KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym run kmat_wpc$w 300 python tools/bench_kmat.py
+      done ;;
     sharded) run sharded 600 python tools/sharded_ask_check.py --ranks 2 --asks 3 --out "$OUT/sharded" ;;
     pmc20)
       cp profiles/hbm_traffic.json "$OUT/hbm_traffic.json"
