@@ -345,9 +345,17 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   const int i0 = by * KT, j0 = bx * KT;
   const double* lsb = ls + (size_t)b * d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 16)   // profiling builds only: the grid's dispatch alone
+  if (lsb[tid & 31] == -1.25) K[0] = 0.0;
+  return;
+#endif
   kmat_stage<DP>(As, Bs, X1, sh1, sc1, X2, sh2, sc2, lsb, n1, n2, d, i0, j0);
   kexp_stage(kexp, tid, 256);
   __syncthreads();
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 4)   // profiling builds only: staging alone
+  if (As[tid & 31][tid >> 5] == -1.25) K[0] = Bs[0][0];
+  return;
+#endif
   kmat_norms<DP>(As, Bs, na, nb2, eqr, i0 == j0);
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int i = lane & 15, kq = lane >> 4;
@@ -362,6 +370,10 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
     acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
   }
   __syncthreads();   // na / nb2
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 8)   // profiling builds only: staging, norms, MFMA
+  if (acc[0][0] + acc[3][3] + na[lane] == -1.25) K[0] = acc[1][1] + acc[2][2];
+  return;
+#endif
   const double scale = os ? os[b] : 1.0;
   const double dadd = dg ? dg[b] : 0.0;
   double* Kb = K + (size_t)b * n1 * n2;
@@ -372,144 +384,6 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   kmat_epilogue_stream<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0 == j0, scale, dadd, Kb, n1, n2, i0, j0, vals);
   // (LDS-staged row-segment epilogues, with and without non-temporal or 16-byte stores, were
   // measured slower at config 5 and removed in round 6: profiles/r05/p/kmat_epi*.json)
-}
-
-// Persistent form of kmat_mfma_kernel (DP | 256): a grid of a few workgroups per CU walks the
-// tiles, each XCD a contiguous run of them (operand panels shared in its L2).  The next tile's
-// operand loads are issued before this tile's epilogue and stores: gfx9's vmcnt retires loads
-// and stores in issue order, so loads issued after the stores would wait for them, while loads
-// issued before let the stores drain under the next tile's staging, MFMA and kernel
-// evaluation.  (The one-shot grid runs every phase chip-wide in lock step — operand loads,
-// then VALU, then a 33.5 MB store burst at config 5 — nothing overlapped.)  Values bitwise
-// those of kmat_mfma_kernel.
-// the tile's values to K through a buffer descriptor: entries outside n1 x n2 take an offset
-// past the descriptor's range, which the hardware drops — every store is issued on every path
-// (no exec-mask branch around a store: the persistent kernel's memory-counter waits assume
-// the 16 stores are always behind the next tile's loads).  n1 n2 8 < 2^31.
-__device__ __forceinline__ void kmat_store_buf(__amdgpu_buffer_rsrc_t rsrc, int n1, int n2, int i0, int j0, int wm,
-                                               int wn, const double (&vals)[4][4]) {
-  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
-  const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gi = gi0 + (q >> 1) * 16 + 4 * r, gj = gj0 + (q & 1) * 16;
-      const int off = (gi < n1 && gj < n2) ? (gi * n2 + gj) * 8 : 0x7ffffff8;
-      const unsigned long long u = __double_as_longlong(vals[q][r]);
-      const __attribute__((ext_vector_type(2))) unsigned int v2 = {(unsigned)u, (unsigned)(u >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b64(v2, rsrc, off, 0, 0);
-    }
-}
-
-template <int DP>
-struct KmatOps {
-  static constexpr int RS = 256 / DP, NE = KT / RS;
-  double v[NE], w[NE];
-  __device__ __forceinline__ void load(const double* X1, const double* X2, int n1, int n2, int d, int i0, int j0) {
-    const int k = threadIdx.x % DP, rr = threadIdx.x / DP, kc = k < d ? k : 0;
-#pragma unroll
-    for (int t = 0; t < NE; ++t) {
-      const int r = rr + RS * t;
-      v[t] = X1[(size_t)min(i0 + r, n1 - 1) * d + kc];
-      w[t] = X2[(size_t)min(j0 + r, n2 - 1) * d + kc];
-    }
-  }
-  // the thread's column constants (one output's lengthscale, the optional shift / scale)
-  double il = 0.0, s1 = 0.0, c1 = 1.0, s2 = 0.0, c2 = 1.0;
-  __device__ __forceinline__ void consts(const double* sh1, const double* sc1, const double* sh2, const double* sc2,
-                                         const double* lsb, int d) {
-    const int k = threadIdx.x % DP, kc = k < d ? k : 0;
-    il = 1.0 / lsb[kc];
-    s1 = sh1 ? sh1[kc] : 0.0;
-    c1 = sc1 ? sc1[kc] : 1.0;
-    s2 = sh2 ? sh2[kc] : 0.0;
-    c2 = sc2 ? sc2[kc] : 1.0;
-  }
-  __device__ __forceinline__ void put(double (*As)[KT + 2], double (*Bs)[KT + 2], int n1, int n2, int d, int i0,
-                                      int j0) const {
-    const int k = threadIdx.x % DP, rr = threadIdx.x / DP;
-    const bool kin = k < d;
-#pragma unroll
-    for (int t = 0; t < NE; ++t) {
-      const int r = rr + RS * t;
-      As[k][r] = (kin && i0 + r < n1) ? (v[t] - s1) * c1 * il : 0.0;
-      Bs[k][r] = (kin && j0 + r < n2) ? (w[t] - s2) * c2 * il : 0.0;
-    }
-  }
-};
-
-template <int DP, int KIND>
-__global__ __launch_bounds__(256, 2) void kmat_mfma_pers(int n1, int n2, int d, const double* __restrict__ X1,
-                                                      const double* __restrict__ sh1, const double* __restrict__ sc1,
-                                                      const double* __restrict__ X2, const double* __restrict__ sh2,
-                                                      const double* __restrict__ sc2, const double* __restrict__ ls,
-                                                      const double* __restrict__ os, const double* __restrict__ dg,
-                                                      double* __restrict__ K) {
-  static_assert(256 % DP == 0, "persistent kernel-matrix staging needs DP | 256");
-  constexpr int OPS = 2 * DP * (KT + 2);
-  __shared__ double smem[OPS];
-  double (*As)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem);
-  double (*Bs)[KT + 2] = reinterpret_cast<double (*)[KT + 2]>(smem + DP * (KT + 2));
-  __shared__ double na[KT], nb2[KT];
-  __shared__ int eqr[KT];
-  __shared__ double kexp[64];
-  const int gx = (n2 + KT - 1) / KT, gy = (n1 + KT - 1) / KT, ntiles = gx * gy;   // one output
-  // gridDim.x is a multiple of 8: workgroup w runs on XCD w % 8 and takes every (nwg / 8)-th
-  // tile of that XCD's contiguous run
-  const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3;
-  const int t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
-  int t = (int)((long long)ntiles * xcd / 8) + (int)(blockIdx.x >> 3);
-  if (t >= t_hi) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const int i = lane & 15, kq = lane >> 4;
-  kexp_stage(kexp, tid, 256);
-  auto decode = [&](int tt, int& i0, int& j0) {
-    i0 = (tt / gx) * KT;
-    j0 = (tt - (tt / gx) * gx) * KT;
-  };
-  KmatOps<DP> R;
-  R.consts(sh1, sc1, sh2, sc2, ls, d);
-  int i0, j0;
-  decode(t, i0, j0);
-  R.load(X1, X2, n1, n2, d, i0, j0);
-  const double scale = os ? os[0] : 1.0, dadd = dg ? dg[0] : 0.0;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(K, 0, n1 * n2 * 8, 0x00020000);
-  // one tile: stage the prefetched operands, issue the next tile's loads, norms, MFMA,
-  // kernel values, stores.  Called once before the loop and then in it, so every entry to
-  // the loop body has the same memory-counter state (loads of the tile, then the previous
-  // tile's stores outstanding) and the staging waits for those loads only.
-  auto step = [&](int i0c, int j0c, int tn) {
-    __syncthreads();   // the previous tile's MFMA / epilogue reads of As, Bs, na, nb2, eqr are done
-    R.put(As, Bs, n1, n2, d, i0c, j0c);
-    __syncthreads();
-    if (tn < t_hi) {   // uniform: the next tile's loads go out ahead of this tile's stores
-      int i0n, j0n;
-      decode(tn, i0n, j0n);
-      R.load(X1, X2, n1, n2, d, i0n, j0n);
-    }
-    kmat_norms<DP>(As, Bs, na, nb2, eqr, i0c == j0c);
-    kd4_t acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-    for (int kk = 0; kk < DP; kk += 4) {
-      const double a0 = As[kk + kq][wm + i], a1 = As[kk + kq][wm + 16 + i];
-      const double b0 = Bs[kk + kq][wn + i], b1 = Bs[kk + kq][wn + 16 + i];
-      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[3], 0, 0, 0);
-    }
-    __syncthreads();   // na / nb2 / eqr
-    double vals[4][4];
-    kmat_epilogue<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0c == j0c, scale, dadd, vals);
-    kmat_store_buf(rsrc, n1, n2, i0c, j0c, wm, wn, vals);
-  };
-  step(i0, j0, t + nslot);
-  for (t += nslot; t < t_hi; t += nslot) {
-    decode(t, i0, j0);
-    step(i0, j0, t + nslot);
-  }
 }
 
 // Symmetric train matrix K(X, X) (the GP fit's case: both operands the same rows with the same
@@ -1150,11 +1024,6 @@ int evr_kernel_matrix(void* stream, int kind, int B, int n1, int n2, int d, cons
 }  // extern "C"
 
 namespace evr {
-// workgroups per CU of the persistent kernel-matrix form (0: one-shot grid); A/B switch
-static int kmat_pers_wpc() {
-  const char* e = std::getenv("EVR_KMAT_WPC");
-  return e ? std::atoi(e) : 0;
-}
 // evr_kernel_matrix with the host-driven chain's copies (the evaluation's sequence number and
 // the candidates to device memory): the VALU kernel (d < 16, one output family) only
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
@@ -1205,27 +1074,10 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
       EVR_LAUNCH_CHECK();
       return 0;
     }
-    // (a persistent pipelined form, n workgroups per CU walking the tiles, measured slower at
-    // config 5 — 33.1 / 34.8 us at n = 2 / 4 vs 24.9 us one-shot — and removed in round 6)
-    const long long ntiles = (long long)grid.x * grid.y * B;
-    const int wpc = kmat_pers_wpc();
-    if (wpc > 0 && B == 1 && d != 48 && ntiles >= 256LL * wpc && (long long)n1 * n2 * 8 < (1LL << 31) - 8) {
-      const unsigned nwg = 256u * wpc;
-#define KPK(DP_, K_) kmat_mfma_pers<DP_, K_><<<nwg, 256, 0, s>>>(n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
-                                                                  lengthscales, outputscale, diag_add, K)
-#define KP(DP_)                                  \
-  if (kind == RBF) KPK(DP_, RBF);                \
-  else if (kind == MATERN05) KPK(DP_, MATERN05); \
-  else if (kind == MATERN15) KPK(DP_, MATERN15); \
-  else KPK(DP_, MATERN25)
-      if (d <= 16) { KP(16); }
-      else if (d <= 32) { KP(32); }
-      else { KP(64); }
-#undef KP
-#undef KPK
-      EVR_LAUNCH_CHECK();
-      return 0;
-    }
+    // (persistent forms — a few workgroups per CU walking the tiles; in round 6 with the next
+    // tile's operand loads issued ahead of this tile's stores and out-of-range entries dropped
+    // by a buffer descriptor — measured slower at config 5: 20.1 / 21.1 / 24.3 us at 4 / 2 / 1
+    // workgroups per CU vs 19.0 us one-shot, profiles/r06/o; removed)
 #define KMK(DP_, K_)                                                                                      \
   kmat_mfma_kernel<DP_, K_><<<grid, 256, 0, s>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, scale2, \
                                                  lengthscales, outputscale, diag_add, K)

@@ -137,6 +137,27 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(int M, int N, int batc
 // ---------------------------------------------------------------------------------------
 constexpr int TT = 64;
 
+// a 64 x 64 tile of op(L) into LDS, T[rr][cc] = op(L)[r0 + rr][c0 + cc] (zero outside n x n):
+// all 16 loads of a thread are issued before the first LDS store — the load -> store loop
+// kept one load in flight (the compiler cannot move a global load above an LDS store it may
+// alias), 16 dependent memory round trips per tile
+template <bool TRANS>
+__device__ __forceinline__ void stage_tile_tt(double (*T)[TT + 1], const double* L, int ldl, int n, int r0, int c0) {
+  double v[16];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = tid + 256 * u, rr = e >> 6, cc = e & 63;
+    const int gr = TRANS ? c0 + cc : r0 + rr, gc = TRANS ? r0 + rr : c0 + cc;
+    v[u] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = tid + 256 * u;
+    T[e >> 6][e & 63] = v[u];
+  }
+}
+
 template <bool TRANS>
 __global__ __launch_bounds__(256) void trsm_kernel(int n, int nrhs, const double* __restrict__ Lm, long long sL,
                                                    int ldl, double* __restrict__ Bm, long long sB, int ldb) {
@@ -162,20 +183,19 @@ __global__ __launch_bounds__(256) void trsm_kernel(int n, int nrhs, const double
     const int jb0 = TRANS ? bi + 1 : 0, jb1 = TRANS ? nblk : bi;
     for (int bj = jb0; bj < jb1; ++bj) {
       const int s0 = bj * TT;
-      for (int e = tid; e < TT * TT; e += 256) {
-        const int rr = e >> 6, cc = e & 63;
-        // Lt[rr][cc] = op(L)[r0+rr][s0+cc]
-        double lv = 0.0;
-        if (!TRANS) {
-          const int gr = r0 + rr, gc = s0 + cc;
-          if (gr < n && gc < n) lv = L[(size_t)gr * ldl + gc];
-        } else {
-          const int gr = s0 + cc, gc = r0 + rr;  // (L^T)[r][s] = L[s][r]
-          if (gr < n && gc < n) lv = L[(size_t)gr * ldl + gc];
+      {
+        double xv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = tid + 256 * u, xr = s0 + (e >> 6), xc = c0 + (e & 63);
+          xv[u] = (xr < n && xc < nrhs) ? B[(size_t)xr * ldb + xc] : 0.0;
         }
-        Lt[rr][cc] = lv;
-        const int xr = s0 + rr, xc = c0 + cc;
-        Xt[rr][cc] = (xr < n && xc < nrhs) ? B[(size_t)xr * ldb + xc] : 0.0;
+        stage_tile_tt<TRANS>(Lt, L, ldl, n, r0, s0);   // Lt[rr][cc] = op(L)[r0 + rr][s0 + cc]
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = tid + 256 * u;
+          Xt[e >> 6][e & 63] = xv[u];
+        }
       }
       __syncthreads();
 #pragma unroll 4
@@ -197,11 +217,7 @@ __global__ __launch_bounds__(256) void trsm_kernel(int n, int nrhs, const double
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) Xt[ty + 16 * a][tx + 16 * c] = acc[a][c];
-    for (int e = tid; e < TT * TT; e += 256) {
-      const int rr = e >> 6, cc = e & 63;
-      const int gr = r0 + rr, gc = r0 + cc;
-      Lt[rr][cc] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;  // L itself (lower)
-    }
+    stage_tile_tt<false>(Lt, L, ldl, n, r0, r0);   // L itself (lower)
     __syncthreads();
     const int rb = min(TT, n - r0);
     if (tid < TT) {
@@ -260,11 +276,7 @@ __global__ __launch_bounds__(256) void trsm16_kernel(int n, int nrhs, const doub
     for (int bj = 0; bj < bi; ++bj) {
       const int s0 = bj * TT;
       __syncthreads();   // Lt reuse
-      for (int e = tid; e < TT * TT; e += 256) {
-        const int rr = e >> 6, cc = e & 63;
-        const int gr = r0 + rr, gc = s0 + cc;
-        Lt[rr][cc] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;
-      }
+      stage_tile_tt<false>(Lt, L, ldl, n, r0, s0);
       __syncthreads();
 #pragma unroll 4
       for (int q = 0; q < TT; ++q) {
@@ -274,11 +286,7 @@ __global__ __launch_bounds__(256) void trsm16_kernel(int n, int nrhs, const doub
       }
     }
     __syncthreads();
-    for (int e = tid; e < TT * TT; e += 256) {
-      const int rr = e >> 6, cc = e & 63;
-      const int gr = r0 + rr, gc = r0 + cc;
-      Lt[rr][cc] = (gr < n && gc < n) ? L[(size_t)gr * ldl + gc] : 0.0;
-    }
+    stage_tile_tt<false>(Lt, L, ldl, n, r0, r0);
     __syncthreads();
     const int rb = min(TT, n - r0);
     const int gl = lane & ~15;

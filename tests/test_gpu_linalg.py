@@ -155,36 +155,41 @@ def test_kernel_matrix_wide_mfma(d, kind):
         assert torch.allclose(Kc[b], ref(X1, X2, b), rtol=1e-10, atol=1e-11)
 
 
-@pytest.mark.parametrize("n1,n2,d,kind", [(2048, 2048, 32, 3), (1100, 1900, 16, 0), (1500, 1600, 64, 1),
-                                          (2048, 2048, 32, 2)])
-def test_kernel_matrix_persistent_equals_one_shot(n1, n2, d, kind, monkeypatch):
-    """The persistent kernel-matrix form (one output, >= 512 tiles: config 5's cross matrix;
-    next tile's operand loads ahead of the stores, buffer stores with out-of-range entries
-    dropped by the descriptor) against the one-shot grid (EVR_KMAT_WPC=0): bitwise equal, ragged
-    edges included; the diagonal of an X-with-itself call (diag_add) exactly k(0) + noise."""
+@pytest.mark.parametrize("n1,n2,d,kind", [(2048, 2048, 32, 3), (1100, 1900, 16, 0), (1030, 1090, 64, 1),
+                                          (257, 1031, 32, 2)])
+def test_kernel_matrix_wide_ragged_and_bounded(n1, n2, d, kind):
+    """The matrix-core kernel-matrix kernel (d >= 16) at config 5's shape and ragged edges,
+    called through the C-ABI into a buffer with a sentinel tail: nothing is written past the
+    n1 x n2 matrix (out-of-range tile entries are computed on zero padding and not stored),
+    every entry matches the float64 restatement, identical rows give the exact k(0) + noise."""
     from everest_amd import ops
 
     rng = np.random.default_rng(n1 + d)
-    X1 = torch.tensor(rng.uniform(0, 2, size=(n1, d)), device="cuda")
-    X2 = torch.tensor(rng.uniform(0, 2, size=(n2, d)), device="cuda")
+    X1 = rng.uniform(0, 2, size=(n1, d))
+    X2 = rng.uniform(0, 2, size=(n2, d))
     X2[: min(n1, n2) // 3] = X1[: min(n1, n2) // 3]          # identical rows on the diagonal tiles
-    ls = torch.tensor(rng.uniform(0.5, 2.0, size=(1, d)), device="cuda")
-    noise = torch.tensor([1e-3], device="cuda", dtype=torch.float64)
-    sh = torch.zeros(d, dtype=torch.float64, device="cuda")
-    sc = torch.full((d,), 0.5, dtype=torch.float64, device="cuda")
-    out = {}
-    for wpc in ("2", "0"):   # persistent (opt-in), one-shot (default)
-        monkeypatch.setenv("EVR_KMAT_WPC", wpc)
-        buf = torch.full((n1 * n2 + 4096,), -7.0, dtype=torch.float64, device="cuda")   # sentinel tail
-        ops.call("evr_kernel_matrix", ops._stream(), kind, 1, n1, n2, d, X1.data_ptr(), sh.data_ptr(), sc.data_ptr(),
-                 X2.data_ptr(), sh.data_ptr(), sc.data_ptr(), ls.data_ptr(), 0, noise.data_ptr(), buf.data_ptr())
-        buf = buf.cpu()
-        assert (buf[n1 * n2:] == -7.0).all(), wpc       # nothing written past the matrix
-        out[wpc] = buf[: n1 * n2].view(1, n1, n2)
-    assert torch.equal(out["2"], out["0"])
+    ls = rng.uniform(0.5, 2.0, size=(1, d))
+    t = lambda a: torch.tensor(a, dtype=torch.float64, device="cuda")  # noqa: E731
+    sh, sc, noise = t(np.zeros(d)), t(np.full(d, 0.5)), t([1e-3])
+    buf = torch.full((n1 * n2 + 4096,), -7.0, dtype=torch.float64, device="cuda")   # sentinel tail
+    x1, x2, lt = t(X1), t(X2), t(ls)
+    ops.call("evr_kernel_matrix", ops._stream(), kind, 1, n1, n2, d, x1.data_ptr(), sh.data_ptr(), sc.data_ptr(),
+             x2.data_ptr(), sh.data_ptr(), sc.data_ptr(), lt.data_ptr(), 0, noise.data_ptr(), buf.data_ptr())
+    buf = buf.cpu()
+    assert (buf[n1 * n2:] == -7.0).all()
+    K = buf[: n1 * n2].view(n1, n2)
+    U, V = torch.tensor(X1 * 0.5 / ls[0]), torch.tensor(X2 * 0.5 / ls[0])
+    d2 = ((U[:, None, :] - V[None, :, :]) ** 2).sum(-1)
+    r = torch.sqrt(torch.clamp(d2, min=1e-30))
+    ref = {0: lambda: torch.exp(-0.5 * d2), 1: lambda: torch.exp(-r),
+           2: lambda: (1 + 3 ** 0.5 * r) * torch.exp(-(3 ** 0.5) * r),
+           3: lambda: (1 + 5 ** 0.5 * r + 5.0 / 3.0 * d2) * torch.exp(-(5 ** 0.5) * r)}[kind]()
+    m = min(n1, n2)
+    ref[torch.arange(m), torch.arange(m)] += 1e-3
+    assert torch.allclose(K, ref, rtol=1e-10, atol=1e-11), float((K - ref).abs().max())
     k0 = {0: 1.0, 1: float(np.exp(-1e-15)), 2: None, 3: None}[kind]
-    diag = torch.diagonal(out["2"][0])[: min(n1, n2) // 3]
     if k0 is not None:
+        diag = torch.diagonal(K)[: m // 3]
         assert torch.allclose(diag, torch.full_like(diag, k0 + 1e-3), rtol=0, atol=2.0 ** -49)
 
 

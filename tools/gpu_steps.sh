@@ -16,8 +16,10 @@
 #   benche      python bench.py --no-cpu-baseline --no-config1 (ask line + evaluation pass + qLog)
 #   kmatab      bench_kmat.py with the shipped library and everest_amd/_lib_ab, twice interleaved
 #   kmatprof    bench_kmat.py with EVR_KMAT_PROF builds in everest_amd/_libkm{1,2,3} (1: no kernel evaluation,
-#               2: no stores, 3: neither) beside the shipped library
+#               2: no stores, 3: neither, 4: staging only, 8: staging + norms + MFMA; KMAT_PROFS picks) beside
+#               the shipped library
 #   kmatsq      two SQ counter passes over bench_kmat.py's MFMA kernel-matrix launches (KMAT_CASES)
+#   trsm        tools/bench_trsm.py (forward substitution at the operator's G = L_base^-1 E shape)
 #   kmatwpc     bench_kmat.py at EVR_KMAT_WPC = 0 (one-shot grid) / 1 / 2 / 4 (persistent, workgroups per CU)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
@@ -80,13 +82,14 @@ for st in "$@"; do
         EVR_LIB_PATH=everest_amd/_lib_ab/libeverest_amd.so KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym,n2048_d6 run kmat_ab_$i 300 python tools/bench_kmat.py
       done ;;
     kmatprof)
-      for k in 0 1 2 3; do
+      for k in ${KMAT_PROFS:-0 1 2 3}; do
         lib=everest_amd/_lib/libeverest_amd.so; [ $k -gt 0 ] && lib=everest_amd/_libkm$k/libeverest_amd.so
         EVR_LIB_PATH=$lib KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym run kmat_prof$k 300 python tools/bench_kmat.py
       done ;;
     kmatsq)
       run kmatsq_a 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_a" -o run --output-format csv -- python tools/bench_kmat.py
       run kmatsq_b 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_b" -o run --output-format csv -- python tools/bench_kmat.py ;;
+    trsm) run trsm 120 python tools/bench_trsm.py ;;
     kmatwpc)
       for w in 0 1 2 4; do
         EVR_KMAT_WPC=$w KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym run kmat_wpc$w 300 python tools/bench_kmat.py
