@@ -150,7 +150,11 @@ __device__ __forceinline__ void kmat_epilogue(const kd4_t (&acc)[4], const doubl
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const double d2 = fmax(fma(-2.0, acc[q][r], na[wm + (q >> 1) * 16 + rq + 4 * r] + nbv[q & 1]), 0.0);
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 1)   // profiling builds only: no kernel evaluation
+      vals[q][r] = scale * d2;
+#else
       vals[q][r] = scale * kernel_value_r(KIND, d2, kexp);
+#endif
     }
   // the diagonal entries, apart (a per-entry test in the loop above became a branch around
   // each entry's LDS read): identical points take d2 = 0, every diagonal entry gets dadd
@@ -165,63 +169,14 @@ __device__ __forceinline__ void kmat_epilogue(const kd4_t (&acc)[4], const doubl
   }
 }
 
-// kmat_epilogue + kmat_store fused per accumulator register group: the four values of
-// acc[q] are stored as soon as they are formed, so the tile's stores stream out under the
-// kernel evaluation of the next group instead of leaving in one burst after all 16 values
-// (the one-shot grid runs every workgroup in the same phase: the burst was the chip's store
-// phase).  Values bitwise those of kmat_epilogue; vals keeps them (the symmetric kernel's
-// transposed write).
-template <int KIND>
-__device__ __forceinline__ void kmat_epilogue_stream(const kd4_t (&acc)[4], const double* na, const double* nb2,
-                                                     const int* eqr, const double* kexp, int wm, int wn, bool dtile,
-                                                     double scale, double dadd, double* Kb, int n1, int n2, int i0,
-                                                     int j0, double (&vals)[4][4]) {
-#pragma clang fp contract(off)
-  const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
-  const double nbv[2] = {nb2[wn + col], nb2[wn + 16 + col]};
-  bool interior = i0 + KT <= n1 && j0 + KT <= n2;
-  const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
-  double* p0 = Kb + (size_t)min(gi0, n1 - 1) * n2 + min(gj0, n2 - 1);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double d2 = fmax(fma(-2.0, acc[q][r], na[wm + (q >> 1) * 16 + rq + 4 * r] + nbv[q & 1]), 0.0);
-#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 1)   // profiling builds only: no kernel evaluation
-      vals[q][r] = scale * d2;
-#else
-      vals[q][r] = scale * kernel_value_r(KIND, d2, kexp);
-#endif
-    }
-    if (dtile) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int li = wm + (q >> 1) * 16 + rq + 4 * r, lj = wn + (q & 1) * 16 + col;
-        if (li == lj) vals[q][r] = (eqr[li] ? scale * kernel_value_r(KIND, 0.0, kexp) : vals[q][r]) + dadd;
-      }
-    }
-#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 2)   // profiling builds only: no output stream
-    if (vals[q][0] == -1.25) interior = false;
-    if (vals[q][1] != -1.25) continue;
-#endif
-    if (interior) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) p0[(size_t)((q >> 1) * 16 + 4 * r) * n2 + (q & 1) * 16] = vals[q][r];
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = gi0 + (q >> 1) * 16 + 4 * r, gj = gj0 + (q & 1) * 16;
-        if (gi < n1 && gj < n2) Kb[(size_t)gi * n2 + gj] = vals[q][r];
-      }
-    }
-  }
-}
-
 // the tile's values to K (n1 x n2, row-major): interior tiles without per-entry guards
 __device__ __forceinline__ void kmat_store(double* Kb, int n1, int n2, int i0, int j0, int wm, int wn,
                                            const double (&vals)[4][4]) {
   const int lane = threadIdx.x & 63, col = lane & 15, rq = lane >> 4;
   const int gi0 = i0 + wm + rq, gj0 = j0 + wn + col;
+#if defined(EVR_KMAT_PROF) && (EVR_KMAT_PROF & 2)   // profiling builds only: no output stream
+  if (vals[0][0] != -1.25) return;
+#endif
   if (i0 + KT <= n1 && j0 + KT <= n2) {
     double* p = Kb + (size_t)gi0 * n2 + gj0;
 #pragma unroll
@@ -381,7 +336,8 @@ __global__ __launch_bounds__(256) void kmat_mfma_kernel(int kind, int n1, int n2
   // kernel evaluation serialised the 16 entries' dependent chains (SQ: ~90 VALU + 39 SALU per
   // entry, round 5); out-of-range entries compute on the zero padding and are not stored
   double vals[4][4];
-  kmat_epilogue_stream<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0 == j0, scale, dadd, Kb, n1, n2, i0, j0, vals);
+  kmat_epilogue<KIND>(acc, na, nb2, eqr, kexp, wm, wn, i0 == j0, scale, dadd, vals);
+  kmat_store(Kb, n1, n2, i0, j0, wm, wn, vals);
   // (LDS-staged row-segment epilogues, with and without non-temporal or 16-byte stores, were
   // measured slower at config 5 and removed in round 6: profiles/r05/p/kmat_epi*.json)
 }
@@ -437,7 +393,8 @@ __global__ __launch_bounds__(256) void kmat_mfma_sym(int n, int d, int B, const 
   double* Kb = K + (size_t)b * n * n;
   const int col = lane & 15, rq = lane >> 4;
   double vals[4][4];
-  kmat_epilogue_stream<KIND>(acc, na, nb2, eqr, kexp, wm, wn, I == J, scale, dadd, Kb, n, n, i0, j0, vals);
+  kmat_epilogue<KIND>(acc, na, nb2, eqr, kexp, wm, wn, I == J, scale, dadd, vals);
+  kmat_store(Kb, n, n, i0, j0, wm, wn, vals);
   if (I == J) return;
   double (*T)[KT + 1] = reinterpret_cast<double (*)[KT + 1]>(smem);
 #pragma unroll

@@ -1,7 +1,7 @@
 """Kernel-matrix assembly bandwidth: the eval-chain cross-covariance (config 3: B=5 outputs,
 512 train rows x b candidates, d=6, RBF), the GP-fit train matrix, and config 5 (2048 x 2048,
 d=32, Matern-2.5), each against a plain device fill of the same output (the write-bandwidth
-ceiling).  Output preallocated; EVR_KMAT / EVR_KMAT_RPT select the variant."""
+ceiling).  Output preallocated; HIP-graph replay between HIP events."""
 import json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -9,22 +9,30 @@ from everest_amd import ops
 from everest_amd.ops import call, _stream, _p
 
 
-def ev(fn, reps=50):
-    for _ in range(5):
+def ev(fn, reps=20, per_graph=10):
+    """ms per call: per_graph calls captured into one HIP graph, the graph replayed reps times
+    between HIP events (no host enqueue in the timed region: a ctypes call per launch is
+    ~7 us of host time, a floor above the short kernels)."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        fn()
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / (reps * per_graph)
 
 
 torch.manual_seed(0)
-out = {"variant": os.environ.get("EVR_KMAT", "rows"), "rpt": os.environ.get("EVR_KMAT_RPT", "4"),
-       "exp": os.environ.get("EVR_KMAT_EXP", "fast")}
+out = {"lib": os.environ.get("EVR_LIB_PATH", "everest_amd/_lib"), "timing": "hip-graph replay"}
 cases = (("cfg3_cross_b512", 5, 512, 512, 6, 0), ("cfg3_cross_b20", 5, 512, 20, 6, 0),
          ("fit_train_n512", 1, 512, 512, 6, 0), ("cfg2_cross", 1, 256, 1024, 6, 0),
          ("cfg5_n2048_d32", 1, 2048, 2048, 32, 3), ("cfg5_train_sym", 1, 2048, 2048, 32, 3),
