@@ -94,7 +94,10 @@ __global__ __launch_bounds__(256, 4) void qn_proj_fwd(int n, int nb, int Rr, int
   const int m0 = by * C::BM, n0 = bx * C::BN;
   const double* A = Mm + (size_t)j * Rr * n;
   const double* B = Kx + (size_t)j * n * b;
-  const int kbeg = kz * kchunk, kend = min(n, kbeg + kchunk);
+  // split root (nb > 0): rows r < n of M are L^-1's, lower triangular, so a row tile below n
+  // contracts over k < m0 + BM only (the skipped k-steps are exact zeros, whole 16-steps at
+  // the same chain positions: bitwise unchanged)
+  const int kend = min(nb > 0 && m0 + C::BM <= n ? m0 + C::BM : n, kz * kchunk + kchunk), kbeg = kz * kchunk;
   dg_double4 acc[C::FM][C::FN];
   dg_mainloop<C>(
       lds, kbeg, kend,
@@ -280,7 +283,9 @@ __global__ __launch_bounds__(256, 4) void qn_proj_bwd(int n, int nb, int nh, int
   // class segments of this slice: [lo, hi) of rows < n, [n, n + nb), the sample rows
   dg_double4 a0[C::FM][C::FN], a1[C::FM][C::FN], a2[C::FM][C::FN];
   {
-    const int lo = kbeg, hi = min(kend, n);
+    // split root: M[k][i] = L^-1[k][i] = 0 for k < i, so output rows i >= m0 start at k = m0
+    // (m0 a multiple of the 16-deep k-step: the same chain positions, bitwise unchanged)
+    const int lo = nb > 0 ? max(kbeg, m0) : kbeg, hi = min(kend, n);
     dg_mainloop<C>(lds, lo, hi, fa, [&](int k, int c) -> dg_double2 {
       return dg_pair<VEC>(Rj + (size_t)k * b + n0 + c, k < hi && n0 + c < b, k < hi && n0 + c + 1 < b);
     }, a0);
