@@ -176,6 +176,8 @@ Lbfgsb::Lbfgsb(int n, int m, const double* lb, const double* ub, double factr, d
   wy_.assign((size_t)n * m, 0.0);
   sy_.assign((size_t)m * m, 0.0);
   ss_.assign((size_t)m * m, 0.0);
+  pcol_.assign(m, 0);
+  refresh_pcol();
 }
 
 void Lbfgsb::reset_memory() {
@@ -184,6 +186,7 @@ void Lbfgsb::reset_memory() {
   theta_ = 1.0;
   iupdat_ = 0;
   minv_ok_ = false;
+  refresh_pcol();
 }
 
 // [active] project the initial point, classify the variables.
@@ -662,6 +665,7 @@ void Lbfgsb::update_memory(double rr, double dr, double stp) {
   } else {
     itail = (head_ + m_) % m_;   // overwrite the oldest column, advance the head
     head_ = (head_ + 1) % m_;
+    refresh_pcol();
   }
   std::copy(d_.begin(), d_.end(), ws_.begin() + (size_t)itail * n_);
   std::copy(r_.begin(), r_.end(), wy_.begin() + (size_t)itail * n_);

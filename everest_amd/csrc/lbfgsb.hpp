@@ -86,7 +86,13 @@ class Lbfgsb {
   int ls_continue();
   void dcsrch(double f, double g, double& stp, double ftol, double gtol, double xtol, double stpmin, double stpmax);
   void update_memory(double rr, double dr, double stp);
-  int col_index(int k) const { return (head_ + k) % m_; }
+  // storage slot of the k-th stored pair (oldest first); a table refreshed when head_ moves
+  // (the modulo in every inner loop of the Cauchy / subspace steps was a division per term)
+  std::vector<int> pcol_;
+  void refresh_pcol() {
+    for (int k = 0; k < m_; ++k) pcol_[k] = (head_ + k) % m_;
+  }
+  int col_index(int k) const { return pcol_[k]; }
 };
 
 }  // namespace evr
