@@ -399,171 +399,15 @@ __device__ __forceinline__ double quad_bcast_f64(double v, int s) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// lane l of the lane's 16-lane DPP row, as an f64 (v_mov_b64 with DPP row_newbcast: gfx90a+
-// 64-bit DPP); l is a compile-time constant after unrolling, so the switch folds
-__device__ __forceinline__ double row_bcast_f64(double v, int l) {
-#define EVR_RB(L_) \
-  case L_: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L_, 0xf, 0xf, false);
-  switch (l) {
-    EVR_RB(0) EVR_RB(1) EVR_RB(2) EVR_RB(3) EVR_RB(4) EVR_RB(5) EVR_RB(6) EVR_RB(7)
-    EVR_RB(8) EVR_RB(9) EVR_RB(10) EVR_RB(11) EVR_RB(12) EVR_RB(13) EVR_RB(14)
-    default: return __builtin_amdgcn_update_dpp(0.0, v, 0x15F, 0xf, 0xf, false);
-  }
-#undef EVR_RB
-}
 
 // one wave: factor A[c0.., c0..] (16x16, lower) in place; inverse into X[c0.., c0..].
-#if defined(EVR_LEAF_DPP)
-// Row-per-lane leaf (EVR_LEAF_DPP build, A/B only: measured slower — 40.0 k vs 32.8 k cycles for
-// the four leaves of a 64-column factor, tools/chol_prof.hip — the 64-bit DPP moves and the
-// 16-wide unrolled row updates cost more issue slots than the paired bpermute exchange saves): lane r of every 16-lane DPP row holds row r of A (16 values)
-// and of the inverse accumulator E; the wave's four DPP rows compute the same thing.  Step j
-// needs the pivot A[j][j], the column entries A[c][j] (c > j) and the finished inverse row
-// E[j][.] — each is one register of one lane of the row, delivered by a DPP row_newbcast move
-// straight from that lane's register: no LDS, no ds_bpermute round trip, no readlane.  The
-// arithmetic is the one-pivot loop's (m = A[r][j] ip, fma(-m, A[c][j], A[r][c]),
-// fma(-m, E[j][c], E[r][c]); ip = rcp + 2 Newton steps; final A / sqrt(pivot)), so the
-// results are bitwise those of the bpermute leaves.  The pivots stay in registers.
-__device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
-                                              double* erow, double* piv) {
-  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  double a[CP], e[CP], pv[CP];
-#pragma unroll
-  for (int c = 0; c < CP; ++c) {
-    a[c] = (c <= r) ? A[c0 + r][c0 + c] : 0.0;
-    e[c] = (c == r) ? 1.0 : 0.0;
-  }
-  int bad = -1;
-#pragma unroll
-  for (int j = 0; j < CP; ++j) {
-    const double p = row_bcast_f64(a[j], j);   // A[j][j]
-    pv[j] = p;
-    if (bad < 0 && !(p > 0.0)) bad = j;
-    double ip = __builtin_amdgcn_rcp(p);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    const double m = a[j] * ip;   // A[r][j] / A[j][j]
-    const bool below = r > j;
-#pragma unroll
-    for (int c = j + 1; c < CP; ++c) {
-      const double col = row_bcast_f64(a[j], c);   // A[c][j]
-      const double dn = fma(-m, col, a[c]);
-      a[c] = (below && c <= r) ? dn : a[c];
-    }
-#pragma unroll
-    for (int c = 0; c <= j; ++c) {
-      const double er = row_bcast_f64(e[c], j);    // E[j][c] (final)
-      const double en = fma(-m, er, e[c]);
-      e[c] = below ? en : e[c];
-    }
-  }
-  (void)colj;
-  (void)erow;
-  (void)piv;
-  if (bad >= 0) return bad;
-  // group g stores columns g, g + 4, ...
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = g + 4 * k;
-    double av = 0.0, xv = 0.0, pc = pv[0], pr = pv[0];
-#pragma unroll
-    for (int t = 0; t < CP; ++t) {   // register-indexed selects (no dynamic private array)
-      if (t == c) { av = a[t]; xv = e[t]; pc = pv[t]; }
-      if (t == r) pr = pv[t];
-    }
-    A[c0 + r][c0 + c] = (c <= r) ? av / sqrt(pc) : 0.0;
-    X[c0 + r][c0 + c] = (c <= r) ? xv / sqrt(pr) : 0.0;
-  }
-  return -1;
-}
-#elif defined(EVR_LEAF_SYM)
-// Symmetric leaf (EVR_LEAF_SYM build; measured slower than the paired quad leaf — 34.9 k vs
-// 32.8 k cycles for the four leaves of a 64-column factor, tools/chol_prof.hip, profiles/r05/m): lane (r, q), r = lane & 15, q = lane >> 4, holds row r of BOTH
-// triangles of the 16x16 block at columns q + 4k, and of the inverse accumulator E.  Keeping
-// the upper triangle lets every exchange of a pivot step stay in VALU cross-lane moves:
-//   the pivot row A[j][c] (= the pivot column by symmetry) and the finished inverse row
-//   E[j][c] sit in lane j of the lane's own 16-lane DPP row (row_newbcast:j, 64-bit DPP);
-//   the lane's own entry A[r][j] sits in DPP row j & 3 at the same r: broadcast to all four
-//   rows by v_permlane32_swap + v_permlane16_swap (two VALU ops per dword);
-//   the pivot by readlane.
-// No LDS round trips (the quad leaf's 16 ds_bpermute per pivot, EVR_LEAF_QUAD build).  Rows
-// r <= j take m = 0 and are left as they are, so no per-entry masks: the eliminated column j
-// of rows below keeps a rounding residue that only ever updates itself (its L entries are
-// read from the upper triangle instead: row j of the upper triangle is final after step
-// j - 1 and equals the unnormalised column j, L[c][j] d_j^1/2 = A[j][c]); E[j][c] is zero for
-// c > j and one at c = j.  The results differ from the quad leaf by rounding only (the
-// upper-triangle operands are other roundings of the same values).
-__device__ __forceinline__ double xrow_bcast_f64(double v, int R) {   // DPP row R -> all rows
-  const long long x = __double_as_longlong(v);
-  unsigned d[2] = {(unsigned)x, (unsigned)(x >> 32)};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const auto t = __builtin_amdgcn_permlane32_swap(d[h], d[h], false, false);   // [0 1 0 1] | [2 3 2 3]
-    const unsigned u = (R >> 1) ? t[1] : t[0];
-    const auto w = __builtin_amdgcn_permlane16_swap(u, u, false, false);          // [0 0 2 2] | [1 1 3 3]
-    d[h] = (R & 1) ? w[1] : w[0];
-  }
-  return __longlong_as_double(((long long)d[1] << 32) | d[0]);
-}
-
-__device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
-                                              double* erow, double* piv) {
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  double a[4], e[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = q + 4 * k;
-    a[k] = (c <= r) ? A[c0 + r][c0 + c] : A[c0 + c][c0 + r];
-    e[k] = (c == r) ? 1.0 : 0.0;
-  }
-  int bad = -1;
-#pragma unroll
-  for (int j = 0; j < CP; ++j) {
-    const double p = readlane_f64(a[j >> 2], j + 16 * (j & 3));   // A[j][j]
-    const double arj = xrow_bcast_f64(a[j >> 2], j & 3);           // A[r][j]
-    double aj[4], ej[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      aj[k] = row_bcast_f64(a[k], j);                              // A[j][q + 4k]
-      ej[k] = row_bcast_f64(e[k], j);                              // E[j][q + 4k]
-    }
-    if (!(p > 0.0)) {
-      bad = j;
-      break;
-    }
-    if (lane == 0) piv[j] = p;
-    double ip = __builtin_amdgcn_rcp(p);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    const double m = (r > j) ? arj * ip : 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      a[k] = fma(-m, aj[k], a[k]);
-      e[k] = fma(-m, ej[k], e[k]);
-    }
-  }
-  (void)colj;
-  (void)erow;
-  if (bad >= 0) return bad;
-  lds_wave_sync();
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = q + 4 * k;
-    if (c >= r) {   // upper entry (r, c): L[c][r] = A[r][c] / d_r^1/2 (c = r: the diagonal)
-      A[c0 + c][c0 + r] = a[k] / sqrt(piv[r]);
-      if (c > r) A[c0 + r][c0 + c] = 0.0;
-    }
-    X[c0 + r][c0 + c] = (c <= r) ? e[k] / sqrt(piv[r]) : 0.0;
-  }
-  return -1;
-}
-#else
 // Lane (row r, quad q) holds A[r][q + 4k].  Per pivot step the pivot comes by readlane (a
 // uniform scalar: its reciprocal starts at once and the failure test is a scalar branch),
 // the lane's own row entry A[r][j] by a DPP quad broadcast, and the column entries of the
-// other rows (A[c][j]) and the finished inverse row by ds_bpermute (EVR_LEAF_LDS builds the
-// LDS store / fence / load exchange instead: 636 vs 532 cycles per pivot, tools/chol_prof.hip;
-// the exchanged values, hence the results, are the same).
+// other rows (A[c][j]) and the finished inverse row by ds_bpermute (an LDS store / fence /
+// load exchange measured 636 vs 532 cycles per pivot; a row-per-lane DPP leaf, a symmetric
+// permlane leaf, a single-pivot bpermute leaf and an 8-column leaf measured slower too — rounds
+// 3 to 6, DESIGN.md §4.3 — and were removed).
 // Returns the first failing local pivot index or -1 (uniform over the wave).
 __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[BNB + 1], int c0, double* colj,
                                               double* erow, double* piv) {
@@ -576,7 +420,6 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
     e[k] = (c == r) ? 1.0 : 0.0;
   }
   int bad = -1;
-#if !defined(EVR_LEAF_LDS) && !defined(EVR_LEAF_SINGLE)
   // two pivots per exchange round: columns j, j1 = j + 1 and inverse rows j, j1 as they are
   // before step j arrive in one round of ds_bpermute; what step j1 reads after step j (its
   // pivot, its column entries A'[c][j1], the lane's own A'[r][j1], the inverse row E'[j1]) is
@@ -651,73 +494,6 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   }
   (void)colj;
   (void)erow;
-#elif !defined(EVR_LEAF_LDS)
-  // pivot column and inverse row by ds_bpermute (one LDS-crossbar round trip, no store /
-  // fence / load): lane (r, q) takes A[q + 4k][j] from lane 4(q + 4k) + (j & 3) and the
-  // inverse row entry E[j][q + 4k] from lane 4j + q — the values the LDS exchange carries
-#pragma unroll
-  for (int j = 0; j < CP; ++j) {
-    const double p = readlane_f64(a[j >> 2], 4 * j + (j & 3));
-    const double arj = quad_bcast_f64(a[j >> 2], j & 3);
-    double cj[4], er[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      cj[k] = bperm_f64(a[j >> 2], 4 * q + 16 * k + (j & 3));
-      er[k] = bperm_f64(e[k], 4 * j + q);
-    }
-    if (!(p > 0.0)) {
-      bad = j;
-      break;
-    }
-    if (lane == 0) piv[j] = p;
-    double ip = __builtin_amdgcn_rcp(p);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    const double m = arj * ip;
-    const bool below = r > j;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = q + 4 * k;
-      const double dn = fma(-m, cj[k], a[k]);
-      const double en = fma(-m, er[k], e[k]);
-      a[k] = (below && c > j && c <= r) ? dn : a[k];
-      e[k] = (below && c <= j) ? en : e[k];
-    }
-  }
-  (void)colj;
-  (void)erow;
-#else
-#pragma unroll
-  for (int j = 0; j < CP; ++j) {
-    const double p = readlane_f64(a[j >> 2], 4 * j + (j & 3));   // A[j][j] (unnormalised pivot)
-    const double arj = quad_bcast_f64(a[j >> 2], j & 3);          // A[r][j]
-    if (q == (j & 3)) colj[r] = a[j >> 2];                        // pivot column for the other rows
-    if (r == j) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) erow[q + 4 * k] = e[k];         // inverse row j (final)
-    }
-    if (!(p > 0.0)) {
-      bad = j;
-      break;
-    }
-    if (lane == 0) piv[j] = p;
-    double ip = __builtin_amdgcn_rcp(p);            // + 2 Newton steps (pivots are normal, > 0)
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    ip = fma(ip, fma(-p, ip, 1.0), ip);
-    lds_wave_sync();
-    const double m = arj * ip;
-    const bool below = r > j;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = q + 4 * k;
-      const double dn = fma(-m, colj[c], a[k]);
-      const double en = fma(-m, erow[c], e[k]);
-      a[k] = (below && c > j && c <= r) ? dn : a[k];
-      e[k] = (below && c <= j) ? en : e[k];
-    }
-    __builtin_amdgcn_wave_barrier();   // one wave: LDS ops complete in order; keep the compiler's order
-  }
-#endif
   if (bad >= 0) return bad;
   lds_wave_sync();
 #pragma unroll
@@ -728,7 +504,6 @@ __device__ __forceinline__ int panel_factor16(double (*A)[BNB + 1], double (*X)[
   }
   return -1;
 }
-#endif
 
 // acc += P Q over one 16x16x16 block product on the f64 matrix cores (fragment maps as in
 // gemm_f64_kernel); P = M1[pr.., pc..] (or its transpose), Q = M2[qr.., qc..] (or transpose).

@@ -1,10 +1,9 @@
 // The training-row class of the restart-batch backward projection (qnehvi_small.hip qs_bwd),
-// apart from the sample rows: it needs only the forward's R.  By default its workgroups are
-// the backward launch's z >= 1 slices, beside the sample-row workgroups (which hold one
-// workgroup on 160 of the 256 CUs at the bench shape); EVR_QS_TAIL=kdw runs them in the tail
-// of the restart scan (hvi.hip hvi_kdw: extra workgroups after the scan's — measured slower,
-// the scan holds every slot), and the op path with that setting launches them on their own
-// (qs_bwd_tail).  For 16 training rows i of output j and a split of the rows r < n + nb of M_j
+// apart from the sample rows: it needs only the forward's R.  Its workgroups are the backward
+// launch's z >= 1 slices, beside the sample-row workgroups (which hold one workgroup on 160 of
+// the 256 CUs at the bench shape; in the tail of the restart scan they measured slower — the
+// scan holds every slot — and that placement was removed).  For 16 training rows i of output
+// j and a split of the rows r < n + nb of M_j
 // (nb = 0: the fused root C; nb > 0: the split root's L^-1 and G blocks):
 //   D[i][c]  = sum_r w_r M_j[r][i] R_j[r][c]                   (f64 MFMA, per-wave k-quarters)
 // with w_r = s_j^2 on the L^-1 rows of the split root and 1 elsewhere: the two blocks' gR

@@ -39,9 +39,8 @@
 #   cpufull     bench.py --cpu-full-ask (one full reference-structure ask on the host cores)
 #   qsprof      per-workgroup phase stamps of qs_bwd at the bench shape (tools/_qs_prof: hipcc
 #               --offload-arch=gfx950 -O3 -std=c++17 -DEVR_QS_PROF tools/qs_prof.hip -o tools/_qs_prof)
-#   cholprof    phase cycles + result digest of the 64x64 diagonal factor, the symmetric
-#               permlane/DPP leaf vs the two-pivot bpermute quad leaf (tools/_chol_prof_{sym,pair}:
-#               hipcc --offload-arch=gfx950 -O3 -DEVR_CHOL_PROF [-DEVR_LEAF_QUAD] tools/chol_prof.hip everest_amd/csrc/gemm.hip -o ...)
+#   cholprof    phase cycles + result digest of the 64x64 diagonal factor (tools/_chol_prof_pair:
+#               hipcc --offload-arch=gfx950 -O3 -DEVR_CHOL_PROF tools/chol_prof.hip everest_amd/csrc/gemm.hip -o ...)
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -115,9 +114,7 @@ for st in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 ;;
     cpufull) run cpufull 1100 python bench.py --no-eval-pass --steps 2 --warmup 1 --cpu-full-ask "$OUT/cpu_full_ask.json" ;;
     qsprof) run qsprof 60 tools/_qs_prof && run qsprof_tail 60 tools/_qs_prof tail ;;
-    cholprof)
-      run cholprof_sym 60 tools/_chol_prof_sym
-      run cholprof_pair 60 tools/_chol_prof_pair ;;
+    cholprof) run cholprof_pair 60 tools/_chol_prof_pair ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
