@@ -19,6 +19,7 @@
 #               2: no stores, 3: neither, 4: staging only, 8: staging + norms + MFMA; KMAT_PROFS picks) beside
 #               the shipped library
 #   kmatsq      two SQ counter passes over bench_kmat.py's MFMA kernel-matrix launches (KMAT_CASES)
+#   digest      tools/ask_digest.py with the shipped library and everest_amd/_lib_ab (bitwise-neutral changes: equal lines)
 #   trsm        tools/bench_trsm.py (forward substitution at the operator's G = L_base^-1 E shape)
 #   kmatwpc     bench_kmat.py at EVR_KMAT_WPC = 0 (one-shot grid) / 1 / 2 / 4 (persistent, workgroups per CU)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
@@ -88,6 +89,9 @@ for st in "$@"; do
     kmatsq)
       run kmatsq_a 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_a" -o run --output-format csv -- python tools/bench_kmat.py
       run kmatsq_b 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS --kernel-include-regex "kmat_mfma" -d "$OUT/kmatsq_b" -o run --output-format csv -- python tools/bench_kmat.py ;;
+    digest)
+      run digest_new 300 python tools/ask_digest.py
+      EVR_LIB_PATH=everest_amd/_lib_ab/libeverest_amd.so run digest_ab 300 python tools/ask_digest.py ;;
     trsm) run trsm 120 python tools/bench_trsm.py ;;
     kmatwpc)
       for w in 0 1 2 4; do
