@@ -54,6 +54,17 @@ def main():
                     "wave_total_us": q(tot), "staging_us": q(stage), "sampling_thresholds_us": q(thr),
                     "group_cell_us": q(grp), "term_rounds_us": q(term), "reduction_us": q(red),
                     "terms": q(rec[:, 6]), "passing_groups": q(rec[:, 7])}
+        # what balancing the variable work (group / cell phases + term rounds) would leave:
+        # within each workgroup's 4 candidates, and within each sample's b candidates
+        var = (grp + term).reshape(S, b)
+        fixed = (stage + thr + red).reshape(S, b)
+        nwg = (b + 3) // 4
+        wg_bal = [fixed[:, 4 * g:4 * g + 4].max(1) + var[:, 4 * g:4 * g + 4].mean(1) for g in range(nwg)]
+        out[tag]["balance"] = {"max_wave_us": round(float(tot.max()), 2),
+                               "max_wg_balanced_us": round(float(np.max(wg_bal)), 2),
+                               "max_sample_balanced_us": round(float((fixed.max(1) + var.mean(1)).max()), 2),
+                               "max_wave_of_heaviest_sample_us": round(float(tot.reshape(S, b).max(1)[
+                                   int(np.argmax(var.mean(1)))]), 2)}
     print(json.dumps(out))
 
 
