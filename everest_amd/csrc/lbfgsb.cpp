@@ -553,7 +553,8 @@ void Lbfgsb::subspace(std::vector<double>& z, const std::vector<double>& c) {
 // [mainlb, label 222] Cauchy point, subspace step, search direction, line-search start.
 int Lbfgsb::begin_iteration() {
   for (int attempt = 0; attempt < 3; ++attempt) {
-    std::vector<double> xcp, c;
+    std::vector<double>& xcp = xcp_tmp_;   // kept between iterations: no allocation per iteration
+    std::vector<double>& c = sc_c_;
     if (!cnstnd_ && col_ > 0) {
       z_ = x_;
       for (int i = 0; i < n_; ++i) iwhere_[i] = -1;

@@ -61,7 +61,7 @@ class Lbfgsb {
   std::vector<double> minv_lu_;            // LU of the 2col x 2col M^-1
   std::vector<double> wf_;                 // subspace scratch: W over the free variables
   // per-iteration scratch kept between iterations (no allocation in the loop)
-  std::vector<double> sc_p_, sc_v_, sc_wbp_, sc_mc_, sc_r_, sc_N_, sc_wv_, sc_dsub_, sc_xp_, sc_gram_;
+  std::vector<double> sc_p_, sc_v_, sc_wbp_, sc_mc_, sc_r_, sc_N_, sc_wv_, sc_dsub_, sc_xp_, sc_gram_, sc_c_;
   std::vector<std::pair<double, int>> sc_bp_;
   std::vector<int> sc_ind_, sc_piv_;
   std::vector<int> minv_piv_;
