@@ -35,6 +35,13 @@ class NotPSDError(RuntimeError):
     pass
 
 
+def require_f64(t, what):
+    """The oracle computes in f64 only; a float32 input (e.g. torch.tensor of a JSON list) is an
+    error of the caller, not something to promote silently."""
+    if isinstance(t, torch.Tensor) and t.is_floating_point() and t.dtype != torch.float64:
+        raise TypeError(f"{what}: oracle inputs must be float64, got {t.dtype}")
+
+
 # ---------------------------------------------------------------------------------------
 # kernels
 # ---------------------------------------------------------------------------------------
@@ -127,6 +134,10 @@ class GPState:
     alpha: torch.Tensor = field(default=None)
 
     def __post_init__(self):
+        # torch.tensor(<python list>) is float32: a state built from JSON lists would silently
+        # round its inputs / lengthscales to f32 (~6e-8 relative) and move the posterior
+        for name in ("X", "y", "lengthscale", "lo", "hi"):
+            require_f64(getattr(self, name), f"GPState.{name}")
         self.refresh()
 
     def refresh(self):
@@ -145,6 +156,7 @@ class GPState:
 def posterior(state: GPState, Xn: torch.Tensor, observation_noise: bool = False, full_cov=False):
     """Exact prediction: mu = c + K*·alpha; cov = K** - (K* L^-T)(K* L^-T)^T,
     un-standardized (mu·s + m, cov·s²); observation_noise adds sigma² before un-standardizing."""
+    require_f64(Xn, "posterior Xn")
     Ks = kernel_matrix(Xn, state.X, state.lengthscale, state.kind)          # nt x n
     mean = state.constant + Ks @ state.alpha
     Linv = torch.linalg.solve_triangular(state.L, torch.eye(state.L.shape[0], **TK), upper=False)

@@ -28,7 +28,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
-from .gp import GPState, TK, kernel_matrix, psd_safe_cholesky
+from .gp import GPState, TK, kernel_matrix, psd_safe_cholesky, require_f64
 from .multiobjective import approximate_cells, is_non_dominated, nondominated_cells, pareto_above_ref
 
 
@@ -115,6 +115,7 @@ def joint_posterior(models: Sequence[GPState], Xn: torch.Tensor, raw: bool = Fal
     and cov (... x m x p x p), computed the GPyTorch way: R = K(X, Xtr) L^-T.  ``raw``: Xn
     holds raw inputs and each model applies its own Normalize bounds (a ModelListGP whose
     members were fitted on different rows, bofire/surrogates/botorch_surrogates.py:79-128)."""
+    require_f64(Xn, "joint_posterior Xn")
     means, covs = [], []
     X_in = Xn
     for st in models:

@@ -46,7 +46,7 @@ def oracle_states(X, Y, lo, hi, hyp, kind=ogp.RBF):
     for j, h in enumerate(hyp):
         y = torch.tensor(Y[:, j], dtype=torch.float64)
         ym, ys = ogp.standardize_params(y.unsqueeze(-1))
-        out.append(ogp.GPState(X=Xn, y=(y - ym) / ys, lengthscale=torch.tensor(h["lengthscale"]),
+        out.append(ogp.GPState(X=Xn, y=(y - ym) / ys, lengthscale=torch.tensor(h["lengthscale"], dtype=torch.float64),
                                noise=h["noise"], constant=h["constant"], y_mean=float(ym), y_std=float(ys),
                                kind=kind, lo=torch.tensor(lo), hi=torch.tensor(hi)))
     return out

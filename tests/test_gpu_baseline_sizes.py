@@ -76,10 +76,11 @@ def test_config3_qnehvi_values_and_grads_match_oracle(config3, oracle3):
 
     # a 16-candidate subset of b = 512 (the MFMA-engine path) and the whole b = 20 restart batch
     # (the restart-batch kernels), both Sobol seed 2; the b = 20 batch holds the candidates
-    # whose new-point variance cancels furthest (L22^2 / (s^2 kxx) down to 1e-11): there the
-    # oracle itself is up to 9e-6 from the 60-digit truth (tests/test_hp_truth_oracle.py), so
-    # values are held to 2e-5 and gradients to 1e-4 of each candidate's scale
-    for b, sub, vtol, gtol in ((512, torch.arange(0, 512, 32), 1e-6, 1e-5), (20, torch.arange(20), 2e-5, 1e-4)):
+    # whose new-point variance cancels furthest (L22^2 / (s^2 kxx) down to 1e-11); the oracle and
+    # the device are each within 2.2e-6 of the 60-digit truth there (tests/test_hp_truth_oracle.py,
+    # tests/test_gpu_hp_truth.py).  Held: values 1e-6 / 2e-6 relative, gradients 1e-5 row-relative
+    # (measured round 6: 4.0e-7 / 5.4e-7 and 1.4e-8 / 2.3e-7)
+    for b, sub, vtol, gtol in ((512, torch.arange(0, 512, 32), 1e-6, 1e-5), (20, torch.arange(20), 2e-6, 1e-5)):
         Xc = bench.candidates(b, c["d"], seed=2, device=c["dev"])
         acq, dX = acqf.forward_backward(Xc)
         xt = Xc.cpu()[sub].clone().requires_grad_(True)
@@ -165,9 +166,9 @@ def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
         a = acq.cpu()[sub]
         r = ref.detach()
         # log values: an absolute error e in log space is a relative error e in the HVI itself.
-        # Every candidate, whatever its HVI, is held to 2e-5 (the oracle's own distance to the
-        # 60-digit truth is up to 9e-6 at this kind of state, tests/test_hp_truth_oracle.py;
-        # measured device-oracle 1.2e-6; north star 1e-3).  With the fused root (round 5)
+        # Every candidate, whatever its HVI, is held to 5e-6 (the oracle's and the device's own
+        # distances to the 60-digit truth are up to 2.2e-6 at this kind of state,
+        # tests/test_hp_truth_oracle.py; measured device-oracle 1.2e-6; north star 1e-3).  With the fused root (round 5)
         # candidates whose new-point variance had cancelled to < 1e-6 of the prior differed by
         # up to 5.6e-4 and were excused from the tight class; the split operator (round 6)
         # leaves nothing to excuse.
@@ -175,7 +176,7 @@ def test_config3_qlognehvi_values_and_grads_match_oracle(config3, oracle3):
         worst = int(err.argmax())
         print(f"qlog b={b}: max |d log| {float(err.max()):.3e} at log HVI {float(r[worst]):.2f}; "
               f"min log HVI {float(r.min()):.2f}")
-        assert (err <= 2e-5).all(), (b, [(float(x), float(y)) for x, y, bad in zip(a, r, err > 2e-5) if bad])
+        assert (err <= 5e-6).all(), (b, [(float(x), float(y)) for x, y, bad in zip(a, r, err > 5e-6) if bad])
         # gradients, every candidate (the fat-smoothed tail of a zero-HVI candidate included):
         # row-relative <= 1e-3 (measured 8.4e-5 at b = 20, 9.8e-7 at b = 512)
         g = dX.cpu()[sub]

@@ -3,8 +3,11 @@
 tests/golden/hp_state.json — the other half of the adjudication whose device half is
 tests/test_gpu_hp_truth.py.  CPU only (~1.5 min: the oracle's 256 Python partitions).
 
-Measured: the oracle is within ~1e-5 of the truth on ordinary candidates (its L22^2 =
-Sigma_xx - |L21|^2 cancels to 1e-7 .. 1e-11 of the prior there); 1e-6 .. 1e-2 from a baseline
+Measured: the oracle is within 2.2e-6 (values) / 1.5e-5 (gradients) of the truth on ordinary
+candidates (its L22^2 = Sigma_xx - |L21|^2 cancels to 1e-7 .. 1e-11 of the prior there) — as
+close as the device (tests/test_gpu_hp_truth.py).  Every input is f64: torch.tensor of a JSON
+list is float32, and f32-rounded candidates / lengthscales had put it 9e-6 away (the oracle now
+refuses non-f64 inputs, oracle/gp.py require_f64); 1e-6 .. 1e-2 from a baseline
 point (near16) neither f64 form resolves L22 (exact L22^2 / (s^2 kxx) 1e-13 .. 1e-19, below
 f64's resolution of Sigma_xx) and both are off by O(1) relative on HVIs of 1e-7 .. 1e-10 — the
 reference itself computes in f64 there."""
@@ -35,7 +38,7 @@ def hp_oracle():
     Y = bench.dtlz2(X, m)
     Xn = torch.tensor(X)
     states = [ogp.GPState(X=Xn, y=(torch.tensor(Y[:, j]) - h["y_mean"]) / h["y_std"],
-                          lengthscale=torch.tensor(h["lengthscale"]), noise=h["noise"], constant=h["constant"],
+                          lengthscale=torch.tensor(h["lengthscale"], dtype=torch.float64), noise=h["noise"], constant=h["constant"],
                           y_mean=h["y_mean"], y_std=h["y_std"]) for j, h in enumerate(st["hypers"])]
     obj = oq.Objective(-torch.ones(m, dtype=torch.float64), torch.zeros(m, dtype=torch.float64))
     ref = torch.full((m,), st["ref"], dtype=torch.float64)
@@ -62,7 +65,7 @@ def _eval(acq, xs):
 def test_oracle_matches_high_precision_truth(hp_oracle, which):
     """Values within 1e-4 of the truth where HVI > 1e-9 (|d log| for qLogNEHVI), gradients
     row-relative <= 1e-4 there (north star: 1e-3); maxima printed."""
-    xs = torch.tensor(hp_oracle["st"]["sets"][which])
+    xs = torch.tensor(hp_oracle["st"]["sets"][which], dtype=torch.float64)
     T = hp_oracle["tr"][which]
     for key, acq in (("qnehvi", hp_oracle["orc"]), ("qlog", hp_oracle["olog"])):
         a, g = _eval(acq, xs)
@@ -85,7 +88,7 @@ def test_oracle_near_training_points(hp_oracle):
     values within 2e-6 absolute of the truth (exact where the truth is 0), |d log| <= 1e-3
     where log HVI > -14 and L22 is resolvable in f64 (exact L22^2 / (s^2 kxx) >= 1e-14);
     maxima printed."""
-    xs = torch.tensor(hp_oracle["st"]["sets"]["near16"])
+    xs = torch.tensor(hp_oracle["st"]["sets"]["near16"], dtype=torch.float64)
     T = hp_oracle["tr"]["near16"]
     a, _ = _eval(hp_oracle["orc"], xs)
     la, _ = _eval(hp_oracle["olog"], xs)
