@@ -828,14 +828,20 @@ __global__ __launch_bounds__(1024) void posterior_finalize_kernel(int B, int n, 
 // row tile [m0, m0 + 32) contracts over k < m0 + 32 only (half the flops of the dense
 // product; the skipped entries are exact zeros).  Longer row tiles are dispatched first.
 // ---------------------------------------------------------------------------------------
+// 32 x 64 tiles where they still give >= 4 workgroups per CU (the metric's 5 x 512 x 1024:
+// 1280; B operand traffic per flop halved, 60.0 vs 64.2 us for the whole posterior), else
+// 32 x 32 (the single-output config 2: 256 workgroups).  Wider (32 x 128) measured slower
+// (67 us), and an XCD-owned column-tile order no different (tools/bench_post.py, profiles/r06/py)
 using PostCfg = DgCfg<32, 32, 16, false>;
+using PostCfgW = DgCfg<32, 64, 16, false>;
 constexpr int POST_NT = PostCfg::BM;
 
 // alpha^T B over the staged k-steps: the step's 16 alpha entries ride in the B image's first
 // padding column (thread t < 16 loads alpha[k0 + t] with the operand fetch and stages it);
-// thread (column c = tid % BN, row group g = tid / BN) accumulates rows g, g + 8 of every step
+// thread (column c = tid % BN, row group g = tid / BN) accumulates rows g, g + NG, ... of every step
+template <class C>
 struct PostMeanHook {
-  static constexpr int NG = 256 / PostCfg::BN, RPG = PostCfg::BK / NG;
+  static constexpr int NG = 256 / C::BN, RPG = C::BK / NG;
   const double* alpha;   // nullptr: not the last row block
   int n;
   double av;
@@ -843,27 +849,26 @@ struct PostMeanHook {
   __device__ __forceinline__ void prefetch(int k0) {
     if (!alpha) return;
     const int k = k0 + (int)threadIdx.x;
-    if (threadIdx.x < PostCfg::BK) av = k < n ? alpha[k] : 0.0;
+    if (threadIdx.x < C::BK) av = k < n ? alpha[k] : 0.0;
   }
   __device__ __forceinline__ void stage(double* Bs) {
-    if (alpha && threadIdx.x < PostCfg::BK) Bs[threadIdx.x * PostCfg::BST + PostCfg::BN] = av;
+    if (alpha && threadIdx.x < C::BK) Bs[threadIdx.x * C::BST + C::BN] = av;
   }
   __device__ __forceinline__ void step(const double* Bs, int, int) {
     if (!alpha) return;
-    const int g = threadIdx.x / PostCfg::BN, c = threadIdx.x % PostCfg::BN;
+    const int g = threadIdx.x / C::BN, c = threadIdx.x % C::BN;
 #pragma unroll
     for (int t = 0; t < RPG; ++t) {
       const int r = g + NG * t;
-      acc = fma(Bs[r * PostCfg::BST + PostCfg::BN], Bs[r * PostCfg::BST + c], acc);
+      acc = fma(Bs[r * C::BST + C::BN], Bs[r * C::BST + c], acc);
     }
   }
 };
 
-template <bool VEC>
+template <class C, bool VEC>
 __global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const double* __restrict__ Mm,
                                                            const double* __restrict__ Kx, double* __restrict__ Pn,
                                                            double* __restrict__ mrow) {
-  using C = PostCfg;
   __shared__ double lds[C::LDS_DOUBLES];
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   // dispatch order = descending k range (the longest row blocks start first), then output,
@@ -876,7 +881,7 @@ __global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const 
   const double* A = Mm + (size_t)j * (n + 1) * n;
   const double* B = Kx + (size_t)j * n * nt;
   const int kend = min(n, m0 + C::BM);
-  PostMeanHook hook{by == gy - 1 ? A + (size_t)n * n : nullptr, n, 0.0, 0.0};
+  PostMeanHook<C> hook{by == gy - 1 ? A + (size_t)n * n : nullptr, n, 0.0, 0.0};
   dg_double4 acc[C::FM][C::FN];
   dg_mainloop<C>(
       lds, 0, kend,
@@ -891,7 +896,7 @@ __global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const 
       acc, hook);
   // the mainloop ended on a barrier: its LDS is free.  Column sums of squares over the
   // tile's rows (fixed order: the 16 rows of a wave by xor-shuffles, then the two waves)
-  constexpr int BN = C::BN, NG = PostMeanHook::NG;
+  constexpr int BN = C::BN, NG = PostMeanHook<C>::NG;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1, i = lane & 15, q = lane >> 4;
   double* red = lds;              // [2][BN]
@@ -1160,11 +1165,16 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
   if (int rc = evr_kernel_matrix(stream, kind, B, n, nt, d, Xn, nullptr, nullptr, X, shift, scale, lengthscales,
                                  nullptr, nullptr, Kx))
     return rc;
-  const dim3 grid(cdiv(nt, PostCfg::BN), nrt, B);
-  if (n % 2 == 0 && nt % 2 == 0 && (uintptr_t)M % 16 == 0 && (uintptr_t)Kx % 16 == 0)
-    post_proj_kernel<true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
-  else
-    post_proj_kernel<false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+  const bool vec = n % 2 == 0 && nt % 2 == 0 && (uintptr_t)M % 16 == 0 && (uintptr_t)Kx % 16 == 0;
+  if ((long long)cdiv(nt, PostCfgW::BN) * nrt * B >= 1024) {
+    const dim3 grid(cdiv(nt, PostCfgW::BN), nrt, B);
+    if (vec) post_proj_kernel<PostCfgW, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+    else post_proj_kernel<PostCfgW, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+  } else {
+    const dim3 grid(cdiv(nt, PostCfg::BN), nrt, B);
+    if (vec) post_proj_kernel<PostCfg, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+    else post_proj_kernel<PostCfg, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+  }
   EVR_LAUNCH_CHECK();
   post_finalize_kernel<<<dim3(cdiv(nt, 256), B), 256, 0, s>>>(B, n, nt, nrt, Pn, mrow, c, ym, ys, kxx, noise_add,
                                                               mean, var);

@@ -21,6 +21,10 @@
 #   kmatsq      two SQ counter passes over bench_kmat.py's MFMA kernel-matrix launches (KMAT_CASES)
 #   digest      tools/ask_digest.py with the shipped library and everest_amd/_lib_ab (bitwise-neutral changes: equal lines)
 #   trsm        tools/bench_trsm.py (forward substitution at the operator's G = L_base^-1 E shape)
+#   post        tools/bench_post.py (GP posterior at the metric's shape, HIP events) and its rocprofv3
+#               --kernel-trace --stats pass -> <tag>/post_prof
+#   postab      tools/bench_post.py with the shipped library and everest_amd/_lib_ab, twice interleaved
+#   postv       the same over the shipped library and the builds everest_amd/<dir> named in $POST_LIBS
 #   kmatwpc     bench_kmat.py at EVR_KMAT_WPC = 0 (one-shot grid) / 1 / 2 / 4 (persistent, workgroups per CU)
 #   sharded     tools/sharded_ask_check.py (config-4 ask at 2 ranks vs 1 rank, same seed)
 #   pmc20       FETCH_SIZE / WRITE_SIZE passes over the bench's restart batch (b = 20 at the
@@ -93,6 +97,19 @@ for st in "$@"; do
       run digest_new 300 python tools/ask_digest.py
       EVR_LIB_PATH=everest_amd/_lib_ab/libeverest_amd.so run digest_ab 300 python tools/ask_digest.py ;;
     trsm) run trsm 120 python tools/bench_trsm.py ;;
+    post)
+      run post 120 python tools/bench_post.py
+      run post_prof 180 rocprofv3 --kernel-trace --stats -d "$OUT/post_prof" -o run --output-format csv -- python tools/bench_post.py ;;
+    postv)   # bench_post.py over the shipped library and the variant builds named in $POST_LIBS, twice
+      for i in 1 2; do
+        run post_lib$i 120 python tools/bench_post.py
+        for L in $POST_LIBS; do EVR_LIB_PATH=everest_amd/$L/libeverest_amd.so run post_$L$i 120 python tools/bench_post.py; done
+      done ;;
+    postab)
+      for i in 1 2; do
+        run post_new$i 120 python tools/bench_post.py
+        EVR_LIB_PATH=everest_amd/_lib_ab/libeverest_amd.so run post_ab$i 120 python tools/bench_post.py
+      done ;;
     kmatwpc)
       for w in 0 1 2 4; do
         EVR_KMAT_WPC=$w KMAT_CASES=cfg5_n2048_d32,cfg5_train_sym run kmat_wpc$w 300 python tools/bench_kmat.py
