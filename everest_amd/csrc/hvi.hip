@@ -1389,7 +1389,6 @@ static long long hvi_kd_workspace(const evr_qnehvi_state* st, int b) {
 template <int M, bool BWD>
 static int hvi_kd_launch(hipStream_t s, const evr_qnehvi_state* st, int b, const double* G, const double* gout,
                          double* part, double* dG, const int* flags, double* acq) {
-  const KdLds Lo = kd_lds(st->pts_stride, M, st->max_groups);
   const int W = hvi_kd_wsplit(b);
   const int ntiles = cdiv(b, KD_CT / W);
   const int nsb = hvi_kd_nsplit(st, b);   // workgroup splits

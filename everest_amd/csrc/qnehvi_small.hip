@@ -243,7 +243,6 @@ __global__ __launch_bounds__(256, 2) void qs_bwd(int n, int nb, int nh, int S, i
   const int rbeg = n + nb + z * rows_per, rend = min(Rr - 1, rbeg + rows_per);
   const double aj = oa[j], sj = ys[j];
   const double* Mj = M + (size_t)j * Rr * n;
-  const double* Rj = R + (size_t)j * Rr * b;
   // the epilogue's candidate coordinates (normalised) and inverse lengthscales, loaded first:
   // X may be the plan's pinned host buffer (PCIe latency, hidden behind the main loop)
   double xc[QS_MAXD];
