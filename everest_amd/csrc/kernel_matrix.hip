@@ -26,8 +26,12 @@ __global__ __launch_bounds__(256) void kmat_kernel(int kind, int n1, int n2, int
                                                    const double* __restrict__ os, const double* __restrict__ dg,
                                                    double* __restrict__ K,
                                                    const unsigned long long* seq_src, unsigned long long* seq_dst,
-                                                   double* __restrict__ x_dst) {
+                                                   double* __restrict__ x_dst, int* __restrict__ zero_dst, int nzero) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  // the posterior's arrival counters (post_proj_kernel) zeroed by the first workgroup: the
+  // projection launches after this kernel has completed
+  if (zero_dst && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    for (int t = threadIdx.x; t < nzero; t += 256) zero_dst[t] = 0;
   // host-driven chains: the evaluation's sequence number (pinned host memory, posted with the
   // candidates) copied to device memory, so the chain's last kernel reads it from L2 instead of
   // across PCIe (this kernel's candidate loads pay that latency anyway)
@@ -865,10 +869,25 @@ struct PostMeanHook {
   }
 };
 
+// Posterior moments, fused into the projection: the last workgroup to finish a column tile
+// (per output; an arrival counter zeroed by the K_* launch) sums the tile's row partials in the
+// fixed order of the former post_finalize_kernel and writes mean and variance — one launch
+// boundary less (the separate kernel took 4.9 us at the metric's shape)
+struct PostMoments {
+  int* cnt;             // B x gx arrival counters, 0 on entry
+  const double* cc;     // constant means (B)
+  const double* ym;
+  const double* ys;
+  const double* kxx;
+  const double* noise;  // nullptr: latent posterior
+  double* mean;
+  double* var;
+};
+
 template <class C, bool VEC>
 __global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const double* __restrict__ Mm,
                                                            const double* __restrict__ Kx, double* __restrict__ Pn,
-                                                           double* __restrict__ mrow) {
+                                                           double* __restrict__ mrow, PostMoments pm) {
   __shared__ double lds[C::LDS_DOUBLES];
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   // dispatch order = descending k range (the longest row blocks start first), then output,
@@ -915,43 +934,54 @@ __global__ __launch_bounds__(256, 4) void post_proj_kernel(int n, int nt, const 
   }
   if (hook.alpha) redm[tid] = hook.acc;
   __syncthreads();
+  // the partials go out as device-coherent stores (past the per-XCD L2s, which a __threadfence
+  // would have to write back whole: 3x slower with K_* dirty in them), each writer waits for
+  // its stores to complete, then one thread counts the tile's arrival; the last arrival reads
+  // the partials with device-coherent loads and finalises the column tile
   if (tid < BN && n0 + tid < nt) {
-    Pn[((size_t)j * gy + by) * nt + n0 + tid] = red[tid] + red[BN + tid];
+    __hip_atomic_store(Pn + ((size_t)j * gy + by) * nt + n0 + tid, red[tid] + red[BN + tid], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     if (hook.alpha) {
       double a = 0.0;
 #pragma unroll
       for (int g = 0; g < NG; ++g) a += redm[g * BN + tid];
-      mrow[(size_t)j * nt + n0 + tid] = a;
+      __hip_atomic_store(mrow + (size_t)j * nt + n0 + tid, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this thread's stores have completed
+  }
+  __syncthreads();
+  __shared__ int last;
+  if (tid == 0) last = atomicAdd(pm.cnt + (size_t)j * gx + bx, 1) == gy - 1;
+  __syncthreads();
+  if (!last) return;
+  const int c = n0 + tid;
+  if (tid < BN && c < nt) {
+    const double* P = Pn + (size_t)j * gy * nt + c;
+    // row tile rt's partial goes to s0 (rt even) or s1 (rt odd) in increasing rt; loads in
+    // batches of 8 so their latencies overlap
+    const double mr = __hip_atomic_load(mrow + (size_t)j * nt + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double s0 = 0.0, s1 = 0.0;
+    for (int r0 = 0; r0 < gy; r0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = r0 + u < gy ? __hip_atomic_load(P + (size_t)(r0 + u) * nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        if (r0 + u < gy) s0 += v[u];
+        if (r0 + u + 1 < gy) s1 += v[u + 1];
+      }
+    }
+    const double ss = s0 + s1;
+    const double sj = pm.ys[j];
+    pm.mean[(size_t)j * nt + c] = pm.ym[j] + sj * (pm.cc[j] + mr);
+    double v = pm.kxx[j] - ss;
+    if (pm.noise) v += pm.noise[j];
+    pm.var[(size_t)j * nt + c] = sj * sj * v;
   }
 }
 
-// mean / variance from the row-tile partials (fixed order) and the mean row
-__global__ __launch_bounds__(256) void post_finalize_kernel(int B, int n, int nt, int nrt, const double* __restrict__ Pn,
-                                                            const double* __restrict__ mrow,
-                                                            const double* __restrict__ cc,
-                                                            const double* __restrict__ ym,
-                                                            const double* __restrict__ ys,
-                                                            const double* __restrict__ kxx,
-                                                            const double* __restrict__ noise,
-                                                            double* __restrict__ mean, double* __restrict__ var) {
-  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= nt) return;
-  const double* P = Pn + (size_t)b * nrt * nt + c;
-  double s0 = 0.0, s1 = 0.0;
-  int rt = 0;
-  for (; rt + 1 < nrt; rt += 2) {
-    s0 += P[(size_t)rt * nt];
-    s1 += P[(size_t)(rt + 1) * nt];
-  }
-  if (rt < nrt) s0 += P[(size_t)rt * nt];
-  const double ss = s0 + s1;
-  const double s = ys[b];
-  mean[(size_t)b * nt + c] = ym[b] + s * (cc[b] + mrow[(size_t)b * nt + c]);
-  double v = kxx[b] - ss;
-  if (noise) v += noise[b];
-  var[(size_t)b * nt + c] = s * s * v;
-}
 
 }  // namespace evr
 
@@ -971,7 +1001,7 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
                          const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
-                         double* x_dst = nullptr);
+                         double* x_dst = nullptr, int* zero_dst = nullptr, int nzero = 0);
 }  // namespace evr
 
 extern "C" {
@@ -991,7 +1021,8 @@ namespace evr {
 int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, const double* X1, const double* shift1,
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
-                         const unsigned long long* seq_src, unsigned long long* seq_dst, double* x_dst) {
+                         const unsigned long long* seq_src, unsigned long long* seq_dst, double* x_dst,
+                         int* zero_dst, int nzero) {
   EVR_CHECK(!seq_dst || (seq_src && d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0),
             "kernel_matrix_launch: the sequence copy needs the VALU kernel (d < 16, one family)");
   EVR_CHECK(!x_dst || (d < 16 && kind < KIND_MIXED && n1 > 0 && n2 > 0 && n2 <= KT),
@@ -1000,6 +1031,12 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
   EVR_CHECK(B >= 1 && n1 >= 0 && n2 >= 0 && d >= 1 && d <= KMAXD, "evr_kernel_matrix: bad sizes B=%d n1=%d n2=%d d=%d",
             B, n1, n2, d);
   if (n1 == 0 || n2 == 0) return 0;
+  // counters to zero (evr_gp_posterior): by kmat_kernel's first workgroup on the VALU path,
+  // by a memset before the launches otherwise
+  if (zero_dst && nzero > 0 && (kind >= KIND_MIXED || d >= 16)) {
+    EVR_HIP(hipMemsetAsync(zero_dst, 0, sizeof(int) * (size_t)nzero, (hipStream_t)stream));
+    zero_dst = nullptr;
+  }
   if (kind >= KIND_MIXED) {
     // one family per output: one launch per run of consecutive outputs of the same family
     for (int b0 = 0; b0 < B;) {
@@ -1063,7 +1100,7 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
 #define KTK(RA_, K_)                                                                              \
   kmat_kernel<RA_, K_><<<g, 256, lds, (hipStream_t)stream>>>(kind, n1, n2, d, X1, shift1, scale1, X2, shift2, \
                                                              scale2, lengthscales, outputscale, diag_add, K,         \
-                                                             seq_src, seq_dst, x_dst)
+                                                             seq_src, seq_dst, x_dst, zero_dst, nzero)
 #define KT_(RA_)                         \
   if (kind == RBF) KTK(RA_, RBF);           \
   else if (kind == MATERN05) KTK(RA_, MATERN05); \
@@ -1147,8 +1184,11 @@ int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* 
 }
 
 long long evr_gp_posterior_workspace_doubles(int B, int n, int nt) {
-  // K_* (B x n x nt), the row-tile partials (B x ceil(n / 32) x nt) and the mean row (B x nt)
-  return (B > 0 && n > 0 && nt > 0) ? (long long)B * nt * ((long long)n + cdiv(n, POST_NT) + 1) : 0;
+  // K_* (B x n x nt), the row-tile partials (B x ceil(n / 32) x nt), the mean row (B x nt) and
+  // the column tiles' arrival counters (B x ceil(nt / 32) ints)
+  return (B > 0 && n > 0 && nt > 0)
+             ? (long long)B * nt * ((long long)n + cdiv(n, POST_NT) + 1) + cdiv(B * cdiv(nt, PostCfg::BN), 2)
+             : 0;
 }
 
 int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const double* Xn, const double* X,
@@ -1162,22 +1202,22 @@ int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const 
   double* Kx = work;                                   // B x n x nt
   double* Pn = Kx + (size_t)B * n * nt;                // B x nrt x nt
   double* mrow = Pn + (size_t)B * nrt * nt;            // B x nt
-  if (int rc = evr_kernel_matrix(stream, kind, B, n, nt, d, Xn, nullptr, nullptr, X, shift, scale, lengthscales,
-                                 nullptr, nullptr, Kx))
+  int* cnt = (int*)(mrow + (size_t)B * nt);            // B x ceil(nt / 32)
+  const int ncnt = B * cdiv(nt, PostCfg::BN);
+  if (int rc = kernel_matrix_launch(stream, kind, B, n, nt, d, Xn, nullptr, nullptr, X, shift, scale, lengthscales,
+                                    nullptr, nullptr, Kx, nullptr, nullptr, nullptr, cnt, ncnt))
     return rc;
+  const PostMoments pm{cnt, c, ym, ys, kxx, noise_add, mean, var};
   const bool vec = n % 2 == 0 && nt % 2 == 0 && (uintptr_t)M % 16 == 0 && (uintptr_t)Kx % 16 == 0;
   if ((long long)cdiv(nt, PostCfgW::BN) * nrt * B >= 1024) {
     const dim3 grid(cdiv(nt, PostCfgW::BN), nrt, B);
-    if (vec) post_proj_kernel<PostCfgW, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
-    else post_proj_kernel<PostCfgW, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+    if (vec) post_proj_kernel<PostCfgW, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow, pm);
+    else post_proj_kernel<PostCfgW, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow, pm);
   } else {
     const dim3 grid(cdiv(nt, PostCfg::BN), nrt, B);
-    if (vec) post_proj_kernel<PostCfg, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
-    else post_proj_kernel<PostCfg, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow);
+    if (vec) post_proj_kernel<PostCfg, true><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow, pm);
+    else post_proj_kernel<PostCfg, false><<<grid, 256, 0, s>>>(n, nt, M, Kx, Pn, mrow, pm);
   }
-  EVR_LAUNCH_CHECK();
-  post_finalize_kernel<<<dim3(cdiv(nt, 256), B), 256, 0, s>>>(B, n, nt, nrt, Pn, mrow, c, ym, ys, kxx, noise_add,
-                                                              mean, var);
   EVR_LAUNCH_CHECK();
   return 0;
 }

@@ -49,7 +49,7 @@ int kernel_matrix_launch(void* stream, int kind, int B, int n1, int n2, int d, c
                          const double* scale1, const double* X2, const double* shift2, const double* scale2,
                          const double* lengthscales, const double* outputscale, const double* diag_add, double* K,
                          const unsigned long long* seq_src = nullptr, unsigned long long* seq_dst = nullptr,
-                         double* x_dst = nullptr);
+                         double* x_dst = nullptr, int* zero_dst = nullptr, int nzero = 0);
 constexpr int QS_TILE_ROWS = 16;
 constexpr int QN_NORM_TILE = 32;   // qnehvi_proj.hip QN_NT (the b > 32 projection tiles)
 bool hvi_kdb_fused_applies(const evr_qnehvi_state* st, int b);
