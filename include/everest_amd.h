@@ -156,9 +156,11 @@ int evr_gp_posterior_finalize(void* stream, int B, int n, int nt, const double* 
                               const double* kxx, const double* noise_add,
                               double* mean, double* var);
 
-/* Whole posterior in one call: K_x = k(Xn, normalize(X)) (kernel_matrix), R = M K_x
- * (M = [Linv; alpha^T], B x (n+1) x n), then the finalize above.  work: B*nt*(2n+1)
- * doubles (evr_gp_posterior_workspace_doubles). */
+/* Whole posterior in one call: K_x = k(Xn, normalize(X)) (kernel_matrix), then the moments
+ * of R = M K_x (M = [Linv; alpha^T], B x (n+1) x n) without storing R: per 32-row tile sums
+ * of squares, finalised as above by each column tile's last-arriving workgroup.  work:
+ * evr_gp_posterior_workspace_doubles(B, n, nt) doubles (K_x, the row-tile partials, the mean
+ * row and the arrival counters), 16-byte aligned, contents irrelevant on entry. */
 long long evr_gp_posterior_workspace_doubles(int B, int n, int nt);
 int evr_gp_posterior(void* stream, int B, int n, int nt, int d, int kind, const double* Xn, const double* X,
                      const double* shift, const double* scale, const double* lengthscales, const double* M,
